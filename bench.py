@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Federation-round benchmark: 8-learner sync FedAvg, CIFAR-10, ResNet-18.
+
+Metric (BASELINE.json): "federation-round time (ms) + rounds/sec, 8-learner
+FedAvg CIFAR-10 ResNet-18".  One benchmark "step" is ONE federation round:
+
+  every learner (one per GPU, one process per GPU) trains its IID shard of
+  the 50,000-image CIFAR-10 training set for ``--local-epochs`` epochs
+  (batch 32, MomentumSGD lr 0.005 / momentum 0.75: the reference's CIFAR-10
+  experiment config, examples/config/cifar10/
+  test_localhost_synchronous_momentumsgd.yaml), evaluates its test shard
+  (the reference learner evaluates at task end, keras_model_ops.py:174-176),
+  then the round closes with NUM_TRAINING_EXAMPLES-weighted FedAvg (scale
+  kernel + one RCCL all-reduce) leaving the community model resident on every
+  GPU.
+
+The dataset is fixed (50k train / 10k test images) and split across the N
+learners, so total work per round is constant: scaling is "strong" and
+``value`` (rounds/s of the whole federation) is the whole-job aggregate.
+Data are synthetic tensors of CIFAR-10's shape, weights random-init of the
+ResNet-18 architecture (no network for datasets/checkpoints).
+
+Launch: ``python bench.py`` (1 GPU) or
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1
+--master-port P bench.py --gpus N``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "federation-round time (ms) + rounds/sec, 8-learner FedAvg CIFAR-10 ResNet-18"
+BASELINE_VALUE = None  # BASELINE.json "published": {} -- no reference number exists
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3, help="timed federation rounds")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed federation rounds")
+    ap.add_argument("--local-epochs", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--train-size", type=int, default=50000)
+    ap.add_argument("--test-size", type=int, default=10000)
+    ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--lr", type=float, default=0.005)
+    ap.add_argument("--momentum", type=float, default=0.75)
+    ap.add_argument("--json-out", type=str, default="")
+    args = ap.parse_args()
+
+    import torch
+
+    from metisfl_amd.models.resnet import ResNet18
+    from metisfl_amd.ops.optim import OptimizerSpec
+    from metisfl_amd.parallel.comm import Comm
+    from metisfl_amd.parallel.federation import CollectiveFederation, FederationConfig
+
+    comm = Comm()
+    n = comm.world
+    if args.gpus != n and comm.rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={n}; using {n}", file=sys.stderr)
+    dev = comm.device
+    torch.manual_seed(1234 + comm.rank)
+
+    # IID shard of the fixed-size dataset (strong scaling).
+    n_train = args.train_size // n + (1 if comm.rank < args.train_size % n else 0)
+    n_test = args.test_size // n + (1 if comm.rank < args.test_size % n else 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + comm.rank)
+    xtr = torch.randn((n_train, 32, 32, 3), generator=g, device=dev)
+    ytr = torch.randint(0, 10, (n_train,), generator=g, device=dev)
+    xte = torch.randn((n_test, 32, 32, 3), generator=g, device=dev)
+    yte = torch.randint(0, 10, (n_test,), generator=g, device=dev)
+
+    opt = OptimizerSpec("momentum_sgd", args.lr, momentum=args.momentum)
+    net = ResNet18(batch_size=args.batch, device=dev, optimizer=opt, seed=7)
+    train_ds = net.make_dataset(xtr, ytr, seed=comm.rank)
+    test_ds = net.make_dataset(xte, yte, seed=comm.rank, shuffle=False)
+    del xtr, xte
+    cfg = FederationConfig(protocol="synchronous", batch_size=args.batch,
+                           local_epochs=args.local_epochs, evaluate_test=not args.no_eval)
+    fed = CollectiveFederation(comm, net, train_ds, cfg, test_ds=test_ds)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        fed.run_round()
+        if comm.rank == 0:
+            r = fed.history[-1]
+            print(f"[bench] warmup round {r.global_iteration}: {r.round_ms:.1f} ms "
+                  f"(train {r.train_ms:.1f}, agg {r.aggregation_ms:.2f})", file=sys.stderr, flush=True)
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fed.run_round()
+        if comm.rank == 0:
+            r = fed.history[-1]
+            print(f"[bench] round {r.global_iteration}: {r.round_ms:.1f} ms "
+                  f"(train {r.train_ms:.1f}, agg {r.aggregation_ms:.2f}) loss "
+                  f"{r.learner_meta[:, 4].mean():.3f}", file=sys.stderr, flush=True)
+    comm.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    elapsed = comm.all_max(elapsed)
+    timed = fed.history[-args.steps:] if args.steps else []
+    round_ms = elapsed * 1e3 / max(1, args.steps)
+    rounds_per_s = args.steps / elapsed if elapsed > 0 else 0.0
+    updates = fed.num_local_updates[0]
+    out = {
+        "metric": METRIC,
+        "value": rounds_per_s,
+        "unit": "rounds/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round_ms,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": (rounds_per_s / BASELINE_VALUE) if BASELINE_VALUE else None,
+        "dtype": "bf16",
+        "data": "synthetic (CIFAR-10 shapes, IID shards), random-init ResNet-18",
+        "config": {
+            "model": "resnet18-cifar",
+            "dataset": "cifar10 (50k train / 10k test, synthetic)",
+            "learners": n,
+            "global_batch": args.batch * n,
+            "per_learner_batch": args.batch,
+            "seq_len": None,
+            "local_epochs": args.local_epochs,
+            "local_updates_per_round": updates,
+            "optimizer": f"momentum_sgd(lr={args.lr}, momentum={args.momentum})",
+            "aggregation": "FedAvg(NUM_TRAINING_EXAMPLES), RCCL all-reduce",
+            "protocol": "synchronous",
+            "parallelism": f"fedavg-dp{n}",
+            "test_eval": not args.no_eval,
+        },
+        "round_ms": round_ms,
+        "rounds_per_s": rounds_per_s,
+        "train_ms_mean": sum(r.train_ms for r in timed) / max(1, len(timed)),
+        "aggregation_ms_mean": sum(r.aggregation_ms for r in timed) / max(1, len(timed)),
+        "samples_per_s": (args.train_size * args.local_epochs) / (round_ms / 1e3) if round_ms else 0.0,
+    }
+    if comm.rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    comm.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

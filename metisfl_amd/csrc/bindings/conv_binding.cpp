@@ -1,0 +1,180 @@
+// torch binding for the implicit-GEMM convolution kernels (conv.hip) and the
+// dense GEMM kernels (gemm.hip).  Geometry is validated here, on the host,
+// before any launch: the kernels index with 32-bit offsets and trust M/K/Ng.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include "kernels/conv.h"
+#include "kernels/gemm.h"
+
+namespace {
+
+hipStream_t cur_stream(const torch::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+uint16_t* bf(const torch::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+void check_bf16(const torch::Tensor& t, int64_t numel, const char* nm) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), nm, " must be a contiguous device tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16, nm, " must be bf16");
+  TORCH_CHECK(t.numel() == numel, nm, " has ", t.numel(), " elements, expected ", numel);
+}
+void check_f32(const torch::Tensor& t, int64_t min_numel, const char* nm) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), nm, " must be a contiguous device tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, nm, " must be fp32");
+  TORCH_CHECK(t.numel() >= min_numel, nm, " too small: ", t.numel(), " < ", min_numel);
+}
+
+int out_dim(int64_t in, int64_t k, int64_t stride, int64_t pad) {
+  return (int)((in + 2 * pad - k) / stride + 1);
+}
+
+mfl::ConvGeom fwd_geom(int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co, int64_t R,
+                       int64_t S, int64_t stride, int64_t pad) {
+  TORCH_CHECK(C % 8 == 0, "conv input channels must be a multiple of 8 (got ", C, ")");
+  TORCH_CHECK(Co % 8 == 0, "conv output channels must be a multiple of 8 (got ", Co, ")");
+  mfl::ConvGeom g{};
+  g.N = (int)N; g.H = (int)H; g.W = (int)W; g.C = (int)C;
+  g.P = out_dim(H, R, stride, pad);
+  g.Q = out_dim(W, S, stride, pad);
+  g.R = (int)R; g.S = (int)S; g.stride = (int)stride; g.pad = (int)pad;
+  g.M = (int)(N * g.P * g.Q);
+  g.K = (int)(R * S * C);
+  g.Ng = (int)Co;
+  TORCH_CHECK((int64_t)N * H * W * C < (1LL << 31), "activation too large for 32-bit indexing");
+  return g;
+}
+
+// dgrad: rows over dX (H x W), source dY (P x Q x Co), B = W^T [Cin][R][S][Co]
+mfl::ConvGeom dgrad_geom(int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co, int64_t R,
+                         int64_t S, int64_t stride, int64_t pad) {
+  mfl::ConvGeom f = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
+  mfl::ConvGeom g{};
+  g.N = f.N; g.H = f.P; g.W = f.Q; g.C = (int)Co;
+  g.P = (int)H; g.Q = (int)W;
+  g.R = f.R; g.S = f.S; g.stride = f.stride; g.pad = f.pad;
+  g.M = (int)(N * H * W);
+  g.K = (int)(R * S * Co);
+  g.Ng = (int)C;
+  return g;
+}
+
+std::vector<int64_t> plan_vec(const mfl::ConvPlan& p, int64_t ws_floats, int64_t stats_rows) {
+  return {p.bm, p.bn, p.splits, p.kchunk, stats_rows, ws_floats};
+}
+
+// mode 0 = fwd, 1 = dgrad, 2 = wgrad.  Returns
+// [bm, bn, splits, kchunk, stats_rows, workspace_floats].
+std::vector<int64_t> conv_plan(int64_t mode, int64_t N, int64_t H, int64_t W, int64_t C,
+                               int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad) {
+  if (mode == 2) {
+    mfl::ConvGeom g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
+    auto p = mfl::plan_conv_wgrad(g);
+    const int64_t ws = p.splits > 1 ? (int64_t)p.splits * g.Ng * g.K : 0;
+    return plan_vec(p, ws, 0);
+  }
+  mfl::ConvGeom g = mode == 0 ? fwd_geom(N, H, W, C, Co, R, S, stride, pad)
+                              : dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
+  auto p = mfl::plan_conv_gemm(g);
+  const int64_t ws = p.splits > 1 ? (int64_t)p.splits * g.M * g.Ng : 0;
+  const int64_t rows = p.splits > 1 ? mfl::splitk_stats_blocks(g.M, g.Ng) : p.stats_rows;
+  return plan_vec(p, ws, rows);
+}
+
+void run_gemm(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const torch::Tensor& w,
+              const torch::Tensor& y, const c10::optional<torch::Tensor>& ws,
+              const c10::optional<torch::Tensor>& stats, bool accum) {
+  auto p = mfl::plan_conv_gemm(g);
+  float* wsp = nullptr;
+  if (p.splits > 1) {
+    TORCH_CHECK(ws.has_value() && ws->defined(), "split-K workspace required");
+    check_f32(*ws, (int64_t)p.splits * g.M * g.Ng, "workspace");
+    wsp = ws->data_ptr<float>();
+  }
+  float* st = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    const int64_t rows = p.splits > 1 ? mfl::splitk_stats_blocks(g.M, g.Ng) : p.stats_rows;
+    check_f32(*stats, rows * 2 * g.Ng, "stats");
+    st = stats->data_ptr<float>();
+  }
+  mfl::launch_conv_gemm(g, dgrad, p, bf(src), bf(w), bf(y), wsp, st, accum, cur_stream(y));
+}
+
+void conv_forward(torch::Tensor x, torch::Tensor w, torch::Tensor y,
+                  c10::optional<torch::Tensor> ws, c10::optional<torch::Tensor> stats, int64_t N,
+                  int64_t H, int64_t W, int64_t C, int64_t Co, int64_t R, int64_t S,
+                  int64_t stride, int64_t pad) {
+  auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
+  check_bf16(x, N * H * W * C, "x");
+  check_bf16(w, Co * R * S * C, "w");
+  check_bf16(y, (int64_t)g.M * Co, "y");
+  run_gemm(g, false, x, w, y, ws, stats, false);
+}
+
+void conv_dgrad(torch::Tensor dy, torch::Tensor wt, torch::Tensor dx,
+                c10::optional<torch::Tensor> ws, int64_t N, int64_t H, int64_t W, int64_t C,
+                int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate) {
+  auto g = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
+  check_bf16(dy, (int64_t)N * g.H * g.W * Co, "dy");
+  check_bf16(wt, C * R * S * Co, "wt");
+  check_bf16(dx, N * H * W * C, "dx");
+  run_gemm(g, true, dy, wt, dx, ws, c10::nullopt, accumulate);
+}
+
+void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw,
+                c10::optional<torch::Tensor> ws, int64_t N, int64_t H, int64_t W, int64_t C,
+                int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad) {
+  auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
+  check_bf16(x, N * H * W * C, "x");
+  check_bf16(dy, (int64_t)g.M * Co, "dy");
+  check_f32(dw, Co * R * S * C, "dw");
+  TORCH_CHECK(dw.numel() == Co * R * S * C, "dw size");
+  auto p = mfl::plan_conv_wgrad(g);
+  float* wsp = nullptr;
+  if (p.splits > 1) {
+    TORCH_CHECK(ws.has_value() && ws->defined(), "wgrad split workspace required");
+    check_f32(*ws, (int64_t)p.splits * g.Ng * g.K, "workspace");
+    wsp = ws->data_ptr<float>();
+  }
+  mfl::launch_conv_wgrad(g, p, bf(x), bf(dy), dw.data_ptr<float>(), wsp, cur_stream(x));
+}
+
+void transpose_krsc(torch::Tensor w, torch::Tensor wt, int64_t Co, int64_t RS, int64_t Ci) {
+  check_bf16(w, Co * RS * Ci, "w");
+  check_bf16(wt, Co * RS * Ci, "wt");
+  mfl::launch_transpose_krsc(bf(w), bf(wt), (int)Co, (int)RS, (int)Ci, cur_stream(w));
+}
+
+// ---------------------------------------------------------------------------
+// Dense GEMM  C[M][N] = A[M][K] . B[N][K]^T  (+bias, +gelu, ...), bf16 in/out.
+void gemm_nt(torch::Tensor a, torch::Tensor b, torch::Tensor c, c10::optional<torch::Tensor> bias,
+             int64_t M, int64_t N, int64_t K, int64_t epilogue, c10::optional<torch::Tensor> aux) {
+  check_bf16(a, M * K, "a");
+  check_bf16(b, N * K, "b");
+  check_bf16(c, M * N, "c");
+  TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "gemm K and N must be multiples of 8");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_f32(*bias, N, "bias");
+    bp = bias->data_ptr<float>();
+  }
+  uint16_t* ap = nullptr;
+  if (aux.has_value() && aux->defined()) {
+    check_bf16(*aux, M * N, "aux");
+    ap = bf(*aux);
+  }
+  mfl::launch_gemm_nt(bf(a), bf(b), bf(c), bp, ap, (int)M, (int)N, (int)K, (int)epilogue,
+                      cur_stream(c));
+}
+
+}  // namespace
+
+void register_conv(pybind11::module& m) {
+  m.def("conv_plan", &conv_plan);
+  m.def("conv_forward", &conv_forward);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("transpose_krsc", &transpose_krsc);
+}
+
+void register_gemm(pybind11::module& m) { m.def("gemm_nt", &gemm_nt); }

@@ -1,0 +1,360 @@
+// torch binding for the metisfl_amd HIP kernels (module ``metisfl_amd._ops``).
+//
+// Every entry point validates shapes/dtypes on the host BEFORE launching (a
+// mis-shaped launch of a hand-written kernel can fault the whole GPU), then
+// launches on the caller's current HIP stream so that the call is capturable
+// into a hipGraph.  No function here allocates device memory.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <vector>
+
+#include "kernels/launchers.h"
+
+namespace {
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a device tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_T(t, dt) \
+  TORCH_CHECK((t).scalar_type() == (dt), #t " has dtype ", (t).scalar_type(), ", expected ", dt)
+#define CHECK_IN(t, dt) \
+  CHECK_DEV(t);         \
+  CHECK_CONTIG(t);      \
+  CHECK_T(t, dt)
+
+hipStream_t cur_stream(const torch::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+template <typename T>
+T* ptr_or_null(const c10::optional<torch::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  CHECK_DEV(*t);
+  CHECK_CONTIG(*t);
+  return reinterpret_cast<T*>(t->data_ptr());
+}
+
+uint16_t* bf(const torch::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+// --------------------------------------------------------------------------
+void fused_optimizer(int64_t mode, torch::Tensor p, torch::Tensor g,
+                     c10::optional<torch::Tensor> m, c10::optional<torch::Tensor> v,
+                     c10::optional<torch::Tensor> anchor, c10::optional<torch::Tensor> p16,
+                     double lr, double l1, double l2, double momentum, double mu, double beta1,
+                     double beta2, double eps, double wd, c10::optional<torch::Tensor> lr_scale,
+                     c10::optional<torch::Tensor> step) {
+  CHECK_IN(p, torch::kFloat32);
+  CHECK_IN(g, torch::kFloat32);
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n, "grad size mismatch");
+  TORCH_CHECK(n % 4 == 0, "flat buffers must be padded to a multiple of 4 elements");
+  auto need = [&](const c10::optional<torch::Tensor>& t, const char* nm) {
+    TORCH_CHECK(t.has_value() && t->defined(), nm, " is required for this optimizer");
+    CHECK_IN((*t), torch::kFloat32);
+    TORCH_CHECK(t->numel() == n, nm, " size mismatch");
+  };
+  if (mode == mfl::OPT_MOMENTUM) need(m, "momentum buffer");
+  if (mode == mfl::OPT_FEDPROX) need(anchor, "proximal anchor");
+  if (mode == mfl::OPT_ADAM || mode == mfl::OPT_ADAMW) {
+    need(m, "m");
+    need(v, "v");
+  }
+  if (p16.has_value() && p16->defined()) {
+    CHECK_IN((*p16), torch::kBFloat16);
+    TORCH_CHECK(p16->numel() == n, "bf16 copy size mismatch");
+  }
+  if (lr_scale.has_value() && lr_scale->defined()) CHECK_IN((*lr_scale), torch::kFloat32);
+  if (step.has_value() && step->defined()) CHECK_IN((*step), torch::kInt32);
+  mfl::OptHyper h;
+  h.lr = (float)lr; h.l1 = (float)l1; h.l2 = (float)l2; h.momentum = (float)momentum;
+  h.mu = (float)mu; h.beta1 = (float)beta1; h.beta2 = (float)beta2; h.eps = (float)eps;
+  h.wd = (float)wd;
+  mfl::launch_fused_optimizer((int)mode, p.data_ptr<float>(), g.data_ptr<float>(),
+                              ptr_or_null<float>(m), ptr_or_null<float>(v),
+                              ptr_or_null<float>(anchor), ptr_or_null<uint16_t>(p16), n, h,
+                              ptr_or_null<float>(lr_scale), ptr_or_null<int>(step), cur_stream(p));
+}
+
+void cast_f32_bf16(torch::Tensor x, torch::Tensor y) {
+  CHECK_IN(x, torch::kFloat32);
+  CHECK_IN(y, torch::kBFloat16);
+  TORCH_CHECK(x.numel() == y.numel() && x.numel() % 4 == 0, "cast size");
+  mfl::launch_cast_f32_bf16(x.data_ptr<float>(), bf(y), x.numel(), cur_stream(x));
+}
+
+void scale_f32(torch::Tensor x, double w, c10::optional<torch::Tensor> wdev) {
+  CHECK_IN(x, torch::kFloat32);
+  TORCH_CHECK(x.numel() % 4 == 0, "scale size");
+  mfl::launch_scale_f32(x.data_ptr<float>(), x.numel(), (float)w, ptr_or_null<float>(wdev),
+                        cur_stream(x));
+}
+
+void tick(torch::Tensor step, int64_t inc) {
+  CHECK_IN(step, torch::kInt32);
+  mfl::launch_tick(step.data_ptr<int>(), (int)inc, cur_stream(step));
+}
+
+// --------------------------------------------------------------------------
+int dtype_code(const torch::Tensor& t) {
+  switch (t.scalar_type()) {
+    case torch::kInt8: return 0;
+    case torch::kInt16: return 1;
+    case torch::kInt32: return 2;
+    case torch::kInt64: return 3;
+    case torch::kUInt8: return 4;
+    case torch::kUInt16: return 5;
+    case torch::kUInt32: return 6;
+    case torch::kUInt64: return 7;
+    case torch::kFloat32: return 8;
+    case torch::kFloat64: return 9;
+    default: TORCH_CHECK(false, "unsupported dtype for aggregation: ", t.scalar_type());
+  }
+  return -1;
+}
+
+void weighted_sum(torch::Tensor out, std::vector<torch::Tensor> xs, std::vector<double> ws) {
+  CHECK_DEV(out);
+  CHECK_CONTIG(out);
+  TORCH_CHECK(xs.size() == ws.size() && !xs.empty(), "inputs/weights mismatch");
+  const int code = dtype_code(out);
+  const int64_t n = out.numel();
+  for (auto& x : xs) {
+    CHECK_DEV(x);
+    CHECK_CONTIG(x);
+    TORCH_CHECK(x.scalar_type() == out.scalar_type() && x.numel() == n, "input mismatch");
+  }
+  // Process learners in the reference's order, 16 per launch, accumulating.
+  for (size_t base = 0; base < xs.size(); base += mfl::kMaxAggInputs) {
+    mfl::AggInputs in{};
+    in.count = (int)std::min<size_t>(mfl::kMaxAggInputs, xs.size() - base);
+    for (int k = 0; k < in.count; ++k) {
+      in.ptr[k] = xs[base + k].data_ptr();
+      in.w[k] = ws[base + k];
+    }
+    mfl::launch_weighted_sum(code, out.data_ptr(), in, n, base > 0, cur_stream(out));
+  }
+}
+
+void rolling_op(torch::Tensor y, c10::optional<torch::Tensor> x, int64_t op, double w) {
+  CHECK_DEV(y);
+  CHECK_CONTIG(y);
+  const void* xp = nullptr;
+  if (op <= 1) {
+    TORCH_CHECK(x.has_value() && x->defined(), "merge needs x");
+    CHECK_DEV(*x);
+    CHECK_CONTIG(*x);
+    TORCH_CHECK(x->scalar_type() == y.scalar_type() && x->numel() == y.numel(), "merge mismatch");
+    xp = x->data_ptr();
+  }
+  mfl::launch_axpby(dtype_code(y), y.data_ptr(), xp, (double)op, w, y.numel(), cur_stream(y));
+}
+
+void count_zeros(torch::Tensor x, torch::Tensor tile_seg, torch::Tensor tile_beg,
+                 torch::Tensor tile_end, torch::Tensor counts) {
+  CHECK_DEV(x);
+  CHECK_CONTIG(x);
+  CHECK_IN(tile_seg, torch::kInt64);
+  CHECK_IN(tile_beg, torch::kInt64);
+  CHECK_IN(tile_end, torch::kInt64);
+  CHECK_IN(counts, torch::kInt64);
+  const int nt = (int)tile_seg.numel();
+  TORCH_CHECK(tile_beg.numel() == nt && tile_end.numel() == nt, "tile table");
+  mfl::launch_count_zeros(dtype_code(x), x.data_ptr(), tile_seg.data_ptr<int64_t>(),
+                          tile_beg.data_ptr<int64_t>(), tile_end.data_ptr<int64_t>(), nt,
+                          reinterpret_cast<unsigned long long*>(counts.data_ptr<int64_t>()),
+                          cur_stream(x));
+}
+
+void ckks_pwa(torch::Tensor ptrs, torch::Tensor wq, torch::Tensor out, torch::Tensor moduli,
+              int64_t nlimbs, int64_t ncoef, int64_t nct) {
+  CHECK_IN(ptrs, torch::kInt64);
+  CHECK_IN(wq, torch::kInt64);
+  CHECK_IN(out, torch::kInt64);
+  CHECK_IN(moduli, torch::kInt64);
+  const int L = (int)ptrs.numel();
+  TORCH_CHECK(wq.numel() == (int64_t)L * nlimbs * 2, "wq size");
+  TORCH_CHECK(out.numel() == nct * 2 * nlimbs * ncoef, "out size");
+  TORCH_CHECK(moduli.numel() == nlimbs, "moduli size");
+  mfl::launch_ckks_pwa(reinterpret_cast<const uint64_t* const*>(ptrs.data_ptr<int64_t>()),
+                       reinterpret_cast<const uint64_t*>(wq.data_ptr<int64_t>()), L,
+                       reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>()),
+                       reinterpret_cast<const uint64_t*>(moduli.data_ptr<int64_t>()), (int)nlimbs,
+                       ncoef, nct, cur_stream(out));
+}
+
+// --------------------------------------------------------------------------
+void check_nhwc(const torch::Tensor& x, int64_t C) {
+  CHECK_IN(x, torch::kBFloat16);
+  TORCH_CHECK(x.numel() % C == 0, "NHWC tensor not divisible by C");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "BN channels must be a multiple of 8, <= 2048");
+}
+
+int64_t bn_stats_blocks(int64_t M, int64_t C) { return mfl::bn_stats_blocks(M, (int)C); }
+
+// Per-channel partial sums [rows][2][C] of an NHWC tensor; returns rows.
+int64_t bn_stats(torch::Tensor x, int64_t C, torch::Tensor partial) {
+  check_nhwc(x, C);
+  const int64_t M = x.numel() / C;
+  const int nb = mfl::bn_stats_blocks(M, (int)C);
+  CHECK_IN(partial, torch::kFloat32);
+  TORCH_CHECK(partial.numel() >= (int64_t)nb * 2 * C, "partial buffer too small");
+  mfl::launch_bn_stats(bf(x), M, (int)C, partial.data_ptr<float>(), nb, cur_stream(x));
+  return nb;
+}
+
+// partial rows -> mean/invstd/scale/shift (+ running-stat update).
+void bn_finalize(torch::Tensor partial, int64_t rows, int64_t M, int64_t C, torch::Tensor gamma,
+                 torch::Tensor beta, torch::Tensor mean, torch::Tensor invstd, torch::Tensor scale,
+                 torch::Tensor shift, c10::optional<torch::Tensor> run_mean,
+                 c10::optional<torch::Tensor> run_var, double momentum, double eps) {
+  CHECK_IN(partial, torch::kFloat32);
+  TORCH_CHECK(partial.numel() >= rows * 2 * C && rows > 0, "partial rows");
+  for (auto* t : {&gamma, &beta, &mean, &invstd, &scale, &shift}) {
+    CHECK_IN((*t), torch::kFloat32);
+    TORCH_CHECK(t->numel() == C, "per-channel tensor size");
+  }
+  mfl::launch_bn_finalize(partial.data_ptr<float>(), (int)rows, M, (int)C, gamma.data_ptr<float>(),
+                          beta.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                          scale.data_ptr<float>(), shift.data_ptr<float>(),
+                          ptr_or_null<float>(run_mean), ptr_or_null<float>(run_var),
+                          (float)momentum, (float)eps, cur_stream(partial));
+}
+
+void bn_apply(torch::Tensor x, int64_t C, torch::Tensor scale, torch::Tensor shift,
+              c10::optional<torch::Tensor> residual, torch::Tensor y, bool relu) {
+  check_nhwc(x, C);
+  check_nhwc(y, C);
+  TORCH_CHECK(y.numel() == x.numel(), "bn y size");
+  CHECK_IN(scale, torch::kFloat32);
+  CHECK_IN(shift, torch::kFloat32);
+  TORCH_CHECK(scale.numel() == C && shift.numel() == C, "scale/shift size");
+  const uint16_t* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    check_nhwc(*residual, C);
+    TORCH_CHECK(residual->numel() == x.numel(), "residual size");
+    rp = bf(*residual);
+  }
+  mfl::launch_bn_apply(bf(x), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, bf(y),
+                       x.numel() / C, (int)C, relu, cur_stream(x));
+}
+
+void bn_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,
+                 torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd,
+                 torch::Tensor partial, torch::Tensor coef, c10::optional<torch::Tensor> dgamma,
+                 c10::optional<torch::Tensor> dbeta, torch::Tensor dx,
+                 c10::optional<torch::Tensor> dy_masked) {
+  check_nhwc(dy, C);
+  check_nhwc(x, C);
+  check_nhwc(dx, C);
+  TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel(), "bn bwd sizes");
+  const uint16_t* yp = nullptr;
+  if (y.has_value() && y->defined()) {
+    check_nhwc(*y, C);
+    TORCH_CHECK(y->numel() == x.numel(), "bn bwd y");
+    yp = bf(*y);
+  }
+  uint16_t* dym = nullptr;
+  if (dy_masked.has_value() && dy_masked->defined()) {
+    check_nhwc(*dy_masked, C);
+    TORCH_CHECK(yp != nullptr, "dy_masked requires y");
+    dym = bf(*dy_masked);
+  }
+  CHECK_IN(coef, torch::kFloat32);
+  TORCH_CHECK(coef.numel() >= 3 * C, "coef size");
+  const int64_t M = x.numel() / C;
+  const int nb = mfl::bn_stats_blocks(M, (int)C);
+  TORCH_CHECK(partial.numel() >= (int64_t)nb * 2 * C, "partial buffer too small");
+  auto s = cur_stream(x);
+  mfl::launch_bn_bwd_reduce(bf(dy), bf(x), yp, mean.data_ptr<float>(), invstd.data_ptr<float>(), M,
+                            (int)C, partial.data_ptr<float>(), nb, s);
+  mfl::launch_bn_bwd_finalize(partial.data_ptr<float>(), nb, M, (int)C, gamma.data_ptr<float>(),
+                              invstd.data_ptr<float>(), ptr_or_null<float>(dgamma),
+                              ptr_or_null<float>(dbeta), coef.data_ptr<float>(), s);
+  mfl::launch_bn_bwd_apply(bf(dy), bf(x), yp, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                           coef.data_ptr<float>(), bf(dx), dym, M, (int)C, s);
+}
+
+// --------------------------------------------------------------------------
+void head_forward_backward(torch::Tensor x, int64_t B, int64_t HW, int64_t C, torch::Tensor W,
+                           c10::optional<torch::Tensor> bias, torch::Tensor labels,
+                           c10::optional<torch::Tensor> feat, c10::optional<torch::Tensor> dlogits,
+                           c10::optional<torch::Tensor> dx, c10::optional<torch::Tensor> stats,
+                           bool backward) {
+  CHECK_IN(x, torch::kBFloat16);
+  TORCH_CHECK(x.numel() == B * HW * C, "head x size");
+  CHECK_IN(W, torch::kFloat32);
+  TORCH_CHECK(W.numel() % C == 0, "head W");
+  const int64_t K = W.numel() / C;
+  CHECK_IN(labels, torch::kInt32);
+  TORCH_CHECK(labels.numel() >= B, "labels");
+  TORCH_CHECK(C + K <= 16384, "head too large for LDS");
+  if (backward) {
+    TORCH_CHECK(feat.has_value() && dlogits.has_value() && dx.has_value(), "bwd buffers");
+    TORCH_CHECK(feat->numel() >= B * C && dlogits->numel() >= B * K, "bwd buffer sizes");
+    CHECK_IN((*dx), torch::kBFloat16);
+    TORCH_CHECK(dx->numel() == x.numel(), "dx size");
+  }
+  mfl::launch_head_fwd_bwd(bf(x), (int)B, (int)HW, (int)C, W.data_ptr<float>(),
+                           ptr_or_null<float>(bias), (int)K, labels.data_ptr<int>(),
+                           ptr_or_null<float>(feat), ptr_or_null<float>(dlogits),
+                           dx.has_value() && dx->defined() ? bf(*dx) : nullptr,
+                           ptr_or_null<float>(stats), backward, cur_stream(x));
+}
+
+void head_wgrad(torch::Tensor feat, torch::Tensor dlogits, int64_t B, int64_t C, int64_t K,
+                torch::Tensor dW, c10::optional<torch::Tensor> db) {
+  CHECK_IN(feat, torch::kFloat32);
+  CHECK_IN(dlogits, torch::kFloat32);
+  CHECK_IN(dW, torch::kFloat32);
+  TORCH_CHECK(feat.numel() >= B * C && dlogits.numel() >= B * K && dW.numel() == K * C, "wgrad");
+  mfl::launch_head_wgrad(feat.data_ptr<float>(), dlogits.data_ptr<float>(), (int)B, (int)C, (int)K,
+                         dW.data_ptr<float>(), ptr_or_null<float>(db), cur_stream(feat));
+}
+
+void gather_batch(torch::Tensor shard, torch::Tensor labels, torch::Tensor perm,
+                  torch::Tensor step, int64_t steps_per_epoch, int64_t B, torch::Tensor xb,
+                  torch::Tensor yb) {
+  CHECK_IN(shard, torch::kBFloat16);
+  CHECK_IN(labels, torch::kInt32);
+  CHECK_IN(perm, torch::kInt32);
+  CHECK_IN(step, torch::kInt32);
+  CHECK_IN(xb, torch::kBFloat16);
+  CHECK_IN(yb, torch::kInt32);
+  const int64_t n = labels.numel();
+  TORCH_CHECK(n > 0 && shard.numel() % n == 0, "shard rows");
+  const int64_t row = shard.numel() / n;
+  TORCH_CHECK(row % 8 == 0, "row must be a multiple of 8 elements");
+  TORCH_CHECK(xb.numel() == B * row && yb.numel() >= B, "batch buffers");
+  TORCH_CHECK(perm.numel() >= steps_per_epoch * B, "permutation too short");
+  TORCH_CHECK(perm.numel() <= n || true, "");
+  mfl::launch_gather_batch(bf(shard), labels.data_ptr<int>(), perm.data_ptr<int>(),
+                           step.data_ptr<int>(), (int)steps_per_epoch, (int)B, row, bf(xb),
+                           yb.data_ptr<int>(), cur_stream(shard));
+}
+
+}  // namespace
+
+void register_conv(pybind11::module& m);
+void register_gemm(pybind11::module& m);
+
+PYBIND11_MODULE(_ops, m) {
+  m.doc() = "metisfl_amd hand-written HIP (gfx950) kernels";
+  m.def("fused_optimizer", &fused_optimizer);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("scale_f32", &scale_f32);
+  m.def("tick", &tick);
+  m.def("weighted_sum", &weighted_sum);
+  m.def("rolling_op", &rolling_op);
+  m.def("count_zeros", &count_zeros);
+  m.def("ckks_pwa", &ckks_pwa);
+  m.def("bn_stats_blocks", &bn_stats_blocks);
+  m.def("bn_stats", &bn_stats);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_backward", &bn_backward);
+  m.def("head_forward_backward", &head_forward_backward);
+  m.def("head_wgrad", &head_wgrad);
+  m.def("gather_batch", &gather_batch);
+  register_conv(m);
+  register_gemm(m);
+}

@@ -1,0 +1,44 @@
+// Convolution geometry / launch plans shared by conv.hip and its binding.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mfl {
+
+// Implicit-GEMM geometry.  For the forward pass (and wgrad):
+//   H, W, C : input activation dims (NHWC, C % 8 == 0)
+//   P, Q    : output spatial dims
+//   M       : N * P * Q      (GEMM rows; for wgrad the reduction length)
+//   K       : R * S * C      (GEMM reduction; for wgrad the output columns)
+//   Ng      : Cout
+// For dgrad the roles swap: H, W, C describe dY, P, Q the dX spatial dims,
+// Ng = Cin and K = R * S * Cout.
+struct ConvGeom {
+  int N, H, W, C;
+  int P, Q;
+  int R, S, stride, pad;
+  int M, K, Ng;
+};
+
+struct ConvPlan {
+  int bm = 64, bn = 64;
+  int splits = 1;
+  int kchunk = 0;      // reduction elements per split (multiple of 64)
+  int stats_rows = 0;  // BN partial rows written by the epilogue (0 = by split reduce)
+};
+
+ConvPlan plan_conv_gemm(const ConvGeom& g);
+ConvPlan plan_conv_wgrad(const ConvGeom& g);
+int splitk_stats_blocks(int M, int C);
+
+// y (bf16 [M][Ng]) and, when stats != nullptr, BN partial sums
+// [rows][2][Ng] (rows = plan.stats_rows, or splitk_stats_blocks() when split).
+void launch_conv_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const uint16_t* src,
+                      const uint16_t* wgt, uint16_t* y, float* ysplit, float* stats, bool accum,
+                      hipStream_t s);
+// dw (fp32 [Cout][R][S][Cin]); wsplit workspace [splits][Cout*K] when split.
+void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, const uint16_t* dy,
+                       float* dw, float* wsplit, hipStream_t s);
+void launch_transpose_krsc(const uint16_t* w, uint16_t* wt, int Co, int RS, int Ci, hipStream_t s);
+
+}  // namespace mfl

@@ -1,0 +1,80 @@
+// Host-callable launch functions for the HIP kernels.  Every launcher takes
+// the HIP stream explicitly, allocates nothing and never synchronises, so all
+// of them are legal inside hipGraph capture (cdna_hip_programming.md G9).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mfl {
+
+enum OptMode { OPT_SGD = 0, OPT_MOMENTUM = 1, OPT_FEDPROX = 2, OPT_ADAM = 3, OPT_ADAMW = 4 };
+
+struct OptHyper {
+  float lr = 0.01f;
+  float l1 = 0.f, l2 = 0.f;
+  float momentum = 0.f;
+  float mu = 0.f;
+  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-7f;
+  float wd = 0.f;
+};
+
+// ---- optim.hip -----------------------------------------------------------
+void launch_fused_optimizer(int mode, float* p, const float* g, float* m, float* v,
+                            const float* anchor, uint16_t* p16, int64_t n, const OptHyper& h,
+                            const float* lr_ptr, const int* step_ptr, hipStream_t s);
+void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
+void launch_scale_f32(float* x, int64_t n, float w, const float* wptr, hipStream_t s);
+void launch_tick(int* step, int inc, hipStream_t s);
+
+// ---- aggregate.hip -------------------------------------------------------
+// dtype codes follow metisfl DType.Type (model.proto): INT8=0 .. FLOAT64=9
+constexpr int kMaxAggInputs = 16;
+struct AggInputs {
+  const void* ptr[kMaxAggInputs];
+  double w[kMaxAggInputs];
+  int count;
+};
+void launch_weighted_sum(int dtype, void* out, const AggInputs& in, int64_t n, bool accumulate,
+                         hipStream_t s);
+void launch_axpby(int dtype, void* y, const void* x, double a, double b, int64_t n, hipStream_t s);
+void launch_count_zeros(int dtype, const void* x, const int64_t* tile_seg, const int64_t* tile_beg,
+                        const int64_t* tile_end, int ntiles, unsigned long long* counts,
+                        hipStream_t s);
+// Exact-form fp32 scaled all-reduce pre-pass: y = (float)((double)x * w)
+void launch_ckks_pwa(const uint64_t* const* cts, const uint64_t* wq, int nlearners, uint64_t* out,
+                     const uint64_t* moduli, int nlimbs, int64_t coeffs_per_limb, int64_t nct,
+                     hipStream_t s);
+
+// ---- bn.hip --------------------------------------------------------------
+void launch_bn_stats(const uint16_t* x, int64_t M, int C, float* partial, int nblocks,
+                     hipStream_t s);
+int bn_stats_blocks(int64_t M, int C);
+void launch_bn_finalize(const float* partial, int nblocks, int64_t M, int C, const float* gamma,
+                        const float* beta, float* mean, float* invstd, float* scale, float* shift,
+                        float* run_mean, float* run_var, float momentum, float eps, hipStream_t s);
+void launch_bn_apply(const uint16_t* x, const float* scale, const float* shift,
+                     const uint16_t* residual, uint16_t* y, int64_t M, int C, bool relu,
+                     hipStream_t s);
+void launch_bn_bwd_reduce(const uint16_t* dy, const uint16_t* x, const uint16_t* y,
+                          const float* mean, const float* invstd, int64_t M, int C, float* partial,
+                          int nblocks, hipStream_t s);
+void launch_bn_bwd_finalize(const float* partial, int nblocks, int64_t M, int C,
+                            const float* gamma, const float* invstd, float* dgamma, float* dbeta,
+                            float* coef, hipStream_t s);
+void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uint16_t* y,
+                         const float* mean, const float* invstd, const float* coef, uint16_t* dx,
+                         uint16_t* dy_masked, int64_t M, int C, hipStream_t s);
+
+// ---- head.hip ------------------------------------------------------------
+void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,
+                         int K, const int* labels, float* feat, float* dlogits, uint16_t* dx,
+                         float* stats, bool backward, hipStream_t s);
+void launch_head_wgrad(const float* feat, const float* dlogits, int B, int C, int K, float* dW,
+                       float* db, hipStream_t s);
+
+// ---- data.hip ------------------------------------------------------------
+void launch_gather_batch(const uint16_t* shard, const int* labels, const int* perm,
+                         const int* step, int steps_per_epoch, int B, int64_t row_elems,
+                         uint16_t* xb, int* yb, hipStream_t s);
+
+}  // namespace mfl

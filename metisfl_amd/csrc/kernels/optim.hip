@@ -1,0 +1,158 @@
+// K3/K4/K5: fused multi-tensor optimizers over a flat fp32 master buffer.
+//
+// Replaces the per-variable optimizer application the reference delegates to
+// Keras (metisfl/models/keras/keras_model_ops.py:245-283) and the FedProx
+// optimizer (metisfl/models/keras/optimizers/fed_prox.py:50-60).  Every
+// trainable variable of a learner lives in ONE flat fp32 buffer, so a whole
+// optimizer step is a single streaming launch that also refreshes the bf16
+// compute copy of the weights (no separate cast pass).  The learning rate and
+// the step counter are read from device memory so the launch can sit inside a
+// captured hipGraph and still follow a schedule.
+//
+// FedProx deviation (documented): the proximal anchor is
+// the community model the learner received this round, not a zero slot.
+#include "kernels/common.h"
+#include "kernels/launchers.h"
+
+namespace mfl {
+
+template <int MODE, bool W16>
+__global__ __launch_bounds__(256) void fused_opt_kernel(
+    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+    float* __restrict__ v, const float* __restrict__ anchor, uint16_t* __restrict__ p16,
+    int64_t n4, OptHyper h, const float* __restrict__ lr_ptr, const int* __restrict__ step_ptr) {
+  const float lr = lr_ptr ? lr_ptr[0] * h.lr : h.lr;
+  float bc1 = 1.f, bc2 = 1.f;
+  if (MODE == OPT_ADAM || MODE == OPT_ADAMW) {
+    const float t = (float)(step_ptr ? step_ptr[0] + 1 : 1);
+    bc1 = 1.f - powf(h.beta1, t);
+    bc2 = 1.f - powf(h.beta2, t);
+  }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float* pp = &pv.x;
+    const float* gg = &gv.x;
+    if (MODE == OPT_SGD) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float gr = gg[k] + h.l2 * pp[k];
+        if (h.l1 != 0.f) gr += h.l1 * ((pp[k] > 0.f) - (pp[k] < 0.f));
+        pp[k] -= lr * gr;
+      }
+    } else if (MODE == OPT_MOMENTUM) {
+      // Keras SGD(momentum) form: v = mu*v - lr*g ; p += v
+      float4 mv = reinterpret_cast<float4*>(m)[i];
+      float* mm = &mv.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        mm[k] = h.momentum * mm[k] - lr * gg[k];
+        pp[k] += mm[k];
+      }
+      reinterpret_cast<float4*>(m)[i] = mv;
+    } else if (MODE == OPT_FEDPROX) {
+      const float4 av = reinterpret_cast<const float4*>(anchor)[i];
+      const float* aa = &av.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pp[k] -= lr * (gg[k] + h.mu * (pp[k] - aa[k]));
+    } else {  // Adam / AdamW
+      float4 mv = reinterpret_cast<float4*>(m)[i];
+      float4 vv = reinterpret_cast<float4*>(v)[i];
+      float* mm = &mv.x;
+      float* vq = &vv.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        mm[k] = h.beta1 * mm[k] + (1.f - h.beta1) * gg[k];
+        vq[k] = h.beta2 * vq[k] + (1.f - h.beta2) * gg[k] * gg[k];
+        const float mh = mm[k] / bc1;
+        const float vh = vq[k] / bc2;
+        float upd = mh / (sqrtf(vh) + h.eps);
+        if (MODE == OPT_ADAMW) upd += h.wd * pp[k];
+        pp[k] -= lr * upd;
+      }
+      reinterpret_cast<float4*>(m)[i] = mv;
+      reinterpret_cast<float4*>(v)[i] = vv;
+    }
+    reinterpret_cast<float4*>(p)[i] = pv;
+    if (W16) {
+      uint2 o;
+      o.x = pack2bf(pp[0], pp[1]);
+      o.y = pack2bf(pp[2], pp[3]);
+      reinterpret_cast<uint2*>(p16)[i] = o;
+    }
+  }
+}
+
+template <int MODE>
+static void launch_mode(float* p, const float* g, float* m, float* v, const float* anchor,
+                        uint16_t* p16, int64_t n, const OptHyper& h, const float* lr_ptr,
+                        const int* step_ptr, hipStream_t s) {
+  const int64_t n4 = n / 4;
+  const unsigned grid = stream_grid(n4, 256, 2048);
+  if (p16)
+    fused_opt_kernel<MODE, true><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr, step_ptr);
+  else
+    fused_opt_kernel<MODE, false><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr, step_ptr);
+}
+
+void launch_fused_optimizer(int mode, float* p, const float* g, float* m, float* v,
+                            const float* anchor, uint16_t* p16, int64_t n, const OptHyper& h,
+                            const float* lr_ptr, const int* step_ptr, hipStream_t s) {
+  switch (mode) {
+    case OPT_SGD: launch_mode<OPT_SGD>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, s); break;
+    case OPT_MOMENTUM: launch_mode<OPT_MOMENTUM>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, s); break;
+    case OPT_FEDPROX: launch_mode<OPT_FEDPROX>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, s); break;
+    case OPT_ADAM: launch_mode<OPT_ADAM>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, s); break;
+    case OPT_ADAMW: launch_mode<OPT_ADAMW>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, s); break;
+    default: break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp32 -> bf16 cast of a flat buffer (community-model refresh of the compute
+// copy after the RCCL all-reduce), optionally scaled.
+__global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ x,
+                                                         uint16_t* __restrict__ y, int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 a = reinterpret_cast<const float4*>(x)[i];
+    uint2 o;
+    o.x = pack2bf(a.x, a.y);
+    o.y = pack2bf(a.z, a.w);
+    reinterpret_cast<uint2*>(y)[i] = o;
+  }
+}
+
+void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s) {
+  const int64_t n4 = n / 4;
+  cast_bf16_kernel<<<stream_grid(n4), 256, 0, s>>>(x, y, n4);
+}
+
+// In-place x *= w  (K1 pre-scale before the all-reduce).  The weight comes
+// from device memory when wptr != nullptr so it can be decided on device.
+__global__ __launch_bounds__(256) void scale_kernel(float* __restrict__ x, int64_t n4, float w,
+                                                     const float* __restrict__ wptr) {
+  const float a = wptr ? wptr[0] : w;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 v = reinterpret_cast<float4*>(x)[i];
+    v.x *= a; v.y *= a; v.z *= a; v.w *= a;
+    reinterpret_cast<float4*>(x)[i] = v;
+  }
+}
+
+void launch_scale_f32(float* x, int64_t n, float w, const float* wptr, hipStream_t s) {
+  const int64_t n4 = n / 4;
+  scale_kernel<<<stream_grid(n4), 256, 0, s>>>(x, n4, w, wptr);
+}
+
+// Scale + cast in one pass: y16 = bf16(x), used after the all-reduce when the
+// averaged model must be copied into the compute copy.
+__global__ void tick_kernel(int* step, int inc) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) step[0] += inc;
+}
+
+void launch_tick(int* step, int inc, hipStream_t s) { tick_kernel<<<1, 64, 0, s>>>(step, inc); }
+
+}  // namespace mfl

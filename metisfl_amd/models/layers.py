@@ -1,0 +1,232 @@
+"""Static-graph layers for the learner's local training step.
+
+A model is a fixed sequence of layers with a fixed batch size, so every
+activation, gradient and workspace buffer is planned once (memory is sized
+for 288 GB of HBM per learner -- nothing is allocated per step) and the whole
+step -- batch gather, forward, loss, backward, optimizer -- is a pure
+sequence of kernel launches on one HIP stream that is captured into a
+hipGraph (see models/net.py).  There is no autograd tape: each layer owns its
+backward and writes weight gradients straight into the flat fp32 gradient
+buffer (models/flat.py), so there is no gradient accumulation pass and no
+per-parameter launch.
+
+These layers replace the Keras layers the reference trains with
+(examples/keras/models/cifar_cnn.py, fashion_mnist_fc.py).
+"""
+from __future__ import annotations
+
+import torch
+
+from metisfl_amd.models.flat import FlatState, VarSpec
+from metisfl_amd.ops import nn as K
+from metisfl_amd.ops.nn import ConvShape
+
+
+class Workspace:
+    """Shared scratch: split-K slabs and BatchNorm partial sums.  Kernels on
+    one stream run in order, so one buffer of the maximum size serves all."""
+
+    def __init__(self):
+        self.split_floats = 0
+        self.partial_floats = 0
+        self.split: torch.Tensor | None = None
+        self.partial: torch.Tensor | None = None
+        self.coef_floats = 0
+        self.coef: torch.Tensor | None = None
+
+    def need_split(self, n: int) -> None:
+        self.split_floats = max(self.split_floats, n)
+
+    def need_partial(self, n: int) -> None:
+        self.partial_floats = max(self.partial_floats, n)
+
+    def need_coef(self, n: int) -> None:
+        self.coef_floats = max(self.coef_floats, n)
+
+    def allocate(self, device) -> None:
+        self.split = torch.zeros(max(4, self.split_floats), dtype=torch.float32, device=device)
+        self.partial = torch.zeros(max(4, self.partial_floats), dtype=torch.float32, device=device)
+        self.coef = torch.zeros(max(4, self.coef_floats), dtype=torch.float32, device=device)
+
+
+class Layer:
+    def specs(self) -> list[VarSpec]:
+        return []
+
+    def bind(self, st: FlatState, ws: Workspace, device) -> None:
+        pass
+
+    def prepare_backward(self) -> None:
+        """Per-step weight re-layouts needed by backward (after optimizer)."""
+
+
+class ConvBN(Layer):
+    """conv(k x k, stride) -> BatchNorm -> [+ residual] -> [ReLU], NHWC bf16."""
+
+    def __init__(self, name: str, N: int, H: int, W: int, cin: int, cout: int, k: int,
+                 stride: int, relu: bool = True, residual: bool = False, momentum: float = 0.1,
+                 eps: float = 1e-5, need_dgrad: bool = True):
+        self.name = name
+        self.shp = ConvShape(N, H, W, cin, cout, k, k, stride, k // 2)
+        self.relu = relu
+        self.residual = residual
+        self.momentum = momentum
+        self.eps = eps
+        self.need_dgrad = need_dgrad
+        self.P, self.Q = self.shp.P, self.shp.Q
+        self.M = N * self.P * self.Q
+
+    @property
+    def out_shape(self):
+        return (self.shp.N, self.P, self.Q, self.shp.Co)
+
+    def specs(self):
+        s, n = self.shp, self.name
+        fan_in = s.R * s.S * s.C
+        return [
+            VarSpec(f"{n}.conv.weight", (s.Co, s.R, s.S, s.C), True, "he_normal", fan_in=fan_in),
+            VarSpec(f"{n}.bn.gamma", (s.Co,), True, "ones"),
+            VarSpec(f"{n}.bn.beta", (s.Co,), True, "zeros"),
+            VarSpec(f"{n}.bn.moving_mean", (s.Co,), False, "zeros"),
+            VarSpec(f"{n}.bn.moving_variance", (s.Co,), False, "ones"),
+        ]
+
+    def bind(self, st: FlatState, ws: Workspace, device):
+        s, n = self.shp, self.name
+        self.st = st
+        self.ws = ws
+        self.w16 = st.bf16(f"{n}.conv.weight")
+        self.dw = st.grad(f"{n}.conv.weight")
+        self.gamma = st.view(f"{n}.bn.gamma")
+        self.beta = st.view(f"{n}.bn.beta")
+        self.dgamma = st.grad(f"{n}.bn.gamma")
+        self.dbeta = st.grad(f"{n}.bn.beta")
+        self.rmean = st.view(f"{n}.bn.moving_mean")
+        self.rvar = st.view(f"{n}.bn.moving_variance")
+        bf = dict(dtype=torch.bfloat16, device=device)
+        f32 = dict(dtype=torch.float32, device=device)
+        self.z = torch.zeros(self.out_shape, **bf)      # conv output (pre-BN)
+        self.y = torch.zeros(self.out_shape, **bf)      # layer output
+        self.dz = torch.zeros(self.out_shape, **bf)
+        self.mean = torch.zeros(s.Co, **f32)
+        self.invstd = torch.zeros(s.Co, **f32)
+        self.scale = torch.zeros(s.Co, **f32)
+        self.shift = torch.zeros(s.Co, **f32)
+        dev = torch.device(device)
+        self.pf = K.conv_plan(0, s, dev)
+        self.pd = K.conv_plan(1, s, dev)
+        self.pw = K.conv_plan(2, s, dev)
+        ws.need_split(self.pf.workspace)
+        ws.need_split(self.pd.workspace)
+        ws.need_split(self.pw.workspace)
+        self.bn_rows = K.bn_stats_rows(self.M, s.Co, dev)
+        ws.need_partial(max(self.pf.stats_rows, self.bn_rows) * 2 * s.Co)
+        ws.need_coef(3 * s.Co)
+
+    def forward(self, x: torch.Tensor, residual: torch.Tensor | None = None, train: bool = True):
+        s = self.shp
+        self.x = x
+        if train:
+            K.conv_forward(x, self.w16, self.z, s, self.ws.split, self.ws.partial)
+            K.bn_finalize(self.ws.partial, self.pf.stats_rows, self.M, s.Co, self.gamma, self.beta,
+                          self.mean, self.invstd, self.scale, self.shift, self.rmean, self.rvar,
+                          self.momentum, self.eps)
+        else:
+            K.conv_forward(x, self.w16, self.z, s, self.ws.split, None)
+            torch.rsqrt(self.rvar + self.eps, out=self.scale)
+            self.scale.mul_(self.gamma)
+            torch.mul(self.rmean, self.scale, out=self.shift)
+            torch.sub(self.beta, self.shift, out=self.shift)
+        K.bn_apply(self.z, s.Co, self.scale, self.shift, self.y, residual, self.relu)
+        return self.y
+
+    def backward(self, dy: torch.Tensor, dx: torch.Tensor | None, accumulate: bool = False,
+                 dres: torch.Tensor | None = None) -> None:
+        """dy: gradient w.r.t. this layer's output.  Writes dgamma/dbeta/dW into
+        the flat gradient buffer and (if dx is given) d input into dx; ``dres``
+        receives the ReLU-masked dy that the residual branch needs."""
+        s = self.shp
+        K.bn_backward(dy, self.z, self.y if self.relu else None, s.Co, self.gamma, self.mean,
+                      self.invstd, self.ws.partial, self.ws.coef, self.dgamma, self.dbeta, self.dz,
+                      dres)
+        if dx is not None:
+            K.conv_dgrad(self.dz, self.w16, dx, s, self.ws.split, accumulate)
+        K.conv_wgrad(self.x, self.dz, self.dw, s, self.ws.split)
+
+
+class BasicBlock(Layer):
+    """ResNet basic block: relu(bn2(conv2(relu(bn1(conv1(x))))) + shortcut(x))."""
+
+    def __init__(self, name: str, N: int, H: int, W: int, cin: int, cout: int, stride: int):
+        self.name = name
+        self.c1 = ConvBN(f"{name}.conv1", N, H, W, cin, cout, 3, stride, relu=True)
+        P, Q = self.c1.P, self.c1.Q
+        self.c2 = ConvBN(f"{name}.conv2", N, P, Q, cout, cout, 3, 1, relu=True, residual=True)
+        self.sc = None
+        if stride != 1 or cin != cout:
+            self.sc = ConvBN(f"{name}.shortcut", N, H, W, cin, cout, 1, stride, relu=False)
+        self.out_shape = self.c2.out_shape
+        self.in_shape = (N, H, W, cin)
+
+    def sublayers(self):
+        return [l for l in (self.c1, self.c2, self.sc) if l is not None]
+
+    def specs(self):
+        return [v for l in self.sublayers() for v in l.specs()]
+
+    def bind(self, st, ws, device):
+        for l in self.sublayers():
+            l.bind(st, ws, device)
+        self.da = torch.zeros(self.c1.out_shape, dtype=torch.bfloat16, device=device)
+        self.dres = None
+        if self.sc is not None:
+            self.dres = torch.zeros(self.out_shape, dtype=torch.bfloat16, device=device)
+
+    def prepare_backward(self):
+        for l in self.sublayers():
+            l.prepare_backward()
+
+    def forward(self, x, train=True):
+        a = self.c1.forward(x, train=train)
+        r = self.sc.forward(x, train=train) if self.sc is not None else x
+        return self.c2.forward(a, residual=r, train=train)
+
+    def backward(self, dout, dx):
+        if self.sc is None:
+            # identity shortcut: masked dout goes straight into dx, conv1's
+            # dgrad then accumulates onto it (no add kernel)
+            self.c2.backward(dout, self.da, dres=dx)
+            self.c1.backward(self.da, dx, accumulate=True)
+        else:
+            self.c2.backward(dout, self.da, dres=self.dres)
+            self.sc.backward(self.dres, dx)
+            self.c1.backward(self.da, dx, accumulate=True)
+
+
+class ClassifierHead(Layer):
+    """Global average pool + Linear(C -> K) + softmax cross-entropy, fused."""
+
+    def __init__(self, name: str, N: int, HW: int, C: int, K_: int):
+        self.name, self.N, self.HW, self.C, self.K = name, N, HW, C, K_
+
+    def specs(self):
+        return [VarSpec(f"{self.name}.kernel", (self.K, self.C), True, "glorot_uniform",
+                        fan_in=self.C, fan_out=self.K),
+                VarSpec(f"{self.name}.bias", (self.K,), True, "zeros")]
+
+    def bind(self, st, ws, device):
+        self.W = st.view(f"{self.name}.kernel")
+        self.b = st.view(f"{self.name}.bias")
+        self.dW = st.grad(f"{self.name}.kernel")
+        self.db = st.grad(f"{self.name}.bias")
+        f32 = dict(dtype=torch.float32, device=device)
+        self.feat = torch.zeros(self.N * self.C, **f32)
+        self.dlogits = torch.zeros(self.N * self.K, **f32)
+        self.dx = torch.zeros((self.N, self.HW, self.C), dtype=torch.bfloat16, device=device)
+
+    def forward_backward(self, x, labels, stats, train=True):
+        K.head_forward_backward(x, self.N, self.HW, self.C, self.W, self.b, labels, self.feat,
+                                self.dlogits, self.dx, stats, backward=train)
+        if train:
+            K.head_wgrad(self.feat, self.dlogits, self.N, self.C, self.K, self.dW, self.db)
+        return self.dx

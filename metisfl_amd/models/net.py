@@ -1,0 +1,209 @@
+"""StaticNet: a learner model whose whole training step is one hipGraph.
+
+The reference delegates the local SGD loop to ``keras.Model.fit`` with a
+step-counter callback (metisfl/models/keras/keras_model_ops.py:117-197,
+callbacks/step_counter.py:39-45).  Here a step is: device-side batch gather
+-> forward -> fused loss/head -> backward -> ONE fused optimizer launch ->
+step-counter tick, all recorded once into a HIP graph and replayed, so the
+host issues one graph launch per local update and never synchronises inside
+a task.  Loss / accuracy are accumulated on device and read once per task.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from metisfl_amd.models.flat import FlatState, VarSpec
+from metisfl_amd.models.layers import Layer, Workspace
+from metisfl_amd.ops import nn as K
+from metisfl_amd.ops import optim as opt_ops
+from metisfl_amd.ops.optim import OptimizerSpec
+
+
+class DeviceDataset:
+    """A learner's shard resident in device memory (bf16 NHWC rows, int32
+    labels) plus a per-epoch permutation buffer.  Rows are padded so each is a
+    multiple of 8 elements (16-B vector gathers)."""
+
+    def __init__(self, x: torch.Tensor, y: torch.Tensor, batch_size: int, seed: int = 0,
+                 shuffle: bool = True, drop_last: bool = True):
+        assert x.shape[0] == y.shape[0]
+        self.x = x.contiguous()
+        self.y = y.to(torch.int32).contiguous()
+        self.n = int(x.shape[0])
+        self.batch_size = batch_size
+        self.steps_per_epoch = max(1, self.n // batch_size) if drop_last else max(1, -(-self.n // batch_size))
+        self.shuffle = shuffle
+        self.gen = torch.Generator(device="cpu")
+        self.gen.manual_seed(seed)
+        self.perm = torch.zeros(self.steps_per_epoch * batch_size, dtype=torch.int32, device=x.device)
+        self.reshuffle()
+
+    def reshuffle(self) -> None:
+        need = self.steps_per_epoch * self.batch_size
+        if self.shuffle:
+            p = torch.randperm(self.n, generator=self.gen)
+        else:
+            p = torch.arange(self.n)
+        if p.numel() < need:  # last partial batch wraps around
+            p = torch.cat([p, p[: need - p.numel()]])
+        self.perm.copy_(p[:need].to(torch.int32), non_blocking=True)
+
+    @property
+    def row_shape(self):
+        return tuple(self.x.shape[1:])
+
+
+class StaticNet:
+    """Base class: subclasses build ``self.layers`` / ``self.head`` via
+    ``build()`` and implement ``forward``/``backward``."""
+
+    input_channels_padded: int = 8
+    num_classes: int = 10
+
+    def __init__(self, batch_size: int, device="cpu", optimizer: OptimizerSpec | None = None,
+                 seed: int = 0):
+        self.B = batch_size
+        self.device = torch.device(device)
+        self.build()
+        specs: list[VarSpec] = []
+        for l in self.all_layers():
+            specs.extend(l.specs())
+        self.state = FlatState(specs, self.device, optimizer or OptimizerSpec(), seed=seed)
+        self.ws = Workspace()
+        for l in self.all_layers():
+            l.bind(self.state, self.ws, self.device)
+        self.ws.allocate(self.device)
+        self.post_bind()
+        dev = self.device
+        self.xb = torch.zeros((self.B,) + self.input_shape, dtype=torch.bfloat16, device=dev)
+        self.yb = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        self.stats = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.eval_step_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._train_graph = None
+        self._train_graph_ds = None
+        self._eval_graph = None
+        self._eval_graph_ds = None
+
+    # -- to override ----------------------------------------------------------
+    input_shape: tuple = (32, 32, 8)
+
+    def build(self) -> None:
+        raise NotImplementedError
+
+    def post_bind(self) -> None:
+        """Allocate model-level buffers once layers are bound."""
+
+    def all_layers(self) -> list[Layer]:
+        raise NotImplementedError
+
+    def forward(self, x, train: bool):
+        raise NotImplementedError
+
+    def backward(self, dlast) -> None:
+        raise NotImplementedError
+
+    # -- step bodies ---------------------------------------------------------
+    def _train_body(self, ds: DeviceDataset) -> None:
+        st = self.state
+        K.gather_batch(ds.x, ds.y, ds.perm, st.step, ds.steps_per_epoch, self.B, self.xb, self.yb)
+        out = self.forward(self.xb, train=True)
+        dlast = self.head.forward_backward(out, self.yb, self.stats, train=True)
+        for l in self.all_layers():
+            l.prepare_backward()
+        self.backward(dlast)
+        st.optimizer_step()
+        opt_ops.tick(st.step, 1)
+
+    def _eval_body(self, ds: DeviceDataset) -> None:
+        K.gather_batch(ds.x, ds.y, ds.perm, self.eval_step_ctr, ds.steps_per_epoch, self.B,
+                       self.xb, self.yb)
+        out = self.forward(self.xb, train=False)
+        self.head.forward_backward(out, self.yb, self.stats, train=False)
+        opt_ops.tick(self.eval_step_ctr, 1)
+
+    # -- graph capture ---------------------------------------------------------
+    def _capture(self, body, ds):
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        # warm-up on a side stream (allocator/library init), state restored below
+        snap = self.state.model32.clone()
+        step0 = self.state.step.clone()
+        slots = [t.clone() if t is not None else None for t in (self.state.m, self.state.v)]
+        with torch.cuda.stream(s):
+            body(ds)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            body(ds)
+        torch.cuda.synchronize(self.device)
+        self.state.model32.copy_(snap)
+        self.state.step.copy_(step0)
+        for t, c in zip((self.state.m, self.state.v), slots):
+            if t is not None:
+                t.copy_(c)
+        self.state.refresh_bf16()
+        return g
+
+    def use_graphs(self) -> bool:
+        return self.device.type == "cuda"
+
+    def train_steps(self, ds: DeviceDataset, nsteps: int, step_offset: int = 0) -> None:
+        """Run ``nsteps`` local updates; reshuffles at epoch boundaries."""
+        if self.use_graphs() and (self._train_graph is None or self._train_graph_ds is not ds):
+            self._train_graph = self._capture(self._train_body, ds)
+            self._train_graph_ds = ds
+        spe = ds.steps_per_epoch
+        for i in range(nsteps):
+            gstep = step_offset + i
+            if gstep > 0 and gstep % spe == 0:
+                ds.reshuffle()
+            if self.use_graphs():
+                self._train_graph.replay()
+            else:
+                self._train_body(ds)
+
+    def evaluate(self, ds: DeviceDataset, max_steps: int | None = None) -> dict:
+        """Loss / accuracy of the current model on ``ds`` (BN in inference mode)."""
+        nsteps = ds.steps_per_epoch if max_steps is None else min(max_steps, ds.steps_per_epoch)
+        self.stats.zero_()
+        self.eval_step_ctr.zero_()
+        if self.use_graphs() and (self._eval_graph is None or self._eval_graph_ds is not ds):
+            self._eval_graph = self._capture(self._eval_body, ds)
+            self._eval_graph_ds = ds
+            self.stats.zero_()
+            self.eval_step_ctr.zero_()
+        for _ in range(nsteps):
+            if self.use_graphs():
+                self._eval_graph.replay()
+            else:
+                self._eval_body(ds)
+        s = self.stats.cpu().numpy()
+        n = max(1.0, float(s[2]))
+        return {"loss": float(s[0] / n), "accuracy": float(s[1] / n)}
+
+    def reset_train_stats(self) -> None:
+        self.stats.zero_()
+
+    def train_stats(self) -> dict:
+        s = self.stats.cpu().numpy()
+        n = max(1.0, float(s[2]))
+        return {"loss": float(s[0] / n), "accuracy": float(s[1] / n)}
+
+    # -- data helpers ----------------------------------------------------------
+    def make_dataset(self, x_nhwc: np.ndarray | torch.Tensor, y: np.ndarray | torch.Tensor,
+                     seed: int = 0, shuffle: bool = True, batch_size: int | None = None) -> DeviceDataset:
+        """Upload a shard: pads channels to the model's input width, casts to bf16."""
+        x = torch.as_tensor(x_nhwc)
+        if x.dim() == 4 and x.shape[-1] < self.input_shape[-1]:
+            pad = self.input_shape[-1] - x.shape[-1]
+            x = torch.nn.functional.pad(x, (0, pad))
+        x = x.to(torch.bfloat16).to(self.device)
+        y = torch.as_tensor(y).to(torch.int32).to(self.device)
+        return DeviceDataset(x, y, batch_size or self.B, seed=seed, shuffle=shuffle)
+
+    @staticmethod
+    def timer():
+        return time.perf_counter()

@@ -1,0 +1,69 @@
+"""ResNet-18 for CIFAR-10 (32x32x3 input, 10 classes) on the static executor.
+
+The north-star config of this framework (BASELINE.json: "8-learner FedAvg
+CIFAR-10 ResNet-18").  The reference ships no ResNet-18 -- its CIFAR model
+is the VGG-style CifarCNN (examples/keras/models/cifar_cnn.py:7-52, provided
+in models/cifar_cnn.py) -- so this is the standard CIFAR ResNet-18 topology:
+3x3 stem (64) -> 4 stages of 2 BasicBlocks (64/128/256/512, strides 1/2/2/2)
+-> global average pool -> Linear(512, 10).  11.17M parameters, 11.18M
+variables including BatchNorm moving statistics.
+
+The 3 input channels are zero-padded to 8 once, at shard upload, so the stem
+conv runs on the same 16-B-vectorised MFMA path as every other conv.
+"""
+from __future__ import annotations
+
+import torch
+
+from metisfl_amd.models.layers import BasicBlock, ClassifierHead, ConvBN
+from metisfl_amd.models.net import StaticNet
+
+
+class ResNet18(StaticNet):
+    input_shape = (32, 32, 8)
+    num_classes = 10
+    widths = (64, 128, 256, 512)
+
+    def __init__(self, batch_size: int = 32, device="cpu", optimizer=None, seed: int = 0,
+                 width_mult: float = 1.0, num_classes: int = 10):
+        self.width_mult = width_mult
+        self.num_classes = num_classes
+        super().__init__(batch_size, device, optimizer, seed)
+
+    def build(self):
+        N = self.B
+        w = [max(8, int(c * self.width_mult) // 8 * 8) for c in self.widths]
+        H = self.input_shape[0]
+        self.stem = ConvBN("stem", N, H, H, self.input_shape[2], w[0], 3, 1, relu=True,
+                           need_dgrad=False)
+        blocks = []
+        cin, h = w[0], H
+        for i, (c, s) in enumerate(zip(w, (1, 2, 2, 2))):
+            b1 = BasicBlock(f"layer{i + 1}.0", N, h, h, cin, c, s)
+            h = b1.out_shape[1]
+            b2 = BasicBlock(f"layer{i + 1}.1", N, h, h, c, c, 1)
+            blocks += [b1, b2]
+            cin = c
+        self.blocks = blocks
+        self.head = ClassifierHead("fc", N, h * h, cin, self.num_classes)
+
+    def all_layers(self):
+        return [self.stem] + self.blocks + [self.head]
+
+    def post_bind(self):
+        dev = self.device
+        # gradient buffers at block boundaries: dx of block i is dout of block i-1
+        self.dacts = [torch.zeros(b.in_shape, dtype=torch.bfloat16, device=dev) for b in self.blocks]
+
+    def forward(self, x, train):
+        h = self.stem.forward(x, train=train)
+        for b in self.blocks:
+            h = b.forward(h, train=train)
+        return h
+
+    def backward(self, dlast):
+        d = dlast.view(self.blocks[-1].out_shape)
+        for i in range(len(self.blocks) - 1, -1, -1):
+            self.blocks[i].backward(d, self.dacts[i])
+            d = self.dacts[i]
+        self.stem.backward(d, None)

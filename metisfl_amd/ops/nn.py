@@ -1,0 +1,264 @@
+"""Neural-network ops of the learner's local-training step.
+
+Device tensors dispatch to the hand-written HIP kernels in ``csrc/kernels``
+(implicit-GEMM MFMA convolution, fused BatchNorm, fused classifier head, the
+batch gather).  CPU tensors use plain-PyTorch references with identical
+semantics; they power the host-only test suite and are what the GPU numerics
+tests compare the kernels against.
+
+Tensor conventions: activations NHWC bf16 ``[N, H, W, C]``; conv weights KRSC
+bf16 ``[Cout, R, S, Cin]`` (compute copy) with an fp32 master elsewhere; all
+per-channel BatchNorm state is fp32.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from metisfl_amd.ops._native import ops
+
+
+def out_dim(n: int, k: int, stride: int, pad: int) -> int:
+    return (n + 2 * pad - k) // stride + 1
+
+
+@dataclass(frozen=True)
+class ConvShape:
+    N: int
+    H: int
+    W: int
+    C: int
+    Co: int
+    R: int
+    S: int
+    stride: int
+    pad: int
+
+    @property
+    def P(self) -> int:
+        return out_dim(self.H, self.R, self.stride, self.pad)
+
+    @property
+    def Q(self) -> int:
+        return out_dim(self.W, self.S, self.stride, self.pad)
+
+    def args(self):
+        return (self.N, self.H, self.W, self.C, self.Co, self.R, self.S, self.stride, self.pad)
+
+
+@dataclass(frozen=True)
+class ConvPlan:
+    bm: int
+    bn: int
+    splits: int
+    kchunk: int
+    stats_rows: int
+    workspace: int
+
+
+def conv_plan(mode: int, shp: ConvShape, device: torch.device) -> ConvPlan:
+    """mode 0 fwd / 1 dgrad / 2 wgrad.  CPU path: no workspace, 1 stats row."""
+    if device.type == "cuda":
+        return ConvPlan(*ops().conv_plan(mode, *shp.args()))
+    return ConvPlan(0, 0, 1, 0, 1, 0)
+
+
+# ---------------------------------------------------------------------------
+# CPU references
+def _nchw(x: torch.Tensor) -> torch.Tensor:
+    return x.float().permute(0, 3, 1, 2)
+
+
+def _wt(w: torch.Tensor) -> torch.Tensor:
+    return w.float().permute(0, 3, 1, 2)
+
+
+def _stats_rows_cpu(y: torch.Tensor, stats: torch.Tensor) -> None:
+    yf = y.float().reshape(-1, y.shape[-1])
+    C = yf.shape[1]
+    stats.view(-1)[:C].copy_(yf.sum(0))
+    stats.view(-1)[C:2 * C].copy_((yf * yf).sum(0))
+
+
+def conv_forward(x, w, y, shp: ConvShape, ws=None, stats=None) -> None:
+    if x.is_cuda:
+        ops().conv_forward(x, w, y, ws, stats, *shp.args())
+        return
+    out = F.conv2d(_nchw(x), _wt(w), stride=shp.stride, padding=shp.pad)
+    y.copy_(out.permute(0, 2, 3, 1).to(torch.bfloat16))
+    if stats is not None:
+        _stats_rows_cpu(y, stats)
+
+
+def conv_dgrad(dy, w, dx, shp: ConvShape, ws=None, accumulate: bool = False) -> None:
+    """dx (+)= conv_transpose(dy, W); ``w`` is the KRSC weight [Cout][R][S][Cin]
+    (the kernel forms W^T fragments with transposing LDS reads)."""
+    if dy.is_cuda:
+        ops().conv_dgrad(dy, w, dx, ws, *shp.args(), accumulate)
+        return
+    w = w.float().permute(0, 3, 1, 2)  # -> [Cout][Cin][R][S]
+    g = torch.nn.grad.conv2d_input((shp.N, shp.C, shp.H, shp.W), w, _nchw(dy),
+                                   stride=shp.stride, padding=shp.pad)
+    g = g.permute(0, 2, 3, 1)
+    if accumulate:
+        g = g + dx.float()
+    dx.copy_(g.to(torch.bfloat16))
+
+
+def conv_wgrad(x, dy, dw, shp: ConvShape, ws=None) -> None:
+    """dw (fp32 [Cout][R][S][Cin]) = sum over pixels of dy x im2col(x)."""
+    if x.is_cuda:
+        ops().conv_wgrad(x, dy, dw, ws, *shp.args())
+        return
+    g = torch.nn.grad.conv2d_weight(_nchw(x), (shp.Co, shp.C, shp.R, shp.S), _nchw(dy),
+                                    stride=shp.stride, padding=shp.pad)
+    dw.copy_(g.permute(0, 2, 3, 1).reshape(dw.shape))
+
+
+def transpose_krsc(w, wt, Co: int, RS: int, Ci: int) -> None:
+    if w.is_cuda:
+        ops().transpose_krsc(w, wt, Co, RS, Ci)
+        return
+    wt.copy_(w.reshape(Co, RS, Ci).permute(2, 1, 0).reshape(wt.shape))
+
+
+# ---------------------------------------------------------------------------
+def bn_stats_rows(M: int, C: int, device: torch.device) -> int:
+    return int(ops().bn_stats_blocks(M, C)) if device.type == "cuda" else 1
+
+
+def bn_stats(x, C: int, partial) -> int:
+    if x.is_cuda:
+        return int(ops().bn_stats(x, C, partial))
+    _stats_rows_cpu(x, partial)
+    return 1
+
+
+def bn_finalize(partial, rows: int, M: int, C: int, gamma, beta, mean, invstd, scale, shift,
+                run_mean=None, run_var=None, momentum: float = 0.1, eps: float = 1e-5) -> None:
+    if partial.is_cuda:
+        ops().bn_finalize(partial, rows, M, C, gamma, beta, mean, invstd, scale, shift, run_mean,
+                          run_var, momentum, eps)
+        return
+    p = partial.view(-1)[: rows * 2 * C].view(rows, 2, C).double().sum(0)
+    mu = p[0] / M
+    var = (p[1] / M - mu * mu).clamp_min(0)
+    istd = 1.0 / torch.sqrt(var + eps)
+    mean.copy_(mu.float())
+    invstd.copy_(istd.float())
+    scale.copy_(gamma * istd.float())
+    shift.copy_(beta - mu.float() * gamma * istd.float())
+    if run_mean is not None:
+        unb = var * M / (M - 1) if M > 1 else var
+        run_mean.mul_(1 - momentum).add_(momentum * mu.float())
+        run_var.mul_(1 - momentum).add_(momentum * unb.float())
+
+
+def bn_apply(x, C: int, scale, shift, y, residual=None, relu: bool = False) -> None:
+    if x.is_cuda:
+        ops().bn_apply(x, C, scale, shift, residual, y, relu)
+        return
+    v = x.float() * scale + shift
+    if residual is not None:
+        v = v + residual.float()
+    if relu:
+        v = v.clamp_min(0)
+    y.copy_(v.to(torch.bfloat16))
+
+
+def bn_backward(dy, x, y, C: int, gamma, mean, invstd, partial, coef, dgamma, dbeta, dx,
+                dy_masked=None) -> None:
+    """BN(+ReLU) backward.  ``y`` (the post-activation output) gives the ReLU
+    mask; ``dy_masked`` optionally receives the masked upstream gradient (the
+    residual-shortcut gradient of an add+ReLU)."""
+    if dy.is_cuda:
+        ops().bn_backward(dy, x, y, C, gamma, mean, invstd, partial, coef, dgamma, dbeta, dx,
+                          dy_masked)
+        return
+    g = dy.float()
+    if y is not None:
+        g = torch.where(y.float() > 0, g, torch.zeros_like(g))
+        if dy_masked is not None:
+            dy_masked.copy_(g.to(torch.bfloat16))
+    xf = x.float()
+    xh = (xf - mean) * invstd
+    gm = g.reshape(-1, C)
+    M = gm.shape[0]
+    s = gm.double().sum(0)
+    q = (gm.double() * xh.reshape(-1, C).double()).sum(0)
+    if dgamma is not None:
+        dgamma.copy_(q.float())
+    if dbeta is not None:
+        dbeta.copy_(s.float())
+    k1 = gamma * invstd
+    out = k1 * (g - (s / M).float() - xh * (q / M).float())
+    dx.copy_(out.to(torch.bfloat16))
+
+
+# ---------------------------------------------------------------------------
+def head_forward_backward(x, B: int, HW: int, C: int, W, bias, labels, feat, dlogits, dx, stats,
+                          backward: bool = True) -> None:
+    """avgpool -> linear -> softmax-CE (+ backward to the pooled input).
+    stats[0:3] += (loss sum, #correct, #samples)."""
+    if x.is_cuda:
+        ops().head_forward_backward(x, B, HW, C, W, bias, labels, feat, dlogits, dx, stats,
+                                    backward)
+        return
+    xf = x.float().reshape(B, HW, C)
+    f = xf.mean(1)
+    K = W.numel() // C
+    logits = f @ W.reshape(K, C).t() + (bias if bias is not None else 0)
+    lab = labels[:B].long()
+    lse = torch.logsumexp(logits, 1)
+    if stats is not None:
+        stats[0] += (lse - logits.gather(1, lab[:, None])[:, 0]).sum()
+        stats[1] += (logits.argmax(1) == lab).float().sum()
+        stats[2] += B
+    if not backward:
+        return
+    p = torch.softmax(logits, 1)
+    d = p.clone()
+    d[torch.arange(B), lab] -= 1
+    d /= B
+    feat.view(-1)[: B * C].copy_(f.reshape(-1))
+    dlogits.view(-1)[: B * K].copy_(d.reshape(-1))
+    dfeat = d @ W.reshape(K, C)
+    dx.copy_((dfeat / HW)[:, None, :].expand(B, HW, C).reshape(dx.shape).to(torch.bfloat16))
+
+
+def head_wgrad(feat, dlogits, B: int, C: int, K: int, dW, db) -> None:
+    if feat.is_cuda:
+        ops().head_wgrad(feat, dlogits, B, C, K, dW, db)
+        return
+    f = feat.view(-1)[: B * C].view(B, C)
+    d = dlogits.view(-1)[: B * K].view(B, K)
+    dW.copy_((d.t() @ f).reshape(dW.shape))
+    if db is not None:
+        db.copy_(d.sum(0))
+
+
+def gather_batch(shard, labels, perm, step, steps_per_epoch: int, B: int, xb, yb) -> None:
+    if shard.is_cuda:
+        ops().gather_batch(shard, labels, perm, step, steps_per_epoch, B, xb, yb)
+        return
+    s = int(step[0]) % steps_per_epoch
+    idx = perm[s * B:(s + 1) * B].long()
+    xb.copy_(shard.view(labels.numel(), -1)[idx].reshape(xb.shape))
+    yb[:B].copy_(labels[idx])
+
+
+def gemm_nt(a, b, c, M: int, N: int, K: int, bias=None, epilogue: int = 0, aux=None) -> None:
+    """c = a . b^T (+bias, +gelu | +residual)."""
+    if a.is_cuda:
+        ops().gemm_nt(a, b, c, bias, M, N, K, epilogue, aux)
+        return
+    out = a.float().reshape(M, K) @ b.float().reshape(N, K).t()
+    if epilogue >= 1 and bias is not None:
+        out = out + bias
+    if epilogue == 2:
+        out = F.gelu(out, approximate="tanh")
+    if epilogue == 3:
+        out = out + aux.float().reshape(M, N)
+    c.copy_(out.reshape(c.shape).to(torch.bfloat16))

@@ -1,0 +1,80 @@
+"""Process-group plumbing: one process per GPU, RCCL over xGMI.
+
+The reference moves every model through the controller over gRPC
+(controller.cc:696-793: one serialized RunTaskRequest per learner, a fresh
+channel per request).  On one MI355X node the data plane is instead a set of
+RCCL collectives between the learner processes (torch.distributed backend
+``nccl`` IS RCCL on ROCm); the gRPC services remain the control plane for
+remote learners and API parity.  CPU-only runs (tests) use ``gloo`` with the
+identical code path.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, backend: str | None = None, timeout_s: float = 1800.0):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        use_cuda = torch.cuda.is_available() and backend != "gloo"
+        if use_cuda:
+            torch.cuda.set_device(self.local_rank)
+            self.device = torch.device("cuda", self.local_rank)
+        else:
+            self.device = torch.device("cpu")
+        self.backend = backend or ("nccl" if use_cuda else "gloo")
+        self.owned = False
+        if self.world > 1 and not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            kw = {}
+            if self.backend == "nccl":
+                kw["device_id"] = self.device
+            dist.init_process_group(self.backend, rank=self.rank, world_size=self.world,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+            self.owned = True
+        self.pg = dist.group.WORLD if self.world > 1 else None
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+    def barrier(self) -> None:
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+    def all_reduce_(self, t: torch.Tensor) -> None:
+        if self.distributed:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> None:
+        if self.distributed:
+            dist.broadcast(t, src=src)
+
+    def all_gather_rows(self, row: torch.Tensor) -> torch.Tensor:
+        """Gather one small 1-D tensor per rank -> [world, n] (on row.device)."""
+        if not self.distributed:
+            return row.reshape(1, -1).clone()
+        out = torch.empty((self.world, row.numel()), dtype=row.dtype, device=row.device)
+        dist.all_gather_into_tensor(out, row.contiguous())
+        return out
+
+    def all_max(self, x: float) -> float:
+        if not self.distributed:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self) -> None:
+        if self.owned and dist.is_initialized():
+            dist.destroy_process_group()
+            self.owned = False

@@ -1,0 +1,275 @@
+"""Numerics of the hand-written HIP kernels vs plain-PyTorch fp32 references.
+
+Run on an MI355X: ``pytest -m gpu``.  Every test drives the native extension
+(``metisfl_amd._ops``) -- there is no eager fallback for device tensors.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _native():
+    from metisfl_amd.ops import ops
+    return ops()
+
+
+def rel_err(a, b):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+CONV_CASES = [
+    # N, H, W, Cin, Cout, k, stride
+    (4, 32, 32, 8, 64, 3, 1),     # stem (3 channels zero-padded to 8)
+    (8, 32, 32, 64, 64, 3, 1),    # layer1
+    (16, 32, 32, 64, 128, 3, 1),  # 128x128 tile (>64 KiB LDS)
+    (8, 32, 32, 64, 128, 3, 2),   # layer2 entry
+    (8, 32, 32, 64, 128, 1, 2),   # projection shortcut
+    (8, 8, 8, 256, 256, 3, 1),    # layer3 (split-K)
+    (4, 4, 4, 512, 512, 3, 1),    # layer4 (split-K)
+    (2, 7, 5, 24, 40, 3, 1),      # ragged tiles / odd spatial
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_forward_matches_fp32(case):
+    from metisfl_amd.ops import nn as K
+    _native()
+    N, H, W, C, Co, k, s = case
+    torch.manual_seed(0)
+    x = bf(torch.randn(N, H, W, C, device=DEV))
+    w = bf(torch.randn(Co, k, k, C, device=DEV) * (2.0 / (k * k * C)) ** 0.5)
+    shp = K.ConvShape(N, H, W, C, Co, k, k, s, k // 2)
+    y = torch.empty(N, shp.P, shp.Q, Co, dtype=torch.bfloat16, device=DEV)
+    plan = K.conv_plan(0, shp, torch.device(DEV))
+    ws = torch.empty(max(4, plan.workspace), device=DEV)
+    stats = torch.zeros(max(1, plan.stats_rows) * 2 * Co, device=DEV)
+    K.conv_forward(x, w, y, shp, ws, stats)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=s,
+                   padding=k // 2).permute(0, 2, 3, 1)
+    assert rel_err(y, ref) < 1e-2
+    # fused BN partial statistics (sum and sum of squares of the bf16 output)
+    st = stats.view(-1, 2, Co).sum(0).cpu()
+    yf = y.float().reshape(-1, Co).cpu()
+    assert torch.allclose(st[0], yf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(st[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("case", CONV_CASES[1:])
+def test_conv_dgrad_matches_fp32(case):
+    from metisfl_amd.ops import nn as K
+    N, H, W, C, Co, k, s = case
+    torch.manual_seed(1)
+    shp = K.ConvShape(N, H, W, C, Co, k, k, s, k // 2)
+    w = bf(torch.randn(Co, k, k, C, device=DEV) * 0.1)
+    dy = bf(torch.randn(N, shp.P, shp.Q, Co, device=DEV))
+    wt = torch.empty(C, k, k, Co, dtype=torch.bfloat16, device=DEV)
+    K.transpose_krsc(w, wt, Co, k * k, C)
+    assert torch.equal(wt.cpu(), w.cpu().permute(3, 1, 2, 0))
+    plan = K.conv_plan(1, shp, torch.device(DEV))
+    ws = torch.empty(max(4, plan.workspace), device=DEV)
+    dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=DEV)
+    K.conv_dgrad(dy, w, dx, shp, ws, accumulate=False)
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.float().permute(0, 3, 1, 2),
+                                     dy.float().permute(0, 3, 1, 2), stride=s,
+                                     padding=k // 2).permute(0, 2, 3, 1)
+    assert rel_err(dx, ref) < 1e-2
+    # accumulate epilogue
+    base = bf(torch.randn(N, H, W, C, device=DEV))
+    dx2 = base.clone()
+    K.conv_dgrad(dy, w, dx2, shp, ws, accumulate=True)
+    assert rel_err(dx2, ref + base.float()) < 1e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_wgrad_matches_fp32(case):
+    from metisfl_amd.ops import nn as K
+    N, H, W, C, Co, k, s = case
+    torch.manual_seed(2)
+    shp = K.ConvShape(N, H, W, C, Co, k, k, s, k // 2)
+    x = bf(torch.randn(N, H, W, C, device=DEV))
+    dy = bf(torch.randn(N, shp.P, shp.Q, Co, device=DEV))
+    plan = K.conv_plan(2, shp, torch.device(DEV))
+    ws = torch.empty(max(4, plan.workspace), device=DEV)
+    dw = torch.empty(Co, k, k, C, device=DEV)
+    K.conv_wgrad(x, dy, dw, shp, ws)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (Co, C, k, k),
+                                      dy.float().permute(0, 3, 1, 2), stride=s,
+                                      padding=k // 2).permute(0, 2, 3, 1)
+    assert rel_err(dw, ref) < 5e-3
+
+
+def test_gemm_nt_with_epilogues():
+    from metisfl_amd.ops import nn as K
+    torch.manual_seed(3)
+    M, N, Kd = 96, 200, 136
+    a = bf(torch.randn(M, Kd, device=DEV))
+    b = bf(torch.randn(N, Kd, device=DEV) * 0.1)
+    bias = torch.randn(N, device=DEV)
+    aux = bf(torch.randn(M, N, device=DEV))
+    ref = a.float() @ b.float().t()
+    for epi, r in ((0, ref), (1, ref + bias), (2, F.gelu(ref + bias, approximate="tanh")),
+                   (3, ref + bias + aux.float())):
+        c = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        K.gemm_nt(a, b, c, M, N, Kd, bias=bias, epilogue=epi, aux=aux)
+        assert rel_err(c, r) < 1e-2, epi
+
+
+@pytest.mark.parametrize("C", [64, 128, 512])
+def test_batchnorm_forward_backward(C):
+    from metisfl_amd.ops import nn as K
+    torch.manual_seed(4)
+    M = 2048 if C < 512 else 512
+    x = bf(torch.randn(M, C, device=DEV) * 3 + 1)
+    res = bf(torch.randn(M, C, device=DEV))
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV)
+    part = torch.zeros(512 * 2 * C, device=DEV)
+    f32 = lambda: torch.zeros(C, device=DEV)
+    mean, invstd, scale, shift = f32(), f32(), f32(), f32()
+    rm, rv = f32(), torch.ones(C, device=DEV)
+    rows = K.bn_stats(x, C, part)
+    K.bn_finalize(part, rows, M, C, gamma, beta, mean, invstd, scale, shift, rm, rv, 0.1, 1e-5)
+    y = torch.empty_like(x)
+    K.bn_apply(x, C, scale, shift, y, residual=res, relu=True)
+    xr = x.float().cpu().requires_grad_(True)
+    g, b_ = gamma.cpu().requires_grad_(True), beta.cpu().requires_grad_(True)
+    bn = F.batch_norm(xr, None, None, g, b_, training=True, eps=1e-5)
+    yr = torch.relu(bn + res.float().cpu())
+    assert rel_err(y, yr) < 1e-2
+    assert torch.allclose(rm.cpu(), 0.1 * x.float().cpu().mean(0), atol=1e-3)
+    dy = bf(torch.randn(M, C, device=DEV))
+    yr.backward(dy.float().cpu())
+    dx = torch.empty_like(x)
+    dres = torch.empty_like(x)
+    dg, db = f32(), f32()
+    coef = torch.zeros(3 * C, device=DEV)
+    K.bn_backward(dy, x, y, C, gamma, mean, invstd, part, coef, dg, db, dx, dres)
+    assert rel_err(dx, xr.grad) < 2e-2
+    assert rel_err(dg, g.grad) < 1e-2
+    assert rel_err(db, b_.grad) < 1e-2
+    mask = (y.float() > 0).float()
+    assert rel_err(dres, dy.float() * mask) < 1e-2
+
+
+def test_head_forward_backward():
+    from metisfl_amd.ops import nn as K
+    torch.manual_seed(5)
+    B, HW, C, Kc = 32, 16, 512, 10
+    x = bf(torch.randn(B, HW, C, device=DEV))
+    W = torch.randn(Kc, C, device=DEV) * 0.05
+    b = torch.randn(Kc, device=DEV) * 0.1
+    lab = torch.randint(0, Kc, (B,), device=DEV, dtype=torch.int32)
+    feat = torch.zeros(B * C, device=DEV)
+    dlog = torch.zeros(B * Kc, device=DEV)
+    dx = torch.empty_like(x)
+    stats = torch.zeros(4, device=DEV)
+    K.head_forward_backward(x, B, HW, C, W, b, lab, feat, dlog, dx, stats, True)
+    dW = torch.empty(Kc, C, device=DEV)
+    db = torch.empty(Kc, device=DEV)
+    K.head_wgrad(feat, dlog, B, C, Kc, dW, db)
+    xr = x.float().cpu().requires_grad_(True)
+    Wr, br = W.cpu().requires_grad_(True), b.cpu().requires_grad_(True)
+    logits = xr.mean(1) @ Wr.t() + br
+    loss = F.cross_entropy(logits, lab.long().cpu())
+    loss.backward()
+    assert abs(float(stats[0].cpu()) / B - float(loss)) < 1e-3
+    assert int(stats[2].cpu()) == B
+    assert int(stats[1].cpu()) == int((logits.argmax(1) == lab.long().cpu()).sum())
+    assert rel_err(dx, xr.grad) < 1e-2
+    assert rel_err(dW, Wr.grad) < 1e-4
+    assert rel_err(db, br.grad) < 1e-4
+
+
+@pytest.mark.parametrize("kind", ["vanilla_sgd", "momentum_sgd", "fed_prox", "adam", "adam_weight_decay"])
+def test_fused_optimizer_matches_reference(kind):
+    from metisfl_amd.ops.optim import OptimizerSpec, fused_step
+    torch.manual_seed(6)
+    n = 4096 * 3 + 64
+    spec = OptimizerSpec(kind, 0.01, l1=1e-4, l2=1e-3, momentum=0.9, proximal_term=0.1,
+                         weight_decay=0.01)
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.randn(n, device=DEV).abs() * 0.1
+    v = torch.randn(n, device=DEV).abs() * 0.1
+    a = torch.randn(n, device=DEV)
+    p16 = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    lr = torch.tensor([0.5], device=DEV)
+    step = torch.tensor([3], dtype=torch.int32, device=DEV)
+    cp = [t.cpu().clone() for t in (p, g, m, v, a)]
+    p16c = torch.empty(n, dtype=torch.bfloat16)
+    fused_step(spec, p, g, m, v, a, p16, lr, step)
+    fused_step(spec, cp[0], cp[1], cp[2], cp[3], cp[4], p16c, lr.cpu(), step.cpu())
+    assert torch.allclose(p.cpu(), cp[0], rtol=1e-5, atol=1e-6)
+    assert torch.equal(p16.cpu(), p16c)
+    if spec.needs_m:
+        assert torch.allclose(m.cpu(), cp[2], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.int8, torch.int16, torch.int32, torch.int64, torch.uint8,
+                                   torch.float32, torch.float64])
+def test_weighted_sum_bit_exact(dtype):
+    from metisfl_amd.ops import aggregate as A
+    rng = np.random.default_rng(7)
+    n = 10007
+    L = 19  # > 16 exercises the accumulate path
+    if dtype.is_floating_point:
+        xs = [torch.from_numpy(rng.standard_normal(n)).to(dtype) for _ in range(L)]
+    else:
+        xs = [torch.from_numpy(rng.integers(0, 100, n)).to(dtype) for _ in range(L)]
+    ws = list(rng.random(L) / L)
+    out = torch.empty(n, dtype=dtype, device=DEV)
+    A.weighted_sum(out, [x.to(DEV) for x in xs], ws)
+    ref = torch.empty(n, dtype=dtype)
+    A.weighted_sum(ref, xs, ws)
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_reference_fedavg_integer_truncation_on_device():
+    # federated_average_test.cc:106-110: two identical 1..10 tensors at w=0.5
+    from metisfl_amd.ops import aggregate as A
+    x = torch.arange(1, 11, dtype=torch.int32, device=DEV)
+    out = torch.empty_like(x)
+    A.weighted_sum(out, [x, x.clone()], [0.5, 0.5])
+    assert out.cpu().tolist() == [0, 2, 2, 4, 4, 6, 6, 8, 8, 10]
+
+
+def test_rolling_ops_and_zero_count():
+    from metisfl_amd.ops import aggregate as A
+    y = torch.arange(0, 64, dtype=torch.float32, device=DEV)
+    x = torch.ones(64, device=DEV)
+    A.rolling_op(y, x, A.MERGE_ADD, 2.0)
+    A.rolling_op(y, None, A.SCALE_DIV, 2.0)
+    assert torch.allclose(y.cpu(), (torch.arange(64.) + 2) / 2)
+    z = torch.zeros(200000, device=DEV)
+    z[::3] = 1
+    segs = [(0, 100), (100, 150000), (150000, 200000)]
+    cnt = A.count_zeros(z, segs)
+    ref = [int((z[b:e] == 0).sum()) for b, e in segs]
+    assert cnt == ref
+
+
+def test_gather_batch():
+    from metisfl_amd.ops import nn as K
+    n, row = 100, 64
+    shard = bf(torch.randn(n, row, device=DEV))
+    lab = torch.arange(n, dtype=torch.int32, device=DEV)
+    perm = torch.randperm(n).to(torch.int32).to(DEV)
+    step = torch.tensor([3], dtype=torch.int32, device=DEV)
+    B = 8
+    xb = torch.empty(B, row, dtype=torch.bfloat16, device=DEV)
+    yb = torch.empty(B, dtype=torch.int32, device=DEV)
+    K.gather_batch(shard, lab, perm, step, 12, B, xb, yb)
+    idx = perm[24:32].long()
+    assert torch.equal(xb.cpu(), shard[idx].cpu())
+    assert torch.equal(yb.cpu(), lab[idx].cpu())
