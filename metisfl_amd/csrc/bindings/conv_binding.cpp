@@ -70,15 +70,13 @@ std::vector<int64_t> conv_plan(int64_t mode, int64_t N, int64_t H, int64_t W, in
   if (mode == 2) {
     mfl::ConvGeom g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
     auto p = mfl::plan_conv_wgrad(g);
-    const int64_t ws = p.splits > 1 ? (int64_t)p.splits * g.Ng * g.K : 0;
-    return plan_vec(p, ws, 0);
+    return plan_vec(p, 0, 0);
   }
   mfl::ConvGeom g = mode == 0 ? fwd_geom(N, H, W, C, Co, R, S, stride, pad)
                               : dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
   auto p = mfl::plan_conv_gemm(g);
   const int64_t ws = p.splits > 1 ? (int64_t)p.splits * g.M * g.Ng : 0;
-  const int64_t rows = p.splits > 1 ? mfl::splitk_stats_blocks(g.M, g.Ng) : p.stats_rows;
-  return plan_vec(p, ws, rows);
+  return plan_vec(p, ws, 1);
 }
 
 void run_gemm(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const torch::Tensor& w,
@@ -91,11 +89,12 @@ void run_gemm(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, cons
     check_f32(*ws, (int64_t)p.splits * g.M * g.Ng, "workspace");
     wsp = ws->data_ptr<float>();
   }
-  float* st = nullptr;
+  double* st = nullptr;
   if (stats.has_value() && stats->defined()) {
-    const int64_t rows = p.splits > 1 ? mfl::splitk_stats_blocks(g.M, g.Ng) : p.stats_rows;
-    check_f32(*stats, rows * 2 * g.Ng, "stats");
-    st = stats->data_ptr<float>();
+    TORCH_CHECK(stats->is_cuda() && stats->is_contiguous() &&
+                    stats->scalar_type() == torch::kFloat64 && stats->numel() >= 2 * g.Ng,
+                "stats must be a contiguous fp64 device tensor of >= 2*Cout elements");
+    st = stats->data_ptr<double>();
   }
   mfl::launch_conv_gemm(g, dgrad, p, bf(src), bf(w), bf(y), wsp, st, accum, cur_stream(y));
 }
@@ -121,22 +120,20 @@ void conv_dgrad(torch::Tensor dy, torch::Tensor wt, torch::Tensor dx,
   run_gemm(g, true, dy, wt, dx, ws, c10::nullopt, accumulate);
 }
 
-void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw,
-                c10::optional<torch::Tensor> ws, int64_t N, int64_t H, int64_t W, int64_t C,
-                int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad) {
+// accumulate=false zeroes dw first when the plan splits the reduction (the
+// training step passes true: its gradient buffer is zeroed by the optimizer).
+void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t N, int64_t H,
+                int64_t W, int64_t C, int64_t Co, int64_t R, int64_t S, int64_t stride,
+                int64_t pad, bool accumulate) {
   auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
   check_bf16(x, N * H * W * C, "x");
   check_bf16(dy, (int64_t)g.M * Co, "dy");
   check_f32(dw, Co * R * S * C, "dw");
   TORCH_CHECK(dw.numel() == Co * R * S * C, "dw size");
   auto p = mfl::plan_conv_wgrad(g);
-  float* wsp = nullptr;
-  if (p.splits > 1) {
-    TORCH_CHECK(ws.has_value() && ws->defined(), "wgrad split workspace required");
-    check_f32(*ws, (int64_t)p.splits * g.Ng * g.K, "workspace");
-    wsp = ws->data_ptr<float>();
-  }
-  mfl::launch_conv_wgrad(g, p, bf(x), bf(dy), dw.data_ptr<float>(), wsp, cur_stream(x));
+  if (p.splits > 1 && !accumulate)
+    (void)hipMemsetAsync(dw.data_ptr<float>(), 0, dw.numel() * sizeof(float), cur_stream(x));
+  mfl::launch_conv_wgrad(g, p, bf(x), bf(dy), dw.data_ptr<float>(), cur_stream(x));
 }
 
 void transpose_krsc(torch::Tensor w, torch::Tensor wt, int64_t Co, int64_t RS, int64_t Ci) {

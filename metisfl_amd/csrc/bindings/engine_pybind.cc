@@ -1,0 +1,245 @@
+// pybind11 module ``metisfl_amd._engine``: the native controller engine and
+// the RNS-CKKS scheme.  Counterpart of the reference's ``controller`` and
+// ``fhe`` pybind modules (controller_pybind.cc:16-68, ckks_pybind.cc:15-100).
+// Protos cross the boundary as serialized bytes.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "common/model.h"
+#include "engine/aggregation.h"
+#include "engine/controller.h"
+#include "engine/policies.h"
+#include "he/ckks.h"
+
+namespace py = pybind11;
+using namespace mfl;
+
+namespace {
+
+py::bytes B(const std::string& s) { return py::bytes(s); }
+
+py::dict dispatch_to_py(const Dispatch& d) {
+  py::list runs, evals;
+  for (auto& [id, req] : d.run_tasks) runs.append(py::make_tuple(id, B(req)));
+  for (auto& e : d.eval_tasks)
+    evals.append(py::make_tuple(e.learner_id, B(e.request), e.comm_eval_index, e.metadata_index));
+  py::dict out;
+  out["run_tasks"] = runs;
+  out["eval_tasks"] = evals;
+  return out;
+}
+
+// Host reference aggregation over serialized models (tests / tools).
+std::vector<ModelT> parse_all(const std::vector<std::string>& models) {
+  std::vector<ModelT> ms;
+  ms.reserve(models.size());
+  for (auto& m : models) ms.push_back(parse_model(m));
+  return ms;
+}
+
+py::bytes aggregate_models(const std::string& rule, const std::vector<std::string>& models,
+                           const std::vector<double>& weights, int stride) {
+  auto ms = parse_all(models);
+  std::unique_ptr<AggregationFunction> agg;
+  if (rule == "fed_avg") agg.reset(new FederatedAverage());
+  else if (rule == "fed_stride") agg.reset(new FederatedStride());
+  else throw std::runtime_error("unknown rule " + rule);
+  FederatedModelT out;
+  {
+    py::gil_scoped_release nogil;
+    const size_t s = (rule == "fed_stride" && stride > 0) ? (size_t)stride : ms.size();
+    for (size_t b = 0; b < ms.size(); b += s) {
+      AggInput in;
+      for (size_t i = b; i < std::min(ms.size(), b + s); ++i) in.push_back({{&ms[i], weights[i]}});
+      out = agg->aggregate(in);
+    }
+  }
+  return B(serialize_federated_model(out));
+}
+
+class PyRecency {
+ public:
+  // lineage: 1 or 2 (old, new) serialized models with weights
+  py::bytes aggregate(const std::vector<std::string>& models, const std::vector<double>& weights) {
+    auto ms = parse_all(models);
+    AggInput in(1);
+    for (size_t i = 0; i < ms.size(); ++i) in[0].push_back({&ms[i], weights[i]});
+    FederatedModelT out = agg_.aggregate(in);
+    return B(serialize_federated_model(out));
+  }
+
+ private:
+  FederatedRecency agg_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_engine, m) {
+  m.doc() = "metisfl_amd native controller engine (scheduler, aggregation, model store, CKKS)";
+
+  static py::exception<StatusError> status_exc(m, "EngineStatusError");
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const StatusError& e) {
+      // args = (grpc status code, message)
+      PyErr_SetObject(status_exc.ptr(), py::make_tuple(e.code, e.what()).ptr());
+    }
+  });
+
+  py::class_<Controller>(m, "Controller")
+      .def(py::init([](py::bytes params) { return new Controller(std::string(params)); }))
+      .def("add_learner",
+           [](Controller& c, py::bytes se, py::bytes ds) {
+             Dispatch d;
+             auto r = c.add_learner(std::string(se), std::string(ds), &d);
+             return py::make_tuple(r.first, r.second, dispatch_to_py(d));
+           })
+      .def("remove_learner", &Controller::remove_learner)
+      .def("learner_ids", &Controller::learner_ids)
+      .def("num_learners", &Controller::num_learners)
+      .def("global_iteration", &Controller::global_iteration)
+      .def("learner_completed_task",
+           [](Controller& c, const std::string& id, const std::string& tok, py::bytes task) {
+             std::string t(task);
+             Dispatch d;
+             {
+               py::gil_scoped_release nogil;
+               d = c.learner_completed_task(id, tok, t);
+             }
+             return dispatch_to_py(d);
+           })
+      .def("replace_community_model",
+           [](Controller& c, py::bytes fm) { c.replace_community_model(std::string(fm)); })
+      .def("record_train_submitted", &Controller::record_train_submitted)
+      .def("record_evaluation",
+           [](Controller& c, const std::string& id, uint32_t ce, uint32_t mi, py::bytes ev) {
+             c.record_evaluation(id, ce, mi, std::string(ev));
+           })
+      .def("scaling_factors", &Controller::scaling_factors)
+      .def("record_collective_round",
+           [](Controller& c, uint32_t gi, const std::vector<std::string>& ids, int64_t s, int64_t e,
+              int64_t as, int64_t ae, const std::vector<py::bytes>& meta,
+              const std::vector<uint64_t>& zeros, const std::vector<uint64_t>& sizes,
+              const std::vector<uint64_t>& lengths) {
+             std::vector<std::string> mm;
+             for (auto& b : meta) mm.emplace_back(b);
+             c.record_collective_round(gi, ids, s, e, as, ae, mm, zeros, sizes, lengths);
+           })
+      .def("community_model", [](const Controller& c) { return B(c.community_model()); })
+      .def("participating_learners", [](const Controller& c) { return B(c.participating_learners()); })
+      .def("runtime_metadata_lineage",
+           [](const Controller& c, int n) { return B(c.runtime_metadata_lineage(n)); })
+      .def("community_evaluation_lineage",
+           [](const Controller& c, int n) { return B(c.community_evaluation_lineage(n)); })
+      .def("local_task_lineage",
+           [](const Controller& c, int n, const std::vector<std::string>& ids) {
+             return B(c.local_task_lineage(n, ids));
+           })
+      .def("community_model_lineage",
+           [](const Controller& c, int n) { return B(c.community_model_lineage(n)); })
+      .def("learner_local_model_lineage",
+           [](Controller& c, int n, const std::vector<py::bytes>& ses) {
+             std::vector<std::string> s;
+             for (auto& b : ses) s.emplace_back(b);
+             return B(c.learner_local_model_lineage(n, s));
+           })
+      .def("config", [](const Controller& c) {
+        const auto& k = c.config();
+        py::dict d;
+        d["hostname"] = k.hostname;
+        d["port"] = k.port;
+        d["rule"] = k.rule;
+        d["stride_length"] = k.stride_length;
+        d["scaling"] = k.scaling;
+        d["protocol"] = k.protocol;
+        d["semi_sync_lambda"] = k.semi_sync_lambda;
+        d["semi_sync_recompute"] = k.semi_sync_recompute;
+        d["lineage"] = k.lineage;
+        d["redis"] = k.redis;
+        d["batch_size"] = k.batch_size;
+        d["epochs"] = k.epochs;
+        d["he_batch_size"] = k.he_batch_size;
+        d["he_scaling_bits"] = k.he_scaling_bits;
+        return d;
+      });
+
+  m.def("scaling_factors",
+        [](int kind, size_t n_all, const std::vector<std::string>& ids,
+           const std::vector<double>& ntrain, const std::vector<double>& batches) {
+          std::vector<ScalerInput> parts;
+          for (size_t i = 0; i < ids.size(); ++i) parts.push_back({ids[i], ntrain[i], batches[i]});
+          return compute_scaling_factors(kind, n_all, parts);
+        });
+  m.def("aggregate_models", &aggregate_models, py::arg("rule"), py::arg("models"),
+        py::arg("weights"), py::arg("stride") = 0);
+  py::class_<PyRecency>(m, "FedRec").def(py::init<>()).def("aggregate", &PyRecency::aggregate);
+  m.def("quantify_model", [](py::bytes model) {
+    auto mm = parse_model(std::string(model));
+    py::list out;
+    for (auto& v : mm.vars) {
+      auto q = quantify(v.t);
+      out.append(py::make_tuple(q.non_zeros, q.zeros, q.size_bytes));
+    }
+    return out;
+  });
+  m.def("roundtrip_model", [](py::bytes model) {
+    return B(serialize_model(parse_model(std::string(model))));
+  });
+
+  py::class_<CKKS>(m, "CKKS")
+      .def(py::init<uint32_t, uint32_t>(), py::arg("batch_size"), py::arg("scaling_factor_bits"))
+      .def("gen_crypto_context_and_keys", &CKKS::gen_crypto_context_and_keys,
+           py::call_guard<py::gil_scoped_release>())
+      .def("get_crypto_params_files",
+           [](const CKKS& c) {
+             auto f = c.files();
+             py::dict d;
+             d["crypto_context_file"] = f.crypto_context_file;
+             d["public_key_file"] = f.public_key_file;
+             d["private_key_file"] = f.private_key_file;
+             d["eval_mult_key_file"] = f.eval_mult_key_file;
+             return d;
+           })
+      .def("load_crypto_context_from_file", &CKKS::load_context)
+      .def("load_public_key_from_file", &CKKS::load_public_key)
+      .def("load_private_key_from_file", &CKKS::load_private_key)
+      .def("load_context_and_keys_from_files", &CKKS::load_context_and_keys)
+      .def("encrypt",
+           [](CKKS& c, py::array_t<double, py::array::c_style | py::array::forcecast> a) {
+             std::vector<double> v(a.data(), a.data() + a.size());
+             std::string ct;
+             {
+               py::gil_scoped_release nogil;
+               ct = c.encrypt(v);
+             }
+             return B(ct);
+           })
+      .def("compute_weighted_average",
+           [](const CKKS& c, const std::vector<py::bytes>& cts, const std::vector<double>& w) {
+             std::vector<std::string> owned;
+             for (auto& b : cts) owned.emplace_back(b);
+             std::vector<std::string_view> views(owned.begin(), owned.end());
+             std::string out;
+             {
+               py::gil_scoped_release nogil;
+               out = c.weighted_average(views, w);
+             }
+             return B(out);
+           })
+      .def("decrypt",
+           [](const CKKS& c, py::bytes ct, size_t n) {
+             std::string s(ct);
+             std::vector<double> v;
+             {
+               py::gil_scoped_release nogil;
+               v = c.decrypt(s, n);
+             }
+             return py::array_t<double>(v.size(), v.data());
+           })
+      .def("encode_decode_roundtrip", &CKKS::encode_decode_roundtrip)
+      .def_property_readonly("ring_dim", &CKKS::ring_dim)
+      .def_property_readonly("slots", &CKKS::slots)
+      .def_property_readonly("moduli", &CKKS::moduli);
+}

@@ -42,7 +42,8 @@ void fused_optimizer(int64_t mode, torch::Tensor p, torch::Tensor g,
                      c10::optional<torch::Tensor> anchor, c10::optional<torch::Tensor> p16,
                      double lr, double l1, double l2, double momentum, double mu, double beta1,
                      double beta2, double eps, double wd, c10::optional<torch::Tensor> lr_scale,
-                     c10::optional<torch::Tensor> step) {
+                     c10::optional<torch::Tensor> step, bool zero_grad,
+                     c10::optional<torch::Tensor> zero_region) {
   CHECK_IN(p, torch::kFloat32);
   CHECK_IN(g, torch::kFloat32);
   const int64_t n = p.numel();
@@ -72,7 +73,12 @@ void fused_optimizer(int64_t mode, torch::Tensor p, torch::Tensor g,
   mfl::launch_fused_optimizer((int)mode, p.data_ptr<float>(), g.data_ptr<float>(),
                               ptr_or_null<float>(m), ptr_or_null<float>(v),
                               ptr_or_null<float>(anchor), ptr_or_null<uint16_t>(p16), n, h,
-                              ptr_or_null<float>(lr_scale), ptr_or_null<int>(step), cur_stream(p));
+                              ptr_or_null<float>(lr_scale), ptr_or_null<int>(step), zero_grad,
+                              zero_region.has_value() && zero_region->defined() ? zero_region->data_ptr() : nullptr,
+                              zero_region.has_value() && zero_region->defined()
+                                  ? (int64_t)(zero_region->numel() * zero_region->element_size()) / 16 * 16
+                                  : 0,
+                              cur_stream(p));
 }
 
 void cast_f32_bf16(torch::Tensor x, torch::Tensor y) {
@@ -189,92 +195,101 @@ void check_nhwc(const torch::Tensor& x, int64_t C) {
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "BN channels must be a multiple of 8, <= 2048");
 }
 
-int64_t bn_stats_blocks(int64_t M, int64_t C) { return mfl::bn_stats_blocks(M, (int)C); }
+void check_acc(const torch::Tensor& acc, int64_t C) {
+  TORCH_CHECK(acc.is_cuda() && acc.is_contiguous() && acc.scalar_type() == torch::kFloat64,
+              "BN accumulator must be a contiguous fp64 device tensor");
+  TORCH_CHECK(acc.numel() >= 2 * C, "BN accumulator needs 2*C elements");
+}
+void check_pc(const torch::Tensor& t, int64_t C, const char* nm) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kFloat32, nm,
+              " must be a contiguous fp32 device tensor");
+  TORCH_CHECK(t.numel() == C, nm, " must have C elements");
+}
 
-// Per-channel partial sums [rows][2][C] of an NHWC tensor; returns rows.
-int64_t bn_stats(torch::Tensor x, int64_t C, torch::Tensor partial) {
+// acc[0:C] += sum x, acc[C:2C] += sum x^2 over the M rows of an NHWC tensor.
+void bn_stats(torch::Tensor x, int64_t C, torch::Tensor acc) {
   check_nhwc(x, C);
-  const int64_t M = x.numel() / C;
-  const int nb = mfl::bn_stats_blocks(M, (int)C);
-  CHECK_IN(partial, torch::kFloat32);
-  TORCH_CHECK(partial.numel() >= (int64_t)nb * 2 * C, "partial buffer too small");
-  mfl::launch_bn_stats(bf(x), M, (int)C, partial.data_ptr<float>(), nb, cur_stream(x));
-  return nb;
+  check_acc(acc, C);
+  mfl::launch_bn_stats(bf(x), x.numel() / C, (int)C, acc.data_ptr<double>(), cur_stream(x));
 }
 
-// partial rows -> mean/invstd/scale/shift (+ running-stat update).
-void bn_finalize(torch::Tensor partial, int64_t rows, int64_t M, int64_t C, torch::Tensor gamma,
-                 torch::Tensor beta, torch::Tensor mean, torch::Tensor invstd, torch::Tensor scale,
-                 torch::Tensor shift, c10::optional<torch::Tensor> run_mean,
-                 c10::optional<torch::Tensor> run_var, double momentum, double eps) {
-  CHECK_IN(partial, torch::kFloat32);
-  TORCH_CHECK(partial.numel() >= rows * 2 * C && rows > 0, "partial rows");
-  for (auto* t : {&gamma, &beta, &mean, &invstd, &scale, &shift}) {
-    CHECK_IN((*t), torch::kFloat32);
-    TORCH_CHECK(t->numel() == C, "per-channel tensor size");
-  }
-  mfl::launch_bn_finalize(partial.data_ptr<float>(), (int)rows, M, (int)C, gamma.data_ptr<float>(),
-                          beta.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                          scale.data_ptr<float>(), shift.data_ptr<float>(),
-                          ptr_or_null<float>(run_mean), ptr_or_null<float>(run_var),
-                          (float)momentum, (float)eps, cur_stream(partial));
-}
-
-void bn_apply(torch::Tensor x, int64_t C, torch::Tensor scale, torch::Tensor shift,
-              c10::optional<torch::Tensor> residual, torch::Tensor y, bool relu) {
+// y = relu?(bn(x) (+ residual)).  train: statistics from acc (sums over M rows),
+// publishes mean/invstd and updates running stats; eval: running statistics.
+void bn_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torch::Tensor gamma,
+              torch::Tensor beta, torch::Tensor mean, torch::Tensor invstd,
+              torch::Tensor run_mean, torch::Tensor run_var, c10::optional<torch::Tensor> residual,
+              torch::Tensor y, bool relu, bool train, double momentum, double eps) {
   check_nhwc(x, C);
   check_nhwc(y, C);
   TORCH_CHECK(y.numel() == x.numel(), "bn y size");
-  CHECK_IN(scale, torch::kFloat32);
-  CHECK_IN(shift, torch::kFloat32);
-  TORCH_CHECK(scale.numel() == C && shift.numel() == C, "scale/shift size");
-  const uint16_t* rp = nullptr;
+  for (auto* t : {&gamma, &beta, &mean, &invstd, &run_mean, &run_var}) check_pc(*t, C, "bn param");
+  mfl::BnFwdArgs a{};
+  a.x = bf(x);
+  a.y = bf(y);
+  if (train) {
+    TORCH_CHECK(acc.has_value() && acc->defined(), "training BN needs the statistics accumulator");
+    check_acc(*acc, C);
+    a.acc = acc->data_ptr<double>();
+  }
   if (residual.has_value() && residual->defined()) {
     check_nhwc(*residual, C);
     TORCH_CHECK(residual->numel() == x.numel(), "residual size");
-    rp = bf(*residual);
+    a.residual = bf(*residual);
   }
-  mfl::launch_bn_apply(bf(x), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, bf(y),
-                       x.numel() / C, (int)C, relu, cur_stream(x));
+  a.gamma = gamma.data_ptr<float>();
+  a.beta = beta.data_ptr<float>();
+  a.mean = mean.data_ptr<float>();
+  a.invstd = invstd.data_ptr<float>();
+  a.run_mean = run_mean.data_ptr<float>();
+  a.run_var = run_var.data_ptr<float>();
+  a.M = x.numel() / C;
+  a.C = (int)C;
+  a.momentum = (float)momentum;
+  a.eps = (float)eps;
+  a.train = train ? 1 : 0;
+  a.relu = relu ? 1 : 0;
+  mfl::launch_bn_apply(a, cur_stream(x));
 }
 
+// BN(+ReLU) backward: reduce into acc (fp64 atomics; must be zero on entry),
+// then dx and (optionally) the masked dy for a residual shortcut.
 void bn_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,
-                 torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd,
-                 torch::Tensor partial, torch::Tensor coef, c10::optional<torch::Tensor> dgamma,
-                 c10::optional<torch::Tensor> dbeta, torch::Tensor dx,
-                 c10::optional<torch::Tensor> dy_masked) {
+                 torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd, torch::Tensor acc,
+                 c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta,
+                 torch::Tensor dx, c10::optional<torch::Tensor> dy_masked) {
   check_nhwc(dy, C);
   check_nhwc(x, C);
   check_nhwc(dx, C);
+  check_acc(acc, C);
   TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel(), "bn bwd sizes");
-  const uint16_t* yp = nullptr;
+  for (auto* t : {&gamma, &mean, &invstd}) check_pc(*t, C, "bn param");
+  mfl::BnBwdArgs a{};
+  a.dy = bf(dy);
+  a.x = bf(x);
   if (y.has_value() && y->defined()) {
     check_nhwc(*y, C);
     TORCH_CHECK(y->numel() == x.numel(), "bn bwd y");
-    yp = bf(*y);
+    a.y = bf(*y);
   }
-  uint16_t* dym = nullptr;
   if (dy_masked.has_value() && dy_masked->defined()) {
     check_nhwc(*dy_masked, C);
-    TORCH_CHECK(yp != nullptr, "dy_masked requires y");
-    dym = bf(*dy_masked);
+    TORCH_CHECK(a.y != nullptr, "dy_masked requires y");
+    a.dy_masked = bf(*dy_masked);
   }
-  CHECK_IN(coef, torch::kFloat32);
-  TORCH_CHECK(coef.numel() >= 3 * C, "coef size");
-  const int64_t M = x.numel() / C;
-  const int nb = mfl::bn_stats_blocks(M, (int)C);
-  TORCH_CHECK(partial.numel() >= (int64_t)nb * 2 * C, "partial buffer too small");
+  if (dgamma.has_value() && dgamma->defined()) { check_pc(*dgamma, C, "dgamma"); a.dgamma = dgamma->data_ptr<float>(); }
+  if (dbeta.has_value() && dbeta->defined()) { check_pc(*dbeta, C, "dbeta"); a.dbeta = dbeta->data_ptr<float>(); }
+  a.acc = acc.data_ptr<double>();
+  a.gamma = gamma.data_ptr<float>();
+  a.mean = mean.data_ptr<float>();
+  a.invstd = invstd.data_ptr<float>();
+  a.dx = bf(dx);
+  a.M = x.numel() / C;
+  a.C = (int)C;
   auto s = cur_stream(x);
-  mfl::launch_bn_bwd_reduce(bf(dy), bf(x), yp, mean.data_ptr<float>(), invstd.data_ptr<float>(), M,
-                            (int)C, partial.data_ptr<float>(), nb, s);
-  mfl::launch_bn_bwd_finalize(partial.data_ptr<float>(), nb, M, (int)C, gamma.data_ptr<float>(),
-                              invstd.data_ptr<float>(), ptr_or_null<float>(dgamma),
-                              ptr_or_null<float>(dbeta), coef.data_ptr<float>(), s);
-  mfl::launch_bn_bwd_apply(bf(dy), bf(x), yp, mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                           coef.data_ptr<float>(), bf(dx), dym, M, (int)C, s);
+  mfl::launch_bn_bwd_reduce(a.dy, a.x, a.y, a.mean, a.invstd, a.M, a.C, acc.data_ptr<double>(), s);
+  mfl::launch_bn_bwd_apply(a, s);
 }
 
-// --------------------------------------------------------------------------
 void head_forward_backward(torch::Tensor x, int64_t B, int64_t HW, int64_t C, torch::Tensor W,
                            c10::optional<torch::Tensor> bias, torch::Tensor labels,
                            c10::optional<torch::Tensor> feat, c10::optional<torch::Tensor> dlogits,
@@ -347,9 +362,7 @@ PYBIND11_MODULE(_ops, m) {
   m.def("rolling_op", &rolling_op);
   m.def("count_zeros", &count_zeros);
   m.def("ckks_pwa", &ckks_pwa);
-  m.def("bn_stats_blocks", &bn_stats_blocks);
   m.def("bn_stats", &bn_stats);
-  m.def("bn_finalize", &bn_finalize);
   m.def("bn_apply", &bn_apply);
   m.def("bn_backward", &bn_backward);
   m.def("head_forward_backward", &head_forward_backward);

@@ -54,36 +54,41 @@ std::string serialize_tensor_spec(const TensorT& t) {
   return w.take();
 }
 
+VariableT parse_variable(std::string_view bytes) {
+  wire::WireMsg vm(bytes);
+  VariableT v;
+  v.name = vm.str(1);
+  v.trainable = vm.b(2);
+  if (vm.has(3)) {
+    v.ciphertext = false;
+    v.t = parse_tensor_spec(vm.msg(3).bytes(1));
+  } else if (vm.has(4)) {
+    v.ciphertext = true;
+    v.t = parse_tensor_spec(vm.msg(4).bytes(1));
+  }
+  return v;
+}
+
+std::string serialize_variable(const VariableT& v) {
+  wire::Writer vw;
+  vw.bytes(1, v.name);
+  vw.boolean(2, v.trainable);
+  wire::Writer tw;
+  tw.bytes(1, serialize_tensor_spec(v.t), true);
+  vw.msg(v.ciphertext ? 4 : 3, tw);
+  return vw.take();
+}
+
 ModelT parse_model(std::string_view bytes) {
   wire::WireMsg m(bytes);
   ModelT out;
-  for (auto& vm : m.msgs(1)) {
-    VariableT v;
-    v.name = vm.str(1);
-    v.trainable = vm.b(2);
-    if (vm.has(3)) {
-      v.ciphertext = false;
-      v.t = parse_tensor_spec(vm.msg(3).bytes(1));
-    } else if (vm.has(4)) {
-      v.ciphertext = true;
-      v.t = parse_tensor_spec(vm.msg(4).bytes(1));
-    }
-    out.vars.push_back(std::move(v));
-  }
+  for (auto sv : m.strs(1)) out.vars.push_back(parse_variable(sv));
   return out;
 }
 
 std::string serialize_model(const ModelT& m) {
   wire::Writer w;
-  for (auto& v : m.vars) {
-    wire::Writer vw;
-    vw.bytes(1, v.name);
-    vw.boolean(2, v.trainable);
-    wire::Writer tw;
-    tw.bytes(1, serialize_tensor_spec(v.t), true);
-    vw.msg(v.ciphertext ? 4 : 3, tw);
-    w.msg(1, vw);
-  }
+  for (auto& v : m.vars) w.bytes(1, serialize_variable(v), true);
   return w.take();
 }
 

@@ -52,6 +52,8 @@ struct Quantifier {
   uint64_t non_zeros = 0, zeros = 0, size_bytes = 0;
 };
 
+VariableT parse_variable(std::string_view bytes);
+std::string serialize_variable(const VariableT& v);
 ModelT parse_model(std::string_view bytes);
 std::string serialize_model(const ModelT& m);
 FederatedModelT parse_federated_model(std::string_view bytes);

@@ -31,14 +31,14 @@ ConvPlan plan_conv_gemm(const ConvGeom& g);
 ConvPlan plan_conv_wgrad(const ConvGeom& g);
 int splitk_stats_blocks(int M, int C);
 
-// y (bf16 [M][Ng]) and, when stats != nullptr, BN partial sums
-// [rows][2][Ng] (rows = plan.stats_rows, or splitk_stats_blocks() when split).
+// y (bf16 [M][Ng]) and, when stats != nullptr, fp64 atomic accumulation of the
+// per-channel BatchNorm sums into stats[0..Ng) / stats[Ng..2Ng).
 void launch_conv_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const uint16_t* src,
-                      const uint16_t* wgt, uint16_t* y, float* ysplit, float* stats, bool accum,
+                      const uint16_t* wgt, uint16_t* y, float* ysplit, double* stats, bool accum,
                       hipStream_t s);
-// dw (fp32 [Cout][R][S][Cin]); wsplit workspace [splits][Cout*K] when split.
+// dw (fp32 [Cout][R][S][Cin]); must be zeroed first when p.splits > 1.
 void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, const uint16_t* dy,
-                       float* dw, float* wsplit, hipStream_t s);
+                       float* dw, hipStream_t s);
 void launch_transpose_krsc(const uint16_t* w, uint16_t* wt, int Co, int RS, int Ci, hipStream_t s);
 
 }  // namespace mfl

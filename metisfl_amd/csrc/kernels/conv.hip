@@ -11,8 +11,9 @@
 //    operand fragments (8 consecutive k per lane) are read from LDS with one
 //    ds_read_b128.  Cin must be a multiple of 8 (the 3-channel CIFAR input is
 //    zero-padded to 8 channels once, at shard creation).
-//  * dgrad is the same kernel with a stride-aware gather of dY and the weight
-//    pre-transposed to [Cin][R][S][Cout] (one small launch per step).
+//  * dgrad is the same kernel with a stride-aware gather of dY; its B operand
+//    (W^T) is staged from the KRSC weight as [k][c] tiles and read with the
+//    transposing ds_read_b64_tr_b16, so no weight transpose pass exists.
 //  * wgrad reduces over the N*P*Q pixels, which are strided in both operands:
 //    tiles are staged [m][col] in LDS and the MFMA fragments are formed with
 //    the gfx950 transposing LDS read ds_read_b64_tr_b16 (guide T10).
@@ -22,8 +23,10 @@
 //    buffering with one barrier per k-step (guide T14 / "minimum 2-phase").
 //  * Small-M layers (CIFAR 4x4/8x8 stages) use split-K so a launch still
 //    fills >= 256 CUs; the split reduction kernel also emits the per-channel
-//    BatchNorm partial sums, and the non-split epilogue emits them directly,
-//    so the BN statistics pass never re-reads the conv output.
+//    BatchNorm sums, and the non-split epilogue emits them directly (fp64
+//    atomics into a [2][C] accumulator), so BN never re-reads the conv output
+//    for statistics.  wgrad split-K slices accumulate with fp32 atomics into
+//    the (pre-zeroed) flat gradient buffer: no reduction launch.
 #include "kernels/common.h"
 #include "kernels/conv.h"
 
@@ -44,7 +47,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
                                                         const uint16_t* __restrict__ wgt,
                                                         uint16_t* __restrict__ y,
                                                         float* __restrict__ ysplit,
-                                                        float* __restrict__ stats, int kchunk,
+                                                        double* __restrict__ stats, int kchunk,
                                                         int accum) {
   constexpr int ACH = BM / 32;  // A 16-B chunks per thread per k-step
   constexpr int BCH = BN / 32;
@@ -287,8 +290,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
   for (int cl = t; cl < BN; cl += 256) {
     const int col = n0 + cl;
     if (col < g.Ng) {
-      stats[(int64_t)blockIdx.x * 2 * g.Ng + col] = red[0 * BN + cl] + red[2 * BN + cl];
-      stats[(int64_t)blockIdx.x * 2 * g.Ng + g.Ng + col] = red[1 * BN + cl] + red[3 * BN + cl];
+      atomicAdd(&stats[col], (double)(red[0 * BN + cl] + red[2 * BN + cl]));
+      atomicAdd(&stats[g.Ng + col], (double)(red[1 * BN + cl] + red[3 * BN + cl]));
     }
   }
 }
@@ -298,7 +301,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ysplit,
                                                             int splits, int M, int C,
                                                             uint16_t* __restrict__ y,
-                                                            float* __restrict__ stats, int accum) {
+                                                            double* __restrict__ stats, int accum) {
   const int tpr = C / 8;
   const int rpp = 256 / tpr;
   const int t = threadIdx.x;
@@ -348,8 +351,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       s0 += sh[0][(r * tpr + (c >> 3)) * 8 + (c & 7)];
       s1 += sh[1][(r * tpr + (c >> 3)) * 8 + (c & 7)];
     }
-    stats[(int64_t)blockIdx.x * 2 * C + c] = s0;
-    stats[(int64_t)blockIdx.x * 2 * C + C + c] = s1;
+    atomicAdd(&stats[c], (double)s0);
+    atomicAdd(&stats[C + c], (double)s1);
   }
 }
 
@@ -501,7 +504,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvGeom g, const uint1
     if (kt + 1 < nk) store_tile(cur ^ 1);
     __syncthreads();
   }
-  float* out = dw + (int64_t)blockIdx.z * g.Ng * g.K;
+  const bool atomic = gridDim.z > 1;  // split-K slices add into the zeroed slot
   const int rbase = ko0 + wm * (BM / 2) + (lane >> 4) * 4;
   const int cbase = j0 + wn * (BN / 2) + li;
 #pragma unroll
@@ -511,22 +514,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvGeom g, const uint1
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = rbase + 16 * i + e, col = cbase + 16 * j;
-        if (row < g.Ng && col < g.K) out[(int64_t)row * g.K + col] = acc[i][j][e];
+        if (row < g.Ng && col < g.K) {
+          if (atomic)
+            atomicAdd(&dw[(int64_t)row * g.K + col], acc[i][j][e]);
+          else
+            dw[(int64_t)row * g.K + col] = acc[i][j][e];
+        }
       }
-}
-
-// Sum wgrad split partials into the fp32 gradient slot (float4 lanes).
-__global__ __launch_bounds__(256) void sum_splits_kernel(const float* __restrict__ part, int splits,
-                                                         int64_t n4, float* __restrict__ out) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 a = reinterpret_cast<const float4*>(part)[i];
-    for (int z = 1; z < splits; ++z) {
-      const float4 b = reinterpret_cast<const float4*>(part)[z * n4 + i];
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-    }
-    reinterpret_cast<float4*>(out)[i] = a;
-  }
 }
 
 // [Cout][R][S][Cin] -> [Cin][R][S][Cout]  (dgrad weight layout)
@@ -548,7 +542,7 @@ __global__ __launch_bounds__(256) void transpose_krsc_kernel(const uint16_t* __r
 // ---------------------------------------------------------------------------
 template <int BM, int BN, bool DG>
 static void launch_gemm_t(const ConvGeom& g, const uint16_t* src, const uint16_t* wgt, uint16_t* y,
-                          float* ysplit, float* stats, int splits, int kchunk, int accum,
+                          float* ysplit, double* stats, int splits, int kchunk, int accum,
                           hipStream_t s) {
   dim3 grid((g.M + BM - 1) / BM, (g.Ng + BN - 1) / BN, splits);
   const size_t btile = DG ? (size_t)kBK * (BN + kPad) : (size_t)BN * kLdsStride;
@@ -578,11 +572,11 @@ ConvPlan plan_conv_gemm(const ConvGeom& g) {
 }
 
 void launch_conv_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const uint16_t* src,
-                      const uint16_t* wgt, uint16_t* y, float* ysplit, float* stats, bool accum,
+                      const uint16_t* wgt, uint16_t* y, float* ysplit, double* stats, bool accum,
                       hipStream_t s) {
   const int ac = accum ? 1 : 0;
   float* ys = p.splits > 1 ? ysplit : nullptr;
-  float* st = p.splits > 1 ? nullptr : stats;
+  double* st = p.splits > 1 ? nullptr : stats;
 #define MFL_CONV_CASE(BM_, BN_)                                                                \
   if (p.bm == BM_ && p.bn == BN_) {                                                            \
     if (dgrad) launch_gemm_t<BM_, BN_, true>(g, src, wgt, y, ys, st, p.splits, p.kchunk, ac, s);   \
@@ -620,16 +614,14 @@ ConvPlan plan_conv_wgrad(const ConvGeom& g) {
   return p;
 }
 
+// dw must be zero on entry when p.splits > 1 (slices accumulate with fp32
+// atomics); the training step gets that for free from the optimizer launch,
+// which zeroes the gradient buffer after consuming it.
 void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, const uint16_t* dy,
-                       float* dw, float* wsplit, hipStream_t s) {
+                       float* dw, hipStream_t s) {
   dim3 grid((g.Ng + 63) / 64, (g.K + 63) / 64, p.splits);
   const size_t lds = (size_t)2 * kBK * ((64 + kPad) + (64 + kPad)) * sizeof(uint16_t);
-  float* out = p.splits > 1 ? wsplit : dw;
-  conv_wgrad_kernel<64, 64><<<grid, 256, lds, s>>>(g, x, dy, out, p.kchunk);
-  if (p.splits > 1) {
-    const int64_t n4 = (int64_t)g.Ng * g.K / 4;
-    sum_splits_kernel<<<stream_grid(n4), 256, 0, s>>>(wsplit, p.splits, n4, dw);
-  }
+  conv_wgrad_kernel<64, 64><<<grid, 256, lds, s>>>(g, x, dy, dw, p.kchunk);
 }
 
 void launch_transpose_krsc(const uint16_t* w, uint16_t* wt, int Co, int RS, int Ci, hipStream_t s) {

@@ -19,9 +19,12 @@ struct OptHyper {
 };
 
 // ---- optim.hip -----------------------------------------------------------
-void launch_fused_optimizer(int mode, float* p, const float* g, float* m, float* v,
+// zero_grad: write 0 back into g after use (next step's atomics start from 0);
+// zero/zero_bytes: an extra region (BN accumulators) zeroed by the same launch.
+void launch_fused_optimizer(int mode, float* p, float* g, float* m, float* v,
                             const float* anchor, uint16_t* p16, int64_t n, const OptHyper& h,
-                            const float* lr_ptr, const int* step_ptr, hipStream_t s);
+                            const float* lr_ptr, const int* step_ptr, bool zero_grad, void* zero,
+                            int64_t zero_bytes, hipStream_t s);
 void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
 void launch_scale_f32(float* x, int64_t n, float w, const float* wptr, hipStream_t s);
 void launch_tick(int* step, int inc, hipStream_t s);
@@ -46,24 +49,44 @@ void launch_ckks_pwa(const uint64_t* const* cts, const uint64_t* wq, int nlearne
                      hipStream_t s);
 
 // ---- bn.hip --------------------------------------------------------------
-void launch_bn_stats(const uint16_t* x, int64_t M, int C, float* partial, int nblocks,
-                     hipStream_t s);
+struct BnFwdArgs {
+  const uint16_t* x;
+  const uint16_t* residual;  // optional
+  uint16_t* y;
+  const double* acc;         // [2][C] sum / sumsq (train)
+  const float* gamma;
+  const float* beta;
+  float* mean;               // saved for backward (train)
+  float* invstd;
+  float* run_mean;           // updated (train) / read (eval)
+  float* run_var;
+  int64_t M;
+  int C;
+  float momentum, eps;
+  int train, relu;
+};
+struct BnBwdArgs {
+  const uint16_t* dy;
+  const uint16_t* x;   // BN input (pre-normalisation)
+  const uint16_t* y;   // BN(+res)(+relu) output: ReLU mask, optional
+  const double* acc;   // [2][C] sum dyr / sum dyr*xhat
+  const float* gamma;
+  const float* mean;
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
+  uint16_t* dx;
+  uint16_t* dy_masked;  // optional
+  int64_t M;
+  int C;
+};
 int bn_stats_blocks(int64_t M, int C);
-void launch_bn_finalize(const float* partial, int nblocks, int64_t M, int C, const float* gamma,
-                        const float* beta, float* mean, float* invstd, float* scale, float* shift,
-                        float* run_mean, float* run_var, float momentum, float eps, hipStream_t s);
-void launch_bn_apply(const uint16_t* x, const float* scale, const float* shift,
-                     const uint16_t* residual, uint16_t* y, int64_t M, int C, bool relu,
-                     hipStream_t s);
+void launch_bn_stats(const uint16_t* x, int64_t M, int C, double* acc, hipStream_t s);
+void launch_bn_apply(const BnFwdArgs& a, hipStream_t s);
 void launch_bn_bwd_reduce(const uint16_t* dy, const uint16_t* x, const uint16_t* y,
-                          const float* mean, const float* invstd, int64_t M, int C, float* partial,
-                          int nblocks, hipStream_t s);
-void launch_bn_bwd_finalize(const float* partial, int nblocks, int64_t M, int C,
-                            const float* gamma, const float* invstd, float* dgamma, float* dbeta,
-                            float* coef, hipStream_t s);
-void launch_bn_bwd_apply(const uint16_t* dy, const uint16_t* x, const uint16_t* y,
-                         const float* mean, const float* invstd, const float* coef, uint16_t* dx,
-                         uint16_t* dy_masked, int64_t M, int C, hipStream_t s);
+                          const float* mean, const float* invstd, int64_t M, int C, double* acc,
+                          hipStream_t s);
+void launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t s);
 
 // ---- head.hip ------------------------------------------------------------
 void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,

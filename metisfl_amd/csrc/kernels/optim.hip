@@ -18,9 +18,10 @@ namespace mfl {
 
 template <int MODE, bool W16>
 __global__ __launch_bounds__(256) void fused_opt_kernel(
-    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-    float* __restrict__ v, const float* __restrict__ anchor, uint16_t* __restrict__ p16,
-    int64_t n4, OptHyper h, const float* __restrict__ lr_ptr, const int* __restrict__ step_ptr) {
+    float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+    const float* __restrict__ anchor, uint16_t* __restrict__ p16, int64_t n4, OptHyper h,
+    const float* __restrict__ lr_ptr, const int* __restrict__ step_ptr, int zero_grad,
+    uint4* __restrict__ zero, int64_t zero16) {
   const float lr = lr_ptr ? lr_ptr[0] * h.lr : h.lr;
   float bc1 = 1.f, bc2 = 1.f;
   if (MODE == OPT_ADAM || MODE == OPT_ADAMW) {
@@ -29,9 +30,12 @@ __global__ __launch_bounds__(256) void fused_opt_kernel(
     bc2 = 1.f - powf(h.beta2, t);
   }
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = tid; i < zero16; i += stride) zero[i] = make_uint4(0, 0, 0, 0);
+  for (int64_t i = tid; i < n4; i += stride) {
     float4 pv = reinterpret_cast<float4*>(p)[i];
     const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     float* pp = &pv.x;
     const float* gg = &gv.x;
     if (MODE == OPT_SGD) {
@@ -85,28 +89,37 @@ __global__ __launch_bounds__(256) void fused_opt_kernel(
 }
 
 template <int MODE>
-static void launch_mode(float* p, const float* g, float* m, float* v, const float* anchor,
+static void launch_mode(float* p, float* g, float* m, float* v, const float* anchor,
                         uint16_t* p16, int64_t n, const OptHyper& h, const float* lr_ptr,
-                        const int* step_ptr, hipStream_t s) {
+                        const int* step_ptr, bool zg, void* zero, int64_t zero_bytes,
+                        hipStream_t s) {
   const int64_t n4 = n / 4;
-  const unsigned grid = stream_grid(n4, 256, 2048);
+  const int64_t z16 = zero ? zero_bytes / 16 : 0;
+  const unsigned grid = stream_grid(n4 > z16 ? n4 : z16, 256, 2048);
+  uint4* z = reinterpret_cast<uint4*>(zero);
   if (p16)
-    fused_opt_kernel<MODE, true><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr, step_ptr);
+    fused_opt_kernel<MODE, true><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr,
+                                                      step_ptr, zg ? 1 : 0, z, z16);
   else
-    fused_opt_kernel<MODE, false><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr, step_ptr);
+    fused_opt_kernel<MODE, false><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr,
+                                                       step_ptr, zg ? 1 : 0, z, z16);
 }
 
-void launch_fused_optimizer(int mode, float* p, const float* g, float* m, float* v,
+void launch_fused_optimizer(int mode, float* p, float* g, float* m, float* v,
                             const float* anchor, uint16_t* p16, int64_t n, const OptHyper& h,
-                            const float* lr_ptr, const int* step_ptr, hipStream_t s) {
+                            const float* lr_ptr, const int* step_ptr, bool zero_grad, void* zero,
+                            int64_t zero_bytes, hipStream_t s) {
+#define MFL_OPT_CASE(M_) \
+  case M_: launch_mode<M_>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, zero_grad, zero, zero_bytes, s); break;
   switch (mode) {
-    case OPT_SGD: launch_mode<OPT_SGD>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, s); break;
-    case OPT_MOMENTUM: launch_mode<OPT_MOMENTUM>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, s); break;
-    case OPT_FEDPROX: launch_mode<OPT_FEDPROX>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, s); break;
-    case OPT_ADAM: launch_mode<OPT_ADAM>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, s); break;
-    case OPT_ADAMW: launch_mode<OPT_ADAMW>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, s); break;
+    MFL_OPT_CASE(OPT_SGD)
+    MFL_OPT_CASE(OPT_MOMENTUM)
+    MFL_OPT_CASE(OPT_FEDPROX)
+    MFL_OPT_CASE(OPT_ADAM)
+    MFL_OPT_CASE(OPT_ADAMW)
     default: break;
   }
+#undef MFL_OPT_CASE
 }
 
 // ---------------------------------------------------------------------------

@@ -133,11 +133,11 @@ class FlatState:
         if spec.needs_anchor and self.anchor is None:
             self.anchor = self.params32.clone()
 
-    def optimizer_step(self) -> None:
+    def optimizer_step(self, zero_grad: bool = True, zero_region: torch.Tensor | None = None) -> None:
         if self.n_params == 0 or self.optimizer is None:
             return
         opt_ops.fused_step(self.optimizer, self.params32, self.grad32, self.m, self.v, self.anchor,
-                           self.p16, self.lr_scale, self.step)
+                           self.p16, self.lr_scale, self.step, zero_grad, zero_region)
 
     def set_anchor(self) -> None:
         """Snapshot the received community model as the FedProx anchor."""

@@ -23,30 +23,31 @@ from metisfl_amd.ops.nn import ConvShape
 
 
 class Workspace:
-    """Shared scratch: split-K slabs and BatchNorm partial sums.  Kernels on
-    one stream run in order, so one buffer of the maximum size serves all."""
+    """Shared scratch: the split-K fp32 slab (kernels on one stream run in
+    order, so one buffer of the maximum size serves every layer) and the
+    model-wide fp64 BatchNorm accumulator buffer, carved per layer.  The
+    accumulators are re-zeroed by the optimizer launch at the end of a step."""
 
     def __init__(self):
         self.split_floats = 0
-        self.partial_floats = 0
         self.split: torch.Tensor | None = None
-        self.partial: torch.Tensor | None = None
-        self.coef_floats = 0
-        self.coef: torch.Tensor | None = None
+        self.acc_len = 0
+        self.bn_acc: torch.Tensor | None = None
 
     def need_split(self, n: int) -> None:
         self.split_floats = max(self.split_floats, n)
 
-    def need_partial(self, n: int) -> None:
-        self.partial_floats = max(self.partial_floats, n)
+    def take_acc(self, n: int) -> tuple[int, int]:
+        off = self.acc_len
+        self.acc_len += (n + 1) // 2 * 2  # keep 16-B alignment of every slice
+        return (off, n)
 
-    def need_coef(self, n: int) -> None:
-        self.coef_floats = max(self.coef_floats, n)
+    def acc(self, sl: tuple[int, int]) -> torch.Tensor:
+        return self.bn_acc[sl[0]: sl[0] + sl[1]]
 
     def allocate(self, device) -> None:
         self.split = torch.zeros(max(4, self.split_floats), dtype=torch.float32, device=device)
-        self.partial = torch.zeros(max(4, self.partial_floats), dtype=torch.float32, device=device)
-        self.coef = torch.zeros(max(4, self.coef_floats), dtype=torch.float32, device=device)
+        self.bn_acc = torch.zeros(max(2, self.acc_len), dtype=torch.float64, device=device)
 
 
 class Layer:
@@ -110,34 +111,24 @@ class ConvBN(Layer):
         self.dz = torch.zeros(self.out_shape, **bf)
         self.mean = torch.zeros(s.Co, **f32)
         self.invstd = torch.zeros(s.Co, **f32)
-        self.scale = torch.zeros(s.Co, **f32)
-        self.shift = torch.zeros(s.Co, **f32)
+        # fp64 [2C] statistics accumulators (forward sums, backward sums),
+        # carved from the model-wide buffer the optimizer launch re-zeroes
+        self.acc_f = ws.take_acc(2 * s.Co)
+        self.acc_b = ws.take_acc(2 * s.Co)
         dev = torch.device(device)
         self.pf = K.conv_plan(0, s, dev)
         self.pd = K.conv_plan(1, s, dev)
         self.pw = K.conv_plan(2, s, dev)
         ws.need_split(self.pf.workspace)
         ws.need_split(self.pd.workspace)
-        ws.need_split(self.pw.workspace)
-        self.bn_rows = K.bn_stats_rows(self.M, s.Co, dev)
-        ws.need_partial(max(self.pf.stats_rows, self.bn_rows) * 2 * s.Co)
-        ws.need_coef(3 * s.Co)
 
     def forward(self, x: torch.Tensor, residual: torch.Tensor | None = None, train: bool = True):
         s = self.shp
         self.x = x
-        if train:
-            K.conv_forward(x, self.w16, self.z, s, self.ws.split, self.ws.partial)
-            K.bn_finalize(self.ws.partial, self.pf.stats_rows, self.M, s.Co, self.gamma, self.beta,
-                          self.mean, self.invstd, self.scale, self.shift, self.rmean, self.rvar,
-                          self.momentum, self.eps)
-        else:
-            K.conv_forward(x, self.w16, self.z, s, self.ws.split, None)
-            torch.rsqrt(self.rvar + self.eps, out=self.scale)
-            self.scale.mul_(self.gamma)
-            torch.mul(self.rmean, self.scale, out=self.shift)
-            torch.sub(self.beta, self.shift, out=self.shift)
-        K.bn_apply(self.z, s.Co, self.scale, self.shift, self.y, residual, self.relu)
+        K.conv_forward(x, self.w16, self.z, s, self.ws.split, self.ws.acc(self.acc_f) if train else None)
+        K.bn_apply(self.z, s.Co, self.ws.acc(self.acc_f), self.gamma, self.beta, self.mean,
+                   self.invstd, self.rmean, self.rvar, self.y, residual, self.relu, train,
+                   self.momentum, self.eps)
         return self.y
 
     def backward(self, dy: torch.Tensor, dx: torch.Tensor | None, accumulate: bool = False,
@@ -147,11 +138,11 @@ class ConvBN(Layer):
         receives the ReLU-masked dy that the residual branch needs."""
         s = self.shp
         K.bn_backward(dy, self.z, self.y if self.relu else None, s.Co, self.gamma, self.mean,
-                      self.invstd, self.ws.partial, self.ws.coef, self.dgamma, self.dbeta, self.dz,
-                      dres)
+                      self.invstd, self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz, dres)
         if dx is not None:
             K.conv_dgrad(self.dz, self.w16, dx, s, self.ws.split, accumulate)
-        K.conv_wgrad(self.x, self.dz, self.dw, s, self.ws.split)
+        # gradient buffer is zero on entry (re-zeroed by the optimizer launch)
+        K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True)
 
 
 class BasicBlock(Layer):

@@ -106,15 +106,22 @@ class StaticNet:
         raise NotImplementedError
 
     # -- step bodies ---------------------------------------------------------
+    # When False (tests that inspect gradients after a step) the gradient
+    # buffer is zeroed at the start of the step instead of by the optimizer.
+    zero_grad_in_optimizer: bool = True
+
     def _train_body(self, ds: DeviceDataset) -> None:
         st = self.state
+        if not self.zero_grad_in_optimizer:
+            st.grad32.zero_()
         K.gather_batch(ds.x, ds.y, ds.perm, st.step, ds.steps_per_epoch, self.B, self.xb, self.yb)
         out = self.forward(self.xb, train=True)
         dlast = self.head.forward_backward(out, self.yb, self.stats, train=True)
         for l in self.all_layers():
             l.prepare_backward()
         self.backward(dlast)
-        st.optimizer_step()
+        # one launch: optimizer + grad re-zero + BN accumulator re-zero
+        st.optimizer_step(zero_grad=self.zero_grad_in_optimizer, zero_region=self.ws.bn_acc)
         opt_ops.tick(st.step, 1)
 
     def _eval_body(self, ds: DeviceDataset) -> None:

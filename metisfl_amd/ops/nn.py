@@ -59,7 +59,8 @@ class ConvPlan:
 
 
 def conv_plan(mode: int, shp: ConvShape, device: torch.device) -> ConvPlan:
-    """mode 0 fwd / 1 dgrad / 2 wgrad.  CPU path: no workspace, 1 stats row."""
+    """mode 0 fwd / 1 dgrad / 2 wgrad (tile sizes, split-K factor, fp32 split-K
+    workspace floats).  CPU path: no workspace."""
     if device.type == "cuda":
         return ConvPlan(*ops().conv_plan(mode, *shp.args()))
     return ConvPlan(0, 0, 1, 0, 1, 0)
@@ -75,21 +76,23 @@ def _wt(w: torch.Tensor) -> torch.Tensor:
     return w.float().permute(0, 3, 1, 2)
 
 
-def _stats_rows_cpu(y: torch.Tensor, stats: torch.Tensor) -> None:
-    yf = y.float().reshape(-1, y.shape[-1])
+def _acc_stats_cpu(y: torch.Tensor, acc: torch.Tensor) -> None:
+    yf = y.float().reshape(-1, y.shape[-1]).double()
     C = yf.shape[1]
-    stats.view(-1)[:C].copy_(yf.sum(0))
-    stats.view(-1)[C:2 * C].copy_((yf * yf).sum(0))
+    acc[:C] += yf.sum(0)
+    acc[C:2 * C] += (yf * yf).sum(0)
 
 
 def conv_forward(x, w, y, shp: ConvShape, ws=None, stats=None) -> None:
+    """y = conv(x, w); ``stats`` (fp64 [2*Cout]) accumulates the per-channel
+    sum / sum-of-squares of the bf16 output for the following BatchNorm."""
     if x.is_cuda:
         ops().conv_forward(x, w, y, ws, stats, *shp.args())
         return
     out = F.conv2d(_nchw(x), _wt(w), stride=shp.stride, padding=shp.pad)
     y.copy_(out.permute(0, 2, 3, 1).to(torch.bfloat16))
     if stats is not None:
-        _stats_rows_cpu(y, stats)
+        _acc_stats_cpu(y, stats)
 
 
 def conv_dgrad(dy, w, dx, shp: ConvShape, ws=None, accumulate: bool = False) -> None:
@@ -107,10 +110,11 @@ def conv_dgrad(dy, w, dx, shp: ConvShape, ws=None, accumulate: bool = False) -> 
     dx.copy_(g.to(torch.bfloat16))
 
 
-def conv_wgrad(x, dy, dw, shp: ConvShape, ws=None) -> None:
-    """dw (fp32 [Cout][R][S][Cin]) = sum over pixels of dy x im2col(x)."""
+def conv_wgrad(x, dy, dw, shp: ConvShape, accumulate: bool = False) -> None:
+    """dw (fp32 [Cout][R][S][Cin]) = sum over pixels of dy x im2col(x).
+    accumulate=True promises dw is already zero (split-K slices add into it)."""
     if x.is_cuda:
-        ops().conv_wgrad(x, dy, dw, ws, *shp.args())
+        ops().conv_wgrad(x, dy, dw, *shp.args(), accumulate)
         return
     g = torch.nn.grad.conv2d_weight(_nchw(x), (shp.Co, shp.C, shp.R, shp.S), _nchw(dy),
                                     stride=shp.stride, padding=shp.pad)
@@ -125,41 +129,40 @@ def transpose_krsc(w, wt, Co: int, RS: int, Ci: int) -> None:
 
 
 # ---------------------------------------------------------------------------
-def bn_stats_rows(M: int, C: int, device: torch.device) -> int:
-    return int(ops().bn_stats_blocks(M, C)) if device.type == "cuda" else 1
-
-
-def bn_stats(x, C: int, partial) -> int:
+def bn_stats(x, C: int, acc) -> None:
+    """acc[0:C] += sum x, acc[C:2C] += sum x^2 (fp64) over the rows of NHWC x."""
     if x.is_cuda:
-        return int(ops().bn_stats(x, C, partial))
-    _stats_rows_cpu(x, partial)
-    return 1
-
-
-def bn_finalize(partial, rows: int, M: int, C: int, gamma, beta, mean, invstd, scale, shift,
-                run_mean=None, run_var=None, momentum: float = 0.1, eps: float = 1e-5) -> None:
-    if partial.is_cuda:
-        ops().bn_finalize(partial, rows, M, C, gamma, beta, mean, invstd, scale, shift, run_mean,
-                          run_var, momentum, eps)
+        ops().bn_stats(x, C, acc)
         return
-    p = partial.view(-1)[: rows * 2 * C].view(rows, 2, C).double().sum(0)
-    mu = p[0] / M
-    var = (p[1] / M - mu * mu).clamp_min(0)
-    istd = 1.0 / torch.sqrt(var + eps)
-    mean.copy_(mu.float())
-    invstd.copy_(istd.float())
-    scale.copy_(gamma * istd.float())
-    shift.copy_(beta - mu.float() * gamma * istd.float())
-    if run_mean is not None:
+    _acc_stats_cpu(x, acc)
+
+
+def bn_apply(x, C: int, acc, gamma, beta, mean, invstd, run_mean, run_var, y, residual=None,
+             relu: bool = False, train: bool = True, momentum: float = 0.1,
+             eps: float = 1e-5) -> None:
+    """y = relu?(BN(x) + residual).  train: batch statistics from ``acc`` (sums
+    over the M rows), publishes mean/invstd, updates running stats; eval:
+    running statistics."""
+    if x.is_cuda:
+        ops().bn_apply(x, C, acc, gamma, beta, mean, invstd, run_mean, run_var, residual, y, relu,
+                       train, momentum, eps)
+        return
+    M = x.numel() // C
+    if train:
+        mu = acc[:C] / M
+        var = (acc[C:2 * C] / M - mu * mu).clamp_min(0)
+        mean.copy_(mu.float())
+        invstd.copy_((1.0 / torch.sqrt(var + eps)).float())
         unb = var * M / (M - 1) if M > 1 else var
         run_mean.mul_(1 - momentum).add_(momentum * mu.float())
         run_var.mul_(1 - momentum).add_(momentum * unb.float())
-
-
-def bn_apply(x, C: int, scale, shift, y, residual=None, relu: bool = False) -> None:
-    if x.is_cuda:
-        ops().bn_apply(x, C, scale, shift, residual, y, relu)
-        return
+        istd = (1.0 / torch.sqrt(var + eps)).float()
+        mu = mu.float()
+    else:
+        mu = run_mean
+        istd = 1.0 / torch.sqrt(run_var.double() + eps).float()
+    scale = gamma * istd
+    shift = beta - mu * scale
     v = x.float() * scale + shift
     if residual is not None:
         v = v + residual.float()
@@ -168,14 +171,14 @@ def bn_apply(x, C: int, scale, shift, y, residual=None, relu: bool = False) -> N
     y.copy_(v.to(torch.bfloat16))
 
 
-def bn_backward(dy, x, y, C: int, gamma, mean, invstd, partial, coef, dgamma, dbeta, dx,
+def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
                 dy_masked=None) -> None:
     """BN(+ReLU) backward.  ``y`` (the post-activation output) gives the ReLU
     mask; ``dy_masked`` optionally receives the masked upstream gradient (the
-    residual-shortcut gradient of an add+ReLU)."""
+    residual-shortcut gradient of an add+ReLU).  ``acc`` (fp64 [2C]) must be
+    zero on entry."""
     if dy.is_cuda:
-        ops().bn_backward(dy, x, y, C, gamma, mean, invstd, partial, coef, dgamma, dbeta, dx,
-                          dy_masked)
+        ops().bn_backward(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked)
         return
     g = dy.float()
     if y is not None:
@@ -188,12 +191,14 @@ def bn_backward(dy, x, y, C: int, gamma, mean, invstd, partial, coef, dgamma, db
     M = gm.shape[0]
     s = gm.double().sum(0)
     q = (gm.double() * xh.reshape(-1, C).double()).sum(0)
+    acc[:C] += s
+    acc[C:2 * C] += q
     if dgamma is not None:
-        dgamma.copy_(q.float())
+        dgamma.copy_(acc[C:2 * C].float())
     if dbeta is not None:
-        dbeta.copy_(s.float())
+        dbeta.copy_(acc[:C].float())
     k1 = gamma * invstd
-    out = k1 * (g - (s / M).float() - xh * (q / M).float())
+    out = k1 * (g - (acc[:C] / M).float() - xh * (acc[C:2 * C] / M).float())
     dx.copy_(out.to(torch.bfloat16))
 
 

@@ -88,14 +88,23 @@ class OptimizerSpec:
 def fused_step(spec: OptimizerSpec, p: torch.Tensor, g: torch.Tensor,
                m: torch.Tensor | None = None, v: torch.Tensor | None = None,
                anchor: torch.Tensor | None = None, p16: torch.Tensor | None = None,
-               lr_scale: torch.Tensor | None = None, step: torch.Tensor | None = None) -> None:
-    """Apply one optimizer step in place over flat buffers."""
+               lr_scale: torch.Tensor | None = None, step: torch.Tensor | None = None,
+               zero_grad: bool = False, zero_region: torch.Tensor | None = None) -> None:
+    """Apply one optimizer step in place over flat buffers.  ``zero_grad``
+    writes 0 back into ``g`` once consumed and ``zero_region`` (e.g. the
+    BatchNorm accumulators) is cleared by the same launch, so the next step's
+    atomic accumulations start from zero without a memset node."""
     if p.is_cuda:
         ops().fused_optimizer(spec.mode, p, g, m, v, anchor, p16, spec.learning_rate, spec.l1,
                               spec.l2, spec.momentum, spec.proximal_term, spec.beta1, spec.beta2,
-                              spec.epsilon, spec.weight_decay, lr_scale, step)
+                              spec.epsilon, spec.weight_decay, lr_scale, step, zero_grad,
+                              zero_region)
         return
     _reference_step(spec, p, g, m, v, anchor, p16, lr_scale, step)
+    if zero_grad:
+        g.zero_()
+    if zero_region is not None:
+        zero_region.zero_()
 
 
 @torch.no_grad()

@@ -53,16 +53,16 @@ def test_conv_forward_matches_fp32(case):
     y = torch.empty(N, shp.P, shp.Q, Co, dtype=torch.bfloat16, device=DEV)
     plan = K.conv_plan(0, shp, torch.device(DEV))
     ws = torch.empty(max(4, plan.workspace), device=DEV)
-    stats = torch.zeros(max(1, plan.stats_rows) * 2 * Co, device=DEV)
+    stats = torch.zeros(2 * Co, dtype=torch.float64, device=DEV)
     K.conv_forward(x, w, y, shp, ws, stats)
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=s,
                    padding=k // 2).permute(0, 2, 3, 1)
     assert rel_err(y, ref) < 1e-2
-    # fused BN partial statistics (sum and sum of squares of the bf16 output)
-    st = stats.view(-1, 2, Co).sum(0).cpu()
-    yf = y.float().reshape(-1, Co).cpu()
-    assert torch.allclose(st[0], yf.sum(0), rtol=1e-3, atol=1e-2)
-    assert torch.allclose(st[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+    # fused BN statistics (sum and sum of squares of the bf16 output, fp64 atomics)
+    st = stats.view(2, Co).cpu()
+    yf = y.double().reshape(-1, Co).cpu()
+    assert torch.allclose(st[0], yf.sum(0), rtol=1e-6, atol=1e-6)
+    assert torch.allclose(st[1], (yf * yf).sum(0), rtol=1e-6, atol=1e-6)
 
 
 @pytest.mark.parametrize("case", CONV_CASES[1:])
@@ -99,10 +99,8 @@ def test_conv_wgrad_matches_fp32(case):
     shp = K.ConvShape(N, H, W, C, Co, k, k, s, k // 2)
     x = bf(torch.randn(N, H, W, C, device=DEV))
     dy = bf(torch.randn(N, shp.P, shp.Q, Co, device=DEV))
-    plan = K.conv_plan(2, shp, torch.device(DEV))
-    ws = torch.empty(max(4, plan.workspace), device=DEV)
-    dw = torch.empty(Co, k, k, C, device=DEV)
-    K.conv_wgrad(x, dy, dw, shp, ws)
+    dw = torch.full((Co, k, k, C), float("nan"), device=DEV)  # accumulate=False must clear it
+    K.conv_wgrad(x, dy, dw, shp, accumulate=False)
     ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (Co, C, k, k),
                                       dy.float().permute(0, 3, 1, 2), stride=s,
                                       padding=k // 2).permute(0, 2, 3, 1)
@@ -134,14 +132,14 @@ def test_batchnorm_forward_backward(C):
     res = bf(torch.randn(M, C, device=DEV))
     gamma = torch.rand(C, device=DEV) + 0.5
     beta = torch.randn(C, device=DEV)
-    part = torch.zeros(512 * 2 * C, device=DEV)
+    acc = torch.zeros(2 * C, dtype=torch.float64, device=DEV)
     f32 = lambda: torch.zeros(C, device=DEV)
-    mean, invstd, scale, shift = f32(), f32(), f32(), f32()
+    mean, invstd = f32(), f32()
     rm, rv = f32(), torch.ones(C, device=DEV)
-    rows = K.bn_stats(x, C, part)
-    K.bn_finalize(part, rows, M, C, gamma, beta, mean, invstd, scale, shift, rm, rv, 0.1, 1e-5)
+    K.bn_stats(x, C, acc)
     y = torch.empty_like(x)
-    K.bn_apply(x, C, scale, shift, y, residual=res, relu=True)
+    K.bn_apply(x, C, acc, gamma, beta, mean, invstd, rm, rv, y, residual=res, relu=True,
+               train=True, momentum=0.1, eps=1e-5)
     xr = x.float().cpu().requires_grad_(True)
     g, b_ = gamma.cpu().requires_grad_(True), beta.cpu().requires_grad_(True)
     bn = F.batch_norm(xr, None, None, g, b_, training=True, eps=1e-5)
@@ -153,13 +151,30 @@ def test_batchnorm_forward_backward(C):
     dx = torch.empty_like(x)
     dres = torch.empty_like(x)
     dg, db = f32(), f32()
-    coef = torch.zeros(3 * C, device=DEV)
-    K.bn_backward(dy, x, y, C, gamma, mean, invstd, part, coef, dg, db, dx, dres)
+    acc_b = torch.zeros(2 * C, dtype=torch.float64, device=DEV)
+    K.bn_backward(dy, x, y, C, gamma, mean, invstd, acc_b, dg, db, dx, dres)
     assert rel_err(dx, xr.grad) < 2e-2
     assert rel_err(dg, g.grad) < 1e-2
     assert rel_err(db, b_.grad) < 1e-2
     mask = (y.float() > 0).float()
     assert rel_err(dres, dy.float() * mask) < 1e-2
+    # inference mode: running statistics, no accumulator
+    y2 = torch.empty_like(x)
+    K.bn_apply(x, C, None, gamma, beta, mean, invstd, rm, rv, y2, residual=None, relu=False,
+               train=False, momentum=0.1, eps=1e-5)
+    ref2 = F.batch_norm(x.float().cpu(), rm.cpu(), rv.cpu(), gamma.cpu(), beta.cpu(),
+                        training=False, eps=1e-5)
+    assert rel_err(y2, ref2) < 1e-2
+
+
+def test_optimizer_zeroes_grad_and_region():
+    from metisfl_amd.ops.optim import OptimizerSpec, fused_step
+    n = 1024
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    region = torch.randn(96, dtype=torch.float64, device=DEV)
+    fused_step(OptimizerSpec("vanilla_sgd", 0.1), p, g, zero_grad=True, zero_region=region)
+    assert int((g != 0).sum()) == 0 and int((region != 0).sum()) == 0
 
 
 def test_head_forward_backward():

@@ -32,6 +32,7 @@ def test_resnet_gradients_gpu_vs_cpu_reference():
     assert torch.equal(cpu.state.model32, gpu.state.model32.cpu())
     dc = cpu.make_dataset(x, y, shuffle=False)
     dg = gpu.make_dataset(x, y, shuffle=False)
+    cpu.zero_grad_in_optimizer = gpu.zero_grad_in_optimizer = False  # keep grads readable
     cpu._train_body(dc)
     gpu._train_body(dg)  # eager launch of the HIP kernels
     torch.cuda.synchronize()
