@@ -89,14 +89,20 @@ PYBIND11_MODULE(_engine, m) {
   });
 
   py::class_<Controller>(m, "Controller")
-      .def(py::init([](py::bytes params) { return new Controller(std::string(params)); }))
+      // the GIL is released around everything that may block on the model
+      // store (a Redis round trip) or aggregate large models
+      .def(py::init([](py::bytes params) {
+        std::string p(params);
+        py::gil_scoped_release nogil;
+        return new Controller(p);
+      }))
       .def("add_learner",
            [](Controller& c, py::bytes se, py::bytes ds) {
              Dispatch d;
              auto r = c.add_learner(std::string(se), std::string(ds), &d);
              return py::make_tuple(r.first, r.second, dispatch_to_py(d));
            })
-      .def("remove_learner", &Controller::remove_learner)
+      .def("remove_learner", &Controller::remove_learner, py::call_guard<py::gil_scoped_release>())
       .def("learner_ids", &Controller::learner_ids)
       .def("num_learners", &Controller::num_learners)
       .def("global_iteration", &Controller::global_iteration)
@@ -143,7 +149,12 @@ PYBIND11_MODULE(_engine, m) {
            [](Controller& c, int n, const std::vector<py::bytes>& ses) {
              std::vector<std::string> s;
              for (auto& b : ses) s.emplace_back(b);
-             return B(c.learner_local_model_lineage(n, s));
+             std::string out;
+             {
+               py::gil_scoped_release nogil;
+               out = c.learner_local_model_lineage(n, s);
+             }
+             return B(out);
            })
       .def("config", [](const Controller& c) {
         const auto& k = c.config();

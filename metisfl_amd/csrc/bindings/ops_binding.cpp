@@ -18,9 +18,11 @@ namespace {
 #define CHECK_T(t, dt) \
   TORCH_CHECK((t).scalar_type() == (dt), #t " has dtype ", (t).scalar_type(), ", expected ", dt)
 #define CHECK_IN(t, dt) \
-  CHECK_DEV(t);         \
-  CHECK_CONTIG(t);      \
-  CHECK_T(t, dt)
+  do {                  \
+    CHECK_DEV(t);       \
+    CHECK_CONTIG(t);    \
+    CHECK_T(t, dt);     \
+  } while (0)
 
 hipStream_t cur_stream(const torch::Tensor& t) {
   return c10::hip::getCurrentHIPStream(t.device().index()).stream();

@@ -313,7 +313,11 @@ Dispatch Controller::schedule_tasks_locked(const std::string& id, uint32_t task_
   if (to_schedule.empty()) return d;
   const uint32_t idx = task_iteration == 0 ? 0 : task_iteration - 1;
   if (!metadata_.empty() && idx < metadata_.size()) metadata_[idx].completed_at = now_ns();
-  const auto selected = select_scheduled_cardinality(to_schedule, active);
+  // FedRec folds ONE learner's (previous, latest) pair into its running state,
+  // so it aggregates the finisher only; the reference hands it every active
+  // learner and silently uses whichever comes first (federated_recency.cc:15).
+  const auto selected =
+      cfg_.rule == 3 ? to_schedule : select_scheduled_cardinality(to_schedule, active);
   FederatedModelT cm = compute_community_model_locked(selected, idx);
   record_quantifiers_locked(cm, idx);
   cm.global_iteration = task_iteration;
@@ -373,6 +377,11 @@ FederatedModelT Controller::compute_community_model_locked(const std::vector<std
   for (auto& id : ids) {
     auto it = learners_.find(id);
     if (it == learners_.end()) continue;
+    // A learner that has not committed a model yet (e.g. an async federation
+    // in its first rounds) cannot contribute: it is excluded before the
+    // scaling factors are normalised (the reference would aggregate an empty
+    // lineage here, controller.cc:885-903).
+    if (store_->lineage_length(id) == 0) continue;
     ScalerInput si;
     si.id = id;
     si.num_training_examples = it->second.num_train;

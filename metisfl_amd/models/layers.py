@@ -47,7 +47,32 @@ class Workspace:
 
     def allocate(self, device) -> None:
         self.split = torch.zeros(max(4, self.split_floats), dtype=torch.float32, device=device)
+        self.split2 = torch.zeros(max(4, self.split_floats), dtype=torch.float32, device=device)
         self.bn_acc = torch.zeros(max(2, self.acc_len), dtype=torch.float64, device=device)
+        # Side stream for work that is off the critical path (weight gradients,
+        # projection shortcuts).  Forked/joined with stream waits, so inside a
+        # captured hipGraph these become parallel branches that fill CUs the
+        # small CIFAR-sized kernels leave idle.
+        dev = torch.device(device)
+        self.side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+
+    # Measured on MI355X (round 1): forking wgrad / shortcuts onto a second
+    # stream inside the graph made the ResNet-18 step ~12% SLOWER (the branches
+    # contend for CUs and add cross-stream waits), so it is opt-in.
+    overlap = False
+
+    def fork(self):
+        """Context: run the enclosed launches on the side stream, ordered after
+        everything already issued on the current stream."""
+        import contextlib
+        if self.side is None or not self.overlap:
+            return contextlib.nullcontext()
+        self.side.wait_stream(torch.cuda.current_stream(self.side.device))
+        return torch.cuda.stream(self.side)
+
+    def join(self) -> None:
+        if self.side is not None and self.overlap:
+            torch.cuda.current_stream(self.side.device).wait_stream(self.side)
 
 
 class Layer:
@@ -77,9 +102,15 @@ class ConvBN(Layer):
         self.P, self.Q = self.shp.P, self.shp.Q
         self.M = N * self.P * self.Q
 
+    # layers that run on the side stream use the second split-K slab
+    alt_workspace = False
+
     @property
     def out_shape(self):
         return (self.shp.N, self.P, self.Q, self.shp.Co)
+
+    def _split(self):
+        return self.ws.split2 if self.alt_workspace else self.ws.split
 
     def specs(self):
         s, n = self.shp, self.name
@@ -125,7 +156,7 @@ class ConvBN(Layer):
     def forward(self, x: torch.Tensor, residual: torch.Tensor | None = None, train: bool = True):
         s = self.shp
         self.x = x
-        K.conv_forward(x, self.w16, self.z, s, self.ws.split, self.ws.acc(self.acc_f) if train else None)
+        K.conv_forward(x, self.w16, self.z, s, self._split(), self.ws.acc(self.acc_f) if train else None)
         K.bn_apply(self.z, s.Co, self.ws.acc(self.acc_f), self.gamma, self.beta, self.mean,
                    self.invstd, self.rmean, self.rvar, self.y, residual, self.relu, train,
                    self.momentum, self.eps)
@@ -139,10 +170,13 @@ class ConvBN(Layer):
         s = self.shp
         K.bn_backward(dy, self.z, self.y if self.relu else None, s.Co, self.gamma, self.mean,
                       self.invstd, self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz, dres)
+        # weight gradient: off the critical path -> side stream (joined before
+        # the optimizer); the gradient buffer is zero on entry (re-zeroed by
+        # the optimizer launch), so split-K slices accumulate atomically
+        with self.ws.fork():
+            K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True)
         if dx is not None:
-            K.conv_dgrad(self.dz, self.w16, dx, s, self.ws.split, accumulate)
-        # gradient buffer is zero on entry (re-zeroed by the optimizer launch)
-        K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True)
+            K.conv_dgrad(self.dz, self.w16, dx, s, self._split(), accumulate)
 
 
 class BasicBlock(Layer):
@@ -156,6 +190,7 @@ class BasicBlock(Layer):
         self.sc = None
         if stride != 1 or cin != cout:
             self.sc = ConvBN(f"{name}.shortcut", N, H, W, cin, cout, 1, stride, relu=False)
+            self.sc.alt_workspace = True
         self.out_shape = self.c2.out_shape
         self.in_shape = (N, H, W, cin)
 
@@ -178,8 +213,15 @@ class BasicBlock(Layer):
             l.prepare_backward()
 
     def forward(self, x, train=True):
+        if self.sc is None:
+            a = self.c1.forward(x, train=train)
+            return self.c2.forward(a, residual=x, train=train)
+        # projection shortcut runs concurrently with conv1 (side stream, own
+        # split-K workspace); conv2 consumes both after the join
+        with self.c1.ws.fork():
+            r = self.sc.forward(x, train=train)
         a = self.c1.forward(x, train=train)
-        r = self.sc.forward(x, train=train) if self.sc is not None else x
+        self.c1.ws.join()
         return self.c2.forward(a, residual=r, train=train)
 
     def backward(self, dout, dx):

@@ -120,6 +120,7 @@ class StaticNet:
         for l in self.all_layers():
             l.prepare_backward()
         self.backward(dlast)
+        self.ws.join()  # weight-gradient branch (side stream) must land first
         # one launch: optimizer + grad re-zero + BN accumulator re-zero
         st.optimizer_step(zero_grad=self.zero_grad_in_optimizer, zero_region=self.ws.bn_acc)
         opt_ops.tick(st.step, 1)

@@ -1,0 +1,240 @@
+"""The native controller state machine driven by fake learners (the
+reference's orchestration-test approach, test/learner_notrain_noeval.py):
+membership, sync / async / semi-sync scheduling, aggregation through the
+model store (in-memory and Redis), runtime metadata and lineage queries."""
+import numpy as np
+import pytest
+
+from metisfl_amd import _engine as E
+from metisfl_amd.proto import controller_pb2, learner_pb2, metis_pb2, model_pb2
+from metisfl_amd.utils.proto_messages_factory import MetisProtoMessages as M
+from metisfl_amd.utils.proto_messages_factory import ModelProtoMessages as MM
+from metisfl_amd.utils.tensor_codec import model_from_arrays, model_to_arrays
+
+from tests.fake_redis import FakeRedis
+
+
+def params(protocol="SYNCHRONOUS", rule="FedAvg", scaling="NumTrainingExamples", stride=0,
+           store="InMemory", eviction="LineageLengthEviction", lineage=1, redis_port=None,
+           batch=10, epochs=2, semi_lambda=2, recompute=False):
+    opt = MM.construct_optimizer_config_pb(MM.construct_vanilla_sgd_optimizer_pb(0.01))
+    p = M.construct_controller_params_pb(
+        M.construct_server_entity_pb("localhost", 50051),
+        M.construct_global_model_specs(M.construct_aggregation_rule_pb(rule, scaling, stride, None), 1.0),
+        M.construct_communication_specs_pb(protocol, semi_lambda, recompute),
+        M.construct_model_store_config_pb(store, eviction, lineage, "127.0.0.1", redis_port),
+        M.construct_controller_modelhyperparams_pb(batch, epochs, opt, 0.0))
+    return p.SerializeToString()
+
+
+def fed_model(vals, it=0):
+    return MM.construct_federated_model_pb(1, model_from_arrays(["w"], [np.asarray(vals, np.float32)]),
+                                           it).SerializeToString()
+
+
+def join(ctrl, port, ntrain):
+    se = M.construct_server_entity_pb("learner-host", port).SerializeToString()
+    ds = M.construct_dataset_spec_pb(ntrain, 0, 0).SerializeToString()
+    return ctrl.add_learner(se, ds)
+
+
+def completed(vals, gi, batches=5, ms_batch=2.0, ms_epoch=10.0):
+    meta = M.construct_task_execution_metadata_pb(gi, None, 1.0, batches, 10, ms_epoch, ms_batch)
+    task = M.construct_completed_learning_task_pb(
+        model_from_arrays(["w"], [np.asarray(vals, np.float32)]), meta, "")
+    return task.SerializeToString()
+
+
+def run_req(b):
+    r = learner_pb2.RunTaskRequest()
+    r.ParseFromString(b)
+    return r
+
+
+def test_join_dispatches_initial_task_and_validates():
+    c = E.Controller(params())
+    lid, tok, d = join(c, 1, 100)
+    assert lid == "learner-host:1" and len(tok) == 64
+    assert d["run_tasks"] == []  # no community model yet (controller.cc:394-397)
+    c.replace_community_model(fed_model([1, 2, 3]))
+    lid2, tok2, d2 = join(c, 2, 35)
+    (who, req), = d2["run_tasks"]
+    r = run_req(req)
+    assert who == lid2
+    assert r.task.global_iteration == 1
+    assert r.task.num_local_updates == 2 * 4  # epochs * ceil(35 / 10)
+    assert r.hyperparameters.batch_size == 10
+    assert r.hyperparameters.optimizer.WhichOneof("config") == "vanilla_sgd"
+    assert model_to_arrays(r.federated_model.model)[1][0].tolist() == [1, 2, 3]
+    with pytest.raises(E.EngineStatusError) as ei:
+        join(c, 2, 10)
+    assert ei.value.args[0] == 6  # ALREADY_EXISTS
+    with pytest.raises(E.EngineStatusError) as ei:
+        c.remove_learner(lid2, "bad-token")
+    assert ei.value.args[0] == 16  # UNAUTHENTICATED
+    with pytest.raises(E.EngineStatusError) as ei:
+        join(c, 3, 0)
+    assert ei.value.args[0] == 3  # INVALID_ARGUMENT
+    c.remove_learner(lid2, tok2)
+    assert c.learner_ids() == [lid]
+
+
+def _three_learners(c):
+    c.replace_community_model(fed_model([0, 0, 0]))
+    return [join(c, p, n)[:2] for p, n in ((1, 100), (2, 100), (3, 200))]
+
+
+def test_sync_round_fedavg_and_metadata():
+    c = E.Controller(params())
+    ls = _three_learners(c)
+    vals = {ls[0][0]: [1, 1, 1], ls[1][0]: [2, 2, 2], ls[2][0]: [4, 4, 4]}
+    d = None
+    for i, (lid, tok) in enumerate(ls):
+        d = c.learner_completed_task(lid, tok, completed(vals[lid], 1))
+        if i < 2:
+            assert d["run_tasks"] == [] and d["eval_tasks"] == []  # barrier not reached
+    assert len(d["run_tasks"]) == 3 and len(d["eval_tasks"]) == 3
+    r = run_req(d["run_tasks"][0][1])
+    assert r.task.global_iteration == 2
+    cm = model_to_arrays(r.federated_model.model)[1][0]
+    assert np.allclose(cm, 0.25 * 1 + 0.25 * 2 + 0.5 * 4)  # NUM_TRAINING_EXAMPLES weights
+    fm = model_pb2.FederatedModel()
+    fm.ParseFromString(c.community_model())
+    assert fm.num_contributors == 3 and fm.global_iteration == 1
+    # evaluation requests carry the community model and TRAIN/VALID/TEST
+    ev = learner_pb2.EvaluateModelRequest()
+    ev.ParseFromString(d["eval_tasks"][0][1])
+    assert list(ev.evaluation_dataset) == [0, 2, 1] and ev.batch_size == 10
+    lid, _, ce_idx, md_idx = d["eval_tasks"][0][0], None, d["eval_tasks"][0][2], d["eval_tasks"][0][3]
+    evals = M.construct_model_evaluations_pb(M.construct_model_evaluation_pb({"accuracy": 0.5}), None, None)
+    c.record_evaluation(lid, ce_idx, md_idx, evals.SerializeToString())
+    # runtime metadata lineage (the benchmark record)
+    resp = controller_pb2.GetRuntimeMetadataLineageResponse()
+    resp.ParseFromString(c.runtime_metadata_lineage(0))
+    assert [m.global_iteration for m in resp.metadata] == [1, 2]
+    m1 = resp.metadata[0]
+    assert sorted(m1.completed_by_learner_id) == sorted(l for l, _ in ls)
+    assert m1.completed_at.ToNanoseconds() >= m1.started_at.ToNanoseconds() > 0
+    assert m1.model_aggregation_total_duration_ms >= 0
+    assert list(m1.model_aggregation_block_size) == [3]
+    assert len(m1.model_tensor_quantifiers) == 1 and m1.model_tensor_quantifiers[0].tensor_size_bytes == 12
+    assert set(m1.eval_task_received_at) == {lid}
+    assert set(m1.model_insertion_duration_ms) == {l for l, _ in ls}
+    ce = controller_pb2.GetCommunityModelEvaluationLineageResponse()
+    ce.ParseFromString(c.community_evaluation_lineage(-1))
+    assert ce.community_evaluation[0].evaluations[lid].training_evaluation.metric_values["accuracy"] == "0.5"
+    lt = controller_pb2.GetLocalTaskLineageResponse()
+    lt.ParseFromString(c.local_task_lineage(1, [ls[0][0]]))
+    assert lt.learner_task[ls[0][0]].task_metadata[0].completed_batches == 5
+    pl = controller_pb2.GetParticipatingLearnersResponse()
+    pl.ParseFromString(c.participating_learners())
+    assert {l.id for l in pl.learner} == {l for l, _ in ls}
+    assert all(l.auth_token == "" for l in pl.learner)
+    cml = controller_pb2.GetCommunityModelLineageResponse()
+    cml.ParseFromString(c.community_model_lineage(1))
+    assert len(cml.federated_models) == 1 and cml.federated_models[0].global_iteration == 1
+    llm = controller_pb2.GetLearnerLocalModelLineageResponse()
+    llm.ParseFromString(c.learner_local_model_lineage(
+        0, [M.construct_server_entity_pb("learner-host", 3).SerializeToString()]))
+    assert model_to_arrays(llm.learner_local_model[0].model[0])[1][0].tolist() == [4, 4, 4]
+
+
+def test_async_protocol_redispatches_finisher_only():
+    c = E.Controller(params(protocol="ASYNCHRONOUS", scaling="NumParticipants"))
+    ls = _three_learners(c)
+    d = c.learner_completed_task(ls[0][0], ls[0][1], completed([3, 3, 3], 1))
+    assert [x[0] for x in d["run_tasks"]] == [ls[0][0]]
+    # selector falls back to all active learners; only one has a model so far
+    r = run_req(d["run_tasks"][0][1])
+    assert r.task.global_iteration == 2
+    d = c.learner_completed_task(ls[1][0], ls[1][1], completed([6, 6, 6], 1))
+    assert [x[0] for x in d["run_tasks"]] == [ls[1][0]]
+    cm = model_to_arrays(run_req(d["run_tasks"][0][1]).federated_model.model)[1][0]
+    assert np.allclose(cm, 0.5 * 3 + 0.5 * 6)
+    assert c.global_iteration() == 3
+
+
+def test_async_fedrec_recency():
+    c = E.Controller(params(protocol="ASYNCHRONOUS", rule="FedRec", scaling="NumParticipants", lineage=2))
+    ls = _three_learners(c)
+    out = []
+    for (lid, tok), v in zip(ls[:2], ([2, 2, 2], [4, 4, 4])):
+        d = c.learner_completed_task(lid, tok, completed(v, 1))
+        out.append(model_to_arrays(run_req(d["run_tasks"][0][1]).federated_model.model)[1][0])
+    assert np.allclose(out[0], 2)     # first committer initialises
+    assert np.allclose(out[1], 3)     # (1/3*2 + 1/3*4) / (2/3)
+
+
+def test_semi_sync_recomputes_budgets_after_round_one():
+    c = E.Controller(params(protocol="SEMI_SYNCHRONOUS", semi_lambda=2))
+    ls = _three_learners(c)
+    speeds = {ls[0][0]: 1.0, ls[1][0]: 2.0, ls[2][0]: 4.0}   # ms per batch
+    d = None
+    for lid, tok in ls:
+        d = c.learner_completed_task(lid, tok, completed([1, 1, 1], 1, ms_batch=speeds[lid],
+                                                         ms_epoch=speeds[lid] * 10))
+    budgets = {w: run_req(r).task.num_local_updates for w, r in d["run_tasks"]}
+    # t_max = lambda * slowest epoch = 2 * 40 = 80 ms -> ceil(80 / ms_per_batch)
+    assert budgets == {ls[0][0]: 80, ls[1][0]: 40, ls[2][0]: 20}
+
+
+def test_fedstride_blocks_recorded():
+    c = E.Controller(params(rule="FedStride", stride=2, scaling="NumParticipants"))
+    ls = _three_learners(c)
+    d = None
+    for (lid, tok), v in zip(ls, ([3, 3, 3], [6, 6, 6], [9, 9, 9])):
+        d = c.learner_completed_task(lid, tok, completed(v, 1))
+    cm = model_to_arrays(run_req(d["run_tasks"][0][1]).federated_model.model)[1][0]
+    assert np.allclose(cm, 6.0)
+    resp = controller_pb2.GetRuntimeMetadataLineageResponse()
+    resp.ParseFromString(c.runtime_metadata_lineage(1))
+    assert list(resp.metadata[0].model_aggregation_block_size) == [2, 1]
+
+
+def test_learner_leaving_does_not_stall_sync_barrier():
+    c = E.Controller(params())
+    ls = _three_learners(c)
+    c.learner_completed_task(ls[0][0], ls[0][1], completed([1, 1, 1], 1))
+    c.learner_completed_task(ls[1][0], ls[1][1], completed([1, 1, 1], 1))
+    c.remove_learner(ls[2][0], ls[2][1])
+    d = c.learner_completed_task(ls[0][0], ls[0][1], completed([1, 1, 1], 1))
+    assert len(d["run_tasks"]) == 2
+
+
+def test_redis_model_store_roundtrip():
+    srv = FakeRedis()
+    try:
+        c = E.Controller(params(store="Redis", redis_port=srv.port, lineage=2))
+        ls = _three_learners(c)
+        d = None
+        for (lid, tok), v in zip(ls, ([1, 1, 1], [2, 2, 2], [4, 4, 4])):
+            d = c.learner_completed_task(lid, tok, completed(v, 1))
+        cm = model_to_arrays(run_req(d["run_tasks"][0][1]).federated_model.model)[1][0]
+        assert np.allclose(cm, 2.75)
+        assert set(k.decode().rsplit("_", 1)[0] for k in srv.store) == {l for l, _ in ls}
+        assert "RPUSH" in srv.commands and "LRANGE" in srv.commands
+        # eviction at lineage 2: three more commits of learner 1 keep 2 keys
+        for _ in range(3):
+            c.learner_completed_task(ls[0][0], ls[0][1], completed([5, 5, 5], 2))
+        assert sum(1 for k in srv.store if k.decode().startswith(ls[0][0] + "_")) == 2
+    finally:
+        srv.close()
+
+
+def test_redis_unreachable_raises_instead_of_exit():
+    with pytest.raises(Exception):
+        E.Controller(params(store="Redis", redis_port=1))
+
+
+def test_collective_round_recording():
+    c = E.Controller(params())
+    meta = M.construct_task_execution_metadata_pb(1, None, 1.0, 100, 32, 50.0, 0.5).SerializeToString()
+    c.record_collective_round(1, ["r0", "r1"], 1_000_000_000, 2_000_000_000, 2_000_000_000,
+                              2_001_000_000, [meta, meta], [0, 2], [40, 8], [10, 2])
+    resp = controller_pb2.GetRuntimeMetadataLineageResponse()
+    resp.ParseFromString(c.runtime_metadata_lineage(0))
+    m = resp.metadata[0]
+    assert (m.completed_at.ToNanoseconds() - m.started_at.ToNanoseconds()) == 1_000_000_000
+    assert m.model_aggregation_total_duration_ms == pytest.approx(1.0)
+    assert m.model_tensor_quantifiers[1].tensor_zeros == 2 and m.model_tensor_quantifiers[1].tensor_non_zeros == 0
+    assert c.scaling_factors(["r0", "r1"], [100, 300], [1, 1]) == pytest.approx({"r0": 0.25, "r1": 0.75})
