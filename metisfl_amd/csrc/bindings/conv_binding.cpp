@@ -59,6 +59,20 @@ mfl::ConvGeom dgrad_geom(int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co,
   return g;
 }
 
+// The counter block has ONE fixed size for every plan: a workspace is shared
+// by all layers of a model, and a per-plan size would let one layer's slabs
+// overlap (and poison) another layer's counters.  Split plans have < 256
+// tiles (plan_conv_gemm only splits while tiles * splits < 256).
+constexpr int64_t kCounterWords = 1024;
+int64_t counter_words(const mfl::ConvGeom& g, const mfl::ConvPlan& p) {
+  TORCH_CHECK(mfl::conv_counter_slots(g, p) <= kCounterWords, "split-K plan has too many tiles");
+  return kCounterWords;
+}
+int64_t workspace_floats(const mfl::ConvGeom& g, const mfl::ConvPlan& p) {
+  if (p.splits <= 1) return 0;
+  return counter_words(g, p) + (int64_t)p.splits * mfl::conv_counter_slots(g, p) * p.bm * p.bn;
+}
+
 std::vector<int64_t> plan_vec(const mfl::ConvPlan& p, int64_t ws_floats, int64_t stats_rows) {
   return {p.bm, p.bn, p.splits, p.kchunk, stats_rows, ws_floats};
 }
@@ -75,8 +89,7 @@ std::vector<int64_t> conv_plan(int64_t mode, int64_t N, int64_t H, int64_t W, in
   mfl::ConvGeom g = mode == 0 ? fwd_geom(N, H, W, C, Co, R, S, stride, pad)
                               : dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
   auto p = mfl::plan_conv_gemm(g);
-  const int64_t ws = p.splits > 1 ? (int64_t)p.splits * g.M * g.Ng : 0;
-  return plan_vec(p, ws, 1);
+  return plan_vec(p, workspace_floats(g, p), 1);
 }
 
 void run_gemm(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const torch::Tensor& w,
@@ -84,10 +97,15 @@ void run_gemm(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, cons
               const c10::optional<torch::Tensor>& stats, bool accum) {
   auto p = mfl::plan_conv_gemm(g);
   float* wsp = nullptr;
+  int* counters = nullptr;
   if (p.splits > 1) {
+    // layout: [arrival counters, padded to 64 words][fp32 slabs]; the
+    // counters must be zero when first used (allocate with torch.zeros) and
+    // are re-armed by the reducing workgroup, so the buffer is reusable.
     TORCH_CHECK(ws.has_value() && ws->defined(), "split-K workspace required");
-    check_f32(*ws, (int64_t)p.splits * g.M * g.Ng, "workspace");
-    wsp = ws->data_ptr<float>();
+    check_f32(*ws, workspace_floats(g, p), "workspace");
+    counters = reinterpret_cast<int*>(ws->data_ptr<float>());
+    wsp = ws->data_ptr<float>() + counter_words(g, p);
   }
   double* st = nullptr;
   if (stats.has_value() && stats->defined()) {
@@ -96,7 +114,8 @@ void run_gemm(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, cons
                 "stats must be a contiguous fp64 device tensor of >= 2*Cout elements");
     st = stats->data_ptr<double>();
   }
-  mfl::launch_conv_gemm(g, dgrad, p, bf(src), bf(w), bf(y), wsp, st, accum, cur_stream(y));
+  mfl::launch_conv_gemm(g, dgrad, p, bf(src), bf(w), bf(y), wsp, counters, st, accum,
+                        cur_stream(y));
 }
 
 void conv_forward(torch::Tensor x, torch::Tensor w, torch::Tensor y,

@@ -24,18 +24,36 @@ struct ConvPlan {
   int bm = 64, bn = 64;
   int splits = 1;
   int kchunk = 0;      // reduction elements per split (multiple of 64)
-  int stats_rows = 0;  // BN partial rows written by the epilogue (0 = by split reduce)
+  int stats_rows = 0;  // 1 = the epilogue accumulates BN statistics
+};
+
+// Kernel argument block.  *_shift = log2 of the divisor when it is a power of
+// two (wave-uniform shift instead of an integer division), else -1.
+struct ConvArgs {
+  ConvGeom g;
+  const uint16_t* src;
+  const uint16_t* wgt;
+  uint16_t* y;
+  float* ysplit;   // split-K slabs [splits][tiles][BM*BN]
+  int* counters;   // split-K arrival tickets [tiles], zero between launches
+  double* stats;
+  int kchunk;
+  int accum;
+  int c_shift, q_shift, pq_shift;
 };
 
 ConvPlan plan_conv_gemm(const ConvGeom& g);
 ConvPlan plan_conv_wgrad(const ConvGeom& g);
-int splitk_stats_blocks(int M, int C);
+// number of output tiles (= split-K counter slots) of a gemm plan
+int conv_counter_slots(const ConvGeom& g, const ConvPlan& p);
 
 // y (bf16 [M][Ng]) and, when stats != nullptr, fp64 atomic accumulation of the
-// per-channel BatchNorm sums into stats[0..Ng) / stats[Ng..2Ng).
+// per-channel BatchNorm sums into stats[0..Ng) / stats[Ng..2Ng).  With
+// p.splits > 1, ysplit holds splits*slots*bm*bn floats and counters `slots`
+// zero-initialised ints (the kernel re-arms them).
 void launch_conv_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const uint16_t* src,
-                      const uint16_t* wgt, uint16_t* y, float* ysplit, double* stats, bool accum,
-                      hipStream_t s);
+                      const uint16_t* wgt, uint16_t* y, float* ysplit, int* counters,
+                      double* stats, bool accum, hipStream_t s);
 // dw (fp32 [Cout][R][S][Cin]); must be zeroed first when p.splits > 1.
 void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, const uint16_t* dy,
                        float* dw, hipStream_t s);

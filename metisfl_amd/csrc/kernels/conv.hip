@@ -16,17 +16,26 @@
 //    transposing ds_read_b64_tr_b16, so no weight transpose pass exists.
 //  * wgrad reduces over the N*P*Q pixels, which are strided in both operands:
 //    tiles are staged [m][col] in LDS and the MFMA fragments are formed with
-//    the gfx950 transposing LDS read ds_read_b64_tr_b16 (guide T10).
+//    ds_read_b64_tr_b16 (guide T10).
+//  * Index math is kept off the VALU critical path: kernel size and stride are
+//    template parameters (constant divisions), channel / spatial divisions by
+//    powers of two become shifts (host-computed, wave-uniform).  Round-1
+//    profiling showed the generic version spending more VALU cycles on
+//    integer division than the MFMAs took.
 //  * Tiles: 256-thread workgroups (4 waves, 2x2), BK = 64, LDS rows padded to
 //    144 B so that a 16-lane ds_read_b128 group touches 16 distinct 4-bank
 //    slots (conflict-free, guide Guideline 4), register-staged double
 //    buffering with one barrier per k-step (guide T14 / "minimum 2-phase").
-//  * Small-M layers (CIFAR 4x4/8x8 stages) use split-K so a launch still
-//    fills >= 256 CUs; the split reduction kernel also emits the per-channel
-//    BatchNorm sums, and the non-split epilogue emits them directly (fp64
-//    atomics into a [2][C] accumulator), so BN never re-reads the conv output
-//    for statistics.  wgrad split-K slices accumulate with fp32 atomics into
-//    the (pre-zeroed) flat gradient buffer: no reduction launch.
+//  * Epilogue through LDS: the fp32 tile is staged in LDS and written as 16-B
+//    bf16 vectors; the per-channel BatchNorm sums of the bf16 output are
+//    reduced in the same pass and added with fp64 atomics into a [2][C]
+//    accumulator (no separate statistics pass).
+//  * Small-M layers (CIFAR 4x4 / 8x8 stages) use split-K to fill >= 256 CUs.
+//    The reduction happens IN the kernel: every slice stores its fp32 tile
+//    slab, then the last-arriving slice (agent-scope release/acquire counter,
+//    guide "In-launch split-K reduction") sums the slabs and runs the
+//    epilogue -- no reduction launch.  wgrad split-K slices accumulate with
+//    fp32 atomics into the pre-zeroed gradient buffer.
 #include "kernels/common.h"
 #include "kernels/conv.h"
 
@@ -40,24 +49,81 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+__device__ __forceinline__ int sdiv(int x, int d, int shift) { return shift >= 0 ? x >> shift : x / d; }
+
+// Vectorised epilogue shared by the direct and the split-K paths:
+// out[row][col] = bf16(v (+ y_old)), BN sums of the rounded output.
+// `get(row_local, col_local_base, float[8])` supplies 8 consecutive fp32 values.
+template <int BM, int BN, typename Getter>
+__device__ __forceinline__ void tile_epilogue(const ConvGeom& g, int m0, int n0, uint16_t* y,
+                                              double* stats, int accum, float* red, Getter get) {
+  constexpr int CPR = BN / 8;        // 16-B column groups per row
+  constexpr int RPP = 256 / CPR;     // rows per pass
+  const int t = threadIdx.x;
+  const int cg = t % CPR, r0 = t / CPR;
+  float s[8] = {0}, q[8] = {0};
+  const int col = n0 + cg * 8;
+  const bool col_ok = col < g.Ng;  // Ng % 8 == 0
+  for (int rl = r0; rl < BM; rl += RPP) {
+    const int row = m0 + rl;
+    if (row >= g.M || !col_ok) continue;
+    float v[8];
+    get(rl, cg * 8, v);
+    uint16_t* dst = y + (int64_t)row * g.Ng + col;
+    if (accum) {
+      float o[8];
+      unpack8(*reinterpret_cast<const uint4*>(dst), o);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += o[k];
+    }
+    const uint4 packed = pack8(v);
+    *reinterpret_cast<uint4*>(dst) = packed;
+    if (stats) {
+      float f[8];
+      unpack8(packed, f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += f[k];
+        q[k] += f[k] * f[k];
+      }
+    }
+  }
+  if (!stats) return;
+  __syncthreads();  // `red` aliases LDS that `get` may have been reading
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[t * 16 + k] = s[k];
+    red[t * 16 + 8 + k] = q[k];
+  }
+  __syncthreads();
+  if (t < BN) {
+    const int cgi = t >> 3, k = t & 7;
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < RPP; ++r) {
+      a += red[(r * CPR + cgi) * 16 + k];
+      b += red[(r * CPR + cgi) * 16 + 8 + k];
+    }
+    const int c = n0 + t;
+    if (c < g.Ng) {
+      atomicAdd(&stats[c], (double)a);
+      atomicAdd(&stats[g.Ng + c], (double)b);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Forward / dgrad implicit GEMM:  Y[m][n] = sum_k A[m][k] * B[n][k]
-template <int BM, int BN, bool DGRAD>
-__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16_t* __restrict__ src,
-                                                        const uint16_t* __restrict__ wgt,
-                                                        uint16_t* __restrict__ y,
-                                                        float* __restrict__ ysplit,
-                                                        double* __restrict__ stats, int kchunk,
-                                                        int accum) {
+template <int BM, int BN, bool DGRAD, int KS, int ST>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   constexpr int ACH = BM / 32;  // A 16-B chunks per thread per k-step
   constexpr int BCH = BN / 32;
   constexpr int TM = BM / 32;   // 16x16 MFMA tiles per wave along M
   constexpr int TN = BN / 32;
+  const ConvGeom& g = a.g;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   // buffer b: A tile at smem + b*STAGE, B tile right after it.  Forward: B is
-  // [BN][BK] (k-contiguous weight rows).  dgrad: B is staged [BK][BN] straight
-  // from the KRSC weight (c-contiguous) and read with ds_read_b64_tr_b16, so no
-  // per-step weight transpose is needed.
+  // [BN][BK] (k-contiguous weight rows).  dgrad: B is [BK][BN] staged from the
+  // KRSC weight (c-contiguous) and read with ds_read_b64_tr_b16.
   constexpr int BST = BN + kPad;
   constexpr int BTILE = DGRAD ? kBK * BST : BN * kLdsStride;
   constexpr int STAGE = BM * kLdsStride + BTILE;
@@ -65,7 +131,6 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
   auto Bs = [&](int b) { return smem + b * STAGE + BM * kLdsStride; };
   constexpr int BCPR = BN / 8;       // dgrad B: 16-B chunks per k-row
   constexpr int BRPP = 256 / BCPR;   // k-rows per pass
-  const int dbch = threadIdx.x % BCPR, dbrow = threadIdx.x / BCPR;
 
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -73,9 +138,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
   const int wm = wv >> 1, wn = wv & 1;
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
-  const int kbeg = blockIdx.z * kchunk;
-  const int kend = min(g.K, kbeg + kchunk);
+  const int kbeg = blockIdx.z * a.kchunk;
+  const int kend = min(g.K, kbeg + a.kchunk);
   const int nk = (kend - kbeg + kBK - 1) / kBK;
+  const int dbch = t % BCPR, dbrow = t / BCPR;
 
   const int lrow = t >> 3;   // 0..31
   const int lch = t & 7;     // chunk within the BK=64 row
@@ -87,18 +153,17 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
   for (int i = 0; i < ACH; ++i) {
     const int m = m0 + lrow + 32 * i;
     if (m < g.M) {
-      const int pq = g.P * g.Q;
-      const int n = m / pq;
-      const int rem = m - n * pq;
-      const int oy = rem / g.Q;
+      const int n = sdiv(m, g.P * g.Q, a.pq_shift);
+      const int rem = m - n * g.P * g.Q;
+      const int oy = sdiv(rem, g.Q, a.q_shift);
       const int ox = rem - oy * g.Q;
       a_nb[i] = n * HWC;
       if (DGRAD) {
         a_y0[i] = oy + g.pad;
         a_x0[i] = ox + g.pad;
       } else {
-        a_y0[i] = oy * g.stride - g.pad;
-        a_x0[i] = ox * g.stride - g.pad;
+        a_y0[i] = oy * ST - g.pad;
+        a_x0[i] = ox * ST - g.pad;
       }
     } else {
       a_nb[i] = 0;
@@ -113,10 +178,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
     const bool kv = k < kend;
     int r = 0, s = 0, c = 0;
     if (kv) {
-      const int rs = k / g.C;
+      const int rs = sdiv(k, g.C, a.c_shift);
       c = k - rs * g.C;
-      r = rs / g.S;
-      s = rs - r * g.S;
+      r = rs / KS;
+      s = rs - r * KS;
     }
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
@@ -125,9 +190,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
       if (DGRAD) {
         const int ty = a_y0[i] - r, tx = a_x0[i] - s;
         ok = ok && ty >= 0 && tx >= 0;
-        if (g.stride > 1) ok = ok && (ty % g.stride == 0) && (tx % g.stride == 0);
-        iy = ty / g.stride;
-        ix = tx / g.stride;
+        if (ST > 1) ok = ok && (ty % ST == 0) && (tx % ST == 0);
+        iy = ty / ST;
+        ix = tx / ST;
       } else {
         iy = a_y0[i] + r;
         ix = a_x0[i] + s;
@@ -135,7 +200,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
       }
       ok = ok && iy < g.H && ix < g.W;
       if (ok)
-        ra[i] = *reinterpret_cast<const uint4*>(src + a_nb[i] + (iy * g.W + ix) * g.C + c);
+        ra[i] = *reinterpret_cast<const uint4*>(a.src + a_nb[i] + (iy * g.W + ix) * g.C + c);
       else
         ra[i] = make_uint4(0, 0, 0, 0);
     }
@@ -146,9 +211,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
         const int kr = kbeg + kt * kBK + dbrow + BRPP * i;
         const int n = n0 + dbch * 8;
         if (kr < kend && n < g.Ng) {
-          const int rs = kr / g.C;
+          const int rs = sdiv(kr, g.C, a.c_shift);
           const int ko = kr - rs * g.C;
-          rb[i] = *reinterpret_cast<const uint4*>(wgt + ((int64_t)ko * g.R * g.S + rs) * g.Ng + n);
+          rb[i] = *reinterpret_cast<const uint4*>(a.wgt + ((int64_t)ko * KS * KS + rs) * g.Ng + n);
         } else {
           rb[i] = make_uint4(0, 0, 0, 0);
         }
@@ -158,7 +223,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
       for (int i = 0; i < BCH; ++i) {
         const int n = n0 + lrow + 32 * i;
         if (kv && n < g.Ng)
-          rb[i] = *reinterpret_cast<const uint4*>(wgt + (int64_t)n * g.K + k);
+          rb[i] = *reinterpret_cast<const uint4*>(a.wgt + (int64_t)n * g.K + k);
         else
           rb[i] = make_uint4(0, 0, 0, 0);
       }
@@ -233,140 +298,85 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvGeom g, const uint16
   }
 
   // ---- epilogue -----------------------------------------------------------
-  const int rbase = m0 + wm * (BM / 2) + (lane >> 4) * 4;
-  const int cbase = n0 + wn * (BN / 2) + fr;
-  if (ysplit) {
-    float* out = ysplit + (int64_t)blockIdx.z * g.M * g.Ng;
+  // fp32 tile in LDS: [BM][BN + 4] (the loop's final barrier freed smem)
+  constexpr int TST = BN + 4;
+  float* tile = reinterpret_cast<float*>(smem);
+  const int rl0 = wm * (BM / 2) + (lane >> 4) * 4;
+  const int cl0 = wn * (BN / 2) + fr;
+  const int splits = gridDim.z;
+  const int tile_id = blockIdx.y * gridDim.x + blockIdx.x;
+  if (splits == 1) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = rbase + 16 * i + e, col = cbase + 16 * j;
-          if (row < g.M && col < g.Ng) out[(int64_t)row * g.Ng + col] = acc[i][j][e];
-        }
+        for (int e = 0; e < 4; ++e) tile[(rl0 + 16 * i + e) * TST + cl0 + 16 * j] = acc[i][j][e];
+    __syncthreads();
+    tile_epilogue<BM, BN>(g, m0, n0, a.y, a.stats, a.accum, tile + BM * TST,
+                          [&](int rl, int cl, float* v) {
+                            const float4 p = *reinterpret_cast<const float4*>(tile + rl * TST + cl);
+                            const float4 q = *reinterpret_cast<const float4*>(tile + rl * TST + cl + 4);
+                            v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w;
+                            v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
+                          });
     return;
   }
-  float cs[TN], cq[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) { cs[j] = 0.f; cq[j] = 0.f; }
+  // split-K: store this slice's slab [BM][BN] (tile-local, row-major)
+  const int ntiles = gridDim.x * gridDim.y;
+  float* slab = a.ysplit + ((int64_t)blockIdx.z * ntiles + tile_id) * (BM * BN);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = rbase + 16 * i + e, col = cbase + 16 * j;
-        if (row < g.M && col < g.Ng) {
-          float a = acc[i][j][e];
-          if (accum) a += bf2f(y[(int64_t)row * g.Ng + col]);
-          const uint16_t h = f2bf(a);
-          y[(int64_t)row * g.Ng + col] = h;
-          const float v = bf2f(h);
-          cs[j] += v;
-          cq[j] += v * v;
-        }
-      }
-  if (!stats) return;
-  // lanes l, l^16, l^32, l^48 share a column
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    cs[j] += __shfl_xor(cs[j], 16, 64);
-    cs[j] += __shfl_xor(cs[j], 32, 64);
-    cq[j] += __shfl_xor(cq[j], 16, 64);
-    cq[j] += __shfl_xor(cq[j], 32, 64);
-  }
-  float* red = reinterpret_cast<float*>(smem);  // [2 wm][2][BN]
-  if (lane < 16) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int cl = wn * (BN / 2) + 16 * j + lane;
-      red[(wm * 2 + 0) * BN + cl] = cs[j];
-      red[(wm * 2 + 1) * BN + cl] = cq[j];
+      for (int e = 0; e < 4; ++e) slab[(rl0 + 16 * i + e) * BN + cl0 + 16 * j] = acc[i][j][e];
+  // publish: every wave drains its stores, one agent-scope release, then the
+  // ticket; the last slice to arrive reduces (guide: In-launch split-K).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(&a.counters[tile_id], 1, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == splits - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // re-arm for the next launch (graph replay): nobody else touches it now
+      __hip_atomic_store(&a.counters[tile_id], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    flag[0] = last;
   }
   __syncthreads();
-  for (int cl = t; cl < BN; cl += 256) {
-    const int col = n0 + cl;
-    if (col < g.Ng) {
-      atomicAdd(&stats[col], (double)(red[0 * BN + cl] + red[2 * BN + cl]));
-      atomicAdd(&stats[g.Ng + col], (double)(red[1 * BN + cl] + red[3 * BN + cl]));
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Split-K reduction: y = bf16(sum_z ysplit[z]) and per-block BN partials.
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ysplit,
-                                                            int splits, int M, int C,
-                                                            uint16_t* __restrict__ y,
-                                                            double* __restrict__ stats, int accum) {
-  const int tpr = C / 8;
-  const int rpp = 256 / tpr;
-  const int t = threadIdx.x;
-  const int cg = t % tpr;
-  const int r0 = t / tpr;
-  float s[8] = {0}, q[8] = {0};
-  const int64_t MC = (int64_t)M * C;
-  if (r0 < rpp) {
-    for (int64_t row = (int64_t)blockIdx.x * rpp + r0; row < M; row += (int64_t)gridDim.x * rpp) {
-      float v[8] = {0};
-      const int64_t off = row * C + cg * 8;
-      for (int z = 0; z < splits; ++z) {
-        const float4 a = *reinterpret_cast<const float4*>(ysplit + z * MC + off);
-        const float4 b = *reinterpret_cast<const float4*>(ysplit + z * MC + off + 4);
-        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
-        v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
-      }
-      if (accum) {
-        float old[8];
-        unpack8(*reinterpret_cast<const uint4*>(y + off), old);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] += old[k];
-      }
-      const uint4 o = pack8(v);
-      *reinterpret_cast<uint4*>(y + off) = o;
-      float f[8];
-      unpack8(o, f);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        s[k] += f[k];
-        q[k] += f[k] * f[k];
-      }
-    }
-  }
-  if (!stats) return;
-  __shared__ float sh[2][256 * 8];
-  const bool act = r0 < rpp;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    sh[0][t * 8 + k] = act ? s[k] : 0.f;
-    sh[1][t * 8 + k] = act ? q[k] : 0.f;
-  }
-  __syncthreads();
-  for (int c = t; c < C; c += 256) {
-    float s0 = 0.f, s1 = 0.f;
-    for (int r = 0; r < rpp; ++r) {
-      s0 += sh[0][(r * tpr + (c >> 3)) * 8 + (c & 7)];
-      s1 += sh[1][(r * tpr + (c >> 3)) * 8 + (c & 7)];
-    }
-    atomicAdd(&stats[c], (double)s0);
-    atomicAdd(&stats[C + c], (double)s1);
-  }
+  if (!flag[0]) return;
+  const float* base = a.ysplit + (int64_t)tile_id * (BM * BN);
+  const int64_t zstride = (int64_t)ntiles * BM * BN;
+  tile_epilogue<BM, BN>(g, m0, n0, a.y, a.stats, a.accum, reinterpret_cast<float*>(smem) + 4,
+                        [&](int rl, int cl, float* v) {
+                          for (int k = 0; k < 8; ++k) v[k] = 0.f;
+                          for (int z = 0; z < splits; ++z) {
+                            const float* p = base + z * zstride + rl * BN + cl;
+                            const float4 x0 = *reinterpret_cast<const float4*>(p);
+                            const float4 x1 = *reinterpret_cast<const float4*>(p + 4);
+                            v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
+                            v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
+                          }
+                        });
 }
 
 // ---------------------------------------------------------------------------
 // wgrad:  dW[ko][j] = sum_m dY[m][ko] * im2col(X)[m][j],  j = (r, s, c)
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvGeom g, const uint16_t* __restrict__ x,
-                                                         const uint16_t* __restrict__ dy,
-                                                         float* __restrict__ dw, int mchunk) {
+template <int BM, int BN, int KS, int ST>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __restrict__ dw) {
   // g: H,W,C = X dims; P,Q = dY spatial; Ng = Cout; K = R*S*C; M = N*P*Q
   constexpr int TM = BM / 32;
   constexpr int TN = BN / 32;
   constexpr int AST = BM + kPad;
   constexpr int BST = BN + kPad;
+  const ConvGeom& g = a.g;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int STAGE = kBK * (AST + BST);
   auto As = [&](int b) { return smem + b * STAGE; };
@@ -378,16 +388,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvGeom g, const uint1
   const int wm = wv >> 1, wn = wv & 1;
   const int ko0 = blockIdx.x * BM;
   const int j0 = blockIdx.y * BN;
-  const int mbeg = blockIdx.z * mchunk;
-  const int mend = min(g.M, mbeg + mchunk);
+  const int mbeg = blockIdx.z * a.kchunk;
+  const int mend = min(g.M, mbeg + a.kchunk);
   const int nk = (mend - mbeg + kBK - 1) / kBK;
 
-  // Load mapping: a [64 m][BN] tile has BN/8 16-B chunks per row, so each
-  // thread owns one fixed column chunk and rows brow + BRPP*i; the im2col
-  // decomposition (r, s, c) of that column chunk is fixed for the k-loop.
+  // A [64 m][BM] and B [64 m][BN] tiles: each thread owns one fixed 16-B
+  // column chunk and rows row + RPP*i; the im2col decomposition (r, s, c) of
+  // the B column chunk is fixed for the whole k-loop.
   constexpr int BCPR = BN / 8;
   constexpr int BRPP = 256 / BCPR;
-  constexpr int BREP = kBK / BRPP;  // row repetitions
+  constexpr int BREP = kBK / BRPP;
   constexpr int ACPR = BM / 8;
   constexpr int ARPP = 256 / ACPR;
   constexpr int AREP = kBK / ARPP;
@@ -399,12 +409,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvGeom g, const uint1
   {
     const int j = j0 + bch * 8;
     b_ok = j < g.K;
-    const int rs = b_ok ? j / g.C : 0;
+    const int rs = b_ok ? sdiv(j, g.C, a.c_shift) : 0;
     b_c = b_ok ? j - rs * g.C : 0;
-    b_r = b_ok ? rs / g.S : 0;
-    b_s = b_ok ? rs - b_r * g.S : 0;
+    b_r = rs / KS;
+    b_s = rs - b_r * KS;
   }
   const int HWC = g.H * g.W * g.C;
+  const int PQ = g.P * g.Q;
   uint4 ra[AREP], rb[BREP];
   auto load_tile = [&](int kt) {
     const int mb = mbeg + kt * kBK;
@@ -413,7 +424,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvGeom g, const uint1
       const int m = mb + arow + ARPP * i;
       const int ko = ko0 + ach * 8;
       if (m < mend && ko < g.Ng)
-        ra[i] = *reinterpret_cast<const uint4*>(dy + (int64_t)m * g.Ng + ko);
+        ra[i] = *reinterpret_cast<const uint4*>(a.src + (int64_t)m * g.Ng + ko);  // src = dY
       else
         ra[i] = make_uint4(0, 0, 0, 0);
     }
@@ -423,17 +434,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvGeom g, const uint1
       bool ok = b_ok && m < mend;
       int n = 0, iy = 0, ix = 0;
       if (ok) {
-        const int pq = g.P * g.Q;
-        n = m / pq;
-        const int rem = m - n * pq;
-        const int oy = rem / g.Q;
+        n = sdiv(m, PQ, a.pq_shift);
+        const int rem = m - n * PQ;
+        const int oy = sdiv(rem, g.Q, a.q_shift);
         const int ox = rem - oy * g.Q;
-        iy = oy * g.stride - g.pad + b_r;
-        ix = ox * g.stride - g.pad + b_s;
+        iy = oy * ST - g.pad + b_r;
+        ix = ox * ST - g.pad + b_s;
         ok = iy >= 0 && ix >= 0 && iy < g.H && ix < g.W;
       }
       if (ok)
-        rb[i] = *reinterpret_cast<const uint4*>(x + (int64_t)n * HWC + (iy * g.W + ix) * g.C + b_c);
+        rb[i] = *reinterpret_cast<const uint4*>(a.wgt + (int64_t)n * HWC + (iy * g.W + ix) * g.C + b_c);  // wgt = X
       else
         rb[i] = make_uint4(0, 0, 0, 0);
     }
@@ -523,14 +533,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvGeom g, const uint1
       }
 }
 
-// [Cout][R][S][Cin] -> [Cin][R][S][Cout]  (dgrad weight layout)
+// [Cout][R][S][Cin] -> [Cin][R][S][Cout]  (layout utility, not on the hot path)
 __global__ __launch_bounds__(256) void transpose_krsc_kernel(const uint16_t* __restrict__ w,
                                                              uint16_t* __restrict__ wt, int Co,
                                                              int RS, int Ci) {
   const int64_t n = (int64_t)Co * RS * Ci;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    // output index i -> (ci, rs, co)
     const int co = (int)(i % Co);
     const int64_t t2 = i / Co;
     const int rs = (int)(t2 % RS);
@@ -540,64 +549,89 @@ __global__ __launch_bounds__(256) void transpose_krsc_kernel(const uint16_t* __r
 }
 
 // ---------------------------------------------------------------------------
-template <int BM, int BN, bool DG>
-static void launch_gemm_t(const ConvGeom& g, const uint16_t* src, const uint16_t* wgt, uint16_t* y,
-                          float* ysplit, double* stats, int splits, int kchunk, int accum,
-                          hipStream_t s) {
-  dim3 grid((g.M + BM - 1) / BM, (g.Ng + BN - 1) / BN, splits);
+static int log2_exact(int v) {
+  if (v <= 0 || (v & (v - 1))) return -1;
+  int s = 0;
+  while ((1 << s) < v) ++s;
+  return s;
+}
+
+static void fill_shifts(ConvArgs& a) {
+  a.c_shift = log2_exact(a.g.C);
+  a.q_shift = log2_exact(a.g.Q);
+  a.pq_shift = log2_exact(a.g.P * a.g.Q);
+}
+
+template <int BM, int BN, bool DG, int KS, int ST>
+static void launch_gemm_t(const ConvArgs& a, const ConvPlan& p, hipStream_t s) {
+  dim3 grid((a.g.M + BM - 1) / BM, (a.g.Ng + BN - 1) / BN, p.splits);
   const size_t btile = DG ? (size_t)kBK * (BN + kPad) : (size_t)BN * kLdsStride;
-  const size_t lds = (size_t)2 * ((size_t)BM * kLdsStride + btile) * sizeof(uint16_t);
+  size_t lds = (size_t)2 * ((size_t)BM * kLdsStride + btile) * sizeof(uint16_t);
+  const size_t epi = ((size_t)BM * (BN + 4) + 256 * 16 + 8) * sizeof(float);
+  if (lds < epi) lds = epi;
   static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into
   if (!attr_set && lds > 65536) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, DG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, DG, KS, ST>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  conv_gemm_kernel<BM, BN, DG><<<grid, 256, lds, s>>>(g, src, wgt, y, ysplit, stats, kchunk, accum);
+  conv_gemm_kernel<BM, BN, DG, KS, ST><<<grid, 256, lds, s>>>(a);
+}
+
+template <int BM, int BN, bool DG>
+static void launch_gemm_ks(const ConvArgs& a, const ConvPlan& p, hipStream_t s) {
+  const int ks = a.g.R, st = a.g.stride;
+  if (ks == 3 && st == 1) launch_gemm_t<BM, BN, DG, 3, 1>(a, p, s);
+  else if (ks == 3 && st == 2) launch_gemm_t<BM, BN, DG, 3, 2>(a, p, s);
+  else if (ks == 1 && st == 1) launch_gemm_t<BM, BN, DG, 1, 1>(a, p, s);
+  else if (ks == 1 && st == 2) launch_gemm_t<BM, BN, DG, 1, 2>(a, p, s);
+}
+
+bool conv_supported(const ConvGeom& g) {
+  return g.R == g.S && (g.R == 1 || g.R == 3) && (g.stride == 1 || g.stride == 2);
 }
 
 ConvPlan plan_conv_gemm(const ConvGeom& g) {
   ConvPlan p;
   p.bm = g.M >= 8192 ? 128 : 64;
-  p.bn = g.Ng >= 128 && g.M >= 8192 ? 128 : 64;
-  if (p.bm == 128 && p.bn == 128 && g.M < 16384) p.bn = 64;
+  p.bn = g.Ng >= 128 && g.M >= 16384 ? 128 : 64;
   const int tiles = ((g.M + p.bm - 1) / p.bm) * ((g.Ng + p.bn - 1) / p.bn);
   const int ksteps = (g.K + kBK - 1) / kBK;
   int splits = 1;
   while (tiles * splits < 256 && ksteps / (splits * 2) >= 4 && splits < 16) splits *= 2;
   p.splits = splits;
   p.kchunk = ((ksteps + splits - 1) / splits) * kBK;
-  p.stats_rows = splits > 1 ? 0 : (g.M + p.bm - 1) / p.bm;
+  p.stats_rows = 1;
   return p;
 }
 
+int conv_counter_slots(const ConvGeom& g, const ConvPlan& p) {
+  return ((g.M + p.bm - 1) / p.bm) * ((g.Ng + p.bn - 1) / p.bn);
+}
+
 void launch_conv_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const uint16_t* src,
-                      const uint16_t* wgt, uint16_t* y, float* ysplit, double* stats, bool accum,
-                      hipStream_t s) {
-  const int ac = accum ? 1 : 0;
-  float* ys = p.splits > 1 ? ysplit : nullptr;
-  double* st = p.splits > 1 ? nullptr : stats;
-#define MFL_CONV_CASE(BM_, BN_)                                                                \
-  if (p.bm == BM_ && p.bn == BN_) {                                                            \
-    if (dgrad) launch_gemm_t<BM_, BN_, true>(g, src, wgt, y, ys, st, p.splits, p.kchunk, ac, s);   \
-    else launch_gemm_t<BM_, BN_, false>(g, src, wgt, y, ys, st, p.splits, p.kchunk, ac, s);        \
+                      const uint16_t* wgt, uint16_t* y, float* ysplit, int* counters,
+                      double* stats, bool accum, hipStream_t s) {
+  ConvArgs a{};
+  a.g = g;
+  a.src = src;
+  a.wgt = wgt;
+  a.y = y;
+  a.ysplit = ysplit;
+  a.counters = counters;
+  a.stats = stats;
+  a.kchunk = p.kchunk;
+  a.accum = accum ? 1 : 0;
+  fill_shifts(a);
+#define MFL_CONV_CASE(BM_, BN_)                                    \
+  if (p.bm == BM_ && p.bn == BN_) {                                \
+    if (dgrad) launch_gemm_ks<BM_, BN_, true>(a, p, s);            \
+    else launch_gemm_ks<BM_, BN_, false>(a, p, s);                 \
   }
   MFL_CONV_CASE(128, 128)
   MFL_CONV_CASE(128, 64)
-  MFL_CONV_CASE(64, 128)
   MFL_CONV_CASE(64, 64)
 #undef MFL_CONV_CASE
-  if (p.splits > 1) {
-    const int nb = splitk_stats_blocks(g.M, g.Ng);
-    splitk_reduce_kernel<<<nb, 256, 0, s>>>(ysplit, p.splits, g.M, g.Ng, y, stats, ac);
-  }
-}
-
-int splitk_stats_blocks(int M, int C) {
-  const int tpr = C / 8;
-  const int rpp = 256 / tpr;
-  int nb = (M + rpp * 4 - 1) / (rpp * 4);
-  return nb < 1 ? 1 : (nb > 512 ? 512 : nb);
 }
 
 ConvPlan plan_conv_wgrad(const ConvGeom& g) {
@@ -619,9 +653,19 @@ ConvPlan plan_conv_wgrad(const ConvGeom& g) {
 // which zeroes the gradient buffer after consuming it.
 void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, const uint16_t* dy,
                        float* dw, hipStream_t s) {
+  ConvArgs a{};
+  a.g = g;
+  a.src = dy;
+  a.wgt = x;
+  a.kchunk = p.kchunk;
+  fill_shifts(a);
   dim3 grid((g.Ng + 63) / 64, (g.K + 63) / 64, p.splits);
   const size_t lds = (size_t)2 * kBK * ((64 + kPad) + (64 + kPad)) * sizeof(uint16_t);
-  conv_wgrad_kernel<64, 64><<<grid, 256, lds, s>>>(g, x, dy, dw, p.kchunk);
+  const int ks = g.R, st = g.stride;
+  if (ks == 3 && st == 1) conv_wgrad_kernel<64, 64, 3, 1><<<grid, 256, lds, s>>>(a, dw);
+  else if (ks == 3 && st == 2) conv_wgrad_kernel<64, 64, 3, 2><<<grid, 256, lds, s>>>(a, dw);
+  else if (ks == 1 && st == 1) conv_wgrad_kernel<64, 64, 1, 1><<<grid, 256, lds, s>>>(a, dw);
+  else if (ks == 1 && st == 2) conv_wgrad_kernel<64, 64, 1, 2><<<grid, 256, lds, s>>>(a, dw);
 }
 
 void launch_transpose_krsc(const uint16_t* w, uint16_t* wt, int Co, int RS, int Ci, hipStream_t s) {

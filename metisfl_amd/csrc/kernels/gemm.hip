@@ -43,7 +43,7 @@ void launch_gemm_nt(const uint16_t* a, const uint16_t* b, uint16_t* c, const flo
   ConvPlan p = plan_conv_gemm(g);
   p.splits = 1;  // no workspace on this path
   p.kchunk = ((K + 63) / 64) * 64;
-  launch_conv_gemm(g, false, p, a, b, c, nullptr, nullptr, false, s);
+  launch_conv_gemm(g, false, p, a, b, c, nullptr, nullptr, nullptr, false, s);
   if (epilogue != EPI_NONE && bias) {
     const int64_t nvec = (int64_t)M * N / 8;
     const unsigned grid = stream_grid(nvec);

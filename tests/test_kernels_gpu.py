@@ -38,6 +38,19 @@ CONV_CASES = [
     (8, 8, 8, 256, 256, 3, 1),    # layer3 (split-K)
     (4, 4, 4, 512, 512, 3, 1),    # layer4 (split-K)
     (2, 7, 5, 24, 40, 3, 1),      # ragged tiles / odd spatial
+    # every distinct ResNet-18 layer at the benchmark batch (32): these pick
+    # the 128-row tiles and the split-K factors the training step really uses
+    (32, 32, 32, 8, 64, 3, 1),
+    (32, 32, 32, 64, 64, 3, 1),
+    (32, 32, 32, 64, 128, 3, 2),
+    (32, 32, 32, 64, 128, 1, 2),
+    (32, 16, 16, 128, 128, 3, 1),
+    (32, 16, 16, 128, 256, 3, 2),
+    (32, 16, 16, 128, 256, 1, 2),
+    (32, 8, 8, 256, 256, 3, 1),
+    (32, 8, 8, 256, 512, 3, 2),
+    (32, 8, 8, 256, 512, 1, 2),
+    (32, 4, 4, 512, 512, 3, 1),
 ]
 
 
@@ -52,7 +65,7 @@ def test_conv_forward_matches_fp32(case):
     shp = K.ConvShape(N, H, W, C, Co, k, k, s, k // 2)
     y = torch.empty(N, shp.P, shp.Q, Co, dtype=torch.bfloat16, device=DEV)
     plan = K.conv_plan(0, shp, torch.device(DEV))
-    ws = torch.empty(max(4, plan.workspace), device=DEV)
+    ws = torch.zeros(max(4, plan.workspace), device=DEV)
     stats = torch.zeros(2 * Co, dtype=torch.float64, device=DEV)
     K.conv_forward(x, w, y, shp, ws, stats)
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=s,
@@ -63,6 +76,43 @@ def test_conv_forward_matches_fp32(case):
     yf = y.double().reshape(-1, Co).cpu()
     assert torch.allclose(st[0], yf.sum(0), rtol=1e-6, atol=1e-6)
     assert torch.allclose(st[1], (yf * yf).sum(0), rtol=1e-6, atol=1e-6)
+    # the split-K arrival counters are re-armed in-kernel: reuse the workspace
+    y2 = torch.empty_like(y)
+    for _ in range(3):
+        K.conv_forward(x, w, y2, shp, ws, None)
+    assert torch.equal(y2, y)
+    if plan.splits > 1:
+        slots = -(-shp.N * shp.P * shp.Q // plan.bm) * -(-Co // plan.bn)
+        assert int(ws[:slots].view(torch.int32).abs().sum()) == 0
+
+
+def test_conv_split_k_shared_workspace():
+    """All layers of a model share one split-K workspace (arrival counters +
+    slabs).  Run every split layer's fwd + dgrad back to back on ONE buffer,
+    twice, and check each output against fp32: a plan-dependent layout would
+    let one layer's slabs poison another layer's counters."""
+    from metisfl_amd.ops import nn as K
+    torch.manual_seed(7)
+    shapes = [K.ConvShape(*c[:5], c[5], c[5], c[6], c[5] // 2) for c in CONV_CASES[-7:]]
+    dev = torch.device(DEV)
+    need = max(max(K.conv_plan(0, s, dev).workspace, K.conv_plan(1, s, dev).workspace) for s in shapes)
+    ws = torch.zeros(max(4, need), device=DEV)
+    for _ in range(2):
+        for s in shapes:
+            x = bf(torch.randn(s.N, s.H, s.W, s.C, device=DEV))
+            w = bf(torch.randn(s.Co, s.R, s.S, s.C, device=DEV) * 0.05)
+            dy = bf(torch.randn(s.N, s.P, s.Q, s.Co, device=DEV))
+            y = torch.empty(s.N, s.P, s.Q, s.Co, dtype=torch.bfloat16, device=DEV)
+            dx = torch.empty_like(x)
+            K.conv_forward(x, w, y, s, ws, None)
+            K.conv_dgrad(dy, w, dx, s, ws, accumulate=False)
+            ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2),
+                           stride=s.stride, padding=s.pad).permute(0, 2, 3, 1)
+            dref = torch.nn.grad.conv2d_input((s.N, s.C, s.H, s.W), w.float().permute(0, 3, 1, 2),
+                                              dy.float().permute(0, 3, 1, 2), stride=s.stride,
+                                              padding=s.pad).permute(0, 2, 3, 1)
+            assert rel_err(y, ref) < 1e-2, s
+            assert rel_err(dx, dref) < 1e-2, s
 
 
 @pytest.mark.parametrize("case", CONV_CASES[1:])
@@ -77,7 +127,7 @@ def test_conv_dgrad_matches_fp32(case):
     K.transpose_krsc(w, wt, Co, k * k, C)
     assert torch.equal(wt.cpu(), w.cpu().permute(3, 1, 2, 0))
     plan = K.conv_plan(1, shp, torch.device(DEV))
-    ws = torch.empty(max(4, plan.workspace), device=DEV)
+    ws = torch.zeros(max(4, plan.workspace), device=DEV)
     dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=DEV)
     K.conv_dgrad(dy, w, dx, shp, ws, accumulate=False)
     ref = torch.nn.grad.conv2d_input((N, C, H, W), w.float().permute(0, 3, 1, 2),
