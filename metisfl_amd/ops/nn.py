@@ -116,8 +116,11 @@ def conv_wgrad(x, dy, dw, shp: ConvShape, accumulate: bool = False) -> None:
     if x.is_cuda:
         ops().conv_wgrad(x, dy, dw, *shp.args(), accumulate)
         return
-    g = torch.nn.grad.conv2d_weight(_nchw(x), (shp.Co, shp.C, shp.R, shp.S), _nchw(dy),
-                                    stride=shp.stride, padding=shp.pad)
+    # contiguous NCHW: torch's CPU weight-gradient kernel corrupts the heap on
+    # channels-last views for strided 1x1 convs with few channels (observed
+    # with torch 2.10: N=4, C=8 -> 16, 1x1 stride 2)
+    g = torch.nn.grad.conv2d_weight(_nchw(x).contiguous(), (shp.Co, shp.C, shp.R, shp.S),
+                                    _nchw(dy).contiguous(), stride=shp.stride, padding=shp.pad)
     dw.copy_(g.permute(0, 2, 3, 1).reshape(dw.shape))
 
 
