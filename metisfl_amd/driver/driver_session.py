@@ -1,0 +1,326 @@
+"""Federation driver (reference: metisfl/driver/driver_session.py:29-585,
+``DriverSessionBase`` / ``DriverSession``; same public methods).
+
+Lifecycle: ``initialize_federation`` starts the controller, waits for its
+health check, ships the initial community model (ReplaceCommunityModel), then
+starts one learner per configured learner (0.1 s stagger);
+``monitor_federation`` polls the controller for the termination signals
+(rounds / metric cutoff / wall clock); ``shutdown_federation`` collects the
+statistics (the reference's four keys) and stops everything.
+
+MI355X-first differences:
+  * learners are launched as LOCAL processes, one per GPU, pinned with
+    HIP_VISIBLE_DEVICES (the reference SSHes even to localhost with fabric,
+    which is not installed); ``Launcher: ssh`` runs the same command lines
+    through the ``ssh`` CLI for remote hosts;
+  * the model is shipped as a small JSON definition of a built-in family
+    (or a cloudpickled TorchModelDef), not a tarred SavedModel;
+  * for the on-node data plane (RCCL all-reduce instead of gRPC model
+    transfer) see ``FederationDriver.run_collective`` in driver/collective.py.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shlex
+import shutil
+import socket
+import subprocess
+import time
+
+from google.protobuf.json_format import MessageToDict
+
+from metisfl_amd.models.model_def import StaticModelDef, TorchModelDef
+from metisfl_amd.utils import fedenv_parser
+from metisfl_amd.utils.grpc_controller_client import GRPCControllerClient
+from metisfl_amd.utils.grpc_learner_client import GRPCLearnerClient
+from metisfl_amd.utils.init_services_factory import MetisInitServicesCmdFactory
+from metisfl_amd.utils.metis_logger import MetisASCIIArt, MetisLogger
+from metisfl_amd.utils.proto_messages_factory import MetisProtoMessages as M
+from metisfl_amd.utils.proto_messages_factory import ModelProtoMessages as MM
+from metisfl_amd.utils.ssl_configurator import SSLConfigurator
+from metisfl_amd.utils.tensor_codec import model_from_arrays
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _ssl_pb(enable: bool, cfg):
+    if not enable:
+        return M.construct_ssl_config_pb(False)
+    if cfg is not None and cfg.public_certificate_file:
+        return M.construct_ssl_config_pb(True, M.construct_ssl_config_files_pb(cfg.public_certificate_file,
+                                                                            cfg.private_key_file))
+    return SSLConfigurator.default_ssl_config_pb()
+
+
+class DriverSessionBase:
+
+    def __init__(self, fed_env, model, train_dataset_recipe_fn, validation_dataset_recipe_fn=None,
+                 test_dataset_recipe_fn=None, working_dir: str = "/tmp/metis_amd/", device: str | None = None,
+                 seed: int = 0):
+        MetisASCIIArt.print()
+        self.federation_environment = fed_env if isinstance(fed_env, fedenv_parser.FederationEnvironment) \
+            else fedenv_parser.FederationEnvironment(fed_env)
+        env = self.federation_environment
+        self.num_participating_learners = len(env.learners)
+        self.working_dir = working_dir
+        if os.path.exists(working_dir):
+            shutil.rmtree(working_dir)
+        os.makedirs(working_dir)
+        self.device = device
+        self.seed = seed
+        self._model_dir = os.path.join(working_dir, "model_definition")
+        self.neural_engine = self._save_model(model)
+        if train_dataset_recipe_fn is None:
+            raise RuntimeError("Train dataset recipe cannot be empty.")
+        self.train_dataset_recipe_fp = self._dump_recipe(train_dataset_recipe_fn, "model_train_dataset_ops.pkl")
+        self.validation_dataset_recipe_fp = self._dump_recipe(validation_dataset_recipe_fn,
+                                                              "model_validation_dataset_ops.pkl")
+        self.test_dataset_recipe_fp = self._dump_recipe(test_dataset_recipe_fn, "model_test_dataset_ops.pkl")
+        self.enable_ssl = env.communication_protocol.enable_ssl
+        self._controller_entity = M.construct_server_entity_pb(
+            env.controller.grpc_servicer.hostname, env.controller.grpc_servicer.port,
+            _ssl_pb(self.enable_ssl, env.controller.ssl_configs))
+        self._learner_entities = {
+            l.learner_id: M.construct_server_entity_pb(l.grpc_servicer.hostname, l.grpc_servicer.port,
+                                                       _ssl_pb(self.enable_ssl, l.ssl_configs))
+            for l in env.learners}
+        self._driver_controller_grpc_client = GRPCControllerClient(self._controller_entity, max_workers=1)
+        self._driver_learner_grpc_clients = {lid: GRPCLearnerClient(e) for lid, e in self._learner_entities.items()}
+        self._federation_statistics: dict = {}
+        self._procs: dict[str, subprocess.Popen] = {}
+        self._init_he(env)
+        self._cmds = MetisInitServicesCmdFactory()
+
+    # -- setup helpers -----------------------------------------------------------------
+    def _save_model(self, model) -> str:
+        if model == "fake" or model is None:  # echo learners: orchestration only
+            self._initial_model = model_from_arrays(["w"], [__import__("numpy").zeros(4, "float32")])
+            return "fake"
+        if isinstance(model, str):
+            model = StaticModelDef(model)
+        if isinstance(model, StaticModelDef):
+            model.save(self._model_dir)
+            net = model.get_model(batch_size=1, device="cpu", seed=self.seed)
+            st = net.state
+            vals = st.to_numpy()
+            self._initial_model = model_from_arrays([s.name for s in st.specs], [vals[s.name] for s in st.specs],
+                                                    [s.trainable for s in st.specs])
+            return "static"
+        if isinstance(model, TorchModelDef):
+            import cloudpickle
+            import inspect
+            os.makedirs(self._model_dir, exist_ok=True)
+            mod = inspect.getmodule(type(model))
+            if mod is not None and mod.__name__ not in ("__main__",):
+                cloudpickle.register_pickle_by_value(mod)
+            with open(os.path.join(self._model_dir, "model_def.pkl"), "wb") as f:
+                cloudpickle.dump(model, f)
+            from metisfl_amd.models.torch_ops import TorchModelOps
+            names, trainable, values = TorchModelOps(model, device="cpu", seed=self.seed).get_model_weights()
+            self._initial_model = model_from_arrays(names, values, trainable)
+            return "torch"
+        if model == "fake" or model is None:
+            self._initial_model = model_from_arrays(["w"], [__import__("numpy").zeros(4, "float32")])
+            return "fake"
+        raise RuntimeError("Not a supported model type (StaticModelDef, family name or TorchModelDef).")
+
+    def _dump_recipe(self, fn, name):
+        if fn is None:
+            return None
+        import cloudpickle
+        p = os.path.join(self.working_dir, name)
+        with open(p, "wb") as f:
+            cloudpickle.dump(fn, f)
+        return p
+
+    def _init_he(self, env):
+        he = env.homomorphic_encryption
+        self._he_scheme = None
+        if he is not None and he.scheme.upper() == "CKKS":
+            from metisfl_amd import _engine
+            d = os.path.join(self.working_dir, "cryptoparams")
+            os.makedirs(d, exist_ok=True)
+            self._he_scheme = _engine.CKKS(he.batch_size, he.scaling_factor_bits)
+            self._he_scheme.gen_crypto_context_and_keys(d)
+            files = self._he_scheme.get_crypto_params_files()
+            ckks = M.construct_ckks_scheme_config_pb(he.batch_size, he.scaling_factor_bits)
+            self._controller_he_scheme_config_pb = M.construct_he_scheme_config_pb(
+                enabled=True, crypto_context_file=files["crypto_context_file"], ckks_scheme_config_pb=ckks)
+            self._learners_he_scheme_config_pb = M.construct_he_scheme_config_pb(
+                enabled=True, crypto_context_file=files["crypto_context_file"],
+                public_key_file=files["public_key_file"], private_key_file=files["private_key_file"],
+                ckks_scheme_config_pb=ckks)
+        else:
+            self._controller_he_scheme_config_pb = M.construct_he_scheme_config_pb(enabled=False)
+            self._learners_he_scheme_config_pb = M.construct_he_scheme_config_pb(enabled=False)
+
+    # -- service command lines ---------------------------------------------------------------
+    def _controller_params(self):
+        env = self.federation_environment
+        rule = env.global_model_config.aggregation_rule
+        agg = M.construct_aggregation_rule_pb(rule.aggregation_rule_name, rule.aggregation_rule_scaling_factor,
+                                              rule.aggregation_rule_stride_length,
+                                              self._controller_he_scheme_config_pb)
+        gms = M.construct_global_model_specs(agg, env.global_model_config.participation_ratio)
+        cp = env.communication_protocol
+        cs = M.construct_communication_specs_pb(cp.name, cp.semi_synchronous_lambda, cp.semi_sync_recompute_num_updates)
+        lm = env.local_model_config
+        opt = MM.construct_optimizer_config_pb_from_kwargs(lm.optimizer_config.optimizer_pb_kwargs)
+        mh = M.construct_controller_modelhyperparams_pb(lm.batch_size, lm.local_epochs, opt,
+                                                        lm.validation_percentage)
+        ms = env.model_store_config
+        store = M.construct_model_store_config_pb(ms.name, ms.eviction_policy, ms.eviction_lineage_length,
+                                                  ms.connection_configs.hostname, ms.connection_configs.port)
+        return gms, cs, mh, store
+
+    def _init_controller_cmd(self):
+        gms, cs, mh, store = self._controller_params()
+        return self._cmds.init_controller_target(self._controller_entity, gms, cs, mh, store)
+
+    def _init_learner_cmd(self, learner_instance, controller_instance=None):
+        lid = learner_instance.learner_id
+        dc = learner_instance.dataset_configs
+        dev = self.device
+        if dev is None:
+            dev = "cuda" if learner_instance.devices else None
+        return self._cmds.init_learner_target(
+            self._learner_entities[lid], self._controller_entity, self._learners_he_scheme_config_pb,
+            self._model_dir, dc.train_dataset_path, dc.validation_dataset_path, dc.test_dataset_path,
+            self.train_dataset_recipe_fp, self.validation_dataset_recipe_fp, self.test_dataset_recipe_fp,
+            neural_engine=self.neural_engine, device=dev,
+            credentials_dir=os.path.join(self.working_dir, f"learner_{learner_instance.grpc_servicer.port}_credentials"),
+            seed=self.seed)
+
+    # -- process control -----------------------------------------------------------------------
+    def _spawn(self, name, cmd, env_extra=None, remote=None):
+        log = open(os.path.join(self.working_dir, f"{name}.log"), "w")
+        env = dict(os.environ)
+        env.update(env_extra or {})
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        if remote is not None:  # Launcher: ssh
+            cc = remote.connection_configs
+            exports = " ".join(f"{k}={shlex.quote(v)}" for k, v in (env_extra or {}).items())
+            remote_cmd = f"{cc.on_login.rstrip(';') + ' && ' if cc.on_login else ''}cd {remote.project_home or '.'} " \
+                         f"&& {exports} {' '.join(shlex.quote(c) for c in cmd)}"
+            target = f"{cc.username}@{cc.hostname}" if cc.username else cc.hostname
+            cmd = ["ssh"] + (["-p", str(cc.port)] if cc.port else []) + \
+                (["-i", cc.key_filename] if cc.key_filename else []) + [target, remote_cmd]
+        self._procs[name] = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT, env=env)
+        return self._procs[name]
+
+    def _init_controller(self):
+        ssh = self.federation_environment.launcher == "ssh"
+        return self._spawn("controller", self._init_controller_cmd(),
+                           remote=self.federation_environment.controller if ssh else None)
+
+    def _init_learner(self, learner_instance, controller_instance=None):
+        extra = {}
+        if learner_instance.devices:
+            extra["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in learner_instance.devices)
+        ssh = self.federation_environment.launcher == "ssh"
+        return self._spawn(f"learner_{learner_instance.learner_id}",
+                           self._init_learner_cmd(learner_instance, controller_instance), extra,
+                           remote=learner_instance if ssh else None)
+
+    def _ship_model_to_controller(self):
+        model = self._initial_model
+        if self._he_scheme is not None:
+            from metisfl_amd.utils.tensor_codec import model_to_arrays
+            names, arrays, tr = model_to_arrays(model)
+            self._he_scheme.load_crypto_context_from_file(self._he_scheme.get_crypto_params_files()["crypto_context_file"])
+            model = model_from_arrays(names, arrays, tr, self._he_scheme)
+        return self._driver_controller_grpc_client.replace_community_model(1, model, request_retries=3)
+
+    # -- public API -----------------------------------------------------------------------------------
+    def initialize_federation(self):
+        self._init_controller()
+        ok = self._driver_controller_grpc_client.check_health_status(request_retries=10, request_timeout=30)
+        if not ok:
+            raise RuntimeError("controller did not come up; see controller.log")
+        self._ship_model_to_controller()
+        for l in self.federation_environment.learners:
+            self._init_learner(l, self.federation_environment.controller)
+            time.sleep(0.1)
+
+    def monitor_federation(self, request_every_secs: float = 10):
+        env = self.federation_environment
+        rounds = env.termination_signals.federation_rounds
+        cp = env.communication_protocol
+        cutoff_mins = env.termination_signals.execution_time_cutoff_mins
+        metric_cutoff = env.termination_signals.metric_cutoff_score
+        metric = env.evaluation_metric
+        st = time.time()
+        while True:
+            time.sleep(request_every_secs)
+            for name, p in self._procs.items():
+                if p.poll() is not None and p.returncode != 0:
+                    raise RuntimeError(f"{name} exited with {p.returncode}; see {name}.log")
+            md = self._driver_controller_grpc_client.get_runtime_metadata(num_backtracks=0).metadata
+            if (cp.is_synchronous or cp.is_semi_synchronous) and rounds and len(md) > 0:
+                if max(m.global_iteration for m in md) > rounds:
+                    MetisLogger.info("Exceeded federation rounds cutoff point. Exiting ...")
+                    return "rounds"
+            evals = self._driver_controller_grpc_client.get_community_model_evaluation_lineage(-1)
+            for res in evals.community_evaluation:
+                scores = [float(e.test_evaluation.metric_values[metric]) for e in res.evaluations.values()
+                          if metric in e.test_evaluation.metric_values]
+                if scores and sum(scores) / len(scores) >= metric_cutoff:
+                    MetisLogger.info("Exceeded evaluation metric cutoff score. Exiting ...")
+                    return "metric"
+            if (time.time() - st) / 60 > cutoff_mins:
+                MetisLogger.info("Exceeded execution time cutoff minutes. Exiting ...")
+                return "time"
+
+    def _collect_local_statistics(self):
+        c = self._driver_controller_grpc_client
+        learners = c.get_participating_learners()
+        ids = [l.id for l in learners.learner]
+        self._federation_statistics["learners_descriptor"] = MessageToDict(learners, preserving_proto_field_name=True)
+        self._federation_statistics["learners_models_results"] = MessageToDict(
+            c.get_local_task_lineage(-1, ids), preserving_proto_field_name=True)
+
+    def _collect_global_statistics(self):
+        c = self._driver_controller_grpc_client
+        self._federation_statistics["federation_runtime_metadata"] = MessageToDict(
+            c.get_runtime_metadata(num_backtracks=0), preserving_proto_field_name=True)
+        self._federation_statistics["community_model_results"] = MessageToDict(
+            c.get_community_model_evaluation_lineage(-1), preserving_proto_field_name=True)
+
+    def get_federation_statistics(self) -> dict:
+        return self._federation_statistics
+
+    def save_statistics(self, path: str) -> None:
+        with open(path, "w") as f:
+            json.dump(self._federation_statistics, f, indent=1)
+
+    def shutdown_federation(self, timeout: float = 60):
+        try:
+            self._collect_local_statistics()
+            for c in self._driver_learner_grpc_clients.values():
+                try:
+                    c.shutdown_learner(request_retries=1, request_timeout=30, block=True)
+                except Exception as e:  # noqa: BLE001 - a dead learner must not block shutdown
+                    MetisLogger.warning("learner shutdown failed: %r", e)
+                c.shutdown()
+            self._collect_global_statistics()
+            self._driver_controller_grpc_client.shutdown_controller(request_retries=2, request_timeout=30)
+            self._driver_controller_grpc_client.shutdown()
+        finally:
+            end = time.time() + timeout
+            for name, p in self._procs.items():
+                try:
+                    p.wait(timeout=max(0.1, end - time.time()))
+                except subprocess.TimeoutExpired:
+                    MetisLogger.warning("%s did not exit; terminating pid %d", name, p.pid)
+                    p.terminate()
+                    p.wait(10)
+
+
+class DriverSession(DriverSessionBase):
+    """Same constructor as the reference DriverSession."""
