@@ -94,7 +94,8 @@ std::vector<int64_t> conv_plan(int64_t mode, int64_t N, int64_t H, int64_t W, in
 
 void run_gemm(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const torch::Tensor& w,
               const torch::Tensor& y, const c10::optional<torch::Tensor>& ws,
-              const c10::optional<torch::Tensor>& stats, bool accum) {
+              const c10::optional<torch::Tensor>& stats, bool accum,
+              const mfl::BnBwdFusion* bnb = nullptr) {
   auto p = mfl::plan_conv_gemm(g);
   float* wsp = nullptr;
   int* counters = nullptr;
@@ -114,8 +115,11 @@ void run_gemm(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, cons
                 "stats must be a contiguous fp64 device tensor of >= 2*Cout elements");
     st = stats->data_ptr<double>();
   }
-  mfl::launch_conv_gemm(g, dgrad, p, bf(src), bf(w), bf(y), wsp, counters, st, accum,
-                        cur_stream(y));
+  if (bnb != nullptr)
+    mfl::launch_conv_dgrad_bnb(g, p, bf(src), bf(w), bf(y), wsp, counters, accum, *bnb, cur_stream(y));
+  else
+    mfl::launch_conv_gemm(g, dgrad, p, bf(src), bf(w), bf(y), wsp, counters, st, accum,
+                          cur_stream(y));
 }
 
 void conv_forward(torch::Tensor x, torch::Tensor w, torch::Tensor y,
@@ -131,11 +135,34 @@ void conv_forward(torch::Tensor x, torch::Tensor w, torch::Tensor y,
 
 void conv_dgrad(torch::Tensor dy, torch::Tensor wt, torch::Tensor dx,
                 c10::optional<torch::Tensor> ws, int64_t N, int64_t H, int64_t W, int64_t C,
-                int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate) {
+                int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate,
+                c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
+                c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
+                c10::optional<torch::Tensor> bn_acc) {
   auto g = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
   check_bf16(dy, (int64_t)N * g.H * g.W * Co, "dy");
   check_bf16(wt, C * R * S * Co, "wt");
   check_bf16(dx, N * H * W * C, "dx");
+  if (bn_acc.has_value() && bn_acc->defined()) {
+    // fused BN-backward reductions of the layer whose output gradient dx is
+    mfl::BnBwdFusion f;
+    TORCH_CHECK(bn_z.has_value() && bn_mean.has_value() && bn_invstd.has_value(), "bn fusion args");
+    check_bf16(*bn_z, N * H * W * C, "bn_z");
+    f.z = bf(*bn_z);
+    if (bn_y.has_value() && bn_y->defined()) {
+      check_bf16(*bn_y, N * H * W * C, "bn_y");
+      f.y = bf(*bn_y);
+    }
+    check_f32(*bn_mean, C, "bn_mean");
+    check_f32(*bn_invstd, C, "bn_invstd");
+    f.mean = bn_mean->data_ptr<float>();
+    f.invstd = bn_invstd->data_ptr<float>();
+    TORCH_CHECK(bn_acc->is_cuda() && bn_acc->is_contiguous() && bn_acc->scalar_type() == torch::kFloat64 &&
+                    bn_acc->numel() >= 2 * C, "bn_acc must be a contiguous fp64 tensor of >= 2*C");
+    f.acc = bn_acc->data_ptr<double>();
+    run_gemm(g, true, dy, wt, dx, ws, c10::nullopt, accumulate, &f);
+    return;
+  }
   run_gemm(g, true, dy, wt, dx, ws, c10::nullopt, accumulate);
 }
 

@@ -258,7 +258,7 @@ void bn_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torc
 void bn_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,
                  torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd, torch::Tensor acc,
                  c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta,
-                 torch::Tensor dx, c10::optional<torch::Tensor> dy_masked) {
+                 torch::Tensor dx, c10::optional<torch::Tensor> dy_masked, bool presummed) {
   check_nhwc(dy, C);
   check_nhwc(x, C);
   check_nhwc(dx, C);
@@ -288,7 +288,10 @@ void bn_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor>
   a.M = x.numel() / C;
   a.C = (int)C;
   auto s = cur_stream(x);
-  mfl::launch_bn_bwd_reduce(a.dy, a.x, a.y, a.mean, a.invstd, a.M, a.C, acc.data_ptr<double>(), s);
+  // presummed: the producer of dy (a conv dgrad epilogue) already added
+  // sum(g) / sum(g*xhat) into acc
+  if (!presummed)
+    mfl::launch_bn_bwd_reduce(a.dy, a.x, a.y, a.mean, a.invstd, a.M, a.C, acc.data_ptr<double>(), s);
   mfl::launch_bn_bwd_apply(a, s);
 }
 

@@ -37,6 +37,17 @@ struct ConvArgs {
   float* ysplit;   // split-K slabs [splits][tiles][BM*BN]
   int* counters;   // split-K arrival tickets [tiles], zero between launches
   double* stats;
+  // dgrad epilogue fusion of the NEXT BatchNorm backward's reductions: dX is
+  // the upstream gradient dy of the layer that produced this conv's input,
+  // so while writing the final dX tile the epilogue adds
+  //   sum(g) and sum(g * xhat),  g = dX * [y > 0],  xhat = (z - mean) * invstd
+  // into bn_acc[2][Ng] (fp64 atomics).  bn_acc == nullptr: off.
+  const uint16_t* bn_z;
+  const uint16_t* bn_y;  // nullptr: that layer has no ReLU
+  const float* bn_mean;
+  const float* bn_invstd;
+  double* bn_acc;
+  uint32_t src_bytes, wgt_bytes;  // buffer-descriptor ranges of src / wgt
   int kchunk;
   int accum;
   int c_shift, q_shift, pq_shift;
@@ -54,6 +65,17 @@ int conv_counter_slots(const ConvGeom& g, const ConvPlan& p);
 void launch_conv_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const uint16_t* src,
                       const uint16_t* wgt, uint16_t* y, float* ysplit, int* counters,
                       double* stats, bool accum, hipStream_t s);
+struct BnBwdFusion {
+  const uint16_t* z = nullptr;
+  const uint16_t* y = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  double* acc = nullptr;
+};
+// dgrad with the fused BN-backward reductions of the consumer layer
+void launch_conv_dgrad_bnb(const ConvGeom& g, const ConvPlan& p, const uint16_t* dy,
+                           const uint16_t* wgt, uint16_t* dx, float* ysplit, int* counters,
+                           bool accum, const BnBwdFusion& f, hipStream_t s);
 // dw (fp32 [Cout][R][S][Cin]); must be zeroed first when p.splits > 1.
 void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, const uint16_t* dy,
                        float* dw, hipStream_t s);

@@ -7,7 +7,7 @@
 //
 //  * Activations NHWC, weights KRSC ([Cout][R][S][Cin]) so that the GEMM
 //    reduction dimension k = (r, s, c) is contiguous in BOTH operands for the
-//    forward pass: every lane fetches 16 B (8 channels) per load, and MFMA
+//    forward pass: every lane moves 16 B (8 channels) per load, and MFMA
 //    operand fragments (8 consecutive k per lane) are read from LDS with one
 //    ds_read_b128.  Cin must be a multiple of 8 (the 3-channel CIFAR input is
 //    zero-padded to 8 channels once, at shard creation).
@@ -17,15 +17,21 @@
 //  * wgrad reduces over the N*P*Q pixels, which are strided in both operands:
 //    tiles are staged [m][col] in LDS and the MFMA fragments are formed with
 //    ds_read_b64_tr_b16 (guide T10).
-//  * Index math is kept off the VALU critical path: kernel size and stride are
-//    template parameters (constant divisions), channel / spatial divisions by
-//    powers of two become shifts (host-computed, wave-uniform).  Round-1
-//    profiling showed the generic version spending more VALU cycles on
-//    integer division than the MFMAs took.
-//  * Tiles: 256-thread workgroups (4 waves, 2x2), BK = 64, LDS rows padded to
-//    144 B so that a 16-lane ds_read_b128 group touches 16 distinct 4-bank
-//    slots (conflict-free, guide Guideline 4), register-staged double
-//    buffering with one barrier per k-step (guide T14 / "minimum 2-phase").
+//  * Operand tiles move global -> LDS with LDS-DMA buffer loads
+//    (buffer_load_dwordx4 ... lds): no VGPR staging, bounds-checked in
+//    hardware (an out-of-range offset reads zeros: padding and ragged edges
+//    cost no branch), 3 LDS stages with 2 k-tiles in flight, ONE barrier
+//    per k-step and hand-counted vmcnt waits (guide §5 'Async global->LDS
+//    copy', Three .s-level traps).  Round-1 measurements: the register-staged
+//    version was latency-bound -- hipcc drained vmcnt(0) before every LDS
+//    store, serialising the pipeline on the small-M CIFAR layers.
+//  * LDS tiles are unpadded 128/256-byte rows (a DMA instruction writes 1 KiB
+//    contiguously) with XOR swizzles chosen per read pattern so that both
+//    ds_read_b128 fragments and ds_read_b64_tr_b16 fragments are bank-
+//    conflict-free (derivation at swz_b128 / swz_tr below).
+//  * Index math stays off the VALU critical path: kernel size and stride are
+//    template parameters, channel / spatial divisions by powers of two become
+//    host-computed shifts.
 //  * Epilogue through LDS: the fp32 tile is staged in LDS and written as 16-B
 //    bf16 vectors; the per-channel BatchNorm sums of the bf16 output are
 //    reduced in the same pass and added with fp64 atomics into a [2][C]
@@ -41,9 +47,12 @@
 
 namespace mfl {
 
-constexpr int kBK = 64;
-constexpr int kPad = 8;                 // elements of row padding (16 B)
-constexpr int kLdsStride = kBK + kPad;  // 72 bf16 = 144 B
+constexpr int kBK = 64;      // k-tile (elements); one 128-byte bf16 row per operand row
+#ifndef MFL_CONV_STAGES
+#define MFL_CONV_STAGES 3  // measured: 4 stages (3 tiles in flight) is 4% slower end to end
+#endif
+constexpr int kStages = MFL_CONV_STAGES;  // LDS ring: tile kt computing, the next kStages-1 landing
+static_assert(kStages >= 2 && kStages <= 4, "dma_k_loop counts at most 3 tiles in flight");
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -51,12 +60,84 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
 
 __device__ __forceinline__ int sdiv(int x, int d, int shift) { return shift >= 0 ? x >> shift : x / d; }
 
+// ---- buffer descriptors / LDS-DMA --------------------------------------------
+constexpr uint32_t kOOB = 0xFFFFFFF0u;  // offset past every range: reads zeros
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+typedef __attribute__((address_space(3))) void lds_void;
+// 16 bytes per lane from `rsrc + off` into LDS at lds_base + 16 * lane
+// (lds_base wave-uniform).  Counted by vmcnt, invisible to hipcc's ds waits.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint8_t* lds_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_base, 16, (int)off, 0, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ---- swizzles ------------------------------------------------------------------
+// Row-major LDS tiles, 16-byte chunks; physical chunk = logical ^ swz(row).
+// b128 fragment reads (A of fwd/dgrad, B of fwd): 16 lanes read 16 consecutive
+// rows at one logical chunk; 128-B rows -> bank slot (16 B) = 8*(row&1) +
+// phys.  swz = (row>>1)&7 makes the 16 slots distinct.
+__device__ __forceinline__ int swz_b128(int row) { return (row >> 1) & 7; }
+// ds_read_b64_tr_b16 reads: 32 lanes per LDS cycle cover rows {R..R+3,
+// R+8..R+11} (R % 4 == 0), two 16-B chunks (c0 even, c0+1) each.
+//   128-B rows (8 chunks): parity classes of rows need the 4 rows of each
+//   class to get distinct even XOR keys: swz = 2*bit1(row) + 4*bit3(row).
+//   256-B rows (16 chunks): all 8 rows share one bank window: swz =
+//   2*(row&3) + 8*bit3(row).
+template <int ROWB>
+__device__ __forceinline__ int swz_tr(int row) {
+  if constexpr (ROWB == 128) return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2);
+  else return ((row & 3) << 1) | (((row >> 3) & 1) << 3);
+}
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+// MFMA B/A fragment from a [k][col] tile via transposing reads: lane gets
+// column (col0 + lane%16), k = 8*(lane/16) + 0..7 of the 32-k slice at kk.
+template <int ROWB>
+__device__ __forceinline__ bf16x8 tr_frag(const uint8_t* tile, int kk, int col0, int lane) {
+  const int grp = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  const int col = col0 + 4 * tp;
+  bf16x8 out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = kk + 8 * grp + 4 * h + tq;
+    const int off = row * ROWB + ((((col >> 3) ^ swz_tr<ROWB>(row))) << 4) + ((col & 4) << 1);
+    const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(tile + off));
+    out[4 * h + 0] = v[0];
+    out[4 * h + 1] = v[1];
+    out[4 * h + 2] = v[2];
+    out[4 * h + 3] = v[3];
+  }
+  return out;
+}
+// fragment from a [row][k] tile (128-B rows): lane reads row r0 + lane%16,
+// k-chunk (kk/8 + lane/16).
+__device__ __forceinline__ bf16x8 b128_frag(const uint8_t* tile, int kk, int r0, int lane) {
+  const int row = r0 + (lane & 15);
+  const int ch = (kk >> 3) + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(tile + row * 128 + ((ch ^ swz_b128(row)) << 4));
+}
+
 // Vectorised epilogue shared by the direct and the split-K paths:
 // out[row][col] = bf16(v (+ y_old)), BN sums of the rounded output.
 // `get(row_local, col_local_base, float[8])` supplies 8 consecutive fp32 values.
 template <int BM, int BN, typename Getter>
-__device__ __forceinline__ void tile_epilogue(const ConvGeom& g, int m0, int n0, uint16_t* y,
-                                              double* stats, int accum, float* red, Getter get) {
+__device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int n0, float* red, Getter get) {
+  const ConvGeom& g = a.g;
+  uint16_t* y = a.y;
+  const int accum = a.accum;
+  // per-channel sums: forward BN statistics (v, v^2) of the output, or the
+  // fused BN-backward reductions (g, g*xhat) of the consumer layer (dgrad)
+  double* stats = a.bn_acc ? a.bn_acc : a.stats;
   constexpr int CPR = BN / 8;        // 16-B column groups per row
   constexpr int RPP = 256 / CPR;     // rows per pass
   const int t = threadIdx.x;
@@ -64,12 +145,21 @@ __device__ __forceinline__ void tile_epilogue(const ConvGeom& g, int m0, int n0,
   float s[8] = {0}, q[8] = {0};
   const int col = n0 + cg * 8;
   const bool col_ok = col < g.Ng;  // Ng % 8 == 0
+  float mu[8], is[8];
+  if (a.bn_acc && col_ok) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      mu[k] = a.bn_mean[col + k];
+      is[k] = a.bn_invstd[col + k];
+    }
+  }
   for (int rl = r0; rl < BM; rl += RPP) {
     const int row = m0 + rl;
     if (row >= g.M || !col_ok) continue;
     float v[8];
     get(rl, cg * 8, v);
-    uint16_t* dst = y + (int64_t)row * g.Ng + col;
+    const int64_t off = (int64_t)row * g.Ng + col;
+    uint16_t* dst = y + off;
     if (accum) {
       float o[8];
       unpack8(*reinterpret_cast<const uint4*>(dst), o);
@@ -81,10 +171,22 @@ __device__ __forceinline__ void tile_epilogue(const ConvGeom& g, int m0, int n0,
     if (stats) {
       float f[8];
       unpack8(packed, f);
+      if (a.bn_acc) {
+        float zz[8], ym[8];
+        unpack8(*reinterpret_cast<const uint4*>(a.bn_z + off), zz);
+        if (a.bn_y) unpack8(*reinterpret_cast<const uint4*>(a.bn_y + off), ym);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        s[k] += f[k];
-        q[k] += f[k] * f[k];
+        for (int k = 0; k < 8; ++k) {
+          const float gk = (a.bn_y && !(ym[k] > 0.f)) ? 0.f : f[k];
+          s[k] += gk;
+          q[k] += gk * ((zz[k] - mu[k]) * is[k]);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          s[k] += f[k];
+          q[k] += f[k] * f[k];
+        }
       }
     }
   }
@@ -111,139 +213,137 @@ __device__ __forceinline__ void tile_epilogue(const ConvGeom& g, int m0, int n0,
   }
 }
 
+// The k-loop shared by the kernels: `issue(kt, stage)` starts the LDS-DMA of
+// k-tile kt (L instructions per thread), `compute(stage)` runs its MFMAs.
+//   iteration kt:  wait own DMA of tile kt (vmcnt: tile kt+1 may stay in
+//   flight) -> barrier (every wave's tile kt landed AND every wave finished
+//   reading stage (kt+2)%3 in iteration kt-1) -> issue tile kt+2 -> compute.
+template <int L, typename Issue, typename Compute>
+__device__ __forceinline__ void dma_k_loop(int nk, Issue& issue, Compute& compute) {
+  constexpr int D = kStages - 1;  // k-tiles in flight
+#pragma unroll
+  for (int u = 0; u < D; ++u)
+    if (u < nk) issue(u, u);
+  int stage = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // own DMA of tile kt complete; the younger in-flight tiles may stay
+    const int younger = min(D - 1, nk - 1 - kt);
+    if (younger >= 2) wait_vmcnt<2 * L>();
+    else if (younger == 1) wait_vmcnt<L>();
+    else wait_vmcnt<0>();
+    lds_barrier();
+    if (kt + D < nk) issue(kt + D, stage == 0 ? kStages - 1 : stage - 1);
+    compute(stage);
+    stage = stage == kStages - 1 ? 0 : stage + 1;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Forward / dgrad implicit GEMM:  Y[m][n] = sum_k A[m][k] * B[n][k]
 template <int BM, int BN, bool DGRAD, int KS, int ST>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
-  constexpr int ACH = BM / 32;  // A 16-B chunks per thread per k-step
-  constexpr int BCH = BN / 32;
+  constexpr int ACH = BM / 32;  // A DMA instructions per thread per k-tile
+  constexpr int BCH = BN / 32;  // B DMA instructions per thread per k-tile
   constexpr int TM = BM / 32;   // 16x16 MFMA tiles per wave along M
   constexpr int TN = BN / 32;
+  constexpr int A_BYTES = BM * 128;
+  constexpr int B_ROWB = DGRAD ? BN * 2 : 128;  // dgrad B: [64 k][BN] rows
+  constexpr int STAGE = A_BYTES + BN * 128;     // both B layouts hold BN*64 bf16
   const ConvGeom& g = a.g;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  // buffer b: A tile at smem + b*STAGE, B tile right after it.  Forward: B is
-  // [BN][BK] (k-contiguous weight rows).  dgrad: B is [BK][BN] staged from the
-  // KRSC weight (c-contiguous) and read with ds_read_b64_tr_b16.
-  constexpr int BST = BN + kPad;
-  constexpr int BTILE = DGRAD ? kBK * BST : BN * kLdsStride;
-  constexpr int STAGE = BM * kLdsStride + BTILE;
-  auto As = [&](int b) { return smem + b * STAGE; };
-  auto Bs = [&](int b) { return smem + b * STAGE + BM * kLdsStride; };
-  constexpr int BCPR = BN / 8;       // dgrad B: 16-B chunks per k-row
-  constexpr int BRPP = 256 / BCPR;   // k-rows per pass
+  const auto rsA = make_rsrc(a.src, a.src_bytes);
+  const auto rsB = make_rsrc(a.wgt, a.wgt_bytes);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int t = threadIdx.x;
   const int lane = t & 63;
-  const int wv = t >> 6;
-  const int wm = wv >> 1, wn = wv & 1;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
   const int kbeg = blockIdx.z * a.kchunk;
   const int kend = min(g.K, kbeg + a.kchunk);
   const int nk = (kend - kbeg + kBK - 1) / kBK;
-  const int dbch = t % BCPR, dbrow = t / BCPR;
-
-  const int lrow = t >> 3;   // 0..31
-  const int lch = t & 7;     // chunk within the BK=64 row
   const int HWC = g.H * g.W * g.C;
 
-  // Per-thread A rows: image base, origin coordinates.
+  // A DMA: instruction i of wave w fills rows (w + 4i)*8 .. +8 (1 KiB); lane
+  // -> row lrow + 32 i, physical chunk lane&7, logical chunk (k offset) below.
+  const int lrow = wave * 8 + (lane >> 3);
+  const int a_kc = ((lane & 7) ^ swz_b128(lrow)) * 8;  // same for every i (32i keeps bits 1-3)
   int a_nb[ACH], a_y0[ACH], a_x0[ACH];
 #pragma unroll
   for (int i = 0; i < ACH; ++i) {
     const int m = m0 + lrow + 32 * i;
-    if (m < g.M) {
-      const int n = sdiv(m, g.P * g.Q, a.pq_shift);
-      const int rem = m - n * g.P * g.Q;
-      const int oy = sdiv(rem, g.Q, a.q_shift);
-      const int ox = rem - oy * g.Q;
-      a_nb[i] = n * HWC;
-      if (DGRAD) {
-        a_y0[i] = oy + g.pad;
-        a_x0[i] = ox + g.pad;
-      } else {
-        a_y0[i] = oy * ST - g.pad;
-        a_x0[i] = ox * ST - g.pad;
-      }
+    const int mm = m < g.M ? m : 0;
+    const int n = sdiv(mm, g.P * g.Q, a.pq_shift);
+    const int rem = mm - n * g.P * g.Q;
+    const int oy = sdiv(rem, g.Q, a.q_shift);
+    const int ox = rem - oy * g.Q;
+    a_nb[i] = n * HWC;
+    if (DGRAD) {
+      a_y0[i] = oy + g.pad;
+      a_x0[i] = ox + g.pad;
     } else {
-      a_nb[i] = 0;
-      a_y0[i] = -(1 << 28);
-      a_x0[i] = -(1 << 28);
+      a_y0[i] = oy * ST - g.pad;
+      a_x0[i] = ox * ST - g.pad;
     }
+    if (m >= g.M) a_y0[i] = -(1 << 28);  // forces the OOB offset
   }
+  // B DMA mapping.  fwd: rows n (128 B = 64 k), same as A.  dgrad: rows k of
+  // B_ROWB bytes; instruction i of wave w fills bytes (w + 4i) KiB.
+  constexpr int B_RPI = 1024 / B_ROWB;  // rows per DMA instruction
+  constexpr int B_CPR = B_ROWB / 16;    // chunks per row
+  const int b_row0 = wave * B_RPI + lane / B_CPR;   // + 4*B_RPI*i
+  const int b_pch = lane % B_CPR;
 
-  uint4 ra[ACH], rb[BCH];
-  auto load_tile = [&](int kt) {
-    const int k = kbeg + kt * kBK + lch * 8;
-    const bool kv = k < kend;
-    int r = 0, s = 0, c = 0;
-    if (kv) {
+  auto issue = [&](int kt, int stage) {
+    uint8_t* st = smem + stage * STAGE;
+    const int kb = kbeg + kt * kBK;
+    {
+      const int k = kb + a_kc;
       const int rs = sdiv(k, g.C, a.c_shift);
-      c = k - rs * g.C;
-      r = rs / KS;
-      s = rs - r * KS;
-    }
+      const int c = k - rs * g.C;
+      const int r = rs / KS;
+      const int s = rs - r * KS;
+      const bool kv = k < kend;
 #pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      int iy, ix;
-      bool ok = kv;
-      if (DGRAD) {
-        const int ty = a_y0[i] - r, tx = a_x0[i] - s;
-        ok = ok && ty >= 0 && tx >= 0;
-        if (ST > 1) ok = ok && (ty % ST == 0) && (tx % ST == 0);
-        iy = ty / ST;
-        ix = tx / ST;
-      } else {
-        iy = a_y0[i] + r;
-        ix = a_x0[i] + s;
-        ok = ok && iy >= 0 && ix >= 0;
-      }
-      ok = ok && iy < g.H && ix < g.W;
-      if (ok)
-        ra[i] = *reinterpret_cast<const uint4*>(a.src + a_nb[i] + (iy * g.W + ix) * g.C + c);
-      else
-        ra[i] = make_uint4(0, 0, 0, 0);
-    }
-    if constexpr (DGRAD) {
-      // B[k][n] = W[ko][r][s][n], k = (r, s, ko): rows of the tile are k
-#pragma unroll
-      for (int i = 0; i < BCH; ++i) {
-        const int kr = kbeg + kt * kBK + dbrow + BRPP * i;
-        const int n = n0 + dbch * 8;
-        if (kr < kend && n < g.Ng) {
-          const int rs = sdiv(kr, g.C, a.c_shift);
-          const int ko = kr - rs * g.C;
-          rb[i] = *reinterpret_cast<const uint4*>(a.wgt + ((int64_t)ko * KS * KS + rs) * g.Ng + n);
+      for (int i = 0; i < ACH; ++i) {
+        int iy, ix;
+        bool ok;
+        if (DGRAD) {
+          const int ty = a_y0[i] - r, tx = a_x0[i] - s;
+          ok = kv & (ty >= 0) & (tx >= 0);
+          if (ST > 1) ok = ok & ((ty % ST) == 0) & ((tx % ST) == 0);
+          iy = ty / ST;
+          ix = tx / ST;
         } else {
-          rb[i] = make_uint4(0, 0, 0, 0);
+          iy = a_y0[i] + r;
+          ix = a_x0[i] + s;
+          ok = kv & (iy >= 0) & (ix >= 0);
         }
+        ok = ok & (iy < g.H) & (ix < g.W);
+        const uint32_t off = ok ? (uint32_t)(a_nb[i] + (iy * g.W + ix) * g.C + c) * 2u : kOOB;
+        dma16(rsA, off, st + (wave + 4 * i) * 1024);
       }
-    } else {
+    }
 #pragma unroll
-      for (int i = 0; i < BCH; ++i) {
+    for (int i = 0; i < BCH; ++i) {
+      uint32_t off;
+      if constexpr (DGRAD) {
+        // B[k][n] = W[ko][r][s][n], k = (r, s, ko)
+        const int row = b_row0 + 4 * B_RPI * i;          // k row within the tile
+        const int n = n0 + ((b_pch ^ swz_tr<B_ROWB>(row)) * 8);
+        const int kr = kb + row;
+        const int rs = sdiv(kr, g.C, a.c_shift);
+        const int ko = kr - rs * g.C;
+        off = ((kr < kend) & (n < g.Ng)) ? (uint32_t)((ko * KS * KS + rs) * g.Ng + n) * 2u : kOOB;
+      } else {
         const int n = n0 + lrow + 32 * i;
-        if (kv && n < g.Ng)
-          rb[i] = *reinterpret_cast<const uint4*>(a.wgt + (int64_t)n * g.K + k);
-        else
-          rb[i] = make_uint4(0, 0, 0, 0);
+        const int k = kb + a_kc;
+        off = ((k < kend) & (n < g.Ng)) ? (uint32_t)(n * g.K + k) * 2u : kOOB;
       }
+      dma16(rsB, off, st + A_BYTES + (wave + 4 * i) * 1024);
     }
   };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < ACH; ++i)
-      *reinterpret_cast<uint4*>(As(buf) + (lrow + 32 * i) * kLdsStride + lch * 8) = ra[i];
-    if constexpr (DGRAD) {
-#pragma unroll
-      for (int i = 0; i < BCH; ++i)
-        *reinterpret_cast<uint4*>(Bs(buf) + (dbrow + BRPP * i) * BST + dbch * 8) = rb[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < BCH; ++i)
-        *reinterpret_cast<uint4*>(Bs(buf) + (lrow + 32 * i) * kLdsStride + lch * 8) = rb[i];
-    }
-  };
-  typedef short v4s __attribute__((ext_vector_type(4)));
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -251,56 +351,32 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    load_tile(0);
-    store_tile(0);
-  }
-  __syncthreads();
-  const int fr = lane & 15;
-  const int fk = (lane >> 4) * 8;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
+  auto compute = [&](int stage) {
+    const uint8_t* As = smem + stage * STAGE;
+    const uint8_t* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < kBK; kk += 32) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As(cur) + (wm * (BM / 2) + 16 * i + fr) * kLdsStride + kk + fk);
-      if constexpr (DGRAD) {
-        const int grp = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+      for (int i = 0; i < TM; ++i) af[i] = b128_frag(As, kk, wm * (BM / 2) + 16 * i, lane);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = wn * (BN / 2) + 16 * j + 4 * tp;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int row = kk + 8 * grp + 4 * h + tq;
-            const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) v4s*)(Bs(cur) + row * BST + col));
-            bfr[j][4 * h + 0] = v[0];
-            bfr[j][4 * h + 1] = v[1];
-            bfr[j][4 * h + 2] = v[2];
-            bfr[j][4 * h + 3] = v[3];
-          }
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs(cur) + (wn * (BN / 2) + 16 * j + fr) * kLdsStride + kk + fk);
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (DGRAD) bfr[j] = tr_frag<B_ROWB>(Bs, kk, wn * (BN / 2) + 16 * j, lane);
+        else bfr[j] = b128_frag(Bs, kk, wn * (BN / 2) + 16 * j, lane);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    if (kt + 1 < nk) store_tile(cur ^ 1);
-    __syncthreads();
-  }
+  };
+  dma_k_loop<ACH + BCH>(nk, issue, compute);
+  __syncthreads();  // every wave done with the ring before smem is reused
 
   // ---- epilogue -----------------------------------------------------------
-  // fp32 tile in LDS: [BM][BN + 4] (the loop's final barrier freed smem)
   constexpr int TST = BN + 4;
   float* tile = reinterpret_cast<float*>(smem);
+  const int fr = lane & 15;
   const int rl0 = wm * (BM / 2) + (lane >> 4) * 4;
   const int cl0 = wn * (BN / 2) + fr;
   const int splits = gridDim.z;
@@ -313,7 +389,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) tile[(rl0 + 16 * i + e) * TST + cl0 + 16 * j] = acc[i][j][e];
     __syncthreads();
-    tile_epilogue<BM, BN>(g, m0, n0, a.y, a.stats, a.accum, tile + BM * TST,
+    tile_epilogue<BM, BN>(a, m0, n0, tile + BM * TST,
                           [&](int rl, int cl, float* v) {
                             const float4 p = *reinterpret_cast<const float4*>(tile + rl * TST + cl);
                             const float4 q = *reinterpret_cast<const float4*>(tile + rl * TST + cl + 4);
@@ -354,7 +430,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   if (!flag[0]) return;
   const float* base = a.ysplit + (int64_t)tile_id * (BM * BN);
   const int64_t zstride = (int64_t)ntiles * BM * BN;
-  tile_epilogue<BM, BN>(g, m0, n0, a.y, a.stats, a.accum, reinterpret_cast<float*>(smem) + 4,
+  tile_epilogue<BM, BN>(a, m0, n0, reinterpret_cast<float*>(smem) + 4,
                         [&](int rl, int cl, float* v) {
                           for (int k = 0; k < 8; ++k) v[k] = 0.f;
                           for (int z = 0; z < splits; ++z) {
@@ -369,166 +445,104 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 
 // ---------------------------------------------------------------------------
 // wgrad:  dW[ko][j] = sum_m dY[m][ko] * im2col(X)[m][j],  j = (r, s, c)
-template <int BM, int BN, int KS, int ST>
+// Tiles: A = dY [64 m][64 ko], B = im2col(X) [64 m][64 j], both 128-B rows,
+// both read with transposing LDS reads.
+template <int KS, int ST>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __restrict__ dw) {
   // g: H,W,C = X dims; P,Q = dY spatial; Ng = Cout; K = R*S*C; M = N*P*Q
-  constexpr int TM = BM / 32;
-  constexpr int TN = BN / 32;
-  constexpr int AST = BM + kPad;
-  constexpr int BST = BN + kPad;
+  constexpr int BM = 64, BN = 64;
+  constexpr int TM = 2, TN = 2;
+  constexpr int T_BYTES = 64 * 128;
+  constexpr int STAGE = 2 * T_BYTES;
   const ConvGeom& g = a.g;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr int STAGE = kBK * (AST + BST);
-  auto As = [&](int b) { return smem + b * STAGE; };
-  auto Bs = [&](int b) { return smem + b * STAGE + kBK * AST; };
+  const auto rsA = make_rsrc(a.src, a.src_bytes);
+  const auto rsB = make_rsrc(a.wgt, a.wgt_bytes);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int t = threadIdx.x;
   const int lane = t & 63;
-  const int wv = t >> 6;
-  const int wm = wv >> 1, wn = wv & 1;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
   const int ko0 = blockIdx.x * BM;
   const int j0 = blockIdx.y * BN;
   const int mbeg = blockIdx.z * a.kchunk;
   const int mend = min(g.M, mbeg + a.kchunk);
   const int nk = (mend - mbeg + kBK - 1) / kBK;
 
-  // A [64 m][BM] and B [64 m][BN] tiles: each thread owns one fixed 16-B
-  // column chunk and rows row + RPP*i; the im2col decomposition (r, s, c) of
-  // the B column chunk is fixed for the whole k-loop.
-  constexpr int BCPR = BN / 8;
-  constexpr int BRPP = 256 / BCPR;
-  constexpr int BREP = kBK / BRPP;
-  constexpr int ACPR = BM / 8;
-  constexpr int ARPP = 256 / ACPR;
-  constexpr int AREP = kBK / ARPP;
-  static_assert(BREP * BRPP == kBK && AREP * ARPP == kBK, "tile mapping");
-  const int bch = t % BCPR, brow = t / BCPR;
-  const int ach = t % ACPR, arow = t / ACPR;
-  int b_r, b_s, b_c;
-  bool b_ok;
-  {
-    const int j = j0 + bch * 8;
-    b_ok = j < g.K;
-    const int rs = b_ok ? sdiv(j, g.C, a.c_shift) : 0;
-    b_c = b_ok ? j - rs * g.C : 0;
-    b_r = rs / KS;
-    b_s = rs - b_r * KS;
-  }
+  // DMA mapping (both operands): instruction i of wave w fills m-rows
+  // (w + 4i)*8 .. +8; lane -> row lrow + 32 i, physical chunk lane&7.
+  const int lrow = wave * 8 + (lane >> 3);
+  const int pch = lane & 7;
+  // The swizzle key of row lrow + 32i equals that of lrow (bits 1 and 3).
+  const int col = (pch ^ swz_tr<128>(lrow)) * 8;  // column offset inside the tile
+  const int ko = ko0 + col;
+  const int j = j0 + col;
+  const bool j_ok = j < g.K;
+  const int rsj = sdiv(j_ok ? j : 0, g.C, a.c_shift);
+  const int b_c = (j_ok ? j : 0) - rsj * g.C;
+  const int b_r = rsj / KS;
+  const int b_s = rsj - b_r * KS;
   const int HWC = g.H * g.W * g.C;
   const int PQ = g.P * g.Q;
-  uint4 ra[AREP], rb[BREP];
-  auto load_tile = [&](int kt) {
+
+  auto issue = [&](int kt, int stage) {
+    uint8_t* st = smem + stage * STAGE;
     const int mb = mbeg + kt * kBK;
 #pragma unroll
-    for (int i = 0; i < AREP; ++i) {
-      const int m = mb + arow + ARPP * i;
-      const int ko = ko0 + ach * 8;
-      if (m < mend && ko < g.Ng)
-        ra[i] = *reinterpret_cast<const uint4*>(a.src + (int64_t)m * g.Ng + ko);  // src = dY
-      else
-        ra[i] = make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < 2; ++i) {
+      const int m = mb + lrow + 32 * i;
+      const bool mv = m < mend;
+      dma16(rsA, (mv & (ko < g.Ng)) ? (uint32_t)(m * g.Ng + ko) * 2u : kOOB, st + (wave + 4 * i) * 1024);
+      const int n = sdiv(m, PQ, a.pq_shift);
+      const int rem = m - n * PQ;
+      const int oy = sdiv(rem, g.Q, a.q_shift);
+      const int ox = rem - oy * g.Q;
+      const int iy = oy * ST - g.pad + b_r;
+      const int ix = ox * ST - g.pad + b_s;
+      const bool ok = j_ok & mv & (iy >= 0) & (ix >= 0) & (iy < g.H) & (ix < g.W);
+      dma16(rsB, ok ? (uint32_t)(n * HWC + (iy * g.W + ix) * g.C + b_c) * 2u : kOOB,
+            st + T_BYTES + (wave + 4 * i) * 1024);
     }
-#pragma unroll
-    for (int i = 0; i < BREP; ++i) {
-      const int m = mb + brow + BRPP * i;
-      bool ok = b_ok && m < mend;
-      int n = 0, iy = 0, ix = 0;
-      if (ok) {
-        n = sdiv(m, PQ, a.pq_shift);
-        const int rem = m - n * PQ;
-        const int oy = sdiv(rem, g.Q, a.q_shift);
-        const int ox = rem - oy * g.Q;
-        iy = oy * ST - g.pad + b_r;
-        ix = ox * ST - g.pad + b_s;
-        ok = iy >= 0 && ix >= 0 && iy < g.H && ix < g.W;
-      }
-      if (ok)
-        rb[i] = *reinterpret_cast<const uint4*>(a.wgt + (int64_t)n * HWC + (iy * g.W + ix) * g.C + b_c);  // wgt = X
-      else
-        rb[i] = make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < AREP; ++i)
-      *reinterpret_cast<uint4*>(As(buf) + (arow + ARPP * i) * AST + ach * 8) = ra[i];
-#pragma unroll
-    for (int i = 0; i < BREP; ++i)
-      *reinterpret_cast<uint4*>(Bs(buf) + (brow + BRPP * i) * BST + bch * 8) = rb[i];
   };
 
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (nk > 0) {
-    load_tile(0);
-    store_tile(0);
-  }
-  __syncthreads();
-  const int grp = lane >> 4;  // 0..3 -> k = 8*grp + e
-  const int li = lane & 15;
-  const int tq = li >> 2, tp = li & 3;
-  typedef short v4s __attribute__((ext_vector_type(4)));
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
+    for (int jj = 0; jj < TN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int stage) {
+    const uint8_t* As = smem + stage * STAGE;
+    const uint8_t* Bs = As + T_BYTES;
 #pragma unroll
     for (int kk = 0; kk < kBK; kk += 32) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int col = wm * (BM / 2) + 16 * i + 4 * tp;
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag<128>(As, kk, wm * (BM / 2) + 16 * i, lane);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int row = kk + 8 * grp + 4 * h + tq;
-          const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) v4s*)(As(cur) + row * AST + col));
-          af[i][4 * h + 0] = v[0];
-          af[i][4 * h + 1] = v[1];
-          af[i][4 * h + 2] = v[2];
-          af[i][4 * h + 3] = v[3];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = wn * (BN / 2) + 16 * j + 4 * tp;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int row = kk + 8 * grp + 4 * h + tq;
-          const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) v4s*)(Bs(cur) + row * BST + col));
-          bfr[j][4 * h + 0] = v[0];
-          bfr[j][4 * h + 1] = v[1];
-          bfr[j][4 * h + 2] = v[2];
-          bfr[j][4 * h + 3] = v[3];
-        }
-      }
+      for (int jj = 0; jj < TN; ++jj) bfr[jj] = tr_frag<128>(Bs, kk, wn * (BN / 2) + 16 * jj, lane);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        for (int jj = 0; jj < TN; ++jj) acc[i][jj] = mfma16(af[i], bfr[jj], acc[i][jj]);
     }
-    if (kt + 1 < nk) store_tile(cur ^ 1);
-    __syncthreads();
-  }
+  };
+  dma_k_loop<4>(nk, issue, compute);
+
   const bool atomic = gridDim.z > 1;  // split-K slices add into the zeroed slot
   const int rbase = ko0 + wm * (BM / 2) + (lane >> 4) * 4;
-  const int cbase = j0 + wn * (BN / 2) + li;
+  const int cbase = j0 + wn * (BN / 2) + (lane & 15);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int jj = 0; jj < TN; ++jj)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int row = rbase + 16 * i + e, col = cbase + 16 * j;
-        if (row < g.Ng && col < g.K) {
+        const int row = rbase + 16 * i + e, cc = cbase + 16 * jj;
+        if (row < g.Ng && cc < g.K) {
           if (atomic)
-            atomicAdd(&dw[(int64_t)row * g.K + col], acc[i][j][e]);
+            atomicAdd(&dw[(int64_t)row * g.K + cc], acc[i][jj][e]);
           else
-            dw[(int64_t)row * g.K + col] = acc[i][j][e];
+            dw[(int64_t)row * g.K + cc] = acc[i][jj][e];
         }
       }
 }
@@ -556,25 +570,36 @@ static int log2_exact(int v) {
   return s;
 }
 
+// bf16 element count -> buffer range in bytes (32-bit descriptor range; the
+// bindings reject tensors this large before launch)
+static uint32_t range_bytes(int64_t elems) {
+  const int64_t b = elems * 2;
+  return b >= (int64_t)kOOB ? kOOB : (uint32_t)b;
+}
+
 static void fill_shifts(ConvArgs& a) {
   a.c_shift = log2_exact(a.g.C);
   a.q_shift = log2_exact(a.g.Q);
   a.pq_shift = log2_exact(a.g.P * a.g.Q);
 }
 
+template <typename K>
+static void set_lds_limit(K* kernel, size_t lds, bool& done) {
+  if (!done && lds > 65536) {  // > 64 KiB of dynamic LDS must be opted into
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    done = true;
+  }
+}
+
 template <int BM, int BN, bool DG, int KS, int ST>
 static void launch_gemm_t(const ConvArgs& a, const ConvPlan& p, hipStream_t s) {
   dim3 grid((a.g.M + BM - 1) / BM, (a.g.Ng + BN - 1) / BN, p.splits);
-  const size_t btile = DG ? (size_t)kBK * (BN + kPad) : (size_t)BN * kLdsStride;
-  size_t lds = (size_t)2 * ((size_t)BM * kLdsStride + btile) * sizeof(uint16_t);
+  size_t lds = (size_t)kStages * (BM * 128 + BN * 128);
   const size_t epi = ((size_t)BM * (BN + 4) + 256 * 16 + 8) * sizeof(float);
   if (lds < epi) lds = epi;
-  static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into
-  if (!attr_set && lds > 65536) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, DG, KS, ST>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
+  static bool attr_set = false;
+  set_lds_limit(&conv_gemm_kernel<BM, BN, DG, KS, ST>, lds, attr_set);
   conv_gemm_kernel<BM, BN, DG, KS, ST><<<grid, 256, lds, s>>>(a);
 }
 
@@ -591,14 +616,27 @@ bool conv_supported(const ConvGeom& g) {
   return g.R == g.S && (g.R == 1 || g.R == 3) && (g.stride == 1 || g.stride == 2);
 }
 
+// Split-K policy.  A block's k-loop is a serial chain of ~latency/2 per
+// k-step (two tiles in flight, almost no MFMA work per step at CIFAR sizes),
+// so the plan trades k-steps per block for blocks: split until the grid
+// reaches `target` workgroups (several per CU to overlap their chains) while
+// every slice keeps >= `min_steps` k-steps.  Tunable for sweeps through
+// MFL_CONV_TARGET_BLOCKS / MFL_CONV_MIN_KSTEPS / MFL_WGRAD_TARGET_BLOCKS.
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
 ConvPlan plan_conv_gemm(const ConvGeom& g) {
+  static const int target = env_int("MFL_CONV_TARGET_BLOCKS", 256);
+  static const int min_steps = env_int("MFL_CONV_MIN_KSTEPS", 4);
   ConvPlan p;
   p.bm = g.M >= 8192 ? 128 : 64;
   p.bn = g.Ng >= 128 && g.M >= 16384 ? 128 : 64;
   const int tiles = ((g.M + p.bm - 1) / p.bm) * ((g.Ng + p.bn - 1) / p.bn);
   const int ksteps = (g.K + kBK - 1) / kBK;
   int splits = 1;
-  while (tiles * splits < 256 && ksteps / (splits * 2) >= 4 && splits < 16) splits *= 2;
+  while (tiles * splits < target && ksteps / (splits * 2) >= min_steps && splits < 16) splits *= 2;
   p.splits = splits;
   p.kchunk = ((ksteps + splits - 1) / splits) * kBK;
   p.stats_rows = 1;
@@ -616,6 +654,8 @@ void launch_conv_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const ui
   a.g = g;
   a.src = src;
   a.wgt = wgt;
+  a.src_bytes = range_bytes((int64_t)g.N * g.H * g.W * g.C);
+  a.wgt_bytes = range_bytes((int64_t)g.Ng * g.K);
   a.y = y;
   a.ysplit = ysplit;
   a.counters = counters;
@@ -634,14 +674,41 @@ void launch_conv_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const ui
 #undef MFL_CONV_CASE
 }
 
+void launch_conv_dgrad_bnb(const ConvGeom& g, const ConvPlan& p, const uint16_t* dy,
+                           const uint16_t* wgt, uint16_t* dx, float* ysplit, int* counters,
+                           bool accum, const BnBwdFusion& f, hipStream_t s) {
+  ConvArgs a{};
+  a.g = g;
+  a.src = dy;
+  a.wgt = wgt;
+  a.src_bytes = range_bytes((int64_t)g.N * g.H * g.W * g.C);
+  a.wgt_bytes = range_bytes((int64_t)g.Ng * g.K);
+  a.y = dx;
+  a.ysplit = ysplit;
+  a.counters = counters;
+  a.kchunk = p.kchunk;
+  a.accum = accum ? 1 : 0;
+  a.bn_z = f.z;
+  a.bn_y = f.y;
+  a.bn_mean = f.mean;
+  a.bn_invstd = f.invstd;
+  a.bn_acc = f.acc;
+  fill_shifts(a);
+  if (p.bm == 128 && p.bn == 128) launch_gemm_ks<128, 128, true>(a, p, s);
+  else if (p.bm == 128 && p.bn == 64) launch_gemm_ks<128, 64, true>(a, p, s);
+  else if (p.bm == 64 && p.bn == 64) launch_gemm_ks<64, 64, true>(a, p, s);
+}
+
 ConvPlan plan_conv_wgrad(const ConvGeom& g) {
+  static const int target = env_int("MFL_WGRAD_TARGET_BLOCKS", 512);
+  static const int min_steps = env_int("MFL_WGRAD_MIN_KSTEPS", 8);
   ConvPlan p;
   p.bm = 64;
   p.bn = 64;
   const int tiles = ((g.Ng + 63) / 64) * ((g.K + 63) / 64);
   const int ksteps = (g.M + kBK - 1) / kBK;
   int splits = 1;
-  while (tiles * splits < 512 && ksteps / (splits * 2) >= 8 && splits < 64) splits *= 2;
+  while (tiles * splits < target && ksteps / (splits * 2) >= min_steps && splits < 64) splits *= 2;
   p.splits = splits;
   p.kchunk = ((ksteps + splits - 1) / splits) * kBK;
   p.stats_rows = 0;
@@ -657,15 +724,17 @@ void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, 
   a.g = g;
   a.src = dy;
   a.wgt = x;
+  a.src_bytes = range_bytes((int64_t)g.M * g.Ng);
+  a.wgt_bytes = range_bytes((int64_t)g.N * g.H * g.W * g.C);
   a.kchunk = p.kchunk;
   fill_shifts(a);
   dim3 grid((g.Ng + 63) / 64, (g.K + 63) / 64, p.splits);
-  const size_t lds = (size_t)2 * kBK * ((64 + kPad) + (64 + kPad)) * sizeof(uint16_t);
+  const size_t lds = (size_t)kStages * 2 * 64 * 128;  // 48 KiB
   const int ks = g.R, st = g.stride;
-  if (ks == 3 && st == 1) conv_wgrad_kernel<64, 64, 3, 1><<<grid, 256, lds, s>>>(a, dw);
-  else if (ks == 3 && st == 2) conv_wgrad_kernel<64, 64, 3, 2><<<grid, 256, lds, s>>>(a, dw);
-  else if (ks == 1 && st == 1) conv_wgrad_kernel<64, 64, 1, 1><<<grid, 256, lds, s>>>(a, dw);
-  else if (ks == 1 && st == 2) conv_wgrad_kernel<64, 64, 1, 2><<<grid, 256, lds, s>>>(a, dw);
+  if (ks == 3 && st == 1) conv_wgrad_kernel<3, 1><<<grid, 256, lds, s>>>(a, dw);
+  else if (ks == 3 && st == 2) conv_wgrad_kernel<3, 2><<<grid, 256, lds, s>>>(a, dw);
+  else if (ks == 1 && st == 1) conv_wgrad_kernel<1, 1><<<grid, 256, lds, s>>>(a, dw);
+  else if (ks == 1 && st == 2) conv_wgrad_kernel<1, 2><<<grid, 256, lds, s>>>(a, dw);
 }
 
 void launch_transpose_krsc(const uint16_t* w, uint16_t* wt, int Co, int RS, int Ci, hipStream_t s) {

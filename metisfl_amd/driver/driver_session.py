@@ -61,7 +61,7 @@ class DriverSessionBase:
 
     def __init__(self, fed_env, model, train_dataset_recipe_fn, validation_dataset_recipe_fn=None,
                  test_dataset_recipe_fn=None, working_dir: str = "/tmp/metis_amd/", device: str | None = None,
-                 seed: int = 0):
+                 seed: int = 0, fake_train_delay: float = 0.0):
         MetisASCIIArt.print()
         self.federation_environment = fed_env if isinstance(fed_env, fedenv_parser.FederationEnvironment) \
             else fedenv_parser.FederationEnvironment(fed_env)
@@ -73,6 +73,7 @@ class DriverSessionBase:
         os.makedirs(working_dir)
         self.device = device
         self.seed = seed
+        self.fake_train_delay = fake_train_delay  # echo learners only
         self._model_dir = os.path.join(working_dir, "model_definition")
         self.neural_engine = self._save_model(model)
         if train_dataset_recipe_fn is None:
@@ -194,7 +195,7 @@ class DriverSessionBase:
             self.train_dataset_recipe_fp, self.validation_dataset_recipe_fp, self.test_dataset_recipe_fp,
             neural_engine=self.neural_engine, device=dev,
             credentials_dir=os.path.join(self.working_dir, f"learner_{learner_instance.grpc_servicer.port}_credentials"),
-            seed=self.seed)
+            seed=self.seed, fake_train_delay=self.fake_train_delay)
 
     # -- process control -----------------------------------------------------------------------
     def _spawn(self, name, cmd, env_extra=None, remote=None):

@@ -162,21 +162,32 @@ class ConvBN(Layer):
                    self.momentum, self.eps)
         return self.y
 
+    def bn_target(self) -> K.BnBwdTarget:
+        """This layer's BN backward as the fused-reduction target of the dgrad
+        that produces its upstream gradient."""
+        return K.BnBwdTarget(self.z, self.y if self.relu else None, self.mean, self.invstd,
+                             self.ws.acc(self.acc_b))
+
     def backward(self, dy: torch.Tensor, dx: torch.Tensor | None, accumulate: bool = False,
-                 dres: torch.Tensor | None = None) -> None:
+                 dres: torch.Tensor | None = None, presummed: bool = False,
+                 bnb: K.BnBwdTarget | None = None) -> None:
         """dy: gradient w.r.t. this layer's output.  Writes dgamma/dbeta/dW into
         the flat gradient buffer and (if dx is given) d input into dx; ``dres``
-        receives the ReLU-masked dy that the residual branch needs."""
+        receives the ReLU-masked dy that the residual branch needs.
+        ``presummed``: dy's producer already accumulated this BN's backward
+        reductions; ``bnb``: the BN whose upstream gradient ``dx`` is (its
+        reductions are fused into this layer's dgrad epilogue)."""
         s = self.shp
         K.bn_backward(dy, self.z, self.y if self.relu else None, s.Co, self.gamma, self.mean,
-                      self.invstd, self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz, dres)
+                      self.invstd, self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz, dres,
+                      presummed=presummed)
         # weight gradient: off the critical path -> side stream (joined before
         # the optimizer); the gradient buffer is zero on entry (re-zeroed by
         # the optimizer launch), so split-K slices accumulate atomically
         with self.ws.fork():
             K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True)
         if dx is not None:
-            K.conv_dgrad(self.dz, self.w16, dx, s, self._split(), accumulate)
+            K.conv_dgrad(self.dz, self.w16, dx, s, self._split(), accumulate, bnb=bnb)
 
 
 class BasicBlock(Layer):
@@ -224,16 +235,19 @@ class BasicBlock(Layer):
         self.c1.ws.join()
         return self.c2.forward(a, residual=r, train=train)
 
-    def backward(self, dout, dx):
+    def backward(self, dout, dx, presummed: bool = False, prev: K.BnBwdTarget | None = None):
+        """``presummed``: conv2's BN reductions were fused into dout's producer;
+        ``prev``: the BN consuming dx (the previous block's conv2 or the stem),
+        whose reductions are fused into the LAST dgrad writing dx (conv1's)."""
         if self.sc is None:
             # identity shortcut: masked dout goes straight into dx, conv1's
             # dgrad then accumulates onto it (no add kernel)
-            self.c2.backward(dout, self.da, dres=dx)
-            self.c1.backward(self.da, dx, accumulate=True)
+            self.c2.backward(dout, self.da, dres=dx, presummed=presummed, bnb=self.c1.bn_target())
+            self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev)
         else:
-            self.c2.backward(dout, self.da, dres=self.dres)
+            self.c2.backward(dout, self.da, dres=self.dres, presummed=presummed, bnb=self.c1.bn_target())
             self.sc.backward(self.dres, dx)
-            self.c1.backward(self.da, dx, accumulate=True)
+            self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev)
 
 
 class ClassifierHead(Layer):

@@ -62,8 +62,14 @@ class ResNet18(StaticNet):
         return h
 
     def backward(self, dlast):
+        # BN-backward reductions ride in the dgrad epilogues: every block's
+        # conv1 dgrad (the last writer of the block's input gradient) sums for
+        # the BN that consumes it -- the previous block's conv2, or the stem.
+        # Only the last block's conv2 (fed by the head) reduces on its own.
         d = dlast.view(self.blocks[-1].out_shape)
         for i in range(len(self.blocks) - 1, -1, -1):
-            self.blocks[i].backward(d, self.dacts[i])
+            prev = self.blocks[i - 1].c2 if i > 0 else self.stem
+            self.blocks[i].backward(d, self.dacts[i], presummed=i < len(self.blocks) - 1,
+                                    prev=prev.bn_target())
             d = self.dacts[i]
-        self.stem.backward(d, None)
+        self.stem.backward(d, None, presummed=True)

@@ -95,12 +95,47 @@ def conv_forward(x, w, y, shp: ConvShape, ws=None, stats=None) -> None:
         _acc_stats_cpu(y, stats)
 
 
-def conv_dgrad(dy, w, dx, shp: ConvShape, ws=None, accumulate: bool = False) -> None:
+@dataclass
+class BnBwdTarget:
+    """The BatchNorm whose upstream gradient a dgrad produces: the dgrad
+    epilogue adds that BN-backward's reductions (sum g, sum g*xhat;
+    g = dx * [y > 0]) into ``acc`` while writing dx, so the BN backward runs
+    with ``presummed=True`` (one launch fewer per layer)."""
+    z: torch.Tensor
+    y: torch.Tensor | None
+    mean: torch.Tensor
+    invstd: torch.Tensor
+    acc: torch.Tensor
+
+
+def _bnb_sums_cpu(dx: torch.Tensor, t: BnBwdTarget) -> None:
+    C = dx.shape[-1]
+    g = dx.float().reshape(-1, C)
+    if t.y is not None:
+        g = torch.where(t.y.float().reshape(-1, C) > 0, g, torch.zeros_like(g))
+    xh = (t.z.float().reshape(-1, C) - t.mean) * t.invstd
+    t.acc[:C] += g.double().sum(0)
+    t.acc[C:2 * C] += (g.double() * xh.double()).sum(0)
+
+
+def conv_dgrad(dy, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
+               bnb: BnBwdTarget | None = None) -> None:
     """dx (+)= conv_transpose(dy, W); ``w`` is the KRSC weight [Cout][R][S][Cin]
-    (the kernel forms W^T fragments with transposing LDS reads)."""
+    (the kernel forms W^T fragments with transposing LDS reads).  ``bnb``:
+    fuse the consumer BatchNorm-backward reductions into the epilogue."""
     if dy.is_cuda:
-        ops().conv_dgrad(dy, w, dx, ws, *shp.args(), accumulate)
+        if bnb is None:
+            ops().conv_dgrad(dy, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None)
+        else:
+            ops().conv_dgrad(dy, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean, bnb.invstd,
+                             bnb.acc)
         return
+    _conv_dgrad_cpu(dy, w, dx, shp, accumulate)
+    if bnb is not None:
+        _bnb_sums_cpu(dx, bnb)
+
+
+def _conv_dgrad_cpu(dy, w, dx, shp: ConvShape, accumulate: bool) -> None:
     w = w.float().permute(0, 3, 1, 2)  # -> [Cout][Cin][R][S]
     g = torch.nn.grad.conv2d_input((shp.N, shp.C, shp.H, shp.W), w, _nchw(dy),
                                    stride=shp.stride, padding=shp.pad)
@@ -175,13 +210,13 @@ def bn_apply(x, C: int, acc, gamma, beta, mean, invstd, run_mean, run_var, y, re
 
 
 def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
-                dy_masked=None) -> None:
+                dy_masked=None, presummed: bool = False) -> None:
     """BN(+ReLU) backward.  ``y`` (the post-activation output) gives the ReLU
     mask; ``dy_masked`` optionally receives the masked upstream gradient (the
     residual-shortcut gradient of an add+ReLU).  ``acc`` (fp64 [2C]) must be
     zero on entry."""
     if dy.is_cuda:
-        ops().bn_backward(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked)
+        ops().bn_backward(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked, presummed)
         return
     g = dy.float()
     if y is not None:
@@ -192,10 +227,9 @@ def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
     xh = (xf - mean) * invstd
     gm = g.reshape(-1, C)
     M = gm.shape[0]
-    s = gm.double().sum(0)
-    q = (gm.double() * xh.reshape(-1, C).double()).sum(0)
-    acc[:C] += s
-    acc[C:2 * C] += q
+    if not presummed:  # else the producer of dy already added the sums
+        acc[:C] += gm.double().sum(0)
+        acc[C:2 * C] += (gm.double() * xh.reshape(-1, C).double()).sum(0)
     if dgamma is not None:
         dgamma.copy_(acc[C:2 * C].float())
     if dbeta is not None:

@@ -73,8 +73,10 @@ def test_driver_session_end_to_end(tmp_path, engine):
     from metisfl_amd.utils.fedenv_parser import FederationEnvironment
     fe = FederationEnvironment(config=env_dict([free_port(), free_port()]))
     model = "fake" if engine == "fake" else StaticModelDef("resnet18", width_mult=0.125)
+    # echo learners take 0.5 s per task so both have joined before the
+    # round cutoff (the first joiner alone already advances sync rounds)
     sess = DriverSession(fe, model, train_recipe, None, eval_recipe, working_dir=str(tmp_path / "w"),
-                         device="cpu")
+                         device="cpu", fake_train_delay=0.5)
     try:
         sess.initialize_federation()
         reason = sess.monitor_federation(request_every_secs=0.3)
