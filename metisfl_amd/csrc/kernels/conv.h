@@ -25,6 +25,7 @@ struct ConvPlan {
   int splits = 1;
   int kchunk = 0;      // reduction elements per split (multiple of 64)
   int stats_rows = 0;  // 1 = the epilogue accumulates BN statistics
+  int bk = 64;         // k-tile depth (64 or 128)
 };
 
 // Kernel argument block.  *_shift = log2 of the divisor when it is a power of

@@ -86,7 +86,13 @@ __device__ __forceinline__ void lds_barrier() {
 // b128 fragment reads (A of fwd/dgrad, B of fwd): 16 lanes read 16 consecutive
 // rows at one logical chunk; 128-B rows -> bank slot (16 B) = 8*(row&1) +
 // phys.  swz = (row>>1)&7 makes the 16 slots distinct.
-__device__ __forceinline__ int swz_b128(int row) { return (row >> 1) & 7; }
+// 256-B rows (BK = 128): one row spans the whole 64-bank window, slot = phys:
+// swz = row & 15.
+template <int ROWB = 128>
+__device__ __forceinline__ int swz_b128(int row) {
+  if constexpr (ROWB == 128) return (row >> 1) & 7;
+  else return row & 15;
+}
 // ds_read_b64_tr_b16 reads: 32 lanes per LDS cycle cover rows {R..R+3,
 // R+8..R+11} (R % 4 == 0), two 16-B chunks (c0 even, c0+1) each.
 //   128-B rows (8 chunks): parity classes of rows need the 4 rows of each
@@ -119,12 +125,13 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint8_t* tile, int kk, int col0,
   }
   return out;
 }
-// fragment from a [row][k] tile (128-B rows): lane reads row r0 + lane%16,
+// fragment from a [row][k] tile (ROWB-byte rows): lane reads row r0 + lane%16,
 // k-chunk (kk/8 + lane/16).
+template <int ROWB>
 __device__ __forceinline__ bf16x8 b128_frag(const uint8_t* tile, int kk, int r0, int lane) {
   const int row = r0 + (lane & 15);
   const int ch = (kk >> 3) + (lane >> 4);
-  return *reinterpret_cast<const bf16x8*>(tile + row * 128 + ((ch ^ swz_b128(row)) << 4));
+  return *reinterpret_cast<const bf16x8*>(tile + row * ROWB + ((ch ^ swz_b128<ROWB>(row)) << 4));
 }
 
 // Vectorised epilogue shared by the direct and the split-K paths:
@@ -240,15 +247,19 @@ __device__ __forceinline__ void dma_k_loop(int nk, Issue& issue, Compute& comput
 
 // ---------------------------------------------------------------------------
 // Forward / dgrad implicit GEMM:  Y[m][n] = sum_k A[m][k] * B[n][k]
-template <int BM, int BN, bool DGRAD, int KS, int ST>
+template <int BM, int BN, bool DGRAD, int KS, int ST, int BK>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
-  constexpr int ACH = BM / 32;  // A DMA instructions per thread per k-tile
-  constexpr int BCH = BN / 32;  // B DMA instructions per thread per k-tile
-  constexpr int TM = BM / 32;   // 16x16 MFMA tiles per wave along M
+  // BK = 64 or 128 k-elements per tile: [row][k] tiles have ROWA-byte rows
+  constexpr int ROWA = BK * 2;
+  constexpr int A_RPI = 1024 / ROWA;   // rows per 1-KiB DMA instruction
+  constexpr int A_CPR = ROWA / 16;     // 16-B chunks per row
+  constexpr int ACH = BM * BK / 2048;  // A DMA instructions per thread per k-tile
+  constexpr int BCH = BN * BK / 2048;  // B DMA instructions per thread per k-tile
+  constexpr int TM = BM / 32;          // 16x16 MFMA tiles per wave along M
   constexpr int TN = BN / 32;
-  constexpr int A_BYTES = BM * 128;
-  constexpr int B_ROWB = DGRAD ? BN * 2 : 128;  // dgrad B: [64 k][BN] rows
-  constexpr int STAGE = A_BYTES + BN * 128;     // both B layouts hold BN*64 bf16
+  constexpr int A_BYTES = BM * ROWA;
+  constexpr int B_ROWB = DGRAD ? BN * 2 : ROWA;  // dgrad B: [BK k][BN] rows
+  constexpr int STAGE = A_BYTES + BN * BK * 2;   // both B layouts hold BN*BK bf16
   const ConvGeom& g = a.g;
   const auto rsA = make_rsrc(a.src, a.src_bytes);
   const auto rsB = make_rsrc(a.wgt, a.wgt_bytes);
@@ -262,17 +273,20 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int n0 = blockIdx.y * BN;
   const int kbeg = blockIdx.z * a.kchunk;
   const int kend = min(g.K, kbeg + a.kchunk);
-  const int nk = (kend - kbeg + kBK - 1) / kBK;
+  const int nk = (kend - kbeg + BK - 1) / BK;
   const int HWC = g.H * g.W * g.C;
 
-  // A DMA: instruction i of wave w fills rows (w + 4i)*8 .. +8 (1 KiB); lane
-  // -> row lrow + 32 i, physical chunk lane&7, logical chunk (k offset) below.
-  const int lrow = wave * 8 + (lane >> 3);
-  const int a_kc = ((lane & 7) ^ swz_b128(lrow)) * 8;  // same for every i (32i keeps bits 1-3)
+  // A DMA: instruction i of wave w fills rows (w + 4i)*A_RPI .. (1 KiB); lane
+  // -> row lrow + 4*A_RPI*i, physical chunk lane % A_CPR, logical chunk (k
+  // offset) below -- the same for every i: the row step (32 or 16) leaves the
+  // swizzle bits unchanged.
+  constexpr int A_ISTEP = 4 * A_RPI;
+  const int lrow = wave * A_RPI + lane / A_CPR;
+  const int a_kc = ((lane % A_CPR) ^ swz_b128<ROWA>(lrow)) * 8;
   int a_nb[ACH], a_y0[ACH], a_x0[ACH];
 #pragma unroll
   for (int i = 0; i < ACH; ++i) {
-    const int m = m0 + lrow + 32 * i;
+    const int m = m0 + lrow + A_ISTEP * i;
     const int mm = m < g.M ? m : 0;
     const int n = sdiv(mm, g.P * g.Q, a.pq_shift);
     const int rem = mm - n * g.P * g.Q;
@@ -297,7 +311,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 
   auto issue = [&](int kt, int stage) {
     uint8_t* st = smem + stage * STAGE;
-    const int kb = kbeg + kt * kBK;
+    const int kb = kbeg + kt * BK;
     {
       const int k = kb + a_kc;
       const int rs = sdiv(k, g.C, a.c_shift);
@@ -337,7 +351,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
         const int ko = kr - rs * g.C;
         off = ((kr < kend) & (n < g.Ng)) ? (uint32_t)((ko * KS * KS + rs) * g.Ng + n) * 2u : kOOB;
       } else {
-        const int n = n0 + lrow + 32 * i;
+        const int n = n0 + lrow + A_ISTEP * i;
         const int k = kb + a_kc;
         off = ((k < kend) & (n < g.Ng)) ? (uint32_t)(n * g.K + k) * 2u : kOOB;
       }
@@ -355,14 +369,14 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     const uint8_t* As = smem + stage * STAGE;
     const uint8_t* Bs = As + A_BYTES;
 #pragma unroll
-    for (int kk = 0; kk < kBK; kk += 32) {
+    for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = b128_frag(As, kk, wm * (BM / 2) + 16 * i, lane);
+      for (int i = 0; i < TM; ++i) af[i] = b128_frag<ROWA>(As, kk, wm * (BM / 2) + 16 * i, lane);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         if constexpr (DGRAD) bfr[j] = tr_frag<B_ROWB>(Bs, kk, wn * (BN / 2) + 16 * j, lane);
-        else bfr[j] = b128_frag(Bs, kk, wn * (BN / 2) + 16 * j, lane);
+        else bfr[j] = b128_frag<ROWA>(Bs, kk, wn * (BN / 2) + 16 * j, lane);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -447,12 +461,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 // wgrad:  dW[ko][j] = sum_m dY[m][ko] * im2col(X)[m][j],  j = (r, s, c)
 // Tiles: A = dY [64 m][64 ko], B = im2col(X) [64 m][64 j], both 128-B rows,
 // both read with transposing LDS reads.
-template <int KS, int ST>
+template <int KS, int ST, int BK>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __restrict__ dw) {
   // g: H,W,C = X dims; P,Q = dY spatial; Ng = Cout; K = R*S*C; M = N*P*Q
   constexpr int BM = 64, BN = 64;
   constexpr int TM = 2, TN = 2;
-  constexpr int T_BYTES = 64 * 128;
+  constexpr int T_BYTES = BK * 128;   // [BK m][64 cols], 128-B rows
+  constexpr int NI = BK / 32;         // DMA instructions per operand per thread
   constexpr int STAGE = 2 * T_BYTES;
   const ConvGeom& g = a.g;
   const auto rsA = make_rsrc(a.src, a.src_bytes);
@@ -467,7 +482,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
   const int j0 = blockIdx.y * BN;
   const int mbeg = blockIdx.z * a.kchunk;
   const int mend = min(g.M, mbeg + a.kchunk);
-  const int nk = (mend - mbeg + kBK - 1) / kBK;
+  const int nk = (mend - mbeg + BK - 1) / BK;
 
   // DMA mapping (both operands): instruction i of wave w fills m-rows
   // (w + 4i)*8 .. +8; lane -> row lrow + 32 i, physical chunk lane&7.
@@ -487,9 +502,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
 
   auto issue = [&](int kt, int stage) {
     uint8_t* st = smem + stage * STAGE;
-    const int mb = mbeg + kt * kBK;
+    const int mb = mbeg + kt * BK;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int m = mb + lrow + 32 * i;
       const bool mv = m < mend;
       dma16(rsA, (mv & (ko < g.Ng)) ? (uint32_t)(m * g.Ng + ko) * 2u : kOOB, st + (wave + 4 * i) * 1024);
@@ -514,7 +529,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
     const uint8_t* As = smem + stage * STAGE;
     const uint8_t* Bs = As + T_BYTES;
 #pragma unroll
-    for (int kk = 0; kk < kBK; kk += 32) {
+    for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) af[i] = tr_frag<128>(As, kk, wm * (BM / 2) + 16 * i, lane);
@@ -526,7 +541,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
         for (int jj = 0; jj < TN; ++jj) acc[i][jj] = mfma16(af[i], bfr[jj], acc[i][jj]);
     }
   };
-  dma_k_loop<4>(nk, issue, compute);
+  dma_k_loop<2 * NI>(nk, issue, compute);
 
   const bool atomic = gridDim.z > 1;  // split-K slices add into the zeroed slot
   const int rbase = ko0 + wm * (BM / 2) + (lane >> 4) * 4;
@@ -592,24 +607,30 @@ static void set_lds_limit(K* kernel, size_t lds, bool& done) {
   }
 }
 
-template <int BM, int BN, bool DG, int KS, int ST>
+template <int BM, int BN, bool DG, int KS, int ST, int BK>
 static void launch_gemm_t(const ConvArgs& a, const ConvPlan& p, hipStream_t s) {
   dim3 grid((a.g.M + BM - 1) / BM, (a.g.Ng + BN - 1) / BN, p.splits);
-  size_t lds = (size_t)kStages * (BM * 128 + BN * 128);
+  size_t lds = (size_t)kStages * (BM + BN) * BK * 2;
   const size_t epi = ((size_t)BM * (BN + 4) + 256 * 16 + 8) * sizeof(float);
   if (lds < epi) lds = epi;
   static bool attr_set = false;
-  set_lds_limit(&conv_gemm_kernel<BM, BN, DG, KS, ST>, lds, attr_set);
-  conv_gemm_kernel<BM, BN, DG, KS, ST><<<grid, 256, lds, s>>>(a);
+  set_lds_limit(&conv_gemm_kernel<BM, BN, DG, KS, ST, BK>, lds, attr_set);
+  conv_gemm_kernel<BM, BN, DG, KS, ST, BK><<<grid, 256, lds, s>>>(a);
+}
+
+template <int BM, int BN, bool DG, int KS, int ST>
+static void launch_gemm_bk(const ConvArgs& a, const ConvPlan& p, hipStream_t s) {
+  if (p.bk == 128) launch_gemm_t<BM, BN, DG, KS, ST, 128>(a, p, s);
+  else launch_gemm_t<BM, BN, DG, KS, ST, 64>(a, p, s);
 }
 
 template <int BM, int BN, bool DG>
 static void launch_gemm_ks(const ConvArgs& a, const ConvPlan& p, hipStream_t s) {
   const int ks = a.g.R, st = a.g.stride;
-  if (ks == 3 && st == 1) launch_gemm_t<BM, BN, DG, 3, 1>(a, p, s);
-  else if (ks == 3 && st == 2) launch_gemm_t<BM, BN, DG, 3, 2>(a, p, s);
-  else if (ks == 1 && st == 1) launch_gemm_t<BM, BN, DG, 1, 1>(a, p, s);
-  else if (ks == 1 && st == 2) launch_gemm_t<BM, BN, DG, 1, 2>(a, p, s);
+  if (ks == 3 && st == 1) launch_gemm_bk<BM, BN, DG, 3, 1>(a, p, s);
+  else if (ks == 3 && st == 2) launch_gemm_bk<BM, BN, DG, 3, 2>(a, p, s);
+  else if (ks == 1 && st == 1) launch_gemm_bk<BM, BN, DG, 1, 1>(a, p, s);
+  else if (ks == 1 && st == 2) launch_gemm_bk<BM, BN, DG, 1, 2>(a, p, s);
 }
 
 bool conv_supported(const ConvGeom& g) {
@@ -634,11 +655,15 @@ ConvPlan plan_conv_gemm(const ConvGeom& g) {
   p.bm = g.M >= 8192 ? 128 : 64;
   p.bn = g.Ng >= 128 && g.M >= 16384 ? 128 : 64;
   const int tiles = ((g.M + p.bm - 1) / p.bm) * ((g.Ng + p.bn - 1) / p.bn);
-  const int ksteps = (g.K + kBK - 1) / kBK;
+  // 128-deep k-tiles halve the serial k-steps (and barriers) of a block when
+  // the reduction is long enough; the 128x128 tile keeps BK = 64 (LDS)
+  static const int bk128_min_k = env_int("MFL_CONV_BK128_MIN_K", 512);  // measured best (r1 sweep)
+  p.bk = (g.K >= bk128_min_k && !(p.bm == 128 && p.bn == 128)) ? 128 : 64;
+  const int ksteps = (g.K + p.bk - 1) / p.bk;
   int splits = 1;
   while (tiles * splits < target && ksteps / (splits * 2) >= min_steps && splits < 16) splits *= 2;
   p.splits = splits;
-  p.kchunk = ((ksteps + splits - 1) / splits) * kBK;
+  p.kchunk = ((ksteps + splits - 1) / splits) * p.bk;
   p.stats_rows = 1;
   return p;
 }
@@ -706,13 +731,34 @@ ConvPlan plan_conv_wgrad(const ConvGeom& g) {
   p.bm = 64;
   p.bn = 64;
   const int tiles = ((g.Ng + 63) / 64) * ((g.K + 63) / 64);
-  const int ksteps = (g.M + kBK - 1) / kBK;
+  static const int bk128_min_m = env_int("MFL_WGRAD_BK128_MIN_M", 1 << 30);
+  p.bk = g.M >= bk128_min_m ? 128 : 64;
+  const int ksteps = (g.M + p.bk - 1) / p.bk;
   int splits = 1;
   while (tiles * splits < target && ksteps / (splits * 2) >= min_steps && splits < 64) splits *= 2;
   p.splits = splits;
-  p.kchunk = ((ksteps + splits - 1) / splits) * kBK;
+  p.kchunk = ((ksteps + splits - 1) / splits) * p.bk;
   p.stats_rows = 0;
   return p;
+}
+
+template <int BK>
+static void launch_wgrad_ks(const ConvArgs& a, dim3 grid, int ks, int st, float* dw, hipStream_t s) {
+  const size_t lds = (size_t)kStages * 2 * BK * 128;
+  static bool attr[4] = {false, false, false, false};
+  if (ks == 3 && st == 1) {
+    set_lds_limit(&conv_wgrad_kernel<3, 1, BK>, lds, attr[0]);
+    conv_wgrad_kernel<3, 1, BK><<<grid, 256, lds, s>>>(a, dw);
+  } else if (ks == 3 && st == 2) {
+    set_lds_limit(&conv_wgrad_kernel<3, 2, BK>, lds, attr[1]);
+    conv_wgrad_kernel<3, 2, BK><<<grid, 256, lds, s>>>(a, dw);
+  } else if (ks == 1 && st == 1) {
+    set_lds_limit(&conv_wgrad_kernel<1, 1, BK>, lds, attr[2]);
+    conv_wgrad_kernel<1, 1, BK><<<grid, 256, lds, s>>>(a, dw);
+  } else if (ks == 1 && st == 2) {
+    set_lds_limit(&conv_wgrad_kernel<1, 2, BK>, lds, attr[3]);
+    conv_wgrad_kernel<1, 2, BK><<<grid, 256, lds, s>>>(a, dw);
+  }
 }
 
 // dw must be zero on entry when p.splits > 1 (slices accumulate with fp32
@@ -729,12 +775,9 @@ void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, 
   a.kchunk = p.kchunk;
   fill_shifts(a);
   dim3 grid((g.Ng + 63) / 64, (g.K + 63) / 64, p.splits);
-  const size_t lds = (size_t)kStages * 2 * 64 * 128;  // 48 KiB
   const int ks = g.R, st = g.stride;
-  if (ks == 3 && st == 1) conv_wgrad_kernel<3, 1><<<grid, 256, lds, s>>>(a, dw);
-  else if (ks == 3 && st == 2) conv_wgrad_kernel<3, 2><<<grid, 256, lds, s>>>(a, dw);
-  else if (ks == 1 && st == 1) conv_wgrad_kernel<1, 1><<<grid, 256, lds, s>>>(a, dw);
-  else if (ks == 1 && st == 2) conv_wgrad_kernel<1, 2><<<grid, 256, lds, s>>>(a, dw);
+  if (p.bk == 128) launch_wgrad_ks<128>(a, grid, ks, st, dw, s);
+  else launch_wgrad_ks<64>(a, grid, ks, st, dw, s);
 }
 
 void launch_transpose_krsc(const uint16_t* w, uint16_t* wt, int Co, int RS, int Ci, hipStream_t s) {

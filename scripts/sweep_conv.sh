@@ -1,5 +1,6 @@
 #!/bin/bash
-# Split-K policy sweep: short benches under different plan knobs.
+# Conv plan sweep: short benches under different plan knobs (env vars read by
+# plan_conv_gemm / plan_conv_wgrad).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/sweep
 ARGS="--local-epochs 1 --steps 2 --warmup 1 --train-size 16384 --test-size 1024"
@@ -11,3 +12,7 @@ run() {  # name, env...
   case $rc in 124|134|137|139) exit $rc;; esac
 }
 run base
+run m2 MFL_CONV_MIN_KSTEPS=2
+run m3 MFL_CONV_MIN_KSTEPS=3
+run t512_m2 MFL_CONV_TARGET_BLOCKS=512 MFL_CONV_MIN_KSTEPS=2
+run t128 MFL_CONV_TARGET_BLOCKS=128
