@@ -86,7 +86,12 @@ def main() -> int:
     del xtr, xte
     cfg = FederationConfig(protocol="synchronous", batch_size=args.batch,
                            local_epochs=args.local_epochs, evaluate_test=not args.no_eval)
-    fed = CollectiveFederation(comm, net, train_ds, cfg, test_ds=test_ds)
+    engine = None
+    if comm.rank == 0:  # the native controller keeps the round bookkeeping
+        from metisfl_amd.parallel.engine_bridge import CollectiveController
+        sizes = [args.train_size // n + (1 if r < args.train_size % n else 0) for r in range(n)]
+        engine = CollectiveController(cfg, sizes)
+    fed = CollectiveFederation(comm, net, train_ds, cfg, test_ds=test_ds, engine=engine)
 
     def sync():
         if dev.type == "cuda":

@@ -109,15 +109,79 @@ class LearnerDispatcher:
         self.pool.shutdown(wait=True, cancel_futures=True)
 
 
+class LearnerHealthMonitor:
+    """Failure detector (the reference has no learner heartbeat
+    and a dead learner stalls the synchronous barrier forever).  Every
+    ``interval_s`` each registered learner gets a GetServicesHealthStatus
+    probe; after ``threshold`` consecutive failures it is evicted from the
+    engine, which re-checks the barrier and may release the pending round."""
+
+    def __init__(self, servicer, interval_s: float = 5.0, threshold: int = 3, timeout_s: float = 2.0):
+        self.srv = servicer
+        self.interval = interval_s
+        self.threshold = threshold
+        self.timeout = timeout_s
+        self.failures: dict[str, int] = {}
+        self.evicted: list[str] = []
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._loop, name="learner-health", daemon=True)
+
+    def start(self):
+        self._thread.start()
+
+    def stop(self):
+        self._stop.set()
+
+    def probe(self, lid: str, entity) -> bool:
+        ch = make_channel(entity)
+        try:
+            raw_unary(ch, LEARNER_SERVICE, "GetServicesHealthStatus")(b"", timeout=self.timeout)
+            return True
+        except grpc.RpcError:
+            return False
+        finally:
+            ch.close()
+
+    def check_once(self) -> None:
+        with self.srv.dispatcher.lock:
+            entities = dict(self.srv.dispatcher.entities)
+        for lid, ent in entities.items():
+            if self.probe(lid, ent):
+                self.failures[lid] = 0
+                continue
+            self.failures[lid] = self.failures.get(lid, 0) + 1
+            if self.failures[lid] >= self.threshold:
+                MetisLogger.warning("learner %s failed %d health checks: evicting", lid, self.failures[lid])
+                try:
+                    dispatch = self.srv.engine.evict_learner(lid)
+                except E.EngineStatusError:
+                    dispatch = None  # already gone
+                self.srv.dispatcher.forget(lid)
+                self.failures.pop(lid, None)
+                self.evicted.append(lid)
+                if dispatch:
+                    self.srv.dispatcher.submit(dispatch)
+
+    def _loop(self):
+        while not self._stop.wait(self.interval):
+            try:
+                self.check_once()
+            except Exception as e:  # noqa: BLE001 - the monitor must survive anything
+                MetisLogger.error("health monitor error: %r", e)
+
+
 class ControllerServicer(controller_pb2_grpc.ControllerServiceServicer):
 
-    def __init__(self, controller_params_pb, dispatch_workers: int = 16):
+    def __init__(self, controller_params_pb, dispatch_workers: int = 16,
+                 heartbeat_interval_s: float | None = 5.0, heartbeat_threshold: int = 3):
         self.params = controller_params_pb
         self.engine = E.Controller(controller_params_pb.SerializeToString())
         self.dispatcher = LearnerDispatcher(self.engine, dispatch_workers)
         self._shutdown = threading.Event()
         self._server: GRPCServerMaxMsgLength | None = None
         self._stop_thread: threading.Thread | None = None
+        self.monitor = LearnerHealthMonitor(self, heartbeat_interval_s or 5.0, heartbeat_threshold) \
+            if heartbeat_interval_s else None
 
     # -- lifecycle --------------------------------------------------------------
     def start(self) -> int:
@@ -125,6 +189,8 @@ class ControllerServicer(controller_pb2_grpc.ControllerServiceServicer):
         controller_pb2_grpc.add_ControllerServiceServicer_to_server(
             self, self._server.server, raw_requests=("MarkTaskCompleted", "ReplaceCommunityModel"))
         self._server.server.start()
+        if self.monitor is not None:
+            self.monitor.start()
         MetisLogger.info("Controller servicer listening on %s (port %d)",
                          self._server.grpc_endpoint.listening_endpoint, self._server.port)
         return self._server.port
@@ -138,6 +204,8 @@ class ControllerServicer(controller_pb2_grpc.ControllerServiceServicer):
 
     def stop(self, grace: float = 0.5) -> None:
         self._shutdown.set()
+        if self.monitor is not None:
+            self.monitor.stop()
         if self._server is not None:
             self._server.server.stop(grace).wait()
         self.dispatcher.shutdown()

@@ -103,6 +103,16 @@ PYBIND11_MODULE(_engine, m) {
              return py::make_tuple(r.first, r.second, dispatch_to_py(d));
            })
       .def("remove_learner", &Controller::remove_learner, py::call_guard<py::gil_scoped_release>())
+      .def("evict_learner",
+           [](Controller& c, const std::string& id) {
+             Dispatch d;
+             {
+               py::gil_scoped_release nogil;
+               d = c.evict_learner(id);
+             }
+             return dispatch_to_py(d);
+           })
+      .def("evicted", &Controller::evicted)
       .def("learner_ids", &Controller::learner_ids)
       .def("num_learners", &Controller::num_learners)
       .def("global_iteration", &Controller::global_iteration)

@@ -307,10 +307,33 @@ Dispatch Controller::learner_completed_task(const std::string& id, const std::st
 }
 
 Dispatch Controller::schedule_tasks_locked(const std::string& id, uint32_t task_iteration) {
-  Dispatch d;
   const auto active = active_ids_locked();
   auto to_schedule = scheduler_->schedule_next(id, active);
-  if (to_schedule.empty()) return d;
+  if (to_schedule.empty()) return Dispatch{};
+  return run_scheduled_locked(to_schedule, active, task_iteration);
+}
+
+// Failure detector hook (no token: the caller is the controller itself).
+// Removing a learner that a synchronous barrier was waiting for may complete
+// the barrier with the remaining learners -- the reference stalls forever in
+// that case; here the round is aggregated right away.
+Dispatch Controller::evict_learner(const std::string& id) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!learners_.count(id)) throw StatusError(NOT_FOUND, "learner " + id + " not found");
+  store_->erase({id});
+  learners_.erase(id);
+  templates_.erase(id);
+  ++evicted_;
+  const auto active = active_ids_locked();
+  auto ready = scheduler_->poll(active);
+  if (ready.empty()) return Dispatch{};
+  return run_scheduled_locked(ready, active, global_iteration_);
+}
+
+Dispatch Controller::run_scheduled_locked(const std::vector<std::string>& to_schedule,
+                                          const std::vector<std::string>& active,
+                                          uint32_t task_iteration) {
+  Dispatch d;
   const uint32_t idx = task_iteration == 0 ? 0 : task_iteration - 1;
   if (!metadata_.empty() && idx < metadata_.size()) metadata_[idx].completed_at = now_ns();
   // FedRec folds ONE learner's (previous, latest) pair into its running state,

@@ -112,6 +112,10 @@ class Controller {
                                                   const std::string& dataset_spec,
                                                   Dispatch* dispatch);
   void remove_learner(const std::string& id, const std::string& token);
+  // failure detector: drop an unresponsive learner; may complete a pending
+  // synchronous barrier (returns that round's dispatch)
+  Dispatch evict_learner(const std::string& id);
+  uint32_t evicted() const { return evicted_; }
   std::vector<std::string> learner_ids() const;
 
   // --- task flow ------------------------------------------------------------
@@ -151,6 +155,8 @@ class Controller {
   std::string make_eval_task(const FederatedModelT& model) const;
   void schedule_initial_task_locked(const std::string& id, Dispatch* d);
   Dispatch schedule_tasks_locked(const std::string& id, uint32_t task_iteration);
+  Dispatch run_scheduled_locked(const std::vector<std::string>& to_schedule,
+                                const std::vector<std::string>& active, uint32_t task_iteration);
   FederatedModelT compute_community_model_locked(const std::vector<std::string>& ids,
                                                  uint32_t meta_idx);
   void update_templates_locked(const std::vector<std::string>& ids);
@@ -176,6 +182,7 @@ class Controller {
   };
   std::vector<CommEval> evaluations_;
   uint32_t global_iteration_ = 0;
+  uint32_t evicted_ = 0;
   std::mt19937_64 rng_;
 };
 

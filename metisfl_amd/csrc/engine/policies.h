@@ -29,6 +29,9 @@ class Scheduler {
   // learner `id` finished; `active` = all learners currently in the federation
   virtual std::vector<std::string> schedule_next(const std::string& id,
                                                  const std::vector<std::string>& active) = 0;
+  // membership changed (a learner was evicted): the learners whose round can
+  // proceed now, if any
+  virtual std::vector<std::string> poll(const std::vector<std::string>&) { return {}; }
   virtual std::string name() const = 0;
 };
 
@@ -37,6 +40,9 @@ class SynchronousScheduler : public Scheduler {
   std::vector<std::string> schedule_next(const std::string& id,
                                          const std::vector<std::string>& active) override {
     done_.insert(id);
+    return poll(active);
+  }
+  std::vector<std::string> poll(const std::vector<std::string>& active) override {
     // only count learners that are still active (a learner that left must not
     // stall the barrier; the reference waits on |active| as well)
     size_t n = 0;

@@ -63,9 +63,10 @@ class Comm:
         """Gather one small 1-D tensor per rank -> [world, n] (on row.device)."""
         if not self.distributed:
             return row.reshape(1, -1).clone()
-        out = torch.empty((self.world, row.numel()), dtype=row.dtype, device=row.device)
-        dist.all_gather_into_tensor(out, row.contiguous())
-        return out
+        # flat output: gloo's allgather_base wants chunks shaped like the input
+        out = torch.empty(self.world * row.numel(), dtype=row.dtype, device=row.device)
+        dist.all_gather_into_tensor(out, row.contiguous().reshape(-1))
+        return out.view(self.world, row.numel())
 
     def all_max(self, x: float) -> float:
         if not self.distributed:

@@ -1,0 +1,98 @@
+"""The native controller engine on the collective (RCCL) data plane.
+
+On one node the models never travel through the controller: they are
+averaged in place by an all-reduce.  Rank 0 still runs the SAME native
+controller state machine as the gRPC path, so a collective federation has the
+reference's bookkeeping and queries: learners registered with their dataset
+specs, scaling factors from the configured scaler (controller.cc:809-830),
+FederatedTaskRuntimeMetadata per round (the benchmark record, metis.proto
+342-365), local task lineages, per-variable model quantifiers
+(controller.cc:952-1004, computed on device by the count-zeros kernel) and
+community-model lineage snapshots.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from metisfl_amd.proto import controller_pb2, metis_pb2
+from metisfl_amd.utils.proto_messages_factory import MetisProtoMessages as M
+from metisfl_amd.utils.proto_messages_factory import ModelProtoMessages as MM
+
+_SCALING_NAMES = {"NUM_TRAINING_EXAMPLES": "NumTrainingExamples", "NUM_COMPLETED_BATCHES": "NumCompletedBatches",
+                  "NUM_PARTICIPANTS": "NumParticipants"}
+_RULES = {"fed_avg": "FedAvg", "fed_stride": "FedStride", "fed_rec": "FedRec"}
+
+
+def controller_params_for(cfg, optimizer_pb=None):
+    """ControllerParams equivalent of a FederationConfig."""
+    rule = M.construct_aggregation_rule_pb(_RULES.get(cfg.aggregation, cfg.aggregation),
+                                           _SCALING_NAMES.get(cfg.scaling_factor.upper(), cfg.scaling_factor),
+                                           cfg.stride_length or None)
+    opt = optimizer_pb or MM.construct_optimizer_config_pb(MM.construct_vanilla_sgd_optimizer_pb(0.01))
+    return M.construct_controller_params_pb(
+        M.construct_server_entity_pb("localhost", 50051),
+        M.construct_global_model_specs(rule, 1.0),
+        M.construct_communication_specs_pb(cfg.protocol.upper(), cfg.semi_sync_lambda, cfg.semi_sync_recompute),
+        M.construct_model_store_config_pb("InMemory", "LineageLengthEviction", 1),
+        M.construct_controller_modelhyperparams_pb(cfg.batch_size, cfg.local_epochs, opt, 0.0))
+
+
+class CollectiveController:
+    """Rank-0 wrapper around ``_engine.Controller`` for collective rounds."""
+
+    def __init__(self, cfg, dataset_sizes: list[int], optimizer_pb=None):
+        from metisfl_amd import _engine
+        self.engine = _engine.Controller(controller_params_for(cfg, optimizer_pb).SerializeToString())
+        self.ids, self.tokens = [], []
+        for r, n in enumerate(dataset_sizes):
+            se = M.construct_server_entity_pb("localhost", 50052 + r).SerializeToString()
+            ds = M.construct_dataset_spec_pb(int(n), 0, 0).SerializeToString()
+            lid, tok, _ = self.engine.add_learner(se, ds)
+            self.ids.append(lid)
+            self.tokens.append(tok)
+
+    # -- aggregation weights ------------------------------------------------------
+    def weights(self, num_train, completed_batches) -> list[float]:
+        f = self.engine.scaling_factors(self.ids, [float(x) for x in num_train],
+                                        [float(x) for x in completed_batches])
+        return [float(f[i]) for i in self.ids]
+
+    # -- bookkeeping ------------------------------------------------------------------
+    @staticmethod
+    def _task_meta(row, batch_size: int) -> bytes:
+        n, batches, ms_b, ms_e, loss, acc, epochs, gi = row[:8]
+        ev = M.construct_task_evaluation_pb([M.construct_epoch_evaluation_pb(
+            max(1, int(np.ceil(epochs))), M.construct_model_evaluation_pb({"loss": loss, "accuracy": acc}))])
+        return M.construct_task_execution_metadata_pb(int(gi), ev, float(epochs), int(batches), batch_size,
+                                                      float(ms_e), float(ms_b)).SerializeToString()
+
+    def record_round(self, rec, batch_size: int, quantifiers=None) -> None:
+        ns = lambda t: int(t * 1e9)
+        zeros, sizes, lengths = quantifiers or ([], [], [])
+        metas = [self._task_meta(rec.learner_meta[i], batch_size) for i in range(len(self.ids))]
+        self.engine.record_collective_round(rec.global_iteration, self.ids, ns(rec.started_at),
+                                            ns(rec.completed_at), ns(rec.aggregation_started_at),
+                                            ns(rec.aggregation_completed_at), metas, zeros, sizes, lengths)
+
+    def snapshot_community(self, names, arrays, trainable, global_iteration: int) -> None:
+        """Community-model lineage entry (an explicit D2H copy: done on
+        checkpoints / on request, not every round)."""
+        from metisfl_amd.utils.tensor_codec import model_from_arrays
+        fm = MM.construct_federated_model_pb(len(self.ids), model_from_arrays(names, arrays, trainable),
+                                             global_iteration)
+        self.engine.replace_community_model(fm.SerializeToString())
+
+    # -- queries (same responses as the gRPC controller) -------------------------------
+    def runtime_metadata(self, n: int = 0):
+        return controller_pb2.GetRuntimeMetadataLineageResponse.FromString(self.engine.runtime_metadata_lineage(n))
+
+    def local_task_lineage(self, n: int = 0):
+        return controller_pb2.GetLocalTaskLineageResponse.FromString(self.engine.local_task_lineage(n, self.ids))
+
+    def participating_learners(self):
+        return controller_pb2.GetParticipatingLearnersResponse.FromString(self.engine.participating_learners())
+
+    def community_model_lineage(self, n: int = 1):
+        return controller_pb2.GetCommunityModelLineageResponse.FromString(self.engine.community_model_lineage(n))

@@ -7,8 +7,8 @@ data shard stay resident in HBM across rounds.  A synchronous FedAvg round is
   2. all-gather of a few scalars per learner (dataset size, completed
      batches, per-batch / per-epoch time, train metrics) -- the payload of the
      reference's MarkTaskCompleted metadata (learner.py:197-206),
-  3. scaling factors from the controller's scaler (C++ engine) -- identical
-     on every rank, so no broadcast is needed,
+  3. scaling factors from the configured scaler (identical on every rank, so
+     no broadcast is needed; rank 0's native controller computes the same),
   4. in-place pre-scale ``theta_i *= w_i`` (K1) and ONE RCCL all-reduce of the
      flat model buffer: every learner now holds the community model, which is
      the reference's gather -> FedAvg -> RunTask broadcast
@@ -16,29 +16,40 @@ data shard stay resident in HBM across rounds.  A synchronous FedAvg round is
 
 Semi-synchronous rounds use the same barrier with per-learner step budgets
 recomputed from the measured per-batch times (controller.cc:520-569).
-Asynchronous rounds are served by parallel/async_fed.py.
+Asynchronous federations (per-learner dispatch, FedRec) run on the controller
+path (gRPC control plane + native engine), where every learner is scheduled
+on its own.
+
+Rank 0 additionally drives the native controller engine (engine_bridge.py)
+so the collective federation has the reference's runtime metadata, task
+lineages and model quantifiers.  ``save_checkpoint`` / ``resume`` implement
+SURVEY §5.4 (the reference has no checkpointing): the community model,
+per-rank optimizer state, step counters and round history.
 """
 from __future__ import annotations
 
+import json
 import math
+import os
 import time
-from dataclasses import dataclass, field
+from dataclasses import asdict, dataclass, field
 
 import numpy as np
 import torch
 
 from metisfl_amd.ops import optim as opt_ops
-from metisfl_amd.parallel.comm import Comm
 from metisfl_amd.parallel import scaling
+from metisfl_amd.parallel.comm import Comm
 
 META_FIELDS = ("num_training_examples", "completed_batches", "ms_per_batch", "ms_per_epoch",
-               "train_loss", "train_accuracy", "completed_epochs", "global_iteration")
+               "train_loss", "train_accuracy", "completed_epochs", "global_iteration",
+               "test_loss", "test_accuracy")
 
 
 @dataclass
 class FederationConfig:
-    protocol: str = "synchronous"          # synchronous | semi_synchronous | asynchronous
-    aggregation: str = "fed_avg"           # fed_avg | fed_stride | fed_rec
+    protocol: str = "synchronous"          # synchronous | semi_synchronous
+    aggregation: str = "fed_avg"           # fed_avg (fed_stride == fed_avg on one all-reduce)
     scaling_factor: str = "NUM_TRAINING_EXAMPLES"
     stride_length: int = 0
     batch_size: int = 32
@@ -47,6 +58,7 @@ class FederationConfig:
     semi_sync_recompute: bool = False
     evaluate_test: bool = True             # learner test-set eval at task end
     eval_max_steps: int | None = None
+    quantify: bool = True                  # per-variable zero counts of each community model
     extra: dict = field(default_factory=dict)
 
 
@@ -65,25 +77,35 @@ class RoundRecord:
     num_local_updates: list
     test_metrics: dict | None = None
 
+    def to_json(self) -> dict:
+        d = asdict(self)
+        d["learner_meta"] = self.learner_meta.tolist()
+        return d
+
 
 class CollectiveFederation:
     """Drives rounds for the learner hosted by this rank."""
 
     def __init__(self, comm: Comm, net, train_ds, cfg: FederationConfig, test_ds=None,
-                 learner_ids: list[str] | None = None, engine=None):
+                 learner_ids: list[str] | None = None, engine=None, broadcast_initial: bool = True):
         self.comm = comm
         self.net = net
         self.train_ds = train_ds
         self.test_ds = test_ds
         self.cfg = cfg
-        self.engine = engine
+        self.engine = engine if comm.rank == 0 else None
         self.world = comm.world
         self.rank = comm.rank
         self.learner_ids = learner_ids or [f"learner_{r}" for r in range(self.world)]
         spe = train_ds.steps_per_epoch
-        # reference: num_local_updates = epochs * ceil(N_train / batch) (controller.cc:148-153)
-        n_updates = cfg.local_epochs * max(1, math.ceil(train_ds.n / cfg.batch_size))
-        self.num_local_updates = [n_updates] * self.world
+        # reference: num_local_updates = epochs * ceil(N_train / batch) per
+        # learner (controller.cc:148-153); the join-time dataset sizes are
+        # exchanged once
+        sizes = comm.all_gather_rows(torch.tensor([float(train_ds.n)], dtype=torch.float64,
+                                                  device=comm.device)).cpu().numpy()[:, 0]
+        self.dataset_sizes = [int(x) for x in sizes]
+        self.num_local_updates = [cfg.local_epochs * max(1, math.ceil(n / cfg.batch_size))
+                                  for n in self.dataset_sizes]
         self.steps_done = 0
         self.global_iteration = 0
         self.history: list[RoundRecord] = []
@@ -91,7 +113,8 @@ class CollectiveFederation:
         dev = comm.device
         self._ev0 = torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else None
         self._ev1 = torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else None
-        self.broadcast_initial_model()
+        if broadcast_initial:
+            self.broadcast_initial_model()
 
     # ------------------------------------------------------------------------
     def broadcast_initial_model(self) -> None:
@@ -128,16 +151,18 @@ class CollectiveFederation:
             out["test"] = net.evaluate(self.test_ds, self.cfg.eval_max_steps)
         return out
 
+    def aggregation_weights(self, meta: np.ndarray) -> list[float]:
+        w = scaling.compute(self.cfg.scaling_factor, meta[:, 0], meta[:, 1], self.world)
+        if self.engine is not None:
+            we = self.engine.weights(meta[:, 0], meta[:, 1])
+            if not np.allclose(we, w, rtol=1e-12, atol=0):
+                raise RuntimeError(f"scaler mismatch: engine {we} vs collective {w}")
+        return w
+
     def aggregate(self, meta: np.ndarray) -> tuple[list[float], float]:
         """Scale + all-reduce; returns (weights, ms)."""
         t0 = time.perf_counter()
-        ids = self.learner_ids
-        if self.engine is not None:
-            weights = self.engine.scaling_factors(self.cfg.scaling_factor, ids,
-                                                  meta[:, 0].tolist(), meta[:, 1].tolist(),
-                                                  self.world)
-        else:
-            weights = scaling.compute(self.cfg.scaling_factor, meta[:, 0], meta[:, 1], self.world)
+        weights = self.aggregation_weights(meta)
         st = self.net.state
         if self.world > 1:
             opt_ops.scale_(st.model32, weights[self.rank])
@@ -159,14 +184,24 @@ class CollectiveFederation:
         self.num_local_updates = [max(1, int(math.ceil(t_max / max(1e-6, float(mpb)))))
                                   for mpb in meta[:, 2]]
 
+    def _quantifiers(self):
+        from metisfl_amd.ops.aggregate import count_zeros
+        st = self.net.state
+        segs = st.segments()
+        zeros = count_zeros(st.model32, segs)
+        lengths = [e - b for b, e in segs]
+        return zeros, [n * 4 for n in lengths], lengths
+
     def run_round(self) -> RoundRecord:
         self.global_iteration += 1
         started = time.time()
         n = self.num_local_updates[self.rank]
         res = self.local_train(n)
+        test = res.get("test") or {}
         row = torch.tensor([self.train_ds.n, res["completed_batches"], res["ms_per_batch"],
                             res["ms_per_epoch"], res["train_loss"], res["train_accuracy"],
-                            res["completed_epochs"], self.global_iteration],
+                            res["completed_epochs"], self.global_iteration,
+                            test.get("loss", float("nan")), test.get("accuracy", float("nan"))],
                            dtype=torch.float64, device=self.comm.device)
         meta = self.comm.all_gather_rows(row).cpu().numpy()
         completed = time.time()
@@ -175,8 +210,55 @@ class CollectiveFederation:
         rec = RoundRecord(self.global_iteration, started, completed, completed, agg_done,
                           (agg_done - started) * 1e3, res["ms"], agg_ms, meta, weights,
                           list(self.num_local_updates), res.get("test"))
-        if self.engine is not None and self.rank == 0:
-            self.engine.record_collective_round(rec, self.learner_ids)
+        if self.engine is not None:
+            self.engine.record_round(rec, self.cfg.batch_size,
+                                     self._quantifiers() if self.cfg.quantify else None)
         self.update_templates(meta)
         self.history.append(rec)
         return rec
+
+    # -- checkpoint / resume ------------------------------------------
+    def save_checkpoint(self, path: str) -> None:
+        """Collective: every rank writes its optimizer state; rank 0 also writes
+        the community model and the federation state.  The layout is plain
+        tensors + JSON (loadable with torch.load(weights_only=True))."""
+        os.makedirs(path, exist_ok=True)
+        st = self.net.state
+        self._sync()
+        per_rank = {"step": st.step.cpu(), "steps_done": torch.tensor(self.steps_done),
+                    "perm": self.train_ds.perm.cpu()}
+        for k in ("m", "v", "anchor"):
+            t = getattr(st, k)
+            if t is not None:
+                per_rank[k] = t.cpu()
+        torch.save(per_rank, os.path.join(path, f"rank{self.rank}.pt"))
+        if self.rank == 0:
+            torch.save({"model32": st.model32.cpu()}, os.path.join(path, "community.pt"))
+            with open(os.path.join(path, "federation.json"), "w") as f:
+                json.dump({"global_iteration": self.global_iteration,
+                           "num_local_updates": self.num_local_updates,
+                           "world": self.world, "learner_ids": self.learner_ids,
+                           "config": {k: v for k, v in asdict(self.cfg).items() if k != "extra"},
+                           "variables": [[s.name, list(s.shape), s.trainable] for s in st.specs],
+                           "history": [r.to_json() for r in self.history]}, f)
+        self.comm.barrier()
+
+    def resume(self, path: str) -> None:
+        """Reload a checkpoint written by ``save_checkpoint`` (same world size)."""
+        with open(os.path.join(path, "federation.json")) as f:
+            meta = json.load(f)
+        if meta["world"] != self.world:
+            raise ValueError(f"checkpoint has {meta['world']} learners, running {self.world}")
+        st = self.net.state
+        dev = st.model32.device
+        st.model32.copy_(torch.load(os.path.join(path, "community.pt"), weights_only=True)["model32"].to(dev))
+        st.refresh_bf16()
+        per_rank = torch.load(os.path.join(path, f"rank{self.rank}.pt"), weights_only=True)
+        st.step.copy_(per_rank["step"].to(dev))
+        for k in ("m", "v", "anchor"):
+            if k in per_rank and getattr(st, k) is not None:
+                getattr(st, k).copy_(per_rank[k].to(dev))
+        self.train_ds.perm.copy_(per_rank["perm"].to(self.train_ds.perm.device))
+        self.steps_done = int(per_rank["steps_done"])
+        self.global_iteration = int(meta["global_iteration"])
+        self.num_local_updates = list(meta["num_local_updates"])

@@ -238,3 +238,24 @@ def test_collective_round_recording():
     assert m.model_aggregation_total_duration_ms == pytest.approx(1.0)
     assert m.model_tensor_quantifiers[1].tensor_zeros == 2 and m.model_tensor_quantifiers[1].tensor_non_zeros == 0
     assert c.scaling_factors(["r0", "r1"], [100, 300], [1, 1]) == pytest.approx({"r0": 0.25, "r1": 0.75})
+
+
+def test_evicting_a_straggler_releases_the_sync_barrier():
+    c = E.Controller(params())
+    c.replace_community_model(fed_model([1, 1, 1]))
+    ids = []
+    for port, n in ((1, 10), (2, 10), (3, 10)):
+        lid, tok, _ = join(c, port, n)
+        ids.append((lid, tok))
+    (a, ta), (b, tb), (dead, _) = ids
+    assert c.learner_completed_task(a, ta, completed([2, 2, 2], 1))["run_tasks"] == []
+    assert c.learner_completed_task(b, tb, completed([4, 4, 4], 1))["run_tasks"] == []
+    gi = c.global_iteration()
+    d = c.evict_learner(dead)  # the straggler died: the barrier is complete now
+    assert sorted(l for l, _ in d["run_tasks"]) == sorted([a, b])
+    assert c.global_iteration() == gi + 1 and c.evicted() == 1 and c.num_learners() == 2
+    fm = controller_pb2.GetCommunityModelLineageResponse.FromString(c.community_model_lineage(1))
+    _, arrays, _ = model_to_arrays(fm.federated_models[0].model)
+    assert np.allclose(arrays[0], [3, 3, 3])
+    with pytest.raises(E.EngineStatusError):
+        c.evict_learner(dead)

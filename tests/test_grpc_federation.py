@@ -157,3 +157,33 @@ def test_static_resnet_learners_train_over_grpc(tmp_path):
     finally:
         client.shutdown()
         ctrl.stop()
+
+
+def test_dead_learner_is_evicted_and_sync_rounds_continue(tmp_path):
+    """Fault injection: a learner dies mid-federation (its server stops, it
+    never reports).  The health monitor evicts it and the synchronous barrier
+    completes with the survivors (the reference would wait forever)."""
+    from metisfl_amd.controller.servicer import ControllerServicer
+    from metisfl_amd.learner.fake import EchoModelOps
+    from metisfl_amd.utils.grpc_controller_client import GRPCControllerClient
+    srv = ControllerServicer(controller_params(), heartbeat_interval_s=0.2, heartbeat_threshold=2)
+    port = srv.start()
+    ent = M.construct_server_entity_pb("127.0.0.1", port)
+    client = GRPCControllerClient(ent)
+    try:
+        client.replace_community_model(1, model_from_arrays(["w"], [np.ones(4, np.float32)]))
+        learners = [start_learner(ent, EchoModelOps(0.05), tmp_path, i) for i in range(3)]
+        wait_for(lambda: srv.engine.global_iteration() >= 2, what="2 rounds with 3 learners")
+        victim, vsrv = learners[2]
+        vsrv.stop()                      # crash: no LeaveFederation
+        victim.shutdown()
+        gi = srv.engine.global_iteration()
+        wait_for(lambda: srv.engine.global_iteration() >= gi + 3, 30, "rounds after the crash")
+        assert victim.learner_id in srv.monitor.evicted
+        assert srv.engine.num_learners() == 2
+        for l, s in learners[:2]:
+            s.stop()
+            l.shutdown()
+    finally:
+        client.shutdown()
+        srv.stop()
