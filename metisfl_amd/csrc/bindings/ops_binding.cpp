@@ -356,6 +356,7 @@ void gather_batch(torch::Tensor shard, torch::Tensor labels, torch::Tensor perm,
 
 void register_conv(pybind11::module& m);
 void register_gemm(pybind11::module& m);
+void register_layers(pybind11::module& m);
 
 PYBIND11_MODULE(_ops, m) {
   m.doc() = "metisfl_amd hand-written HIP (gfx950) kernels";
@@ -375,4 +376,5 @@ PYBIND11_MODULE(_ops, m) {
   m.def("gather_batch", &gather_batch);
   register_conv(m);
   register_gemm(m);
+  register_layers(m);
 }

@@ -100,4 +100,18 @@ void launch_gather_batch(const uint16_t* shard, const int* labels, const int* pe
                          const int* step, int steps_per_epoch, int B, int64_t row_elems,
                          uint16_t* xb, int* yb, hipStream_t s);
 
+// ---- layers.hip (example-model layers) -------------------------------------
+void launch_bias_act_fwd(uint16_t* y, const float* bias, int64_t M, int N, int act, hipStream_t s);
+void launch_bias_act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dz, float* dbias, int64_t M,
+                         int N, int act, hipStream_t s);
+void launch_maxpool2(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, hipStream_t s);
+void launch_maxpool2_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, uint16_t* dx, int N,
+                         int H, int W, int C, hipStream_t s);
+void launch_dropout(const uint16_t* in, uint16_t* out, int64_t n, float p, uint32_t seed, const int* step,
+                    hipStream_t s);
+void launch_xent(const uint16_t* logits, const int* labels, int B, int Kp, int K, uint16_t* dlogits,
+                 float* stats, bool backward, hipStream_t s);
+void launch_mse(const uint16_t* pred, const float* target, int B, int Kp, uint16_t* dpred, float* stats,
+                bool backward, hipStream_t s);
+
 }  // namespace mfl

@@ -42,6 +42,9 @@ class VarSpec:
     fan_in: int = 0
     fan_out: int = 0
     offset: int = 0            # filled by FlatState
+    # rows (dim 0) >= live_rows are zero-initialised: padding units that the
+    # 8-wide kernels need stay exactly zero (inert) through training
+    live_rows: int | None = None
 
     @property
     def numel(self) -> int:
@@ -113,6 +116,10 @@ class FlatState:
                 val = rng.normal(0.0, 0.02, n).astype(np.float32)
             else:
                 val = np.zeros(n, np.float32)
+            if s.live_rows is not None and s.shape:
+                val = val.reshape(s.shape[0], -1)
+                val[s.live_rows:] = 0.0
+                val = val.reshape(-1)
             host[s.offset: s.offset + n] = val
         self.model32.copy_(torch.from_numpy(host))
         self.refresh_bf16()

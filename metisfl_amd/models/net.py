@@ -205,11 +205,16 @@ class StaticNet:
                      seed: int = 0, shuffle: bool = True, batch_size: int | None = None) -> DeviceDataset:
         """Upload a shard: pads channels to the model's input width, casts to bf16."""
         x = torch.as_tensor(x_nhwc)
-        if x.dim() == 4 and x.shape[-1] < self.input_shape[-1]:
+        if x.dim() > 2 and len(self.input_shape) == 1:
+            x = x.reshape(x.shape[0], -1)  # (N, H, W[, 1]) images into a flat MLP input
+        if x.shape[-1] < self.input_shape[-1]:
             pad = self.input_shape[-1] - x.shape[-1]
-            x = torch.nn.functional.pad(x, (0, pad))
+            x = torch.nn.functional.pad(x, (0, pad))  # zero channels / features up to the 8-wide rows
         x = x.to(torch.bfloat16).to(self.device)
-        y = torch.as_tensor(y).to(torch.int32).to(self.device)
+        y = torch.as_tensor(y)
+        if y.is_floating_point():  # regression targets: fp32 bits in the int32 label slots
+            y = y.to(torch.float32).contiguous().view(torch.int32)
+        y = y.to(torch.int32).to(self.device)
         return DeviceDataset(x, y, batch_size or self.B, seed=seed, shuffle=shuffle)
 
     @staticmethod

@@ -8,3 +8,21 @@ from metisfl_amd.models.model_def import register_family
 def _resnet18(batch_size, device="cpu", optimizer=None, seed=0, **kw):
     from metisfl_amd.models.resnet import ResNet18
     return ResNet18(batch_size=batch_size, device=device, optimizer=optimizer, seed=seed, **kw)
+
+
+@register_family("cifar_cnn")
+def _cifar_cnn(batch_size, device="cpu", optimizer=None, seed=0, **kw):
+    from metisfl_amd.models.sequential import CifarCNN
+    return CifarCNN(batch_size=batch_size, device=device, optimizer=optimizer, seed=seed, **kw)
+
+
+@register_family("fashion_mnist_fc")
+def _fashion_mnist_fc(batch_size, device="cpu", optimizer=None, seed=0, **kw):
+    from metisfl_amd.models.sequential import FashionMnistFC
+    return FashionMnistFC(batch_size=batch_size, device=device, optimizer=optimizer, seed=seed, **kw)
+
+
+@register_family("housing_mlp")
+def _housing_mlp(batch_size, device="cpu", optimizer=None, seed=0, **kw):
+    from metisfl_amd.models.sequential import HousingMLP
+    return HousingMLP(batch_size=batch_size, device=device, optimizer=optimizer, seed=seed, **kw)

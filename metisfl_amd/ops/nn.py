@@ -304,3 +304,116 @@ def gemm_nt(a, b, c, M: int, N: int, K: int, bias=None, epilogue: int = 0, aux=N
     if epilogue == 3:
         out = out + aux.float().reshape(M, N)
     c.copy_(out.reshape(c.shape).to(torch.bfloat16))
+
+
+# ---------------------------------------------------------------------------
+# example-model layers (layers.hip)
+ACT_NONE, ACT_RELU = 0, 1
+
+
+def bias_act(y, bias, N: int, act: int) -> None:
+    """y = act(y + bias) in place (bf16 [M][N], fp32 bias)."""
+    if y.is_cuda:
+        ops().bias_act(y, bias, N, act)
+        return
+    v = y.float().reshape(-1, N) + bias[:N]
+    if act == ACT_RELU:
+        v = v.clamp_min(0)
+    y.copy_(v.reshape(y.shape).to(torch.bfloat16))
+
+
+def bias_act_backward(dy, y, dz, dbias, N: int, act: int) -> None:
+    """dz = dy * act'(y); dbias += column sums of dz (dbias zero on entry)."""
+    if dy.is_cuda:
+        ops().bias_act_backward(dy, y, dz, dbias, N, act)
+        return
+    g = dy.float().reshape(-1, N)
+    if act == ACT_RELU:
+        g = torch.where(y.float().reshape(-1, N) > 0, g, torch.zeros_like(g))
+    g16 = g.to(torch.bfloat16)
+    dz.copy_(g16.reshape(dz.shape))
+    dbias[:N] += g16.float().sum(0)
+
+
+def maxpool2(x, y, N: int, H: int, W: int, C: int) -> None:
+    if x.is_cuda:
+        ops().maxpool2(x, y, N, H, W, C)
+        return
+    v = x.float().reshape(N, H // 2, 2, W // 2, 2, C).amax(dim=(2, 4))
+    y.copy_(v.reshape(y.shape).to(torch.bfloat16))
+
+
+def maxpool2_backward(dy, x, y, dx, N: int, H: int, W: int, C: int) -> None:
+    if dy.is_cuda:
+        ops().maxpool2_backward(dy, x, y, dx, N, H, W, C)
+        return
+    xv = x.float().reshape(N, H // 2, 2, W // 2, 2, C).permute(0, 1, 3, 5, 2, 4).reshape(N, H // 2, W // 2, C, 4)
+    m = y.float().reshape(N, H // 2, W // 2, C, 1)
+    hit = xv == m
+    first = hit & (hit.long().cumsum(-1) == 1)  # first maximal element of each window
+    g = first.float() * dy.float().reshape(N, H // 2, W // 2, C, 1)
+    g = g.reshape(N, H // 2, W // 2, C, 2, 2).permute(0, 1, 4, 2, 5, 3).reshape(N, H, W, C)
+    dx.copy_(g.to(torch.bfloat16))
+
+
+def _keep_mask_cpu(n: int, p: float, seed: int, step: int) -> torch.Tensor:
+    """Same hash as the HIP dropout kernel (lowbias32), on the host."""
+    M32 = 0xFFFFFFFF
+
+    def mix(x):
+        x = x ^ (x >> 16)
+        x = (x * 0x7FEB352D) & M32
+        x = x ^ (x >> 15)
+        x = (x * 0x846CA68B) & M32
+        return x ^ (x >> 16)
+
+    idx = torch.arange(n, dtype=torch.int64)
+    inner = ((step * 0x9E3779B9) & M32) ^ (idx & M32) ^ (((idx >> 32) * 0x85EBCA6B) & M32)
+    h = mix(seed ^ mix(inner))
+    thresh = min(int(p * 4294967296.0), M32)
+    return h >= thresh
+
+
+def dropout(inp, out, p: float, seed: int, step=None) -> None:
+    """Inverted dropout; the mask is a hash of (seed, device step, index), so
+    the backward pass (same call on dy) applies the identical mask."""
+    if inp.is_cuda:
+        ops().dropout(inp, out, p, seed, step)
+        return
+    st = int(step[0]) if step is not None else 0
+    keep = _keep_mask_cpu(inp.numel(), p, seed & 0xFFFFFFFF, st).reshape(inp.shape)
+    scale = 1.0 / (1.0 - p) if p < 1 else 0.0
+    out.copy_(torch.where(keep, inp.float() * scale, torch.zeros(())).to(torch.bfloat16))
+
+
+def xent(logits, labels, B: int, Kp: int, K: int, dlogits, stats) -> None:
+    """Softmax cross-entropy over the first K of Kp logit columns; dlogits =
+    (softmax - onehot)/B (None: forward only); stats += (loss, correct, n)."""
+    if logits.is_cuda:
+        ops().xent(logits, labels, B, Kp, K, dlogits, stats)
+        return
+    z = logits.float().reshape(B, Kp)[:, :K]
+    y = labels[:B].long()
+    lse = torch.logsumexp(z, 1)
+    stats[0] += float((lse - z.gather(1, y[:, None])[:, 0]).sum())
+    stats[1] += float((z.argmax(1) == y).sum())
+    stats[2] += float(B)
+    if dlogits is not None:
+        g = torch.zeros(B, Kp)
+        g[:, :K] = (torch.softmax(z, 1) - F.one_hot(y, K).float()) / B
+        dlogits.copy_(g.reshape(dlogits.shape).to(torch.bfloat16))
+
+
+def mse(pred, target, B: int, Kp: int, dpred, stats) -> None:
+    """Squared error on column 0 (fp32 targets); dpred = 2 (pred - t) / B."""
+    if pred.is_cuda:
+        ops().mse(pred, target, B, Kp, dpred, stats)
+        return
+    t = target[:B].view(torch.float32) if target.dtype == torch.int32 else target[:B].float()
+    d = pred.float().reshape(B, Kp)[:, 0] - t
+    stats[0] += float((d * d).sum())
+    stats[2] += float(B)
+    if dpred is not None:
+        g = torch.zeros(B, Kp)
+        g[:, 0] = 2 * d / B
+        dpred.copy_(g.reshape(dpred.shape).to(torch.bfloat16))
