@@ -51,6 +51,7 @@ struct ConvArgs {
   uint32_t src_bytes, wgt_bytes;  // buffer-descriptor ranges of src / wgt
   int kchunk;
   int accum;
+  int dbg;  // timing experiments only (MFL_CONV_DEBUG): bit0 skip MFMAs, bit1 skip operand DMA
   int c_shift, q_shift, pq_shift;
 };
 

@@ -310,6 +310,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int b_pch = lane % B_CPR;
 
   auto issue = [&](int kt, int stage) {
+    if (a.dbg & 2) return;
     uint8_t* st = smem + stage * STAGE;
     const int kb = kbeg + kt * BK;
     {
@@ -366,6 +367,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int stage) {
+    if (a.dbg & 1) return;
     const uint8_t* As = smem + stage * STAGE;
     const uint8_t* Bs = As + A_BYTES;
 #pragma unroll
@@ -395,65 +397,90 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int cl0 = wn * (BN / 2) + fr;
   const int splits = gridDim.z;
   const int tile_id = blockIdx.y * gridDim.x + blockIdx.x;
-  if (splits == 1) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) tile[(rl0 + 16 * i + e) * TST + cl0 + 16 * j] = acc[i][j][e];
-    __syncthreads();
-    tile_epilogue<BM, BN>(a, m0, n0, tile + BM * TST,
-                          [&](int rl, int cl, float* v) {
-                            const float4 p = *reinterpret_cast<const float4*>(tile + rl * TST + cl);
-                            const float4 q = *reinterpret_cast<const float4*>(tile + rl * TST + cl + 4);
-                            v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w;
-                            v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
-                          });
-    return;
-  }
-  // split-K: store this slice's slab [BM][BN] (tile-local, row-major)
-  const int ntiles = gridDim.x * gridDim.y;
-  float* slab = a.ysplit + ((int64_t)blockIdx.z * ntiles + tile_id) * (BM * BN);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) slab[(rl0 + 16 * i + e) * BN + cl0 + 16 * j] = acc[i][j][e];
-  // publish: every wave drains its stores, one agent-scope release, then the
-  // ticket; the last slice to arrive reduces (guide: In-launch split-K).
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int e = 0; e < 4; ++e) tile[(rl0 + 16 * i + e) * TST + cl0 + 16 * j] = acc[i][j][e];
   __syncthreads();
-  int* flag = reinterpret_cast<int*>(smem);
-  if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int prev = __hip_atomic_fetch_add(&a.counters[tile_id], 1, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == splits - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // re-arm for the next launch (graph replay): nobody else touches it now
-      __hip_atomic_store(&a.counters[tile_id], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (splits > 1) {
+    // Split-K, in-launch (guide §5 'In-launch split-K reduction', write-
+    // through form).  Every slice publishes its fp32 slab [BM][BN] with sc1
+    // (write-through) 16-B stores -- no agent release, whose L2 write-back
+    // of the freshly dirtied slab measured ~5 µs per launch here -- drains
+    // them, and draws a ticket; the last arriver adds the other slabs (sc1
+    // loads: misses its own possibly stale L2) onto its own LDS tile.
+    constexpr int F = BM * BN / 1024;  // float4 per thread
+    constexpr int C4 = BN / 4;
+    const int ntiles = gridDim.x * gridDim.y;
+    const int64_t zstride = (int64_t)ntiles * BM * BN * 4;  // bytes between slices
+    const auto rsS = make_rsrc(a.ysplit + (int64_t)tile_id * (BM * BN), 0x7FFFFFF0u);
+    const uint32_t zoff = (uint32_t)(blockIdx.z * zstride);
+#pragma unroll
+    for (int u = 0; u < F; ++u) {
+      const int f = t + 256 * u;
+      const float4 v = *reinterpret_cast<const float4*>(tile + (f / C4) * TST + (f % C4) * 4);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)},
+          rsS, (int)(zoff + f * 16), 0, 16);
     }
-    flag[0] = last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(tile + BM * TST + 256 * 16);
+    if (t == 0) {
+      const int prev = __hip_atomic_fetch_add(&a.counters[tile_id], 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == splits - 1;
+      // re-arm for the next launch (graph replay): nobody else touches it now
+      if (last) __hip_atomic_store(&a.counters[tile_id], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    float4 sum[F];
+#pragma unroll
+    for (int u = 0; u < F; ++u) sum[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // slices summed in z order whichever slice reduces: bitwise deterministic
+    for (int z = 0; z < splits; ++z) {
+      float4 r[F];
+      if (z == (int)blockIdx.z) {
+#pragma unroll
+        for (int u = 0; u < F; ++u) {
+          const int f = t + 256 * u;
+          r[u] = *reinterpret_cast<const float4*>(tile + (f / C4) * TST + (f % C4) * 4);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < F; ++u) {
+          const u32x4 b =
+              __builtin_amdgcn_raw_buffer_load_b128(rsS, (int)(z * zstride + (t + 256 * u) * 16), 0, 16);
+          r[u] = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]),
+                             __uint_as_float(b[3]));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < F; ++u) {
+        sum[u].x += r[u].x;
+        sum[u].y += r[u].y;
+        sum[u].z += r[u].z;
+        sum[u].w += r[u].w;
+      }
+    }
+    __syncthreads();  // every thread has read its own-slice values from the tile
+#pragma unroll
+    for (int u = 0; u < F; ++u) {
+      const int f = t + 256 * u;
+      *reinterpret_cast<float4*>(tile + (f / C4) * TST + (f % C4) * 4) = sum[u];
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  if (!flag[0]) return;
-  const float* base = a.ysplit + (int64_t)tile_id * (BM * BN);
-  const int64_t zstride = (int64_t)ntiles * BM * BN;
-  tile_epilogue<BM, BN>(a, m0, n0, reinterpret_cast<float*>(smem) + 4,
+  tile_epilogue<BM, BN>(a, m0, n0, tile + BM * TST,
                         [&](int rl, int cl, float* v) {
-                          for (int k = 0; k < 8; ++k) v[k] = 0.f;
-                          for (int z = 0; z < splits; ++z) {
-                            const float* p = base + z * zstride + rl * BN + cl;
-                            const float4 x0 = *reinterpret_cast<const float4*>(p);
-                            const float4 x1 = *reinterpret_cast<const float4*>(p + 4);
-                            v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
-                            v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
-                          }
+                          const float4 p = *reinterpret_cast<const float4*>(tile + rl * TST + cl);
+                          const float4 q = *reinterpret_cast<const float4*>(tile + rl * TST + cl + 4);
+                          v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w;
+                          v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
                         });
 }
 
@@ -501,6 +528,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
   const int PQ = g.P * g.Q;
 
   auto issue = [&](int kt, int stage) {
+    if (a.dbg & 2) return;
     uint8_t* st = smem + stage * STAGE;
     const int mb = mbeg + kt * BK;
 #pragma unroll
@@ -526,6 +554,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
 #pragma unroll
     for (int jj = 0; jj < TN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int stage) {
+    if (a.dbg & 1) return;
     const uint8_t* As = smem + stage * STAGE;
     const uint8_t* Bs = As + T_BYTES;
 #pragma unroll
@@ -596,6 +625,11 @@ static void fill_shifts(ConvArgs& a) {
   a.c_shift = log2_exact(a.g.C);
   a.q_shift = log2_exact(a.g.Q);
   a.pq_shift = log2_exact(a.g.P * a.g.Q);
+  static const int dbg = [] {
+    const char* v = getenv("MFL_CONV_DEBUG");
+    return v && *v ? atoi(v) : 0;
+  }();
+  a.dbg = dbg;
 }
 
 template <typename K>

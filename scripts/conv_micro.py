@@ -1,7 +1,10 @@
 """Per-layer conv microbenchmark (ResNet-18 CIFAR shapes, batch 32): times
 fwd / dgrad / wgrad of every distinct layer with HIP events and prints a
 table; also the workload for rocprofv3 --pmc counter runs."""
+import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 import torch
 
@@ -13,8 +16,27 @@ SHAPES = [(32, 32, 32, 8, 64, 3, 1), (32, 32, 32, 64, 64, 3, 1), (32, 32, 32, 64
           (32, 8, 8, 256, 512, 1, 2), (32, 4, 4, 512, 512, 3, 1)]
 
 
+def graph_us(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
 def main(iters=50):
     dev = torch.device("cuda")
+    one = torch.zeros(1, device=dev)
+    print(f"trivial kernel (1-element add_) per launch in a graph: {graph_us(lambda: one.add_(1), 200):.2f}us")
     for (N, H, W, C, Co, k, s) in SHAPES:
         shp = K.ConvShape(N, H, W, C, Co, k, k, s, k // 2)
         x = torch.randn(N, H, W, C, device=dev).bfloat16()
@@ -33,10 +55,17 @@ def main(iters=50):
                 continue
             fn()
             torch.cuda.synchronize()
+            # replay a captured graph of `iters` launches: per-launch CPU
+            # overhead is out of the measurement, as in the training step
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(iters):
+                    fn()
+            g.replay()
+            torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for _ in range(iters):
-                fn()
+            g.replay()
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / iters
