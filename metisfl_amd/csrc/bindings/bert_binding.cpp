@@ -1,0 +1,320 @@
+// torch binding for the BERT-base path: Linear-layer GEMMs (gemm.hip) and the
+// encoder kernels (bert.hip).  Shapes are validated here before any launch.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include "kernels/bert.h"
+#include "kernels/gemm.h"
+
+namespace {
+
+hipStream_t stream_of(const torch::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+uint16_t* bfp(const torch::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+void need(const torch::Tensor& t, torch::ScalarType dt, int64_t numel, const char* nm) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), nm, " must be a contiguous device tensor");
+  TORCH_CHECK(t.scalar_type() == dt, nm, " has the wrong dtype");
+  TORCH_CHECK(numel < 0 || t.numel() == numel, nm, " has ", t.numel(), " elements, expected ", numel);
+}
+void need_min(const torch::Tensor& t, torch::ScalarType dt, int64_t numel, const char* nm) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), nm, " must be a contiguous device tensor");
+  TORCH_CHECK(t.scalar_type() == dt, nm, " has the wrong dtype");
+  TORCH_CHECK(t.numel() >= numel, nm, " too small");
+}
+template <typename T>
+T* opt_ptr(const c10::optional<torch::Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+void dense_dims(int64_t M, int64_t N, int64_t K) {
+  TORCH_CHECK(M > 0 && N % 8 == 0 && K % 8 == 0, "GEMM N and K must be multiples of 8");
+  TORCH_CHECK(M * std::max(N, K) < (1LL << 31), "GEMM operand too large for 32-bit indexing");
+}
+
+// y[M][N] = x[M][K] w[N][K]^T (+ bias) (+ resid); act_out = gelu(y)
+void gemm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::optional<torch::Tensor> bias,
+              c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> act_out, int64_t M, int64_t N,
+              int64_t K) {
+  dense_dims(M, N, K);
+  need(x, torch::kBFloat16, M * K, "x");
+  need(w, torch::kBFloat16, N * K, "w");
+  need(y, torch::kBFloat16, M * N, "y");
+  if (bias.has_value() && bias->defined()) need_min(*bias, torch::kFloat32, N, "bias");
+  if (resid.has_value() && resid->defined()) need(*resid, torch::kBFloat16, M * N, "resid");
+  if (act_out.has_value() && act_out->defined()) need(*act_out, torch::kBFloat16, M * N, "act_out");
+  mfl::launch_gemm_fwd(bfp(x), bfp(w), bfp(y), opt_ptr<const float>(bias), opt_ptr<const uint16_t>(resid),
+                       opt_ptr<uint16_t>(act_out), (int)M, (int)N, (int)K, stream_of(x));
+}
+
+// dx[M][K] (+)= dy[M][N] w[N][K]
+void gemm_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, int64_t M, int64_t N, int64_t K,
+                bool accumulate) {
+  dense_dims(M, N, K);
+  need(dy, torch::kBFloat16, M * N, "dy");
+  need(w, torch::kBFloat16, N * K, "w");
+  need(dx, torch::kBFloat16, M * K, "dx");
+  mfl::launch_gemm_dgrad(bfp(dy), bfp(w), bfp(dx), (int)M, (int)N, (int)K, accumulate, stream_of(dy));
+}
+
+// dw[N][K] (+)= dy^T x  (fp32)
+void gemm_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t M, int64_t N, int64_t K,
+                bool accumulate) {
+  dense_dims(M, N, K);
+  need(x, torch::kBFloat16, M * K, "x");
+  need(dy, torch::kBFloat16, M * N, "dy");
+  need(dw, torch::kFloat32, N * K, "dw");
+  if (!accumulate && mfl::gemm_wgrad_splits((int)M, (int)N, (int)K))
+    (void)hipMemsetAsync(dw.data_ptr<float>(), 0, dw.numel() * sizeof(float), stream_of(x));
+  mfl::launch_gemm_wgrad(bfp(x), bfp(dy), dw.data_ptr<float>(), (int)M, (int)N, (int)K, accumulate,
+                         stream_of(x));
+}
+
+void ln_dims(int64_t H) {
+  TORCH_CHECK(H % 256 == 0 && H <= 1024, "LayerNorm width must be 256, 512, 768 or 1024");
+}
+
+void ln_fwd(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, torch::Tensor y, torch::Tensor mean,
+            torch::Tensor rstd, int64_t M, int64_t H, double eps) {
+  ln_dims(H);
+  need(x, torch::kBFloat16, M * H, "x");
+  need(y, torch::kBFloat16, M * H, "y");
+  need(gamma, torch::kFloat32, H, "gamma");
+  need(beta, torch::kFloat32, H, "beta");
+  need_min(mean, torch::kFloat32, M, "mean");
+  need_min(rstd, torch::kFloat32, M, "rstd");
+  mfl::LnFwdArgs a;
+  a.x = bfp(x);
+  a.gamma = gamma.data_ptr<float>();
+  a.beta = beta.data_ptr<float>();
+  a.y = bfp(y);
+  a.mean = mean.data_ptr<float>();
+  a.rstd = rstd.data_ptr<float>();
+  a.M = (int)M;
+  a.eps = (float)eps;
+  mfl::launch_ln_fwd(a, (int)H, false, stream_of(x));
+}
+
+void emb_ln_fwd(torch::Tensor rec, int64_t rec_stride, int64_t B, int64_t T, torch::Tensor word,
+                torch::Tensor pos, torch::Tensor type, torch::Tensor xsave, torch::Tensor gamma,
+                torch::Tensor beta, torch::Tensor y, torch::Tensor mean, torch::Tensor rstd, int64_t H,
+                double eps) {
+  ln_dims(H);
+  const int64_t M = B * T;
+  need_min(rec, torch::kInt32, B * rec_stride, "rec");
+  TORCH_CHECK(rec_stride >= T, "record stride");
+  TORCH_CHECK(word.numel() % H == 0 && pos.numel() >= T * H && type.numel() >= H, "embedding tables");
+  need(word, torch::kBFloat16, -1, "word");
+  need(pos, torch::kBFloat16, -1, "pos");
+  need(type, torch::kBFloat16, -1, "type");
+  need(xsave, torch::kBFloat16, M * H, "xsave");
+  need(y, torch::kBFloat16, M * H, "y");
+  need(gamma, torch::kFloat32, H, "gamma");
+  need(beta, torch::kFloat32, H, "beta");
+  need_min(mean, torch::kFloat32, M, "mean");
+  need_min(rstd, torch::kFloat32, M, "rstd");
+  mfl::LnFwdArgs a;
+  a.tokens = rec.data_ptr<int>();
+  a.tok_stride = (int)rec_stride;
+  a.T = (int)T;
+  a.word = bfp(word);
+  a.pos = bfp(pos);
+  a.type = bfp(type);
+  a.xsave = bfp(xsave);
+  a.gamma = gamma.data_ptr<float>();
+  a.beta = beta.data_ptr<float>();
+  a.y = bfp(y);
+  a.mean = mean.data_ptr<float>();
+  a.rstd = rstd.data_ptr<float>();
+  a.M = (int)M;
+  a.eps = (float)eps;
+  mfl::launch_ln_fwd(a, (int)H, true, stream_of(y));
+}
+
+void ln_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd, torch::Tensor gamma,
+            torch::Tensor dx, c10::optional<torch::Tensor> dx2, torch::Tensor dgamma, torch::Tensor dbeta,
+            c10::optional<torch::Tensor> dbias_prev, int64_t M, int64_t H) {
+  ln_dims(H);
+  need(dy, torch::kBFloat16, M * H, "dy");
+  need(x, torch::kBFloat16, M * H, "x");
+  need(dx, torch::kBFloat16, M * H, "dx");
+  if (dx2.has_value() && dx2->defined()) need(*dx2, torch::kBFloat16, M * H, "dx2");
+  need(gamma, torch::kFloat32, H, "gamma");
+  need(dgamma, torch::kFloat32, H, "dgamma");
+  need(dbeta, torch::kFloat32, H, "dbeta");
+  if (dbias_prev.has_value() && dbias_prev->defined()) need(*dbias_prev, torch::kFloat32, H, "dbias_prev");
+  need_min(mean, torch::kFloat32, M, "mean");
+  need_min(rstd, torch::kFloat32, M, "rstd");
+  mfl::LnBwdArgs a;
+  a.dy = bfp(dy);
+  a.x = bfp(x);
+  a.mean = mean.data_ptr<float>();
+  a.rstd = rstd.data_ptr<float>();
+  a.gamma = gamma.data_ptr<float>();
+  a.dx = bfp(dx);
+  a.dx2 = opt_ptr<uint16_t>(dx2);
+  a.dgamma = dgamma.data_ptr<float>();
+  a.dbeta = dbeta.data_ptr<float>();
+  a.dbias_prev = opt_ptr<float>(dbias_prev);
+  a.M = (int)M;
+  mfl::launch_ln_bwd(a, (int)H, false, stream_of(dy));
+}
+
+void emb_ln_bwd(torch::Tensor dy, torch::Tensor xsave, torch::Tensor mean, torch::Tensor rstd,
+                torch::Tensor gamma, torch::Tensor rec, int64_t rec_stride, int64_t B, int64_t T,
+                torch::Tensor dword, torch::Tensor dpos, torch::Tensor dtype, torch::Tensor dgamma,
+                torch::Tensor dbeta, int64_t H) {
+  ln_dims(H);
+  const int64_t M = B * T;
+  need(dy, torch::kBFloat16, M * H, "dy");
+  need(xsave, torch::kBFloat16, M * H, "xsave");
+  need(gamma, torch::kFloat32, H, "gamma");
+  need(dgamma, torch::kFloat32, H, "dgamma");
+  need(dbeta, torch::kFloat32, H, "dbeta");
+  need_min(rec, torch::kInt32, B * rec_stride, "rec");
+  need(dword, torch::kFloat32, -1, "dword");
+  need_min(dpos, torch::kFloat32, T * H, "dpos");
+  need_min(dtype, torch::kFloat32, H, "dtype");
+  TORCH_CHECK(dword.numel() % H == 0, "dword shape");
+  need_min(mean, torch::kFloat32, M, "mean");
+  need_min(rstd, torch::kFloat32, M, "rstd");
+  mfl::LnBwdArgs a;
+  a.dy = bfp(dy);
+  a.x = bfp(xsave);
+  a.mean = mean.data_ptr<float>();
+  a.rstd = rstd.data_ptr<float>();
+  a.gamma = gamma.data_ptr<float>();
+  a.dgamma = dgamma.data_ptr<float>();
+  a.dbeta = dbeta.data_ptr<float>();
+  a.tokens = rec.data_ptr<int>();
+  a.tok_stride = (int)rec_stride;
+  a.T = (int)T;
+  a.dword = dword.data_ptr<float>();
+  a.dpos = dpos.data_ptr<float>();
+  a.dtype = dtype.data_ptr<float>();
+  a.M = (int)M;
+  mfl::launch_ln_bwd(a, (int)H, true, stream_of(dy));
+}
+
+void gelu_bwd(torch::Tensor dh, torch::Tensor z, torch::Tensor dz, c10::optional<torch::Tensor> dbias,
+              int64_t M, int64_t N) {
+  TORCH_CHECK(N % 8 == 0, "gelu_bwd width");
+  need(dh, torch::kBFloat16, M * N, "dh");
+  need(z, torch::kBFloat16, M * N, "z");
+  need(dz, torch::kBFloat16, M * N, "dz");
+  if (dbias.has_value() && dbias->defined()) need(*dbias, torch::kFloat32, N, "dbias");
+  mfl::launch_gelu_bwd(bfp(dh), bfp(z), bfp(dz), opt_ptr<float>(dbias), (int)M, (int)N, stream_of(dh));
+}
+
+void colsum(torch::Tensor dy, torch::Tensor dbias, int64_t M, int64_t N) {
+  TORCH_CHECK(N % 8 == 0, "colsum width");
+  need(dy, torch::kBFloat16, M * N, "dy");
+  need(dbias, torch::kFloat32, N, "dbias");
+  mfl::launch_colsum(bfp(dy), dbias.data_ptr<float>(), (int)M, (int)N, stream_of(dy));
+}
+
+void attn_dims(const torch::Tensor& qkv, int64_t B, int64_t heads) {
+  TORCH_CHECK(heads > 0 && B > 0, "attention dims");
+  need(qkv, torch::kBFloat16, B * 128 * 3 * heads * 64, "qkv (seq 128, head dim 64)");
+}
+
+void attn_fwd(torch::Tensor qkv, torch::Tensor ctx, torch::Tensor lse, int64_t B, int64_t heads, double scale) {
+  attn_dims(qkv, B, heads);
+  need(ctx, torch::kBFloat16, B * 128 * heads * 64, "ctx");
+  need_min(lse, torch::kFloat32, B * heads * 128, "lse");
+  mfl::AttnArgs a;
+  a.qkv = bfp(qkv);
+  a.ctx = bfp(ctx);
+  a.lse = lse.data_ptr<float>();
+  a.batch = (int)B;
+  a.heads = (int)heads;
+  a.scale = (float)scale;
+  mfl::launch_attn_fwd(a, stream_of(qkv));
+}
+
+void attn_bwd(torch::Tensor qkv, torch::Tensor ctx, torch::Tensor lse, torch::Tensor dctx, torch::Tensor dqkv,
+              c10::optional<torch::Tensor> dbias, int64_t B, int64_t heads, double scale) {
+  attn_dims(qkv, B, heads);
+  need(ctx, torch::kBFloat16, B * 128 * heads * 64, "ctx");
+  need(dctx, torch::kBFloat16, B * 128 * heads * 64, "dctx");
+  need(dqkv, torch::kBFloat16, qkv.numel(), "dqkv");
+  need_min(lse, torch::kFloat32, B * heads * 128, "lse");
+  if (dbias.has_value() && dbias->defined()) need(*dbias, torch::kFloat32, 3 * heads * 64, "dbias");
+  mfl::AttnArgs a;
+  a.qkv = bfp(qkv);
+  a.ctx = bfp(ctx);
+  a.lse = lse.data_ptr<float>();
+  a.dctx = bfp(dctx);
+  a.dqkv = bfp(dqkv);
+  a.dbias = opt_ptr<float>(dbias);
+  a.batch = (int)B;
+  a.heads = (int)heads;
+  a.scale = (float)scale;
+  mfl::launch_attn_bwd(a, stream_of(qkv));
+}
+
+void rec_dims(const torch::Tensor& rec, int64_t rec_stride, int64_t B, int64_t T, int64_t P) {
+  need_min(rec, torch::kInt32, B * rec_stride, "rec");
+  TORCH_CHECK(rec_stride >= 2 * T + 2 * P, "record stride < 2T + 2P");
+}
+
+void mlm_gather(torch::Tensor x, torch::Tensor rec, int64_t rec_stride, int64_t B, int64_t T, int64_t P,
+                torch::Tensor out, int64_t H) {
+  rec_dims(rec, rec_stride, B, T, P);
+  TORCH_CHECK(H % 8 == 0, "width");
+  need(x, torch::kBFloat16, B * T * H, "x");
+  need(out, torch::kBFloat16, B * P * H, "out");
+  mfl::launch_mlm_gather(bfp(x), rec.data_ptr<int>(), (int)rec_stride, (int)B, (int)T, (int)P, (int)H, bfp(out),
+                         stream_of(x));
+}
+
+void mlm_scatter(torch::Tensor dsel, torch::Tensor rec, int64_t rec_stride, int64_t B, int64_t T, int64_t P,
+                 torch::Tensor dx, int64_t H) {
+  rec_dims(rec, rec_stride, B, T, P);
+  TORCH_CHECK(H % 8 == 0, "width");
+  need(dsel, torch::kBFloat16, B * P * H, "dsel");
+  need(dx, torch::kBFloat16, B * T * H, "dx");
+  mfl::launch_mlm_scatter(bfp(dsel), rec.data_ptr<int>(), (int)rec_stride, (int)B, (int)T, (int)P, (int)H,
+                          bfp(dx), stream_of(dx));
+}
+
+void vocab_xent(torch::Tensor logits, c10::optional<torch::Tensor> dlogits, torch::Tensor rec, int64_t rec_stride,
+                int64_t B, int64_t T, int64_t P, int64_t V, int64_t Vp, torch::Tensor stats) {
+  rec_dims(rec, rec_stride, B, T, P);
+  TORCH_CHECK(Vp % 8 == 0 && V <= Vp, "vocab padding");
+  need(logits, torch::kBFloat16, B * P * Vp, "logits");
+  if (dlogits.has_value() && dlogits->defined()) need(*dlogits, torch::kBFloat16, B * P * Vp, "dlogits");
+  need_min(stats, torch::kFloat32, 3, "stats");
+  mfl::VocabXentArgs a;
+  a.logits = bfp(logits);
+  a.dlogits = opt_ptr<uint16_t>(dlogits);
+  a.rec = rec.data_ptr<int>();
+  a.rec_stride = (int)rec_stride;
+  a.T = (int)T;
+  a.P = (int)P;
+  a.R = (int)(B * P);
+  a.V = (int)V;
+  a.Vp = (int)Vp;
+  a.stats = stats.data_ptr<float>();
+  mfl::launch_vocab_xent(a, stream_of(logits));
+}
+
+}  // namespace
+
+void register_bert(pybind11::module& m) {
+  m.def("gemm_fwd", &gemm_fwd);
+  m.def("gemm_dgrad", &gemm_dgrad);
+  m.def("gemm_wgrad", &gemm_wgrad);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("emb_ln_fwd", &emb_ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
+  m.def("emb_ln_bwd", &emb_ln_bwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("colsum", &colsum);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("mlm_gather", &mlm_gather);
+  m.def("mlm_scatter", &mlm_scatter);
+  m.def("vocab_xent", &vocab_xent);
+}

@@ -357,6 +357,7 @@ void gather_batch(torch::Tensor shard, torch::Tensor labels, torch::Tensor perm,
 void register_conv(pybind11::module& m);
 void register_gemm(pybind11::module& m);
 void register_layers(pybind11::module& m);
+void register_bert(pybind11::module& m);
 
 PYBIND11_MODULE(_ops, m) {
   m.doc() = "metisfl_amd hand-written HIP (gfx950) kernels";
@@ -377,4 +378,5 @@ PYBIND11_MODULE(_ops, m) {
   register_conv(m);
   register_gemm(m);
   register_layers(m);
+  register_bert(m);
 }

@@ -1,0 +1,82 @@
+// BERT-base kernel entry points (bert.hip).  All launchers take the stream
+// explicitly and allocate nothing (hipGraph-capturable).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mfl {
+
+struct LnFwdArgs {
+  const uint16_t* x = nullptr;  // [M][H] LN input (non-embedding variant)
+  // embedding variant: x = word[tok] + pos[t] + type[0], stored to xsave
+  const int* tokens = nullptr;
+  int tok_stride = 0, T = 1;
+  const uint16_t* word = nullptr;
+  const uint16_t* pos = nullptr;
+  const uint16_t* type = nullptr;
+  uint16_t* xsave = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  uint16_t* y = nullptr;
+  float* mean = nullptr;
+  float* rstd = nullptr;
+  int M = 0;
+  float eps = 1e-12f;
+};
+
+struct LnBwdArgs {
+  const uint16_t* dy = nullptr;
+  const uint16_t* x = nullptr;  // LN input
+  const float* mean = nullptr;
+  const float* rstd = nullptr;
+  const float* gamma = nullptr;
+  uint16_t* dx = nullptr;
+  uint16_t* dx2 = nullptr;        // optional second copy (residual branch)
+  float* dgamma = nullptr;
+  float* dbeta = nullptr;
+  float* dbias_prev = nullptr;    // optional: += column sums of dx
+  // embedding variant: dx scattered into the tables (fp32 grads)
+  const int* tokens = nullptr;
+  int tok_stride = 0, T = 1;
+  float* dword = nullptr;
+  float* dpos = nullptr;
+  float* dtype = nullptr;
+  int M = 0;
+};
+
+struct AttnArgs {
+  const uint16_t* qkv = nullptr;  // [B*T][3H]: q | k | v, head h at columns h*64
+  uint16_t* ctx = nullptr;        // [B*T][H] (forward output)
+  float* lse = nullptr;           // [B][heads][T] natural-log softmax normaliser
+  const uint16_t* dctx = nullptr;
+  uint16_t* dqkv = nullptr;
+  float* dbias = nullptr;         // optional [3H] qkv bias gradient (+=)
+  int batch = 0, heads = 0;
+  float scale = 0.125f;
+};
+
+struct VocabXentArgs {
+  const uint16_t* logits = nullptr;  // [R][Vp]
+  uint16_t* dlogits = nullptr;       // optional [R][Vp]
+  const int* rec = nullptr;          // batch records (labels inside)
+  int rec_stride = 0, T = 0, P = 0;
+  int R = 0, V = 0, Vp = 0;
+  float* stats = nullptr;            // [loss, correct, count]
+};
+
+void launch_ln_fwd(const LnFwdArgs& a, int H, bool emb, hipStream_t s);
+void launch_ln_bwd(const LnBwdArgs& a, int H, bool emb, hipStream_t s);
+void launch_gelu_bwd(const uint16_t* dh, const uint16_t* z, uint16_t* dz, float* dbias, int M, int N,
+                     hipStream_t s);
+void launch_colsum(const uint16_t* dy, float* dbias, int M, int N, hipStream_t s);
+size_t attn_fwd_lds();
+size_t attn_bwd_lds();
+void launch_attn_fwd(const AttnArgs& a, hipStream_t s);
+void launch_attn_bwd(const AttnArgs& a, hipStream_t s);
+void launch_mlm_gather(const uint16_t* x, const int* rec, int rec_stride, int B, int T, int P, int H,
+                       uint16_t* out, hipStream_t s);
+void launch_mlm_scatter(const uint16_t* dsel, const int* rec, int rec_stride, int B, int T, int P, int H,
+                        uint16_t* dx, hipStream_t s);
+void launch_vocab_xent(const VocabXentArgs& a, hipStream_t s);
+
+}  // namespace mfl

@@ -1,0 +1,714 @@
+// BERT-base training kernels for gfx950 (SURVEY §2.10 K12/K13 LayerNorm, K14
+// softmax cross-entropy, K15 fused epilogues, §5.7 fused attention).  The
+// reference has no transformer (its largest model is a Keras CNN); SURVEY
+// §7.2 step 10 adds BERT-base as the GEMM-heavy workload of the new build.
+// The GEMMs run on gemm.hip (MFMA implicit-GEMM core with fused bias /
+// residual / GELU epilogue); everything else of a post-LN encoder layer is
+// here, each op fused so that one launch reads its inputs once:
+//
+//  * ln_fwd       LayerNorm (+ the embedding gather word+pos+type for the
+//                 first one), mean / rstd saved for backward.
+//  * ln_bwd       LayerNorm backward + dgamma / dbeta + the bias gradient of
+//                 the GEMM that produced the LN input (= column sums of dx)
+//                 + an optional second copy of dx (the residual branch) --
+//                 or, for the embedding LN, the scatter of dx into the word /
+//                 position / type tables.
+//  * gelu_bwd     dz = dh * gelu'(z) and the FFN-1 bias gradient.
+//  * attention    seq 128, head dim 64: one workgroup per (sequence, head)
+//                 holds K, V (and for backward Q, dO, P, dS) in LDS; QK^T,
+//                 PV, dO V^T, dS K, dS^T Q, P^T dO all on MFMA 16x16x32 with
+//                 transposing LDS reads for the column-major operands; the
+//                 softmax never leaves registers; the qkv bias gradient is
+//                 reduced in the same kernel.
+//  * mlm_*        gather of the masked positions, vocab-wide softmax CE with
+//                 16-B loads, scatter of their gradient back to the sequence.
+#include "kernels/common.h"
+#include "kernels/bert.h"
+
+namespace mfl {
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float hsum32(float v) {  // sum over a 32-lane half-wave
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// =============================================================================
+// LayerNorm.  Rows of H = 256 * V elements; a half-wave (32 lanes) per row,
+// lane j owns the 16-B column groups (v * 32 + j) for v < V; 8 rows per
+// 256-thread block and pass.
+template <int V, bool EMB>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwdArgs a) {
+  const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
+  const int row = blockIdx.x * 8 + hw;
+  if (row >= a.M) return;
+  constexpr int H = 256 * V;
+  float x[V][8];
+  if constexpr (EMB) {
+    const int b = row / a.T, t = row - b * a.T;
+    const int tok = a.tokens[(int64_t)b * a.tok_stride + t];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int c = (v * 32 + j) * 8;
+      float w[8], p[8], ty[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.word + (int64_t)tok * H + c), w);
+      unpack8(*reinterpret_cast<const uint4*>(a.pos + (int64_t)t * H + c), p);
+      unpack8(*reinterpret_cast<const uint4*>(a.type + c), ty);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[v][k] = w[k] + p[k] + ty[k];
+      // keep the (bf16-rounded) LN input for backward
+      const uint4 pk = pack8(x[v]);
+      *reinterpret_cast<uint4*>(a.xsave + (int64_t)row * H + c) = pk;
+      unpack8(pk, x[v]);
+    }
+  } else {
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      unpack8(*reinterpret_cast<const uint4*>(a.x + (int64_t)row * H + (v * 32 + j) * 8), x[v]);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += x[v][k];
+  const float mean = hsum32(s) * (1.f / H);
+  float q = 0.f;
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float d = x[v][k] - mean;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(hsum32(q) * (1.f / H) + a.eps);
+  if (j == 0) {
+    a.mean[row] = mean;
+    a.rstd[row] = rstd;
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int c = (v * 32 + j) * 8;
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = (x[v][k] - mean) * rstd * a.gamma[c + k] + a.beta[c + k];
+    *reinterpret_cast<uint4*>(a.y + (int64_t)row * H + c) = pack8(o);
+  }
+}
+
+constexpr int kLnBwdRows = 32;  // rows per block (4 passes of 8 half-waves)
+
+template <int V, bool EMB>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
+  constexpr int H = 256 * V;
+  __shared__ float red[3][H];  // dgamma, dbeta, dbias_prev (or dtype) partials
+  for (int i = threadIdx.x; i < 3 * H; i += 256) (&red[0][0])[i] = 0.f;
+  __syncthreads();
+  const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
+  float pg[V][8], pb[V][8], pd[V][8];
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pg[v][k] = pb[v][k] = pd[v][k] = 0.f;
+  for (int pass = 0; pass < kLnBwdRows / 8; ++pass) {
+    const int row = blockIdx.x * kLnBwdRows + pass * 8 + hw;
+    if (row >= a.M) break;  // uniform per half-wave
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    float dy[V][8], xh[V][8], gg[V][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int c = (v * 32 + j) * 8;
+      float xv[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.dy + (int64_t)row * H + c), dy[v]);
+      unpack8(*reinterpret_cast<const uint4*>(a.x + (int64_t)row * H + c), xv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        xh[v][k] = (xv[k] - mean) * rstd;
+        gg[v][k] = dy[v][k] * a.gamma[c + k];
+        s1 += gg[v][k];
+        s2 += gg[v][k] * xh[v][k];
+        pg[v][k] += dy[v][k] * xh[v][k];
+        pb[v][k] += dy[v][k];
+      }
+    }
+    const float m1 = hsum32(s1) * (1.f / H), m2 = hsum32(s2) * (1.f / H);
+    int b = 0, t = 0, tok = 0;
+    if constexpr (EMB) {
+      b = row / a.T;
+      t = row - b * a.T;
+      tok = a.tokens[(int64_t)b * a.tok_stride + t];
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int c = (v * 32 + j) * 8;
+      float dx[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        dx[k] = rstd * (gg[v][k] - m1 - xh[v][k] * m2);
+        pd[v][k] += dx[k];
+      }
+      if constexpr (EMB) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          atomicAdd(a.dword + (int64_t)tok * H + c + k, dx[k]);
+          atomicAdd(a.dpos + (int64_t)t * H + c + k, dx[k]);
+        }
+      } else {
+        const uint4 pk = pack8(dx);
+        *reinterpret_cast<uint4*>(a.dx + (int64_t)row * H + c) = pk;
+        if (a.dx2) *reinterpret_cast<uint4*>(a.dx2 + (int64_t)row * H + c) = pk;
+      }
+    }
+  }
+  // block reduction of the column partials (LDS atomics), then one global
+  // atomic per column per block
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = (v * 32 + j) * 8 + k;
+      atomicAdd(&red[0][c], pg[v][k]);
+      atomicAdd(&red[1][c], pb[v][k]);
+      atomicAdd(&red[2][c], pd[v][k]);
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < H; c += 256) {
+    atomicAdd(a.dgamma + c, red[0][c]);
+    atomicAdd(a.dbeta + c, red[1][c]);
+    // EMB: the type table's gradient (token type 0 for every position);
+    // otherwise the bias gradient of the GEMM that produced the LN input
+    float* d3 = EMB ? a.dtype : a.dbias_prev;
+    if (d3) atomicAdd(d3 + c, red[2][c]);
+  }
+}
+
+void launch_ln_fwd(const LnFwdArgs& a, int H, bool emb, hipStream_t s) {
+  const unsigned grid = (a.M + 7) / 8;
+#define MFL_LN_F(V_)                                                               \
+  if (H == 256 * V_) {                                                             \
+    if (emb) ln_fwd_kernel<V_, true><<<grid, 256, 0, s>>>(a);                     \
+    else ln_fwd_kernel<V_, false><<<grid, 256, 0, s>>>(a);                        \
+    return;                                                                        \
+  }
+  MFL_LN_F(1) MFL_LN_F(2) MFL_LN_F(3) MFL_LN_F(4)
+#undef MFL_LN_F
+}
+
+void launch_ln_bwd(const LnBwdArgs& a, int H, bool emb, hipStream_t s) {
+  const unsigned grid = (a.M + kLnBwdRows - 1) / kLnBwdRows;
+#define MFL_LN_B(V_)                                                               \
+  if (H == 256 * V_) {                                                             \
+    if (emb) ln_bwd_kernel<V_, true><<<grid, 256, 0, s>>>(a);                     \
+    else ln_bwd_kernel<V_, false><<<grid, 256, 0, s>>>(a);                        \
+    return;                                                                        \
+  }
+  MFL_LN_B(1) MFL_LN_B(2) MFL_LN_B(3) MFL_LN_B(4)
+#undef MFL_LN_B
+}
+
+// =============================================================================
+// dz = dh * gelu'(z) (exact erf GELU) and dbias += column sums of dz.
+// Thread = one 16-B column group, rows [blockIdx.x*kColRows, +kColRows).
+constexpr int kColRows = 64;
+
+template <bool GELU>
+__global__ __launch_bounds__(256) void colsum_kernel(const uint16_t* __restrict__ dh,
+                                                     const uint16_t* __restrict__ z,
+                                                     uint16_t* __restrict__ dz, float* __restrict__ dbias,
+                                                     int M, int N) {
+  const int cv = blockIdx.y * 256 + threadIdx.x;
+  if (cv * 8 >= N) return;
+  const int r0 = blockIdx.x * kColRows, r1 = min(M, r0 + kColRows);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = r0; r < r1; ++r) {
+    const int64_t off = (int64_t)r * N + cv * 8;
+    float g[8];
+    unpack8(*reinterpret_cast<const uint4*>(dh + off), g);
+    if (GELU) {
+      float zz[8];
+      unpack8(*reinterpret_cast<const uint4*>(z + off), zz);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float cdf = 0.5f * (1.f + erff(zz[k] * 0.70710678f));
+        const float pdf = 0.39894228f * __expf(-0.5f * zz[k] * zz[k]);
+        g[k] *= cdf + zz[k] * pdf;
+      }
+      const uint4 pk = pack8(g);
+      *reinterpret_cast<uint4*>(dz + off) = pk;
+      unpack8(pk, g);  // the bias gradient of what the GEMMs consume
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += g[k];
+  }
+  if (dbias)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(dbias + cv * 8 + k, acc[k]);
+}
+
+void launch_gelu_bwd(const uint16_t* dh, const uint16_t* z, uint16_t* dz, float* dbias, int M, int N,
+                     hipStream_t s) {
+  dim3 grid((M + kColRows - 1) / kColRows, (N / 8 + 255) / 256);
+  colsum_kernel<true><<<grid, 256, 0, s>>>(dh, z, dz, dbias, M, N);
+}
+
+void launch_colsum(const uint16_t* dy, float* dbias, int M, int N, hipStream_t s) {
+  dim3 grid((M + kColRows - 1) / kColRows, (N / 8 + 255) / 256);
+  colsum_kernel<false><<<grid, 256, 0, s>>>(dy, nullptr, nullptr, dbias, M, N);
+}
+
+// =============================================================================
+// Attention, T = 128 keys, head dim 64.  LDS tiles are row-major bf16 with
+// 16-B chunk XOR swizzles (128-B rows: (row>>1)&7, 256-B rows: row&15, the
+// conflict-free keys for 16-row b128 fragment reads, see conv.hip).
+constexpr int kT = 128, kD = 64;
+
+template <int ROWB>
+__device__ __forceinline__ int toff(int row, int col) {
+  const int sw = ROWB == 128 ? ((row >> 1) & 7) : (row & 15);
+  return row * ROWB + ((((col >> 3) ^ sw)) << 4) + ((col & 7) << 1);
+}
+// A/B fragment X[r0 + lane%16][k0 + 8*(lane/16) + 0..7] (row-major operand)
+template <int ROWB>
+__device__ __forceinline__ bf16x8 frag_row(const uint8_t* t, int r0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(t + toff<ROWB>(r0 + (lane & 15), k0 + 8 * (lane >> 4)));
+}
+// fragment X[k0 + 8*(lane/16) + 0..7][n0 + lane%16] (column-major use of a
+// row-major tile) from two transposing reads
+template <int ROWB>
+__device__ __forceinline__ bf16x8 frag_col(const uint8_t* t, int k0, int n0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  bf16x8 out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4s*)(t + toff<ROWB>(k0 + 8 * g + 4 * h + q, n0 + 4 * p)));
+    out[4 * h + 0] = v[0];
+    out[4 * h + 1] = v[1];
+    out[4 * h + 2] = v[2];
+    out[4 * h + 3] = v[3];
+  }
+  return out;
+}
+__device__ __forceinline__ f32x4 mma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void st_bf16(uint8_t* t, int off, float v) {
+  *reinterpret_cast<uint16_t*>(t + off) = f2bf(v);
+}
+
+// stage a [128][64] head slice of a [rows][ld] bf16 matrix into LDS
+__device__ __forceinline__ void load_head(uint8_t* dst, const uint16_t* src, int64_t row0, int ld, int col0) {
+  for (int i = threadIdx.x; i < kT * 8; i += 256) {
+    const int r = i >> 3, c = (i & 7) * 8;
+    *reinterpret_cast<uint4*>(dst + toff<128>(r, c)) =
+        *reinterpret_cast<const uint4*>(src + (row0 + r) * ld + col0 + c);
+  }
+}
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* Ks = smem;
+  uint8_t* Vs = smem + kT * kD * 2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* Pw = smem + 2 * kT * kD * 2 + wave * (32 * kT * 2);  // this wave's [32][128]
+  const int b = blockIdx.x / a.heads, h = blockIdx.x - b * a.heads;
+  const int H = a.heads * kD, ld = 3 * H;
+  const int64_t row0 = (int64_t)b * kT;
+  load_head(Ks, a.qkv, row0, ld, H + h * kD);
+  load_head(Vs, a.qkv, row0, ld, 2 * H + h * kD);
+  const int t0 = wave * 32;
+  bf16x8 qf[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      qf[i][kk] = *reinterpret_cast<const bf16x8*>(a.qkv + (row0 + t0 + 16 * i + (lane & 15)) * ld + h * kD +
+                                                   32 * kk + 8 * (lane >> 4));
+  __syncthreads();
+  f32x4 s[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jt = 0; jt < 8; ++jt) s[i][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int jt = 0; jt < 8; ++jt) {
+      const bf16x8 kf = frag_row<128>(Ks, 16 * jt, 32 * kk, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) s[i][jt] = mma(qf[i][kk], kf, s[i][jt]);
+    }
+  // row softmax: a row's 128 scores sit in 8 tiles x the 16 lanes of a group
+  const float c = a.scale * kLog2e;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int jt = 0; jt < 8; ++jt) mx = fmaxf(mx, s[i][jt][e]);
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      float sum = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < 8; ++jt) {
+        const float p = exp2f((s[i][jt][e] - mx) * c);
+        s[i][jt][e] = p;
+        sum += p;
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+      const float inv = 1.f / sum;
+      const int r = 16 * i + 4 * (lane >> 4) + e;
+#pragma unroll
+      for (int jt = 0; jt < 8; ++jt) st_bf16(Pw, toff<256>(r, 16 * jt + (lane & 15)), s[i][jt][e] * inv);
+      if ((lane & 15) == 0) a.lse[((int64_t)b * a.heads + h) * kT + t0 + r] = mx * a.scale + __logf(sum);
+    }
+  __builtin_amdgcn_wave_barrier();
+  f32x4 o[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int dj = 0; dj < 4; ++dj) o[i][dj] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < kT; kk += 32) {
+    bf16x8 pf[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) pf[i] = frag_row<256>(Pw, 16 * i, kk, lane);
+#pragma unroll
+    for (int dj = 0; dj < 4; ++dj) {
+      const bf16x8 vf = frag_col<128>(Vs, kk, 16 * dj, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) o[i][dj] = mma(pf[i], vf, o[i][dj]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int dj = 0; dj < 4; ++dj)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int t = t0 + 16 * i + 4 * (lane >> 4) + e;
+        a.ctx[(row0 + t) * H + h * kD + 16 * dj + (lane & 15)] = f2bf(o[i][dj][e]);
+      }
+}
+
+__device__ __forceinline__ void colsum_tile(const f32x4 (&acc)[2][4], float* cs, int lane, float mul) {
+#pragma unroll
+  for (int dj = 0; dj < 4; ++dj) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v += acc[i][dj][e] * mul;
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane < 16) atomicAdd(cs + 16 * dj + lane, v);
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int HT = kT * kD * 2;  // 16 KiB head tile
+  uint8_t* Qs = smem;
+  uint8_t* Ks = smem + HT;
+  uint8_t* Vs = smem + 2 * HT;
+  uint8_t* dOs = smem + 3 * HT;
+  uint8_t* Ps = smem + 4 * HT;             // [128][128] bf16
+  uint8_t* dSs = Ps + kT * kT * 2;          // [128][128] bf16
+  float* Dd = reinterpret_cast<float*>(dSs + kT * kT * 2);
+  float* Ls = Dd + kT;
+  float* cs = Ls + kT;  // [3][64] bias-gradient partials
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b = blockIdx.x / a.heads, h = blockIdx.x - b * a.heads;
+  const int H = a.heads * kD, ld = 3 * H;
+  const int64_t row0 = (int64_t)b * kT;
+  load_head(Qs, a.qkv, row0, ld, h * kD);
+  load_head(Ks, a.qkv, row0, ld, H + h * kD);
+  load_head(Vs, a.qkv, row0, ld, 2 * H + h * kD);
+  {
+    // dO into LDS and D[t] = sum_d dO[t][d] * O[t][d]: thread -> row tid/2, half tid&1
+    const int r = threadIdx.x >> 1, half = threadIdx.x & 1;
+    float dsum = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const int col = half * 32 + cc * 8;
+      const uint4 dov = *reinterpret_cast<const uint4*>(a.dctx + (row0 + r) * H + h * kD + col);
+      const uint4 ov = *reinterpret_cast<const uint4*>(a.ctx + (row0 + r) * H + h * kD + col);
+      *reinterpret_cast<uint4*>(dOs + toff<128>(r, col)) = dov;
+      float f1[8], f2[8];
+      unpack8(dov, f1);
+      unpack8(ov, f2);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dsum += f1[k] * f2[k];
+    }
+    dsum += __shfl_xor(dsum, 1);
+    if (!half) {
+      Dd[r] = dsum;
+      Ls[r] = a.lse[((int64_t)b * a.heads + h) * kT + r];
+    }
+    if (threadIdx.x < 3 * kD) cs[threadIdx.x] = 0.f;
+  }
+  __syncthreads();
+  const int t0 = wave * 32;
+  const float c = a.scale * kLog2e;
+  {
+    f32x4 s[2][8], dp[2][8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jt = 0; jt < 8; ++jt) s[i][jt] = dp[i][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < kD; kk += 32) {
+      bf16x8 qf[2], df[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        qf[i] = frag_row<128>(Qs, t0 + 16 * i, kk, lane);
+        df[i] = frag_row<128>(dOs, t0 + 16 * i, kk, lane);
+      }
+#pragma unroll
+      for (int jt = 0; jt < 8; ++jt) {
+        const bf16x8 kf = frag_row<128>(Ks, 16 * jt, kk, lane);
+        const bf16x8 vf = frag_row<128>(Vs, 16 * jt, kk, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          s[i][jt] = mma(qf[i], kf, s[i][jt]);
+          dp[i][jt] = mma(df[i], vf, dp[i][jt]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = t0 + 16 * i + 4 * (lane >> 4) + e;
+        const float l2 = Ls[r] * kLog2e, dd = Dd[r];
+#pragma unroll
+        for (int jt = 0; jt < 8; ++jt) {
+          const float p = exp2f(s[i][jt][e] * c - l2);
+          const int off = toff<256>(r, 16 * jt + (lane & 15));
+          st_bf16(Ps, off, p);
+          st_bf16(dSs, off, p * (dp[i][jt][e] - dd));
+        }
+      }
+  }
+  __builtin_amdgcn_wave_barrier();
+  // dQ = scale * dS K  (this wave's rows; dS rows written by this wave)
+  {
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int dj = 0; dj < 4; ++dj) acc[i][dj] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < kT; kk += 32) {
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = frag_row<256>(dSs, t0 + 16 * i, kk, lane);
+#pragma unroll
+      for (int dj = 0; dj < 4; ++dj) {
+        const bf16x8 kf = frag_col<128>(Ks, kk, 16 * dj, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][dj] = mma(af[i], kf, acc[i][dj]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int dj = 0; dj < 4; ++dj)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int t = t0 + 16 * i + 4 * (lane >> 4) + e;
+          a.dqkv[(row0 + t) * ld + h * kD + 16 * dj + (lane & 15)] = f2bf(acc[i][dj][e] * a.scale);
+        }
+    colsum_tile(acc, cs, lane, a.scale);
+  }
+  __syncthreads();  // every wave's P and dS rows are in LDS
+  // dK = scale * dS^T Q and dV = P^T dO for key rows s0 .. s0+31
+  {
+    const int s0 = wave * 32;
+    f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int dj = 0; dj < 4; ++dj) dk[i][dj] = dv[i][dj] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < kT; kk += 32) {
+      bf16x8 sf[2], pf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        sf[i] = frag_col<256>(dSs, kk, s0 + 16 * i, lane);
+        pf[i] = frag_col<256>(Ps, kk, s0 + 16 * i, lane);
+      }
+#pragma unroll
+      for (int dj = 0; dj < 4; ++dj) {
+        const bf16x8 qf = frag_col<128>(Qs, kk, 16 * dj, lane);
+        const bf16x8 of = frag_col<128>(dOs, kk, 16 * dj, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          dk[i][dj] = mma(sf[i], qf, dk[i][dj]);
+          dv[i][dj] = mma(pf[i], of, dv[i][dj]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int dj = 0; dj < 4; ++dj)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int sr = s0 + 16 * i + 4 * (lane >> 4) + e;
+          uint16_t* rowp = a.dqkv + (row0 + sr) * ld + h * kD + 16 * dj + (lane & 15);
+          rowp[H] = f2bf(dk[i][dj][e] * a.scale);
+          rowp[2 * H] = f2bf(dv[i][dj][e]);
+        }
+    colsum_tile(dk, cs + kD, lane, a.scale);
+    colsum_tile(dv, cs + 2 * kD, lane, 1.f);
+  }
+  __syncthreads();
+  if (a.dbias && threadIdx.x < 3 * kD) {
+    const int part = threadIdx.x / kD, d = threadIdx.x - part * kD;
+    atomicAdd(a.dbias + part * H + h * kD + d, cs[threadIdx.x]);
+  }
+}
+
+static void lds_attr(const void* k, size_t bytes, bool& done) {
+  if (!done && bytes > 65536) {
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    done = true;
+  }
+}
+
+size_t attn_fwd_lds() { return 2 * kT * kD * 2 + 4 * 32 * kT * 2; }
+size_t attn_bwd_lds() { return 4 * kT * kD * 2 + 2 * kT * kT * 2 + (2 * kT + 3 * kD) * 4; }
+
+void launch_attn_fwd(const AttnArgs& a, hipStream_t s) {
+  attn_fwd_kernel<<<a.batch * a.heads, 256, attn_fwd_lds(), s>>>(a);
+}
+
+void launch_attn_bwd(const AttnArgs& a, hipStream_t s) {
+  static bool done = false;
+  lds_attr(reinterpret_cast<const void*>(&attn_bwd_kernel), attn_bwd_lds(), done);
+  attn_bwd_kernel<<<a.batch * a.heads, 256, attn_bwd_lds(), s>>>(a);
+}
+
+// =============================================================================
+// Masked-LM head plumbing.  Batch rows are int32 records
+//   [tokens T | mlm positions P | mlm label ids P | inverse map T]
+// (inverse map: t -> prediction slot p, or -1).
+__global__ __launch_bounds__(256) void mlm_gather_kernel(const uint16_t* __restrict__ x,
+                                                         const int* __restrict__ rec, int rec_stride, int T,
+                                                         int P, int H, uint16_t* __restrict__ out, int64_t nvec) {
+  const int vpr = H / 8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int r = (int)(i / vpr), cv = (int)(i - (int64_t)r * vpr);
+    const int b = r / P, p = r - b * P;
+    const int t = rec[(int64_t)b * rec_stride + T + p];
+    reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(x + ((int64_t)b * T + t) * H)[cv];
+  }
+}
+
+__global__ __launch_bounds__(256) void mlm_scatter_kernel(const uint16_t* __restrict__ dsel,
+                                                          const int* __restrict__ rec, int rec_stride, int T,
+                                                          int P, int H, uint16_t* __restrict__ dx, int64_t nvec) {
+  const int vpr = H / 8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int row = (int)(i / vpr), cv = (int)(i - (int64_t)row * vpr);
+    const int b = row / T, t = row - b * T;
+    const int p = rec[(int64_t)b * rec_stride + T + 2 * P + t];
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (p >= 0) v = reinterpret_cast<const uint4*>(dsel + ((int64_t)b * P + p) * H)[cv];
+    reinterpret_cast<uint4*>(dx)[i] = v;
+  }
+}
+
+void launch_mlm_gather(const uint16_t* x, const int* rec, int rec_stride, int B, int T, int P, int H,
+                       uint16_t* out, hipStream_t s) {
+  const int64_t nvec = (int64_t)B * P * H / 8;
+  mlm_gather_kernel<<<stream_grid(nvec), 256, 0, s>>>(x, rec, rec_stride, T, P, H, out, nvec);
+}
+
+void launch_mlm_scatter(const uint16_t* dsel, const int* rec, int rec_stride, int B, int T, int P, int H,
+                        uint16_t* dx, hipStream_t s) {
+  const int64_t nvec = (int64_t)B * T * H / 8;
+  mlm_scatter_kernel<<<stream_grid(nvec), 256, 0, s>>>(dsel, rec, rec_stride, T, P, H, dx, nvec);
+}
+
+// Vocab-wide softmax cross entropy, one 256-thread block per prediction row;
+// logits [R][Vp] bf16 with V valid columns; label of row r at
+// rec[(r / P) * rec_stride + T + P + r % P] (-1: ignored).  dlogits =
+// (softmax - onehot) / R; stats += {loss, correct, count}.
+__global__ __launch_bounds__(256) void vocab_xent_kernel(VocabXentArgs a) {
+  __shared__ float sm[8], ss[8];
+  __shared__ int sa[8];
+  const int r = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint16_t* z = a.logits + (int64_t)r * a.Vp;
+  const int nv = a.V / 8;  // V % 8 == 0 is not required: the tail is scalar
+  float m = -INFINITY, s = 0.f;
+  for (int v = t; v < nv; v += 256) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(z)[v], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float nm = fmaxf(m, f[k]);
+      s = s * __expf(m - nm) + __expf(f[k] - nm);
+      m = nm;
+    }
+  }
+  for (int k = nv * 8 + t; k < a.V; k += 256) {
+    const float f = bf2f(z[k]);
+    const float nm = fmaxf(m, f);
+    s = s * __expf(m - nm) + __expf(f - nm);
+    m = nm;
+  }
+  // block max / sum
+  float bm = wave_max(m);
+  if (lane == 0) sm[w] = bm;
+  __syncthreads();
+  bm = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+  float bs = wave_sum(m == -INFINITY ? 0.f : s * __expf(m - bm));
+  if (lane == 0) ss[w] = bs;
+  // first index of the maximum (accuracy)
+  int am = a.V;
+  for (int k = t; k < a.V; k += 256)
+    if (bf2f(z[k]) == bm) { am = k; break; }
+  for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o));
+  if (lane == 0) sa[w] = am;
+  __syncthreads();
+  bs = ss[0] + ss[1] + ss[2] + ss[3];
+  am = min(min(sa[0], sa[1]), min(sa[2], sa[3]));
+  const int b = r / a.P, p = r - b * a.P;
+  const int y = a.rec[(int64_t)b * a.rec_stride + a.T + a.P + p];
+  const bool valid = y >= 0 && y < a.V;
+  const float inv_s = 1.f / bs, inv_r = 1.f / (float)a.R;
+  if (a.dlogits) {
+    uint16_t* d = a.dlogits + (int64_t)r * a.Vp;
+    for (int v = t; v < a.Vp / 8; v += 256) {
+      float f[8];
+      unpack8(reinterpret_cast<const uint4*>(z)[v], f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int col = v * 8 + k;
+        float g = 0.f;
+        if (valid && col < a.V) g = (__expf(f[k] - bm) * inv_s - (col == y ? 1.f : 0.f)) * inv_r;
+        f[k] = g;
+      }
+      reinterpret_cast<uint4*>(d)[v] = pack8(f);
+    }
+  }
+  if (t == 0 && valid) {
+    atomicAdd(&a.stats[0], __logf(bs) + bm - bf2f(z[y]));
+    atomicAdd(&a.stats[1], am == y ? 1.f : 0.f);
+    atomicAdd(&a.stats[2], 1.f);
+  }
+}
+
+void launch_vocab_xent(const VocabXentArgs& a, hipStream_t s) {
+  vocab_xent_kernel<<<a.R, 256, 0, s>>>(a);
+}
+
+}  // namespace mfl

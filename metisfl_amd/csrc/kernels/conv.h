@@ -48,6 +48,11 @@ struct ConvArgs {
   const float* bn_mean;
   const float* bn_invstd;
   double* bn_acc;
+  // dense-GEMM epilogue (1x1 geometry, BERT path): y = acc + bias[col] +
+  // resid[row][col]; act_out (optional) = gelu(y).  All nullptr on conv paths.
+  const float* bias;
+  const uint16_t* resid;
+  uint16_t* act_out;
   uint32_t src_bytes, wgt_bytes;  // buffer-descriptor ranges of src / wgt
   int kchunk;
   int accum;
@@ -78,9 +83,18 @@ struct BnBwdFusion {
 void launch_conv_dgrad_bnb(const ConvGeom& g, const ConvPlan& p, const uint16_t* dy,
                            const uint16_t* wgt, uint16_t* dx, float* ysplit, int* counters,
                            bool accum, const BnBwdFusion& f, hipStream_t s);
+struct GemmEpilogueArgs {
+  const float* bias = nullptr;
+  const uint16_t* resid = nullptr;
+  uint16_t* act_out = nullptr;
+};
+// forward implicit GEMM with the dense epilogue (bias / residual / GELU copy)
+void launch_conv_gemm_epi(const ConvGeom& g, const ConvPlan& p, const uint16_t* src,
+                          const uint16_t* wgt, uint16_t* y, float* ysplit, int* counters,
+                          const GemmEpilogueArgs& e, hipStream_t s);
 // dw (fp32 [Cout][R][S][Cin]); must be zeroed first when p.splits > 1.
 void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, const uint16_t* dy,
-                       float* dw, hipStream_t s);
+                       float* dw, hipStream_t s, bool accumulate = false);
 void launch_transpose_krsc(const uint16_t* w, uint16_t* wt, int Co, int RS, int Ci, hipStream_t s);
 
 }  // namespace mfl

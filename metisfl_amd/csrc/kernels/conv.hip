@@ -152,13 +152,17 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int n0,
   float s[8] = {0}, q[8] = {0};
   const int col = n0 + cg * 8;
   const bool col_ok = col < g.Ng;  // Ng % 8 == 0
-  float mu[8], is[8];
+  float mu[8], is[8], bv[8];
   if (a.bn_acc && col_ok) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       mu[k] = a.bn_mean[col + k];
       is[k] = a.bn_invstd[col + k];
     }
+  }
+  if (a.bias && col_ok) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bv[k] = a.bias[col + k];
   }
   for (int rl = r0; rl < BM; rl += RPP) {
     const int row = m0 + rl;
@@ -173,8 +177,25 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int n0,
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += o[k];
     }
+    if (a.bias) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += bv[k];
+    }
+    if (a.resid) {
+      float o[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.resid + off), o);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += o[k];
+    }
     const uint4 packed = pack8(v);
     *reinterpret_cast<uint4*>(dst) = packed;
+    if (a.act_out) {  // exact (erf) GELU of the stored pre-activation
+      float f[8], h[8];
+      unpack8(packed, f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) h[k] = 0.5f * f[k] * (1.f + erff(f[k] * 0.70710678f));
+      *reinterpret_cast<uint4*>(a.act_out + off) = pack8(h);
+    }
     if (stats) {
       float f[8];
       unpack8(packed, f);
@@ -572,7 +593,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
   };
   dma_k_loop<2 * NI>(nk, issue, compute);
 
-  const bool atomic = gridDim.z > 1;  // split-K slices add into the zeroed slot
+  // split-K slices (or an accumulating caller) add into the gradient slot
   const int rbase = ko0 + wm * (BM / 2) + (lane >> 4) * 4;
   const int cbase = j0 + wn * (BN / 2) + (lane & 15);
 #pragma unroll
@@ -583,7 +604,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
       for (int e = 0; e < 4; ++e) {
         const int row = rbase + 16 * i + e, cc = cbase + 16 * jj;
         if (row < g.Ng && cc < g.K) {
-          if (atomic)
+          if (gridDim.z > 1 || a.accum)
             atomicAdd(&dw[(int64_t)row * g.K + cc], acc[i][jj][e]);
           else
             dw[(int64_t)row * g.K + cc] = acc[i][jj][e];
@@ -733,6 +754,28 @@ void launch_conv_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const ui
 #undef MFL_CONV_CASE
 }
 
+void launch_conv_gemm_epi(const ConvGeom& g, const ConvPlan& p, const uint16_t* src,
+                          const uint16_t* wgt, uint16_t* y, float* ysplit, int* counters,
+                          const GemmEpilogueArgs& e, hipStream_t s) {
+  ConvArgs a{};
+  a.g = g;
+  a.src = src;
+  a.wgt = wgt;
+  a.src_bytes = range_bytes((int64_t)g.N * g.H * g.W * g.C);
+  a.wgt_bytes = range_bytes((int64_t)g.Ng * g.K);
+  a.y = y;
+  a.ysplit = ysplit;
+  a.counters = counters;
+  a.kchunk = p.kchunk;
+  a.bias = e.bias;
+  a.resid = e.resid;
+  a.act_out = e.act_out;
+  fill_shifts(a);
+  if (p.bm == 128 && p.bn == 128) launch_gemm_ks<128, 128, false>(a, p, s);
+  else if (p.bm == 128 && p.bn == 64) launch_gemm_ks<128, 64, false>(a, p, s);
+  else if (p.bm == 64 && p.bn == 64) launch_gemm_ks<64, 64, false>(a, p, s);
+}
+
 void launch_conv_dgrad_bnb(const ConvGeom& g, const ConvPlan& p, const uint16_t* dy,
                            const uint16_t* wgt, uint16_t* dx, float* ysplit, int* counters,
                            bool accum, const BnBwdFusion& f, hipStream_t s) {
@@ -799,8 +842,9 @@ static void launch_wgrad_ks(const ConvArgs& a, dim3 grid, int ks, int st, float*
 // atomics); the training step gets that for free from the optimizer launch,
 // which zeroes the gradient buffer after consuming it.
 void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, const uint16_t* dy,
-                       float* dw, hipStream_t s) {
+                       float* dw, hipStream_t s, bool accumulate) {
   ConvArgs a{};
+  a.accum = accumulate ? 1 : 0;
   a.g = g;
   a.src = dy;
   a.wgt = x;

@@ -3,13 +3,30 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kernels/conv.h"
+
 namespace mfl {
 
 enum GemmEpilogue { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RESIDUAL = 3 };
 
+ConvPlan plan_gemm(int M, int N, int K);
+
 // C[M][N] = A[M][K] . B[N][K]^T  with an optional fused epilogue
-// (bias, bias+GELU(tanh), bias+residual(aux)).
+// (bias, bias+GELU(erf) in place, bias+residual(aux)).
 void launch_gemm_nt(const uint16_t* a, const uint16_t* b, uint16_t* c, const float* bias,
                     const uint16_t* aux, int M, int N, int K, int epilogue, hipStream_t s);
+
+// Linear layer GEMMs (W is [N][K], K-contiguous):
+//   y = x W^T + bias (+ resid);  act_out = gelu(y) when given
+void launch_gemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
+                     const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s);
+//   dx (+)= dy W
+void launch_gemm_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
+                       bool accumulate, hipStream_t s);
+//   dw = dy^T x, or dw += with accumulate (fp32 atomics; split-K plans always
+//   add, so dw must be zero on entry unless accumulating on purpose)
+void launch_gemm_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,
+                       bool accumulate, hipStream_t s);
+bool gemm_wgrad_splits(int M, int N, int K);
 
 }  // namespace mfl

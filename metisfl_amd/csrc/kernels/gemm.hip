@@ -1,56 +1,86 @@
-// K7: dense bf16 GEMM  C = A . B^T  on the MFMA implicit-GEMM core of conv.hip
-// (a 1x1 convolution over an M x 1 x 1 "image" is exactly an NT GEMM with
-// both operands K-contiguous), followed by a fused vectorised epilogue.
+// K7: dense bf16 GEMMs on the MFMA implicit-GEMM core of conv.hip.  A 1x1
+// convolution over an M x 1 x 1 "image" is exactly a GEMM with both operands
+// K-contiguous, so the three training GEMMs of a Linear layer map onto the
+// three conv kernels with no new tiling code:
+//   forward  Y[M][N]  = X[M][K] . W[N][K]^T  (+bias, +residual, GELU copy:
+//                       fused into the tile epilogue, no extra pass)
+//   dgrad    dX[M][K] = dY[M][N] . W[N][K]   (conv dgrad, W read through
+//                       transposing LDS reads -- no weight transpose)
+//   wgrad    dW[N][K] += dY^T . X            (conv wgrad, fp32 accumulation
+//                       into the flat gradient buffer)
+// Reference: the Keras Dense layers of the example models
+// (examples/keras/models/fashion_mnist_fc.py:19-21, cifar_cnn.py:38-41) and
+// the BERT-base FFN / attention projections of SURVEY §2.10 K7.
 #include "kernels/common.h"
 #include "kernels/conv.h"
 #include "kernels/gemm.h"
 
 namespace mfl {
 
-template <int EPI>
-__global__ __launch_bounds__(256) void gemm_epilogue_kernel(uint16_t* __restrict__ c,
-                                                            const float* __restrict__ bias,
-                                                            const uint16_t* __restrict__ aux,
-                                                            int64_t nvec, int N) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int vpr = N / 8;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-    const int cb = (int)(i % vpr) * 8;
-    float f[8];
-    unpack8(reinterpret_cast<const uint4*>(c)[i], f);
-    float r[8];
-    if (EPI == EPI_BIAS_RESIDUAL) unpack8(reinterpret_cast<const uint4*>(aux)[i], r);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float v = f[k] + bias[cb + k];
-      if (EPI == EPI_BIAS_GELU) {
-        const float u = 0.7978845608f * (v + 0.044715f * v * v * v);
-        v = 0.5f * v * (1.f + tanhf(u));
-      }
-      if (EPI == EPI_BIAS_RESIDUAL) v += r[k];
-      f[k] = v;
-    }
-    reinterpret_cast<uint4*>(c)[i] = pack8(f);
-  }
-}
-
-void launch_gemm_nt(const uint16_t* a, const uint16_t* b, uint16_t* c, const float* bias,
-                    const uint16_t* aux, int M, int N, int K, int epilogue, hipStream_t s) {
+static ConvGeom dense_geom(int M, int Nout, int K) {
   ConvGeom g{};
   g.N = M; g.H = 1; g.W = 1; g.C = K;
   g.P = 1; g.Q = 1; g.R = 1; g.S = 1; g.stride = 1; g.pad = 0;
-  g.M = M; g.K = K; g.Ng = N;
-  ConvPlan p = plan_conv_gemm(g);
-  p.splits = 1;  // no workspace on this path
-  p.kchunk = ((K + 63) / 64) * 64;
-  launch_conv_gemm(g, false, p, a, b, c, nullptr, nullptr, nullptr, false, s);
-  if (epilogue != EPI_NONE && bias) {
-    const int64_t nvec = (int64_t)M * N / 8;
-    const unsigned grid = stream_grid(nvec);
-    if (epilogue == EPI_BIAS) gemm_epilogue_kernel<EPI_BIAS><<<grid, 256, 0, s>>>(c, bias, aux, nvec, N);
-    else if (epilogue == EPI_BIAS_GELU) gemm_epilogue_kernel<EPI_BIAS_GELU><<<grid, 256, 0, s>>>(c, bias, aux, nvec, N);
-    else gemm_epilogue_kernel<EPI_BIAS_RESIDUAL><<<grid, 256, 0, s>>>(c, bias, aux, nvec, N);
+  g.M = M; g.K = K; g.Ng = Nout;
+  return g;
+}
+
+// Tile plan for a dense GEMM with M rows, N columns, K reduction.  Bigger
+// tiles re-read fewer operand bytes per FLOP (a 128x128 tile does twice the
+// MFMA work per staged byte of a 128x64 one) but give fewer workgroups; take
+// the biggest tile that still puts >= 2 workgroups on each of the 256 CUs,
+// and never split K (the BERT GEMMs have >= 768 tiles of work already).
+ConvPlan plan_gemm(int M, int N, int K) {
+  auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  ConvPlan p;
+  if (blocks(128, 128) >= 512) {
+    p.bm = 128; p.bn = 128;
+  } else if (blocks(128, 64) >= 256) {
+    p.bm = 128; p.bn = 64;
+  } else {
+    p.bm = 64; p.bn = 64;
   }
+  p.bk = (K >= 512 && !(p.bm == 128 && p.bn == 128)) ? 128 : 64;
+  p.splits = 1;
+  p.kchunk = ((K + p.bk - 1) / p.bk) * p.bk;
+  p.stats_rows = 0;
+  return p;
+}
+
+void launch_gemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
+                     const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s) {
+  const ConvGeom g = dense_geom(M, N, K);
+  GemmEpilogueArgs e;
+  e.bias = bias;
+  e.resid = resid;
+  e.act_out = act_out;
+  launch_conv_gemm_epi(g, plan_gemm(M, N, K), x, w, y, nullptr, nullptr, e, s);
+}
+
+void launch_gemm_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
+                       bool accumulate, hipStream_t s) {
+  // dgrad geometry: "dY" has C = N channels, the output dX has Ng = K columns
+  ConvGeom g = dense_geom(M, K, N);
+  ConvPlan p = plan_gemm(M, K, N);
+  launch_conv_gemm(g, true, p, dy, w, dx, nullptr, nullptr, nullptr, accumulate, s);
+}
+
+void launch_gemm_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,
+                       bool accumulate, hipStream_t s) {
+  const ConvGeom g = dense_geom(M, N, K);
+  launch_conv_wgrad(g, plan_conv_wgrad(g), x, dy, dw, s, accumulate);
+}
+
+bool gemm_wgrad_splits(int M, int N, int K) { return plan_conv_wgrad(dense_geom(M, N, K)).splits > 1; }
+
+void launch_gemm_nt(const uint16_t* a, const uint16_t* b, uint16_t* c, const float* bias,
+                    const uint16_t* aux, int M, int N, int K, int epilogue, hipStream_t s) {
+  GemmEpilogueArgs e;
+  if (epilogue != EPI_NONE) e.bias = bias;
+  if (epilogue == EPI_BIAS_RESIDUAL) e.resid = aux;
+  // GELU in place: the same thread stores the pre-activation, then gelu()
+  if (epilogue == EPI_BIAS_GELU) e.act_out = c;
+  launch_conv_gemm_epi(dense_geom(M, N, K), plan_gemm(M, N, K), a, b, c, nullptr, nullptr, e, s);
 }
 
 }  // namespace mfl

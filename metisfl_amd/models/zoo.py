@@ -26,3 +26,16 @@ def _fashion_mnist_fc(batch_size, device="cpu", optimizer=None, seed=0, **kw):
 def _housing_mlp(batch_size, device="cpu", optimizer=None, seed=0, **kw):
     from metisfl_amd.models.sequential import HousingMLP
     return HousingMLP(batch_size=batch_size, device=device, optimizer=optimizer, seed=seed, **kw)
+
+
+@register_family("bert_base")
+def _bert_base(batch_size, device="cpu", optimizer=None, seed=0, **kw):
+    from metisfl_amd.models.bert import BertMLM
+    return BertMLM(batch_size=batch_size, device=device, optimizer=optimizer, seed=seed, **kw)
+
+
+@register_family("bert_tiny")
+def _bert_tiny(batch_size, device="cpu", optimizer=None, seed=0, **kw):
+    from metisfl_amd.models.bert import BERT_TINY, BertMLM
+    return BertMLM(batch_size=batch_size, device=device, optimizer=optimizer, seed=seed,
+                   config=kw.pop("config", BERT_TINY), **kw)

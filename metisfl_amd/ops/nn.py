@@ -292,15 +292,15 @@ def gather_batch(shard, labels, perm, step, steps_per_epoch: int, B: int, xb, yb
 
 
 def gemm_nt(a, b, c, M: int, N: int, K: int, bias=None, epilogue: int = 0, aux=None) -> None:
-    """c = a . b^T (+bias, +gelu | +residual)."""
+    """c = a . b^T (+bias, +exact-erf gelu | +residual)."""
     if a.is_cuda:
         ops().gemm_nt(a, b, c, bias, M, N, K, epilogue, aux)
         return
     out = a.float().reshape(M, K) @ b.float().reshape(N, K).t()
     if epilogue >= 1 and bias is not None:
         out = out + bias
-    if epilogue == 2:
-        out = F.gelu(out, approximate="tanh")
+    if epilogue == 2:  # gelu of the bf16-rounded pre-activation, as on the GPU
+        out = F.gelu(out.to(torch.bfloat16).float())
     if epilogue == 3:
         out = out + aux.float().reshape(M, N)
     c.copy_(out.reshape(c.shape).to(torch.bfloat16))

@@ -1,0 +1,202 @@
+"""BERT-path HIP kernels (bert.hip, gemm.hip) vs the fp32 CPU reference ops,
+and the BERT-tiny training step GPU vs CPU."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def _native():
+    from metisfl_amd.ops._native import ops
+    ops()
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (4096, 2304, 768), (640, 1000, 256), (200, 136, 72)])
+def test_linear_gemms(M, N, K):
+    from metisfl_amd.ops import bert as BO
+    _native()
+    torch.manual_seed(0)
+    x = torch.randn(M, K).to(BF)
+    w = (torch.randn(N, K) * 0.05).to(BF)
+    b = torch.randn(N)
+    r = torch.randn(M, N).to(BF)
+    outs = {}
+    for dev in ("cpu", DEV):
+        y, h = torch.empty(M, N, dtype=BF, device=dev), torch.empty(M, N, dtype=BF, device=dev)
+        BO.gemm_fwd(x.to(dev), w.to(dev), y, M, N, K, bias=b.to(dev), resid=r.to(dev), act_out=h)
+        dy = (torch.randn(M, N, generator=torch.Generator().manual_seed(1))).to(BF).to(dev)
+        dx = x.clone().to(dev)
+        BO.gemm_dgrad(dy, w.to(dev), dx, M, N, K, accumulate=True)
+        dw = torch.ones(N, K, device=dev)
+        BO.gemm_wgrad(x.to(dev), dy, dw, M, N, K, accumulate=True)
+        dw2 = torch.full((N, K), 7.0, device=dev)
+        BO.gemm_wgrad(x.to(dev), dy, dw2, M, N, K, accumulate=False)
+        outs[dev] = (y, h, dx, dw, dw2)
+    for a, c in zip(outs[DEV], outs["cpu"]):
+        assert rel(a, c) < 1e-2
+
+
+@pytest.mark.parametrize("H", [256, 768])
+def test_layernorm_fwd_bwd(H):
+    from metisfl_amd.ops import bert as BO
+    _native()
+    torch.manual_seed(1)
+    M = 300
+    x = (torch.randn(M, H) * 2 + 0.5).to(BF)
+    gam, bet = torch.rand(H) + 0.5, torch.randn(H)
+    dy = torch.randn(M, H).to(BF)
+    res = {}
+    for dev in ("cpu", DEV):
+        y = torch.empty(M, H, dtype=BF, device=dev)
+        mean, rstd = torch.zeros(M, device=dev), torch.zeros(M, device=dev)
+        BO.ln_fwd(x.to(dev), gam.to(dev), bet.to(dev), y, mean, rstd, M, H, 1e-12)
+        dx, dx2 = torch.empty(M, H, dtype=BF, device=dev), torch.empty(M, H, dtype=BF, device=dev)
+        dg, db, dbp = (torch.zeros(H, device=dev) for _ in range(3))
+        BO.ln_bwd(dy.to(dev), x.to(dev), mean, rstd, gam.to(dev), dx, dg, db, M, H, dx2=dx2, dbias_prev=dbp)
+        res[dev] = (y, mean, rstd, dx, dx2, dg, db, dbp)
+    for a, c in zip(res[DEV], res["cpu"]):
+        assert rel(a, c) < 1e-2
+
+
+def test_embedding_layernorm_fwd_bwd():
+    from metisfl_amd.datasets import synthetic_mlm
+    from metisfl_amd.ops import bert as BO
+    _native()
+    torch.manual_seed(2)
+    B, T, P, H, V = 3, 128, 8, 256, 500
+    rec = torch.as_tensor(synthetic_mlm(B, T, P, V, seed=1))
+    stride = rec.shape[1]
+    word, pos, typ = (torch.randn(V, H) * 0.1).to(BF), (torch.randn(T, H) * 0.1).to(BF), (torch.randn(2, H) * 0.1).to(BF)
+    gam, bet = torch.rand(H) + 0.5, torch.randn(H)
+    dy = torch.randn(B * T, H).to(BF)
+    res = {}
+    for dev in ("cpu", DEV):
+        M = B * T
+        xs, y = torch.empty(M, H, dtype=BF, device=dev), torch.empty(M, H, dtype=BF, device=dev)
+        mean, rstd = torch.zeros(M, device=dev), torch.zeros(M, device=dev)
+        r = rec.to(dev)
+        BO.emb_ln_fwd(r, stride, B, T, word.to(dev), pos.to(dev), typ.to(dev), xs, gam.to(dev), bet.to(dev), y,
+                      mean, rstd, H, 1e-12)
+        dw, dp, dt = torch.zeros(V, H, device=dev), torch.zeros(T, H, device=dev), torch.zeros(2, H, device=dev)
+        dg, db = torch.zeros(H, device=dev), torch.zeros(H, device=dev)
+        BO.emb_ln_bwd(dy.to(dev), xs, mean, rstd, gam.to(dev), r, stride, B, T, dw, dp, dt, dg, db, H)
+        res[dev] = (xs, y, dw, dp, dt, dg, db)
+    for a, c in zip(res[DEV], res["cpu"]):
+        assert rel(a, c) < 1e-2
+
+
+def test_gelu_bwd_and_colsum():
+    from metisfl_amd.ops import bert as BO
+    _native()
+    torch.manual_seed(3)
+    M, N = 333, 3072
+    dh, z = torch.randn(M, N).to(BF), (torch.randn(M, N) * 2).to(BF)
+    res = {}
+    for dev in ("cpu", DEV):
+        dz = torch.empty(M, N, dtype=BF, device=dev)
+        db, cs = torch.zeros(N, device=dev), torch.zeros(N, device=dev)
+        BO.gelu_bwd(dh.to(dev), z.to(dev), dz, M, N, dbias=db)
+        BO.colsum(dh.to(dev), cs, M, N)
+        res[dev] = (dz, db, cs)
+    for a, c in zip(res[DEV], res["cpu"]):
+        assert rel(a, c) < 1e-2
+
+
+@pytest.mark.parametrize("heads", [4, 12])
+def test_attention_fwd_bwd(heads):
+    from metisfl_amd.ops import bert as BO
+    _native()
+    torch.manual_seed(4)
+    B, T, H = 2, 128, heads * 64
+    qkv = (torch.randn(B * T, 3 * H) * 1.5).to(BF)
+    dctx = torch.randn(B * T, H).to(BF)
+    scale = 1.0 / math.sqrt(64)
+    res = {}
+    for dev in ("cpu", DEV):
+        ctx = torch.empty(B * T, H, dtype=BF, device=dev)
+        lse = torch.zeros(B * heads * T, device=dev)
+        BO.attn_fwd(qkv.to(dev), ctx, lse, B, heads, scale)
+        dqkv = torch.empty(B * T, 3 * H, dtype=BF, device=dev)
+        db = torch.zeros(3 * H, device=dev)
+        BO.attn_bwd(qkv.to(dev), ctx, lse, dctx.to(dev), dqkv, B, heads, scale, dbias=db)
+        res[dev] = (ctx, lse, dqkv, db)
+    for nm, a, c in zip(("ctx", "lse", "dqkv", "dbias"), res[DEV], res["cpu"]):
+        assert rel(a, c) < 2e-2, nm
+    # against autograd of plain fp32 attention
+    q = qkv.float().reshape(B, T, 3, heads, 64).permute(2, 0, 3, 1, 4).requires_grad_(True)
+    o = torch.softmax(q[0] @ q[1].transpose(-1, -2) * scale, -1) @ q[2]
+    o.permute(0, 2, 1, 3).reshape(B * T, H).backward(dctx.float())
+    g = q.grad.permute(1, 3, 0, 2, 4).reshape(B * T, 3 * H)
+    assert rel(res[DEV][2], g) < 2e-2
+
+
+def test_mlm_gather_scatter_and_vocab_xent():
+    from metisfl_amd.datasets import synthetic_mlm
+    from metisfl_amd.ops import bert as BO
+    _native()
+    torch.manual_seed(5)
+    B, T, P, H, V, Vp = 4, 128, 20, 256, 30522, 30528
+    rec = torch.as_tensor(synthetic_mlm(B, T, P, V, seed=3))
+    stride = rec.shape[1]
+    x = torch.randn(B * T, H).to(BF)
+    logits = (torch.randn(B * P, Vp) * 3).to(BF)
+    res = {}
+    for dev in ("cpu", DEV):
+        r = rec.to(dev)
+        sel = torch.empty(B * P, H, dtype=BF, device=dev)
+        BO.mlm_gather(x.to(dev), r, stride, B, T, P, sel, H)
+        back = torch.empty(B * T, H, dtype=BF, device=dev)
+        BO.mlm_scatter(sel, r, stride, B, T, P, back, H)
+        st = torch.zeros(4, device=dev)
+        dl = torch.empty(B * P, Vp, dtype=BF, device=dev)
+        BO.vocab_xent(logits.to(dev), r, stride, B, T, P, V, Vp, st, dlogits=dl)
+        res[dev] = (sel, back, st[:3], dl)
+    for a, c in zip(res[DEV], res["cpu"]):
+        assert rel(a, c) < 1e-2
+    assert float(res[DEV][3][:, V:].float().abs().sum()) == 0.0
+
+
+def test_bert_tiny_step_gpu_vs_cpu():
+    from metisfl_amd.datasets import synthetic_mlm
+    from metisfl_amd.models.bert import BERT_TINY, BertMLM
+    from metisfl_amd.ops.optim import OptimizerSpec
+    _native()
+    nets = {}
+    c = BERT_TINY
+    rec = synthetic_mlm(4, c.seq, c.max_pred, c.vocab, seed=7, rec_stride=c.rec_stride)
+    for dev in ("cpu", DEV):
+        n = BertMLM(batch_size=4, device=dev, seed=2, config=c, optimizer=OptimizerSpec("vanilla_sgd", 0.0))
+        n.zero_grad_in_optimizer = False
+        n._train_body(n.make_dataset(rec, shuffle=False))
+        nets[dev] = n
+    torch.cuda.synchronize()
+    a, b = nets["cpu"].state.grad32.double(), nets[DEV].state.grad32.double().cpu()
+    cos = float(a @ b / (a.norm() * b.norm()))
+    assert cos > 0.98, cos
+    la = float(nets["cpu"].stats[0]) / float(nets["cpu"].stats[2])
+    lb = float(nets[DEV].stats[0].cpu()) / float(nets[DEV].stats[2].cpu())
+    assert abs(la - lb) < 0.02 * la
+
+
+def test_bert_base_graph_step_runs():
+    """Full BERT-base (110M) training steps through the captured hipGraph."""
+    from metisfl_amd.datasets import synthetic_mlm
+    from metisfl_amd.models.bert import BertMLM
+    _native()
+    net = BertMLM(batch_size=8, device=DEV, seed=0)
+    c = net.cfg
+    ds = net.make_dataset(synthetic_mlm(32, c.seq, c.max_pred, c.vocab, seed=1, rec_stride=c.rec_stride))
+    net.reset_train_stats()
+    net.train_steps(ds, 3)
+    s = net.train_stats()
+    assert np.isfinite(s["loss"]) and abs(s["loss"] - math.log(c.vocab)) < 1.5, s
