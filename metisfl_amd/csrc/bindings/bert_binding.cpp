@@ -59,13 +59,15 @@ void gemm_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, int64_t M, 
 }
 
 // dw[N][K] (+)= dy^T x  (fp32)
+// zeroed: dw is known to be zero on entry (the training step's gradient
+// buffer, re-zeroed by the optimizer launch) -> no memset before split plans
 void gemm_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t M, int64_t N, int64_t K,
-                bool accumulate) {
+                bool accumulate, bool zeroed) {
   dense_dims(M, N, K);
   need(x, torch::kBFloat16, M * K, "x");
   need(dy, torch::kBFloat16, M * N, "dy");
   need(dw, torch::kFloat32, N * K, "dw");
-  if (!accumulate && mfl::gemm_wgrad_splits((int)M, (int)N, (int)K))
+  if (!accumulate && !zeroed && mfl::gemm_wgrad_splits((int)M, (int)N, (int)K))
     (void)hipMemsetAsync(dw.data_ptr<float>(), 0, dw.numel() * sizeof(float), stream_of(x));
   mfl::launch_gemm_wgrad(bfp(x), bfp(dy), dw.data_ptr<float>(), (int)M, (int)N, (int)K, accumulate,
                          stream_of(x));
@@ -193,6 +195,8 @@ void emb_ln_bwd(torch::Tensor dy, torch::Tensor xsave, torch::Tensor mean, torch
   a.dword = dword.data_ptr<float>();
   a.dpos = dpos.data_ptr<float>();
   a.dtype = dtype.data_ptr<float>();
+  a.B = (int)B;
+  a.pos_reduced = (B % 16 == 0) ? 1 : 0;  // bert.hip kLnBwdRows
   a.M = (int)M;
   mfl::launch_ln_bwd(a, (int)H, true, stream_of(dy));
 }

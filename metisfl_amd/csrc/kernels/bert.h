@@ -41,6 +41,8 @@ struct LnBwdArgs {
   float* dword = nullptr;
   float* dpos = nullptr;
   float* dtype = nullptr;
+  int B = 1, pos_reduced = 0;  // see ln_bwd_kernel
+  int rows = 16;               // rows per block (set by the launcher)
   int M = 0;
 };
 

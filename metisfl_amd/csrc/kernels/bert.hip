@@ -97,12 +97,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwdArgs a) {
   }
 }
 
-constexpr int kLnBwdRows = 32;  // rows per block (4 passes of 8 half-waves)
+constexpr int kLnBwdRows = 16;  // rows per block of the embedding variant (pos_reduced needs B % 16 == 0)
 
+// Embedding variant with a.pos_reduced (B % kLnBwdRows == 0): rows are
+// visited position-major (i -> b = i % B, t = i / B), so a block's rows share
+// one position t and the position-table gradient is reduced in the block
+// instead of by one atomic per element.
 template <int V, bool EMB>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
   constexpr int H = 256 * V;
-  __shared__ float red[3][H];  // dgamma, dbeta, dbias_prev (or dtype) partials
+  __shared__ float red[3][H];  // dgamma, dbeta, sum(dx) partials
   for (int i = threadIdx.x; i < 3 * H; i += 256) (&red[0][0])[i] = 0.f;
   __syncthreads();
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
@@ -111,9 +115,22 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
   for (int v = 0; v < V; ++v)
 #pragma unroll
     for (int k = 0; k < 8; ++k) pg[v][k] = pb[v][k] = pd[v][k] = 0.f;
-  for (int pass = 0; pass < kLnBwdRows / 8; ++pass) {
-    const int row = blockIdx.x * kLnBwdRows + pass * 8 + hw;
-    if (row >= a.M) break;  // uniform per half-wave
+  const int rows = EMB ? kLnBwdRows : a.rows;  // multiple of 8
+  for (int pass = 0; pass < rows / 8; ++pass) {
+    const int i = blockIdx.x * rows + pass * 8 + hw;
+    if (i >= a.M) break;  // uniform per half-wave
+    int row = i, b = 0, t = 0, tok = 0;
+    if constexpr (EMB) {
+      if (a.pos_reduced) {
+        b = i % a.B;
+        t = i / a.B;
+        row = b * a.T + t;
+      } else {
+        b = i / a.T;
+        t = i - b * a.T;
+      }
+      tok = a.tokens[(int64_t)b * a.tok_stride + t];
+    }
     const float mean = a.mean[row], rstd = a.rstd[row];
     float dy[V][8], xh[V][8], gg[V][8];
     float s1 = 0.f, s2 = 0.f;
@@ -134,12 +151,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
       }
     }
     const float m1 = hsum32(s1) * (1.f / H), m2 = hsum32(s2) * (1.f / H);
-    int b = 0, t = 0, tok = 0;
-    if constexpr (EMB) {
-      b = row / a.T;
-      t = row - b * a.T;
-      tok = a.tokens[(int64_t)b * a.tok_stride + t];
-    }
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const int c = (v * 32 + j) * 8;
@@ -153,7 +164,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           atomicAdd(a.dword + (int64_t)tok * H + c + k, dx[k]);
-          atomicAdd(a.dpos + (int64_t)t * H + c + k, dx[k]);
+          if (!a.pos_reduced) atomicAdd(a.dpos + (int64_t)t * H + c + k, dx[k]);
         }
       } else {
         const uint4 pk = pack8(dx);
@@ -181,6 +192,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
     // otherwise the bias gradient of the GEMM that produced the LN input
     float* d3 = EMB ? a.dtype : a.dbias_prev;
     if (d3) atomicAdd(d3 + c, red[2][c]);
+    if (EMB && a.pos_reduced) atomicAdd(a.dpos + (int64_t)((blockIdx.x * kLnBwdRows) / a.B) * H + c, red[2][c]);
   }
 }
 
@@ -196,8 +208,13 @@ void launch_ln_fwd(const LnFwdArgs& a, int H, bool emb, hipStream_t s) {
 #undef MFL_LN_F
 }
 
-void launch_ln_bwd(const LnBwdArgs& a, int H, bool emb, hipStream_t s) {
-  const unsigned grid = (a.M + kLnBwdRows - 1) / kLnBwdRows;
+void launch_ln_bwd(const LnBwdArgs& args, int H, bool emb, hipStream_t s) {
+  // ~256 blocks: enough to fill the CUs, few enough that the per-block
+  // column partials (3 H global atomics each) stay cheap
+  LnBwdArgs a = args;
+  a.rows = max(16, ((a.M + 255) / 256 + 7) / 8 * 8);
+  const int rows = emb ? kLnBwdRows : a.rows;
+  const unsigned grid = (a.M + rows - 1) / rows;
 #define MFL_LN_B(V_)                                                               \
   if (H == 256 * V_) {                                                             \
     if (emb) ln_bwd_kernel<V_, true><<<grid, 256, 0, s>>>(a);                     \
@@ -210,7 +227,9 @@ void launch_ln_bwd(const LnBwdArgs& a, int H, bool emb, hipStream_t s) {
 
 // =============================================================================
 // dz = dh * gelu'(z) (exact erf GELU) and dbias += column sums of dz.
-// Thread = one 16-B column group, rows [blockIdx.x*kColRows, +kColRows).
+// Block = 512 columns (a wave's 64 lanes x 16 B) x kColRows rows; wave w
+// takes rows w, w+4, ... with 4 rows' loads in flight per step, the 4 waves'
+// column partials meet in LDS, then one atomic per column per block.
 constexpr int kColRows = 64;
 
 template <bool GELU>
@@ -218,43 +237,64 @@ __global__ __launch_bounds__(256) void colsum_kernel(const uint16_t* __restrict_
                                                      const uint16_t* __restrict__ z,
                                                      uint16_t* __restrict__ dz, float* __restrict__ dbias,
                                                      int M, int N) {
-  const int cv = blockIdx.y * 256 + threadIdx.x;
-  if (cv * 8 >= N) return;
-  const int r0 = blockIdx.x * kColRows, r1 = min(M, r0 + kColRows);
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cv = blockIdx.y * 64 + lane;
+  const bool col_ok = cv * 8 < N;
+  const int r0 = blockIdx.x * kColRows;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int r = r0; r < r1; ++r) {
-    const int64_t off = (int64_t)r * N + cv * 8;
-    float g[8];
-    unpack8(*reinterpret_cast<const uint4*>(dh + off), g);
-    if (GELU) {
-      float zz[8];
-      unpack8(*reinterpret_cast<const uint4*>(z + off), zz);
+  if (col_ok) {
+    for (int rb = r0 + w; rb < min(M, r0 + kColRows); rb += 16) {
+      uint4 gv[4], zv[4];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float cdf = 0.5f * (1.f + erff(zz[k] * 0.70710678f));
-        const float pdf = 0.39894228f * __expf(-0.5f * zz[k] * zz[k]);
-        g[k] *= cdf + zz[k] * pdf;
+      for (int u = 0; u < 4; ++u) {
+        const int r = min(rb + 4 * u, M - 1);  // clamped rows are loaded but not used
+        const int64_t off = (int64_t)r * N + cv * 8;
+        gv[u] = *reinterpret_cast<const uint4*>(dh + off);
+        if (GELU) zv[u] = *reinterpret_cast<const uint4*>(z + off);
       }
-      const uint4 pk = pack8(g);
-      *reinterpret_cast<uint4*>(dz + off) = pk;
-      unpack8(pk, g);  // the bias gradient of what the GEMMs consume
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + 4 * u;
+        if (r >= min(M, r0 + kColRows)) break;
+        float g[8];
+        unpack8(gv[u], g);
+        if (GELU) {
+          float zz[8];
+          unpack8(zv[u], zz);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float cdf = 0.5f * (1.f + erff(zz[k] * 0.70710678f));
+            const float pdf = 0.39894228f * __expf(-0.5f * zz[k] * zz[k]);
+            g[k] *= cdf + zz[k] * pdf;
+          }
+          const uint4 pk = pack8(g);
+          *reinterpret_cast<uint4*>(dz + (int64_t)r * N + cv * 8) = pk;
+          unpack8(pk, g);  // the bias gradient of what the GEMMs consume
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += g[k];
+      }
     }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] += g[k];
   }
-  if (dbias)
+  if (!dbias) return;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) atomicAdd(dbias + cv * 8 + k, acc[k]);
+  for (int k = 0; k < 8; ++k) red[w][lane * 8 + k] = acc[k];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int col = blockIdx.y * 512 + c;
+    if (col < N) atomicAdd(dbias + col, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+  }
 }
 
 void launch_gelu_bwd(const uint16_t* dh, const uint16_t* z, uint16_t* dz, float* dbias, int M, int N,
                      hipStream_t s) {
-  dim3 grid((M + kColRows - 1) / kColRows, (N / 8 + 255) / 256);
+  dim3 grid((M + kColRows - 1) / kColRows, (N + 511) / 512);
   colsum_kernel<true><<<grid, 256, 0, s>>>(dh, z, dz, dbias, M, N);
 }
 
 void launch_colsum(const uint16_t* dy, float* dbias, int M, int N, hipStream_t s) {
-  dim3 grid((M + kColRows - 1) / kColRows, (N / 8 + 255) / 256);
+  dim3 grid((M + kColRows - 1) / kColRows, (N + 511) / 512);
   colsum_kernel<false><<<grid, 256, 0, s>>>(dy, nullptr, nullptr, dbias, M, N);
 }
 

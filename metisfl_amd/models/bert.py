@@ -207,7 +207,7 @@ class BertMLM(StaticNet):
         BO.ln_bwd(self.g_u, self.th, self.hm_mean, self.hm_rstd, self._p("head.ln.gamma"), self.g_th,
                   g("head.ln.gamma"), g("head.ln.beta"), R, H)
         BO.gelu_bwd(self.g_th, self.tz, self.g_tz, R, H, dbias=g("head.b"))
-        BO.gemm_wgrad(self.hm, self.g_tz, g("head.w"), R, H, H)
+        BO.gemm_wgrad(self.hm, self.g_tz, g("head.w"), R, H, H, zeroed=True)
         BO.gemm_dgrad(self.g_tz, self._w("head.w"), self.g_hm, R, H, H)
         dout = self.g_out[0]
         BO.mlm_scatter(self.g_hm, self.rec, c.rec_stride, B, T, P, dout, H)
@@ -217,18 +217,18 @@ class BertMLM(StaticNet):
             dx = self.g_out[1] if dout is self.g_out[0] else self.g_out[0]
             BO.ln_bwd(dout, A["fo"], A["m2"], A["r2"], self._p(p + "ln2.gamma"), self.g_fo, g(p + "ln2.gamma"),
                       g(p + "ln2.beta"), M, H, dx2=self.g_a, dbias_prev=g(p + "ffn2.b"))
-            BO.gemm_wgrad(A["h"], self.g_fo, g(p + "ffn2.w"), M, H, F)
+            BO.gemm_wgrad(A["h"], self.g_fo, g(p + "ffn2.w"), M, H, F, zeroed=True)
             BO.gemm_dgrad(self.g_fo, self._w(p + "ffn2.w"), self.g_h, M, H, F)
             BO.gelu_bwd(self.g_h, A["z"], self.g_z, M, F, dbias=g(p + "ffn1.b"))
-            BO.gemm_wgrad(A["a"], self.g_z, g(p + "ffn1.w"), M, F, H)
+            BO.gemm_wgrad(A["a"], self.g_z, g(p + "ffn1.w"), M, F, H, zeroed=True)
             BO.gemm_dgrad(self.g_z, self._w(p + "ffn1.w"), self.g_a, M, F, H, accumulate=True)
             BO.ln_bwd(self.g_a, A["ao"], A["m1"], A["r1"], self._p(p + "ln1.gamma"), self.g_ao, g(p + "ln1.gamma"),
                       g(p + "ln1.beta"), M, H, dx2=dx, dbias_prev=g(p + "out.b"))
-            BO.gemm_wgrad(A["ctx"], self.g_ao, g(p + "out.w"), M, H, H)
+            BO.gemm_wgrad(A["ctx"], self.g_ao, g(p + "out.w"), M, H, H, zeroed=True)
             BO.gemm_dgrad(self.g_ao, self._w(p + "out.w"), self.g_ctx, M, H, H)
             BO.attn_bwd(A["qkv"], A["ctx"], A["lse"], self.g_ctx, self.g_qkv, B, c.heads, scale,
                         dbias=g(p + "qkv.b"))
-            BO.gemm_wgrad(A["x"], self.g_qkv, g(p + "qkv.w"), M, 3 * H, H)
+            BO.gemm_wgrad(A["x"], self.g_qkv, g(p + "qkv.w"), M, 3 * H, H, zeroed=True)
             BO.gemm_dgrad(self.g_qkv, self._w(p + "qkv.w"), dx, M, 3 * H, H, accumulate=True)
             dout = dx
         BO.emb_ln_bwd(dout, self.emb_x, self.emb_mean, self.emb_rstd, self._p("emb.ln.gamma"), self.rec,

@@ -57,10 +57,11 @@ def gemm_dgrad(dy, w, dx, M, N, K, accumulate=False) -> None:
     _put(dx, v)
 
 
-def gemm_wgrad(x, dy, dw, M, N, K, accumulate=False) -> None:
-    """dw (+)= dy^T x  (fp32)."""
+def gemm_wgrad(x, dy, dw, M, N, K, accumulate=False, zeroed=False) -> None:
+    """dw (+)= dy^T x  (fp32).  ``zeroed``: dw is already zero (skips the
+    pre-zeroing of split-K plans; the training step's gradient buffer)."""
     if x.is_cuda:
-        ops().gemm_wgrad(x, dy, dw, M, N, K, accumulate)
+        ops().gemm_wgrad(x, dy, dw, M, N, K, accumulate, zeroed)
         return
     v = _b(dy).reshape(M, N).t() @ _b(x).reshape(M, K)
     if accumulate:
