@@ -88,7 +88,7 @@ std::vector<int64_t> conv_plan(int64_t mode, int64_t N, int64_t H, int64_t W, in
   }
   mfl::ConvGeom g = mode == 0 ? fwd_geom(N, H, W, C, Co, R, S, stride, pad)
                               : dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
-  auto p = mfl::plan_conv_gemm(g);
+  auto p = mfl::plan_conv_gemm(g, mode == 1);
   return plan_vec(p, workspace_floats(g, p), 1);
 }
 
@@ -96,7 +96,7 @@ void run_gemm(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, cons
               const torch::Tensor& y, const c10::optional<torch::Tensor>& ws,
               const c10::optional<torch::Tensor>& stats, bool accum,
               const mfl::BnBwdFusion* bnb = nullptr) {
-  auto p = mfl::plan_conv_gemm(g);
+  auto p = mfl::plan_conv_gemm(g, dgrad);
   float* wsp = nullptr;
   int* counters = nullptr;
   if (p.splits > 1) {

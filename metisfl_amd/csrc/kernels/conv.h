@@ -26,6 +26,7 @@ struct ConvPlan {
   int kchunk = 0;      // reduction elements per split (multiple of 64)
   int stats_rows = 0;  // 1 = the epilogue accumulates BN statistics
   int bk = 64;         // k-tile depth (64 or 128)
+  int par_mc = 0;      // stride-2 dgrad parity decomposition: rows per class (0 = off)
 };
 
 // Kernel argument block.  *_shift = log2 of the divisor when it is a power of
@@ -57,10 +58,11 @@ struct ConvArgs {
   int kchunk;
   int accum;
   int dbg;  // timing experiments only (MFL_CONV_DEBUG): bit0 skip MFMAs, bit1 skip operand DMA
+  int par_mc;  // stride-2 dgrad parity decomposition: rows per class (0 = off)
   int c_shift, q_shift, pq_shift;
 };
 
-ConvPlan plan_conv_gemm(const ConvGeom& g);
+ConvPlan plan_conv_gemm(const ConvGeom& g, bool dgrad = false);
 ConvPlan plan_conv_wgrad(const ConvGeom& g);
 // number of output tiles (= split-K counter slots) of a gemm plan
 int conv_counter_slots(const ConvGeom& g, const ConvPlan& p);

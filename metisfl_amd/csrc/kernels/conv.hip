@@ -37,11 +37,14 @@
 //    reduced in the same pass and added with fp64 atomics into a [2][C]
 //    accumulator (no separate statistics pass).
 //  * Small-M layers (CIFAR 4x4 / 8x8 stages) use split-K to fill >= 256 CUs.
-//    The reduction happens IN the kernel: every slice stores its fp32 tile
-//    slab, then the last-arriving slice (agent-scope release/acquire counter,
-//    guide "In-launch split-K reduction") sums the slabs and runs the
-//    epilogue -- no reduction launch.  wgrad split-K slices accumulate with
-//    fp32 atomics into the pre-zeroed gradient buffer.
+//    The reduction happens IN the kernel: every slice publishes its fp32
+//    tile slab with write-through (sc1) stores and draws an arrival ticket;
+//    the last-arriving slice (guide "In-launch split-K reduction", write-
+//    through form) sums the slabs in slice order with sc1 loads and runs the
+//    epilogue -- no reduction launch, no L2 write-back fence.  wgrad split-K
+//    slices accumulate with fp32 atomics into the pre-zeroed gradient buffer.
+//  * Stride-2 dgrad runs parity-class decomposed (conv_gemm_kernel PAR): no
+//    MFMA work or operand traffic on the structurally zero taps.
 #include "kernels/common.h"
 #include "kernels/conv.h"
 
@@ -134,6 +137,20 @@ __device__ __forceinline__ bf16x8 b128_frag(const uint8_t* tile, int kk, int r0,
   return *reinterpret_cast<const bf16x8*>(tile + row * ROWB + ((ch ^ swz_b128<ROWB>(row)) << 4));
 }
 
+// GEMM row -> output pixel: identity, or the parity-class order of a
+// stride-2 dgrad (see conv_gemm_kernel PAR): row = cls * Mc + (n, y, x) ->
+// pixel (n, 2y + cls/2, 2x + cls%2) of the P x Q output.
+__device__ __forceinline__ int out_pixel(const ConvArgs& a, int row) {
+  if (!a.par_mc) return row;
+  const int q2 = a.g.Q >> 1, pq2 = (a.g.P >> 1) * q2;
+  const int cls = row / a.par_mc;
+  const int mc = row - cls * a.par_mc;
+  const int n = mc / pq2;
+  const int rem = mc - n * pq2;
+  const int y = rem / q2, x = rem - y * q2;
+  return (n * a.g.P + 2 * y + (cls >> 1)) * a.g.Q + 2 * x + (cls & 1);
+}
+
 // Vectorised epilogue shared by the direct and the split-K paths:
 // out[row][col] = bf16(v (+ y_old)), BN sums of the rounded output.
 // `get(row_local, col_local_base, float[8])` supplies 8 consecutive fp32 values.
@@ -169,7 +186,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int n0,
     if (row >= g.M || !col_ok) continue;
     float v[8];
     get(rl, cg * 8, v);
-    const int64_t off = (int64_t)row * g.Ng + col;
+    const int64_t off = (int64_t)out_pixel(a, row) * g.Ng + col;
     uint16_t* dst = y + off;
     if (accum) {
       float o[8];
@@ -268,7 +285,16 @@ __device__ __forceinline__ void dma_k_loop(int nk, Issue& issue, Compute& comput
 
 // ---------------------------------------------------------------------------
 // Forward / dgrad implicit GEMM:  Y[m][n] = sum_k A[m][k] * B[n][k]
-template <int BM, int BN, bool DGRAD, int KS, int ST, int BK>
+//
+// PAR (stride-2 dgrad only): parity-class decomposition.  dX pixel (ih, iw)
+// only receives the taps r == ih + pad (mod 2), s == iw + pad (mod 2): for a
+// 3x3 kernel 4 / 2 / 2 / 1 of the 9 taps, for 1x1 one class gets its single
+// tap and three get none.  The M rows are ordered class-major (4 classes of
+// N x H/2 x W/2 pixels, a tile never straddles two), each class reduces only
+// over its own taps (K_c = taps * Cout), and the epilogue scatters rows back
+// to NHWC pixels.  Without it 3/4 of a stride-2 dgrad's MFMA work and operand
+// traffic multiplies structural zeros.
+template <int BM, int BN, bool DGRAD, int KS, int ST, int BK, bool PAR = false>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   // BK = 64 or 128 k-elements per tile: [row][k] tiles have ROWA-byte rows
   constexpr int ROWA = BK * 2;
@@ -293,8 +319,22 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
   const int kbeg = blockIdx.z * a.kchunk;
-  const int kend = min(g.K, kbeg + a.kchunk);
-  const int nk = (kend - kbeg + BK - 1) / BK;
+  // parity class of this tile (block-uniform): first taps r0 / s0, tap counts
+  // ns (along s), offsets dh / dw of the dY row / column of tap 0
+  int cls = 0, r0 = 0, s0 = 0, ns = 1, dh = 0, dw = 0, kc_end = g.K;
+  if constexpr (PAR) {
+    cls = m0 / a.par_mc;
+    const int qh = cls >> 1, qw = cls & 1;
+    r0 = (qh + g.pad) & 1;
+    s0 = (qw + g.pad) & 1;
+    const int nr = (KS - r0 + 1) >> 1;
+    ns = (KS - s0 + 1) >> 1;
+    dh = (qh + g.pad - r0) >> 1;
+    dw = (qw + g.pad - s0) >> 1;
+    kc_end = nr * ns * g.C;
+  }
+  const int kend = min(kc_end, kbeg + a.kchunk);
+  const int nk = max(0, (kend - kbeg + BK - 1) / BK);
   const int HWC = g.H * g.W * g.C;
 
   // A DMA: instruction i of wave w fills rows (w + 4i)*A_RPI .. (1 KiB); lane
@@ -309,6 +349,20 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   for (int i = 0; i < ACH; ++i) {
     const int m = m0 + lrow + A_ISTEP * i;
     const int mm = m < g.M ? m : 0;
+    if constexpr (PAR) {
+      // (n, y, x) inside the class; dY row of tap j_r is y + dh - j_r
+      const int q2 = g.Q >> 1;
+      const int pq2 = (g.P >> 1) * q2;
+      const int mc = mm - cls * a.par_mc;
+      const int n = mc / pq2;
+      const int rem = mc - n * pq2;
+      const int y = rem / q2;
+      a_nb[i] = n * HWC;
+      a_y0[i] = y + dh;
+      a_x0[i] = rem - y * q2 + dw;
+      if (m >= g.M) a_y0[i] = -(1 << 28);
+      continue;
+    }
     const int n = sdiv(mm, g.P * g.Q, a.pq_shift);
     const int rem = mm - n * g.P * g.Q;
     const int oy = sdiv(rem, g.Q, a.q_shift);
@@ -338,14 +392,19 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
       const int k = kb + a_kc;
       const int rs = sdiv(k, g.C, a.c_shift);
       const int c = k - rs * g.C;
-      const int r = rs / KS;
-      const int s = rs - r * KS;
+      // PAR: rs is the class tap index (j_r, j_s), j_s fastest
+      const int r = PAR ? (ns == 2 ? rs >> 1 : rs) : rs / KS;
+      const int s = PAR ? rs - r * ns : rs - r * KS;
       const bool kv = k < kend;
 #pragma unroll
       for (int i = 0; i < ACH; ++i) {
         int iy, ix;
         bool ok;
-        if (DGRAD) {
+        if (PAR) {
+          iy = a_y0[i] - r;
+          ix = a_x0[i] - s;
+          ok = kv & (iy >= 0) & (ix >= 0);
+        } else if (DGRAD) {
           const int ty = a_y0[i] - r, tx = a_x0[i] - s;
           ok = kv & (ty >= 0) & (tx >= 0);
           if (ST > 1) ok = ok & ((ty % ST) == 0) & ((tx % ST) == 0);
@@ -369,8 +428,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
         const int row = b_row0 + 4 * B_RPI * i;          // k row within the tile
         const int n = n0 + ((b_pch ^ swz_tr<B_ROWB>(row)) * 8);
         const int kr = kb + row;
-        const int rs = sdiv(kr, g.C, a.c_shift);
+        int rs = sdiv(kr, g.C, a.c_shift);
         const int ko = kr - rs * g.C;
+        if (PAR) {  // class tap index -> kernel tap (r0 + 2 j_r, s0 + 2 j_s)
+          const int jr = ns == 2 ? rs >> 1 : rs;
+          rs = (r0 + 2 * jr) * KS + s0 + 2 * (rs - jr * ns);
+        }
         off = ((kr < kend) & (n < g.Ng)) ? (uint32_t)((ko * KS * KS + rs) * g.Ng + n) * 2u : kOOB;
       } else {
         const int n = n0 + lrow + A_ISTEP * i;
@@ -662,21 +725,28 @@ static void set_lds_limit(K* kernel, size_t lds, bool& done) {
   }
 }
 
-template <int BM, int BN, bool DG, int KS, int ST, int BK>
+template <int BM, int BN, bool DG, int KS, int ST, int BK, bool PAR>
 static void launch_gemm_t(const ConvArgs& a, const ConvPlan& p, hipStream_t s) {
   dim3 grid((a.g.M + BM - 1) / BM, (a.g.Ng + BN - 1) / BN, p.splits);
   size_t lds = (size_t)kStages * (BM + BN) * BK * 2;
   const size_t epi = ((size_t)BM * (BN + 4) + 256 * 16 + 8) * sizeof(float);
   if (lds < epi) lds = epi;
   static bool attr_set = false;
-  set_lds_limit(&conv_gemm_kernel<BM, BN, DG, KS, ST, BK>, lds, attr_set);
-  conv_gemm_kernel<BM, BN, DG, KS, ST, BK><<<grid, 256, lds, s>>>(a);
+  set_lds_limit(&conv_gemm_kernel<BM, BN, DG, KS, ST, BK, PAR>, lds, attr_set);
+  conv_gemm_kernel<BM, BN, DG, KS, ST, BK, PAR><<<grid, 256, lds, s>>>(a);
 }
 
 template <int BM, int BN, bool DG, int KS, int ST>
 static void launch_gemm_bk(const ConvArgs& a, const ConvPlan& p, hipStream_t s) {
-  if (p.bk == 128) launch_gemm_t<BM, BN, DG, KS, ST, 128>(a, p, s);
-  else launch_gemm_t<BM, BN, DG, KS, ST, 64>(a, p, s);
+  if constexpr (DG && ST == 2) {
+    if (a.par_mc) {  // parity-decomposed stride-2 dgrad
+      if (p.bk == 128) launch_gemm_t<BM, BN, DG, KS, ST, 128, true>(a, p, s);
+      else launch_gemm_t<BM, BN, DG, KS, ST, 64, true>(a, p, s);
+      return;
+    }
+  }
+  if (p.bk == 128) launch_gemm_t<BM, BN, DG, KS, ST, 128, false>(a, p, s);
+  else launch_gemm_t<BM, BN, DG, KS, ST, 64, false>(a, p, s);
 }
 
 template <int BM, int BN, bool DG>
@@ -703,18 +773,31 @@ static int env_int(const char* name, int dflt) {
   return v && *v ? atoi(v) : dflt;
 }
 
-ConvPlan plan_conv_gemm(const ConvGeom& g) {
+ConvPlan plan_conv_gemm(const ConvGeom& g, bool dgrad) {
   static const int target = env_int("MFL_CONV_TARGET_BLOCKS", 256);
   static const int min_steps = env_int("MFL_CONV_MIN_KSTEPS", 4);
+  static const int parity_on = env_int("MFL_DGRAD_PARITY", 1);
   ConvPlan p;
   p.bm = g.M >= 8192 ? 128 : 64;
   p.bn = g.Ng >= 128 && g.M >= 16384 ? 128 : 64;
   const int tiles = ((g.M + p.bm - 1) / p.bm) * ((g.Ng + p.bn - 1) / p.bn);
+  // stride-2 dgrad: parity classes of N x P/2 x Q/2 rows (whole tiles each);
+  // a class reduces over at most ceil(R/2) * ceil(S/2) taps
+  int K = g.K;
+  // (3x3 only: a 1x1 stride-2 dgrad already skips its zero taps through the
+  // out-of-range DMA path, and measured no faster decomposed)
+  if (dgrad && parity_on && g.R == 3 && g.stride == 2 && g.P % 2 == 0 && g.Q % 2 == 0) {
+    const int mc = g.N * (g.P / 2) * (g.Q / 2);
+    if (mc % p.bm == 0) {
+      p.par_mc = mc;
+      K = ((g.R + 1) / 2) * ((g.S + 1) / 2) * g.C;
+    }
+  }
   // 128-deep k-tiles halve the serial k-steps (and barriers) of a block when
   // the reduction is long enough; the 128x128 tile keeps BK = 64 (LDS)
   static const int bk128_min_k = env_int("MFL_CONV_BK128_MIN_K", 512);  // measured best (r1 sweep)
-  p.bk = (g.K >= bk128_min_k && !(p.bm == 128 && p.bn == 128)) ? 128 : 64;
-  const int ksteps = (g.K + p.bk - 1) / p.bk;
+  p.bk = (K >= bk128_min_k && !(p.bm == 128 && p.bn == 128)) ? 128 : 64;
+  const int ksteps = (K + p.bk - 1) / p.bk;
   int splits = 1;
   while (tiles * splits < target && ksteps / (splits * 2) >= min_steps && splits < 16) splits *= 2;
   p.splits = splits;
@@ -742,6 +825,7 @@ void launch_conv_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const ui
   a.stats = stats;
   a.kchunk = p.kchunk;
   a.accum = accum ? 1 : 0;
+  a.par_mc = dgrad ? p.par_mc : 0;
   fill_shifts(a);
 #define MFL_CONV_CASE(BM_, BN_)                                    \
   if (p.bm == BM_ && p.bn == BN_) {                                \
@@ -795,6 +879,7 @@ void launch_conv_dgrad_bnb(const ConvGeom& g, const ConvPlan& p, const uint16_t*
   a.bn_mean = f.mean;
   a.bn_invstd = f.invstd;
   a.bn_acc = f.acc;
+  a.par_mc = p.par_mc;
   fill_shifts(a);
   if (p.bm == 128 && p.bn == 128) launch_gemm_ks<128, 128, true>(a, p, s);
   else if (p.bm == 128 && p.bn == 64) launch_gemm_ks<128, 64, true>(a, p, s);
