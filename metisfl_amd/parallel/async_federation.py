@@ -1,0 +1,180 @@
+"""Asynchronous collective federation: FedRec over point-to-point RCCL.
+
+The reference's asynchronous protocol re-dispatches every learner the moment
+its task completes (AsynchronousScheduler, scheduling/asynchronous_scheduler.h:
+12-18), aggregates over the latest model of every active learner
+(ScheduledCardinality selector, selection/scheduled_cardinality.h:21-29) with
+the recency rule FedRec (aggregation/federated_recency.cc:8-100: replace the
+finisher's previous contribution in a running weighted sum) and sends the new
+community model to the finisher only.  All models cross the controller as
+serialized gRPC messages.
+
+Here one process per GPU hosts a learner; rank 0
+is also the aggregator.  A finished learner posts its task metadata to the
+process group's key-value store (the control channel), then ``send``s its
+flat fp32 model to rank 0 and ``recv``s the community model back -- one
+point-to-point RCCL transfer each way over xGMI, nothing through the host.
+Rank 0 keeps, in HBM, the running sum S = sum_i w_i theta_i, Z = sum_i w_i
+and every learner's last contribution, and applies the FedRec update with
+the K2 rolling kernels:
+
+    S -= w_old * theta_old ; Z -= w_old        (learner seen before)
+    S += w_new * theta_new ; Z += w_new
+    community = S / Z
+
+Rank 0 trains its own shard in chunks of ``poll_every`` local steps and
+serves pending submissions between chunks, so a finisher waits at most one
+chunk.  The weights are the NUM_TRAINING_EXAMPLES (or batch / participant)
+scaling inputs, un-normalised, as FedRec consumes them.
+"""
+from __future__ import annotations
+
+import json
+import time
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from metisfl_amd.ops import aggregate as agg
+from metisfl_amd.parallel.comm import Comm
+from metisfl_amd.parallel.federation import FederationConfig
+
+_KEY = "metisfl_async/{}/{}"
+
+
+@dataclass
+class AsyncUpdate:
+    learner: int
+    task: int
+    weight: float
+    received_at: float
+    aggregation_ms: float
+    train_loss: float
+    completed_batches: int
+
+
+class AsyncCollectiveFederation:
+    def __init__(self, comm: Comm, net, train_ds, cfg: FederationConfig, tasks_per_learner: int = 2,
+                 poll_every: int = 16, store=None, broadcast_initial: bool = True):
+        self.comm, self.net, self.train_ds, self.cfg = comm, net, train_ds, cfg
+        self.rank, self.world = comm.rank, comm.world
+        self.tasks = tasks_per_learner
+        self.poll_every = max(1, poll_every)
+        self.store = store if store is not None else (
+            dist.distributed_c10d._get_default_store() if comm.distributed else None)
+        n = int(train_ds.n)
+        self.num_local_updates = cfg.local_epochs * max(1, -(-n // cfg.batch_size))
+        self.steps_done = 0
+        self.updates: list[AsyncUpdate] = []   # rank 0: every FedRec update applied
+        st = net.state
+        if broadcast_initial and comm.distributed:
+            comm.broadcast_(st.model32, src=0)
+            st.refresh_bf16()
+            st.set_anchor()
+        if self.rank == 0:
+            dev = st.model32.device
+            self.S = torch.zeros_like(st.model32)
+            self.Z = 0.0
+            self.last = [None] * self.world        # each learner's last contribution (HBM)
+            self.last_w = [0.0] * self.world
+            self.next_task = [0] * self.world       # next expected task per learner
+            self.rbuf = torch.empty_like(st.model32, device=dev)
+
+    # ---- learner side ------------------------------------------------------------
+    def _weight(self, completed_batches: int) -> float:
+        sf = self.cfg.scaling_factor
+        if sf == "NUM_TRAINING_EXAMPLES":
+            return float(self.train_ds.n)
+        if sf == "NUM_COMPLETED_BATCHES":
+            return float(completed_batches)
+        return 1.0  # NUM_PARTICIPANTS
+
+    def _train(self, nsteps: int) -> None:
+        self.net.train_steps(self.train_ds, nsteps, step_offset=self.steps_done)
+        self.steps_done += nsteps
+
+    def run(self) -> list[AsyncUpdate]:
+        """Run ``tasks_per_learner`` asynchronous tasks on this learner; rank 0
+        also serves every other learner's submissions until all are done."""
+        for task in range(self.tasks):
+            self.net.reset_train_stats()
+            left = self.num_local_updates
+            while left > 0:
+                k = min(left, self.poll_every) if self.rank == 0 else left
+                self._train(k)
+                left -= k
+                if self.rank == 0:
+                    self.serve(block=False)
+            meta = {"task": task, "weight": self._weight(self.num_local_updates),
+                    "loss": self.net.train_stats()["loss"], "batches": self.num_local_updates}
+            if self.rank == 0:
+                self._fedrec(0, self.net.state.model32, meta)
+                self.net.state.model32.copy_(self._community())
+                self._install()
+            else:
+                self.store.set(_KEY.format(self.rank, task), json.dumps(meta))
+                dist.send(self.net.state.model32, dst=0)
+                dist.recv(self.net.state.model32, src=0)
+                self._install()
+        if self.rank == 0:
+            while any(self.next_task[r] < self.tasks for r in range(1, self.world)):
+                if not self.serve(block=False):
+                    time.sleep(0.001)
+        return self.updates
+
+    def _install(self) -> None:
+        st = self.net.state
+        st.refresh_bf16()
+        st.set_anchor()
+
+    # ---- aggregator side (rank 0) ---------------------------------------------------
+    def serve(self, block: bool = False) -> int:
+        """Apply every pending submission (FedRec) and answer it with the
+        community model.  Returns the number served."""
+        served = 0
+        for r in range(1, self.world):
+            t = self.next_task[r]
+            if t >= self.tasks:
+                continue
+            key = _KEY.format(r, t)
+            if not block and not self.store.check([key]):
+                continue
+            meta = json.loads(self.store.get(key))
+            dist.recv(self.rbuf, src=r)
+            self._fedrec(r, self.rbuf, meta)
+            dist.send(self._community(), dst=r)
+            self.next_task[r] = t + 1
+            served += 1
+        return served
+
+    def _fedrec(self, r: int, theta: torch.Tensor, meta: dict) -> None:
+        t0 = time.perf_counter()
+        w = float(meta["weight"])
+        if self.last[r] is not None:
+            agg.rolling_op(self.S, self.last[r], agg.MERGE_SUB, self.last_w[r])
+            self.Z -= self.last_w[r]
+        else:
+            self.last[r] = torch.empty_like(theta)
+        agg.rolling_op(self.S, theta, agg.MERGE_ADD, w)
+        self.Z += w
+        self.last[r].copy_(theta)
+        self.last_w[r] = w
+        if theta.is_cuda:
+            torch.cuda.synchronize(theta.device)
+        self.updates.append(AsyncUpdate(r, int(meta["task"]), w, time.time(),
+                                        (time.perf_counter() - t0) * 1e3, float(meta["loss"]),
+                                        int(meta["batches"])))
+
+    def _community(self) -> torch.Tensor:
+        c = self.S.clone()
+        agg.rolling_op(c, None, agg.SCALE_DIV, self.Z)
+        return c
+
+    def community_reference(self) -> np.ndarray:
+        """Host recomputation of sum_i w_i theta_i / sum_i w_i over the latest
+        contributions (tests)."""
+        xs = [x.double().cpu().numpy() for x in self.last if x is not None]
+        ws = [w for x, w in zip(self.last, self.last_w) if x is not None]
+        return sum(w * x for w, x in zip(ws, xs)) / sum(ws)

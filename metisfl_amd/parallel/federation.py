@@ -16,9 +16,10 @@ data shard stay resident in HBM across rounds.  A synchronous FedAvg round is
 
 Semi-synchronous rounds use the same barrier with per-learner step budgets
 recomputed from the measured per-batch times (controller.cc:520-569).
-Asynchronous federations (per-learner dispatch, FedRec) run on the controller
-path (gRPC control plane + native engine), where every learner is scheduled
-on its own.
+Asynchronous federations (per-learner dispatch, FedRec) are
+``async_federation.AsyncCollectiveFederation`` (point-to-point send / recv to
+the aggregator rank) on this data plane, or the controller path (gRPC
+control plane + native engine's asynchronous scheduler).
 
 Rank 0 additionally drives the native controller engine (engine_bridge.py)
 so the collective federation has the reference's runtime metadata, task
