@@ -41,6 +41,7 @@ import torch
 from metisfl_amd.ops import optim as opt_ops
 from metisfl_amd.parallel import scaling
 from metisfl_amd.parallel.comm import Comm
+from metisfl_amd.utils import tracing
 
 META_FIELDS = ("num_training_examples", "completed_batches", "ms_per_batch", "ms_per_epoch",
                "train_loss", "train_accuracy", "completed_epochs", "global_iteration",
@@ -60,6 +61,7 @@ class FederationConfig:
     evaluate_test: bool = True             # learner test-set eval at task end
     eval_max_steps: int | None = None
     quantify: bool = True                  # per-variable zero counts of each community model
+    jsonl_log: str | None = None           # rank 0: one JSON line per round (utils/tracing.py)
     extra: dict = field(default_factory=dict)
 
 
@@ -77,6 +79,9 @@ class RoundRecord:
     weights: list
     num_local_updates: list
     test_metrics: dict | None = None
+    allreduce_ms: float = 0.0              # the model all-reduce alone
+    allreduce_gbps: float = 0.0            # algorithm bandwidth: model bytes / all-reduce time
+    hbm_used_bytes: int = 0
 
     def to_json(self) -> dict:
         d = asdict(self)
@@ -114,6 +119,7 @@ class CollectiveFederation:
         dev = comm.device
         self._ev0 = torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else None
         self._ev1 = torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else None
+        self._log = tracing.JsonlLog(cfg.jsonl_log if comm.rank == 0 else None)
         if broadcast_initial:
             self.broadcast_initial_model()
 
@@ -133,15 +139,16 @@ class CollectiveFederation:
         net = self.net
         net.reset_train_stats()
         t0 = time.perf_counter()
-        if self._ev0 is not None:
-            self._ev0.record()
-        net.train_steps(self.train_ds, nsteps, step_offset=self.steps_done)
-        if self._ev1 is not None:
-            self._ev1.record()
-            self._ev1.synchronize()
-            ms = self._ev0.elapsed_time(self._ev1)
-        else:
-            ms = (time.perf_counter() - t0) * 1e3
+        with tracing.range("metisfl.local_train"):
+            if self._ev0 is not None:
+                self._ev0.record()
+            net.train_steps(self.train_ds, nsteps, step_offset=self.steps_done)
+            if self._ev1 is not None:
+                self._ev1.record()
+                self._ev1.synchronize()
+                ms = self._ev0.elapsed_time(self._ev1)
+            else:
+                ms = (time.perf_counter() - t0) * 1e3
         self.steps_done += nsteps
         tr = net.train_stats()
         out = {"ms": ms, "ms_per_batch": ms / max(1, nsteps),
@@ -149,7 +156,8 @@ class CollectiveFederation:
                "completed_batches": nsteps, "completed_epochs": nsteps / self._spe,
                "train_loss": tr["loss"], "train_accuracy": tr["accuracy"]}
         if self.cfg.evaluate_test and self.test_ds is not None:
-            out["test"] = net.evaluate(self.test_ds, self.cfg.eval_max_steps)
+            with tracing.range("metisfl.evaluate"):
+                out["test"] = net.evaluate(self.test_ds, self.cfg.eval_max_steps)
         return out
 
     def aggregation_weights(self, meta: np.ndarray) -> list[float]:
@@ -165,9 +173,16 @@ class CollectiveFederation:
         t0 = time.perf_counter()
         weights = self.aggregation_weights(meta)
         st = self.net.state
+        self.last_allreduce_ms = 0.0
         if self.world > 1:
-            opt_ops.scale_(st.model32, weights[self.rank])
-            self.comm.all_reduce_(st.model32)
+            with tracing.range("metisfl.scale"):
+                opt_ops.scale_(st.model32, weights[self.rank])
+            self._sync()
+            t1 = time.perf_counter()
+            with tracing.range("metisfl.all_reduce"):
+                self.comm.all_reduce_(st.model32)
+                self._sync()
+            self.last_allreduce_ms = (time.perf_counter() - t1) * 1e3
         st.refresh_bf16()
         st.set_anchor()
         self._sync()
@@ -208,9 +223,17 @@ class CollectiveFederation:
         completed = time.time()
         weights, agg_ms = self.aggregate(meta)
         agg_done = time.time()
+        ar_ms = getattr(self, "last_allreduce_ms", 0.0)
+        nbytes = self.net.state.model32.numel() * 4
         rec = RoundRecord(self.global_iteration, started, completed, completed, agg_done,
                           (agg_done - started) * 1e3, res["ms"], agg_ms, meta, weights,
-                          list(self.num_local_updates), res.get("test"))
+                          list(self.num_local_updates), res.get("test"), ar_ms,
+                          nbytes / (ar_ms * 1e6) if ar_ms > 0 else 0.0,
+                          tracing.hbm_usage(self.comm.device).get("used_bytes", 0)
+                          if self.comm.device.type == "cuda" else 0)
+        if self.rank == 0:
+            self._log.write({"kind": "round", **rec.to_json(),
+                             "rounds_per_s": 1e3 / rec.round_ms if rec.round_ms > 0 else 0.0})
         if self.engine is not None:
             self.engine.record_round(rec, self.cfg.batch_size,
                                      self._quantifiers() if self.cfg.quantify else None)
