@@ -44,6 +44,8 @@ def main(argv=None):
     p.add_argument("-c", "--communication_specs_protobuff_serialized_hexadecimal", default=None)
     p.add_argument("-m", "--model_hyperparameters_protobuff_serialized_hexadecimal", default=None)
     p.add_argument("-s", "--model_store_config_protobuff_serialized_hexadecimal", default=None)
+    p.add_argument("--checkpoint_dir", default=None,
+                   help="snapshot the controller state here; resume from it if present")
     a = p.parse_args(argv)
     params = build_params(a.controller_server_entity_protobuff_serialized_hexadecimal,
                           a.global_model_specs_protobuff_serialized_hexadecimal,
@@ -52,7 +54,7 @@ def main(argv=None):
                           a.model_store_config_protobuff_serialized_hexadecimal)
     MetisLogger.info('Controller Parameters: """%s"""', params)
     inst = ControllerInstance()
-    inst.start(params)
+    inst.start(params, checkpoint_dir=a.checkpoint_dir)
     inst.shutdown()
 
 

@@ -19,9 +19,11 @@ class ControllerInstance:
         self.servicer: ControllerServicer | None = None
         self._signal = False
 
-    def start(self, controller_params_pb) -> int:
+    def start(self, controller_params_pb, checkpoint_dir: str | None = None) -> int:
+        """``checkpoint_dir``: snapshot the engine there after every round /
+        membership change and resume from it when it already holds one."""
         assert isinstance(controller_params_pb, metis_pb2.ControllerParams)
-        self.servicer = ControllerServicer(controller_params_pb)
+        self.servicer = ControllerServicer(controller_params_pb, checkpoint_dir=checkpoint_dir)
         return self.servicer.start()
 
     def shutdown(self, instantly: bool = False) -> None:

@@ -21,6 +21,7 @@ Structure here:
 """
 from __future__ import annotations
 
+import os
 import threading
 from concurrent import futures
 
@@ -173,10 +174,25 @@ class LearnerHealthMonitor:
 class ControllerServicer(controller_pb2_grpc.ControllerServiceServicer):
 
     def __init__(self, controller_params_pb, dispatch_workers: int = 16,
-                 heartbeat_interval_s: float | None = 5.0, heartbeat_threshold: int = 3):
+                 heartbeat_interval_s: float | None = 5.0, heartbeat_threshold: int = 3,
+                 checkpoint_dir: str | None = None):
         self.params = controller_params_pb
         self.engine = E.Controller(controller_params_pb.SerializeToString())
         self.dispatcher = LearnerDispatcher(self.engine, dispatch_workers)
+        # the engine state is snapshotted after every membership
+        # change and every completed round; a controller started on an
+        # existing checkpoint restores it and re-dispatches the round
+        self.checkpoint_dir = checkpoint_dir
+        self._ckpt_lock = threading.Lock()
+        self._ckpt_gi = -1
+        self.resumed = False
+        if checkpoint_dir and os.path.exists(self._ckpt_path()):
+            with open(self._ckpt_path(), "rb") as f:
+                self.engine.restore(f.read())
+            self.resumed = True
+            self._ckpt_gi = self.engine.global_iteration()
+            MetisLogger.info("Controller restored from %s (round %d, %d learners)", self._ckpt_path(),
+                             self._ckpt_gi, self.engine.num_learners())
         self._shutdown = threading.Event()
         self._server: GRPCServerMaxMsgLength | None = None
         self._stop_thread: threading.Thread | None = None
@@ -193,7 +209,32 @@ class ControllerServicer(controller_pb2_grpc.ControllerServiceServicer):
             self.monitor.start()
         MetisLogger.info("Controller servicer listening on %s (port %d)",
                          self._server.grpc_endpoint.listening_endpoint, self._server.port)
+        if self.resumed:  # re-broadcast the current round to the restored learners
+            for d in controller_pb2.GetParticipatingLearnersResponse.FromString(
+                    self.engine.participating_learners()).learner:
+                self.dispatcher.register(d.id, d.server_entity)
+            self.dispatcher.submit(self.engine.resume_dispatch())
         return self._server.port
+
+    # -- checkpoint ------------------------------------------------------
+    def _ckpt_path(self) -> str:
+        return os.path.join(self.checkpoint_dir, "controller.ckpt")
+
+    def checkpoint(self, force: bool = False) -> bool:
+        """Write the engine snapshot (atomic rename) if the round advanced."""
+        if not self.checkpoint_dir:
+            return False
+        with self._ckpt_lock:
+            gi = self.engine.global_iteration()
+            if not force and gi == self._ckpt_gi:
+                return False
+            os.makedirs(self.checkpoint_dir, exist_ok=True)
+            tmp = self._ckpt_path() + ".tmp"
+            with open(tmp, "wb") as f:
+                f.write(self.engine.checkpoint())
+            os.replace(tmp, self._ckpt_path())
+            self._ckpt_gi = gi
+            return True
 
     @property
     def port(self) -> int:
@@ -266,6 +307,7 @@ class ControllerServicer(controller_pb2_grpc.ControllerServiceServicer):
             self._abort(context, 6 if code == 6 else 3, msg)
         self.dispatcher.register(lid, request.server_entity)
         MetisLogger.info("Learner %s joined the federation.", lid)
+        self.checkpoint(force=True)
         self.dispatcher.submit(dispatch)
         return controller_pb2.JoinFederationResponse(ack=_ack(True), learner_id=lid, auth_token=tok)
 
@@ -278,6 +320,7 @@ class ControllerServicer(controller_pb2_grpc.ControllerServiceServicer):
             self._abort(context, grpc.StatusCode.CANCELLED.value[0], e.args[1])
         self.dispatcher.forget(request.learner_id)
         MetisLogger.info("Learner %s left the federation.", request.learner_id)
+        self.checkpoint(force=True)
         return controller_pb2.LeaveFederationResponse(ack=_ack(True))
 
     # -- task flow ---------------------------------------------------------------------------
@@ -291,6 +334,7 @@ class ControllerServicer(controller_pb2_grpc.ControllerServiceServicer):
         except E.EngineStatusError as e:
             code, msg = e.args
             self._abort(context, code if code in (3, 5, 7, 16) else 13, msg)
+        self.checkpoint()
         self.dispatcher.submit(dispatch)
         return controller_pb2.MarkTaskCompletedResponse(ack=_ack(True))
 
@@ -301,6 +345,7 @@ class ControllerServicer(controller_pb2_grpc.ControllerServiceServicer):
         except (E.EngineStatusError, RuntimeError, ValueError) as e:
             self._abort(context, grpc.StatusCode.UNAUTHENTICATED.value[0], str(e))
         MetisLogger.info("Replaced the community model.")
+        self.checkpoint(force=True)
         return controller_pb2.ReplaceCommunityModelResponse(ack=_ack(True))
 
     def ShutDown(self, request, context):

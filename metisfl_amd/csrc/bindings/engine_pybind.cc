@@ -112,6 +112,25 @@ PYBIND11_MODULE(_engine, m) {
              }
              return dispatch_to_py(d);
            })
+      .def("checkpoint",
+           [](const Controller& c) {
+             std::string s;
+             {
+               py::gil_scoped_release nogil;
+               s = c.checkpoint();
+             }
+             return B(s);
+           })
+      .def("restore", [](Controller& c, const std::string& blob) { c.restore(blob); })
+      .def("resume_dispatch",
+           [](Controller& c) {
+             Dispatch d;
+             {
+               py::gil_scoped_release nogil;
+               d = c.resume_dispatch();
+             }
+             return dispatch_to_py(d);
+           })
       .def("evicted", &Controller::evicted)
       .def("learner_ids", &Controller::learner_ids)
       .def("num_learners", &Controller::num_learners)

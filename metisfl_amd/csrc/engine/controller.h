@@ -148,6 +148,11 @@ class Controller {
   uint32_t global_iteration() const;
   size_t num_learners() const;
 
+  // --- checkpoint / resume (checkpoint.cc) -------------------------------------
+  std::string checkpoint() const;          // self-describing binary snapshot
+  void restore(const std::string& blob);   // into a controller built with the same params
+  Dispatch resume_dispatch();              // the current round's RunTask for every learner
+
  private:
   void validate(const std::string& id, const std::string& token) const;
   std::string make_run_task(const std::string& id, const FederatedModelT& model,

@@ -259,3 +259,35 @@ def test_evicting_a_straggler_releases_the_sync_barrier():
     assert np.allclose(arrays[0], [3, 3, 3])
     with pytest.raises(E.EngineStatusError):
         c.evict_learner(dead)
+
+
+def test_checkpoint_restore_resumes_the_federation():
+    """snapshot after two rounds, restore into a fresh engine,
+    identical lineages / learners / community model, the round is re-dispatched
+    and the old credentials keep working."""
+    c = E.Controller(params())
+    c.replace_community_model(fed_model([0, 0, 0]))
+    a = join(c, 1, 20)
+    b = join(c, 2, 60)
+    for gi in (1, 2):
+        c.learner_completed_task(a[0], a[1], completed([1, 1, 1], gi))
+        c.learner_completed_task(b[0], b[1], completed([3, 3, 3], gi))
+    assert c.global_iteration() == 3
+    blob = c.checkpoint()
+    r = E.Controller(params())
+    r.restore(blob)
+    assert r.global_iteration() == 3
+    assert r.learner_ids() == c.learner_ids()
+    assert r.community_model() == c.community_model()
+    assert r.runtime_metadata_lineage(-1) == c.runtime_metadata_lineage(-1)
+    assert r.participating_learners() == c.participating_learners()
+    assert r.local_task_lineage(-1, c.learner_ids()) == c.local_task_lineage(-1, c.learner_ids())
+    d = r.resume_dispatch()
+    assert sorted(w for w, _ in d["run_tasks"]) == sorted(c.learner_ids())
+    assert all(run_req(q).task.global_iteration == 3 for _, q in d["run_tasks"])
+    # old tokens are valid on the restored controller; the next round closes
+    r.learner_completed_task(a[0], a[1], completed([2, 2, 2], 3))
+    d = r.learner_completed_task(b[0], b[1], completed([2, 2, 2], 3))
+    assert r.global_iteration() == 4 and len(d["run_tasks"]) == 2
+    with pytest.raises(E.EngineStatusError):
+        r.restore(b"garbage-not-a-checkpoint")

@@ -187,3 +187,48 @@ def test_dead_learner_is_evicted_and_sync_rounds_continue(tmp_path):
     finally:
         client.shutdown()
         srv.stop()
+
+
+def test_controller_restart_resumes_from_checkpoint(tmp_path):
+    """the controller snapshots its engine; a new controller
+    process on the same address restores it, re-dispatches the round and the
+    still-running learners carry the federation on with their credentials."""
+    import socket
+
+    from metisfl_amd.controller.servicer import ControllerServicer
+    from metisfl_amd.learner.fake import EchoModelOps
+    from metisfl_amd.utils.grpc_controller_client import GRPCControllerClient
+    from metisfl_amd.utils.grpc_learner_client import GRPCLearnerClient
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ckpt = str(tmp_path / "ckpt")
+    params = controller_params(port=port)
+    ctrl = ControllerServicer(params, heartbeat_interval_s=None, checkpoint_dir=ckpt)
+    ctrl.start()
+    ent = M.construct_server_entity_pb("127.0.0.1", port)
+    client = GRPCControllerClient(ent)
+    learners = []
+    try:
+        model = model_from_arrays(["w"], [np.arange(4, dtype=np.float32)])
+        assert client.replace_community_model(1, model)
+        learners = [start_learner(ent, EchoModelOps(0.05), tmp_path, i, n_train=10 * (i + 1)) for i in range(2)]
+        wait_for(lambda: ctrl.engine.global_iteration() >= 3, what="rounds before the restart")
+        ctrl.stop()
+        gi = ctrl.engine.global_iteration()
+        ctrl2 = ControllerServicer(params, heartbeat_interval_s=None, checkpoint_dir=ckpt)
+        assert ctrl2.resumed and ctrl2.engine.num_learners() == 2
+        assert ctrl2.engine.global_iteration() >= gi - 1
+        ctrl2.start()
+        ctrl = ctrl2
+        wait_for(lambda: ctrl2.engine.global_iteration() >= gi + 2, what="rounds after the restart")
+        md = client.get_runtime_metadata(0)
+        assert len(md.metadata) >= gi + 1
+    finally:
+        for l, s in learners:
+            try:
+                GRPCLearnerClient(l.learner_server_entity).shutdown_learner()
+            except Exception:
+                pass
+        client.shutdown()
+        ctrl.stop()
