@@ -125,9 +125,6 @@ class DriverSessionBase:
             names, trainable, values = TorchModelOps(model, device="cpu", seed=self.seed).get_model_weights()
             self._initial_model = model_from_arrays(names, values, trainable)
             return "torch"
-        if model == "fake" or model is None:
-            self._initial_model = model_from_arrays(["w"], [__import__("numpy").zeros(4, "float32")])
-            return "fake"
         raise RuntimeError("Not a supported model type (StaticModelDef, family name or TorchModelDef).")
 
     def _dump_recipe(self, fn, name):

@@ -39,3 +39,13 @@ def _bert_tiny(batch_size, device="cpu", optimizer=None, seed=0, **kw):
     from metisfl_amd.models.bert import BERT_TINY, BertMLM
     return BertMLM(batch_size=batch_size, device=device, optimizer=optimizer, seed=seed,
                    config=kw.pop("config", BERT_TINY), **kw)
+
+
+@register_family("mnist_fc")
+def _mnist_fc(batch_size, device="cpu", optimizer=None, seed=0, **kw):
+    """MNIST dense model (examples/keras/models/mnist_fc.py: 784-128-128-10,
+    the FashionMNIST topology; its SGD lr 0.02 is the learner's optimizer)."""
+    from metisfl_amd.models.sequential import FashionMnistFC
+    from metisfl_amd.ops.optim import OptimizerSpec
+    return FashionMnistFC(batch_size=batch_size, device=device,
+                          optimizer=optimizer or OptimizerSpec("vanilla_sgd", 0.02), seed=seed, **kw)

@@ -1,0 +1,53 @@
+"""The reference's other example model families on the TorchModelDef path
+(neuroimaging 2D/3D CNNs, IMDB LSTM, PyTorch MLP) train through
+TorchModelOps with the fused flat-buffer optimizer; MNIST FC is a static
+family."""
+import numpy as np
+import pytest
+
+from metisfl_amd.models.model_dataset import ModelDataset
+from metisfl_amd.utils.proto_messages_factory import MetisProtoMessages as M
+from metisfl_amd.utils.proto_messages_factory import ModelProtoMessages as MM
+
+
+def _task(n, lr=0.01):
+    hp = M.construct_hyperparameters_pb(4, MM.construct_optimizer_config_pb(MM.construct_vanilla_sgd_optimizer_pb(lr)))
+    return M.construct_learning_task_pb(n, 0.0), hp
+
+
+@pytest.mark.parametrize("name", ["brainage2d", "brainage3d", "ad2d", "ad3d", "imdb", "mlp"])
+def test_torch_example_model_trains(name):
+    import examples.models.torch_models as TM
+    from metisfl_amd.models.torch_ops import TorchModelOps
+    small = (4, 8)
+    if name == "brainage2d":
+        d, (x, y) = TM.BrainAge2DCNN(small), TM.synthetic_volumes(8, (16, 16))
+    elif name == "brainage3d":
+        d, (x, y) = TM.BrainAge3DCNN(small), TM.synthetic_volumes(8, (8, 8, 8))
+    elif name == "ad2d":
+        d, (x, y) = TM.AlzheimersDisease2DCNN(small), TM.synthetic_volumes(8, (16, 16), classes=2)
+    elif name == "ad3d":
+        d, (x, y) = TM.AlzheimersDisease3DCNN(small), TM.synthetic_volumes(8, (8, 8, 8), classes=2)
+    elif name == "imdb":
+        rng = np.random.default_rng(0)
+        d, x, y = TM.ImdbLSTM(vocab=100, emb=8, hidden=8), rng.integers(0, 100, (8, 12)), rng.integers(0, 2, 8)
+    else:
+        rng = np.random.default_rng(0)
+        d, x, y = TM.IonosphereMLP(), rng.standard_normal((8, 34)).astype(np.float32), rng.integers(0, 2, 8)
+    ops = TorchModelOps(d, device="cpu")
+    task, hp = _task(4)
+    ds = ModelDataset(x=x, y=y, size=len(x))
+    res = ops.train_model(ds, task, hp)
+    assert res is not None
+    names, trainable, arrays = ops.get_model_weights()
+    assert len(names) == len(arrays) and all(np.all(np.isfinite(a)) for a in arrays)
+    ops.set_model_weights(names, arrays)
+    ev = ops.evaluate_model(ds, 4)
+    assert np.isfinite(ev["loss"])
+
+
+def test_mnist_fc_family():
+    from metisfl_amd.models.model_def import StaticModelDef, families
+    assert "mnist_fc" in families()
+    net = StaticModelDef("mnist_fc").get_model(batch_size=8, device="cpu")
+    assert net.state.n_params > 100000
