@@ -51,3 +51,20 @@ def test_mnist_fc_family():
     assert "mnist_fc" in families()
     net = StaticModelDef("mnist_fc").get_model(batch_size=8, device="cpu")
     assert net.state.n_params > 100000
+
+
+def test_convergence_plots_from_experiment(tmp_path):
+    import json
+
+    from examples.utils.convergence_plots import main
+    stats = {"federation_runtime_metadata": {"metadata": [
+        {"global_iteration": 1, "started_at": "2026-01-01T00:00:00.000000100Z",
+         "completed_at": "2026-01-01T00:00:02.5Z", "model_aggregation_total_duration_ms": 3.0}]},
+        "community_model_results": {"community_evaluation": [
+            {"global_iteration": 1, "evaluations": {"a": {"test_evaluation": {"metric_values": {"accuracy": "0.5"}}},
+                                                    "b": {"test_evaluation": {"metric_values": {"accuracy": "0.7"}}}}}]}}
+    p = tmp_path / "experiment.json"
+    p.write_text(json.dumps(stats))
+    rows = main([str(p), "--out", str(tmp_path / "plots")])
+    assert rows[0]["round_s"] == 2.5 and abs(rows[0]["test_accuracy_mean"] - 0.6) < 1e-9
+    assert (tmp_path / "plots" / "rounds.csv").exists()
