@@ -23,7 +23,7 @@ def _ts(s: str | None) -> float | None:
     s = s.rstrip("Z")
     if "." in s:
         head, frac = s.split(".", 1)
-        s = head + "." + frac[:6]
+        s = head + "." + frac[:6].ljust(6, "0")  # protobuf ns -> the us fromisoformat takes
     return datetime.fromisoformat(s).timestamp()
 
 
