@@ -52,6 +52,9 @@ def main() -> int:
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--lr", type=float, default=0.005)
     ap.add_argument("--momentum", type=float, default=0.75)
+    ap.add_argument("--secure-aggregation", action="store_true",
+                    help="BASELINE config 4: CKKS secure aggregation (device encrypt / int64 "
+                         "all-reduce of ciphertexts / device decrypt)")
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
 
@@ -85,7 +88,8 @@ def main() -> int:
     test_ds = net.make_dataset(xte, yte, seed=comm.rank, shuffle=False)
     del xtr, xte
     cfg = FederationConfig(protocol="synchronous", batch_size=args.batch,
-                           local_epochs=args.local_epochs, evaluate_test=not args.no_eval)
+                           local_epochs=args.local_epochs, evaluate_test=not args.no_eval,
+                           secure_aggregation=args.secure_aggregation)
     engine = None
     if comm.rank == 0:  # the native controller keeps the round bookkeeping
         from metisfl_amd.parallel.engine_bridge import CollectiveController
@@ -144,7 +148,9 @@ def main() -> int:
             "local_epochs": args.local_epochs,
             "local_updates_per_round": updates,
             "optimizer": f"momentum_sgd(lr={args.lr}, momentum={args.momentum})",
-            "aggregation": "FedAvg(NUM_TRAINING_EXAMPLES), RCCL all-reduce",
+            "aggregation": ("PWA(NUM_TRAINING_EXAMPLES) over RNS-CKKS (N=8192, 52-bit scale): "
+                            "device encrypt, int64 RCCL all-reduce of ciphertexts, device decrypt"
+                            if args.secure_aggregation else "FedAvg(NUM_TRAINING_EXAMPLES), RCCL all-reduce"),
             "protocol": "synchronous",
             "parallelism": f"fedavg-dp{n}",
             "test_eval": not args.no_eval,
@@ -153,6 +159,9 @@ def main() -> int:
         "rounds_per_s": rounds_per_s,
         "train_ms_mean": sum(r.train_ms for r in timed) / max(1, len(timed)),
         "aggregation_ms_mean": sum(r.aggregation_ms for r in timed) / max(1, len(timed)),
+        "he_ms_mean": ({k: sum(r.he_stats[k] for r in timed) / max(1, len(timed))
+                        for k in ("encrypt_ms", "allreduce_ms", "decrypt_ms")}
+                       if args.secure_aggregation and timed else None),
         "samples_per_s": (args.train_size * args.local_epochs) / (round_ms / 1e3) if round_ms else 0.0,
     }
     if comm.rank == 0:

@@ -281,5 +281,36 @@ PYBIND11_MODULE(_engine, m) {
       .def("encode_decode_roundtrip", &CKKS::encode_decode_roundtrip)
       .def_property_readonly("ring_dim", &CKKS::ring_dim)
       .def_property_readonly("slots", &CKKS::slots)
-      .def_property_readonly("moduli", &CKKS::moduli);
+      .def_property_readonly("moduli", &CKKS::moduli)
+      .def_property_readonly("scaling_bits", &CKKS::scaling_bits)
+      .def("device_tables",
+           [](const CKKS& c) {
+             // flat numpy copies of everything the HIP encrypt / decrypt path
+             // needs (encryption/device.py uploads them once)
+             auto u64 = [](const std::vector<uint64_t>& v) {
+               return py::array_t<uint64_t>(v.size(), v.data());
+             };
+             auto u64_2d = [](const std::vector<std::vector<uint64_t>>& v) {
+               std::vector<uint64_t> flat;
+               for (auto& r : v) flat.insert(flat.end(), r.begin(), r.end());
+               return py::array_t<uint64_t>(flat.size(), flat.data());
+             };
+             py::dict d;
+             d["moduli"] = u64(c.moduli());
+             d["psi"] = u64_2d(c.psi_rev());
+             d["psi_shoup"] = u64_2d(c.psi_rev_shoup());
+             d["ipsi"] = u64_2d(c.ipsi_rev());
+             d["ipsi_shoup"] = u64_2d(c.ipsi_rev_shoup());
+             d["n_inv"] = u64(c.n_inv());
+             d["n_inv_shoup"] = u64(c.n_inv_shoup());
+             d["rot"] = u64(c.rot());
+             d["ksi_re"] = py::array_t<double>(c.ksi_re().size(), c.ksi_re().data());
+             d["ksi_im"] = py::array_t<double>(c.ksi_im().size(), c.ksi_im().data());
+             if (c.has_public_key()) {
+               d["pk_b"] = u64(c.pk_b());
+               d["pk_a"] = u64(c.pk_a());
+             }
+             if (c.has_private_key()) d["sk"] = u64(c.sk());
+             return d;
+           });
 }

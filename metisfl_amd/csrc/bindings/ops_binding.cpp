@@ -358,6 +358,7 @@ void register_conv(pybind11::module& m);
 void register_gemm(pybind11::module& m);
 void register_layers(pybind11::module& m);
 void register_bert(pybind11::module& m);
+void register_ckks(pybind11::module& m);
 
 PYBIND11_MODULE(_ops, m) {
   m.doc() = "metisfl_amd hand-written HIP (gfx950) kernels";
@@ -379,4 +380,5 @@ PYBIND11_MODULE(_ops, m) {
   register_gemm(m);
   register_layers(m);
   register_bert(m);
+  register_ckks(m);
 }

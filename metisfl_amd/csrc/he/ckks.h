@@ -57,6 +57,25 @@ class CKKS {
   const std::vector<uint64_t>& moduli() const { return q_; }
   static constexpr int kWeightBits = 30;
 
+  // Read-only views for the device (HIP) encrypt / decrypt path
+  // (kernels/ckks.hip): NTT twiddles in bit-reversed order with their Shoup
+  // companions, N^-1, keys in NTT form [limb][N], canonical-embedding tables.
+  bool has_public_key() const { return has_pk_; }
+  bool has_private_key() const { return has_sk_; }
+  uint32_t scaling_bits() const { return bits_; }
+  const std::vector<std::vector<uint64_t>>& psi_rev() const { return psi_rev_; }
+  const std::vector<std::vector<uint64_t>>& psi_rev_shoup() const { return psi_rev_sh_; }
+  const std::vector<std::vector<uint64_t>>& ipsi_rev() const { return ipsi_rev_; }
+  const std::vector<std::vector<uint64_t>>& ipsi_rev_shoup() const { return ipsi_rev_sh_; }
+  const std::vector<uint64_t>& n_inv() const { return ninv_; }
+  const std::vector<uint64_t>& n_inv_shoup() const { return ninv_sh_; }
+  const std::vector<uint64_t>& pk_b() const { return pk_b_; }
+  const std::vector<uint64_t>& pk_a() const { return pk_a_; }
+  const std::vector<uint64_t>& sk() const { return sk_; }
+  const std::vector<uint64_t>& rot() const { return rot_; }
+  const std::vector<double>& ksi_re() const { return ksi_re_; }
+  const std::vector<double>& ksi_im() const { return ksi_im_; }
+
  private:
   void setup_primes();
   void precompute();

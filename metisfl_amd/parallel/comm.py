@@ -59,6 +59,18 @@ class Comm:
         if self.distributed:
             dist.broadcast(t, src=src)
 
+    def broadcast_bytes(self, data: bytes | None, src: int = 0) -> bytes:
+        """Small host blob (keys, configs) from ``src`` to every rank."""
+        if not self.distributed:
+            return data or b""
+        n = torch.tensor([len(data) if self.rank == src else 0], dtype=torch.int64, device=self.device)
+        dist.broadcast(n, src=src)
+        buf = torch.empty(int(n.item()), dtype=torch.uint8, device=self.device)
+        if self.rank == src:
+            buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+        dist.broadcast(buf, src=src)
+        return bytes(buf.cpu().numpy().tobytes())
+
     def all_gather_rows(self, row: torch.Tensor) -> torch.Tensor:
         """Gather one small 1-D tensor per rank -> [world, n] (on row.device)."""
         if not self.distributed:

@@ -62,6 +62,11 @@ class FederationConfig:
     eval_max_steps: int | None = None
     quantify: bool = True                  # per-variable zero counts of each community model
     jsonl_log: str | None = None           # rank 0: one JSON line per round (utils/tracing.py)
+    # CKKS secure aggregation (reference: PWA over Palisade CKKS, HESchemeConfig
+    # metis.proto:281-299, batch 4096 / 52 scaling bits in template_with_fhe.yaml)
+    secure_aggregation: bool = False
+    he_batch_size: int = 4096
+    he_scaling_bits: int = 52
     extra: dict = field(default_factory=dict)
 
 
@@ -82,6 +87,7 @@ class RoundRecord:
     allreduce_ms: float = 0.0              # the model all-reduce alone
     allreduce_gbps: float = 0.0            # algorithm bandwidth: model bytes / all-reduce time
     hbm_used_bytes: int = 0
+    he_stats: dict | None = None           # secure aggregation: encrypt / all-reduce / decrypt ms
 
     def to_json(self) -> dict:
         d = asdict(self)
@@ -120,6 +126,11 @@ class CollectiveFederation:
         self._ev0 = torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else None
         self._ev1 = torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else None
         self._log = tracing.JsonlLog(cfg.jsonl_log if comm.rank == 0 else None)
+        self.he = self.he_dev = None
+        self._he_ct = None
+        self.last_he_stats: dict = {}
+        if cfg.secure_aggregation:
+            self._setup_he()
         if broadcast_initial:
             self.broadcast_initial_model()
 
@@ -168,13 +179,73 @@ class CollectiveFederation:
                 raise RuntimeError(f"scaler mismatch: engine {we} vs collective {w}")
         return w
 
+    def _setup_he(self) -> None:
+        """One CKKS key pair shared by all learners (the reference's driver
+        generates it once, driver_session.py:122-135): rank 0 generates,
+        the key files travel as bytes over the process group."""
+        import tempfile
+
+        from metisfl_amd.encryption import CKKS
+        cfg = self.cfg
+        names = ("cryptocontext.txt", "key-public.txt", "key-private.txt")
+        self._he_dir = tempfile.mkdtemp(prefix=f"metisfl_amd_ckks_r{self.rank}_")
+        scheme = CKKS(cfg.he_batch_size, cfg.he_scaling_bits)
+        blobs = []
+        if self.rank == 0:
+            scheme.gen_crypto_context_and_keys(self._he_dir)
+            for nm in names:
+                with open(os.path.join(self._he_dir, nm), "rb") as f:
+                    blobs.append(f.read())
+        for i, nm in enumerate(names):
+            b = self.comm.broadcast_bytes(blobs[i] if self.rank == 0 else None)
+            if self.rank != 0:
+                with open(os.path.join(self._he_dir, nm), "wb") as f:
+                    f.write(b)
+        if self.rank != 0:
+            scheme.load_context_and_keys_from_files(*(os.path.join(self._he_dir, nm) for nm in names))
+        self.he = scheme
+        if self.comm.device.type == "cuda":
+            from metisfl_amd.encryption.device import DeviceCKKS
+            self.he_dev = DeviceCKKS(scheme, self.comm.device)
+
+    def _secure_aggregate(self, weights: list[float]) -> None:
+        """model32 <- Dec(PWA(Enc(model32_r), w_r)): ciphertexts are what
+        crosses the process boundary; plaintext weights stay on their GPU."""
+        st = self.net.state
+        if self.he_dev is not None:
+            with tracing.range("metisfl.secure_allreduce"):
+                if self._he_ct is None:
+                    self._he_ct = torch.empty(self.he_dev.ct_numel(st.model32.numel()),
+                                              dtype=torch.int64, device=self.comm.device)
+                self.last_he_stats = self.he_dev.secure_weighted_allreduce(
+                    self.comm, st.model32, weights[self.rank], ct=self._he_ct)
+            self.last_allreduce_ms = self.last_he_stats["allreduce_ms"]
+            return
+        # host path (CPU / gloo): host encrypt, all-gather ciphertexts, host PWA
+        t0 = time.perf_counter()
+        n = st.model32.numel()
+        ct = self.he.encrypt(st.model32.double().numpy())
+        t1 = time.perf_counter()
+        buf = torch.frombuffer(bytearray(ct), dtype=torch.uint8)
+        rows = self.comm.all_gather_rows(buf)
+        t2 = time.perf_counter()
+        cts = [bytes(rows[r].numpy().tobytes()) for r in range(self.world)]
+        agg = self.he.compute_weighted_average(cts, [float(w) for w in weights])
+        st.model32.copy_(torch.from_numpy(self.he.decrypt(agg, n)).to(st.model32.dtype))
+        t3 = time.perf_counter()
+        self.last_he_stats = {"encrypt_ms": (t1 - t0) * 1e3, "allreduce_ms": (t2 - t1) * 1e3,
+                              "decrypt_ms": (t3 - t2) * 1e3, "ciphertext_bytes": len(ct)}
+        self.last_allreduce_ms = (t2 - t1) * 1e3
+
     def aggregate(self, meta: np.ndarray) -> tuple[list[float], float]:
         """Scale + all-reduce; returns (weights, ms)."""
         t0 = time.perf_counter()
         weights = self.aggregation_weights(meta)
         st = self.net.state
         self.last_allreduce_ms = 0.0
-        if self.world > 1:
+        if self.cfg.secure_aggregation:
+            self._secure_aggregate(weights)
+        elif self.world > 1:
             with tracing.range("metisfl.scale"):
                 opt_ops.scale_(st.model32, weights[self.rank])
             self._sync()
@@ -231,6 +302,8 @@ class CollectiveFederation:
                           nbytes / (ar_ms * 1e6) if ar_ms > 0 else 0.0,
                           tracing.hbm_usage(self.comm.device).get("used_bytes", 0)
                           if self.comm.device.type == "cuda" else 0)
+        if self.cfg.secure_aggregation:
+            rec.he_stats = dict(self.last_he_stats)
         if self.rank == 0:
             self._log.write({"kind": "round", **rec.to_json(),
                              "rounds_per_s": 1e3 / rec.round_ms if rec.round_ms > 0 else 0.0})

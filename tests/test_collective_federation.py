@@ -36,7 +36,8 @@ def _worker(rank, world, port, out_dir, mode):
     ds = net.make_dataset(rng.standard_normal((n, 32, 32, 3)).astype(np.float32), rng.integers(0, 10, n),
                           seed=rank)
     cfg = FederationConfig(protocol="semi_synchronous" if mode == "semi" else "synchronous", batch_size=4,
-                           local_epochs=1, semi_sync_lambda=2.0, evaluate_test=False)
+                           local_epochs=1, semi_sync_lambda=2.0, evaluate_test=False,
+                           secure_aggregation=mode == "secure")
     sizes = [8 + 4 * r for r in range(world)]
     engine = CollectiveController(cfg, sizes) if rank == 0 else None
     fed = CollectiveFederation(comm, net, ds, cfg, engine=engine)
@@ -92,6 +93,21 @@ def test_sync_fedavg_two_ranks_matches_host_reference(tmp_path):
     eng = res[0]["engine"]
     assert eng["rounds"] == 2 and eng["learners"] == 2 and eng["quantifiers"] > 0
     assert sorted(eng["lineage"].values()) == [2, 2]
+
+
+def test_secure_ckks_aggregation_two_ranks(tmp_path):
+    """CKKS secure aggregation (reference PWA path): ciphertexts cross the
+    process boundary, every rank decrypts the same weighted average."""
+    res = _run(tmp_path, "secure")
+    w = res[0]["rounds"][0]["weights"]
+    for r in (0, 1):
+        gi = r + 1
+        a = np.load(tmp_path / f"community_r{gi}_rank0.npy")
+        b = np.load(tmp_path / f"community_r{gi}_rank1.npy")
+        assert np.array_equal(a, b)
+        l0 = np.load(tmp_path / f"local_r{r}_rank0.npy").astype(np.float64)
+        l1 = np.load(tmp_path / f"local_r{r}_rank1.npy").astype(np.float64)
+        assert np.abs(a - (w[0] * l0 + w[1] * l1)).max() < 1e-5
 
 
 def test_semi_sync_step_budgets(tmp_path):
