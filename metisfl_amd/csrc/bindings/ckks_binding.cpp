@@ -86,13 +86,17 @@ void ckks_decrypt_dev(std::vector<torch::Tensor> tabs, int64_t N, int64_t L, tor
                       torch::Tensor m, torch::Tensor out, double inv_scale) {
   auto T = tables(tabs, N, L);
   TORCH_CHECK(T.sk && T.sk_sh, "ckks decrypt: private key not loaded");
-  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.scalar_type() == torch::kFloat32, "out fp32");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() &&
+                  (out.scalar_type() == torch::kFloat32 || out.scalar_type() == torch::kFloat64),
+              "out must be a contiguous fp32 / fp64 device tensor");
+  const bool f64 = out.scalar_type() == torch::kFloat64;
   const int64_t nct = num_ct(out.numel(), T.S);
   check_u64(ct, nct * 2 * L * N, "ct");
   check_u64(m, nct * L * N, "m scratch");
   mfl::launch_ckks_decrypt(T, reinterpret_cast<const uint64_t*>(ct.data_ptr()), nct, inv_scale,
-                           reinterpret_cast<uint64_t*>(m.data_ptr()), out.data_ptr<float>(), out.numel(),
-                           cur_stream(out));
+                           reinterpret_cast<uint64_t*>(m.data_ptr()),
+                           f64 ? nullptr : out.data_ptr<float>(), f64 ? out.data_ptr<double>() : nullptr,
+                           out.numel(), cur_stream(out));
 }
 
 void ckks_ntt_dev(std::vector<torch::Tensor> tabs, int64_t N, int64_t L, torch::Tensor rows, bool inverse) {

@@ -34,9 +34,9 @@ struct CkksTables {
 // x: fp32 [n] -> ct: u64 [nct][2][L][N] (nct = ceil(n / S)); u_scratch: u64 [nct][L][N]
 void launch_ckks_encrypt(const CkksTables& T, const float* x, int64_t n, int64_t nct, double delta,
                          uint64_t seed, uint64_t* ct, uint64_t* u_scratch, hipStream_t s);
-// ct [nct][2][L][N] -> out fp32 [n]; m_scratch: u64 [nct][L][N]
+// ct [nct][2][L][N] -> out fp32 [n] (or fp64 into out64 when non-null); m_scratch: u64 [nct][L][N]
 void launch_ckks_decrypt(const CkksTables& T, const uint64_t* ct, int64_t nct, double inv_scale,
-                         uint64_t* m_scratch, float* out, int64_t n, hipStream_t s);
+                         uint64_t* m_scratch, float* out, double* out64, int64_t n, hipStream_t s);
 // in-place NTT of nrows rows (row r in limb r % L)
 void launch_ckks_ntt(const CkksTables& T, uint64_t* rows, int64_t nrows, bool inverse, hipStream_t s);
 // x[.][.][l][.] *= w_l (mod q_l); wq [L][2] = {w_l, shoup(w_l)}

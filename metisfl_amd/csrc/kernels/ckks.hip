@@ -238,7 +238,7 @@ __device__ __forceinline__ double crt_centred(const CkksTables& T, const uint64_
 
 __global__ __launch_bounds__(512) void ckks_crt_decode_kernel(CkksTables T, const uint64_t* __restrict__ m,
                                                               double inv_scale, float* __restrict__ out,
-                                                              int64_t n) {
+                                                              double* __restrict__ out64, int64_t n) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   cplx* v = reinterpret_cast<cplx*>(smem);
   const int S = T.S, N = T.N;
@@ -268,7 +268,10 @@ __global__ __launch_bounds__(512) void ckks_crt_decode_kernel(CkksTables T, cons
   __syncthreads();
   const int64_t off = c * S;
   for (int i = threadIdx.x; i < S; i += blockDim.x)
-    if (off + i < n) out[off + i] = (float)v[i].re;
+    if (off + i < n) {
+      if (out64) out64[off + i] = v[i].re;
+      else out[off + i] = (float)v[i].re;
+    }
 }
 
 // x[c][p][l][k] = x * w_l mod q_l  (w = round(weight * 2^30) mod q_l, Shoup)
@@ -302,11 +305,11 @@ void launch_ckks_encrypt(const CkksTables& T, const float* x, int64_t n, int64_t
 }
 
 void launch_ckks_decrypt(const CkksTables& T, const uint64_t* ct, int64_t nct, double inv_scale,
-                         uint64_t* m_scratch, float* out, int64_t n, hipStream_t s) {
+                         uint64_t* m_scratch, float* out, double* out64, int64_t n, hipStream_t s) {
   const size_t lds = (size_t)T.N * 8;
   ckks_dec_prep_kernel<<<stream_grid(nct * T.L * T.N, 256, 8192), 256, 0, s>>>(T, ct, m_scratch, nct);
   ckks_ntt_inv_kernel<<<(unsigned)(nct * T.L), 512, lds, s>>>(T, m_scratch);
-  ckks_crt_decode_kernel<<<(unsigned)nct, 512, lds, s>>>(T, m_scratch, inv_scale, out, n);
+  ckks_crt_decode_kernel<<<(unsigned)nct, 512, lds, s>>>(T, m_scratch, inv_scale, out, out64, n);
 }
 
 void launch_ckks_ntt(const CkksTables& T, uint64_t* rows, int64_t nrows, bool inverse, hipStream_t s) {

@@ -124,10 +124,10 @@ class DeviceCKKS:
         return out
 
     def decrypt(self, ct: torch.Tensor, n: int, log2_scale: float | None = None,
-                out: torch.Tensor | None = None) -> torch.Tensor:
-        """ciphertext limbs -> fp32 [n]; ``log2_scale`` defaults to a fresh encryption's."""
+                out: torch.Tensor | None = None, dtype=torch.float32) -> torch.Tensor:
+        """ciphertext limbs -> fp32 / fp64 [n]; ``log2_scale`` defaults to a fresh encryption's."""
         if out is None:
-            out = torch.empty(n, dtype=torch.float32, device=self.device)
+            out = torch.empty(n, dtype=dtype, device=self.device)
         ls = self.bits if log2_scale is None else log2_scale
         _ops().ckks_decrypt(self.tables, self.N, self.L, ct, self._scratch_for(n), out,
                             float(2.0 ** (-ls)))
@@ -189,3 +189,33 @@ class DeviceCKKS:
             raise ValueError("ciphertext from another CKKS context")
         body = np.frombuffer(blob, dtype="<i8", count=nct * 2 * nl * n, offset=24 + 8 * nl)
         return torch.from_numpy(body.copy()).to(self.device), ls
+
+
+class AcceleratedCKKS:
+    """``fhe.CKKS`` whose ``encrypt`` / ``decrypt`` run on the GPU.
+
+    Drop-in for the learner-side scheme of the gRPC path (learner/he.py): the
+    ciphertext bytes are the host format, so the controller's PWA (host or
+    ``pwa_device``) and any host-side decrypt are unaffected.  Inputs that are
+    not exactly representable in fp32 (true float64 variables) take the host
+    encoder, which keeps full double precision; decryption is fp64 on device.
+    """
+
+    def __init__(self, scheme, device="cuda"):
+        self._scheme = scheme
+        self._dev = DeviceCKKS(scheme, device)
+
+    def __getattr__(self, name):
+        return getattr(self._scheme, name)
+
+    def encrypt(self, values) -> bytes:
+        v = np.ascontiguousarray(values, dtype=np.float64).reshape(-1)
+        f = v.astype(np.float32)
+        if not np.array_equal(f.astype(np.float64), v):
+            return self._scheme.encrypt(v)
+        ct = self._dev.encrypt(torch.from_numpy(f).to(self._dev.device))
+        return self._dev.to_bytes(ct)
+
+    def decrypt(self, ct: bytes, n: int) -> np.ndarray:
+        t, ls = self._dev.from_bytes(bytes(ct))
+        return self._dev.decrypt(t, int(n), ls, dtype=torch.float64).cpu().numpy()

@@ -22,6 +22,13 @@ the K2 rolling kernels:
     S += w_new * theta_new ; Z += w_new
     community = S / Z
 
+Staleness-aware weighting (the reference's FedRec has
+none): rank 0 versions the community model (+1 per applied update) and
+answers every submission with the new version through the store; a
+learner's next submission carries the version it trained from, and its
+FedRec weight is multiplied by cfg.staleness's discount of
+t = version_now - version_base (``staleness_discount``).
+
 Rank 0 trains its own shard in chunks of ``poll_every`` local steps and
 serves pending submissions between chunks, so a finisher waits at most one
 chunk.  The weights are the NUM_TRAINING_EXAMPLES (or batch / participant)
@@ -41,7 +48,21 @@ from metisfl_amd.ops import aggregate as agg
 from metisfl_amd.parallel.comm import Comm
 from metisfl_amd.parallel.federation import FederationConfig
 
-_KEY = "metisfl_async/{}/{}"
+_KEY = "metisfl_async/{}/{}/{}"
+_VER = "metisfl_async/ver/{}/{}/{}"
+_INSTANCES = [0]  # federations built so far in this process (identical on every rank)
+
+
+def staleness_discount(kind: str, t: int, a: float = 0.5, b: int = 4) -> float:
+    """FedAsync staleness functions (Xie et al. 2019): none / polynomial / hinge."""
+    t = max(0, int(t))
+    if kind in ("none", "", None):
+        return 1.0
+    if kind == "polynomial":
+        return float((1.0 + t) ** (-a))
+    if kind == "hinge":
+        return 1.0 if t <= b else 1.0 / (a * (t - b) + 1.0)
+    raise ValueError(f"unknown staleness function {kind!r}")
 
 
 @dataclass
@@ -53,6 +74,8 @@ class AsyncUpdate:
     aggregation_ms: float
     train_loss: float
     completed_batches: int
+    staleness: int = 0
+    base_weight: float = 0.0
 
 
 class AsyncCollectiveFederation:
@@ -60,6 +83,8 @@ class AsyncCollectiveFederation:
                  poll_every: int = 16, store=None, broadcast_initial: bool = True):
         self.comm, self.net, self.train_ds, self.cfg = comm, net, train_ds, cfg
         self.rank, self.world = comm.rank, comm.world
+        _INSTANCES[0] += 1
+        self.tag = _INSTANCES[0]  # store-key namespace: repeated federations never see old keys
         self.tasks = tasks_per_learner
         self.poll_every = max(1, poll_every)
         self.store = store if store is not None else (
@@ -68,6 +93,8 @@ class AsyncCollectiveFederation:
         self.num_local_updates = cfg.local_epochs * max(1, -(-n // cfg.batch_size))
         self.steps_done = 0
         self.updates: list[AsyncUpdate] = []   # rank 0: every FedRec update applied
+        self.version = 0                       # rank 0: community model version
+        self.base_version = 0                  # version this learner's current task started from
         st = net.state
         if broadcast_initial and comm.distributed:
             comm.broadcast_(st.model32, src=0)
@@ -108,15 +135,18 @@ class AsyncCollectiveFederation:
                 if self.rank == 0:
                     self.serve(block=False)
             meta = {"task": task, "weight": self._weight(self.num_local_updates),
-                    "loss": self.net.train_stats()["loss"], "batches": self.num_local_updates}
+                    "loss": self.net.train_stats()["loss"], "batches": self.num_local_updates,
+                    "base_version": self.base_version}
             if self.rank == 0:
                 self._fedrec(0, self.net.state.model32, meta)
                 self.net.state.model32.copy_(self._community())
+                self.base_version = self.version
                 self._install()
             else:
-                self.store.set(_KEY.format(self.rank, task), json.dumps(meta))
+                self.store.set(_KEY.format(self.tag, self.rank, task), json.dumps(meta))
                 dist.send(self.net.state.model32, dst=0)
                 dist.recv(self.net.state.model32, src=0)
+                self.base_version = int(self.store.get(_VER.format(self.tag, self.rank, task)))
                 self._install()
         if self.rank == 0:
             while any(self.next_task[r] < self.tasks for r in range(1, self.world)):
@@ -138,12 +168,13 @@ class AsyncCollectiveFederation:
             t = self.next_task[r]
             if t >= self.tasks:
                 continue
-            key = _KEY.format(r, t)
+            key = _KEY.format(self.tag, r, t)
             if not block and not self.store.check([key]):
                 continue
             meta = json.loads(self.store.get(key))
             dist.recv(self.rbuf, src=r)
             self._fedrec(r, self.rbuf, meta)
+            self.store.set(_VER.format(self.tag, r, t), str(self.version))
             dist.send(self._community(), dst=r)
             self.next_task[r] = t + 1
             served += 1
@@ -151,7 +182,9 @@ class AsyncCollectiveFederation:
 
     def _fedrec(self, r: int, theta: torch.Tensor, meta: dict) -> None:
         t0 = time.perf_counter()
-        w = float(meta["weight"])
+        stale = self.version - int(meta.get("base_version", self.version))
+        w0 = float(meta["weight"])
+        w = w0 * staleness_discount(self.cfg.staleness, stale, self.cfg.staleness_a, self.cfg.staleness_b)
         if self.last[r] is not None:
             agg.rolling_op(self.S, self.last[r], agg.MERGE_SUB, self.last_w[r])
             self.Z -= self.last_w[r]
@@ -161,11 +194,12 @@ class AsyncCollectiveFederation:
         self.Z += w
         self.last[r].copy_(theta)
         self.last_w[r] = w
+        self.version += 1
         if theta.is_cuda:
             torch.cuda.synchronize(theta.device)
         self.updates.append(AsyncUpdate(r, int(meta["task"]), w, time.time(),
                                         (time.perf_counter() - t0) * 1e3, float(meta["loss"]),
-                                        int(meta["batches"])))
+                                        int(meta["batches"]), stale, w0))
 
     def _community(self) -> torch.Tensor:
         c = self.S.clone()

@@ -64,6 +64,13 @@ class FederationConfig:
     jsonl_log: str | None = None           # rank 0: one JSON line per round (utils/tracing.py)
     # CKKS secure aggregation (reference: PWA over Palisade CKKS, HESchemeConfig
     # metis.proto:281-299, batch 4096 / 52 scaling bits in template_with_fhe.yaml)
+    # asynchronous protocol: staleness-aware FedRec weights (FedAsync-style
+    # discount s(t) of the staleness t = community version at submission -
+    # version the learner trained from): "none" | "polynomial" (1+t)^-a |
+    # "hinge" 1 if t <= b else 1 / (a (t - b) + 1)
+    staleness: str = "none"
+    staleness_a: float = 0.5
+    staleness_b: int = 4
     secure_aggregation: bool = False
     he_batch_size: int = 4096
     he_scaling_bits: int = 52

@@ -17,7 +17,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, staleness="none"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
@@ -33,7 +33,7 @@ def _worker(rank, world, port, out_dir):
     n = 8 + 4 * rank
     ds = net.make_dataset(rng.standard_normal((n, 13)).astype(np.float32),
                           rng.standard_normal(n).astype(np.float32), seed=rank)
-    cfg = FederationConfig(batch_size=4, local_epochs=1, evaluate_test=False)
+    cfg = FederationConfig(batch_size=4, local_epochs=1, evaluate_test=False, staleness=staleness)
     fed = AsyncCollectiveFederation(comm, net, ds, cfg, tasks_per_learner=3, poll_every=1)
     ups = fed.run()
     res = {"rank": rank, "final": net.state.model32.numpy().tolist()}
@@ -41,8 +41,9 @@ def _worker(rank, world, port, out_dir):
         ref = fed.community_reference()
         got = fed._community().double().numpy()
         res["updates"] = [(u.learner, u.task, u.weight) for u in ups]
+        res["stale"] = [(u.staleness, u.base_weight, u.weight) for u in ups]
         res["max_err"] = float(np.abs(got - ref).max() / (np.abs(ref).max() + 1e-12))
-    with open(os.path.join(out_dir, f"async_{rank}.json"), "w") as f:
+    with open(os.path.join(out_dir, f"async_{staleness}_{rank}.json"), "w") as f:
         json.dump(res, f)
     comm.barrier()
     comm.close()
@@ -52,7 +53,7 @@ def test_async_fedrec_three_learners(tmp_path):
     world = 3
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
-    res = [json.load(open(tmp_path / f"async_{r}.json")) for r in range(world)]
+    res = [json.load(open(tmp_path / f"async_none_{r}.json")) for r in range(world)]
     ups = res[0]["updates"]
     assert len(ups) == world * 3
     for r in range(world):
@@ -62,3 +63,28 @@ def test_async_fedrec_three_learners(tmp_path):
     assert res[0]["max_err"] < 1e-5
     for r in res:
         assert np.all(np.isfinite(r["final"]))
+
+
+def test_staleness_functions():
+    from metisfl_amd.parallel.async_federation import staleness_discount as sd
+    assert sd("none", 7) == 1.0
+    assert sd("polynomial", 0) == 1.0 and abs(sd("polynomial", 3, a=0.5) - 0.5) < 1e-12
+    assert sd("hinge", 4, a=0.5, b=4) == 1.0 and abs(sd("hinge", 6, a=0.5, b=4) - 0.5) < 1e-12
+
+
+def test_async_staleness_aware_weights(tmp_path):
+    """Polynomial staleness discount: every applied weight is the
+    NUM_TRAINING_EXAMPLES weight times (1 + staleness)^-0.5, staleness counts
+    the community versions published since the learner's base model, and the
+    incremental community still equals the host recomputation."""
+    world = 3
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), "polynomial"), nprocs=world,
+                       join=True, start_method="spawn")
+    r0 = json.load(open(tmp_path / "async_polynomial_0.json"))
+    assert len(r0["stale"]) == world * 3
+    for i, (st, w0, w) in enumerate(r0["stale"]):
+        assert 0 <= st <= i
+        assert abs(w - w0 * (1.0 + st) ** -0.5) < 1e-9
+    assert r0["stale"][0][0] == 0          # the very first update is fresh
+    assert any(st > 0 for st, _, _ in r0["stale"])
+    assert r0["max_err"] < 1e-5
