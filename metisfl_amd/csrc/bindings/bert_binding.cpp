@@ -308,6 +308,8 @@ void vocab_xent(torch::Tensor logits, c10::optional<torch::Tensor> dlogits, torc
 
 void register_bert(pybind11::module& m) {
   m.def("gemm_fwd", &gemm_fwd);
+  m.def("set_gemm_big", [](bool on) { mfl::set_gemm_big(on ? 1 : 0); });
+  m.def("gemm_big_enabled", []() { return mfl::gemm_big_enabled() != 0; });
   m.def("gemm_dgrad", &gemm_dgrad);
   m.def("gemm_wgrad", &gemm_wgrad);
   m.def("ln_fwd", &ln_fwd);

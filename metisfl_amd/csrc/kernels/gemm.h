@@ -29,4 +29,17 @@ void launch_gemm_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, 
                        bool accumulate, hipStream_t s);
 bool gemm_wgrad_splits(int M, int N, int K);
 
+// Large-tile path (gemm_big.hip): 256x256 tiles, exact-tiling shapes only.
+bool gemm_big_ok(int M, int N, int K);
+void launch_gemm_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
+                         const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s);
+void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
+                           bool accumulate, hipStream_t s);
+void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,
+                           bool accumulate, hipStream_t s);
+int gemm_big_wgrad_splits(int M, int N, int K);  // > 1: adds into dw (atomics)
+// 1 (default; env MFL_GEMM_BIG=0 turns it off): eligible shapes take the large-tile path
+void set_gemm_big(int on);
+int gemm_big_enabled();
+
 }  // namespace mfl

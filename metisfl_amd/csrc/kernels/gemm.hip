@@ -47,8 +47,22 @@ ConvPlan plan_gemm(int M, int N, int K) {
   return p;
 }
 
+static int g_big = -1;
+void set_gemm_big(int on) { g_big = on ? 1 : 0; }
+int gemm_big_enabled() {
+  if (g_big < 0) {
+    const char* v = getenv("MFL_GEMM_BIG");
+    g_big = (v && *v == '0') ? 0 : 1;
+  }
+  return g_big;
+}
+
 void launch_gemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
                      const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s) {
+  if (gemm_big_enabled() && gemm_big_ok(M, N, K)) {
+    launch_gemm_big_fwd(x, w, y, bias, resid, act_out, M, N, K, s);
+    return;
+  }
   const ConvGeom g = dense_geom(M, N, K);
   GemmEpilogueArgs e;
   e.bias = bias;
@@ -59,6 +73,10 @@ void launch_gemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const fl
 
 void launch_gemm_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
                        bool accumulate, hipStream_t s) {
+  if (gemm_big_enabled() && gemm_big_ok(M, K, N)) {
+    launch_gemm_big_dgrad(dy, w, dx, M, N, K, accumulate, s);
+    return;
+  }
   // dgrad geometry: "dY" has C = N channels, the output dX has Ng = K columns
   ConvGeom g = dense_geom(M, K, N);
   ConvPlan p = plan_gemm(M, K, N);
@@ -67,14 +85,26 @@ void launch_gemm_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int 
 
 void launch_gemm_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,
                        bool accumulate, hipStream_t s) {
+  if (gemm_big_enabled() && gemm_big_ok(N, K, M)) {
+    launch_gemm_big_wgrad(x, dy, dw, M, N, K, accumulate, s);
+    return;
+  }
   const ConvGeom g = dense_geom(M, N, K);
   launch_conv_wgrad(g, plan_conv_wgrad(g), x, dy, dw, s, accumulate);
 }
 
-bool gemm_wgrad_splits(int M, int N, int K) { return plan_conv_wgrad(dense_geom(M, N, K)).splits > 1; }
+bool gemm_wgrad_splits(int M, int N, int K) {
+  if (gemm_big_enabled() && gemm_big_ok(N, K, M)) return gemm_big_wgrad_splits(M, N, K) > 1;
+  return plan_conv_wgrad(dense_geom(M, N, K)).splits > 1; }
 
 void launch_gemm_nt(const uint16_t* a, const uint16_t* b, uint16_t* c, const float* bias,
                     const uint16_t* aux, int M, int N, int K, int epilogue, hipStream_t s) {
+  if (gemm_big_enabled() && gemm_big_ok(M, N, K)) {
+    launch_gemm_big_fwd(a, b, c, epilogue != EPI_NONE ? bias : nullptr,
+                        epilogue == EPI_BIAS_RESIDUAL ? aux : nullptr,
+                        epilogue == EPI_BIAS_GELU ? c : nullptr, M, N, K, s);
+    return;
+  }
   GemmEpilogueArgs e;
   if (epilogue != EPI_NONE) e.bias = bias;
   if (epilogue == EPI_BIAS_RESIDUAL) e.resid = aux;
