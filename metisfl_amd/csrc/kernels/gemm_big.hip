@@ -49,28 +49,39 @@ struct BigGemmArgs {
   int accum;
   int splits;            // split-K slices (fp32 output only; atomics into c32)
   int kt_per_split;      // k-tiles per slice
+  int dbg;               // timing experiments (MFL_GB_DEBUG): bit0 skip MFMAs, bit1 skip operand DMA
 };
 
 namespace {
 
-constexpr int GB_BM = 256, GB_BN = 256, GB_BK = 64;
-constexpr int GB_TILE = GB_BM * GB_BK * 2;  // bytes of one operand tile (32 KiB)
-constexpr int GB_STAGE = 2 * GB_TILE;       // A + B
+constexpr int GB_BM = 256, GB_BN = 256;
 constexpr int GB_EPI_LD = 68;               // fp32 staging row pitch (64 + 4)
-constexpr size_t GB_LDS = 2 * GB_STAGE;     // 128 KiB (epilogue: 8 x 32 x 68 x 4 = 69.6 KiB)
+constexpr int GB_KQ = 64;                   // K granularity the shapes must meet
+// Pipeline variants: BK = 64 with a 2-stage ring (one tile in flight across
+// the compute), or BK = 32 with a 4-stage ring (three tiles in flight).
+template <int BK, int NST>
+struct GbCfg {
+  static constexpr int TILE = GB_BM * BK * 2;  // bytes of one operand tile
+  static constexpr int STAGE = 2 * TILE;       // A + B
+  static constexpr int DMA = GB_BM * BK * 2 / 1024 / 8;  // DMA instructions per wave per operand
+  static constexpr size_t LDS = (size_t)NST * STAGE > (size_t)8 * 32 * GB_EPI_LD * 4
+                                    ? (size_t)NST * STAGE : (size_t)8 * 32 * GB_EPI_LD * 4;
+};
 
-// One operand tile (256 rows x 64 k) global -> LDS, 4 DMA instructions per wave.
-template <bool T>
+// One operand tile (256 rows x BK k) global -> LDS.
+template <bool T, int BK>
 __device__ __forceinline__ void stage_operand(__amdgpu_buffer_rsrc_t rs, int ld, int row0, int k0,
                                               uint8_t* dst, int wave, int lane) {
+  constexpr int NI = GbCfg<BK, 2>::DMA;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < NI; ++u) {
     const int i = wave + 8 * u;  // 1-KiB instruction index within the tile
     uint32_t off;
     if constexpr (!T) {
-      // [row][k]: 8 rows of 128 B per instruction
-      const int row = 8 * i + (lane >> 3);
-      const int lc = (lane & 7) ^ swz_b128<128>(row);
+      // [row][k]: 1024 / (2 BK) rows of 2 BK bytes per instruction
+      constexpr int RPI = 512 / BK, CPR = BK / 8;
+      const int row = RPI * i + lane / CPR;
+      const int lc = (lane % CPR) ^ swz_b128<2 * BK>(row);
       off = (uint32_t)((row0 + row) * ld + k0 + 8 * lc) * 2u;
     } else {
       // [k][row]: 2 k-rows of 512 B per instruction
@@ -82,14 +93,20 @@ __device__ __forceinline__ void stage_operand(__amdgpu_buffer_rsrc_t rs, int ld,
   }
 }
 
-template <bool T>
+template <bool T, int BK>
 __device__ __forceinline__ bf16x8 frag(const uint8_t* tile, int kk, int r0, int lane) {
   if constexpr (T) return tr_frag<512>(tile, kk, r0, lane);
-  else return b128_frag<128>(tile, kk, r0, lane);
+  else return b128_frag<2 * BK>(tile, kk, r0, lane);
 }
 
-template <bool AT, bool BT, bool OUT32>
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool AT, bool BT, bool OUT32, int BK, int NST>
 __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
+  using C = GbCfg<BK, NST>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -107,7 +124,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
   const auto rsA = make_rsrc(p.a, p.a_bytes);
   const auto rsB = make_rsrc(p.b, p.b_bytes);
   const int kt0 = blockIdx.y * p.kt_per_split;
-  const int nk = min(p.K / GB_BK - kt0, p.kt_per_split);
+  const int nk = min(p.K / BK - kt0, p.kt_per_split);
   if (nk <= 0) return;  // block-uniform: an empty trailing slice
 
   f32x4 acc[8][4];
@@ -117,20 +134,22 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto issue = [&](int kt, int stage) {
-    uint8_t* st = smem + stage * GB_STAGE;
-    stage_operand<AT>(rsA, p.lda, m0, (kt0 + kt) * GB_BK, st, wave, lane);
-    stage_operand<BT>(rsB, p.ldb, n0, (kt0 + kt) * GB_BK, st + GB_TILE, wave, lane);
+    if (p.dbg & 2) return;
+    uint8_t* st = smem + stage * C::STAGE;
+    stage_operand<AT, BK>(rsA, p.lda, m0, (kt0 + kt) * BK, st, wave, lane);
+    stage_operand<BT, BK>(rsB, p.ldb, n0, (kt0 + kt) * BK, st + C::TILE, wave, lane);
   };
   auto compute = [&](int stage) {
-    const uint8_t* As = smem + stage * GB_STAGE;
-    const uint8_t* Bs = As + GB_TILE;
+    if (p.dbg & 1) return;
+    const uint8_t* As = smem + stage * C::STAGE;
+    const uint8_t* Bs = As + C::TILE;
 #pragma unroll
-    for (int kk = 0; kk < GB_BK; kk += 32) {
+    for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 bfr[4], af[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag<BT>(Bs, kk, wn * 64 + 16 * j, lane);
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<BT, BK>(Bs, kk, wn * 64 + 16 * j, lane);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = frag<AT>(As, kk, wm * 128 + 16 * i, lane);
+      for (int i = 0; i < 8; ++i) af[i] = frag<AT, BK>(As, kk, wm * 128 + 16 * i, lane);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -138,13 +157,30 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
     }
   };
 
-  issue(0, 0);
+  // NST-stage ring, NST-1 tiles in flight; per tile each thread issues
+  // L = 2 * DMA LDS-DMA instructions (counted by vmcnt, hand-waited).
+  constexpr int D = NST - 1, L = 2 * C::DMA;
+#pragma unroll
+  for (int u = 0; u < D; ++u)
+    if (u < nk) issue(u, u);
+  int stage = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    wait_vmcnt<0>();                                   // own DMA of tile kt landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own reads of the other stage retired
-    lds_barrier();  // everyone's tile kt landed; everyone done reading stage (kt+1)&1
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);     // in flight across the compute
-    compute(kt & 1);
+    const int younger = min(D - 1, nk - 1 - kt);  // tiles after kt still allowed in flight
+    if constexpr (D >= 3) {
+      if (younger >= 2) wait_vm<2 * L>();
+      else if (younger == 1) wait_vm<L>();
+      else wait_vm<0>();
+    } else if constexpr (D == 2) {
+      if (younger >= 1) wait_vm<L>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own reads of the recycled stage retired
+    lds_barrier();  // everyone's tile kt landed; everyone done reading stage (kt-1)%NST
+    if (kt + D < nk) issue(kt + D, stage == 0 ? NST - 1 : stage - 1);
+    compute(stage);
+    stage = stage == NST - 1 ? 0 : stage + 1;
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   lds_barrier();  // the ring is free for the epilogue staging
@@ -236,22 +272,51 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
   }
 }
 
-template <bool AT, bool BT, bool OUT32>
-void launch_big(const BigGemmArgs& p, hipStream_t s) {
+template <bool AT, bool BT, bool OUT32, int BK, int NST>
+void launch_big_t(const BigGemmArgs& p, hipStream_t s) {
+  using C = GbCfg<BK, NST>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<AT, BT, OUT32>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GB_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<AT, BT, OUT32, BK, NST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
     attr = true;
   }
   const dim3 grid((unsigned)((p.M / GB_BM) * (p.N / GB_BN)), (unsigned)p.splits);
-  gemm_big_kernel<AT, BT, OUT32><<<grid, 512, GB_LDS, s>>>(p);
+  gemm_big_kernel<AT, BT, OUT32, BK, NST><<<grid, 512, C::LDS, s>>>(p);
+}
+
+// pipeline variant: 0 = BK 64 / 2 stages (default), 1 = BK 32 / 4 stages (env
+// MFL_GB_PIPE).  Measured on the BERT shapes (scripts/gemm_sweep.sh): equal
+// forward time, BK 64 8-25 % faster on dgrad / wgrad -- the k-loop is not
+// DMA-latency bound at 256x256; its bubbles are the per-k-step barrier and
+// the per-tile epilogue.
+int gb_pipe() {
+  static const int v = [] {
+    const char* e = getenv("MFL_GB_PIPE");
+    return e && *e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <bool AT, bool BT, bool OUT32>
+void launch_big(BigGemmArgs p, int kdim, hipStream_t s) {
+  static const int dbg = [] {
+    const char* v = getenv("MFL_GB_DEBUG");
+    return v && *v ? atoi(v) : 0;
+  }();
+  p.dbg = dbg;
+  const int bk = gb_pipe() == 1 ? 32 : 64;
+  // p.kt_per_split arrives in units of GB_KQ (64) k-elements
+  p.kt_per_split *= GB_KQ / bk;
+  (void)kdim;
+  if (bk == 32) launch_big_t<AT, BT, OUT32, 32, 4>(p, s);
+  else launch_big_t<AT, BT, OUT32, 64, 2>(p, s);
 }
 
 }  // namespace
 
 bool gemm_big_ok(int M, int N, int K) {
-  return M > 0 && N > 0 && K > 0 && M % GB_BM == 0 && N % GB_BN == 0 && K % GB_BK == 0 &&
+  return M > 0 && N > 0 && K > 0 && M % GB_BM == 0 && N % GB_BN == 0 && K % GB_KQ == 0 &&
          (int64_t)M * K * 2 < (1LL << 32) && (int64_t)N * K * 2 < (1LL << 32) &&
          (int64_t)M * N * 2 < (1LL << 32);
 }
@@ -262,8 +327,8 @@ void launch_gemm_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
   p.a = x; p.b = w; p.M = M; p.N = N; p.K = K; p.lda = K; p.ldb = K;
   p.a_bytes = (uint32_t)((int64_t)M * K * 2); p.b_bytes = (uint32_t)((int64_t)N * K * 2);
   p.c16 = y; p.ldc = N; p.bias = bias; p.resid = resid; p.act_out = act_out;
-  p.splits = 1; p.kt_per_split = K / GB_BK;
-  launch_big<false, false, false>(p, s);
+  p.splits = 1; p.kt_per_split = K / GB_KQ;
+  launch_big<false, false, false>(p, K, s);
 }
 
 void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
@@ -273,8 +338,8 @@ void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, 
   p.a = dy; p.b = w; p.M = M; p.N = K; p.K = N; p.lda = N; p.ldb = K;
   p.a_bytes = (uint32_t)((int64_t)M * N * 2); p.b_bytes = (uint32_t)((int64_t)N * K * 2);
   p.c16 = dx; p.ldc = K; p.accum = accumulate;
-  p.splits = 1; p.kt_per_split = N / GB_BK;
-  launch_big<false, true, false>(p, s);
+  p.splits = 1; p.kt_per_split = N / GB_KQ;
+  launch_big<false, true, false>(p, N, s);
 }
 
 void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,
@@ -285,18 +350,23 @@ void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int
   p.a_bytes = (uint32_t)((int64_t)M * N * 2); p.b_bytes = (uint32_t)((int64_t)M * K * 2);
   p.c32 = dw; p.ldc = K; p.accum = accumulate;
   p.splits = gemm_big_wgrad_splits(M, N, K);
-  p.kt_per_split = (M / GB_BK + p.splits - 1) / p.splits;
-  launch_big<true, true, true>(p, s);
+  if (const char* v = getenv("MFL_GB_SPLITS")) p.splits = std::max(1, atoi(v));
+  p.kt_per_split = (M / GB_KQ + p.splits - 1) / p.splits;
+  launch_big<true, true, true>(p, M, s);
 }
 
-// Few output tiles, long reduction: split M so >= 256 workgroups run, each
-// slice >= 8 k-tiles.  > 1 means the kernel ADDS into dw with atomics (the
-// caller zeroes dw unless accumulating).
+// Few output tiles, long reduction: split M into the largest power-of-two
+// slice count that keeps tiles * slices <= 256 (one wave of workgroups) and
+// >= 8 k-tiles per slice.  Measured (scripts/gemm_sweep.sh, BERT shapes):
+// going past one wave of workgroups costs more in fp32 atomics than the
+// extra CUs return (qkv 108 us at 8 slices vs 148 at 16; ffn 151 at 4 vs 180
+// at 8).  > 1 means the kernel ADDS into dw (the caller zeroes dw unless
+// accumulating).
 int gemm_big_wgrad_splits(int M, int N, int K) {
   const int tiles = (N / GB_BM) * (K / GB_BN);
-  const int nk = M / GB_BK;
+  const int nk = M / GB_KQ;
   int s = 1;
-  while (tiles * s < 256 && nk / (2 * s) >= 8) s *= 2;
+  while (tiles * s * 2 <= 256 && nk / (2 * s) >= 8) s *= 2;
   return s;
 }
 

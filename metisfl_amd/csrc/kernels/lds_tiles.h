@@ -41,9 +41,18 @@ __device__ __forceinline__ void lds_barrier() {
 // swz = row & 15.
 template <int ROWB = 128>
 __device__ __forceinline__ int swz_b128(int row) {
-  static_assert(ROWB == 128 || ROWB == 256, "b128 swizzle defined for 128/256-B rows");
-  if constexpr (ROWB == 128) return (row >> 1) & 7;
-  else return row & 15;
+  static_assert(ROWB == 64 || ROWB == 128 || ROWB == 256, "b128 swizzle defined for 64/128/256-B rows");
+  if constexpr (ROWB == 64) {
+    // 64-B rows (BK = 32, gemm_big.hip): slot = 4*(row&3) + phys.  A b128
+    // lane group takes 4 rows of each residue class mod 4 at chunks
+    // {c, c, c^1, c^1} (e.g. rows 0,12 at c and rows 4,8 at c^1); the key
+    // {0,2,3,1}[(row>>2)&3] sends those four to distinct slots for every c.
+    return (0x78 >> (2 * ((row >> 2) & 3))) & 3;
+  } else if constexpr (ROWB == 128) {
+    return (row >> 1) & 7;
+  } else {
+    return row & 15;
+  }
 }
 // ds_read_b64_tr_b16 reads: 32 lanes per LDS cycle cover rows {R..R+3,
 // R+8..R+11} (R % 4 == 0), two 16-B chunks (c0 even, c0+1) each.
