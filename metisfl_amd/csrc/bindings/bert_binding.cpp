@@ -166,7 +166,8 @@ void ln_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor
 void emb_ln_bwd(torch::Tensor dy, torch::Tensor xsave, torch::Tensor mean, torch::Tensor rstd,
                 torch::Tensor gamma, torch::Tensor rec, int64_t rec_stride, int64_t B, int64_t T,
                 torch::Tensor dword, torch::Tensor dpos, torch::Tensor dtype, torch::Tensor dgamma,
-                torch::Tensor dbeta, int64_t H) {
+                torch::Tensor dbeta, int64_t H, c10::optional<torch::Tensor> demb,
+                c10::optional<torch::Tensor> idx, c10::optional<torch::Tensor> tmp) {
   ln_dims(H);
   const int64_t M = B * T;
   need(dy, torch::kBFloat16, M * H, "dy");
@@ -198,7 +199,25 @@ void emb_ln_bwd(torch::Tensor dy, torch::Tensor xsave, torch::Tensor mean, torch
   a.B = (int)B;
   a.pos_reduced = (B % 16 == 0) ? 1 : 0;  // bert.hip kLnBwdRows
   a.M = (int)M;
+  const bool sorted = demb.has_value() && demb->defined();
+  const int64_t V = dword.numel() / H;
+  int bits = 1;
+  while ((1LL << bits) < V) ++bits;
+  if (sorted) {
+    need(*demb, torch::kFloat32, M * H, "demb");
+    TORCH_CHECK(idx.has_value() && idx->defined() && tmp.has_value() && tmp->defined(),
+                "emb_ln_bwd: demb needs idx and tmp scratch");
+    need(*idx, torch::kInt32, 4 * M, "idx");
+    TORCH_CHECK(tmp->is_cuda() && (size_t)tmp->numel() >= mfl::emb_sort_temp_bytes((int)M, bits),
+                "emb_ln_bwd: tmp scratch too small (emb_sort_temp_bytes)");
+    a.demb = demb->data_ptr<float>();
+    a.keys = idx->data_ptr<int>();
+    a.vals = a.keys + M;
+  }
   mfl::launch_ln_bwd(a, (int)H, true, stream_of(dy));
+  if (sorted)
+    mfl::launch_emb_word_grad(a.demb, a.keys, a.vals, a.keys + 2 * M, a.keys + 3 * M, tmp->data_ptr(),
+                              (size_t)tmp->numel(), (int)M, (int)H, bits, a.dword, stream_of(dy));
 }
 
 void gelu_bwd(torch::Tensor dh, torch::Tensor z, torch::Tensor dz, c10::optional<torch::Tensor> dbias,
@@ -315,7 +334,17 @@ void register_bert(pybind11::module& m) {
   m.def("ln_fwd", &ln_fwd);
   m.def("emb_ln_fwd", &emb_ln_fwd);
   m.def("ln_bwd", &ln_bwd);
-  m.def("emb_ln_bwd", &emb_ln_bwd);
+  m.def("emb_ln_bwd", &emb_ln_bwd, pybind11::arg("dy"), pybind11::arg("xsave"), pybind11::arg("mean"),
+        pybind11::arg("rstd"), pybind11::arg("gamma"), pybind11::arg("rec"), pybind11::arg("rec_stride"),
+        pybind11::arg("B"), pybind11::arg("T"), pybind11::arg("dword"), pybind11::arg("dpos"),
+        pybind11::arg("dtype"), pybind11::arg("dgamma"), pybind11::arg("dbeta"), pybind11::arg("H"),
+        pybind11::arg("demb") = pybind11::none(), pybind11::arg("idx") = pybind11::none(),
+        pybind11::arg("tmp") = pybind11::none());
+  m.def("emb_sort_temp_bytes", [](int64_t M, int64_t V) {
+    int bits = 1;
+    while ((1LL << bits) < V) ++bits;
+    return (int64_t)mfl::emb_sort_temp_bytes((int)M, bits);
+  });
   m.def("gelu_bwd", &gelu_bwd);
   m.def("colsum", &colsum);
   m.def("attn_fwd", &attn_fwd);

@@ -42,9 +42,26 @@ struct LnBwdArgs {
   float* dpos = nullptr;
   float* dtype = nullptr;
   int B = 1, pos_reduced = 0;  // see ln_bwd_kernel
+  // contention-free word-table gradient (optional): dx rows go to demb
+  // [M][H] fp32 and (token, row) pairs to keys / vals [M]; launch_emb_word_grad
+  // then sorts by token and reduces each token's rows (no same-address
+  // atomics for frequent tokens such as [MASK] / [CLS])
+  float* demb = nullptr;
+  int* keys = nullptr;
+  int* vals = nullptr;
   int rows = 16;               // rows per block (set by the launcher)
   int M = 0;
 };
+
+// Word-embedding gradient from the demb / keys / vals scratch written by the
+// embedding LN backward: radix sort of (token, row) pairs (hipCUB) into
+// skeys / svals, then a chunked segmented reduction -- each token's rows are
+// summed in registers, only segments that straddle a 64-row chunk boundary
+// use atomics.  tmp: emb_sort_temp_bytes(M, key_bits) bytes.
+size_t emb_sort_temp_bytes(int M, int key_bits);
+void launch_emb_word_grad(const float* demb, const int* keys, const int* vals, int* skeys, int* svals,
+                          void* tmp, size_t tmp_bytes, int M, int H, int key_bits, float* dword,
+                          hipStream_t s);
 
 struct AttnArgs {
   const uint16_t* qkv = nullptr;  // [B*T][3H]: q | k | v, head h at columns h*64

@@ -23,6 +23,8 @@
 //  * mlm_*        gather of the masked positions, vocab-wide softmax CE with
 //                 16-B loads, scatter of their gradient back to the sequence.
 #include "kernels/common.h"
+#include <hipcub/hipcub.hpp>
+
 #include "kernels/bert.h"
 
 namespace mfl {
@@ -161,9 +163,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
         pd[v][k] += dx[k];
       }
       if constexpr (EMB) {
+        if (a.demb) {
+          float4* d = reinterpret_cast<float4*>(a.demb + (int64_t)row * H + c);
+          d[0] = float4{dx[0], dx[1], dx[2], dx[3]};
+          d[1] = float4{dx[4], dx[5], dx[6], dx[7]};
+          if (v == 0 && j == 0) {
+            a.keys[row] = tok;
+            a.vals[row] = row;
+          }
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          atomicAdd(a.dword + (int64_t)tok * H + c + k, dx[k]);
+          if (!a.demb) atomicAdd(a.dword + (int64_t)tok * H + c + k, dx[k]);
           if (!a.pos_reduced) atomicAdd(a.dpos + (int64_t)t * H + c + k, dx[k]);
         }
       } else {
@@ -194,6 +205,55 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
     if (d3) atomicAdd(d3 + c, red[2][c]);
     if (EMB && a.pos_reduced) atomicAdd(a.dpos + (int64_t)((blockIdx.x * kLnBwdRows) / a.B) * H + c, red[2][c]);
   }
+}
+
+// Segmented reduction of the token-sorted embedding-gradient rows: block =
+// 64 consecutive sorted positions x H/4 float4 columns.
+constexpr int kEmbChunk = 64;
+__global__ __launch_bounds__(256) void emb_word_reduce_kernel(const float* __restrict__ demb,
+                                                              const int* __restrict__ skeys,
+                                                              const int* __restrict__ svals, int M, int H,
+                                                              float* __restrict__ dword) {
+  const int c0 = blockIdx.x * kEmbChunk, c1 = min(M, c0 + kEmbChunk);
+  const int q = threadIdx.x;
+  if (4 * q >= H) return;
+  float4 acc = {0.f, 0.f, 0.f, 0.f};
+  int seg0 = c0;
+  for (int p = c0; p < c1; ++p) {
+    const int tok = skeys[p];
+    const float4 v = *reinterpret_cast<const float4*>(demb + (int64_t)svals[p] * H + 4 * q);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    const bool end = (p + 1 == c1) || (skeys[p + 1] != tok);
+    if (!end) continue;
+    // a segment touching a chunk edge may continue in the neighbouring chunk
+    const bool shared = (seg0 == c0 && c0 > 0 && skeys[c0 - 1] == tok) ||
+                        (p + 1 == c1 && c1 < M && skeys[c1] == tok);
+    float* d = dword + (int64_t)tok * H + 4 * q;
+    if (shared) {
+      atomicAdd(d + 0, acc.x); atomicAdd(d + 1, acc.y); atomicAdd(d + 2, acc.z); atomicAdd(d + 3, acc.w);
+    } else {  // the only writer of this token's row in this launch
+      float4 o = *reinterpret_cast<float4*>(d);
+      o.x += acc.x; o.y += acc.y; o.z += acc.z; o.w += acc.w;
+      *reinterpret_cast<float4*>(d) = o;
+    }
+    acc = float4{0.f, 0.f, 0.f, 0.f};
+    seg0 = p + 1;
+  }
+}
+
+size_t emb_sort_temp_bytes(int M, int key_bits) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int*)nullptr, (int*)nullptr,
+                                           (const int*)nullptr, (int*)nullptr, M, 0, key_bits);
+  return bytes;
+}
+
+void launch_emb_word_grad(const float* demb, const int* keys, const int* vals, int* skeys, int* svals,
+                          void* tmp, size_t tmp_bytes, int M, int H, int key_bits, float* dword,
+                          hipStream_t s) {
+  size_t bytes = tmp_bytes;
+  (void)hipcub::DeviceRadixSort::SortPairs(tmp, bytes, keys, skeys, vals, svals, M, 0, key_bits, s);
+  emb_word_reduce_kernel<<<(M + kEmbChunk - 1) / kEmbChunk, 256, 0, s>>>(demb, skeys, svals, M, H, dword);
 }
 
 void launch_ln_fwd(const LnFwdArgs& a, int H, bool emb, hipStream_t s) {

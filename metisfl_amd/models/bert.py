@@ -146,6 +146,9 @@ class BertMLM(StaticNet):
         self.g_h, self.g_z = e(M, F), e(M, F)
         self.g_qkv = e(M, 3 * H)
         self.g_u, self.g_th, self.g_tz, self.g_hm = e(R, H), e(R, H), e(R, H), e(R, H)
+        # word-embedding gradient by token sort + segmented sum (no same-address
+        # atomics for [MASK] / [CLS] rows); device only
+        self.emb_scratch = BO.EmbGradScratch(M, H, c.vocab, dev) if torch.device(dev).type == "cuda" else None
 
     def all_layers(self):
         return []
@@ -233,7 +236,7 @@ class BertMLM(StaticNet):
             dout = dx
         BO.emb_ln_bwd(dout, self.emb_x, self.emb_mean, self.emb_rstd, self._p("emb.ln.gamma"), self.rec,
                       c.rec_stride, B, T, g("emb.word"), g("emb.pos"), g("emb.type"), g("emb.ln.gamma"),
-                      g("emb.ln.beta"), H)
+                      g("emb.ln.beta"), H, scratch=self.emb_scratch)
 
     # ---- step bodies (captured into hipGraphs by StaticNet) ------------------------
     def _train_body(self, ds: DeviceDataset) -> None:

@@ -127,10 +127,27 @@ def ln_bwd(dy, x, mean, rstd, gamma, dx, dgamma, dbeta, M, H, dx2=None, dbias_pr
         dbias_prev.add_(d.sum(0).reshape(dbias_prev.shape))
 
 
-def emb_ln_bwd(dy, xsave, mean, rstd, gamma, rec, rec_stride, B, T, dword, dpos, dtype, dgamma, dbeta, H) -> None:
+class EmbGradScratch:
+    """Device scratch of the sorted (contention-free) word-embedding gradient:
+    fp32 dx rows [M][H], (token, row) pairs + their sorted copies, hipCUB
+    radix-sort temp storage."""
+
+    def __init__(self, M: int, H: int, V: int, device):
+        self.demb = torch.empty(M * H, dtype=torch.float32, device=device)
+        self.idx = torch.empty(4 * M, dtype=torch.int32, device=device)
+        nbytes = int(ops().emb_sort_temp_bytes(M, V)) if torch.device(device).type == "cuda" else 1
+        self.tmp = torch.empty(max(1, nbytes), dtype=torch.uint8, device=device)
+
+
+def emb_ln_bwd(dy, xsave, mean, rstd, gamma, rec, rec_stride, B, T, dword, dpos, dtype, dgamma, dbeta, H,
+               scratch: EmbGradScratch | None = None) -> None:
     if dy.is_cuda:
-        ops().emb_ln_bwd(dy, xsave, mean, rstd, gamma, rec, rec_stride, B, T, dword, dpos, dtype, dgamma,
-                         dbeta, H)
+        if scratch is not None:
+            ops().emb_ln_bwd(dy, xsave, mean, rstd, gamma, rec, rec_stride, B, T, dword, dpos, dtype, dgamma,
+                             dbeta, H, scratch.demb, scratch.idx, scratch.tmp)
+        else:
+            ops().emb_ln_bwd(dy, xsave, mean, rstd, gamma, rec, rec_stride, B, T, dword, dpos, dtype, dgamma,
+                             dbeta, H)
         return
     M = B * T
     d, dg, db = _ln_bwd_ref(dy, xsave, mean, rstd, gamma, M, H)

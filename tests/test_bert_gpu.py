@@ -68,12 +68,16 @@ def test_layernorm_fwd_bwd(H):
         assert rel(a, c) < 1e-2
 
 
-def test_embedding_layernorm_fwd_bwd():
+@pytest.mark.parametrize("sorted_grad", [False, True])
+def test_embedding_layernorm_fwd_bwd(sorted_grad):
+    """Embedding LN forward / backward vs CPU; ``sorted_grad``: the word-table
+    gradient by token sort + segmented sum (B = 32 puts [CLS] rows and ~640
+    [MASK] rows in long segments that cross many 64-row chunks)."""
     from metisfl_amd.datasets import synthetic_mlm
     from metisfl_amd.ops import bert as BO
     _native()
     torch.manual_seed(2)
-    B, T, P, H, V = 3, 128, 8, 256, 500
+    B, T, P, H, V = (32 if sorted_grad else 3), 128, (20 if sorted_grad else 8), 256, 500
     rec = torch.as_tensor(synthetic_mlm(B, T, P, V, seed=1))
     stride = rec.shape[1]
     word, pos, typ = (torch.randn(V, H) * 0.1).to(BF), (torch.randn(T, H) * 0.1).to(BF), (torch.randn(2, H) * 0.1).to(BF)
@@ -89,7 +93,13 @@ def test_embedding_layernorm_fwd_bwd():
                       mean, rstd, H, 1e-12)
         dw, dp, dt = torch.zeros(V, H, device=dev), torch.zeros(T, H, device=dev), torch.zeros(2, H, device=dev)
         dg, db = torch.zeros(H, device=dev), torch.zeros(H, device=dev)
-        BO.emb_ln_bwd(dy.to(dev), xs, mean, rstd, gam.to(dev), r, stride, B, T, dw, dp, dt, dg, db, H)
+        scr = BO.EmbGradScratch(M, H, V, dev) if (sorted_grad and dev != "cpu") else None
+        if scr is not None:
+            dw.fill_(0.5)  # the sorted path adds into the buffer (tied decoder grads land there too)
+        BO.emb_ln_bwd(dy.to(dev), xs, mean, rstd, gam.to(dev), r, stride, B, T, dw, dp, dt, dg, db, H,
+                      scratch=scr)
+        if scr is not None:
+            dw.sub_(0.5)
         res[dev] = (xs, y, dw, dp, dt, dg, db)
     for a, c in zip(res[DEV], res["cpu"]):
         assert rel(a, c) < 1e-2
