@@ -299,7 +299,8 @@ void head_forward_backward(torch::Tensor x, int64_t B, int64_t HW, int64_t C, to
                            c10::optional<torch::Tensor> bias, torch::Tensor labels,
                            c10::optional<torch::Tensor> feat, c10::optional<torch::Tensor> dlogits,
                            c10::optional<torch::Tensor> dx, c10::optional<torch::Tensor> stats,
-                           bool backward) {
+                           bool backward, c10::optional<torch::Tensor> dW,
+                           c10::optional<torch::Tensor> db) {
   CHECK_IN(x, torch::kBFloat16);
   TORCH_CHECK(x.numel() == B * HW * C, "head x size");
   CHECK_IN(W, torch::kFloat32);
@@ -307,7 +308,16 @@ void head_forward_backward(torch::Tensor x, int64_t B, int64_t HW, int64_t C, to
   const int64_t K = W.numel() / C;
   CHECK_IN(labels, torch::kInt32);
   TORCH_CHECK(labels.numel() >= B, "labels");
-  TORCH_CHECK(C + K <= 16384, "head too large for LDS");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && K <= 1024, "head: C must be a multiple of 8 (<= 2048), K <= 1024");
+  const bool fuse = dW.has_value() && dW->defined();
+  if (fuse) {
+    CHECK_IN((*dW), torch::kFloat32);
+    TORCH_CHECK(dW->numel() == K * C, "head dW size");
+    if (db.has_value() && db->defined()) {
+      CHECK_IN((*db), torch::kFloat32);
+      TORCH_CHECK(db->numel() == K, "head db size");
+    }
+  }
   if (backward) {
     TORCH_CHECK(feat.has_value() && dlogits.has_value() && dx.has_value(), "bwd buffers");
     TORCH_CHECK(feat->numel() >= B * C && dlogits->numel() >= B * K, "bwd buffer sizes");
@@ -318,7 +328,8 @@ void head_forward_backward(torch::Tensor x, int64_t B, int64_t HW, int64_t C, to
                            ptr_or_null<float>(bias), (int)K, labels.data_ptr<int>(),
                            ptr_or_null<float>(feat), ptr_or_null<float>(dlogits),
                            dx.has_value() && dx->defined() ? bf(*dx) : nullptr,
-                           ptr_or_null<float>(stats), backward, cur_stream(x));
+                           ptr_or_null<float>(stats), backward, cur_stream(x),
+                           fuse ? dW->data_ptr<float>() : nullptr, fuse ? ptr_or_null<float>(db) : nullptr);
 }
 
 void head_wgrad(torch::Tensor feat, torch::Tensor dlogits, int64_t B, int64_t C, int64_t K,
@@ -373,7 +384,11 @@ PYBIND11_MODULE(_ops, m) {
   m.def("bn_stats", &bn_stats);
   m.def("bn_apply", &bn_apply);
   m.def("bn_backward", &bn_backward);
-  m.def("head_forward_backward", &head_forward_backward);
+  m.def("head_forward_backward", &head_forward_backward, pybind11::arg("x"), pybind11::arg("B"),
+        pybind11::arg("HW"), pybind11::arg("C"), pybind11::arg("W"), pybind11::arg("bias"),
+        pybind11::arg("labels"), pybind11::arg("feat"), pybind11::arg("dlogits"), pybind11::arg("dx"),
+        pybind11::arg("stats"), pybind11::arg("backward"), pybind11::arg("dW") = pybind11::none(),
+        pybind11::arg("db") = pybind11::none());
   m.def("head_wgrad", &head_wgrad);
   m.def("gather_batch", &gather_batch);
   register_conv(m);

@@ -12,24 +12,48 @@
 
 namespace mfl {
 
+// One sample per workgroup.  Pooling and the dx broadcast move 8 channels
+// (16 B) per lane: thread t owns channel group t % G (G = C / 8) and pixel rows
+// t / G, t / G + R, ... (R = 256 / G row groups), partial sums meet in LDS.
+// With dW != nullptr the weight / bias gradient is fused too: the sample's
+// dlogits x feat outer product is added with fp32 atomics (B adders per
+// address; dW / db must be zero on entry -- the training step's gradient
+// buffer is) and head_wgrad_kernel is not launched.
 __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ x, int HW, int C,
                                                    const float* __restrict__ W,
                                                    const float* __restrict__ bias, int K,
                                                    const int* __restrict__ labels,
                                                    float* __restrict__ feat, float* __restrict__ dlog,
                                                    uint16_t* __restrict__ dx,
-                                                   float* __restrict__ stats, int B, int backward) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];  // feat[C] | logits[K]
+                                                   float* __restrict__ stats, int B, int backward,
+                                                   float* __restrict__ dW, float* __restrict__ db) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // feat[C] | logits[K] | partials[R][C]
   float* f = sm;
   float* lg = sm + C;
+  const int G = C >> 3;
+  const int R = max(1, 256 / G);
+  float* part = sm + C + ((K + 3) & ~3);
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
   const float inv_hw = 1.f / (float)HW;
   const uint16_t* xb = x + (int64_t)b * HW * C;
+  const int cg = t % G, rg = t / G;
+  if (rg < R) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int h = rg; h < HW; h += R) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(xb + (int64_t)h * C + 8 * cg), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[rg * C + 8 * cg + k] = s[k];
+  }
+  __syncthreads();
   for (int c = t; c < C; c += 256) {
     float s = 0.f;
-    for (int h = 0; h < HW; ++h) s += bf2f(xb[(int64_t)h * C + c]);
+    for (int r = 0; r < R; ++r) s += part[r * C + c];
     s *= inv_hw;
     f[c] = s;
     if (feat) feat[(int64_t)b * C + c] = s;
@@ -75,26 +99,39 @@ __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ 
         const float d = (p - (k == y ? 1.f : 0.f)) * invB;
         lg[k] = d;
         dlog[(int64_t)b * K + k] = d;
+        if (db) atomicAdd(&db[k], d);
       }
     }
   }
   if (!backward) return;
   __syncthreads();
-  uint16_t* dxb = dx + (int64_t)b * HW * C;
-  for (int c = t; c < C; c += 256) {
-    float s = 0.f;
-    for (int k = 0; k < K; ++k) s += lg[k] * W[(int64_t)k * C + c];
-    const uint16_t v = f2bf(s * inv_hw);
-    for (int h = 0; h < HW; ++h) dxb[(int64_t)h * C + c] = v;
+  if (dW) {
+    for (int i = t; i < K * C; i += 256) {
+      const int k = i / C, c = i - k * C;
+      atomicAdd(&dW[i], lg[k] * f[c]);
+    }
+  }
+  if (rg < R) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float s = 0.f;
+      for (int k = 0; k < K; ++k) s += lg[k] * W[(int64_t)k * C + 8 * cg + e];
+      v[e] = s * inv_hw;
+    }
+    const uint4 pk = pack8(v);
+    uint16_t* dxb = dx + (int64_t)b * HW * C + 8 * cg;
+    for (int h = rg; h < HW; h += R) *reinterpret_cast<uint4*>(dxb + (int64_t)h * C) = pk;
   }
 }
 
 void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,
                          int K, const int* labels, float* feat, float* dlogits, uint16_t* dx,
-                         float* stats, bool backward, hipStream_t s) {
-  const size_t sm = (size_t)(C + K) * sizeof(float);
+                         float* stats, bool backward, hipStream_t s, float* dW, float* db) {
+  const int G = C / 8, R = G >= 256 ? 1 : 256 / G;
+  const size_t sm = (size_t)(C + ((K + 3) & ~3) + (size_t)R * C) * sizeof(float);
   head_kernel<<<B, 256, sm, s>>>(x, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, B,
-                                 backward ? 1 : 0);
+                                 backward ? 1 : 0, backward ? dW : nullptr, backward ? db : nullptr);
 }
 
 __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict__ feat,

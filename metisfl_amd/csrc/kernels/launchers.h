@@ -91,7 +91,8 @@ void launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t s);
 // ---- head.hip ------------------------------------------------------------
 void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,
                          int K, const int* labels, float* feat, float* dlogits, uint16_t* dx,
-                         float* stats, bool backward, hipStream_t s);
+                         float* stats, bool backward, hipStream_t s, float* dW = nullptr,
+                         float* db = nullptr);
 void launch_head_wgrad(const float* feat, const float* dlogits, int B, int C, int K, float* dW,
                        float* db, hipStream_t s);
 

@@ -272,8 +272,9 @@ class ClassifierHead(Layer):
         self.dx = torch.zeros((self.N, self.HW, self.C), dtype=torch.bfloat16, device=device)
 
     def forward_backward(self, x, labels, stats, train=True):
+        # the weight gradient rides in the same launch (atomics into the
+        # step's zeroed gradient buffer): one kernel for the whole head
         K.head_forward_backward(x, self.N, self.HW, self.C, self.W, self.b, labels, self.feat,
-                                self.dlogits, self.dx, stats, backward=train)
-        if train:
-            K.head_wgrad(self.feat, self.dlogits, self.N, self.C, self.K, self.dW, self.db)
+                                self.dlogits, self.dx, stats, backward=train,
+                                dW=self.dW if train else None, db=self.db if train else None)
         return self.dx

@@ -241,12 +241,14 @@ def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
 
 # ---------------------------------------------------------------------------
 def head_forward_backward(x, B: int, HW: int, C: int, W, bias, labels, feat, dlogits, dx, stats,
-                          backward: bool = True) -> None:
+                          backward: bool = True, dW=None, db=None) -> None:
     """avgpool -> linear -> softmax-CE (+ backward to the pooled input).
-    stats[0:3] += (loss sum, #correct, #samples)."""
+    stats[0:3] += (loss sum, #correct, #samples).  With ``dW`` (and ``db``)
+    the weight / bias gradients are ADDED in the same launch (fused
+    head_wgrad; the buffers must hold zeros or a running sum)."""
     if x.is_cuda:
         ops().head_forward_backward(x, B, HW, C, W, bias, labels, feat, dlogits, dx, stats,
-                                    backward)
+                                    backward, dW, db)
         return
     xf = x.float().reshape(B, HW, C)
     f = xf.mean(1)
@@ -268,6 +270,10 @@ def head_forward_backward(x, B: int, HW: int, C: int, W, bias, labels, feat, dlo
     dlogits.view(-1)[: B * K].copy_(d.reshape(-1))
     dfeat = d @ W.reshape(K, C)
     dx.copy_((dfeat / HW)[:, None, :].expand(B, HW, C).reshape(dx.shape).to(torch.bfloat16))
+    if dW is not None:
+        dW.add_((d.t() @ f).reshape(dW.shape))
+        if db is not None:
+            db.add_(d.sum(0))
 
 
 def head_wgrad(feat, dlogits, B: int, C: int, K: int, dW, db) -> None:

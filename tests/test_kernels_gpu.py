@@ -254,6 +254,22 @@ def test_head_forward_backward():
     assert rel_err(dx, xr.grad) < 1e-2
     assert rel_err(dW, Wr.grad) < 1e-4
     assert rel_err(db, br.grad) < 1e-4
+    # fused weight gradient (one launch, atomics into a zeroed buffer)
+    dW2, db2 = torch.zeros(Kc, C, device=DEV), torch.zeros(Kc, device=DEV)
+    dx2 = torch.empty_like(x)
+    K.head_forward_backward(x, B, HW, C, W, b, lab, feat, dlog, dx2, None, True, dW=dW2, db=db2)
+    assert rel_err(dW2, Wr.grad) < 1e-4
+    assert rel_err(db2, br.grad) < 1e-4
+    assert torch.equal(dx2, dx)
+    # odd channel count: C = 200 (G = 25 channel groups, ragged row groups)
+    C2 = 200
+    x3 = bf(torch.randn(B, HW, C2, device=DEV))
+    W3 = torch.randn(Kc, C2, device=DEV) * 0.05
+    feat3, dx3 = torch.zeros(B * C2, device=DEV), torch.empty_like(x3)
+    K.head_forward_backward(x3, B, HW, C2, W3, b, lab, feat3, dlog, dx3, None, True)
+    xr3 = x3.float().cpu().requires_grad_(True)
+    F.cross_entropy(xr3.mean(1) @ W3.cpu().t() + b.cpu(), lab.long().cpu()).backward()
+    assert rel_err(dx3, xr3.grad) < 1e-2
 
 
 @pytest.mark.parametrize("kind", ["vanilla_sgd", "momentum_sgd", "fed_prox", "adam", "adam_weight_decay"])
