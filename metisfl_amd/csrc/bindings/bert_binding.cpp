@@ -58,6 +58,19 @@ void gemm_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, int64_t M, 
   mfl::launch_gemm_dgrad(bfp(dy), bfp(w), bfp(dx), (int)M, (int)N, (int)K, accumulate, stream_of(dy));
 }
 
+// dz = (dy w) * gelu'(z); dbias += colsum(dz)  (FFN1 backward, one launch)
+void gemm_dgrad_gelu(torch::Tensor dy, torch::Tensor w, torch::Tensor dz, torch::Tensor z,
+                     c10::optional<torch::Tensor> dbias, int64_t M, int64_t N, int64_t K) {
+  dense_dims(M, N, K);
+  need(dy, torch::kBFloat16, M * N, "dy");
+  need(w, torch::kBFloat16, N * K, "w");
+  need(dz, torch::kBFloat16, M * K, "dz");
+  need(z, torch::kBFloat16, M * K, "z");
+  if (dbias.has_value() && dbias->defined()) need(*dbias, torch::kFloat32, K, "dbias");
+  mfl::launch_gemm_dgrad_gelu(bfp(dy), bfp(w), bfp(dz), bfp(z), opt_ptr<float>(dbias), (int)M, (int)N,
+                              (int)K, stream_of(dy));
+}
+
 // dw[N][K] (+)= dy^T x  (fp32)
 // zeroed: dw is known to be zero on entry (the training step's gradient
 // buffer, re-zeroed by the optimizer launch) -> no memset before split plans
@@ -330,6 +343,7 @@ void register_bert(pybind11::module& m) {
   m.def("set_gemm_big", [](bool on) { mfl::set_gemm_big(on ? 1 : 0); });
   m.def("gemm_big_enabled", []() { return mfl::gemm_big_enabled() != 0; });
   m.def("gemm_dgrad", &gemm_dgrad);
+  m.def("gemm_dgrad_gelu", &gemm_dgrad_gelu);
   m.def("gemm_wgrad", &gemm_wgrad);
   m.def("ln_fwd", &ln_fwd);
   m.def("emb_ln_fwd", &emb_ln_fwd);

@@ -37,7 +37,13 @@ void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, 
                            bool accumulate, hipStream_t s);
 void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,
                            bool accumulate, hipStream_t s);
-int gemm_big_wgrad_splits(int M, int N, int K);  // > 1: adds into dw (atomics)
+int gemm_big_wgrad_splits(int M, int N, int K);
+void launch_gemm_big_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t* dz, const uint16_t* z,
+                                float* dbias, int M, int N, int K, hipStream_t s);
+// dz[M][K] = (dy W) * gelu'(z) (exact erf), dbias[K] += column sums of dz:
+// the FFN1 backward in one launch on the large-tile path (else dgrad + gelu_bwd)
+void launch_gemm_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t* dz, const uint16_t* z,
+                            float* dbias, int M, int N, int K, hipStream_t s);  // > 1: adds into dw (atomics)
 // 1 (default; env MFL_GEMM_BIG=0 turns it off): eligible shapes take the large-tile path
 void set_gemm_big(int on);
 int gemm_big_enabled();

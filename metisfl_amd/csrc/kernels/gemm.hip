@@ -14,6 +14,7 @@
 #include "kernels/common.h"
 #include "kernels/conv.h"
 #include "kernels/gemm.h"
+#include "kernels/bert.h"
 
 namespace mfl {
 
@@ -81,6 +82,16 @@ void launch_gemm_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int 
   ConvGeom g = dense_geom(M, K, N);
   ConvPlan p = plan_gemm(M, K, N);
   launch_conv_gemm(g, true, p, dy, w, dx, nullptr, nullptr, nullptr, accumulate, s);
+}
+
+void launch_gemm_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t* dz, const uint16_t* z,
+                            float* dbias, int M, int N, int K, hipStream_t s) {
+  if (gemm_big_enabled() && gemm_big_ok(M, K, N)) {
+    launch_gemm_big_dgrad_gelu(dy, w, dz, z, dbias, M, N, K, s);
+    return;
+  }
+  launch_gemm_dgrad(dy, w, dz, M, N, K, false, s);
+  launch_gelu_bwd(dz, z, dz, dbias, M, K, s);  // in place: each element read then written by one thread
 }
 
 void launch_gemm_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,

@@ -50,6 +50,10 @@ struct BigGemmArgs {
   int splits;            // split-K slices (fp32 output only; atomics into c32)
   int kt_per_split;      // k-tiles per slice
   int dbg;               // timing experiments (MFL_GB_DEBUG): bit0 skip MFMAs, bit1 skip operand DMA
+  // dgrad epilogue fusion of the GELU backward (bf16 output only):
+  //   out = bf16(acc * gelu'(z)),  colsum[col] += sum over rows of out
+  const uint16_t* gelu_z;
+  float* colsum;
 };
 
 namespace {
@@ -207,6 +211,9 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
   // ---- epilogue: per wave, 4 chunks of 32 rows x 64 cols through LDS --------
   float* W = reinterpret_cast<float*>(smem) + wave * (32 * GB_EPI_LD);
   const int fq = lane >> 4, fr = lane & 15;
+  // every item a lane stores has column group lane & 7 (item = lane + 64 u):
+  // per-lane column partial sums for the fused bias gradient
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
 #pragma unroll
@@ -256,8 +263,24 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] += o[k];
         }
+        if (p.gelu_z) {  // dz = dh * gelu'(z), exact erf GELU
+          float zz[8];
+          unpack8(*reinterpret_cast<const uint4*>(p.gelu_z + off), zz);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float cdf = 0.5f * (1.f + erff(zz[k] * 0.70710678f));
+            const float pdf = 0.39894228f * __expf(-0.5f * zz[k] * zz[k]);
+            v[k] *= cdf + zz[k] * pdf;
+          }
+        }
         const uint4 packed = pack8(v);
         *reinterpret_cast<uint4*>(dst) = packed;
+        if (p.colsum) {  // bias gradient of what the next GEMMs consume (rounded)
+          float f[8];
+          unpack8(packed, f);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) cs[k] += f[k];
+        }
         if (p.act_out) {  // exact (erf) GELU of the stored pre-activation
           float f[8], h[8];
           unpack8(packed, f);
@@ -269,6 +292,24 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();  // reads of this chunk done before the next overwrites W
+  }
+  if constexpr (!OUT32) {
+    if (p.colsum) {
+      // lanes sharing lane & 7 hold the same 8 columns: butterfly over lane >> 3
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float x = cs[k];
+        x += __shfl_xor(x, 8, 64);
+        x += __shfl_xor(x, 16, 64);
+        x += __shfl_xor(x, 32, 64);
+        cs[k] = x;
+      }
+      if (lane < 8) {
+        const int col = n0 + wn * 64 + lane * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) atomicAdd(p.colsum + col + k, cs[k]);
+      }
+    }
   }
 }
 
@@ -338,6 +379,16 @@ void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, 
   p.a = dy; p.b = w; p.M = M; p.N = K; p.K = N; p.lda = N; p.ldb = K;
   p.a_bytes = (uint32_t)((int64_t)M * N * 2); p.b_bytes = (uint32_t)((int64_t)N * K * 2);
   p.c16 = dx; p.ldc = K; p.accum = accumulate;
+  p.splits = 1; p.kt_per_split = N / GB_KQ;
+  launch_big<false, true, false>(p, N, s);
+}
+
+void launch_gemm_big_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t* dz, const uint16_t* z,
+                                float* dbias, int M, int N, int K, hipStream_t s) {
+  BigGemmArgs p{};
+  p.a = dy; p.b = w; p.M = M; p.N = K; p.K = N; p.lda = N; p.ldb = K;
+  p.a_bytes = (uint32_t)((int64_t)M * N * 2); p.b_bytes = (uint32_t)((int64_t)N * K * 2);
+  p.c16 = dz; p.ldc = K; p.gelu_z = z; p.colsum = dbias;
   p.splits = 1; p.kt_per_split = N / GB_KQ;
   launch_big<false, true, false>(p, N, s);
 }

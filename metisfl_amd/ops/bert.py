@@ -57,6 +57,19 @@ def gemm_dgrad(dy, w, dx, M, N, K, accumulate=False) -> None:
     _put(dx, v)
 
 
+def gemm_dgrad_gelu(dy, w, dz, z, M, N, K, dbias=None) -> None:
+    """dz = (dy w) * gelu'(z) (exact erf), dbias += column sums of dz: the
+    FFN1 backward GEMM with the GELU backward fused into its epilogue."""
+    if dy.is_cuda:
+        ops().gemm_dgrad_gelu(dy, w, dz, z, dbias, M, N, K)
+        return
+    v = _b(dy).reshape(M, N) @ _b(w).reshape(N, K)
+    g = (v * gelu_grad_ref(_b(z).reshape(M, K))).to(BF)
+    _put(dz, g)
+    if dbias is not None:
+        dbias.add_(g.float().sum(0).reshape(dbias.shape))
+
+
 def gemm_wgrad(x, dy, dw, M, N, K, accumulate=False, zeroed=False) -> None:
     """dw (+)= dy^T x  (fp32).  ``zeroed``: dw is already zero (skips the
     pre-zeroing of split-K plans; the training step's gradient buffer)."""

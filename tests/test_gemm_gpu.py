@@ -85,3 +85,23 @@ def test_big_and_conv_paths_agree():
         outs.append((y.float(), dw))
     assert _rel(outs[0][0], outs[1][0]) < 1e-2
     assert _rel(outs[0][1], outs[1][1]) < 1e-2
+
+
+@pytest.mark.parametrize("on", [True, False])
+def test_dgrad_gelu_fused_epilogue(on):
+    """FFN1 backward in one launch: dz = (dy W) * gelu'(z), dbias += colsum(dz);
+    large-tile fused epilogue (on) and the dgrad + gelu_bwd fallback (off)."""
+    from metisfl_amd.ops import bert as BO
+    _ops().set_gemm_big(on)
+    M, N, K = 1024, 768, 3072
+    g = torch.Generator(device="cuda").manual_seed(21)
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.05).bfloat16()
+    z = (torch.randn(M, K, device="cuda", generator=g) * 2).bfloat16()
+    dz = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+    db = torch.full((K,), 0.25, device="cuda")
+    BO.gemm_dgrad_gelu(dy, w, dz, z, M, N, K, dbias=db)
+    dh = dy.float() @ w.float()
+    ref = dh * BO.gelu_grad_ref(z.float())
+    assert _rel(dz, ref) < 1e-2
+    assert _rel(db - 0.25, ref.sum(0)) < 1e-2
