@@ -61,6 +61,10 @@ namespace {
 constexpr int GB_BM = 256, GB_BN = 256;
 constexpr int GB_EPI_LD = 68;               // fp32 staging row pitch (64 + 4)
 constexpr int GB_KQ = 64;                   // K granularity the shapes must meet
+#ifndef MFL_GB_PIN_ORDER
+#define MFL_GB_PIN_ORDER 1
+#endif
+constexpr bool kGbPinOrder = MFL_GB_PIN_ORDER;
 // Pipeline variants: BK = 64 with a 2-stage ring (one tile in flight across
 // the compute), or BK = 32 with a 4-stage ring (three tiles in flight).
 template <int BK, int NST>
@@ -147,6 +151,32 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
     if (p.dbg & 1) return;
     const uint8_t* As = smem + stage * C::STAGE;
     const uint8_t* Bs = As + C::TILE;
+    if constexpr (kGbPinOrder && BK == 64 && !(AT && BT)) {
+      // Both 32-deep slices' fragments (24 reads) go out before the first
+      // MFMA, so slice 1's LDS latency hides under slice 0's 32 MFMAs.
+      bf16x8 b0[4], a0[8], b1[4], a1[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b0[j] = frag<BT, BK>(Bs, 0, wn * 64 + 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a0[i] = frag<AT, BK>(As, 0, wm * 128 + 16 * i, lane);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b1[j] = frag<BT, BK>(Bs, 32, wn * 64 + 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a1[i] = frag<AT, BK>(As, 32, wm * 128 + 16 * i, lane);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 bfr[4], af[8];
@@ -154,10 +184,16 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
       for (int j = 0; j < 4; ++j) bfr[j] = frag<BT, BK>(Bs, kk, wn * 64 + 16 * j, lane);
 #pragma unroll
       for (int i = 0; i < 8; ++i) af[i] = frag<AT, BK>(As, kk, wm * 128 + 16 * i, lane);
+      // Pin the order: all 12 fragment reads in flight together, then the 32
+      // MFMAs.  Left alone, hipcc interleaves read -> lgkmcnt(0) -> 4 MFMAs
+      // eight times per slice (register-pressure heuristic), exposing eight
+      // LDS latencies per 512 MFMA cycles.
+      if constexpr (kGbPinOrder) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      if constexpr (kGbPinOrder) __builtin_amdgcn_sched_barrier(0);
     }
   };
 
