@@ -387,6 +387,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
         if constexpr (DGRAD) bfr[j] = tr_frag<B_ROWB>(Bs, kk, wn * (BN / 2) + 16 * j, lane);
         else bfr[j] = b128_frag<ROWA>(Bs, kk, wn * (BN / 2) + 16 * j, lane);
       }
+      if constexpr (DGRAD) frags_ready(bfr);  // asm tr-reads: not tracked by hipcc
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -571,6 +572,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
       for (int i = 0; i < TM; ++i) af[i] = tr_frag<128>(As, kk, wm * (BM / 2) + 16 * i, lane);
 #pragma unroll
       for (int jj = 0; jj < TN; ++jj) bfr[jj] = tr_frag<128>(Bs, kk, wn * (BN / 2) + 16 * jj, lane);
+      frags_ready(af);  // asm tr-reads: not tracked by hipcc
+      frags_ready(bfr);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll

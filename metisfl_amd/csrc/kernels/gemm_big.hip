@@ -151,7 +151,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
     if (p.dbg & 1) return;
     const uint8_t* As = smem + stage * C::STAGE;
     const uint8_t* Bs = As + C::TILE;
-    if constexpr (kGbPinOrder && BK == 64 && !(AT && BT)) {
+    if constexpr (kGbPinOrder && BK == 64 && !AT && !BT) {
       // Both 32-deep slices' fragments (24 reads) go out before the first
       // MFMA, so slice 1's LDS latency hides under slice 0's 32 MFMAs.
       bf16x8 b0[4], a0[8], b1[4], a1[8];
@@ -184,6 +184,9 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
       for (int j = 0; j < 4; ++j) bfr[j] = frag<BT, BK>(Bs, kk, wn * 64 + 16 * j, lane);
 #pragma unroll
       for (int i = 0; i < 8; ++i) af[i] = frag<AT, BK>(As, kk, wm * 128 + 16 * i, lane);
+      // transposing reads go through asm (lds_tiles.h): wait for them explicitly
+      if constexpr (AT) frags_ready(af);
+      if constexpr (BT) frags_ready(bfr);
       // Pin the order: all 12 fragment reads in flight together, then the 32
       // MFMAs.  Left alone, hipcc interleaves read -> lgkmcnt(0) -> 4 MFMAs
       // eight times per slice (register-pressure heuristic), exposing eight

@@ -70,6 +70,21 @@ __device__ __forceinline__ int swz_tr(int row) {
 typedef short v4s __attribute__((ext_vector_type(4)));
 // MFMA B/A fragment from a [k][col] tile via transposing reads: lane gets
 // column (col0 + lane%16), k = 8*(lane/16) + 0..7 of the 32-k slice at kk.
+//
+// The reads are issued through inline asm, NOT __builtin_amdgcn_ds_read_tr16_b64:
+// hipcc's waitcnt pass treats the builtin as possibly aliasing every LDS-DMA
+// write still in flight and emits s_waitcnt vmcnt(0) in front of the first
+// one -- inside a k-loop that drains the whole DMA ring each step (measured:
+// conv dgrad / wgrad ran with zero tiles in flight).  The tile being read was
+// already made visible by the caller's counted vmcnt + barrier.  The price:
+// the compiler no longer tracks these reads, so every fragment must pass
+// frags_ready() (an lgkmcnt(0) wait tied to its registers) before use.
+__device__ __forceinline__ v4s ds_read_tr_b64(const uint8_t* p) {
+  v4s r;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
 template <int ROWB>
 __device__ __forceinline__ bf16x8 tr_frag(const uint8_t* tile, int kk, int col0, int lane) {
   const int grp = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
@@ -79,13 +94,21 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint8_t* tile, int kk, int col0,
   for (int h = 0; h < 2; ++h) {
     const int row = kk + 8 * grp + 4 * h + tq;
     const int off = row * ROWB + ((((col >> 3) ^ swz_tr<ROWB>(row))) << 4) + ((col & 4) << 1);
-    const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(tile + off));
+    const v4s v = ds_read_tr_b64(tile + off);
     out[4 * h + 0] = v[0];
     out[4 * h + 1] = v[1];
     out[4 * h + 2] = v[2];
     out[4 * h + 3] = v[3];
   }
   return out;
+}
+// Wait for every outstanding LDS read of this wave, then pin the fragments
+// behind the wait (their consumers cannot be scheduled above it).
+template <int N>
+__device__ __forceinline__ void frags_ready(bf16x8 (&f)[N]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(f[i]));
 }
 // fragment from a [row][k] tile (ROWB-byte rows): lane reads row r0 + lane%16,
 // k-chunk (kk/8 + lane/16).
