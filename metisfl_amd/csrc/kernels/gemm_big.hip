@@ -445,19 +445,19 @@ void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int
   launch_big<true, true, true>(p, M, s);
 }
 
-// Few output tiles, long reduction: split M into the largest power-of-two
-// slice count that keeps tiles * slices <= 256 (one wave of workgroups) and
-// >= 8 k-tiles per slice.  Measured (scripts/gemm_sweep.sh, BERT shapes):
-// going past one wave of workgroups costs more in fp32 atomics than the
-// extra CUs return (qkv 108 us at 8 slices vs 148 at 16; ffn 151 at 4 vs 180
-// at 8).  > 1 means the kernel ADDS into dw (the caller zeroes dw unless
-// accumulating).
+// Few output tiles, long reduction: split M so that tiles * slices fills ONE
+// wave of workgroups (<= 256 = one per CU; the kernel holds 128 KiB of LDS)
+// with >= 16 k-tiles per slice (attn-out: 28 slices of 9 k-tiles 66 us vs 16
+// of 16 62 us -- short slices are all prologue / epilogue).  Measured (scripts/gemm_sweep.sh, BERT shapes):
+// a second, partial wave of workgroups costs more than it returns (qkv 108 us
+// at 216 workgroups vs 148 at 432), and power-of-two slice counts left up to
+// 44 % of the CUs idle (ffn: 36 tiles x 4 = 144 workgroups) -- hence
+// floor(256 / tiles) slices.  > 1 means the kernel ADDS into dw (the caller
+// zeroes dw unless accumulating).
 int gemm_big_wgrad_splits(int M, int N, int K) {
   const int tiles = (N / GB_BM) * (K / GB_BN);
   const int nk = M / GB_KQ;
-  int s = 1;
-  while (tiles * s * 2 <= 256 && nk / (2 * s) >= 8) s *= 2;
-  return s;
+  return std::max(1, std::min(256 / std::max(1, tiles), nk / 16));
 }
 
 }  // namespace mfl
