@@ -66,16 +66,23 @@ def test_graph_replay_equals_eager():
     x, y = _data(64, 1)
     a = _make("cuda", lr=0.05)
     b = _make("cuda", lr=0.05)
+    c = _make("cuda", lr=0.05)
     da = a.make_dataset(x, y, shuffle=False)
     db = b.make_dataset(x, y, shuffle=False)
+    dc = c.make_dataset(x, y, shuffle=False)
     for _ in range(3):
         a._train_body(da)
+        c._train_body(dc)
     b.train_steps(db, 3)  # captured hipGraph
     torch.cuda.synchronize()
     assert int(a.state.step.cpu()) == int(b.state.step.cpu()) == 3
-    # atomics (BN statistics, split-K wgrad) make summation order vary run to
-    # run, so equality is up to floating-point reassociation
-    assert torch.allclose(a.state.model32, b.state.model32, rtol=1e-3, atol=1e-4)
+    # atomics (BN statistics, split-K wgrad) make the summation order vary
+    # run to run, and three lr-0.05 steps amplify it: the graph must agree
+    # with eager as well as eager agrees with itself (calibrated, floor 1e-3)
+    noise = float((a.state.model32 - c.state.model32).abs().max())
+    diff = float((a.state.model32 - b.state.model32).abs().max())
+    print(f"graph-vs-eager max |diff| {diff:.2e}, eager-vs-eager {noise:.2e}")
+    assert diff <= max(1e-3, 8 * noise), (diff, noise)
 
 
 def test_full_width_resnet18_trains():
