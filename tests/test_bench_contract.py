@@ -1,0 +1,70 @@
+"""The benchmark-script contract the round driver depends on (bench.py and
+benchmarks/*): one JSON line from rank 0 with the BASELINE metric and the
+required keys, on 1 process and on 2 processes (torch.distributed.run, gloo
+on the CPU -- the same code path the RCCL run takes on GPUs), with tiny
+synthetic shards so it finishes in seconds."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+            "scaling", "vs_baseline", "dtype", "data", "config"}
+TINY = ["--train-size", "64", "--test-size", "32", "--batch", "8", "--local-epochs", "1", "--steps", "1",
+        "--warmup", "0"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env():
+    env = dict(os.environ)
+    env["CUDA_VISIBLE_DEVICES"] = ""  # CPU path even on a GPU box
+    env["HIP_VISIBLE_DEVICES"] = ""
+    env["OMP_NUM_THREADS"] = "2"
+    env["PYTHONPATH"] = ROOT
+    return env
+
+
+def _json_line(out: str) -> dict:
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_single_process_json_contract():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *TINY], cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert REQUIRED <= set(d)
+    assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert d["n_gpus"] == 1 and d["steps"] == 1 and d["value"] > 0 and d["higher_is_better"] is True
+    assert d["config"]["model"] == "resnet18-cifar"
+
+
+def test_bench_two_ranks_one_json_line():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", *TINY]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)  # rank 0 only
+    assert d["n_gpus"] == 2 and d["config"]["learners"] == 2
+    assert d["config"]["parallelism"] == "fedavg-dp2"
+
+
+def test_async_bench_json_contract():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "async_bench.py"), "--train-size", "32",
+                        "--batch", "8", "--tasks", "1", "--warmup", "0", "--poll-every", "2"], cwd=ROOT,
+                       env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert REQUIRED <= set(d) and d["updates"] == 1
