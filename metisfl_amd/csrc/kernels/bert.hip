@@ -399,8 +399,9 @@ __device__ __forceinline__ void st_bf16(uint8_t* t, int off, float v) {
 }
 
 // stage a [128][64] head slice of a [rows][ld] bf16 matrix into LDS
+template <int NT = 256>
 __device__ __forceinline__ void load_head(uint8_t* dst, const uint16_t* src, int64_t row0, int ld, int col0) {
-  for (int i = threadIdx.x; i < kT * 8; i += 256) {
+  for (int i = threadIdx.x; i < kT * 8; i += NT) {
     const int r = i >> 3, c = (i & 7) * 8;
     *reinterpret_cast<uint4*>(dst + toff<128>(r, c)) =
         *reinterpret_cast<const uint4*>(src + (row0 + r) * ld + col0 + c);
@@ -497,12 +498,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       }
 }
 
-__device__ __forceinline__ void colsum_tile(const f32x4 (&acc)[2][4], float* cs, int lane, float mul) {
+template <int NI>
+__device__ __forceinline__ void colsum_tile(const f32x4 (&acc)[NI][4], float* cs, int lane, float mul) {
 #pragma unroll
   for (int dj = 0; dj < 4; ++dj) {
     float v = 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) v += acc[i][dj][e] * mul;
     v += __shfl_xor(v, 16);
@@ -511,7 +513,12 @@ __device__ __forceinline__ void colsum_tile(const f32x4 (&acc)[2][4], float* cs,
   }
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
+// NW waves per workgroup, kT / NW query rows (and key rows) per wave.  The
+// K/V/Q/dO + P/dS tiles take 130 KiB of LDS (one workgroup per CU), so the
+// wave count is the only occupancy lever: NW = 8 runs two waves per SIMD.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
+  constexpr int RW = kT / NW, NI = RW / 16, NT = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int HT = kT * kD * 2;  // 16 KiB head tile
   uint8_t* Qs = smem;
@@ -527,10 +534,10 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
   const int b = blockIdx.x / a.heads, h = blockIdx.x - b * a.heads;
   const int H = a.heads * kD, ld = 3 * H;
   const int64_t row0 = (int64_t)b * kT;
-  load_head(Qs, a.qkv, row0, ld, h * kD);
-  load_head(Ks, a.qkv, row0, ld, H + h * kD);
-  load_head(Vs, a.qkv, row0, ld, 2 * H + h * kD);
-  {
+  load_head<NT>(Qs, a.qkv, row0, ld, h * kD);
+  load_head<NT>(Ks, a.qkv, row0, ld, H + h * kD);
+  load_head<NT>(Vs, a.qkv, row0, ld, 2 * H + h * kD);
+  if (threadIdx.x < 2 * kT) {
     // dO into LDS and D[t] = sum_d dO[t][d] * O[t][d]: thread -> row tid/2, half tid&1
     const int r = threadIdx.x >> 1, half = threadIdx.x & 1;
     float dsum = 0.f;
@@ -551,22 +558,22 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
       Dd[r] = dsum;
       Ls[r] = a.lse[((int64_t)b * a.heads + h) * kT + r];
     }
-    if (threadIdx.x < 3 * kD) cs[threadIdx.x] = 0.f;
   }
+  if (threadIdx.x < 3 * kD) cs[threadIdx.x] = 0.f;
   __syncthreads();
-  const int t0 = wave * 32;
+  const int t0 = wave * RW;
   const float c = a.scale * kLog2e;
   {
-    f32x4 s[2][8], dp[2][8];
+    f32x4 s[NI][8], dp[NI][8];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int jt = 0; jt < 8; ++jt) s[i][jt] = dp[i][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < kD; kk += 32) {
-      bf16x8 qf[2], df[2];
+      bf16x8 qf[NI], df[NI];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NI; ++i) {
         qf[i] = frag_row<128>(Qs, t0 + 16 * i, kk, lane);
         df[i] = frag_row<128>(dOs, t0 + 16 * i, kk, lane);
       }
@@ -575,14 +582,14 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
         const bf16x8 kf = frag_row<128>(Ks, 16 * jt, kk, lane);
         const bf16x8 vf = frag_row<128>(Vs, 16 * jt, kk, lane);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < NI; ++i) {
           s[i][jt] = mma(qf[i], kf, s[i][jt]);
           dp[i][jt] = mma(df[i], vf, dp[i][jt]);
         }
       }
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = t0 + 16 * i + 4 * (lane >> 4) + e;
@@ -599,25 +606,25 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
   __builtin_amdgcn_wave_barrier();
   // dQ = scale * dS K  (this wave's rows; dS rows written by this wave)
   {
-    f32x4 acc[2][4];
+    f32x4 acc[NI][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int dj = 0; dj < 4; ++dj) acc[i][dj] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < kT; kk += 32) {
-      bf16x8 af[2];
+      bf16x8 af[NI];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = frag_row<256>(dSs, t0 + 16 * i, kk, lane);
+      for (int i = 0; i < NI; ++i) af[i] = frag_row<256>(dSs, t0 + 16 * i, kk, lane);
 #pragma unroll
       for (int dj = 0; dj < 4; ++dj) {
         const bf16x8 kf = frag_col<128>(Ks, kk, 16 * dj, lane);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) acc[i][dj] = mma(af[i], kf, acc[i][dj]);
+        for (int i = 0; i < NI; ++i) acc[i][dj] = mma(af[i], kf, acc[i][dj]);
       }
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int dj = 0; dj < 4; ++dj)
 #pragma unroll
@@ -630,17 +637,17 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
   __syncthreads();  // every wave's P and dS rows are in LDS
   // dK = scale * dS^T Q and dV = P^T dO for key rows s0 .. s0+31
   {
-    const int s0 = wave * 32;
-    f32x4 dk[2][4], dv[2][4];
+    const int s0 = wave * RW;
+    f32x4 dk[NI][4], dv[NI][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int dj = 0; dj < 4; ++dj) dk[i][dj] = dv[i][dj] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < kT; kk += 32) {
-      bf16x8 sf[2], pf[2];
+      bf16x8 sf[NI], pf[NI];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NI; ++i) {
         sf[i] = frag_col<256>(dSs, kk, s0 + 16 * i, lane);
         pf[i] = frag_col<256>(Ps, kk, s0 + 16 * i, lane);
       }
@@ -649,14 +656,14 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
         const bf16x8 qf = frag_col<128>(Qs, kk, 16 * dj, lane);
         const bf16x8 of = frag_col<128>(dOs, kk, 16 * dj, lane);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < NI; ++i) {
           dk[i][dj] = mma(sf[i], qf, dk[i][dj]);
           dv[i][dj] = mma(pf[i], of, dv[i][dj]);
         }
       }
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int dj = 0; dj < 4; ++dj)
 #pragma unroll
@@ -691,9 +698,19 @@ void launch_attn_fwd(const AttnArgs& a, hipStream_t s) {
 }
 
 void launch_attn_bwd(const AttnArgs& a, hipStream_t s) {
-  static bool done = false;
-  lds_attr(reinterpret_cast<const void*>(&attn_bwd_kernel), attn_bwd_lds(), done);
-  attn_bwd_kernel<<<a.batch * a.heads, 256, attn_bwd_lds(), s>>>(a);
+  // 8 waves by default; MFL_ATTN_BWD_WAVES=4 for the one-wave-per-SIMD variant
+  static const int nw = [] {
+    const char* v = getenv("MFL_ATTN_BWD_WAVES");
+    return v && *v == '4' ? 4 : 8;
+  }();
+  static bool done4 = false, done8 = false;
+  if (nw == 4) {
+    lds_attr(reinterpret_cast<const void*>(&attn_bwd_kernel<4>), attn_bwd_lds(), done4);
+    attn_bwd_kernel<4><<<a.batch * a.heads, 256, attn_bwd_lds(), s>>>(a);
+  } else {
+    lds_attr(reinterpret_cast<const void*>(&attn_bwd_kernel<8>), attn_bwd_lds(), done8);
+    attn_bwd_kernel<8><<<a.batch * a.heads, 512, attn_bwd_lds(), s>>>(a);
+  }
 }
 
 // =============================================================================
