@@ -50,6 +50,7 @@ struct LnBwdArgs {
   int* keys = nullptr;
   int* vals = nullptr;
   int rows = 16;               // rows per block (set by the launcher)
+  int dbg = 0;                 // timing experiments (MFL_LN_BWD_DEBUG): bit0 skip global column atomics, bit1 skip LDS reduction
   int M = 0;
 };
 

@@ -108,9 +108,9 @@ constexpr int kLnBwdRows = 16;  // rows per block of the embedding variant (pos_
 template <int V, bool EMB>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
   constexpr int H = 256 * V;
-  __shared__ float red[3][H];  // dgamma, dbeta, sum(dx) partials
-  for (int i = threadIdx.x; i < 3 * H; i += 256) (&red[0][0])[i] = 0.f;
-  __syncthreads();
+  // per-wave column partials [wave][dgamma | dbeta | sum dx][H]; every slot is
+  // written exactly once (no zeroing, no LDS atomics)
+  __shared__ __attribute__((aligned(16))) float red[4][3][H];
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
   float pg[V][8], pb[V][8], pd[V][8];
 #pragma unroll
@@ -184,26 +184,51 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
       }
     }
   }
-  // block reduction of the column partials (LDS atomics), then one global
-  // atomic per column per block
+  if (a.dbg & 2) return;
+  // Block reduction of the column partials.  The two half-waves of a wave own
+  // the same columns: fold them with one cross-half shuffle, write the wave's
+  // row of red[w] with 16-B stores, then every thread sums its columns over
+  // the 4 waves.  (LDS atomics from all 8 half-waves onto shared columns cost
+  // 22 of the kernel's 45 us at the BERT shape: scripts/ln_micro.py.)
+  const int w = threadIdx.x >> 6;
 #pragma unroll
   for (int v = 0; v < V; ++v)
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = (v * 32 + j) * 8 + k;
-      atomicAdd(&red[0][c], pg[v][k]);
-      atomicAdd(&red[1][c], pb[v][k]);
-      atomicAdd(&red[2][c], pd[v][k]);
+      pg[v][k] += __shfl_xor(pg[v][k], 32);
+      pb[v][k] += __shfl_xor(pb[v][k], 32);
+      pd[v][k] += __shfl_xor(pd[v][k], 32);
     }
+  if ((threadIdx.x & 63) < 32) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int c = (v * 32 + j) * 8;
+      float4* r0 = reinterpret_cast<float4*>(&red[w][0][c]);
+      float4* r1 = reinterpret_cast<float4*>(&red[w][1][c]);
+      float4* r2 = reinterpret_cast<float4*>(&red[w][2][c]);
+      r0[0] = float4{pg[v][0], pg[v][1], pg[v][2], pg[v][3]};
+      r0[1] = float4{pg[v][4], pg[v][5], pg[v][6], pg[v][7]};
+      r1[0] = float4{pb[v][0], pb[v][1], pb[v][2], pb[v][3]};
+      r1[1] = float4{pb[v][4], pb[v][5], pb[v][6], pb[v][7]};
+      r2[0] = float4{pd[v][0], pd[v][1], pd[v][2], pd[v][3]};
+      r2[1] = float4{pd[v][4], pd[v][5], pd[v][6], pd[v][7]};
+    }
+  }
   __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    for (int c = threadIdx.x; c < H; c += 256)
+      red[0][q][c] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
+  __syncthreads();
+  if (a.dbg & 1) return;
   for (int c = threadIdx.x; c < H; c += 256) {
-    atomicAdd(a.dgamma + c, red[0][c]);
-    atomicAdd(a.dbeta + c, red[1][c]);
+    atomicAdd(a.dgamma + c, red[0][0][c]);
+    atomicAdd(a.dbeta + c, red[0][1][c]);
     // EMB: the type table's gradient (token type 0 for every position);
     // otherwise the bias gradient of the GEMM that produced the LN input
     float* d3 = EMB ? a.dtype : a.dbias_prev;
-    if (d3) atomicAdd(d3 + c, red[2][c]);
-    if (EMB && a.pos_reduced) atomicAdd(a.dpos + (int64_t)((blockIdx.x * kLnBwdRows) / a.B) * H + c, red[2][c]);
+    if (d3) atomicAdd(d3 + c, red[0][2][c]);
+    if (EMB && a.pos_reduced) atomicAdd(a.dpos + (int64_t)((blockIdx.x * kLnBwdRows) / a.B) * H + c, red[0][2][c]);
   }
 }
 
@@ -272,7 +297,16 @@ void launch_ln_bwd(const LnBwdArgs& args, int H, bool emb, hipStream_t s) {
   // ~256 blocks: enough to fill the CUs, few enough that the per-block
   // column partials (3 H global atomics each) stay cheap
   LnBwdArgs a = args;
-  a.rows = max(16, ((a.M + 255) / 256 + 7) / 8 * 8);
+  static const int target_blocks = [] {  // env MFL_LN_BWD_BLOCKS (timing experiments)
+    const char* v = getenv("MFL_LN_BWD_BLOCKS");
+    return v && *v ? atoi(v) : 256;
+  }();
+  a.rows = max(16, ((a.M + target_blocks - 1) / target_blocks + 7) / 8 * 8);
+  static const int dbg = [] {
+    const char* v = getenv("MFL_LN_BWD_DEBUG");
+    return v && *v ? atoi(v) : 0;
+  }();
+  a.dbg = dbg;
   const int rows = emb ? kLnBwdRows : a.rows;
   const unsigned grid = (a.M + rows - 1) / rows;
 #define MFL_LN_B(V_)                                                               \
