@@ -126,7 +126,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int tiles_n = p.N / GB_BN;
+  const int tiles_n = (p.N + GB_BN - 1) / GB_BN;  // ragged last tile: reads OOB-zero / skipped stores
   const int m0 = (wgid / tiles_n) * GB_BM;
   const int n0 = (wgid - (wgid / tiles_n) * tiles_n) * GB_BN;
   const auto rsA = make_rsrc(p.a, p.a_bytes);
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
           for (int e = 0; e < 4; ++e) {
             const int row = m0 + wm * 128 + 16 * i + 4 * fq + e;
             const int col = n0 + wn * 64 + 16 * j + fr;
-            atomicAdd(p.c32 + (int64_t)row * p.ldc + col, acc[i][j][e]);
+            if (row < p.M && col < p.N) atomicAdd(p.c32 + (int64_t)row * p.ldc + col, acc[i][j][e]);
           }
       return;
     }
@@ -273,6 +273,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       const int row = m0 + wm * 128 + 32 * c + rl;
       const int col = n0 + wn * 64 + cg * 8;
+      if (row >= p.M || col >= p.N) continue;  // ragged edge tiles (N % 8 == 0)
       const int64_t off = (int64_t)row * p.ldc + col;
       if constexpr (OUT32) {
         float4* dst = reinterpret_cast<float4*>(p.c32 + off);
@@ -343,7 +344,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
         x += __shfl_xor(x, 32, 64);
         cs[k] = x;
       }
-      if (lane < 8) {
+      if (lane < 8 && n0 + wn * 64 + lane * 8 < p.N) {
         const int col = n0 + wn * 64 + lane * 8;
 #pragma unroll
         for (int k = 0; k < 8; ++k) atomicAdd(p.colsum + col + k, cs[k]);
@@ -361,7 +362,7 @@ void launch_big_t(const BigGemmArgs& p, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
     attr = true;
   }
-  const dim3 grid((unsigned)((p.M / GB_BM) * (p.N / GB_BN)), (unsigned)p.splits);
+  const dim3 grid((unsigned)(((p.M + GB_BM - 1) / GB_BM) * ((p.N + GB_BN - 1) / GB_BN)), (unsigned)p.splits);
   gemm_big_kernel<AT, BT, OUT32, BK, NST><<<grid, 512, C::LDS, s>>>(p);
 }
 
@@ -395,8 +396,11 @@ void launch_big(BigGemmArgs p, int kdim, hipStream_t s) {
 
 }  // namespace
 
+// Exact 256-multiples, or large ragged dimensions (>= 2048: the MLM decoder's
+// 30,528-wide vocabulary) whose partial edge tile is a small fraction of the work.
 bool gemm_big_ok(int M, int N, int K) {
-  return M > 0 && N > 0 && K > 0 && M % GB_BM == 0 && N % GB_BN == 0 && K % GB_KQ == 0 &&
+  auto dim_ok = [](int d) { return d % GB_BM == 0 || (d >= 2048 && d % 8 == 0); };
+  return M > 0 && N > 0 && K > 0 && dim_ok(M) && dim_ok(N) && K % GB_KQ == 0 &&
          (int64_t)M * K * 2 < (1LL << 32) && (int64_t)N * K * 2 < (1LL << 32) &&
          (int64_t)M * N * 2 < (1LL << 32);
 }
@@ -455,7 +459,7 @@ void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int
 // floor(256 / tiles) slices.  > 1 means the kernel ADDS into dw (the caller
 // zeroes dw unless accumulating).
 int gemm_big_wgrad_splits(int M, int N, int K) {
-  const int tiles = (N / GB_BM) * (K / GB_BN);
+  const int tiles = ((N + GB_BM - 1) / GB_BM) * ((K + GB_BN - 1) / GB_BN);
   const int nk = M / GB_KQ;
   return std::max(1, std::min(256 / std::max(1, tiles), nk / 16));
 }

@@ -6,7 +6,8 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(512, 768, 768), (1024, 3072, 768), (512, 768, 3072), (256, 2304, 768)]
+SHAPES = [(512, 768, 768), (1024, 3072, 768), (512, 768, 3072), (256, 2304, 768),
+          (2560, 2112, 768)]  # ragged N (the MLM decoder's vocabulary is 30,528 wide)
 
 
 def _ops():
