@@ -95,11 +95,24 @@ template <bool RES, bool RELU>
 __global__ __launch_bounds__(256) void bn_apply_kernel(BnFwdArgs a, int64_t nvec) {
   extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
   const int C = a.C;
+  const uint4* X = reinterpret_cast<const uint4*>(a.x);
+  const uint4* R = reinterpret_cast<const uint4*>(a.residual);
+  // The first vectors go out before the per-channel prologue: its acc loads
+  // and fp64 math then overlap the activation loads instead of preceding them
+  // (at ResNet-18 sizes every thread handles one or two vectors).
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint4 xv = {0, 0, 0, 0}, rv = {0, 0, 0, 0};
+  if (i < nvec) {
+    xv = X[i];
+    if (RES) rv = R[i];
+  }
+  const double inv_m = 1.0 / (double)a.M;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     double mu, var;
     if (a.train) {
-      mu = a.acc[c] / (double)a.M;
-      var = a.acc[C + c] / (double)a.M - mu * mu;
+      mu = a.acc[c] * inv_m;
+      var = a.acc[C + c] * inv_m - mu * mu;
       if (var < 0.0) var = 0.0;
     } else {
       mu = a.run_mean[c];
@@ -122,13 +135,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(BnFwdArgs a, int64_t nvec
   }
   __syncthreads();
   const int tpr = C / 8;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+  for (; i < nvec; i += stride) {
+    const uint4 xc = xv, rc = rv;
+    if (i + stride < nvec) {  // one vector of prefetch
+      xv = X[i + stride];
+      if (RES) rv = R[i + stride];
+    }
     const int cg = (int)(i % tpr);
     float f[8];
-    unpack8(reinterpret_cast<const uint4*>(a.x)[i], f);
+    unpack8(xc, f);
     float r[8];
-    if (RES) unpack8(reinterpret_cast<const uint4*>(a.residual)[i], r);
+    if (RES) unpack8(rc, r);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float v = f[k] * coef[cg * 8 + k] + coef[C + cg * 8 + k];
@@ -205,11 +222,24 @@ template <bool MASK, bool WRITE_DYM>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a, int64_t nvec) {
   extern __shared__ __attribute__((aligned(16))) float sc[];  // [5][C]: k1,k2,k3,mean,invstd
   const int C = a.C;
+  const uint4* DY = reinterpret_cast<const uint4*>(a.dy);
+  const uint4* X = reinterpret_cast<const uint4*>(a.x);
+  const uint4* Y = reinterpret_cast<const uint4*>(a.y);
+  // first vectors in flight across the prologue (see bn_apply_kernel)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint4 gv = {0, 0, 0, 0}, xv = {0, 0, 0, 0}, yv = {0, 0, 0, 0};
+  if (i < nvec) {
+    gv = DY[i];
+    xv = X[i];
+    if (MASK) yv = Y[i];
+  }
+  const double inv_m = 1.0 / (double)a.M;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const double s = a.acc[c], q = a.acc[C + c];
     sc[c] = a.gamma[c] * a.invstd[c];
-    sc[C + c] = (float)(s / (double)a.M);
-    sc[2 * C + c] = (float)(q / (double)a.M);
+    sc[C + c] = (float)(s * inv_m);
+    sc[2 * C + c] = (float)(q * inv_m);
     sc[3 * C + c] = a.mean[c];
     sc[4 * C + c] = a.invstd[c];
     if (blockIdx.x == 0) {
@@ -219,24 +249,29 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a, int64_t 
   }
   __syncthreads();
   const int tpr = C / 8;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+  for (; i < nvec; i += stride) {
+    const uint4 gc = gv, xc = xv, yc = yv;
+    if (i + stride < nvec) {
+      gv = DY[i + stride];
+      xv = X[i + stride];
+      if (MASK) yv = Y[i + stride];
+    }
     const int cb = (int)(i % tpr) * 8;
-    float g[8], xv[8];
-    unpack8(reinterpret_cast<const uint4*>(a.dy)[i], g);
-    unpack8(reinterpret_cast<const uint4*>(a.x)[i], xv);
+    float g[8], xf[8];
+    unpack8(gc, g);
+    unpack8(xc, xf);
     if (MASK) {
-      float yv[8];
-      unpack8(reinterpret_cast<const uint4*>(a.y)[i], yv);
+      float yf[8];
+      unpack8(yc, yf);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+      for (int k = 0; k < 8; ++k) g[k] = yf[k] > 0.f ? g[k] : 0.f;
       if (WRITE_DYM) reinterpret_cast<uint4*>(a.dy_masked)[i] = pack8(g);
     }
     float o[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int c = cb + k;
-      const float xh = (xv[k] - sc[3 * C + c]) * sc[4 * C + c];
+      const float xh = (xf[k] - sc[3 * C + c]) * sc[4 * C + c];
       o[k] = sc[c] * (g[k] - sc[C + c] - xh * sc[2 * C + c]);
     }
     reinterpret_cast<uint4*>(a.dx)[i] = pack8(o);

@@ -112,122 +112,13 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool AT, bool BT, bool OUT32, int BK, int NST>
-__global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
-  using C = GbCfg<BK, NST>;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int t = threadIdx.x;
-  const int lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  // XCD-aware bijective remap (guide §5: 'XCD swizzle must be bijective'):
-  // consecutive tile ids -- same A row panel, N fastest -- share an XCD.
-  // blockIdx.y = split-K slice (wgrad: the long M reduction over few output tiles)
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int tiles_n = (p.N + GB_BN - 1) / GB_BN;  // ragged last tile: reads OOB-zero / skipped stores
-  const int m0 = (wgid / tiles_n) * GB_BM;
-  const int n0 = (wgid - (wgid / tiles_n) * tiles_n) * GB_BN;
-  const auto rsA = make_rsrc(p.a, p.a_bytes);
-  const auto rsB = make_rsrc(p.b, p.b_bytes);
-  const int kt0 = blockIdx.y * p.kt_per_split;
-  const int nk = min(p.K / BK - kt0, p.kt_per_split);
-  if (nk <= 0) return;  // block-uniform: an empty trailing slice
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto issue = [&](int kt, int stage) {
-    if (p.dbg & 2) return;
-    uint8_t* st = smem + stage * C::STAGE;
-    stage_operand<AT, BK>(rsA, p.lda, m0, (kt0 + kt) * BK, st, wave, lane);
-    stage_operand<BT, BK>(rsB, p.ldb, n0, (kt0 + kt) * BK, st + C::TILE, wave, lane);
-  };
-  auto compute = [&](int stage) {
-    if (p.dbg & 1) return;
-    const uint8_t* As = smem + stage * C::STAGE;
-    const uint8_t* Bs = As + C::TILE;
-    if constexpr (kGbPinOrder && BK == 64 && !AT && !BT) {
-      // Both 32-deep slices' fragments (24 reads) go out before the first
-      // MFMA, so slice 1's LDS latency hides under slice 0's 32 MFMAs.
-      bf16x8 b0[4], a0[8], b1[4], a1[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b0[j] = frag<BT, BK>(Bs, 0, wn * 64 + 16 * j, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a0[i] = frag<AT, BK>(As, 0, wm * 128 + 16 * i, lane);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b1[j] = frag<BT, BK>(Bs, 32, wn * 64 + 16 * j, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a1[i] = frag<AT, BK>(As, 32, wm * 128 + 16 * i, lane);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
-      __builtin_amdgcn_sched_barrier(0);
-      return;
-    }
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 32) {
-      bf16x8 bfr[4], af[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag<BT, BK>(Bs, kk, wn * 64 + 16 * j, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = frag<AT, BK>(As, kk, wm * 128 + 16 * i, lane);
-      // transposing reads go through asm (lds_tiles.h): wait for them explicitly
-      if constexpr (AT) frags_ready(af);
-      if constexpr (BT) frags_ready(bfr);
-      // Pin the order: all 12 fragment reads in flight together, then the 32
-      // MFMAs.  Left alone, hipcc interleaves read -> lgkmcnt(0) -> 4 MFMAs
-      // eight times per slice (register-pressure heuristic), exposing eight
-      // LDS latencies per 512 MFMA cycles.
-      if constexpr (kGbPinOrder) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-      if constexpr (kGbPinOrder) __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  // NST-stage ring, NST-1 tiles in flight; per tile each thread issues
-  // L = 2 * DMA LDS-DMA instructions (counted by vmcnt, hand-waited).
-  constexpr int D = NST - 1, L = 2 * C::DMA;
-#pragma unroll
-  for (int u = 0; u < D; ++u)
-    if (u < nk) issue(u, u);
-  int stage = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int younger = min(D - 1, nk - 1 - kt);  // tiles after kt still allowed in flight
-    if constexpr (D >= 3) {
-      if (younger >= 2) wait_vm<2 * L>();
-      else if (younger == 1) wait_vm<L>();
-      else wait_vm<0>();
-    } else if constexpr (D == 2) {
-      if (younger >= 1) wait_vm<L>();
-      else wait_vm<0>();
-    } else {
-      wait_vm<0>();
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own reads of the recycled stage retired
-    lds_barrier();  // everyone's tile kt landed; everyone done reading stage (kt-1)%NST
-    if (kt + D < nk) issue(kt + D, stage == 0 ? NST - 1 : stage - 1);
-    compute(stage);
-    stage = stage == NST - 1 ? 0 : stage + 1;
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  lds_barrier();  // the ring is free for the epilogue staging
-
+// Output stage shared by both pipelines: split-K fp32 atomics straight from
+// the accumulators, or per wave 4 chunks of 32 rows x 64 cols through LDS
+// (the operand ring must be drained) with the fused bias / residual / GELU /
+// GELU-backward / column-sum options.
+template <bool OUT32>
+__device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[8][4], uint8_t* smem, int m0,
+                                             int n0, int wm, int wn, int wave, int lane) {
   if constexpr (OUT32) {
     if (p.splits > 1) {
       // split-K: fp32 atomics straight from the accumulators (16 lanes cover
@@ -354,6 +245,327 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
 }
 
 template <bool AT, bool BT, bool OUT32, int BK, int NST>
+__global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
+  using C = GbCfg<BK, NST>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  // XCD-aware bijective remap (guide §5: 'XCD swizzle must be bijective'):
+  // consecutive tile ids -- same A row panel, N fastest -- share an XCD.
+  // blockIdx.y = split-K slice (wgrad: the long M reduction over few output tiles)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int tiles_n = (p.N + GB_BN - 1) / GB_BN;  // ragged last tile: reads OOB-zero / skipped stores
+  const int m0 = (wgid / tiles_n) * GB_BM;
+  const int n0 = (wgid - (wgid / tiles_n) * tiles_n) * GB_BN;
+  const auto rsA = make_rsrc(p.a, p.a_bytes);
+  const auto rsB = make_rsrc(p.b, p.b_bytes);
+  const int kt0 = blockIdx.y * p.kt_per_split;
+  const int nk = min(p.K / BK - kt0, p.kt_per_split);
+  if (nk <= 0) return;  // block-uniform: an empty trailing slice
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int kt, int stage) {
+    if (p.dbg & 2) return;
+    uint8_t* st = smem + stage * C::STAGE;
+    stage_operand<AT, BK>(rsA, p.lda, m0, (kt0 + kt) * BK, st, wave, lane);
+    stage_operand<BT, BK>(rsB, p.ldb, n0, (kt0 + kt) * BK, st + C::TILE, wave, lane);
+  };
+  auto compute = [&](int stage) {
+    if (p.dbg & 1) return;
+    const uint8_t* As = smem + stage * C::STAGE;
+    const uint8_t* Bs = As + C::TILE;
+    if constexpr (kGbPinOrder && BK == 64 && !AT && !BT) {
+      // Both 32-deep slices' fragments (24 reads) go out before the first
+      // MFMA, so slice 1's LDS latency hides under slice 0's 32 MFMAs.
+      bf16x8 b0[4], a0[8], b1[4], a1[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b0[j] = frag<BT, BK>(Bs, 0, wn * 64 + 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a0[i] = frag<AT, BK>(As, 0, wm * 128 + 16 * i, lane);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b1[j] = frag<BT, BK>(Bs, 32, wn * 64 + 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a1[i] = frag<AT, BK>(As, 32, wm * 128 + 16 * i, lane);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 bfr[4], af[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<BT, BK>(Bs, kk, wn * 64 + 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = frag<AT, BK>(As, kk, wm * 128 + 16 * i, lane);
+      // transposing reads go through asm (lds_tiles.h): wait for them explicitly
+      if constexpr (AT) frags_ready(af);
+      if constexpr (BT) frags_ready(bfr);
+      // Pin the order: all 12 fragment reads in flight together, then the 32
+      // MFMAs.  Left alone, hipcc interleaves read -> lgkmcnt(0) -> 4 MFMAs
+      // eight times per slice (register-pressure heuristic), exposing eight
+      // LDS latencies per 512 MFMA cycles.
+      if constexpr (kGbPinOrder) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      if constexpr (kGbPinOrder) __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // NST-stage ring, NST-1 tiles in flight; per tile each thread issues
+  // L = 2 * DMA LDS-DMA instructions (counted by vmcnt, hand-waited).
+  constexpr int D = NST - 1, L = 2 * C::DMA;
+#pragma unroll
+  for (int u = 0; u < D; ++u)
+    if (u < nk) issue(u, u);
+  int stage = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int younger = min(D - 1, nk - 1 - kt);  // tiles after kt still allowed in flight
+    if constexpr (D >= 3) {
+      if (younger >= 2) wait_vm<2 * L>();
+      else if (younger == 1) wait_vm<L>();
+      else wait_vm<0>();
+    } else if constexpr (D == 2) {
+      if (younger >= 1) wait_vm<L>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own reads of the recycled stage retired
+    lds_barrier();  // everyone's tile kt landed; everyone done reading stage (kt-1)%NST
+    if (kt + D < nk) issue(kt + D, stage == 0 ? NST - 1 : stage - 1);
+    compute(stage);
+    stage = stage == NST - 1 ? 0 : stage + 1;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  lds_barrier();  // the ring is free for the epilogue staging
+
+  big_epilogue<OUT32>(p, acc, smem, m0, n0, wm, wn, wave, lane);
+}
+
+// ---- ping-pong pipeline (MFL_GB_PIPE=2) ---------------------------------------
+// The same 256x256 tile and wave layout, scheduled after the guide's 256^2
+// 8-phase template (cdna_hip_programming.md §5): each k-tile is split into 4
+// half-tiles of 16 KiB -- A rows {0-63, 128-191} (A0), B cols {64w + 0-31}
+// (B0), B cols {64w + 32-63} (B1), A rows {64-127, 192-255} (A1) -- and
+// computed in 4 phases, one 64x32 quadrant of every wave's 128x64 output per
+// phase: (mi, ni) = (0,0) (0,1) (1,1) (1,0), fragment reads 12 / 4 / 8 / 0.
+// A phase is a LOAD section (this phase's fragment reads, ONE half-tile of
+// LDS-DMA, vmcnt) and an MFMA section (16 MFMAs), each closed by a barrier.
+// Wave rows 0 and 1 share every SIMD (waves w, w + 4) and run one barrier
+// apart, so one wave's MFMAs always overlap the other's loads.
+//
+// Hazards (phase index f, one barrier per section, rows staggered by one):
+//  * RAW: the half-tile issued in phase f is retired by vmcnt(8) (4 younger
+//    half-tiles in flight) in phase f + 4 and read from phase f + 5 on --
+//    every wave's wait precedes a barrier every reader passes before reading.
+//  * WAR: a half-tile read in phase f is restaged no earlier than f + 2
+//    (both rows' reads have retired by then).
+//  Issue order (steady state): phase 4t+0 -> B1(t+1), 4t+1 -> A1(t+1),
+//  4t+2 -> A0(t+2), 4t+3 -> B0(t+2); read: A0, B0 at 4t, B1 at 4t+1, A1 at
+//  4t+2.  Half-tiles past the slice's last k-tile load out-of-range zeros so
+//  the vmcnt count is the same in every phase.
+constexpr int PP_HALF = 128 * 64 * 2;  // one half-tile, bytes
+
+// local row l (0..127) of a half-tile -> row of the 256-row operand tile
+template <bool ISB>
+__device__ __forceinline__ int pp_row(int l, int sub) {
+  return ISB ? (l >> 5) * 64 + sub * 32 + (l & 31) : (l >> 6) * 128 + sub * 64 + (l & 63);
+}
+
+template <bool T, bool ISB>
+__device__ __forceinline__ void pp_stage(__amdgpu_buffer_rsrc_t rs, int ld, int row0, int k0, int sub,
+                                         uint8_t* dst, int wave, int lane, bool valid) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = wave + 8 * u;  // 1-KiB instruction index within the half-tile
+    uint32_t off;
+    if constexpr (!T) {
+      // [row][k]: 8 rows of 128 B per instruction
+      const int l = 8 * i + (lane >> 3);
+      const int lc = (lane & 7) ^ swz_b128<128>(l);
+      off = (uint32_t)((row0 + pp_row<ISB>(l, sub)) * ld + k0 + 8 * lc) * 2u;
+    } else {
+      // [k][row]: 4 k-rows of 256 B (128 local rows) per instruction
+      const int kr = 4 * i + (lane >> 4);
+      const int lc = (lane & 15) ^ swz_tr<256>(kr);
+      off = (uint32_t)((k0 + kr) * ld + row0 + pp_row<ISB>(8 * lc, sub)) * 2u;
+    }
+    dma16(rs, valid ? off : kOOB, dst + i * 1024);
+  }
+}
+
+template <bool T>
+__device__ __forceinline__ bf16x8 pp_frag(const uint8_t* half, int kk, int r0, int lane) {
+  if constexpr (T) return tr_frag<256>(half, kk, r0, lane);
+  else return b128_frag<128>(half, kk, r0, lane);
+}
+
+template <bool AT, bool BT, bool OUT32>
+__global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int tiles_n = (p.N + GB_BN - 1) / GB_BN;
+  const int m0 = (wgid / tiles_n) * GB_BM;
+  const int n0 = (wgid - (wgid / tiles_n) * tiles_n) * GB_BN;
+  const auto rsA = make_rsrc(p.a, p.a_bytes);
+  const auto rsB = make_rsrc(p.b, p.b_bytes);
+  const int kt0 = blockIdx.y * p.kt_per_split;
+  const int nk = min(p.K / 64 - kt0, p.kt_per_split);
+  if (nk <= 0) return;  // block-uniform
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bfr[2][2][2];
+
+  // half-tile h (0 A0, 1 B0, 2 B1, 3 A1) of k-tile kt into ring slot kt & 1
+  auto stage = [&](int h, int kt) {
+    if (p.dbg & 2) return;
+    uint8_t* dst = smem + ((kt & 1) * 4 + h) * PP_HALF;
+    const bool v = kt < nk;
+    const int k0 = (kt0 + (v ? kt : 0)) * 64;
+    if (h == 0 || h == 3) pp_stage<AT, false>(rsA, p.lda, m0, k0, h == 3, dst, wave, lane, v);
+    else pp_stage<BT, true>(rsB, p.ldb, n0, k0, h - 1, dst, wave, lane, v);
+  };
+  auto read_a = [&](int kt, int mi) {
+    const uint8_t* h = smem + ((kt & 1) * 4 + (mi ? 3 : 0)) * PP_HALF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = pp_frag<AT>(h, 32 * ks, wm * 64 + 16 * i, lane);
+  };
+  auto read_b = [&](int kt, int ni) {
+    const uint8_t* h = smem + ((kt & 1) * 4 + 1 + ni) * PP_HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bfr[ni][j][ks] = pp_frag<BT>(h, 32 * ks, wn * 32 + 16 * j, lane);
+  };
+  auto mfma_quadrant = [&](int mi, int ni) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          acc[4 * mi + i][2 * ni + j] = mfma16(af[i][ks], bfr[ni][j][ks], acc[4 * mi + i][2 * ni + j]);
+  };
+  // the transposing reads are inline asm: retire them and pin their registers
+  auto frags_in = [&](bool a_read, int ni) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (a_read) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) asm volatile("" : "+v"(af[i][ks]));
+    }
+    if (ni >= 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) asm volatile("" : "+v"(bfr[ni][j][ks]));
+    }
+  };
+  auto mfma_section = [&](int mi, int ni) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    if (!(p.dbg & 1)) mfma_quadrant(mi, ni);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_barrier();
+  };
+
+  // prologue: the half-tiles of phases -6 .. -1, then A0(0) / B0(0) retired
+  stage(0, 0);
+  stage(1, 0);
+  stage(2, 0);
+  stage(3, 0);
+  stage(0, 1);
+  stage(1, 1);
+  wait_vm<8>();
+  lds_barrier();
+  if (wm == 1) lds_barrier();  // row 1 runs one barrier behind row 0
+
+  for (int kt = 0; kt < nk; ++kt) {
+    // phase 0: quadrant (0,0)
+    read_b(kt, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(kt, 0);
+    stage(2, kt + 1);
+    wait_vm<8>();
+    lds_barrier();
+    frags_in(true, 0);
+    mfma_section(0, 0);
+    // phase 1: quadrant (0,1)
+    read_b(kt, 1);
+    stage(3, kt + 1);
+    wait_vm<8>();
+    lds_barrier();
+    frags_in(false, 1);
+    mfma_section(0, 1);
+    // phase 2: quadrant (1,1)
+    read_a(kt, 1);
+    stage(0, kt + 2);
+    wait_vm<8>();
+    lds_barrier();
+    frags_in(true, -1);
+    mfma_section(1, 1);
+    // phase 3: quadrant (1,0), fragments already in registers
+    stage(1, kt + 2);
+    wait_vm<8>();
+    lds_barrier();
+    mfma_section(1, 0);
+  }
+  if (wm == 0) lds_barrier();  // rebalance the barrier count
+  wait_vm<0>();                // trailing out-of-range half-tiles land before the LDS is reused
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  lds_barrier();
+  big_epilogue<OUT32>(p, acc, smem, m0, n0, wm, wn, wave, lane);
+}
+
+template <bool AT, bool BT, bool OUT32>
+void launch_pp_t(const BigGemmArgs& p, hipStream_t s) {
+  constexpr size_t kLds = 8 * (size_t)PP_HALF;  // 2 k-tiles x 4 half-tiles = 128 KiB
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<AT, BT, OUT32>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
+    attr = true;
+  }
+  const dim3 grid((unsigned)(((p.M + GB_BM - 1) / GB_BM) * ((p.N + GB_BN - 1) / GB_BN)), (unsigned)p.splits);
+  gemm_pp_kernel<AT, BT, OUT32><<<grid, 512, kLds, s>>>(p);
+}
+
+template <bool AT, bool BT, bool OUT32, int BK, int NST>
 void launch_big_t(const BigGemmArgs& p, hipStream_t s) {
   using C = GbCfg<BK, NST>;
   static bool attr = false;
@@ -366,15 +578,16 @@ void launch_big_t(const BigGemmArgs& p, hipStream_t s) {
   gemm_big_kernel<AT, BT, OUT32, BK, NST><<<grid, 512, C::LDS, s>>>(p);
 }
 
-// pipeline variant: 0 = BK 64 / 2 stages (default), 1 = BK 32 / 4 stages (env
-// MFL_GB_PIPE).  Measured on the BERT shapes (scripts/gemm_sweep.sh): equal
-// forward time, BK 64 8-25 % faster on dgrad / wgrad -- the k-loop is not
-// DMA-latency bound at 256x256; its bubbles are the per-k-step barrier and
-// the per-tile epilogue.
+// pipeline variant (env MFL_GB_PIPE): 2 = the ping-pong half-tile schedule
+// (default), 0 = BK 64 / 2-stage ring, one barrier per k-step, 1 = BK 32 /
+// 4 stages.  Measured on the BERT shapes (scripts/gemm_sweep.sh,
+// profiles/bert/gemm_sweep_pp.log): 2 is 3-12 % faster than 0 on every
+// fwd / dgrad / wgrad shape (ffn2 fwd 988 -> 1037 TFLOP/s on 192 of 256 CUs);
+// 1 ties 0 on forward and loses 8-25 % on dgrad / wgrad.
 int gb_pipe() {
   static const int v = [] {
     const char* e = getenv("MFL_GB_PIPE");
-    return e && *e ? atoi(e) : 0;
+    return e && *e ? atoi(e) : 2;
   }();
   return v;
 }
@@ -390,7 +603,8 @@ void launch_big(BigGemmArgs p, int kdim, hipStream_t s) {
   // p.kt_per_split arrives in units of GB_KQ (64) k-elements
   p.kt_per_split *= GB_KQ / bk;
   (void)kdim;
-  if (bk == 32) launch_big_t<AT, BT, OUT32, 32, 4>(p, s);
+  if (gb_pipe() == 2) launch_pp_t<AT, BT, OUT32>(p, s);
+  else if (bk == 32) launch_big_t<AT, BT, OUT32, 32, 4>(p, s);
   else launch_big_t<AT, BT, OUT32, 64, 2>(p, s);
 }
 
