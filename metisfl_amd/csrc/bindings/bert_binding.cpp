@@ -80,10 +80,15 @@ void gemm_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t M, 
   need(x, torch::kBFloat16, M * K, "x");
   need(dy, torch::kBFloat16, M * N, "dy");
   need(dw, torch::kFloat32, N * K, "dw");
-  if (!accumulate && !zeroed && mfl::gemm_wgrad_splits((int)M, (int)N, (int)K))
+  // split-K slabs from the caching allocator: stream-ordered, and legal inside
+  // graph capture (the block comes from the capture's private pool)
+  const int64_t ws_n = mfl::gemm_wgrad_workspace((int)M, (int)N, (int)K);
+  torch::Tensor ws;
+  if (ws_n > 0) ws = torch::empty({ws_n}, dw.options());
+  else if (!accumulate && !zeroed && mfl::gemm_wgrad_splits((int)M, (int)N, (int)K))
     (void)hipMemsetAsync(dw.data_ptr<float>(), 0, dw.numel() * sizeof(float), stream_of(x));
   mfl::launch_gemm_wgrad(bfp(x), bfp(dy), dw.data_ptr<float>(), (int)M, (int)N, (int)K, accumulate,
-                         stream_of(x));
+                         stream_of(x), ws_n > 0 ? ws.data_ptr<float>() : nullptr);
 }
 
 void ln_dims(int64_t H) {

@@ -25,9 +25,13 @@ void launch_gemm_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int 
                        bool accumulate, hipStream_t s);
 //   dw = dy^T x, or dw += with accumulate (fp32 atomics; split-K plans always
 //   add, so dw must be zero on entry unless accumulating on purpose)
+//   ws: optional split-K slab workspace of gemm_wgrad_workspace(M, N, K) fp32
+//   elements -- the slices store partials and one reduce launch sums them
+//   (then dw needs no zeroing); without it split plans add with atomics
 void launch_gemm_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,
-                       bool accumulate, hipStream_t s);
+                       bool accumulate, hipStream_t s, float* ws = nullptr);
 bool gemm_wgrad_splits(int M, int N, int K);
+int64_t gemm_wgrad_workspace(int M, int N, int K);
 
 // Large-tile path (gemm_big.hip): 256x256 tiles, exact-tiling shapes only.
 bool gemm_big_ok(int M, int N, int K);
@@ -36,8 +40,9 @@ void launch_gemm_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
 void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
                            bool accumulate, hipStream_t s);
 void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,
-                           bool accumulate, hipStream_t s);
+                           bool accumulate, hipStream_t s, float* ws = nullptr);
 int gemm_big_wgrad_splits(int M, int N, int K);
+int64_t gemm_big_wgrad_workspace(int M, int N, int K);
 void launch_gemm_big_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t* dz, const uint16_t* z,
                                 float* dbias, int M, int N, int K, hipStream_t s);
 // dz[M][K] = (dy W) * gelu'(z) (exact erf), dbias[K] += column sums of dz:

@@ -95,13 +95,17 @@ void launch_gemm_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t* dz,
 }
 
 void launch_gemm_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,
-                       bool accumulate, hipStream_t s) {
+                       bool accumulate, hipStream_t s, float* ws) {
   if (gemm_big_enabled() && gemm_big_ok(N, K, M)) {
-    launch_gemm_big_wgrad(x, dy, dw, M, N, K, accumulate, s);
+    launch_gemm_big_wgrad(x, dy, dw, M, N, K, accumulate, s, ws);
     return;
   }
   const ConvGeom g = dense_geom(M, N, K);
   launch_conv_wgrad(g, plan_conv_wgrad(g), x, dy, dw, s, accumulate);
+}
+
+int64_t gemm_wgrad_workspace(int M, int N, int K) {
+  return (gemm_big_enabled() && gemm_big_ok(N, K, M)) ? gemm_big_wgrad_workspace(M, N, K) : 0;
 }
 
 bool gemm_wgrad_splits(int M, int N, int K) {

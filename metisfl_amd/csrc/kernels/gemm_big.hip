@@ -42,6 +42,7 @@ struct BigGemmArgs {
   uint32_t a_bytes, b_bytes;
   uint16_t* c16;         // bf16 output (forward / dgrad)
   float* c32;            // fp32 output (wgrad)
+  float* ws;             // split-K partial slabs [splits][M][ldc] (ping-pong kernel), else fp32 atomics
   int ldc;
   const float* bias;     // [N]
   const uint16_t* resid; // [M][ldc]
@@ -49,7 +50,7 @@ struct BigGemmArgs {
   int accum;
   int splits;            // split-K slices (fp32 output only; atomics into c32)
   int kt_per_split;      // k-tiles per slice
-  int dbg;               // timing experiments (MFL_GB_DEBUG): bit0 skip MFMAs, bit1 skip operand DMA
+  int dbg;               // timing experiments (MFL_GB_DEBUG): bit0 skip MFMAs, bit1 skip operand DMA, bit2 skip the output stage (ping-pong kernel)
   // dgrad epilogue fusion of the GELU backward (bf16 output only):
   //   out = bf16(acc * gelu'(z)),  colsum[col] += sum over rows of out
   const uint16_t* gelu_z;
@@ -115,10 +116,12 @@ __device__ __forceinline__ void wait_vm() {
 // Output stage shared by both pipelines: split-K fp32 atomics straight from
 // the accumulators, or per wave 4 chunks of 32 rows x 64 cols through LDS
 // (the operand ring must be drained) with the fused bias / residual / GELU /
-// GELU-backward / column-sum options.
-template <bool OUT32>
+// GELU-backward / column-sum options.  WN = columns per wave (64, or 48 for
+// the 256x192 tile); the column-sum option needs WN = 64.
+template <bool OUT32, int WN = 64>
 __device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[8][4], uint8_t* smem, int m0,
                                              int n0, int wm, int wn, int wave, int lane) {
+  constexpr int NJ = WN / 16, CG = WN / 8, NU = 32 * CG / 64;
   if constexpr (OUT32) {
     if (p.splits > 1) {
       // split-K: fp32 atomics straight from the accumulators (16 lanes cover
@@ -127,11 +130,11 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int row = m0 + wm * 128 + 16 * i + 4 * fq + e;
-            const int col = n0 + wn * 64 + 16 * j + fr;
+            const int col = n0 + wn * WN + 16 * j + fr;
             if (row < p.M && col < p.N) atomicAdd(p.c32 + (int64_t)row * p.ldc + col, acc[i][j][e]);
           }
       return;
@@ -149,21 +152,21 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           W[(16 * i2 + 4 * fq + e) * GB_EPI_LD + 16 * j + fr] = acc[2 * c + i2][j][e];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < NU; ++u) {
       const int item = lane + 64 * u;
-      const int rl = item >> 3, cg = item & 7;
+      const int rl = item / CG, cg = item - rl * CG;
       const float4 lo = *reinterpret_cast<const float4*>(W + rl * GB_EPI_LD + cg * 8);
       const float4 hi = *reinterpret_cast<const float4*>(W + rl * GB_EPI_LD + cg * 8 + 4);
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       const int row = m0 + wm * 128 + 32 * c + rl;
-      const int col = n0 + wn * 64 + cg * 8;
+      const int col = n0 + wn * WN + cg * 8;
       if (row >= p.M || col >= p.N) continue;  // ragged edge tiles (N % 8 == 0)
       const int64_t off = (int64_t)row * p.ldc + col;
       if constexpr (OUT32) {
@@ -224,7 +227,7 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();  // reads of this chunk done before the next overwrites W
   }
-  if constexpr (!OUT32) {
+  if constexpr (!OUT32 && WN == 64) {
     if (p.colsum) {
       // lanes sharing lane & 7 hold the same 8 columns: butterfly over lane >> 3
 #pragma unroll
@@ -387,42 +390,62 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
 //  the vmcnt count is the same in every phase.
 constexpr int PP_HALF = 128 * 64 * 2;  // one half-tile, bytes
 
-// local row l (0..127) of a half-tile -> row of the 256-row operand tile
-template <bool ISB>
-__device__ __forceinline__ int pp_row(int l, int sub) {
-  return ISB ? (l >> 5) * 64 + sub * 32 + (l & 31) : (l >> 6) * 128 + sub * 64 + (l & 63);
-}
+// Tile width: 256 (BW = 64 columns per wave) or 192 (BW = 48: the B1
+// half-tile then holds 4 x 16 columns, 8 KiB, one DMA instruction per wave --
+// N = 768 / 2304 tile into 256 / 768 workgroups instead of 192 / 576).
+// Half-tile rows: HR(sub) local rows; local row l -> operand-tile row.
+template <bool ISB, int BW>
+struct PpHalf {
+  static constexpr int W1 = ISB ? BW - 32 : 64;             // rows per wave column in half `sub`
+  static __device__ __forceinline__ int rows(int sub) { return ISB ? 4 * (sub ? W1 : 32) : 128; }
+  static __device__ __forceinline__ int map(int l, int sub) {
+    if constexpr (!ISB) return (l >> 6) * 128 + sub * 64 + (l & 63);
+    else return sub ? (l / W1) * BW + 32 + (l % W1) : (l >> 5) * BW + (l & 31);
+  }
+};
 
-template <bool T, bool ISB>
+// NR local rows (128, or 64 for a 192-wide B1) x 64 k, 16 B per lane per DMA
+// instruction, NR * 128 / 1024 instructions spread over the 8 waves.
+template <bool T, bool ISB, int BW, int NR>
 __device__ __forceinline__ void pp_stage(__amdgpu_buffer_rsrc_t rs, int ld, int row0, int k0, int sub,
                                          uint8_t* dst, int wave, int lane, bool valid) {
+  constexpr int NI = NR * 128 / 1024 / 8;  // instructions per wave
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < NI; ++u) {
     const int i = wave + 8 * u;  // 1-KiB instruction index within the half-tile
     uint32_t off;
     if constexpr (!T) {
       // [row][k]: 8 rows of 128 B per instruction
       const int l = 8 * i + (lane >> 3);
       const int lc = (lane & 7) ^ swz_b128<128>(l);
-      off = (uint32_t)((row0 + pp_row<ISB>(l, sub)) * ld + k0 + 8 * lc) * 2u;
-    } else {
-      // [k][row]: 4 k-rows of 256 B (128 local rows) per instruction
+      off = (uint32_t)((row0 + PpHalf<ISB, BW>::map(l, sub)) * ld + k0 + 8 * lc) * 2u;
+    } else if constexpr (NR == 128) {
+      // [k][row]: 4 k-rows of 256 B per instruction
       const int kr = 4 * i + (lane >> 4);
       const int lc = (lane & 15) ^ swz_tr<256>(kr);
-      off = (uint32_t)((k0 + kr) * ld + row0 + pp_row<ISB>(8 * lc, sub)) * 2u;
+      off = (uint32_t)((k0 + kr) * ld + row0 + PpHalf<ISB, BW>::map(8 * lc, sub)) * 2u;
+    } else {
+      // [k][row]: 8 k-rows of 128 B per instruction
+      const int kr = 8 * i + (lane >> 3);
+      const int lc = (lane & 7) ^ swz_tr<128>(kr);
+      off = (uint32_t)((k0 + kr) * ld + row0 + PpHalf<ISB, BW>::map(8 * lc, sub)) * 2u;
     }
     dma16(rs, valid ? off : kOOB, dst + i * 1024);
   }
 }
 
-template <bool T>
+template <bool T, int NR = 128>
 __device__ __forceinline__ bf16x8 pp_frag(const uint8_t* half, int kk, int r0, int lane) {
-  if constexpr (T) return tr_frag<256>(half, kk, r0, lane);
+  if constexpr (T) return tr_frag<2 * NR>(half, kk, r0, lane);
   else return b128_frag<128>(half, kk, r0, lane);
 }
 
-template <bool AT, bool BT, bool OUT32>
+template <bool AT, bool BT, bool OUT32, int BN>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
+  constexpr int BW = BN / 4;            // columns per wave
+  constexpr int NJ1 = (BW - 32) / 16;   // 16-column tiles of a wave in the B1 half
+  constexpr int NR1 = 4 * (BW - 32);    // B1 half-tile rows
+  constexpr int VM = 6 + NR1 / 64;      // DMA instructions per wave per k-tile
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -431,9 +454,9 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int tiles_n = (p.N + GB_BN - 1) / GB_BN;
+  const int tiles_n = (p.N + BN - 1) / BN;
   const int m0 = (wgid / tiles_n) * GB_BM;
-  const int n0 = (wgid - (wgid / tiles_n) * tiles_n) * GB_BN;
+  const int n0 = (wgid - (wgid / tiles_n) * tiles_n) * BN;
   const auto rsA = make_rsrc(p.a, p.a_bytes);
   const auto rsB = make_rsrc(p.b, p.b_bytes);
   const int kt0 = blockIdx.y * p.kt_per_split;
@@ -453,8 +476,9 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
     uint8_t* dst = smem + ((kt & 1) * 4 + h) * PP_HALF;
     const bool v = kt < nk;
     const int k0 = (kt0 + (v ? kt : 0)) * 64;
-    if (h == 0 || h == 3) pp_stage<AT, false>(rsA, p.lda, m0, k0, h == 3, dst, wave, lane, v);
-    else pp_stage<BT, true>(rsB, p.ldb, n0, k0, h - 1, dst, wave, lane, v);
+    if (h == 0 || h == 3) pp_stage<AT, false, BW, 128>(rsA, p.lda, m0, k0, h == 3, dst, wave, lane, v);
+    else if (h == 1) pp_stage<BT, true, BW, 128>(rsB, p.ldb, n0, k0, 0, dst, wave, lane, v);
+    else pp_stage<BT, true, BW, NR1>(rsB, p.ldb, n0, k0, 1, dst, wave, lane, v);
   };
   auto read_a = [&](int kt, int mi) {
     const uint8_t* h = smem + ((kt & 1) * 4 + (mi ? 3 : 0)) * PP_HALF;
@@ -465,16 +489,24 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
   };
   auto read_b = [&](int kt, int ni) {
     const uint8_t* h = smem + ((kt & 1) * 4 + 1 + ni) * PP_HALF;
+    if (ni == 0) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bfr[ni][j][ks] = pp_frag<BT>(h, 32 * ks, wn * 32 + 16 * j, lane);
+        for (int ks = 0; ks < 2; ++ks) bfr[0][j][ks] = pp_frag<BT>(h, 32 * ks, wn * 32 + 16 * j, lane);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NJ1; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          bfr[1][j][ks] = pp_frag<BT, NR1>(h, 32 * ks, wn * (BW - 32) + 16 * j, lane);
+    }
   };
   auto mfma_quadrant = [&](int mi, int ni) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < (ni ? NJ1 : 2); ++j)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           acc[4 * mi + i][2 * ni + j] = mfma16(af[i][ks], bfr[ni][j][ks], acc[4 * mi + i][2 * ni + j]);
@@ -490,7 +522,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
     }
     if (ni >= 0) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < (ni ? NJ1 : 2); ++j)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) asm volatile("" : "+v"(bfr[ni][j][ks]));
     }
@@ -511,7 +543,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
   stage(3, 0);
   stage(0, 1);
   stage(1, 1);
-  wait_vm<8>();
+  wait_vm<VM>();
   lds_barrier();
   if (wm == 1) lds_barrier();  // row 1 runs one barrier behind row 0
 
@@ -521,27 +553,27 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
     __builtin_amdgcn_sched_barrier(0);
     read_a(kt, 0);
     stage(2, kt + 1);
-    wait_vm<8>();
+    wait_vm<VM>();
     lds_barrier();
     frags_in(true, 0);
     mfma_section(0, 0);
     // phase 1: quadrant (0,1)
     read_b(kt, 1);
     stage(3, kt + 1);
-    wait_vm<8>();
+    wait_vm<VM>();
     lds_barrier();
     frags_in(false, 1);
     mfma_section(0, 1);
     // phase 2: quadrant (1,1)
     read_a(kt, 1);
     stage(0, kt + 2);
-    wait_vm<8>();
+    wait_vm<VM>();
     lds_barrier();
     frags_in(true, -1);
     mfma_section(1, 1);
     // phase 3: quadrant (1,0), fragments already in registers
     stage(1, kt + 2);
-    wait_vm<8>();
+    wait_vm<VM>();
     lds_barrier();
     mfma_section(1, 0);
   }
@@ -549,20 +581,66 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
   wait_vm<0>();                // trailing out-of-range half-tiles land before the LDS is reused
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   lds_barrier();
-  big_epilogue<OUT32>(p, acc, smem, m0, n0, wm, wn, wave, lane);
+  if (p.dbg & 4) {  // timing experiment: no output stage (keep the accumulators live)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+  if (OUT32 && p.splits > 1 && p.ws) {
+    // split-K through plain stores into this slice's slab (summed by
+    // splitk_reduce_kernel): memory-side float atomics run at ~1.3 TB/s of
+    // added bytes, streaming stores at ~6 (MI355X_MICROARCH 'Global float atomics')
+    BigGemmArgs q = p;
+    q.c32 = p.ws + (int64_t)blockIdx.y * p.M * p.ldc;
+    q.accum = 0;
+    q.splits = 1;
+    big_epilogue<OUT32, BW>(q, acc, smem, m0, n0, wm, wn, wave, lane);
+    return;
+  }
+  big_epilogue<OUT32, BW>(p, acc, smem, m0, n0, wm, wn, wave, lane);
 }
 
-template <bool AT, bool BT, bool OUT32>
+// out (+)= sum over the split-K slabs, 16 B per lane
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float4* __restrict__ ws, int splits,
+                                                            int64_t n4, float4* __restrict__ out, int accum) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 a = accum ? out[i] : float4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < splits; ++k) {
+      const float4 v = ws[(int64_t)k * n4 + i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    out[i] = a;
+  }
+}
+
+template <bool AT, bool BT, bool OUT32, int BN>
 void launch_pp_t(const BigGemmArgs& p, hipStream_t s) {
-  constexpr size_t kLds = 8 * (size_t)PP_HALF;  // 2 k-tiles x 4 half-tiles = 128 KiB
+  constexpr size_t kLds = 8 * (size_t)PP_HALF;  // 2 k-tiles x 4 half-tile slots = 128 KiB
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<AT, BT, OUT32>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<AT, BT, OUT32, BN>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
     attr = true;
   }
-  const dim3 grid((unsigned)(((p.M + GB_BM - 1) / GB_BM) * ((p.N + GB_BN - 1) / GB_BN)), (unsigned)p.splits);
-  gemm_pp_kernel<AT, BT, OUT32><<<grid, 512, kLds, s>>>(p);
+  const dim3 grid((unsigned)(((p.M + GB_BM - 1) / GB_BM) * ((p.N + BN - 1) / BN)), (unsigned)p.splits);
+  gemm_pp_kernel<AT, BT, OUT32, BN><<<grid, 512, kLds, s>>>(p);
+}
+
+// Tile width for the ping-pong kernel: 192 when it needs fewer workgroup
+// rounds x tile width (N = 768: 192 -> 256 tiles in one round; N = 2304: 2.25
+// -> 3 rounds of narrower tiles), 256 otherwise (and for the fused column sum).
+int pp_width(const BigGemmArgs& p) {
+  if (p.colsum || p.N % 192 != 0) return 256;
+  if (const char* e = getenv("MFL_GB_WIDTH")) return atoi(e) == 192 ? 192 : 256;
+  const int64_t mt = (p.M + GB_BM - 1) / GB_BM;
+  auto cost = [&](int bn) {
+    const int64_t tiles = mt * ((p.N + bn - 1) / bn) * p.splits;
+    return ((tiles + 255) / 256) * bn;
+  };
+  return cost(192) < cost(256) ? 192 : 256;
 }
 
 template <bool AT, bool BT, bool OUT32, int BK, int NST>
@@ -603,7 +681,10 @@ void launch_big(BigGemmArgs p, int kdim, hipStream_t s) {
   // p.kt_per_split arrives in units of GB_KQ (64) k-elements
   p.kt_per_split *= GB_KQ / bk;
   (void)kdim;
-  if (gb_pipe() == 2) launch_pp_t<AT, BT, OUT32>(p, s);
+  if (gb_pipe() == 2) {
+    if (pp_width(p) == 192) launch_pp_t<AT, BT, OUT32, 192>(p, s);
+    else launch_pp_t<AT, BT, OUT32, 256>(p, s);
+  }
   else if (bk == 32) launch_big_t<AT, BT, OUT32, 32, 4>(p, s);
   else launch_big_t<AT, BT, OUT32, 64, 2>(p, s);
 }
@@ -650,16 +731,41 @@ void launch_gemm_big_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t*
   launch_big<false, true, false>(p, N, s);
 }
 
+namespace {
+int wgrad_splits_env(int M, int N, int K) {
+  if (const char* v = getenv("MFL_GB_SPLITS")) return std::max(1, atoi(v));
+  return gemm_big_wgrad_splits(M, N, K);
+}
+}  // namespace
+
+// fp32 elements of split-K slab workspace the wgrad wants (0: no split, or
+// the atomics path: MFL_GB_SLABS=0 / a pipeline other than the ping-pong one)
+int64_t gemm_big_wgrad_workspace(int M, int N, int K) {
+  static const bool slabs = [] {
+    const char* e = getenv("MFL_GB_SLABS");
+    return !(e && *e == '0');
+  }();
+  const int sp = wgrad_splits_env(M, N, K);
+  return (slabs && gb_pipe() == 2 && sp > 1) ? (int64_t)sp * N * K : 0;
+}
+
 void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,
-                           bool accumulate, hipStream_t s) {
+                           bool accumulate, hipStream_t s, float* ws) {
   // dW[N][K] (+)= dY^T X: output rows = N, columns = K, reduction = M
   BigGemmArgs p{};
   p.a = dy; p.b = x; p.M = N; p.N = K; p.K = M; p.lda = N; p.ldb = K;
   p.a_bytes = (uint32_t)((int64_t)M * N * 2); p.b_bytes = (uint32_t)((int64_t)M * K * 2);
   p.c32 = dw; p.ldc = K; p.accum = accumulate;
-  p.splits = gemm_big_wgrad_splits(M, N, K);
-  if (const char* v = getenv("MFL_GB_SPLITS")) p.splits = std::max(1, atoi(v));
+  p.splits = wgrad_splits_env(M, N, K);
   p.kt_per_split = (M / GB_KQ + p.splits - 1) / p.splits;
+  if (ws && p.splits > 1 && gemm_big_wgrad_workspace(M, N, K) > 0) {
+    p.ws = ws;
+    launch_big<true, true, true>(p, M, s);
+    const int64_t n4 = (int64_t)N * K / 4;
+    splitk_reduce_kernel<<<stream_grid(n4, 256, 2048), 256, 0, s>>>(
+        reinterpret_cast<const float4*>(ws), p.splits, n4, reinterpret_cast<float4*>(dw), accumulate ? 1 : 0);
+    return;
+  }
   launch_big<true, true, true>(p, M, s);
 }
 

@@ -106,3 +106,15 @@ def test_dgrad_gelu_fused_epilogue(on):
     ref = dh * BO.gelu_grad_ref(z.float())
     assert _rel(dz, ref) < 1e-2
     assert _rel(db - 0.25, ref.sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("width", ["192", "256"])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (768, 2304, 1536), (2560, 2112, 768)])
+def test_pp_tile_widths(width, M, N, K, monkeypatch):
+    """The ping-pong kernel's 256x192 and 256x256 tiles, forced (MFL_GB_WIDTH),
+    on all three layouts -- including the transposing-read B1 half-tile of
+    the 192-wide tile (dgrad / wgrad) and a ragged M."""
+    monkeypatch.setenv("MFL_GB_WIDTH", width)
+    test_fwd_bias_resid_gelu(M, N, K)
+    test_dgrad_accumulate(M, N, K)
+    test_wgrad_fp32_accumulate(M, N, K)
