@@ -358,9 +358,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const uint16_t* __restrict_
           unpack8(zv[u], zz);
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            const float cdf = 0.5f * (1.f + erff(zz[k] * 0.70710678f));
-            const float pdf = 0.39894228f * __expf(-0.5f * zz[k] * zz[k]);
-            g[k] *= cdf + zz[k] * pdf;
+            g[k] *= gelu_grad_f(zz[k]);
           }
           const uint4 pk = pack8(g);
           *reinterpret_cast<uint4*>(dz + (int64_t)r * N + cv * 8) = pk;

@@ -36,6 +36,32 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
+// Exact-erf GELU pieces at bf16-output accuracy: erfc(|z|/sqrt2) by Abramowitz
+// & Stegun 7.1.26 (|erf error| <= 1.5e-7; bf16 resolves 2^-9 relative), one
+// exp shared by Phi(z) and phi(z), no cancellation in the negative tail.
+// ocml's erff is ~3x the VALU work: it made gelu_bwd and the fused GEMM GELU
+// epilogues VALU-bound (50M elements per BERT-base FFN).
+__device__ __forceinline__ void gelu_parts(float z, float& cdf, float& pdf) {
+  const float x = fabsf(z) * 0.70710678f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, x, 1.f));
+  const float e = __expf(-x * x);  // exp(-z^2 / 2)
+  const float poly =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
+               0.254829592f);
+  const float q = 0.5f * poly * e;  // Phi(-|z|)
+  cdf = z < 0.f ? q : 1.f - q;
+  pdf = 0.39894228f * e;
+}
+__device__ __forceinline__ float gelu_f(float z) {
+  float c, p;
+  gelu_parts(z, c, p);
+  return z * c;
+}
+__device__ __forceinline__ float gelu_grad_f(float z) {
+  float c, p;
+  gelu_parts(z, c, p);
+  return c + z * p;
+}
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll

@@ -133,7 +133,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int n0,
       float f[8], h[8];
       unpack8(packed, f);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) h[k] = 0.5f * f[k] * (1.f + erff(f[k] * 0.70710678f));
+      for (int k = 0; k < 8; ++k) h[k] = gelu_f(f[k]);
       *reinterpret_cast<uint4*>(a.act_out + off) = pack8(h);
     }
     if (stats) {

@@ -202,9 +202,7 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[
           unpack8(*reinterpret_cast<const uint4*>(p.gelu_z + off), zz);
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            const float cdf = 0.5f * (1.f + erff(zz[k] * 0.70710678f));
-            const float pdf = 0.39894228f * __expf(-0.5f * zz[k] * zz[k]);
-            v[k] *= cdf + zz[k] * pdf;
+            v[k] *= gelu_grad_f(zz[k]);
           }
         }
         const uint4 packed = pack8(v);
@@ -219,7 +217,7 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[
           float f[8], h[8];
           unpack8(packed, f);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) h[k] = 0.5f * f[k] * (1.f + erff(f[k] * 0.70710678f));
+          for (int k = 0; k < 8; ++k) h[k] = gelu_f(f[k]);
           *reinterpret_cast<uint4*>(p.act_out + off) = pack8(h);
         }
       }

@@ -221,11 +221,11 @@ class BertMLM(StaticNet):
             BO.ln_bwd(dout, A["fo"], A["m2"], A["r2"], self._p(p + "ln2.gamma"), self.g_fo, g(p + "ln2.gamma"),
                       g(p + "ln2.beta"), M, H, dx2=self.g_a, dbias_prev=g(p + "ffn2.b"))
             BO.gemm_wgrad(A["h"], self.g_fo, g(p + "ffn2.w"), M, H, F, zeroed=True)
-            # Unfused on purpose: gemm_dgrad_gelu (GELU backward + bias colsum in
-            # the large-tile epilogue) measured +1.1 ms/step of epilogue VALU at
-            # one workgroup per CU against 0.74 ms for the streaming gelu_bwd.
-            BO.gemm_dgrad(self.g_fo, self._w(p + "ffn2.w"), self.g_h, M, H, F)
-            BO.gelu_bwd(self.g_h, A["z"], self.g_z, M, F, dbias=g(p + "ffn1.b"))
+            # GELU backward + FFN1 bias gradient in the dgrad epilogue: saves the
+            # 300 MB round trip of a separate gelu_bwd (scripts/gelu_fuse_probe.py:
+            # 128-134 us fused vs 137-150 unfused, with the A&S erf of common.h)
+            BO.gemm_dgrad_gelu(self.g_fo, self._w(p + "ffn2.w"), self.g_z, A["z"], M, H, F,
+                               dbias=g(p + "ffn1.b"))
             BO.gemm_wgrad(A["a"], self.g_z, g(p + "ffn1.w"), M, F, H, zeroed=True)
             BO.gemm_dgrad(self.g_z, self._w(p + "ffn1.w"), self.g_a, M, F, H, accumulate=True)
             BO.ln_bwd(self.g_a, A["ao"], A["m1"], A["r1"], self._p(p + "ln1.gamma"), self.g_ao, g(p + "ln1.gamma"),
