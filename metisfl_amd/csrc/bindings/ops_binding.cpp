@@ -45,7 +45,7 @@ void fused_optimizer(int64_t mode, torch::Tensor p, torch::Tensor g,
                      double lr, double l1, double l2, double momentum, double mu, double beta1,
                      double beta2, double eps, double wd, c10::optional<torch::Tensor> lr_scale,
                      c10::optional<torch::Tensor> step, bool zero_grad,
-                     c10::optional<torch::Tensor> zero_region) {
+                     c10::optional<torch::Tensor> zero_region, bool tick) {
   CHECK_IN(p, torch::kFloat32);
   CHECK_IN(g, torch::kFloat32);
   const int64_t n = p.numel();
@@ -68,6 +68,7 @@ void fused_optimizer(int64_t mode, torch::Tensor p, torch::Tensor g,
   }
   if (lr_scale.has_value() && lr_scale->defined()) CHECK_IN((*lr_scale), torch::kFloat32);
   if (step.has_value() && step->defined()) CHECK_IN((*step), torch::kInt32);
+  TORCH_CHECK(!tick || (step.has_value() && step->defined()), "tick needs the step counter");
   mfl::OptHyper h;
   h.lr = (float)lr; h.l1 = (float)l1; h.l2 = (float)l2; h.momentum = (float)momentum;
   h.mu = (float)mu; h.beta1 = (float)beta1; h.beta2 = (float)beta2; h.eps = (float)eps;
@@ -80,7 +81,7 @@ void fused_optimizer(int64_t mode, torch::Tensor p, torch::Tensor g,
                               zero_region.has_value() && zero_region->defined()
                                   ? (int64_t)(zero_region->numel() * zero_region->element_size()) / 16 * 16
                                   : 0,
-                              cur_stream(p));
+                              cur_stream(p), tick ? step->data_ptr<int>() : nullptr);
 }
 
 void cast_f32_bf16(torch::Tensor x, torch::Tensor y) {

@@ -24,7 +24,9 @@ struct OptHyper {
 void launch_fused_optimizer(int mode, float* p, float* g, float* m, float* v,
                             const float* anchor, uint16_t* p16, int64_t n, const OptHyper& h,
                             const float* lr_ptr, const int* step_ptr, bool zero_grad, void* zero,
-                            int64_t zero_bytes, hipStream_t s);
+                            int64_t zero_bytes, hipStream_t s, int* tick_step = nullptr);
+// tick_step: also increment *tick_step once, after the optimizer's reads of
+// step_ptr (in the same launch for the modes that never read it)
 void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
 void launch_scale_f32(float* x, int64_t n, float w, const float* wptr, hipStream_t s);
 void launch_tick(int* step, int inc, hipStream_t s);

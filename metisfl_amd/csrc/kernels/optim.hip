@@ -21,7 +21,7 @@ __global__ __launch_bounds__(256) void fused_opt_kernel(
     float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
     const float* __restrict__ anchor, uint16_t* __restrict__ p16, int64_t n4, OptHyper h,
     const float* __restrict__ lr_ptr, const int* __restrict__ step_ptr, int zero_grad,
-    uint4* __restrict__ zero, int64_t zero16) {
+    uint4* __restrict__ zero, int64_t zero16, int* __restrict__ tick_step) {
   const float lr = lr_ptr ? lr_ptr[0] * h.lr : h.lr;
   float bc1 = 1.f, bc2 = 1.f;
   if (MODE == OPT_ADAM || MODE == OPT_ADAMW) {
@@ -86,31 +86,37 @@ __global__ __launch_bounds__(256) void fused_opt_kernel(
       reinterpret_cast<uint2*>(p16)[i] = o;
     }
   }
+  // the step-counter increment that used to be its own launch; these modes
+  // never read the counter, so one lane bumps it (Adam / AdamW read it in
+  // every block: their launcher ticks in a separate launch -- a last-block
+  // arrival counter over 2048 blocks serialised ~23 us of same-word atomics)
+  if (MODE != OPT_ADAM && MODE != OPT_ADAMW && tick_step && blockIdx.x == 0 && threadIdx.x == 0)
+    atomicAdd(tick_step, 1);
 }
 
 template <int MODE>
 static void launch_mode(float* p, float* g, float* m, float* v, const float* anchor,
                         uint16_t* p16, int64_t n, const OptHyper& h, const float* lr_ptr,
                         const int* step_ptr, bool zg, void* zero, int64_t zero_bytes,
-                        hipStream_t s) {
+                        hipStream_t s, int* tick_step) {
   const int64_t n4 = n / 4;
   const int64_t z16 = zero ? zero_bytes / 16 : 0;
   const unsigned grid = stream_grid(n4 > z16 ? n4 : z16, 256, 2048);
   uint4* z = reinterpret_cast<uint4*>(zero);
   if (p16)
     fused_opt_kernel<MODE, true><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr,
-                                                      step_ptr, zg ? 1 : 0, z, z16);
+                                                      step_ptr, zg ? 1 : 0, z, z16, tick_step);
   else
     fused_opt_kernel<MODE, false><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr,
-                                                       step_ptr, zg ? 1 : 0, z, z16);
+                                                       step_ptr, zg ? 1 : 0, z, z16, tick_step);
 }
 
 void launch_fused_optimizer(int mode, float* p, float* g, float* m, float* v,
                             const float* anchor, uint16_t* p16, int64_t n, const OptHyper& h,
                             const float* lr_ptr, const int* step_ptr, bool zero_grad, void* zero,
-                            int64_t zero_bytes, hipStream_t s) {
+                            int64_t zero_bytes, hipStream_t s, int* tick_step) {
 #define MFL_OPT_CASE(M_) \
-  case M_: launch_mode<M_>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, zero_grad, zero, zero_bytes, s); break;
+  case M_: launch_mode<M_>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, zero_grad, zero, zero_bytes, s, tick_step); break;
   switch (mode) {
     MFL_OPT_CASE(OPT_SGD)
     MFL_OPT_CASE(OPT_MOMENTUM)
@@ -120,6 +126,7 @@ void launch_fused_optimizer(int mode, float* p, float* g, float* m, float* v,
     default: break;
   }
 #undef MFL_OPT_CASE
+  if (tick_step && (mode == OPT_ADAM || mode == OPT_ADAMW)) launch_tick(tick_step, 1, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -250,8 +250,8 @@ class BertMLM(StaticNet):
         self._forward()
         self._head(train=True)
         self._backward()
-        st.optimizer_step(zero_grad=self.zero_grad_in_optimizer)
-        opt_ops.tick(st.step, 1)
+        if not st.optimizer_step(zero_grad=self.zero_grad_in_optimizer, tick=True):
+            opt_ops.tick(st.step, 1)
 
     def _eval_body(self, ds: DeviceDataset) -> None:
         K.gather_batch(ds.x, ds.y, ds.perm, self.eval_step_ctr, ds.steps_per_epoch, self.B, self.xb, self.yb)

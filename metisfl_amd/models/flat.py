@@ -140,11 +140,16 @@ class FlatState:
         if spec.needs_anchor and self.anchor is None:
             self.anchor = self.params32.clone()
 
-    def optimizer_step(self, zero_grad: bool = True, zero_region: torch.Tensor | None = None) -> None:
+    def optimizer_step(self, zero_grad: bool = True, zero_region: torch.Tensor | None = None,
+                       tick: bool = False) -> bool:
+        """One fused optimizer launch; ``tick``: it also increments the step
+        counter (returns False when no launch happened -- the caller ticks)."""
         if self.n_params == 0 or self.optimizer is None:
-            return
+            return False
         opt_ops.fused_step(self.optimizer, self.params32, self.grad32, self.m, self.v, self.anchor,
-                           self.p16, self.lr_scale, self.step, zero_grad, zero_region)
+                           self.p16, self.lr_scale, self.step, zero_grad, zero_region,
+                           tick)
+        return True
 
     def set_anchor(self) -> None:
         """Snapshot the received community model as the FedProx anchor."""

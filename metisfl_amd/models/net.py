@@ -121,9 +121,10 @@ class StaticNet:
             l.prepare_backward()
         self.backward(dlast)
         self.ws.join()  # weight-gradient branch (side stream) must land first
-        # one launch: optimizer + grad re-zero + BN accumulator re-zero
-        st.optimizer_step(zero_grad=self.zero_grad_in_optimizer, zero_region=self.ws.bn_acc)
-        opt_ops.tick(st.step, 1)
+        # one launch: optimizer + grad re-zero + BN accumulator re-zero + step tick
+        if not st.optimizer_step(zero_grad=self.zero_grad_in_optimizer, zero_region=self.ws.bn_acc,
+                                 tick=True):
+            opt_ops.tick(st.step, 1)
 
     def _eval_body(self, ds: DeviceDataset) -> None:
         K.gather_batch(ds.x, ds.y, ds.perm, self.eval_step_ctr, ds.steps_per_epoch, self.B,

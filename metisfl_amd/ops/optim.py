@@ -89,22 +89,27 @@ def fused_step(spec: OptimizerSpec, p: torch.Tensor, g: torch.Tensor,
                m: torch.Tensor | None = None, v: torch.Tensor | None = None,
                anchor: torch.Tensor | None = None, p16: torch.Tensor | None = None,
                lr_scale: torch.Tensor | None = None, step: torch.Tensor | None = None,
-               zero_grad: bool = False, zero_region: torch.Tensor | None = None) -> None:
+               zero_grad: bool = False, zero_region: torch.Tensor | None = None,
+               tick: bool = False) -> None:
     """Apply one optimizer step in place over flat buffers.  ``zero_grad``
     writes 0 back into ``g`` once consumed and ``zero_region`` (e.g. the
     BatchNorm accumulators) is cleared by the same launch, so the next step's
-    atomic accumulations start from zero without a memset node."""
+    atomic accumulations start from zero without a memset node.
+    ``tick``: also increment ``step`` once, after the optimizer has read it
+    (inside the same launch for the modes that never read it)."""
     if p.is_cuda:
         ops().fused_optimizer(spec.mode, p, g, m, v, anchor, p16, spec.learning_rate, spec.l1,
                               spec.l2, spec.momentum, spec.proximal_term, spec.beta1, spec.beta2,
                               spec.epsilon, spec.weight_decay, lr_scale, step, zero_grad,
-                              zero_region)
+                              zero_region, tick)
         return
     _reference_step(spec, p, g, m, v, anchor, p16, lr_scale, step)
     if zero_grad:
         g.zero_()
     if zero_region is not None:
         zero_region.zero_()
+    if tick:
+        step.add_(1)
 
 
 @torch.no_grad()

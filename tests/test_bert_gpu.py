@@ -208,5 +208,6 @@ def test_bert_base_graph_step_runs():
     ds = net.make_dataset(synthetic_mlm(32, c.seq, c.max_pred, c.vocab, seed=1, rec_stride=c.rec_stride))
     net.reset_train_stats()
     net.train_steps(ds, 3)
+    assert int(net.state.step.cpu()) == 3  # the optimizer launch's fused step tick
     s = net.train_stats()
     assert np.isfinite(s["loss"]) and abs(s["loss"] - math.log(c.vocab)) < 1.5, s
