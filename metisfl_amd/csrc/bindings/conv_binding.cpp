@@ -133,6 +133,29 @@ void conv_forward(torch::Tensor x, torch::Tensor w, torch::Tensor y,
   run_gemm(g, false, x, w, y, ws, stats, false);
 }
 
+// fused BN-backward target of a dgrad (all optional; bn_acc undefined: off)
+bool bnb_args(int64_t M, int64_t C, const c10::optional<torch::Tensor>& bn_z,
+              const c10::optional<torch::Tensor>& bn_y, const c10::optional<torch::Tensor>& bn_mean,
+              const c10::optional<torch::Tensor>& bn_invstd, const c10::optional<torch::Tensor>& bn_acc,
+              mfl::BnBwdFusion& f) {
+  if (!(bn_acc.has_value() && bn_acc->defined())) return false;
+  TORCH_CHECK(bn_z.has_value() && bn_mean.has_value() && bn_invstd.has_value(), "bn fusion args");
+  check_bf16(*bn_z, M * C, "bn_z");
+  f.z = bf(*bn_z);
+  if (bn_y.has_value() && bn_y->defined()) {
+    check_bf16(*bn_y, M * C, "bn_y");
+    f.y = bf(*bn_y);
+  }
+  check_f32(*bn_mean, C, "bn_mean");
+  check_f32(*bn_invstd, C, "bn_invstd");
+  f.mean = bn_mean->data_ptr<float>();
+  f.invstd = bn_invstd->data_ptr<float>();
+  TORCH_CHECK(bn_acc->is_cuda() && bn_acc->is_contiguous() && bn_acc->scalar_type() == torch::kFloat64 &&
+                  bn_acc->numel() >= 2 * C, "bn_acc must be a contiguous fp64 tensor of >= 2*C");
+  f.acc = bn_acc->data_ptr<double>();
+  return true;
+}
+
 void conv_dgrad(torch::Tensor dy, torch::Tensor wt, torch::Tensor dx,
                 c10::optional<torch::Tensor> ws, int64_t N, int64_t H, int64_t W, int64_t C,
                 int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate,
@@ -182,6 +205,43 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t N, 
   mfl::launch_conv_wgrad(g, p, bf(x), bf(dy), dw.data_ptr<float>(), cur_stream(x));
 }
 
+// A layer's backward GEMMs: dw += dy^T im2col(x) (dw zero on entry, the
+// training step's gradient buffer) and dx (+)= conv_transpose(dy, W) with the
+// optional fused BN-backward reductions -- in one paired launch when the
+// shapes allow (launch_conv_bwd_pair), else as the two launches.
+void conv_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, torch::Tensor wt,
+                        torch::Tensor dx, c10::optional<torch::Tensor> ws, int64_t N, int64_t H, int64_t W,
+                        int64_t C, int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                        bool accumulate, c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
+                        c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
+                        c10::optional<torch::Tensor> bn_acc) {
+  auto gw = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
+  auto gd = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
+  check_bf16(x, N * H * W * C, "x");
+  check_bf16(dy, (int64_t)gw.M * Co, "dy");
+  check_f32(dw, Co * R * S * C, "dw");
+  TORCH_CHECK(dw.numel() == Co * R * S * C, "dw size");
+  check_bf16(wt, C * R * S * Co, "wt");
+  check_bf16(dx, N * H * W * C, "dx");
+  mfl::BnBwdFusion f;
+  const bool fused = bnb_args(N * H * W, C, bn_z, bn_y, bn_mean, bn_invstd, bn_acc, f);
+  auto pd = mfl::plan_conv_gemm(gd, true);
+  float* wsp = nullptr;
+  int* counters = nullptr;
+  if (pd.splits > 1) {
+    TORCH_CHECK(ws.has_value() && ws->defined(), "split-K workspace required");
+    check_f32(*ws, workspace_floats(gd, pd), "workspace");
+    counters = reinterpret_cast<int*>(ws->data_ptr<float>());
+    wsp = ws->data_ptr<float>() + counter_words(gd, pd);
+  }
+  if (mfl::launch_conv_bwd_pair(gd, pd, bf(dy), bf(wt), bf(dx), wsp, counters, accumulate, fused ? &f : nullptr,
+                                gw, bf(x), dw.data_ptr<float>(), cur_stream(dx)))
+    return;
+  mfl::launch_conv_wgrad(gw, mfl::plan_conv_wgrad(gw), bf(x), bf(dy), dw.data_ptr<float>(), cur_stream(x));
+  if (fused) run_gemm(gd, true, dy, wt, dx, ws, c10::nullopt, accumulate, &f);
+  else run_gemm(gd, true, dy, wt, dx, ws, c10::nullopt, accumulate);
+}
+
 void transpose_krsc(torch::Tensor w, torch::Tensor wt, int64_t Co, int64_t RS, int64_t Ci) {
   check_bf16(w, Co * RS * Ci, "w");
   check_bf16(wt, Co * RS * Ci, "wt");
@@ -217,6 +277,7 @@ void register_conv(pybind11::module& m) {
   m.def("conv_forward", &conv_forward);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_backward_pair", &conv_backward_pair);
   m.def("transpose_krsc", &transpose_krsc);
 }
 

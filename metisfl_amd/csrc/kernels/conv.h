@@ -81,6 +81,13 @@ struct BnBwdFusion {
   const float* invstd = nullptr;
   double* acc = nullptr;
 };
+// A layer's dgrad (geometry gd, plan pd as sized for the caller's workspace,
+// optional fused BN-backward reductions f) and wgrad (forward geometry gw,
+// dw += ..., zero on entry) in one launch.  false: not supported for this
+// shape (or MFL_CONV_PAIR=0) -- nothing was launched.
+bool launch_conv_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const uint16_t* dy, const uint16_t* wt,
+                          uint16_t* dx, float* ysplit, int* counters, bool accum, const BnBwdFusion* f,
+                          const ConvGeom& gw, const uint16_t* x, float* dw, hipStream_t s);
 // dgrad with the fused BN-backward reductions of the consumer layer
 void launch_conv_dgrad_bnb(const ConvGeom& g, const ConvPlan& p, const uint16_t* dy,
                            const uint16_t* wgt, uint16_t* dx, float* ysplit, int* counters,

@@ -217,8 +217,18 @@ __device__ __forceinline__ void dma_k_loop(int nk, Issue& issue, Compute& comput
 // over its own taps (K_c = taps * Cout), and the epilogue scatters rows back
 // to NHWC pixels.  Without it 3/4 of a stride-2 dgrad's MFMA work and operand
 // traffic multiplies structural zeros.
+// Block coordinates of a workgroup: blockIdx / gridDim of a plain launch, or
+// decoded from the linear id of a paired launch (conv_bwd_pair_kernel).
+struct BlkCoord {
+  int x, y, z, gx, gy, gz;
+};
+__device__ __forceinline__ BlkCoord hw_coord() {
+  return BlkCoord{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z,
+                  (int)gridDim.x,  (int)gridDim.y,  (int)gridDim.z};
+}
+
 template <int BM, int BN, bool DGRAD, int KS, int ST, int BK, bool PAR = false>
-__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
+__device__ __forceinline__ void conv_gemm_body(const ConvArgs& a, const BlkCoord bc, uint8_t* smem) {
   // BK = 64 or 128 k-elements per tile: [row][k] tiles have ROWA-byte rows
   constexpr int ROWA = BK * 2;
   constexpr int A_RPI = 1024 / ROWA;   // rows per 1-KiB DMA instruction
@@ -233,15 +243,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const ConvGeom& g = a.g;
   const auto rsA = make_rsrc(a.src, a.src_bytes);
   const auto rsB = make_rsrc(a.wgt, a.wgt_bytes);
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  const int kbeg = blockIdx.z * a.kchunk;
+  const int m0 = bc.x * BM;
+  const int n0 = bc.y * BN;
+  const int kbeg = bc.z * a.kchunk;
   // parity class of this tile (block-uniform): first taps r0 / s0, tap counts
   // ns (along s), offsets dh / dw of the dY row / column of tap 0
   int cls = 0, r0 = 0, s0 = 0, ns = 1, dh = 0, dw = 0, kc_end = g.K;
@@ -403,8 +411,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int fr = lane & 15;
   const int rl0 = wm * (BM / 2) + (lane >> 4) * 4;
   const int cl0 = wn * (BN / 2) + fr;
-  const int splits = gridDim.z;
-  const int tile_id = blockIdx.y * gridDim.x + blockIdx.x;
+  const int splits = bc.gz;
+  const int tile_id = bc.y * bc.gx + bc.x;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -421,10 +429,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     // loads: misses its own possibly stale L2) onto its own LDS tile.
     constexpr int F = BM * BN / 1024;  // float4 per thread
     constexpr int C4 = BN / 4;
-    const int ntiles = gridDim.x * gridDim.y;
+    const int ntiles = bc.gx * bc.gy;
     const int64_t zstride = (int64_t)ntiles * BM * BN * 4;  // bytes between slices
     const auto rsS = make_rsrc(a.ysplit + (int64_t)tile_id * (BM * BN), 0x7FFFFFF0u);
-    const uint32_t zoff = (uint32_t)(blockIdx.z * zstride);
+    const uint32_t zoff = (uint32_t)(bc.z * zstride);
 #pragma unroll
     for (int u = 0; u < F; ++u) {
       const int f = t + 256 * u;
@@ -452,7 +460,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     // slices summed in z order whichever slice reduces: bitwise deterministic
     for (int z = 0; z < splits; ++z) {
       float4 r[F];
-      if (z == (int)blockIdx.z) {
+      if (z == bc.z) {
 #pragma unroll
         for (int u = 0; u < F; ++u) {
           const int f = t + 256 * u;
@@ -496,8 +504,16 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 // wgrad:  dW[ko][j] = sum_m dY[m][ko] * im2col(X)[m][j],  j = (r, s, c)
 // Tiles: A = dY [64 m][64 ko], B = im2col(X) [64 m][64 j], both 128-B rows,
 // both read with transposing LDS reads.
+
+template <int BM, int BN, bool DGRAD, int KS, int ST, int BK, bool PAR = false>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  conv_gemm_body<BM, BN, DGRAD, KS, ST, BK, PAR>(a, hw_coord(), smem);
+}
+
 template <int KS, int ST, int BK>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __restrict__ dw) {
+__device__ __forceinline__ void conv_wgrad_body(const ConvArgs& a, float* __restrict__ dw, const BlkCoord bc,
+                                                uint8_t* smem) {
   // g: H,W,C = X dims; P,Q = dY spatial; Ng = Cout; K = R*S*C; M = N*P*Q
   constexpr int BM = 64, BN = 64;
   constexpr int TM = 2, TN = 2;
@@ -507,15 +523,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
   const ConvGeom& g = a.g;
   const auto rsA = make_rsrc(a.src, a.src_bytes);
   const auto rsB = make_rsrc(a.wgt, a.wgt_bytes);
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int ko0 = blockIdx.x * BM;
-  const int j0 = blockIdx.y * BN;
-  const int mbeg = blockIdx.z * a.kchunk;
+  const int ko0 = bc.x * BM;
+  const int j0 = bc.y * BN;
+  const int mbeg = bc.z * a.kchunk;
   const int mend = min(g.M, mbeg + a.kchunk);
   const int nk = (mend - mbeg + BK - 1) / BK;
 
@@ -593,12 +607,48 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
       for (int e = 0; e < 4; ++e) {
         const int row = rbase + 16 * i + e, cc = cbase + 16 * jj;
         if (row < g.Ng && cc < g.K) {
-          if (gridDim.z > 1 || a.accum)
+          if (bc.gz > 1 || a.accum)
             atomicAdd(&dw[(int64_t)row * g.K + cc], acc[i][jj][e]);
           else
             dw[(int64_t)row * g.K + cc] = acc[i][jj][e];
         }
       }
+}
+
+template <int KS, int ST, int BK>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __restrict__ dw) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  conv_wgrad_body<KS, ST, BK>(a, dw, hw_coord(), smem);
+}
+
+// ---------------------------------------------------------------------------
+// A layer's dgrad and wgrad in ONE launch (horizontal fusion).  Both consume
+// the same dY and are independent; as two launches each is latency-bound
+// (256-576 small workgroups, few k-steps) and the second starts only after
+// the first's tail.  In one grid their workgroups share the CUs -- the dgrad
+// runs with BK = 64 here so that every workgroup of the launch fits in
+// <= 74 KiB of LDS (two per CU).  Block ids [0, nd) are the dgrad grid
+// (x fastest, then y, z), [nd, nd + nw) the wgrad grid.  Measured upper bound
+// (scripts/conv_pair_probe.py, two unsynchronised streams): 28-30 -> 20-23 us
+// per layer pair.
+struct PairGrid {
+  int dgx, dgy, dgz, wgx, wgy, wgz;
+};
+template <int BM, int BN, int KS, int ST, bool PAR>
+__global__ __launch_bounds__(256) void conv_bwd_pair_kernel(ConvArgs da, ConvArgs wa, float* __restrict__ dw,
+                                                            PairGrid pg) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  int id = blockIdx.x;
+  const int nd = pg.dgx * pg.dgy * pg.dgz;
+  if (id < nd) {
+    const int x = id % pg.dgx, r = id / pg.dgx;
+    conv_gemm_body<BM, BN, true, KS, ST, 64, PAR>(
+        da, BlkCoord{x, r % pg.dgy, r / pg.dgy, pg.dgx, pg.dgy, pg.dgz}, smem);
+  } else {
+    id -= nd;
+    const int x = id % pg.wgx, r = id / pg.wgx;
+    conv_wgrad_body<KS, ST, 64>(wa, dw, BlkCoord{x, r % pg.wgy, r / pg.wgy, pg.wgx, pg.wgy, pg.wgz}, smem);
+  }
 }
 
 // [Cout][R][S][Cin] -> [Cin][R][S][Cout]  (layout utility, not on the hot path)
@@ -867,6 +917,91 @@ void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, 
   const int ks = g.R, st = g.stride;
   if (p.bk == 128) launch_wgrad_ks<128>(a, grid, ks, st, dw, s);
   else launch_wgrad_ks<64>(a, grid, ks, st, dw, s);
+}
+
+// ---- paired dgrad + wgrad ----------------------------------------------------
+namespace {
+template <int BM, int BN, int KS, int ST, bool PAR>
+void launch_pair_t(const ConvArgs& da, const ConvArgs& wa, float* dw, const PairGrid& pg, hipStream_t s) {
+  size_t lds = (size_t)kStages * (BM + BN) * 64 * 2;
+  const size_t epi = ((size_t)BM * (BN + 4) + 256 * 16 + 8) * sizeof(float);
+  const size_t wl = (size_t)kStages * 2 * 64 * 128;
+  lds = std::max(lds, std::max(epi, wl));
+  static bool attr = false;
+  set_lds_limit(&conv_bwd_pair_kernel<BM, BN, KS, ST, PAR>, lds, attr);
+  const unsigned n = (unsigned)(pg.dgx * pg.dgy * pg.dgz + pg.wgx * pg.wgy * pg.wgz);
+  conv_bwd_pair_kernel<BM, BN, KS, ST, PAR><<<n, 256, lds, s>>>(da, wa, dw, pg);
+}
+
+template <int BM, int BN>
+bool launch_pair_bm(const ConvArgs& da, const ConvArgs& wa, float* dw, const PairGrid& pg, hipStream_t s) {
+  const int ks = da.g.R, st = da.g.stride;
+  if (ks == 3 && st == 1) launch_pair_t<BM, BN, 3, 1, false>(da, wa, dw, pg, s);
+  else if (ks == 3 && st == 2 && da.par_mc) launch_pair_t<BM, BN, 3, 2, true>(da, wa, dw, pg, s);
+  else if (ks == 3 && st == 2) launch_pair_t<BM, BN, 3, 2, false>(da, wa, dw, pg, s);
+  else if (ks == 1 && st == 2) launch_pair_t<BM, BN, 1, 2, false>(da, wa, dw, pg, s);
+  else return false;
+  return true;
+}
+}  // namespace
+
+bool conv_pair_enabled() {
+  static const int on = env_int("MFL_CONV_PAIR", 1);
+  return on != 0;
+}
+
+bool launch_conv_bwd_pair(const ConvGeom& gd, const ConvPlan& pd_in, const uint16_t* dy, const uint16_t* wt,
+                          uint16_t* dx, float* ysplit, int* counters, bool accum, const BnBwdFusion* f,
+                          const ConvGeom& gw, const uint16_t* x, float* dw, hipStream_t s) {
+  if (!conv_pair_enabled()) return false;
+  if (!((pd_in.bm == 128 && pd_in.bn == 64) || (pd_in.bm == 64 && pd_in.bn == 64))) return false;
+  const ConvPlan pw = plan_conv_wgrad(gw);
+  if (pw.bk != 64) return false;
+  // the dgrad at BK = 64 with the SAME split count (the caller's workspace
+  // and counter slots were sized for this plan)
+  ConvPlan pd = pd_in;
+  const int K = pd.par_mc ? ((gd.R + 1) / 2) * ((gd.S + 1) / 2) * gd.C : gd.K;
+  const int ks64 = (K + 63) / 64;
+  pd.bk = 64;
+  pd.kchunk = ((ks64 + pd.splits - 1) / pd.splits) * 64;
+  ConvArgs da{};
+  da.g = gd;
+  da.src = dy;
+  da.wgt = wt;
+  da.src_bytes = range_bytes((int64_t)gd.N * gd.H * gd.W * gd.C);
+  da.wgt_bytes = range_bytes((int64_t)gd.Ng * gd.K);
+  da.y = dx;
+  da.ysplit = ysplit;
+  da.counters = counters;
+  da.kchunk = pd.kchunk;
+  da.accum = accum ? 1 : 0;
+  if (f) {
+    da.bn_z = f->z;
+    da.bn_y = f->y;
+    da.bn_mean = f->mean;
+    da.bn_invstd = f->invstd;
+    da.bn_acc = f->acc;
+  }
+  da.par_mc = pd.par_mc;
+  fill_shifts(da);
+  ConvArgs wa{};
+  wa.accum = 1;  // the training step's gradient buffer is zero on entry
+  wa.g = gw;
+  wa.src = dy;
+  wa.wgt = x;
+  wa.src_bytes = range_bytes((int64_t)gw.M * gw.Ng);
+  wa.wgt_bytes = range_bytes((int64_t)gw.N * gw.H * gw.W * gw.C);
+  wa.kchunk = pw.kchunk;
+  fill_shifts(wa);
+  PairGrid pg;
+  pg.dgx = (gd.M + pd.bm - 1) / pd.bm;
+  pg.dgy = (gd.Ng + pd.bn - 1) / pd.bn;
+  pg.dgz = pd.splits;
+  pg.wgx = (gw.Ng + 63) / 64;
+  pg.wgy = (gw.K + 63) / 64;
+  pg.wgz = pw.splits;
+  if (pd.bm == 128) return launch_pair_bm<128, 64>(da, wa, dw, pg, s);
+  return launch_pair_bm<64, 64>(da, wa, dw, pg, s);
 }
 
 void launch_transpose_krsc(const uint16_t* w, uint16_t* wt, int Co, int RS, int Ci, hipStream_t s) {

@@ -15,6 +15,8 @@ These layers replace the Keras layers the reference trains with
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from metisfl_amd.models.flat import FlatState, VarSpec
@@ -58,8 +60,9 @@ class Workspace:
 
     # Measured on MI355X (round 1): forking wgrad / shortcuts onto a second
     # stream inside the graph made the ResNet-18 step ~12% SLOWER (the branches
-    # contend for CUs and add cross-stream waits), so it is opt-in.
-    overlap = False
+    # contend for CUs and add cross-stream waits), so it is opt-in
+    # (MFL_OVERLAP=1).
+    overlap = os.environ.get("MFL_OVERLAP", "0") == "1"
 
     def fork(self):
         """Context: run the enclosed launches on the side stream, ordered after
@@ -184,6 +187,11 @@ class ConvBN(Layer):
         # weight gradient: off the critical path -> side stream (joined before
         # the optimizer); the gradient buffer is zero on entry (re-zeroed by
         # the optimizer launch), so split-K slices accumulate atomically
+        if dx is not None and not self.ws.overlap:
+            # both GEMMs in one launch (their workgroups share the CUs)
+            K.conv_backward_pair(self.x, self.dz, self.dw, self.w16, dx, s, self._split(), accumulate,
+                                 bnb=bnb)
+            return
         with self.ws.fork():
             K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True)
         if dx is not None:

@@ -159,6 +159,24 @@ def conv_wgrad(x, dy, dw, shp: ConvShape, accumulate: bool = False) -> None:
     dw.copy_(g.permute(0, 2, 3, 1).reshape(dw.shape))
 
 
+def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
+                       bnb: BnBwdTarget | None = None) -> None:
+    """A layer's weight gradient (dw += ..., dw zero on entry) and input
+    gradient (as conv_dgrad) -- on the GPU in ONE paired launch, so the two
+    independent, latency-bound GEMMs share the CUs (conv.hip
+    conv_bwd_pair_kernel; MFL_CONV_PAIR=0 for two launches)."""
+    if dy.is_cuda:
+        if bnb is None:
+            ops().conv_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None,
+                                     None)
+        else:
+            ops().conv_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
+                                     bnb.invstd, bnb.acc)
+        return
+    conv_wgrad(x, dy, dw, shp, accumulate=True)
+    conv_dgrad(dy, w, dx, shp, ws, accumulate, bnb=bnb)
+
+
 def transpose_krsc(w, wt, Co: int, RS: int, Ci: int) -> None:
     if w.is_cuda:
         ops().transpose_krsc(w, wt, Co, RS, Ci)

@@ -157,6 +157,55 @@ def test_conv_wgrad_matches_fp32(case):
     assert rel_err(dw, ref) < 5e-3
 
 
+@pytest.mark.parametrize("case", CONV_CASES[1:])
+@pytest.mark.parametrize("with_bnb", [False, True])
+def test_conv_backward_pair_matches_separate(case, with_bnb):
+    """One paired dgrad + wgrad launch (conv_bwd_pair_kernel, the dgrad at
+    BK = 64) against the fp32 references and, for the fused BN-backward
+    reductions, against the separate dgrad launch."""
+    from metisfl_amd.ops import nn as K
+    N, H, W, C, Co, k, s = case
+    torch.manual_seed(5)
+    shp = K.ConvShape(N, H, W, C, Co, k, k, s, k // 2)
+    x = bf(torch.randn(N, H, W, C, device=DEV))
+    w = bf(torch.randn(Co, k, k, C, device=DEV) * 0.1)
+    dy = bf(torch.randn(N, shp.P, shp.Q, Co, device=DEV))
+    plan = K.conv_plan(1, shp, torch.device(DEV))
+    ws = torch.zeros(max(4, plan.workspace), device=DEV)
+
+    def target():
+        if not with_bnb:
+            return None
+        g = torch.Generator(device=DEV).manual_seed(9)
+        z = bf(torch.randn(N, H, W, C, device=DEV, generator=g))
+        return K.BnBwdTarget(z, torch.relu(z), torch.randn(C, device=DEV, generator=g) * 0.1,
+                             torch.rand(C, device=DEV, generator=g) + 0.5,
+                             torch.zeros(2 * C, dtype=torch.float64, device=DEV))
+
+    t_pair, t_sep = target(), target()
+    dw = torch.zeros(Co, k, k, C, device=DEV)
+    dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=DEV)
+    K.conv_backward_pair(x, dy, dw, w, dx, shp, ws, accumulate=False, bnb=t_pair)
+    dx_sep = torch.empty_like(dx)
+    K.conv_dgrad(dy, w, dx_sep, shp, ws, accumulate=False, bnb=t_sep)
+    wref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (Co, C, k, k),
+                                       dy.float().permute(0, 3, 1, 2), stride=s,
+                                       padding=k // 2).permute(0, 2, 3, 1)
+    xref = torch.nn.grad.conv2d_input((N, C, H, W), w.float().permute(0, 3, 1, 2),
+                                      dy.float().permute(0, 3, 1, 2), stride=s,
+                                      padding=k // 2).permute(0, 2, 3, 1)
+    assert rel_err(dw, wref) < 5e-3
+    assert rel_err(dx, xref) < 1e-2
+    if with_bnb:
+        assert rel_err(t_pair.acc, t_sep.acc) < 1e-2
+    # accumulate epilogue into an existing dx
+    base = bf(torch.randn(N, H, W, C, device=DEV))
+    dx2 = base.clone()
+    dw.zero_()
+    K.conv_backward_pair(x, dy, dw, w, dx2, shp, ws, accumulate=True)
+    assert rel_err(dx2, xref + base.float()) < 1e-2
+
+
 def test_gemm_nt_with_epilogues():
     from metisfl_amd.ops import nn as K
     torch.manual_seed(3)
