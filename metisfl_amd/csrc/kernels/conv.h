@@ -63,7 +63,7 @@ struct ConvArgs {
 };
 
 ConvPlan plan_conv_gemm(const ConvGeom& g, bool dgrad = false);
-ConvPlan plan_conv_wgrad(const ConvGeom& g);
+ConvPlan plan_conv_wgrad(const ConvGeom& g, int target_blocks = 0);
 // number of output tiles (= split-K counter slots) of a gemm plan
 int conv_counter_slots(const ConvGeom& g, const ConvPlan& p);
 

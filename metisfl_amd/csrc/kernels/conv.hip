@@ -633,20 +633,38 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(ConvArgs a, float* __re
 // per layer pair.
 struct PairGrid {
   int dgx, dgy, dgz, wgx, wgy, wgz;
+  int order;  // block-id order: 0 dgrad first, 1 wgrad first, 2 alternating (MFL_CONV_PAIR_ORDER)
 };
 template <int BM, int BN, int KS, int ST, bool PAR>
 __global__ __launch_bounds__(256) void conv_bwd_pair_kernel(ConvArgs da, ConvArgs wa, float* __restrict__ dw,
                                                             PairGrid pg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  int id = blockIdx.x;
-  const int nd = pg.dgx * pg.dgy * pg.dgz;
-  if (id < nd) {
-    const int x = id % pg.dgx, r = id / pg.dgx;
+  const int id = blockIdx.x;
+  const int nd = pg.dgx * pg.dgy * pg.dgz, nw = pg.wgx * pg.wgy * pg.wgz;
+  bool isd;
+  int lid;
+  if (pg.order == 0) {
+    isd = id < nd;
+    lid = isd ? id : id - nd;
+  } else if (pg.order == 1) {
+    isd = id >= nw;
+    lid = isd ? id - nw : id;
+  } else {
+    const int m = min(nd, nw);
+    if (id < 2 * m) {
+      isd = !(id & 1);
+      lid = id >> 1;
+    } else {
+      isd = nd > nw;
+      lid = id - m;
+    }
+  }
+  if (isd) {
+    const int x = lid % pg.dgx, r = lid / pg.dgx;
     conv_gemm_body<BM, BN, true, KS, ST, 64, PAR>(
         da, BlkCoord{x, r % pg.dgy, r / pg.dgy, pg.dgx, pg.dgy, pg.dgz}, smem);
   } else {
-    id -= nd;
-    const int x = id % pg.wgx, r = id / pg.wgx;
+    const int x = lid % pg.wgx, r = lid / pg.wgx;
     conv_wgrad_body<KS, ST, 64>(wa, dw, BlkCoord{x, r % pg.wgy, r / pg.wgy, pg.wgx, pg.wgy, pg.wgz}, smem);
   }
 }
@@ -862,8 +880,9 @@ void launch_conv_dgrad_bnb(const ConvGeom& g, const ConvPlan& p, const uint16_t*
   else if (p.bm == 64 && p.bn == 64) launch_gemm_ks<64, 64, true>(a, p, s);
 }
 
-ConvPlan plan_conv_wgrad(const ConvGeom& g) {
-  static const int target = env_int("MFL_WGRAD_TARGET_BLOCKS", 512);
+ConvPlan plan_conv_wgrad(const ConvGeom& g, int target_blocks) {
+  static const int target_env = env_int("MFL_WGRAD_TARGET_BLOCKS", 512);
+  const int target = target_blocks > 0 ? target_blocks : target_env;
   static const int min_steps = env_int("MFL_WGRAD_MIN_KSTEPS", 8);
   ConvPlan p;
   p.bm = 64;
@@ -955,11 +974,14 @@ bool launch_conv_bwd_pair(const ConvGeom& gd, const ConvPlan& pd_in, const uint1
                           const ConvGeom& gw, const uint16_t* x, float* dw, hipStream_t s) {
   if (!conv_pair_enabled()) return false;
   if (!((pd_in.bm == 128 && pd_in.bn == 64) || (pd_in.bm == 64 && pd_in.bn == 64))) return false;
-  const ConvPlan pw = plan_conv_wgrad(gw);
+  static const int wg_target = env_int("MFL_PAIR_WGRAD_TARGET", 0);
+  const ConvPlan pw = plan_conv_wgrad(gw, wg_target);
   if (pw.bk != 64) return false;
   // the dgrad at BK = 64 with the SAME split count (the caller's workspace
   // and counter slots were sized for this plan)
   ConvPlan pd = pd_in;
+  static const int dg_div = env_int("MFL_PAIR_DGRAD_SPLIT_DIV", 1);
+  if (dg_div > 1) pd.splits = std::max(1, pd.splits / dg_div);  // fewer slices: fits the same workspace
   const int K = pd.par_mc ? ((gd.R + 1) / 2) * ((gd.S + 1) / 2) * gd.C : gd.K;
   const int ks64 = (K + 63) / 64;
   pd.bk = 64;
@@ -1000,6 +1022,8 @@ bool launch_conv_bwd_pair(const ConvGeom& gd, const ConvPlan& pd_in, const uint1
   pg.wgx = (gw.Ng + 63) / 64;
   pg.wgy = (gw.K + 63) / 64;
   pg.wgz = pw.splits;
+  static const int order = env_int("MFL_CONV_PAIR_ORDER", 0);
+  pg.order = order;
   if (pd.bm == 128) return launch_pair_bm<128, 64>(da, wa, dw, pg, s);
   return launch_pair_bm<64, 64>(da, wa, dw, pg, s);
 }
