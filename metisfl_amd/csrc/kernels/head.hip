@@ -27,18 +27,30 @@ __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ 
                                                    uint16_t* __restrict__ dx,
                                                    float* __restrict__ stats, int B, int backward,
                                                    float* __restrict__ dW, float* __restrict__ db) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];  // feat[C] | logits[K] | partials[R][C]
+  // feat[C] | logits[K] | partials[R][C] | W[K][C]
+  extern __shared__ __attribute__((aligned(16))) float sm[];
   float* f = sm;
   float* lg = sm + C;
   const int G = C >> 3;
   const int R = max(1, 256 / G);
   float* part = sm + C + ((K + 3) & ~3);
+  float* Ws = part + R * C;
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
   const float inv_hw = 1.f / (float)HW;
   const uint16_t* xb = x + (int64_t)b * HW * C;
   const int cg = t % G, rg = t / G;
+  // the classifier weights go to LDS alongside the pooling loads: the logits
+  // and the dx broadcast then read LDS instead of paying two more dependent
+  // global round trips in this one-workgroup-per-sample serial chain
+  {
+    const int n4 = K * C / 4;
+    const float4* W4 = reinterpret_cast<const float4*>(W);
+    float4* Ws4 = reinterpret_cast<float4*>(Ws);
+#pragma unroll 4
+    for (int i = t; i < n4; i += 256) Ws4[i] = W4[i];
+  }
   if (rg < R) {
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int h = rg; h < HW; h += R) {
@@ -61,7 +73,7 @@ __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ 
   __syncthreads();
   for (int k = wv; k < K; k += 4) {
     float s = 0.f;
-    for (int c = lane; c < C; c += 64) s += f[c] * W[(int64_t)k * C + c];
+    for (int c = lane; c < C; c += 64) s += f[c] * Ws[k * C + c];
     s = wave_sum(s);
     if (lane == 0) lg[k] = s + (bias ? bias[k] : 0.f);
   }
@@ -116,7 +128,7 @@ __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ 
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float s = 0.f;
-      for (int k = 0; k < K; ++k) s += lg[k] * W[(int64_t)k * C + 8 * cg + e];
+      for (int k = 0; k < K; ++k) s += lg[k] * Ws[k * C + 8 * cg + e];
       v[e] = s * inv_hw;
     }
     const uint4 pk = pack8(v);
@@ -129,7 +141,13 @@ void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W
                          int K, const int* labels, float* feat, float* dlogits, uint16_t* dx,
                          float* stats, bool backward, hipStream_t s, float* dW, float* db) {
   const int G = C / 8, R = G >= 256 ? 1 : 256 / G;
-  const size_t sm = (size_t)(C + ((K + 3) & ~3) + (size_t)R * C) * sizeof(float);
+  const size_t sm = (size_t)(C + ((K + 3) & ~3) + (size_t)R * C + (size_t)K * C) * sizeof(float);
+  static bool attr = false;
+  if (!attr && sm > 65536) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    attr = true;
+  }
   head_kernel<<<B, 256, sm, s>>>(x, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, B,
                                  backward ? 1 : 0, backward ? dW : nullptr, backward ? db : nullptr);
 }
