@@ -122,6 +122,53 @@ void run_gemm(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, cons
                           cur_stream(y));
 }
 
+// split-K workspace / stats pointers of a forward plan (as run_gemm)
+void gemm_ptrs(const mfl::ConvGeom& g, const mfl::ConvPlan& p, const c10::optional<torch::Tensor>& ws,
+               const c10::optional<torch::Tensor>& stats, float*& wsp, int*& counters, double*& st) {
+  wsp = nullptr;
+  counters = nullptr;
+  st = nullptr;
+  if (p.splits > 1) {
+    TORCH_CHECK(ws.has_value() && ws->defined(), "split-K workspace required");
+    check_f32(*ws, workspace_floats(g, p), "workspace");
+    counters = reinterpret_cast<int*>(ws->data_ptr<float>());
+    wsp = ws->data_ptr<float>() + counter_words(g, p);
+  }
+  if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(stats->is_cuda() && stats->is_contiguous() &&
+                    stats->scalar_type() == torch::kFloat64 && stats->numel() >= 2 * g.Ng,
+                "stats must be a contiguous fp64 device tensor of >= 2*Cout elements");
+    st = stats->data_ptr<double>();
+  }
+}
+
+// A downsampling block's conv1 (3x3, stride 2, pad 1) and projection shortcut
+// (1x1, stride 2) of the same x: one paired launch, else two.
+void conv_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c10::optional<torch::Tensor> ws1,
+                       c10::optional<torch::Tensor> stats1, torch::Tensor w2, torch::Tensor y2,
+                       c10::optional<torch::Tensor> ws2, c10::optional<torch::Tensor> stats2, int64_t N,
+                       int64_t H, int64_t W, int64_t C, int64_t Co) {
+  auto g1 = fwd_geom(N, H, W, C, Co, 3, 3, 2, 1);
+  auto g2 = fwd_geom(N, H, W, C, Co, 1, 1, 2, 0);
+  TORCH_CHECK(g1.M == g2.M, "conv1 / shortcut output sizes differ");
+  check_bf16(x, N * H * W * C, "x");
+  check_bf16(w1, Co * 9 * C, "w1");
+  check_bf16(w2, Co * C, "w2");
+  check_bf16(y1, (int64_t)g1.M * Co, "y1");
+  check_bf16(y2, (int64_t)g2.M * Co, "y2");
+  const auto p1 = mfl::plan_conv_gemm(g1, false), p2 = mfl::plan_conv_gemm(g2, false);
+  float *ys1, *ys2;
+  int *c1, *c2;
+  double *st1, *st2;
+  gemm_ptrs(g1, p1, ws1, stats1, ys1, c1, st1);
+  gemm_ptrs(g2, p2, ws2, stats2, ys2, c2, st2);
+  if (mfl::launch_conv_fwd_pair(g1, p1, bf(w1), bf(y1), ys1, c1, st1, g2, p2, bf(w2), bf(y2), ys2, c2, st2,
+                                bf(x), cur_stream(x)))
+    return;
+  run_gemm(g1, false, x, w1, y1, ws1, stats1, false);
+  run_gemm(g2, false, x, w2, y2, ws2, stats2, false);
+}
+
 void conv_forward(torch::Tensor x, torch::Tensor w, torch::Tensor y,
                   c10::optional<torch::Tensor> ws, c10::optional<torch::Tensor> stats, int64_t N,
                   int64_t H, int64_t W, int64_t C, int64_t Co, int64_t R, int64_t S,
@@ -278,6 +325,7 @@ void register_conv(pybind11::module& m) {
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_backward_pair", &conv_backward_pair);
+  m.def("conv_forward_pair", &conv_forward_pair);
   m.def("transpose_krsc", &transpose_krsc);
 }
 

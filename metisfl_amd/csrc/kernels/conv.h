@@ -88,6 +88,12 @@ struct BnBwdFusion {
 bool launch_conv_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const uint16_t* dy, const uint16_t* wt,
                           uint16_t* dx, float* ysplit, int* counters, bool accum, const BnBwdFusion* f,
                           const ConvGeom& gw, const uint16_t* x, float* dw, hipStream_t s);
+// A downsampling block's 3x3/s2 conv1 (g1) and 1x1/s2 shortcut (g2) forward
+// convolutions of the same input x in one launch (plans / workspaces / stats
+// as for launch_conv_gemm); false: not supported -- nothing was launched.
+bool launch_conv_fwd_pair(const ConvGeom& g1, const ConvPlan& p1, const uint16_t* w1, uint16_t* y1, float* ys1,
+                          int* cnt1, double* st1, const ConvGeom& g2, const ConvPlan& p2, const uint16_t* w2,
+                          uint16_t* y2, float* ys2, int* cnt2, double* st2, const uint16_t* x, hipStream_t s);
 // dgrad with the fused BN-backward reductions of the consumer layer
 void launch_conv_dgrad_bnb(const ConvGeom& g, const ConvPlan& p, const uint16_t* dy,
                            const uint16_t* wgt, uint16_t* dx, float* ysplit, int* counters,

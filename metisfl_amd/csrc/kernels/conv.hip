@@ -669,6 +669,27 @@ __global__ __launch_bounds__(256) void conv_bwd_pair_kernel(ConvArgs da, ConvArg
   }
 }
 
+// Two forward convolutions of one input in ONE launch: a downsampling
+// block's 3x3 / stride-2 conv1 and its 1x1 / stride-2 projection shortcut
+// (independent, each latency-bound at 64-128 workgroups), BK = 64 for both.
+// Block ids [0, n1) run conv1 (grid dgx/dgy/dgz), the rest the shortcut.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_fwd_pair_kernel(ConvArgs a1, ConvArgs a2, PairGrid pg) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int id = blockIdx.x;
+  const int n1 = pg.dgx * pg.dgy * pg.dgz;
+  if (id < n1) {
+    const int x = id % pg.dgx, r = id / pg.dgx;
+    conv_gemm_body<BM, BN, false, 3, 2, 64, false>(
+        a1, BlkCoord{x, r % pg.dgy, r / pg.dgy, pg.dgx, pg.dgy, pg.dgz}, smem);
+  } else {
+    const int lid = id - n1;
+    const int x = lid % pg.wgx, r = lid / pg.wgx;
+    conv_gemm_body<BM, BN, false, 1, 2, 64, false>(
+        a2, BlkCoord{x, r % pg.wgy, r / pg.wgy, pg.wgx, pg.wgy, pg.wgz}, smem);
+  }
+}
+
 // [Cout][R][S][Cin] -> [Cin][R][S][Cout]  (layout utility, not on the hot path)
 __global__ __launch_bounds__(256) void transpose_krsc_kernel(const uint16_t* __restrict__ w,
                                                              uint16_t* __restrict__ wt, int Co,
@@ -1026,6 +1047,56 @@ bool launch_conv_bwd_pair(const ConvGeom& gd, const ConvPlan& pd_in, const uint1
   pg.order = order;
   if (pd.bm == 128) return launch_pair_bm<128, 64>(da, wa, dw, pg, s);
   return launch_pair_bm<64, 64>(da, wa, dw, pg, s);
+}
+
+namespace {
+template <int BM, int BN>
+void launch_fwd_pair_t(const ConvArgs& a1, const ConvArgs& a2, const PairGrid& pg, hipStream_t s) {
+  size_t lds = (size_t)kStages * (BM + BN) * 64 * 2;
+  const size_t epi = ((size_t)BM * (BN + 4) + 256 * 16 + 8) * sizeof(float);
+  lds = std::max(lds, epi);
+  static bool attr = false;
+  set_lds_limit(&conv_fwd_pair_kernel<BM, BN>, lds, attr);
+  const unsigned n = (unsigned)(pg.dgx * pg.dgy * pg.dgz + pg.wgx * pg.wgy * pg.wgz);
+  conv_fwd_pair_kernel<BM, BN><<<n, 256, lds, s>>>(a1, a2, pg);
+}
+}  // namespace
+
+bool launch_conv_fwd_pair(const ConvGeom& g1, const ConvPlan& p1, const uint16_t* w1, uint16_t* y1, float* ys1,
+                          int* cnt1, double* st1, const ConvGeom& g2, const ConvPlan& p2, const uint16_t* w2,
+                          uint16_t* y2, float* ys2, int* cnt2, double* st2, const uint16_t* x, hipStream_t s) {
+  if (!conv_pair_enabled()) return false;
+  if (g1.R != 3 || g1.stride != 2 || g2.R != 1 || g2.stride != 2) return false;
+  if (p1.bm != p2.bm || p1.bn != p2.bn) return false;
+  if (!((p1.bm == 128 && p1.bn == 64) || (p1.bm == 64 && p1.bn == 64))) return false;
+  auto mk = [&](const ConvGeom& g, ConvPlan p, const uint16_t* w, uint16_t* y, float* ys, int* cn, double* st,
+                ConvArgs& a, int& gx, int& gy, int& gz) {
+    const int ks64 = (g.K + 63) / 64;
+    p.bk = 64;
+    p.kchunk = ((ks64 + p.splits - 1) / p.splits) * 64;  // same slices: the caller's workspace fits
+    a = ConvArgs{};
+    a.g = g;
+    a.src = x;
+    a.wgt = w;
+    a.src_bytes = range_bytes((int64_t)g.N * g.H * g.W * g.C);
+    a.wgt_bytes = range_bytes((int64_t)g.Ng * g.K);
+    a.y = y;
+    a.ysplit = ys;
+    a.counters = cn;
+    a.stats = st;
+    a.kchunk = p.kchunk;
+    fill_shifts(a);
+    gx = (g.M + p.bm - 1) / p.bm;
+    gy = (g.Ng + p.bn - 1) / p.bn;
+    gz = p.splits;
+  };
+  ConvArgs a1, a2;
+  PairGrid pg{};
+  mk(g1, p1, w1, y1, ys1, cnt1, st1, a1, pg.dgx, pg.dgy, pg.dgz);
+  mk(g2, p2, w2, y2, ys2, cnt2, st2, a2, pg.wgx, pg.wgy, pg.wgz);
+  if (p1.bm == 128) launch_fwd_pair_t<128, 64>(a1, a2, pg, s);
+  else launch_fwd_pair_t<64, 64>(a1, a2, pg, s);
+  return true;
 }
 
 void launch_transpose_krsc(const uint16_t* w, uint16_t* wt, int Co, int RS, int Ci, hipStream_t s) {

@@ -160,6 +160,11 @@ class ConvBN(Layer):
         s = self.shp
         self.x = x
         K.conv_forward(x, self.w16, self.z, s, self._split(), self.ws.acc(self.acc_f) if train else None)
+        return self.bn_forward(residual, train)
+
+    def bn_forward(self, residual: torch.Tensor | None = None, train: bool = True):
+        """The BN (+residual, +ReLU) half of forward(), for a z already computed."""
+        s = self.shp
         K.bn_apply(self.z, s.Co, self.ws.acc(self.acc_f), self.gamma, self.beta, self.mean,
                    self.invstd, self.rmean, self.rvar, self.y, residual, self.relu, train,
                    self.momentum, self.eps)
@@ -235,6 +240,15 @@ class BasicBlock(Layer):
         if self.sc is None:
             a = self.c1.forward(x, train=train)
             return self.c2.forward(a, residual=x, train=train)
+        if not self.c1.ws.overlap and self.c1.shp.R == 3 and self.c1.shp.stride == 2:
+            # conv1 and the projection shortcut in one paired launch
+            c1, sc = self.c1, self.sc
+            c1.x = sc.x = x
+            K.conv_forward_pair(x, c1.w16, c1.z, c1._split(), c1.ws.acc(c1.acc_f) if train else None,
+                                sc.w16, sc.z, sc._split(), sc.ws.acc(sc.acc_f) if train else None, c1.shp)
+            r = sc.bn_forward(train=train)
+            a = c1.bn_forward(train=train)
+            return self.c2.forward(a, residual=r, train=train)
         # projection shortcut runs concurrently with conv1 (side stream, own
         # split-K workspace); conv2 consumes both after the join
         with self.c1.ws.fork():

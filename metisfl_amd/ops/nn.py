@@ -159,6 +159,17 @@ def conv_wgrad(x, dy, dw, shp: ConvShape, accumulate: bool = False) -> None:
     dw.copy_(g.permute(0, 2, 3, 1).reshape(dw.shape))
 
 
+def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShape) -> None:
+    """A downsampling block's conv1 (3x3, stride 2; ``shp``) and its 1x1 / stride-2
+    projection shortcut of the same x -- one paired launch on the GPU."""
+    assert shp.R == 3 and shp.stride == 2
+    if x.is_cuda:
+        ops().conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp.N, shp.H, shp.W, shp.C, shp.Co)
+        return
+    conv_forward(x, w1, y1, shp, ws1, stats1)
+    conv_forward(x, w2, y2, ConvShape(shp.N, shp.H, shp.W, shp.C, shp.Co, 1, 1, 2, 0), ws2, stats2)
+
+
 def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
                        bnb: BnBwdTarget | None = None) -> None:
     """A layer's weight gradient (dw += ..., dw zero on entry) and input

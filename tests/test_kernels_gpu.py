@@ -206,6 +206,34 @@ def test_conv_backward_pair_matches_separate(case, with_bnb):
     assert rel_err(dx2, xref + base.float()) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(8, 32, 32, 64, 128), (32, 32, 32, 64, 128), (32, 16, 16, 128, 256),
+                                  (32, 8, 8, 256, 512)])
+def test_conv_forward_pair_matches_separate(case):
+    """A downsampling block's conv1 (3x3/s2) + shortcut (1x1/s2) in one paired
+    launch vs the two separate launches (outputs and fused BN statistics)."""
+    from metisfl_amd.ops import nn as K
+    N, H, W, C, Co = case
+    torch.manual_seed(6)
+    s1 = K.ConvShape(N, H, W, C, Co, 3, 3, 2, 1)
+    s2 = K.ConvShape(N, H, W, C, Co, 1, 1, 2, 0)
+    x = bf(torch.randn(N, H, W, C, device=DEV))
+    w1 = bf(torch.randn(Co, 3, 3, C, device=DEV) * 0.1)
+    w2 = bf(torch.randn(Co, 1, 1, C, device=DEV) * 0.1)
+    n = lambda s, m: max(4, K.conv_plan(m, s, torch.device(DEV)).workspace)
+    ws = [torch.zeros(max(n(s1, 0), n(s2, 0)), device=DEV) for _ in range(4)]
+    y = [torch.empty(N, s1.P, s1.Q, Co, dtype=torch.bfloat16, device=DEV) for _ in range(4)]
+    st = [torch.zeros(2 * Co, dtype=torch.float64, device=DEV) for _ in range(4)]
+    K.conv_forward_pair(x, w1, y[0], ws[0], st[0], w2, y[1], ws[1], st[1], s1)
+    K.conv_forward(x, w1, y[2], s1, ws[2], st[2])
+    K.conv_forward(x, w2, y[3], s2, ws[3], st[3])
+    r1 = F.conv2d(x.float().permute(0, 3, 1, 2), w1.float().permute(0, 3, 1, 2), stride=2, padding=1)
+    r2 = F.conv2d(x.float().permute(0, 3, 1, 2), w2.float().permute(0, 3, 1, 2), stride=2)
+    assert rel_err(y[0], r1.permute(0, 2, 3, 1)) < 1e-2
+    assert rel_err(y[1], r2.permute(0, 2, 3, 1)) < 1e-2
+    assert rel_err(y[0], y[2]) < 1e-2 and rel_err(y[1], y[3]) < 1e-2
+    assert rel_err(st[0], st[2]) < 1e-3 and rel_err(st[1], st[3]) < 1e-3
+
+
 def test_gemm_nt_with_epilogues():
     from metisfl_amd.ops import nn as K
     torch.manual_seed(3)
