@@ -218,10 +218,38 @@ void bn_stats(torch::Tensor x, int64_t C, torch::Tensor acc) {
 
 // y = relu?(bn(x) (+ residual)).  train: statistics from acc (sums over M rows),
 // publishes mean/invstd and updates running stats; eval: running statistics.
+mfl::BnFwdArgs bn_fwd_args(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torch::Tensor gamma,
+                           torch::Tensor beta, torch::Tensor mean, torch::Tensor invstd,
+                           torch::Tensor run_mean, torch::Tensor run_var, c10::optional<torch::Tensor> residual,
+                           torch::Tensor y, bool relu, bool train, double momentum, double eps);
+
 void bn_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torch::Tensor gamma,
               torch::Tensor beta, torch::Tensor mean, torch::Tensor invstd,
               torch::Tensor run_mean, torch::Tensor run_var, c10::optional<torch::Tensor> residual,
               torch::Tensor y, bool relu, bool train, double momentum, double eps) {
+  mfl::launch_bn_apply(bn_fwd_args(x, C, acc, gamma, beta, mean, invstd, run_mean, run_var, residual, y, relu,
+                                   train, momentum, eps),
+                       cur_stream(x));
+}
+
+// shortcut BN (no ReLU) + conv1 BN (ReLU) of a downsampling block, one launch
+void bn_apply_pair(torch::Tensor x1, torch::Tensor gamma1, torch::Tensor beta1, torch::Tensor mean1,
+                   torch::Tensor invstd1, torch::Tensor rm1, torch::Tensor rv1, c10::optional<torch::Tensor> acc1,
+                   torch::Tensor y1, torch::Tensor x2, torch::Tensor gamma2, torch::Tensor beta2,
+                   torch::Tensor mean2, torch::Tensor invstd2, torch::Tensor rm2, torch::Tensor rv2,
+                   c10::optional<torch::Tensor> acc2, torch::Tensor y2, int64_t C, bool train, double momentum,
+                   double eps) {
+  const auto a1 = bn_fwd_args(x1, C, acc1, gamma1, beta1, mean1, invstd1, rm1, rv1, c10::nullopt, y1, false,
+                              train, momentum, eps);
+  const auto a2 = bn_fwd_args(x2, C, acc2, gamma2, beta2, mean2, invstd2, rm2, rv2, c10::nullopt, y2, true,
+                              train, momentum, eps);
+  mfl::launch_bn_apply_pair(a1, a2, cur_stream(x1));
+}
+
+mfl::BnFwdArgs bn_fwd_args(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torch::Tensor gamma,
+                           torch::Tensor beta, torch::Tensor mean, torch::Tensor invstd,
+                           torch::Tensor run_mean, torch::Tensor run_var, c10::optional<torch::Tensor> residual,
+                           torch::Tensor y, bool relu, bool train, double momentum, double eps) {
   check_nhwc(x, C);
   check_nhwc(y, C);
   TORCH_CHECK(y.numel() == x.numel(), "bn y size");
@@ -251,7 +279,7 @@ void bn_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torc
   a.eps = (float)eps;
   a.train = train ? 1 : 0;
   a.relu = relu ? 1 : 0;
-  mfl::launch_bn_apply(a, cur_stream(x));
+  return a;
 }
 
 // BN(+ReLU) backward: reduce into acc (fp64 atomics; must be zero on entry),
@@ -375,6 +403,7 @@ void register_ckks(pybind11::module& m);
 PYBIND11_MODULE(_ops, m) {
   m.doc() = "metisfl_amd hand-written HIP (gfx950) kernels";
   m.def("fused_optimizer", &fused_optimizer);
+  m.def("bn_apply_pair", &bn_apply_pair);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("scale_f32", &scale_f32);
   m.def("tick", &tick);

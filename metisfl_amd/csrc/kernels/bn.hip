@@ -92,16 +92,16 @@ void launch_bn_stats(const uint16_t* x, int64_t M, int C, double* acc, hipStream
 // Forward apply: y = relu?(x * scale + shift (+ residual)).
 // train: statistics from acc (sum, sumsq over M rows); else from running stats.
 template <bool RES, bool RELU>
-__global__ __launch_bounds__(256) void bn_apply_kernel(BnFwdArgs a, int64_t nvec) {
-  extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
+__device__ __forceinline__ void bn_apply_body(const BnFwdArgs& a, int64_t nvec, int bx, int gx,
+                                              float* coef /* [2][C] LDS */) {
   const int C = a.C;
   const uint4* X = reinterpret_cast<const uint4*>(a.x);
   const uint4* R = reinterpret_cast<const uint4*>(a.residual);
   // The first vectors go out before the per-channel prologue: its acc loads
   // and fp64 math then overlap the activation loads instead of preceding them
   // (at ResNet-18 sizes every thread handles one or two vectors).
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gx * blockDim.x;
+  int64_t i = (int64_t)bx * blockDim.x + threadIdx.x;
   uint4 xv = {0, 0, 0, 0}, rv = {0, 0, 0, 0};
   if (i < nvec) {
     xv = X[i];
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(BnFwdArgs a, int64_t nvec
     const float sc = g * is;
     coef[c] = sc;
     coef[C + c] = a.beta[c] - (float)mu * sc;
-    if (a.train && blockIdx.x == 0) {
+    if (a.train && bx == 0) {
       a.mean[c] = (float)mu;
       a.invstd[c] = is;
       if (a.run_mean) {
@@ -155,6 +155,28 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(BnFwdArgs a, int64_t nvec
     }
     reinterpret_cast<uint4*>(a.y)[i] = pack8(f);
   }
+}
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_kernel(BnFwdArgs a, int64_t nvec) {
+  extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
+  bn_apply_body<RES, RELU>(a, nvec, blockIdx.x, gridDim.x, coef);
+}
+
+// A downsampling block's two BatchNorms (projection shortcut: no ReLU; conv1:
+// ReLU; neither with a residual) in one launch: blocks [0, g1) apply a1.
+__global__ __launch_bounds__(256) void bn_apply_pair_kernel(BnFwdArgs a1, int64_t n1, int g1, BnFwdArgs a2,
+                                                            int64_t n2) {
+  extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][max C]
+  if ((int)blockIdx.x < g1) bn_apply_body<false, false>(a1, n1, blockIdx.x, g1, coef);
+  else bn_apply_body<false, true>(a2, n2, blockIdx.x - g1, gridDim.x - g1, coef);
+}
+
+void launch_bn_apply_pair(const BnFwdArgs& a1, const BnFwdArgs& a2, hipStream_t s) {
+  const int64_t n1 = a1.M * a1.C / 8, n2 = a2.M * a2.C / 8;
+  const unsigned g1 = stream_grid(n1, 256, 2048), g2 = stream_grid(n2, 256, 2048);
+  const size_t sm = 2 * (size_t)(a1.C > a2.C ? a1.C : a2.C) * sizeof(float);
+  bn_apply_pair_kernel<<<g1 + g2, 256, sm, s>>>(a1, n1, (int)g1, a2, n2);
 }
 
 void launch_bn_apply(const BnFwdArgs& a, hipStream_t s) {

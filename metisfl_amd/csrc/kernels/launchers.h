@@ -85,6 +85,9 @@ struct BnBwdArgs {
 int bn_stats_blocks(int64_t M, int C);
 void launch_bn_stats(const uint16_t* x, int64_t M, int C, double* acc, hipStream_t s);
 void launch_bn_apply(const BnFwdArgs& a, hipStream_t s);
+// a1: no residual, no ReLU; a2: no residual, ReLU (a downsampling block's
+// shortcut and conv1 BatchNorms) in one launch
+void launch_bn_apply_pair(const BnFwdArgs& a1, const BnFwdArgs& a2, hipStream_t s);
 void launch_bn_bwd_reduce(const uint16_t* dy, const uint16_t* x, const uint16_t* y,
                           const float* mean, const float* invstd, int64_t M, int C, double* acc,
                           hipStream_t s);

@@ -246,8 +246,17 @@ class BasicBlock(Layer):
             c1.x = sc.x = x
             K.conv_forward_pair(x, c1.w16, c1.z, c1._split(), c1.ws.acc(c1.acc_f) if train else None,
                                 sc.w16, sc.z, sc._split(), sc.ws.acc(sc.acc_f) if train else None, c1.shp)
-            r = sc.bn_forward(train=train)
-            a = c1.bn_forward(train=train)
+            if x.is_cuda and hasattr(K.ops(), "bn_apply_pair") and not sc.relu and c1.relu:
+                # ... and their two BatchNorms in one launch
+                K.ops().bn_apply_pair(sc.z, sc.gamma, sc.beta, sc.mean, sc.invstd, sc.rmean, sc.rvar,
+                                      sc.ws.acc(sc.acc_f) if train else None, sc.y,
+                                      c1.z, c1.gamma, c1.beta, c1.mean, c1.invstd, c1.rmean, c1.rvar,
+                                      c1.ws.acc(c1.acc_f) if train else None, c1.y,
+                                      c1.shp.Co, train, c1.momentum, c1.eps)
+                r, a = sc.y, c1.y
+            else:
+                r = sc.bn_forward(train=train)
+                a = c1.bn_forward(train=train)
             return self.c2.forward(a, residual=r, train=train)
         # projection shortcut runs concurrently with conv1 (side stream, own
         # split-K workspace); conv2 consumes both after the join
