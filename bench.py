@@ -20,7 +20,13 @@ learners, so total work per round is constant: scaling is "strong" and
 Data are synthetic tensors of CIFAR-10's shape, weights random-init of the
 ResNet-18 architecture (no network for datasets/checkpoints).
 
-Launch: ``python bench.py`` (1 GPU) or
+Precision: ``--dtype fp32`` (default) is the reference's precision -- the
+reference trains fp32 Keras models (examples/keras/models/cifar_cnn.py:19-41,
+keras_model_ops.py:117-197) -- on the exact fp32 MFMA kernels (conv32.hip);
+``--dtype bf16`` is the mixed-precision option, reported separately.
+
+Launch: ``python bench.py`` (1 GPU), ``python bench.py --gpus N`` (spawns its
+own N rank processes before touching any GPU), or under
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1
 --master-port P bench.py --gpus N``.
 """
@@ -55,8 +61,18 @@ def main() -> int:
     ap.add_argument("--secure-aggregation", action="store_true",
                     help="BASELINE config 4: CKKS secure aggregation (device encrypt / int64 "
                          "all-reduce of ciphertexts / device decrypt)")
+    ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="compute precision: fp32 = reference precision (default), bf16 = mixed")
+    ap.add_argument("--width-mult", type=float, default=1.0, help=argparse.SUPPRESS)  # CPU plumbing tests only
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return _spawn_ranks(args.gpus)
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+        return 2
 
     import torch
 
@@ -67,8 +83,6 @@ def main() -> int:
 
     comm = Comm()
     n = comm.world
-    if args.gpus != n and comm.rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={n}; using {n}", file=sys.stderr)
     dev = comm.device
     torch.manual_seed(1234 + comm.rank)
 
@@ -83,7 +97,8 @@ def main() -> int:
     yte = torch.randint(0, 10, (n_test,), generator=g, device=dev)
 
     opt = OptimizerSpec("momentum_sgd", args.lr, momentum=args.momentum)
-    net = ResNet18(batch_size=args.batch, device=dev, optimizer=opt, seed=7)
+    net = ResNet18(batch_size=args.batch, device=dev, optimizer=opt, seed=7, dtype=args.dtype,
+                   width_mult=args.width_mult)
     train_ds = net.make_dataset(xtr, ytr, seed=comm.rank)
     test_ds = net.make_dataset(xte, yte, seed=comm.rank, shuffle=False)
     del xtr, xte
@@ -125,6 +140,15 @@ def main() -> int:
     round_ms = elapsed * 1e3 / max(1, args.steps)
     rounds_per_s = args.steps / elapsed if elapsed > 0 else 0.0
     updates = fed.num_local_updates[0]
+    agg_ms = sum(r.aggregation_ms for r in timed) / max(1, len(timed))
+    model_bytes = net.state.model32.numel() * 4
+    if n == 1:
+        aggregation = "none (single learner: the round ends with the local model)"
+    elif args.secure_aggregation:
+        aggregation = ("PWA(NUM_TRAINING_EXAMPLES) over RNS-CKKS (N=8192, 52-bit scale): "
+                       "device encrypt, int64 RCCL all-reduce of ciphertexts, device decrypt")
+    else:
+        aggregation = "FedAvg(NUM_TRAINING_EXAMPLES): scale kernel + one RCCL all-reduce"
     out = {
         "metric": METRIC,
         "value": rounds_per_s,
@@ -136,7 +160,7 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": (rounds_per_s / BASELINE_VALUE) if BASELINE_VALUE else None,
-        "dtype": "bf16",
+        "dtype": args.dtype,
         "data": "synthetic (CIFAR-10 shapes, IID shards), random-init ResNet-18",
         "config": {
             "model": "resnet18-cifar",
@@ -148,17 +172,18 @@ def main() -> int:
             "local_epochs": args.local_epochs,
             "local_updates_per_round": updates,
             "optimizer": f"momentum_sgd(lr={args.lr}, momentum={args.momentum})",
-            "aggregation": ("PWA(NUM_TRAINING_EXAMPLES) over RNS-CKKS (N=8192, 52-bit scale): "
-                            "device encrypt, int64 RCCL all-reduce of ciphertexts, device decrypt"
-                            if args.secure_aggregation else "FedAvg(NUM_TRAINING_EXAMPLES), RCCL all-reduce"),
+            "aggregation": aggregation,
             "protocol": "synchronous",
             "parallelism": f"fedavg-dp{n}",
             "test_eval": not args.no_eval,
+            **({"width_mult": args.width_mult} if args.width_mult != 1.0 else {}),
         },
         "round_ms": round_ms,
         "rounds_per_s": rounds_per_s,
         "train_ms_mean": sum(r.train_ms for r in timed) / max(1, len(timed)),
-        "aggregation_ms_mean": sum(r.aggregation_ms for r in timed) / max(1, len(timed)),
+        "aggregation_ms_mean": agg_ms,
+        "collective": {"backend": comm.backend, "world_size": n, "model_bytes": model_bytes,
+                       "allreduce_gbps": (model_bytes / (agg_ms * 1e-3) / 1e9) if n > 1 and agg_ms > 0 else None},
         "he_ms_mean": ({k: sum(r.he_stats[k] for r in timed) / max(1, len(timed))
                         for k in ("encrypt_ms", "allreduce_ms", "decrypt_ms")}
                        if args.secure_aggregation and timed else None),
@@ -172,6 +197,22 @@ def main() -> int:
                 f.write(line + "\n")
     comm.close()
     return 0
+
+
+def _spawn_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: start N rank processes with
+    torch.distributed.run (before this process touches any GPU) and relay
+    their output; rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
 
 
 if __name__ == "__main__":

@@ -1,0 +1,303 @@
+// torch binding for the fp32 (reference-precision) learner kernels:
+// conv32.hip (fwd / dgrad / wgrad), bn32.hip, the fp32 head and the batch
+// gather.  As in the other bindings, shapes / dtypes are validated on the
+// host before any launch (the kernels index with 32-bit offsets and trust
+// their geometry) and every launch goes to the caller's current HIP stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include "kernels/conv32.h"
+#include "kernels/launchers.h"
+
+namespace {
+
+hipStream_t cur_stream(const torch::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+void check_f32(const torch::Tensor& t, int64_t numel, const char* nm, bool exact = true) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), nm, " must be a contiguous device tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, nm, " must be fp32");
+  if (exact) {
+    TORCH_CHECK(t.numel() == numel, nm, " has ", t.numel(), " elements, expected ", numel);
+  } else {
+    TORCH_CHECK(t.numel() >= numel, nm, " too small: ", t.numel(), " < ", numel);
+  }
+}
+float* fp(const torch::Tensor& t) { return t.data_ptr<float>(); }
+template <typename T>
+T* opt_ptr(const c10::optional<torch::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->is_contiguous(), "optional operand must be a contiguous device tensor");
+  return reinterpret_cast<T*>(t->data_ptr());
+}
+
+int out_dim(int64_t in, int64_t k, int64_t stride, int64_t pad) { return (int)((in + 2 * pad - k) / stride + 1); }
+
+mfl::ConvGeom fwd_geom(int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co, int64_t R, int64_t S, int64_t stride,
+                       int64_t pad) {
+  TORCH_CHECK(C % 4 == 0 && Co % 4 == 0, "fp32 conv channels must be multiples of 4 (got ", C, ", ", Co, ")");
+  TORCH_CHECK(R == S && (R == 1 || R == 3) && (stride == 1 || stride == 2),
+              "fp32 conv supports 1x1 / 3x3 kernels at stride 1 / 2");
+  mfl::ConvGeom g{};
+  g.N = (int)N; g.H = (int)H; g.W = (int)W; g.C = (int)C;
+  g.P = out_dim(H, R, stride, pad);
+  g.Q = out_dim(W, S, stride, pad);
+  g.R = (int)R; g.S = (int)S; g.stride = (int)stride; g.pad = (int)pad;
+  g.M = (int)(N * g.P * g.Q);
+  g.K = (int)(R * S * C);
+  g.Ng = (int)Co;
+  TORCH_CHECK((int64_t)N * H * W * C * 4 < (1LL << 31) && (int64_t)g.M * Co * 4 < (1LL << 31),
+              "activation too large for 32-bit byte offsets");
+  return g;
+}
+mfl::ConvGeom dgrad_geom(int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co, int64_t R, int64_t S,
+                         int64_t stride, int64_t pad) {
+  const mfl::ConvGeom f = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
+  mfl::ConvGeom g{};
+  g.N = f.N; g.H = f.P; g.W = f.Q; g.C = (int)Co;
+  g.P = (int)H; g.Q = (int)W;
+  g.R = f.R; g.S = f.S; g.stride = f.stride; g.pad = f.pad;
+  g.M = (int)(N * H * W);
+  g.K = (int)(R * S * Co);
+  g.Ng = (int)C;
+  return g;
+}
+
+constexpr int64_t kCounterWords = 1024;
+int64_t ws_floats(const mfl::ConvGeom& g, const mfl::ConvPlan& p) {
+  if (p.splits <= 1) return 0;
+  TORCH_CHECK(mfl::conv32_counter_slots(g, p) <= kCounterWords, "split-K plan has too many tiles");
+  return kCounterWords + (int64_t)p.splits * mfl::conv32_counter_slots(g, p) * p.bm * p.bn;
+}
+
+// mode 0 fwd / 1 dgrad / 2 wgrad -> [bm, bn, splits, kchunk, stats_rows, workspace_floats]
+std::vector<int64_t> conv32_plan(int64_t mode, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co, int64_t R,
+                                 int64_t S, int64_t stride, int64_t pad) {
+  if (mode == 2) {
+    const auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
+    const auto p = mfl::plan_conv32(g, 2);
+    return {p.bm, p.bn, p.splits, p.kchunk, 0, 0};
+  }
+  const auto g = mode == 0 ? fwd_geom(N, H, W, C, Co, R, S, stride, pad) : dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
+  const auto p = mfl::plan_conv32(g, (int)mode);
+  return {p.bm, p.bn, p.splits, p.kchunk, mode == 0 ? 1 : 0, ws_floats(g, p)};
+}
+
+void run(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const torch::Tensor& w, const torch::Tensor& y,
+         const c10::optional<torch::Tensor>& ws, double* stats, bool accum, const mfl::BnBwdFusion32* bnb) {
+  const auto p = mfl::plan_conv32(g, dgrad ? 1 : 0);
+  float* slab = nullptr;
+  int* counters = nullptr;
+  if (p.splits > 1) {
+    TORCH_CHECK(ws.has_value() && ws->defined(), "split-K workspace required");
+    check_f32(*ws, ws_floats(g, p), "workspace", false);
+    counters = reinterpret_cast<int*>(ws->data_ptr<float>());
+    slab = ws->data_ptr<float>() + kCounterWords;
+  }
+  mfl::launch_conv32_gemm(g, dgrad, p, fp(src), fp(w), fp(y), slab, counters, stats, accum, bnb, cur_stream(y));
+}
+
+double* stats_ptr(const c10::optional<torch::Tensor>& st, int64_t C) {
+  if (!st.has_value() || !st->defined()) return nullptr;
+  TORCH_CHECK(st->is_cuda() && st->is_contiguous() && st->scalar_type() == torch::kFloat64 && st->numel() >= 2 * C,
+              "stats must be a contiguous fp64 device tensor of >= 2*C elements");
+  return st->data_ptr<double>();
+}
+
+void conv32_forward(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::optional<torch::Tensor> ws,
+                    c10::optional<torch::Tensor> stats, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co,
+                    int64_t R, int64_t S, int64_t stride, int64_t pad) {
+  const auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
+  check_f32(x, (int64_t)N * H * W * C, "x");
+  check_f32(w, (int64_t)Co * R * S * C, "w");
+  check_f32(y, (int64_t)g.M * Co, "y");
+  run(g, false, x, w, y, ws, stats_ptr(stats, Co), false, nullptr);
+}
+
+void conv32_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, c10::optional<torch::Tensor> ws, int64_t N,
+                  int64_t H, int64_t W, int64_t C, int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                  bool accumulate, c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
+                  c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
+                  c10::optional<torch::Tensor> bn_acc) {
+  const auto g = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
+  check_f32(dy, (int64_t)N * g.H * g.W * Co, "dy");
+  check_f32(w, (int64_t)Co * R * S * C, "w");
+  check_f32(dx, (int64_t)N * H * W * C, "dx");
+  mfl::BnBwdFusion32 f;
+  const bool fuse = bn_acc.has_value() && bn_acc->defined();
+  if (fuse) {
+    TORCH_CHECK(bn_z.has_value() && bn_mean.has_value() && bn_invstd.has_value(), "bn fusion operands");
+    check_f32(*bn_z, dx.numel(), "bn_z");
+    if (bn_y.has_value() && bn_y->defined()) check_f32(*bn_y, dx.numel(), "bn_y");
+    check_f32(*bn_mean, C, "bn_mean");
+    check_f32(*bn_invstd, C, "bn_invstd");
+    f.z = fp(*bn_z);
+    f.y = opt_ptr<float>(bn_y);
+    f.mean = fp(*bn_mean);
+    f.invstd = fp(*bn_invstd);
+    f.acc = stats_ptr(bn_acc, C);
+  }
+  run(g, true, dy, w, dx, ws, nullptr, accumulate, fuse ? &f : nullptr);
+}
+
+void conv32_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t N, int64_t H, int64_t W, int64_t C,
+                  int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate) {
+  const auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
+  check_f32(x, (int64_t)N * H * W * C, "x");
+  check_f32(dy, (int64_t)g.M * Co, "dy");
+  check_f32(dw, (int64_t)Co * R * S * C, "dw");
+  const auto p = mfl::plan_conv32(g, 2);
+  if (!accumulate && p.splits > 1) dw.zero_();
+  mfl::launch_conv32_wgrad(g, p, fp(x), fp(dy), fp(dw), accumulate, cur_stream(dw));
+}
+
+// ---- BatchNorm -----------------------------------------------------------
+void check_nhwc32(const torch::Tensor& x, int64_t C) {
+  check_f32(x, 0, "activation", false);
+  TORCH_CHECK(x.numel() % C == 0, "NHWC tensor not divisible by C");
+  TORCH_CHECK(C % 4 == 0 && C <= 4096, "BN channels must be a multiple of 4, <= 4096");
+}
+void check_pc(const torch::Tensor& t, int64_t C, const char* nm) { check_f32(t, C, nm); }
+const double* acc_ptr(const torch::Tensor& acc, int64_t C) {
+  TORCH_CHECK(acc.is_cuda() && acc.is_contiguous() && acc.scalar_type() == torch::kFloat64 && acc.numel() >= 2 * C,
+              "BN accumulator must be a contiguous fp64 device tensor of >= 2*C elements");
+  return acc.data_ptr<double>();
+}
+
+void bn32_stats(torch::Tensor x, int64_t C, torch::Tensor acc) {
+  check_nhwc32(x, C);
+  acc_ptr(acc, C);
+  mfl::launch_bn32_stats(fp(x), x.numel() / C, (int)C, acc.data_ptr<double>(), cur_stream(x));
+}
+
+void bn32_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torch::Tensor gamma, torch::Tensor beta,
+                torch::Tensor mean, torch::Tensor invstd, torch::Tensor run_mean, torch::Tensor run_var,
+                c10::optional<torch::Tensor> residual, torch::Tensor y, bool relu, bool train, double momentum,
+                double eps) {
+  check_nhwc32(x, C);
+  check_nhwc32(y, C);
+  TORCH_CHECK(y.numel() == x.numel(), "bn y size");
+  for (auto* t : {&gamma, &beta, &mean, &invstd, &run_mean, &run_var}) check_pc(*t, C, "bn param");
+  mfl::BnFwdArgs32 a{};
+  a.x = fp(x);
+  if (residual.has_value() && residual->defined()) {
+    check_nhwc32(*residual, C);
+    TORCH_CHECK(residual->numel() == x.numel(), "residual size");
+    a.residual = fp(*residual);
+  }
+  a.y = fp(y);
+  if (train) {
+    TORCH_CHECK(acc.has_value() && acc->defined(), "train-mode BN needs the statistics accumulator");
+    a.acc = acc_ptr(*acc, C);
+  }
+  a.gamma = fp(gamma);
+  a.beta = fp(beta);
+  a.mean = fp(mean);
+  a.invstd = fp(invstd);
+  a.run_mean = fp(run_mean);
+  a.run_var = fp(run_var);
+  a.M = x.numel() / C;
+  a.C = (int)C;
+  a.momentum = (float)momentum;
+  a.eps = (float)eps;
+  a.train = train ? 1 : 0;
+  a.relu = relu ? 1 : 0;
+  mfl::launch_bn32_apply(a, cur_stream(x));
+}
+
+void bn32_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C, torch::Tensor gamma,
+                   torch::Tensor mean, torch::Tensor invstd, torch::Tensor acc, c10::optional<torch::Tensor> dgamma,
+                   c10::optional<torch::Tensor> dbeta, torch::Tensor dx, c10::optional<torch::Tensor> dy_masked,
+                   bool presummed) {
+  check_nhwc32(dy, C);
+  check_nhwc32(x, C);
+  check_nhwc32(dx, C);
+  TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel(), "bn bwd sizes");
+  for (auto* t : {&gamma, &mean, &invstd}) check_pc(*t, C, "bn param");
+  mfl::BnBwdArgs32 a{};
+  a.dy = fp(dy);
+  a.x = fp(x);
+  if (y.has_value() && y->defined()) {
+    check_nhwc32(*y, C);
+    TORCH_CHECK(y->numel() == x.numel(), "bn bwd y");
+    a.y = fp(*y);
+  }
+  if (dy_masked.has_value() && dy_masked->defined()) {
+    check_nhwc32(*dy_masked, C);
+    TORCH_CHECK(a.y != nullptr && dy_masked->numel() == x.numel(), "dy_masked requires y");
+    a.dy_masked = fp(*dy_masked);
+  }
+  if (dgamma.has_value() && dgamma->defined()) { check_pc(*dgamma, C, "dgamma"); a.dgamma = fp(*dgamma); }
+  if (dbeta.has_value() && dbeta->defined()) { check_pc(*dbeta, C, "dbeta"); a.dbeta = fp(*dbeta); }
+  a.acc = acc_ptr(acc, C);
+  a.gamma = fp(gamma);
+  a.mean = fp(mean);
+  a.invstd = fp(invstd);
+  a.dx = fp(dx);
+  a.M = x.numel() / C;
+  a.C = (int)C;
+  auto s = cur_stream(x);
+  if (!presummed)
+    mfl::launch_bn32_bwd_reduce(a.dy, a.x, a.y, a.mean, a.invstd, a.M, a.C, acc.data_ptr<double>(), s);
+  mfl::launch_bn32_bwd_apply(a, s);
+}
+
+// ---- head / data ---------------------------------------------------------
+void head32_forward_backward(torch::Tensor x, int64_t B, int64_t HW, int64_t C, torch::Tensor W,
+                             c10::optional<torch::Tensor> bias, torch::Tensor labels,
+                             c10::optional<torch::Tensor> feat, c10::optional<torch::Tensor> dlogits,
+                             c10::optional<torch::Tensor> dx, c10::optional<torch::Tensor> stats, bool backward,
+                             c10::optional<torch::Tensor> dW, c10::optional<torch::Tensor> db) {
+  check_f32(x, B * HW * C, "head x");
+  check_f32(W, 0, "head W", false);
+  TORCH_CHECK(W.numel() % C == 0, "head W");
+  const int64_t K = W.numel() / C;
+  TORCH_CHECK(labels.is_cuda() && labels.is_contiguous() && labels.scalar_type() == torch::kInt32 &&
+                  labels.numel() >= B, "labels");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && K <= 1024, "head: C must be a multiple of 8 (<= 2048), K <= 1024");
+  const bool fuse = dW.has_value() && dW->defined();
+  if (fuse) {
+    check_f32(*dW, K * C, "head dW");
+    if (db.has_value() && db->defined()) check_f32(*db, K, "head db");
+  }
+  if (backward) {
+    TORCH_CHECK(feat.has_value() && dlogits.has_value() && dx.has_value(), "bwd buffers");
+    TORCH_CHECK(feat->numel() >= B * C && dlogits->numel() >= B * K, "bwd buffer sizes");
+    check_f32(*dx, x.numel(), "head dx");
+  }
+  mfl::launch_head32_fwd_bwd(fp(x), (int)B, (int)HW, (int)C, fp(W), opt_ptr<float>(bias), (int)K,
+                             labels.data_ptr<int>(), opt_ptr<float>(feat), opt_ptr<float>(dlogits),
+                             opt_ptr<float>(dx), opt_ptr<float>(stats), backward, cur_stream(x),
+                             fuse ? fp(*dW) : nullptr, fuse ? opt_ptr<float>(db) : nullptr);
+}
+
+// fp32 rows are gathered as 16-B units, like the bf16 ones
+void gather_batch32(torch::Tensor shard, torch::Tensor labels, torch::Tensor perm, torch::Tensor step,
+                    int64_t steps_per_epoch, int64_t B, torch::Tensor xb, torch::Tensor yb) {
+  check_f32(shard, 0, "shard", false);
+  check_f32(xb, 0, "xb", false);
+  for (auto* t : {&labels, &perm, &step, &yb})
+    TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == torch::kInt32, "int32 operand");
+  const int64_t n = labels.numel();
+  TORCH_CHECK(n > 0 && shard.numel() % n == 0, "shard rows");
+  const int64_t row = shard.numel() / n;
+  TORCH_CHECK(row % 4 == 0, "row must be a multiple of 4 fp32 elements");
+  TORCH_CHECK(xb.numel() == B * row && yb.numel() >= B, "batch buffers");
+  TORCH_CHECK(perm.numel() >= steps_per_epoch * B, "permutation too short");
+  mfl::launch_gather_batch(reinterpret_cast<const uint16_t*>(shard.data_ptr()), labels.data_ptr<int>(),
+                           perm.data_ptr<int>(), step.data_ptr<int>(), (int)steps_per_epoch, (int)B, row * 2,
+                           reinterpret_cast<uint16_t*>(xb.data_ptr()), yb.data_ptr<int>(), cur_stream(shard));
+}
+
+}  // namespace
+
+void register_fp32(pybind11::module& m) {
+  m.def("conv32_plan", &conv32_plan);
+  m.def("conv32_forward", &conv32_forward);
+  m.def("conv32_dgrad", &conv32_dgrad);
+  m.def("conv32_wgrad", &conv32_wgrad);
+  m.def("bn32_stats", &bn32_stats);
+  m.def("bn32_apply", &bn32_apply);
+  m.def("bn32_backward", &bn32_backward);
+  m.def("head32_forward_backward", &head32_forward_backward);
+  m.def("gather_batch32", &gather_batch32);
+}

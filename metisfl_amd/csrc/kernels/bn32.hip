@@ -1,0 +1,264 @@
+// K12 (fp32): BatchNorm forward / backward for NHWC fp32 activations -- the
+// reference-precision twin of bn.hip (same launch design: statistics arrive
+// as fp64 sums from the producing conv's epilogue, the apply kernel derives
+// mean / inv-std / scale / shift in its prologue and block 0 publishes the
+// saved statistics and the running averages; backward is one reduce (or
+// none, when the dgrad epilogue already summed) plus one apply).
+// Each lane moves 4 channels (one 16-B float4).  C % 4 == 0.
+#include "kernels/common.h"
+#include "kernels/launchers.h"
+
+namespace mfl {
+
+namespace {
+
+int blocks_for(int64_t M, int C) {
+  const int tpr = C / 4;
+  const int rpp = tpr >= 256 ? 1 : 256 / tpr;
+  int64_t nb = (M + (int64_t)rpp * 8 - 1) / ((int64_t)rpp * 8);
+  if (nb > 512) nb = 512;
+  if (nb < 1) nb = 1;
+  return (int)nb;
+}
+
+// per-thread float4 partials (s, q) over rows -> fp64 atomics into acc[0|1][C]
+__device__ __forceinline__ void channel_atomic4(float4 s, float4 q, int C, int tpr, int rpp, double* acc) {
+  __shared__ float4 sh[2][256];
+  const int t = threadIdx.x;
+  const bool act = t < rpp * tpr;
+  sh[0][t] = act ? s : make_float4(0.f, 0.f, 0.f, 0.f);
+  sh[1][t] = act ? q : make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  const float* s0 = reinterpret_cast<const float*>(sh[0]);
+  const float* s1 = reinterpret_cast<const float*>(sh[1]);
+  for (int c = t; c < C && c < tpr * 4; c += 256) {
+    double a = 0.0, b = 0.0;
+    const int cg = c >> 2, k = c & 3;
+    for (int r = 0; r < rpp; ++r) {
+      a += s0[(r * tpr + cg) * 4 + k];
+      b += s1[(r * tpr + cg) * 4 + k];
+    }
+    atomicAdd(&acc[c], a);
+    atomicAdd(&acc[C + c], b);
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void bn32_stats_kernel(const float* __restrict__ x, int64_t M, int C,
+                                                         double* __restrict__ acc) {
+  // channel groups beyond 256 threads: grid.y slices the channels
+  const int tpr_all = C / 4;
+  const int tpr = min(tpr_all - (int)blockIdx.y * 256, 256);
+  const int rpp = 256 / tpr;
+  const int t = threadIdx.x;
+  const int cg = t % tpr, r0 = t / tpr;
+  const int cbase = blockIdx.y * 1024;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  if (r0 < rpp) {
+    for (int64_t row = (int64_t)blockIdx.x * rpp + r0; row < M; row += (int64_t)gridDim.x * rpp) {
+      const float4 v = *reinterpret_cast<const float4*>(x + row * C + cbase + cg * 4);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      q.x += v.x * v.x; q.y += v.y * v.y; q.z += v.z * v.z; q.w += v.w * v.w;
+    }
+  }
+  channel_atomic4(s, q, C, tpr, rpp, acc + cbase);
+}
+
+void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_t s) {
+  // acc + cbase: the [C] halves stay at stride C, so pass the base and C
+  const int gy = (C / 4 + 255) / 256;
+  bn32_stats_kernel<<<dim3(blocks_for(M, C), gy), 256, 0, s>>>(x, M, C, acc);
+}
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(256) void bn32_apply_kernel(BnFwdArgs32 a, int64_t nvec) {
+  extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
+  const int C = a.C;
+  const float4* X = reinterpret_cast<const float4*>(a.x);
+  const float4* R = reinterpret_cast<const float4*>(a.residual);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), rv = xv;
+  if (i < nvec) {  // first vectors in flight across the prologue
+    xv = X[i];
+    if (RES) rv = R[i];
+  }
+  const double inv_m = 1.0 / (double)a.M;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double mu, var;
+    if (a.train) {
+      mu = a.acc[c] * inv_m;
+      var = a.acc[C + c] * inv_m - mu * mu;
+      if (var < 0.0) var = 0.0;
+    } else {
+      mu = a.run_mean[c];
+      var = a.run_var[c];
+    }
+    const double isd = 1.0 / sqrt(var + (double)a.eps);
+    const float sc = (float)((double)a.gamma[c] * isd);
+    coef[c] = sc;
+    coef[C + c] = (float)((double)a.beta[c] - mu * (double)a.gamma[c] * isd);
+    if (a.train && blockIdx.x == 0) {
+      a.mean[c] = (float)mu;
+      a.invstd[c] = (float)isd;
+      if (a.run_mean) {
+        const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
+        a.run_mean[c] = (1.f - a.momentum) * a.run_mean[c] + a.momentum * (float)mu;
+        a.run_var[c] = (1.f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
+      }
+    }
+  }
+  __syncthreads();
+  const int tpr = C / 4;
+  for (; i < nvec; i += stride) {
+    const float4 xc = xv, rc = rv;
+    if (i + stride < nvec) {
+      xv = X[i + stride];
+      if (RES) rv = R[i + stride];
+    }
+    const int cb = (int)(i % tpr) * 4;
+    const float4 sc = *reinterpret_cast<const float4*>(coef + cb);
+    const float4 sh = *reinterpret_cast<const float4*>(coef + C + cb);
+    float4 v = make_float4(fmaf(xc.x, sc.x, sh.x), fmaf(xc.y, sc.y, sh.y), fmaf(xc.z, sc.z, sh.z),
+                           fmaf(xc.w, sc.w, sh.w));
+    if (RES) {
+      v.x += rc.x; v.y += rc.y; v.z += rc.z; v.w += rc.w;
+    }
+    if (RELU) {
+      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+    }
+    reinterpret_cast<float4*>(a.y)[i] = v;
+  }
+}
+
+void launch_bn32_apply(const BnFwdArgs32& a, hipStream_t s) {
+  const int64_t nvec = a.M * a.C / 4;
+  const unsigned g = stream_grid(nvec, 256, 2048);
+  const size_t sm = 2 * a.C * sizeof(float);
+  if (a.residual) {
+    if (a.relu) bn32_apply_kernel<true, true><<<g, 256, sm, s>>>(a, nvec);
+    else bn32_apply_kernel<true, false><<<g, 256, sm, s>>>(a, nvec);
+  } else {
+    if (a.relu) bn32_apply_kernel<false, true><<<g, 256, sm, s>>>(a, nvec);
+    else bn32_apply_kernel<false, false><<<g, 256, sm, s>>>(a, nvec);
+  }
+}
+
+// Backward reduce: acc[c] += sum g, acc[C+c] += sum g * xhat, g = dy [* (y > 0)]
+__global__ __launch_bounds__(256) void bn32_bwd_reduce_kernel(const float* __restrict__ dy,
+                                                              const float* __restrict__ x,
+                                                              const float* __restrict__ y,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd, int64_t M,
+                                                              int C, double* __restrict__ acc) {
+  const int tpr_all = C / 4;
+  const int tpr = min(tpr_all - (int)blockIdx.y * 256, 256);
+  const int rpp = 256 / tpr;
+  const int t = threadIdx.x;
+  const int cg = t % tpr, r0 = t / tpr;
+  const int cb = blockIdx.y * 1024 + cg * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  if (r0 < rpp) {
+    const float4 mu = *reinterpret_cast<const float4*>(mean + cb);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + cb);
+    for (int64_t row = (int64_t)blockIdx.x * rpp + r0; row < M; row += (int64_t)gridDim.x * rpp) {
+      const int64_t off = row * C + cb;
+      float4 g = *reinterpret_cast<const float4*>(dy + off);
+      const float4 xv = *reinterpret_cast<const float4*>(x + off);
+      if (y) {
+        const float4 yv = *reinterpret_cast<const float4*>(y + off);
+        g.x = yv.x > 0.f ? g.x : 0.f;
+        g.y = yv.y > 0.f ? g.y : 0.f;
+        g.z = yv.z > 0.f ? g.z : 0.f;
+        g.w = yv.w > 0.f ? g.w : 0.f;
+      }
+      s.x += g.x; s.y += g.y; s.z += g.z; s.w += g.w;
+      q.x += g.x * ((xv.x - mu.x) * is.x);
+      q.y += g.y * ((xv.y - mu.y) * is.y);
+      q.z += g.z * ((xv.z - mu.z) * is.z);
+      q.w += g.w * ((xv.w - mu.w) * is.w);
+    }
+  }
+  channel_atomic4(s, q, C, tpr, rpp, acc + blockIdx.y * 1024);
+}
+
+void launch_bn32_bwd_reduce(const float* dy, const float* x, const float* y, const float* mean,
+                            const float* invstd, int64_t M, int C, double* acc, hipStream_t s) {
+  const int gy = (C / 4 + 255) / 256;
+  bn32_bwd_reduce_kernel<<<dim3(blocks_for(M, C), gy), 256, 0, s>>>(dy, x, y, mean, invstd, M, C, acc);
+}
+
+// Backward apply: dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat))
+template <bool MASK, bool WRITE_DYM>
+__global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int64_t nvec) {
+  extern __shared__ __attribute__((aligned(16))) float sc[];  // [5][C]: k1, mean g, mean g*xh, mean, invstd
+  const int C = a.C;
+  const float4* DY = reinterpret_cast<const float4*>(a.dy);
+  const float4* X = reinterpret_cast<const float4*>(a.x);
+  const float4* Y = reinterpret_cast<const float4*>(a.y);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), xv = gv, yv = gv;
+  if (i < nvec) {
+    gv = DY[i];
+    xv = X[i];
+    if (MASK) yv = Y[i];
+  }
+  const double inv_m = 1.0 / (double)a.M;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const double s = a.acc[c], q = a.acc[C + c];
+    sc[c] = a.gamma[c] * a.invstd[c];
+    sc[C + c] = (float)(s * inv_m);
+    sc[2 * C + c] = (float)(q * inv_m);
+    sc[3 * C + c] = a.mean[c];
+    sc[4 * C + c] = a.invstd[c];
+    if (blockIdx.x == 0) {
+      if (a.dgamma) a.dgamma[c] = (float)q;
+      if (a.dbeta) a.dbeta[c] = (float)s;
+    }
+  }
+  __syncthreads();
+  const int tpr = C / 4;
+  for (; i < nvec; i += stride) {
+    float4 g = gv;
+    const float4 xc = xv, yc = yv;
+    if (i + stride < nvec) {
+      gv = DY[i + stride];
+      xv = X[i + stride];
+      if (MASK) yv = Y[i + stride];
+    }
+    const int cb = (int)(i % tpr) * 4;
+    if (MASK) {
+      g.x = yc.x > 0.f ? g.x : 0.f;
+      g.y = yc.y > 0.f ? g.y : 0.f;
+      g.z = yc.z > 0.f ? g.z : 0.f;
+      g.w = yc.w > 0.f ? g.w : 0.f;
+      if (WRITE_DYM) reinterpret_cast<float4*>(a.dy_masked)[i] = g;
+    }
+    const float gg[4] = {g.x, g.y, g.z, g.w};
+    const float xx[4] = {xc.x, xc.y, xc.z, xc.w};
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = cb + k;
+      const float xh = (xx[k] - sc[3 * C + c]) * sc[4 * C + c];
+      o[k] = sc[c] * (gg[k] - sc[C + c] - xh * sc[2 * C + c]);
+    }
+    reinterpret_cast<float4*>(a.dx)[i] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s) {
+  const int64_t nvec = a.M * a.C / 4;
+  const unsigned g = stream_grid(nvec, 256, 2048);
+  const size_t sm = 5 * a.C * sizeof(float);
+  if (a.y) {
+    if (a.dy_masked) bn32_bwd_apply_kernel<true, true><<<g, 256, sm, s>>>(a, nvec);
+    else bn32_bwd_apply_kernel<true, false><<<g, 256, sm, s>>>(a, nvec);
+  } else {
+    bn32_bwd_apply_kernel<false, false><<<g, 256, sm, s>>>(a, nvec);
+  }
+}
+
+}  // namespace mfl

@@ -1,0 +1,50 @@
+// fp32 (reference-precision) convolution: geometry reuse of conv.h, fp32
+// operand pointers.  Shared by conv32.hip and its torch binding.
+#pragma once
+#include "kernels/conv.h"
+
+namespace mfl {
+
+struct Conv32Args {
+  ConvGeom g;          // fwd geometry, or the role-swapped dgrad geometry (conv.h)
+  const float* src;    // fwd: X; dgrad: dY
+  const float* wgt;    // OHWI weights [Cout][R][S][Cin]
+  float* y;            // fwd: Y; dgrad: dX
+  float* ysplit;       // split-K slabs [splits][tiles][BM*BN]
+  int* counters;       // split-K arrival tickets, zero between launches
+  double* stats;       // fwd: BN sums of Y (sum, sumsq) [2][Ng]
+  // dgrad: BN-backward reductions of the consumer layer (see conv.h ConvArgs)
+  const float* bn_z;
+  const float* bn_y;
+  const float* bn_mean;
+  const float* bn_invstd;
+  double* bn_acc;
+  uint32_t src_bytes, wgt_bytes;
+  int kchunk;
+  int accum;
+  int par_mc;
+  int c_shift, q_shift, pq_shift;
+};
+
+struct BnBwdFusion32 {
+  const float* z = nullptr;
+  const float* y = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  double* acc = nullptr;
+};
+
+// mode 0 fwd, 1 dgrad, 2 wgrad.  kchunk in k elements (multiple of 32).
+ConvPlan plan_conv32(const ConvGeom& g, int mode);
+int conv32_counter_slots(const ConvGeom& g, const ConvPlan& p);
+
+void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const float* src, const float* wgt,
+                        float* y, float* ysplit, int* counters, double* stats, bool accum,
+                        const BnBwdFusion32* bnb, hipStream_t s);
+// dw (fp32 OHWI); accumulate: dw holds a running sum (zero for a fresh step)
+// and every slice adds atomically; otherwise the split-1 plan stores and a
+// split plan requires dw zeroed by the caller.
+void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, const float* dy, float* dw,
+                         bool accumulate, hipStream_t s);
+
+}  // namespace mfl

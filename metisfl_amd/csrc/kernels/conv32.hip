@@ -1,0 +1,732 @@
+// K6 (fp32): NHWC fp32 convolution forward / backward-data / backward-weight
+// as implicit GEMMs on the gfx950 fp32 matrix cores (v_mfma_f32_32x32x2_f32).
+//
+// The reference trains in fp32 through Keras Conv2D layers
+// (examples/keras/models/cifar_cnn.py:19-41, metisfl/models/keras/
+// keras_model_ops.py:117-197: plain fit, no mixed-precision policy).  This is
+// the reference-precision learner path: operands, accumulators and outputs
+// are IEEE fp32, and gfx950 has no xf32/TF32 shortcut, so every product is an
+// exact fp32 FMA (cdna_hip_programming.md 'FP32-input MFMA').  The bf16 family
+// (conv.hip) stays as the explicit mixed-precision option.
+//
+// Design for CDNA4 (not a port of anything -- the reference has no kernels):
+//  * fp32 MFMA runs at 1/16 of the bf16 rate (64 FLOP/clk/SIMD), so here the
+//    step is COMPUTE-bound where the bf16 one is latency-bound: tiles are
+//    chosen to keep every SIMD's matrix pipe fed (>= 256 workgroups, split-K
+//    on the small-M CIFAR stages), not to shave launch latency.
+//  * v_mfma_f32_32x32x2_f32 takes ONE fp32 per lane per operand:
+//    lane l = (i = l&31, h = l>>5) supplies A[i][h] and B[h][i].  Which real
+//    reduction index sits in each (MFMA, h) slot is free as long as A and B
+//    agree, so a lane reads 4 consecutive k of its row with one ds_read_b128
+//    and feeds them to 4 successive MFMAs: MFMA e of k-group g reduces
+//    k = 8g + 4h + e.  Operands whose global layout is k-contiguous (im2col
+//    rows of X / dY, the OHWI weight rows of the forward pass) are staged
+//    [row][k]; operands whose layout is row-contiguous (W^T for dgrad, both
+//    wgrad operands) are staged [k][row] and read with ds_read_b32 at the same
+//    k index -- no transpose pass, no transposing LDS writes.
+//  * Operand tiles move global -> LDS by LDS-DMA (buffer_load_dwordx4 ...
+//    lds, 16 B per lane), 3-stage ring with 2 k-tiles in flight and counted
+//    vmcnt waits, hardware bounds checks for padding (an out-of-range offset
+//    reads zeros) -- the same staging machinery as the bf16 kernels
+//    (lds_tiles.h).  [row][k] tiles are 128-B rows (32 fp32) with the
+//    (row>>1)&7 XOR chunk swizzle: the 4 lane groups of a ds_read_b128
+//    (rows {0-3,12-15,20-27} / {4-11,16-19,28-31} at one chunk) land on 16
+//    distinct 16-B bank slots.
+//  * Epilogue through LDS: the tile is written as float4 rows (coalesced), the
+//    forward BN statistics (sum, sum^2 per channel) -- or, for dgrad, the
+//    consumer BN-backward reductions -- are reduced in the same pass and added
+//    with fp64 atomics.  Split-K slices reduce in-launch (last arriver sums
+//    the write-through slabs in slice order: bitwise deterministic).
+//  * Stride-2 dgrad runs parity-class decomposed (PAR), as in conv.hip.
+#include "kernels/common.h"
+#include "kernels/conv32.h"
+#include "kernels/lds_tiles.h"
+
+namespace mfl {
+
+namespace {
+
+constexpr int kBK = 32;      // fp32 k-elements per tile = 128-B rows
+constexpr int kStages = 3;   // LDS ring
+constexpr int kTiles = kStages - 1;  // k-tiles in flight
+
+__device__ __forceinline__ f32x16 mfma_f32(float a, float b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int sdiv(int x, int d, int shift) { return shift >= 0 ? x >> shift : x / d; }
+
+// fp32 [row][32] tile, 128-B rows: 16-B chunk ch of `row`
+__device__ __forceinline__ int rk_off(int row, int ch) { return row * 128 + ((ch ^ swz_b128<128>(row)) << 4); }
+
+template <int L, typename Issue, typename Compute>
+__device__ __forceinline__ void ring_loop(int nk, Issue& issue, Compute& compute) {
+#pragma unroll
+  for (int u = 0; u < kTiles; ++u)
+    if (u < nk) issue(u, u);
+  int stage = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // own DMA of tile kt landed; the next one may still be in flight
+    if (kt + 1 < nk) wait_vmcnt<L>();
+    else wait_vmcnt<0>();
+    lds_barrier();  // every wave's tile kt landed, every wave left stage (kt-1)%3
+    if (kt + kTiles < nk) issue(kt + kTiles, stage == 0 ? kStages - 1 : stage - 1);
+    compute(stage);
+    stage = stage == kStages - 1 ? 0 : stage + 1;
+  }
+}
+
+// GEMM row -> output pixel (identity, or the parity-class order of PAR dgrad)
+__device__ __forceinline__ int out_pixel32(const Conv32Args& a, int row) {
+  if (!a.par_mc) return row;
+  const int q2 = a.g.Q >> 1, pq2 = (a.g.P >> 1) * q2;
+  const int cls = row / a.par_mc;
+  const int mc = row - cls * a.par_mc;
+  const int n = mc / pq2;
+  const int rem = mc - n * pq2;
+  const int y = rem / q2, x = rem - y * q2;
+  return (n * a.g.P + 2 * y + (cls >> 1)) * a.g.Q + 2 * x + (cls & 1);
+}
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// Output tile [BM][BN + 4] fp32 in LDS -> y (float4 rows), + fused channel sums.
+template <int BM, int BN>
+__device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, int m0, int n0, const float* tile,
+                                                float* red) {
+  constexpr int TST = BN + 4;
+  constexpr int CPR = BN / 4;      // float4 per row
+  constexpr int RPP = 256 / CPR;   // rows per pass
+  const ConvGeom& g = a.g;
+  double* stats = a.bn_acc ? a.bn_acc : a.stats;
+  const int t = threadIdx.x;
+  const int cg = t % CPR, r0 = t / CPR;
+  const int col = n0 + cg * 4;
+  const bool col_ok = col < g.Ng;  // Ng % 4 == 0
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s, mu = s, is = s;
+  if (a.bn_acc && col_ok) {
+    mu = *reinterpret_cast<const float4*>(a.bn_mean + col);
+    is = *reinterpret_cast<const float4*>(a.bn_invstd + col);
+  }
+  for (int rl = r0; rl < BM; rl += RPP) {
+    const int row = m0 + rl;
+    if (row >= g.M || !col_ok) continue;
+    float4 v = *reinterpret_cast<const float4*>(tile + rl * TST + cg * 4);
+    const int64_t off = (int64_t)out_pixel32(a, row) * g.Ng + col;
+    float4* dst = reinterpret_cast<float4*>(a.y + off);
+    if (a.accum) v = f4add(v, *dst);
+    *dst = v;
+    if (stats) {
+      if (a.bn_acc) {
+        const float4 z = *reinterpret_cast<const float4*>(a.bn_z + off);
+        float4 gk = v;
+        if (a.bn_y) {
+          const float4 ym = *reinterpret_cast<const float4*>(a.bn_y + off);
+          gk.x = ym.x > 0.f ? gk.x : 0.f;
+          gk.y = ym.y > 0.f ? gk.y : 0.f;
+          gk.z = ym.z > 0.f ? gk.z : 0.f;
+          gk.w = ym.w > 0.f ? gk.w : 0.f;
+        }
+        s = f4add(s, gk);
+        q.x += gk.x * ((z.x - mu.x) * is.x);
+        q.y += gk.y * ((z.y - mu.y) * is.y);
+        q.z += gk.z * ((z.z - mu.z) * is.z);
+        q.w += gk.w * ((z.w - mu.w) * is.w);
+      } else {
+        s = f4add(s, v);
+        q.x += v.x * v.x;
+        q.y += v.y * v.y;
+        q.z += v.z * v.z;
+        q.w += v.w * v.w;
+      }
+    }
+  }
+  if (!stats) return;
+  reinterpret_cast<float4*>(red)[2 * t] = s;
+  reinterpret_cast<float4*>(red)[2 * t + 1] = q;
+  __syncthreads();
+  if (t < BN) {
+    const int cgi = t >> 2, k = t & 3;
+    double sa = 0.0, sb = 0.0;
+#pragma unroll 4
+    for (int r = 0; r < RPP; ++r) {
+      sa += red[(r * CPR + cgi) * 8 + k];
+      sb += red[(r * CPR + cgi) * 8 + 4 + k];
+    }
+    const int c = n0 + t;
+    if (c < g.Ng) {
+      atomicAdd(&stats[c], sa);
+      atomicAdd(&stats[g.Ng + c], sb);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Forward / dgrad:  Y[m][n] = sum_k A[m][k] * B[k][n]
+//   fwd:   A = im2col(X) [M][R*S*C],  B[k][n] = W[n][k]   (both [row][k] tiles)
+//   dgrad: A = stride-aware gather of dY [M = N*H*W][R*S*Co],
+//          B[k = (r,s,co)][n = ci] = W[co][r][s][ci]      ([k][n] tile, b32 reads)
+template <int BM, int BN, bool DGRAD, int KS, int ST, bool PAR>
+__global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int A_BYTES = BM * 128;
+  constexpr int STAGE = A_BYTES + BN * 128;
+  constexpr int ACH = BM / 32;  // DMA instructions per wave per k-tile (1 KiB each)
+  constexpr int BCH = BN / 32;
+  constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 MFMA tiles per wave
+  constexpr int BRB = BN * 4;                // dgrad B row bytes
+  constexpr int B_RPI = 1024 / BRB, B_CPR = BRB / 16;
+  const ConvGeom& g = a.g;
+  const auto rsA = make_rsrc(a.src, a.src_bytes);
+  const auto rsB = make_rsrc(a.wgt, a.wgt_bytes);
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int kbeg = blockIdx.z * a.kchunk;
+  int cls = 0, r0 = 0, s0 = 0, ns = 1, dh = 0, dw = 0, kc_end = g.K;
+  if constexpr (PAR) {
+    cls = m0 / a.par_mc;
+    const int qh = cls >> 1, qw = cls & 1;
+    r0 = (qh + g.pad) & 1;
+    s0 = (qw + g.pad) & 1;
+    const int nr = (KS - r0 + 1) >> 1;
+    ns = (KS - s0 + 1) >> 1;
+    dh = (qh + g.pad - r0) >> 1;
+    dw = (qw + g.pad - s0) >> 1;
+    kc_end = nr * ns * g.C;
+  }
+  const int kend = min(kc_end, kbeg + a.kchunk);
+  const int nk = max(0, (kend - kbeg + kBK - 1) / kBK);
+  const int HWC = g.H * g.W * g.C;
+
+  // [row][k] DMA: instruction i of wave w fills rows 32i + 8w + lane/8,
+  // physical chunk lane%8 <- logical chunk (k offset) a_kc (i-independent).
+  const int lrow = wave * 8 + (lane >> 3);
+  const int a_kc = ((lane & 7) ^ swz_b128<128>(lrow)) * 4;
+  int a_nb[ACH], a_y0[ACH], a_x0[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int m = m0 + lrow + 32 * i;
+    const int mm = m < g.M ? m : 0;
+    if constexpr (PAR) {
+      const int q2 = g.Q >> 1;
+      const int pq2 = (g.P >> 1) * q2;
+      const int mc = mm - cls * a.par_mc;
+      const int n = mc / pq2;
+      const int rem = mc - n * pq2;
+      const int y = rem / q2;
+      a_nb[i] = n * HWC;
+      a_y0[i] = y + dh;
+      a_x0[i] = rem - y * q2 + dw;
+    } else {
+      const int n = sdiv(mm, g.P * g.Q, a.pq_shift);
+      const int rem = mm - n * g.P * g.Q;
+      const int oy = sdiv(rem, g.Q, a.q_shift);
+      const int ox = rem - oy * g.Q;
+      a_nb[i] = n * HWC;
+      a_y0[i] = DGRAD ? oy + g.pad : oy * ST - g.pad;
+      a_x0[i] = DGRAD ? ox + g.pad : ox * ST - g.pad;
+    }
+    if (m >= g.M) a_y0[i] = -(1 << 28);  // forces the OOB offset
+  }
+
+  auto issue = [&](int kt, int stage) {
+    uint8_t* st = smem + stage * STAGE;
+    const int kb = kbeg + kt * kBK;
+    {
+      const int k = kb + a_kc;
+      const int rs = sdiv(k, g.C, a.c_shift);
+      const int c = k - rs * g.C;
+      const int r = PAR ? (ns == 2 ? rs >> 1 : rs) : rs / KS;
+      const int s = PAR ? rs - r * ns : rs - r * KS;
+      const bool kv = k < kend;
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        int iy, ix;
+        bool ok;
+        if (PAR) {
+          iy = a_y0[i] - r;
+          ix = a_x0[i] - s;
+          ok = kv & (iy >= 0) & (ix >= 0);
+        } else if (DGRAD) {
+          const int ty = a_y0[i] - r, tx = a_x0[i] - s;
+          ok = kv & (ty >= 0) & (tx >= 0);
+          if (ST > 1) ok = ok & ((ty % ST) == 0) & ((tx % ST) == 0);
+          iy = ty / ST;
+          ix = tx / ST;
+        } else {
+          iy = a_y0[i] + r;
+          ix = a_x0[i] + s;
+          ok = kv & (iy >= 0) & (ix >= 0);
+        }
+        ok = ok & (iy < g.H) & (ix < g.W);
+        const uint32_t off = ok ? (uint32_t)(a_nb[i] + (iy * g.W + ix) * g.C + c) * 4u : kOOB;
+        dma16(rsA, off, st + (wave + 4 * i) * 1024);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      uint32_t off;
+      if constexpr (DGRAD) {
+        const int row = (wave + 4 * i) * B_RPI + lane / B_CPR;  // k within the tile
+        const int n = n0 + (lane % B_CPR) * 4;
+        const int kr = kb + row;
+        int rs = sdiv(kr, g.C, a.c_shift);
+        const int ko = kr - rs * g.C;
+        if (PAR) {  // class tap index -> kernel tap (r0 + 2 j_r, s0 + 2 j_s)
+          const int jr = ns == 2 ? rs >> 1 : rs;
+          rs = (r0 + 2 * jr) * KS + s0 + 2 * (rs - jr * ns);
+        }
+        off = ((kr < kend) & (n < g.Ng)) ? (uint32_t)((ko * KS * KS + rs) * g.Ng + n) * 4u : kOOB;
+      } else {
+        const int n = n0 + lrow + 32 * i;
+        const int k = kb + a_kc;
+        off = ((k < kend) & (n < g.Ng)) ? (uint32_t)(n * g.K + k) * 4u : kOOB;
+      }
+      dma16(rsB, off, st + A_BYTES + (wave + 4 * i) * 1024);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int li = lane & 31, lh = lane >> 5;
+  auto compute = [&](int stage) {
+    const uint8_t* As = smem + stage * STAGE;
+    const uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int grp = 0; grp < kBK / 8; ++grp) {
+      f32x4 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * (BM / 2) + 32 * i + li;
+        af[i] = *reinterpret_cast<const f32x4*>(As + rk_off(row, 2 * grp + lh));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (BN / 2) + 32 * j + li;
+        if constexpr (DGRAD) {
+          const float* Bf = reinterpret_cast<const float*>(Bs);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfr[j][e] = Bf[(8 * grp + 4 * lh + e) * BN + col];
+        } else {
+          bfr[j] = *reinterpret_cast<const f32x4*>(Bs + rk_off(col, 2 * grp + lh));
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(af[i][e], bfr[j][e], acc[i][j]);
+    }
+  };
+  ring_loop<ACH + BCH>(nk, issue, compute);
+  __syncthreads();  // every wave done with the ring before smem is reused
+
+  // ---- epilogue -----------------------------------------------------------
+  constexpr int TST = BN + 4;
+  float* tile = reinterpret_cast<float*>(smem);
+  float* red = tile + BM * TST;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rl = wm * (BM / 2) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        tile[rl * TST + wn * (BN / 2) + 32 * j + li] = acc[i][j][e];
+      }
+  __syncthreads();
+  const int splits = gridDim.z;
+  if (splits > 1) {
+    // in-launch split-K (write-through slabs + arrival ticket; conv.hip)
+    constexpr int F = BM * BN / 1024;  // float4 per thread
+    constexpr int C4 = BN / 4;
+    const int tile_id = blockIdx.y * gridDim.x + blockIdx.x;
+    const int ntiles = gridDim.x * gridDim.y;
+    const int64_t zstride = (int64_t)ntiles * BM * BN * 4;
+    const auto rsS = make_rsrc(a.ysplit + (int64_t)tile_id * (BM * BN), 0x7FFFFFF0u);
+    const uint32_t zoff = (uint32_t)(blockIdx.z * zstride);
+#pragma unroll
+    for (int u = 0; u < F; ++u) {
+      const int f = t + 256 * u;
+      const float4 v = *reinterpret_cast<const float4*>(tile + (f / C4) * TST + (f % C4) * 4);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)}, rsS,
+          (int)(zoff + f * 16), 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(red + 256 * 8);
+    if (t == 0) {
+      const int prev =
+          __hip_atomic_fetch_add(&a.counters[tile_id], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == splits - 1;
+      if (last) __hip_atomic_store(&a.counters[tile_id], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    float4 sum[F];
+#pragma unroll
+    for (int u = 0; u < F; ++u) sum[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int z = 0; z < splits; ++z) {
+#pragma unroll
+      for (int u = 0; u < F; ++u) {
+        const int f = t + 256 * u;
+        float4 r;
+        if (z == (int)blockIdx.z) {
+          r = *reinterpret_cast<const float4*>(tile + (f / C4) * TST + (f % C4) * 4);
+        } else {
+          const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rsS, (int)(z * zstride + f * 16), 0, 16);
+          r = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]),
+                          __uint_as_float(b[3]));
+        }
+        sum[u] = f4add(sum[u], r);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < F; ++u) {
+      const int f = t + 256 * u;
+      *reinterpret_cast<float4*>(tile + (f / C4) * TST + (f % C4) * 4) = sum[u];
+    }
+    __syncthreads();
+  }
+  tile_epilogue32<BM, BN>(a, m0, n0, tile, red);
+}
+
+// ---------------------------------------------------------------------------
+// wgrad:  dW[co][j] = sum_m dY[m][co] * im2col(X)[m][j],  j = (r, s, c)
+// Both operands are row-contiguous in memory: tiles [32 m][BM co] and
+// [32 m][BN j], b32 fragment reads, MFMA (g, e) slot h reduces m = 8g + 4h + e.
+template <int BM, int BN, int KS, int ST>
+__global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, float* __restrict__ dw, int atomic) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int A_BYTES = kBK * BM * 4;
+  constexpr int STAGE = A_BYTES + kBK * BN * 4;
+  constexpr int ARB = BM * 4, A_RPI = 1024 / ARB, A_CPR = ARB / 16;
+  constexpr int BRB = BN * 4, B_RPI = 1024 / BRB, B_CPR = BRB / 16;
+  constexpr int ACH = BM / 32, BCH = BN / 32;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  const ConvGeom& g = a.g;  // H,W,C = X; P,Q = dY spatial; Ng = Cout; K = R*S*C; M = N*P*Q
+  const auto rsA = make_rsrc(a.src, a.src_bytes);  // dY
+  const auto rsB = make_rsrc(a.wgt, a.wgt_bytes);  // X
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int i0 = blockIdx.x * BM;
+  const int j0 = blockIdx.y * BN;
+  const int kbeg = blockIdx.z * a.kchunk;
+  const int kend = min(g.M, kbeg + a.kchunk);
+  const int nk = max(0, (kend - kbeg + kBK - 1) / kBK);
+
+  const int a_co = i0 + (lane % A_CPR) * 4;
+  const bool a_ok = a_co < g.Ng;
+  const int jcol = j0 + (lane % B_CPR) * 4;
+  const bool jok = jcol < g.K;
+  const int rs = sdiv(jcol, g.C, a.c_shift);
+  const int jc = jcol - rs * g.C;
+  const int jr = rs / KS, js = rs - (rs / KS) * KS;
+  const int PQ = g.P * g.Q;
+
+  auto issue = [&](int kt, int stage) {
+    uint8_t* st = smem + stage * STAGE;
+    const int kb = kbeg + kt * kBK;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int m = kb + (wave + 4 * i) * A_RPI + lane / A_CPR;
+      const uint32_t off = ((m < kend) & a_ok) ? (uint32_t)(m * g.Ng + a_co) * 4u : kOOB;
+      dma16(rsA, off, st + (wave + 4 * i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int m = kb + (wave + 4 * i) * B_RPI + lane / B_CPR;
+      const int n = sdiv(m, PQ, a.pq_shift);
+      const int rem = m - n * PQ;
+      const int oy = sdiv(rem, g.Q, a.q_shift);
+      const int ox = rem - oy * g.Q;
+      const int iy = oy * ST - g.pad + jr, ix = ox * ST - g.pad + js;
+      const bool ok = (m < kend) & jok & (iy >= 0) & (iy < g.H) & (ix >= 0) & (ix < g.W);
+      const uint32_t off = ok ? (uint32_t)(((n * g.H + iy) * g.W + ix) * g.C + jc) * 4u : kOOB;
+      dma16(rsB, off, st + A_BYTES + (wave + 4 * i) * 1024);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const int li = lane & 31, lh = lane >> 5;
+  auto compute = [&](int stage) {
+    const float* As = reinterpret_cast<const float*>(smem + stage * STAGE);
+    const float* Bs = reinterpret_cast<const float*>(smem + stage * STAGE + A_BYTES);
+#pragma unroll
+    for (int grp = 0; grp < kBK / 8; ++grp) {
+      f32x4 af[TM], bfr[TN];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kr = 8 * grp + 4 * lh + e;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i][e] = As[kr * BM + wm * (BM / 2) + 32 * i + li];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j][e] = Bs[kr * BN + wn * (BN / 2) + 32 * j + li];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(af[i][e], bfr[j][e], acc[i][j]);
+    }
+  };
+  ring_loop<ACH + BCH>(nk, issue, compute);
+
+  // epilogue straight from the accumulators: each register store covers two
+  // 128-B row segments (the full-rate atomic shape, MI355X_MICROARCH.md)
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = j0 + wn * (BN / 2) + 32 * j + li;
+      if (col >= g.K) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = i0 + wm * (BM / 2) + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        if (co >= g.Ng) continue;
+        float* p = dw + (int64_t)co * g.K + col;
+        if (atomic) atomicAdd(p, acc[i][j][e]);
+        else *p = acc[i][j][e];
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+int log2_exact(int v) {
+  if (v <= 0 || (v & (v - 1))) return -1;
+  int s = 0;
+  while ((1 << s) < v) ++s;
+  return s;
+}
+uint32_t range_bytes(int64_t elems) {
+  const int64_t b = elems * 4;
+  return b >= 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)b;
+}
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+template <typename K>
+void set_lds(K* kernel, size_t lds) {
+  if (lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+}
+
+size_t gemm_lds(int bm, int bn) {
+  const size_t ring = (size_t)kStages * (bm + bn) * 128;
+  const size_t epi = (size_t)bm * (bn + 4) * 4 + 256 * 8 * 4 + 16;
+  return ring > epi ? ring : epi;
+}
+
+template <int BM, int BN, bool DG, int KS, int ST, bool PAR>
+void launch_t(const Conv32Args& a, dim3 grid, hipStream_t s) {
+  static bool init = false;
+  const size_t lds = gemm_lds(BM, BN);
+  if (!init) {
+    set_lds(&conv32_gemm_kernel<BM, BN, DG, KS, ST, PAR>, lds);
+    init = true;
+  }
+  conv32_gemm_kernel<BM, BN, DG, KS, ST, PAR><<<grid, 256, lds, s>>>(a);
+}
+
+template <int BM, int BN, bool DG>
+void launch_geom(const Conv32Args& a, dim3 grid, hipStream_t s) {
+  const ConvGeom& g = a.g;
+  const bool par = a.par_mc != 0;
+  if (g.R == 3 && g.stride == 1) launch_t<BM, BN, DG, 3, 1, false>(a, grid, s);
+  else if (g.R == 1 && g.stride == 1) launch_t<BM, BN, DG, 1, 1, false>(a, grid, s);
+  else if (g.R == 3 && g.stride == 2) {
+    if (DG && par) launch_t<BM, BN, DG, 3, 2, true>(a, grid, s);
+    else launch_t<BM, BN, DG, 3, 2, false>(a, grid, s);
+  } else if (g.R == 1 && g.stride == 2) {
+    if (DG && par) launch_t<BM, BN, DG, 1, 2, true>(a, grid, s);
+    else launch_t<BM, BN, DG, 1, 2, false>(a, grid, s);
+  }
+}
+
+// Plan: pick (BM, BN, split) minimising a throughput model of the fp32 matrix
+// pipe.  A workgroup of a BMxBN tile over kt k-tiles keeps its CU's 4 SIMDs
+// busy for BM*BN*kt*32*2 / 256 cycles; 64x64 tiles run 2 workgroups per CU.
+// Costs added: the pipeline fill + epilogue per workgroup, and for split-K
+// the last arriver's serial slab reads (~100 GB/s per workgroup).
+struct Cand {
+  int bm, bn;
+};
+constexpr Cand kCands[] = {{64, 64}, {128, 64}, {64, 128}, {128, 128}};
+
+}  // namespace
+
+int conv32_counter_slots(const ConvGeom& g, const ConvPlan& p) {
+  return cdiv(g.M, p.bm) * cdiv(g.Ng, p.bn);
+}
+
+static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
+  const int rows = mode == 2 ? g.Ng : g.M;
+  const int cols = mode == 2 ? g.K : g.Ng;
+  int kred = mode == 2 ? g.M : g.K;
+  bool par = false;
+  if (allow_par && mode == 1 && g.stride == 2 && (g.P % 2 == 0) && (g.Q % 2 == 0)) {
+    par = true;
+    kred = ((g.R + 1) / 2) * ((g.S + 1) / 2) * g.C;  // the largest parity class
+  }
+  const int fb = env_int("MFL_C32_BM", 0), fn = env_int("MFL_C32_BN", 0), fs = env_int("MFL_C32_SPLIT", 0);
+  const double clk = 2.4e3;  // cycles per us
+  ConvPlan best;
+  double best_t = 1e30;
+  const int nkt_all = cdiv(kred, kBK);
+  for (const Cand& c : kCands) {
+    if (fb && c.bm != fb) continue;
+    if (fn && c.bn != fn) continue;
+    if (par && ((g.N * (g.P / 2) * (g.Q / 2)) % c.bm)) continue;
+    const int tiles = cdiv(rows, c.bm) * cdiv(cols, c.bn);
+    const int occ = c.bm * c.bn <= 4096 ? 2 : 1;
+    const int slots = 256 * occ;
+    for (int sp = 1; sp <= 64 && sp <= nkt_all; ++sp) {
+      if (fs && sp != fs) continue;
+      const int kt = cdiv(nkt_all, sp);
+      const int s_eff = cdiv(nkt_all, kt);
+      if (s_eff != sp) continue;
+      if (mode != 2 && s_eff > 1 && tiles > 1024) continue;  // counter block size
+      const int nwg = tiles * s_eff;
+      const double t_alone = (double)c.bm * c.bn * kt * kBK * 2 / 256.0 / clk + 1.2;
+      const int full = nwg / slots, rem = nwg % slots;
+      double tt = full * occ * t_alone + (rem ? (rem > 256 ? occ : 1) * t_alone : 0.0);
+      if (s_eff > 1) {
+        if (mode == 2) tt += (double)tiles * s_eff * c.bm * c.bn * 4 / 1.3e6;  // atomic bytes at 1.3 TB/s
+        else tt += (double)s_eff * c.bm * c.bn * 4 / 1.0e5 + 1.0;              // serial slab reduce
+      }
+      if (tt < best_t - 1e-9) {
+        best_t = tt;
+        best.bm = c.bm;
+        best.bn = c.bn;
+        best.splits = s_eff;
+        best.kchunk = kt * kBK;
+      }
+    }
+  }
+  best.stats_rows = mode == 0 ? 1 : 0;
+  best.bk = kBK;
+  best.par_mc = par && mode == 1 ? g.N * (g.P / 2) * (g.Q / 2) : 0;
+  if (best_t >= 1e30) best.kchunk = 0;  // no feasible tile
+  return best;
+}
+
+ConvPlan plan_conv32(const ConvGeom& g, int mode) {
+  // parity-class dgrad needs class sizes that are whole tiles; otherwise the
+  // masked stride-aware gather
+  ConvPlan p = plan_conv32_impl(g, mode, true);
+  if (p.kchunk == 0) p = plan_conv32_impl(g, mode, false);
+  return p;
+}
+
+static void fill_shifts(Conv32Args& a) {
+  a.c_shift = log2_exact(a.g.C);
+  a.q_shift = log2_exact(a.g.Q);
+  a.pq_shift = log2_exact(a.g.P * a.g.Q);
+}
+
+void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const float* src, const float* wgt,
+                        float* y, float* ysplit, int* counters, double* stats, bool accum,
+                        const BnBwdFusion32* bnb, hipStream_t s) {
+  Conv32Args a{};
+  a.g = g;
+  a.src = src;
+  a.wgt = wgt;
+  a.y = y;
+  a.ysplit = ysplit;
+  a.counters = counters;
+  a.stats = dgrad ? nullptr : stats;
+  if (bnb && bnb->acc) {
+    a.bn_z = bnb->z;
+    a.bn_y = bnb->y;
+    a.bn_mean = bnb->mean;
+    a.bn_invstd = bnb->invstd;
+    a.bn_acc = bnb->acc;
+  }
+  a.src_bytes = range_bytes((int64_t)g.N * g.H * g.W * g.C);
+  a.wgt_bytes = range_bytes((int64_t)g.K * g.Ng);
+  a.kchunk = p.kchunk;
+  a.accum = accum ? 1 : 0;
+  a.par_mc = dgrad ? p.par_mc : 0;
+  fill_shifts(a);
+  const dim3 grid(cdiv(g.M, p.bm), cdiv(g.Ng, p.bn), p.splits);
+  const int key = p.bm * 1000 + p.bn;
+  switch (key) {
+    case 64064: dgrad ? launch_geom<64, 64, true>(a, grid, s) : launch_geom<64, 64, false>(a, grid, s); break;
+    case 128064: dgrad ? launch_geom<128, 64, true>(a, grid, s) : launch_geom<128, 64, false>(a, grid, s); break;
+    case 64128: dgrad ? launch_geom<64, 128, true>(a, grid, s) : launch_geom<64, 128, false>(a, grid, s); break;
+    default: dgrad ? launch_geom<128, 128, true>(a, grid, s) : launch_geom<128, 128, false>(a, grid, s); break;
+  }
+}
+
+namespace {
+template <int BM, int BN, int KS, int ST>
+void launch_w(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStream_t s) {
+  static bool init = false;
+  const size_t lds = (size_t)kStages * kBK * (BM + BN) * 4;
+  if (!init) {
+    set_lds(&conv32_wgrad_kernel<BM, BN, KS, ST>, lds);
+    init = true;
+  }
+  conv32_wgrad_kernel<BM, BN, KS, ST><<<grid, 256, lds, s>>>(a, dw, atomic);
+}
+template <int BM, int BN>
+void launch_w_geom(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStream_t s) {
+  const ConvGeom& g = a.g;
+  if (g.R == 3 && g.stride == 1) launch_w<BM, BN, 3, 1>(a, grid, dw, atomic, s);
+  else if (g.R == 3 && g.stride == 2) launch_w<BM, BN, 3, 2>(a, grid, dw, atomic, s);
+  else if (g.R == 1 && g.stride == 1) launch_w<BM, BN, 1, 1>(a, grid, dw, atomic, s);
+  else launch_w<BM, BN, 1, 2>(a, grid, dw, atomic, s);
+}
+}  // namespace
+
+void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, const float* dy, float* dw,
+                         bool accumulate, hipStream_t s) {
+  Conv32Args a{};
+  a.g = g;
+  a.src = dy;
+  a.wgt = x;
+  a.src_bytes = range_bytes((int64_t)g.M * g.Ng);
+  a.wgt_bytes = range_bytes((int64_t)g.N * g.H * g.W * g.C);
+  a.kchunk = p.kchunk;
+  fill_shifts(a);
+  const dim3 grid(cdiv(g.Ng, p.bm), cdiv(g.K, p.bn), p.splits);
+  const int atomic = (accumulate || p.splits > 1) ? 1 : 0;
+  const int key = p.bm * 1000 + p.bn;
+  switch (key) {
+    case 64064: launch_w_geom<64, 64>(a, grid, dw, atomic, s); break;
+    case 128064: launch_w_geom<128, 64>(a, grid, dw, atomic, s); break;
+    case 64128: launch_w_geom<64, 128>(a, grid, dw, atomic, s); break;
+    default: launch_w_geom<128, 128>(a, grid, dw, atomic, s); break;
+  }
+}
+
+}  // namespace mfl

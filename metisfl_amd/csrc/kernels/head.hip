@@ -19,12 +19,35 @@ namespace mfl {
 // dlogits x feat outer product is added with fp32 atomics (B adders per
 // address; dW / db must be zero on entry -- the training step's gradient
 // buffer is) and head_wgrad_kernel is not launched.
-__global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ x, int HW, int C,
+// Activations arrive as bf16 (mixed-precision path) or fp32 (reference-
+// precision path); 8 channels per lane either way.
+__device__ __forceinline__ void load8(const uint16_t* p, float* v) { unpack8(*reinterpret_cast<const uint4*>(p), v); }
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+struct Pack8 {
+  uint4 h;
+  float4 a, b;
+};
+__device__ __forceinline__ void pack_out(const float* v, uint16_t*, Pack8& p) { p.h = pack8(v); }
+__device__ __forceinline__ void pack_out(const float* v, float*, Pack8& p) {
+  p.a = make_float4(v[0], v[1], v[2], v[3]);
+  p.b = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void store8(uint16_t* d, const Pack8& p) { *reinterpret_cast<uint4*>(d) = p.h; }
+__device__ __forceinline__ void store8(float* d, const Pack8& p) {
+  reinterpret_cast<float4*>(d)[0] = p.a;
+  reinterpret_cast<float4*>(d)[1] = p.b;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int HW, int C,
                                                    const float* __restrict__ W,
                                                    const float* __restrict__ bias, int K,
                                                    const int* __restrict__ labels,
                                                    float* __restrict__ feat, float* __restrict__ dlog,
-                                                   uint16_t* __restrict__ dx,
+                                                   T* __restrict__ dx,
                                                    float* __restrict__ stats, int B, int backward,
                                                    float* __restrict__ dW, float* __restrict__ db) {
   // feat[C] | logits[K] | partials[R][C] | W[K][C]
@@ -39,7 +62,7 @@ __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ 
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
   const float inv_hw = 1.f / (float)HW;
-  const uint16_t* xb = x + (int64_t)b * HW * C;
+  const T* xb = x + (int64_t)b * HW * C;
   const int cg = t % G, rg = t / G;
   // the classifier weights go to LDS alongside the pooling loads: the logits
   // and the dx broadcast then read LDS instead of paying two more dependent
@@ -55,7 +78,7 @@ __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ 
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int h = rg; h < HW; h += R) {
       float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(xb + (int64_t)h * C + 8 * cg), v);
+      load8(xb + (int64_t)h * C + 8 * cg, v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) s[k] += v[k];
     }
@@ -131,25 +154,38 @@ __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ 
       for (int k = 0; k < K; ++k) s += lg[k] * Ws[k * C + 8 * cg + e];
       v[e] = s * inv_hw;
     }
-    const uint4 pk = pack8(v);
-    uint16_t* dxb = dx + (int64_t)b * HW * C + 8 * cg;
-    for (int h = rg; h < HW; h += R) *reinterpret_cast<uint4*>(dxb + (int64_t)h * C) = pk;
+    Pack8 pk;
+    T* dxb = dx + (int64_t)b * HW * C + 8 * cg;
+    pack_out(v, dxb, pk);
+    for (int h = rg; h < HW; h += R) store8(dxb + (int64_t)h * C, pk);
   }
+}
+
+template <typename T>
+static void head_launch(const T* x, int B, int HW, int C, const float* W, const float* bias, int K,
+                        const int* labels, float* feat, float* dlogits, T* dx, float* stats, bool backward,
+                        hipStream_t s, float* dW, float* db) {
+  const int G = C / 8, R = G >= 256 ? 1 : 256 / G;
+  const size_t sm = (size_t)(C + ((K + 3) & ~3) + (size_t)R * C + (size_t)K * C) * sizeof(float);
+  static bool attr = false;
+  if (!attr && sm > 65536) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_kernel<T>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    attr = true;
+  }
+  head_kernel<T><<<B, 256, sm, s>>>(x, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, B, backward ? 1 : 0,
+                                    backward ? dW : nullptr, backward ? db : nullptr);
 }
 
 void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,
                          int K, const int* labels, float* feat, float* dlogits, uint16_t* dx,
                          float* stats, bool backward, hipStream_t s, float* dW, float* db) {
-  const int G = C / 8, R = G >= 256 ? 1 : 256 / G;
-  const size_t sm = (size_t)(C + ((K + 3) & ~3) + (size_t)R * C + (size_t)K * C) * sizeof(float);
-  static bool attr = false;
-  if (!attr && sm > 65536) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    attr = true;
-  }
-  head_kernel<<<B, 256, sm, s>>>(x, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, B,
-                                 backward ? 1 : 0, backward ? dW : nullptr, backward ? db : nullptr);
+  head_launch(x, B, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, backward, s, dW, db);
+}
+void launch_head32_fwd_bwd(const float* x, int B, int HW, int C, const float* W, const float* bias, int K,
+                           const int* labels, float* feat, float* dlogits, float* dx, float* stats, bool backward,
+                           hipStream_t s, float* dW, float* db) {
+  head_launch(x, B, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, backward, s, dW, db);
 }
 
 __global__ __launch_bounds__(256) void head_wgrad_kernel(const float* __restrict__ feat,

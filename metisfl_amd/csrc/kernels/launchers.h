@@ -93,7 +93,48 @@ void launch_bn_bwd_reduce(const uint16_t* dy, const uint16_t* x, const uint16_t*
                           hipStream_t s);
 void launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t s);
 
+// ---- bn32.hip (fp32 reference-precision path) -----------------------------
+struct BnFwdArgs32 {
+  const float* x;
+  const float* residual;  // optional
+  float* y;
+  const double* acc;
+  const float* gamma;
+  const float* beta;
+  float* mean;
+  float* invstd;
+  float* run_mean;
+  float* run_var;
+  int64_t M;
+  int C;
+  float momentum, eps;
+  int train, relu;
+};
+struct BnBwdArgs32 {
+  const float* dy;
+  const float* x;
+  const float* y;
+  const double* acc;
+  const float* gamma;
+  const float* mean;
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
+  float* dx;
+  float* dy_masked;
+  int64_t M;
+  int C;
+};
+void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_t s);
+void launch_bn32_apply(const BnFwdArgs32& a, hipStream_t s);
+void launch_bn32_bwd_reduce(const float* dy, const float* x, const float* y, const float* mean,
+                            const float* invstd, int64_t M, int C, double* acc, hipStream_t s);
+void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s);
+
 // ---- head.hip ------------------------------------------------------------
+void launch_head32_fwd_bwd(const float* x, int B, int HW, int C, const float* W, const float* bias, int K,
+                           const int* labels, float* feat, float* dlogits, float* dx, float* stats, bool backward,
+                           hipStream_t s, float* dW = nullptr, float* db = nullptr);
 void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,
                          int K, const int* labels, float* feat, float* dlogits, uint16_t* dx,
                          float* stats, bool backward, hipStream_t s, float* dW = nullptr,

@@ -53,8 +53,12 @@ class VarSpec:
 
 class FlatState:
     def __init__(self, specs: list[VarSpec], device: torch.device | str = "cpu",
-                 optimizer: OptimizerSpec | None = None, seed: int = 0):
+                 optimizer: OptimizerSpec | None = None, seed: int = 0,
+                 compute_dtype: torch.dtype = torch.bfloat16):
         self.device = torch.device(device)
+        # fp32 models compute straight from the master (no mirror); bf16
+        # models keep a bf16 compute copy refreshed by the optimizer launch
+        self.compute_dtype = compute_dtype
         train = [s for s in specs if s.trainable]
         frozen = [s for s in specs if not s.trainable]
         off = 0
@@ -72,7 +76,8 @@ class FlatState:
         self.model32 = torch.zeros(self.n_total, dtype=torch.float32, device=dev)
         self.params32 = self.model32[: self.n_params]
         self.grad32 = torch.zeros(max(self.n_params, ALIGN), dtype=torch.float32, device=dev)[: self.n_params]
-        self.p16 = torch.zeros(self.n_params, dtype=torch.bfloat16, device=dev)
+        self.p16 = (torch.zeros(self.n_params, dtype=torch.bfloat16, device=dev)
+                    if compute_dtype == torch.bfloat16 else None)
         self.anchor: torch.Tensor | None = None
         self.m: torch.Tensor | None = None
         self.v: torch.Tensor | None = None
@@ -95,8 +100,13 @@ class FlatState:
 
     def bf16(self, name: str) -> torch.Tensor:
         s = self.by_name[name]
-        assert s.trainable
+        assert s.trainable and self.p16 is not None
         return self.p16[s.offset: s.offset + s.numel].view(s.shape)
+
+    def compute(self, name: str) -> torch.Tensor:
+        """The weight view the kernels read: the bf16 mirror, or the fp32
+        master itself for reference-precision models."""
+        return self.bf16(name) if self.p16 is not None else self.view(name)
 
     # ---- init ---------------------------------------------------------------
     def initialize(self, seed: int = 0) -> None:
@@ -125,7 +135,7 @@ class FlatState:
         self.refresh_bf16()
 
     def refresh_bf16(self) -> None:
-        if self.n_params:
+        if self.n_params and self.p16 is not None:
             opt_ops.cast_bf16(self.params32, self.p16)
 
     # ---- optimizer ----------------------------------------------------------

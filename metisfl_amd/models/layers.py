@@ -30,7 +30,8 @@ class Workspace:
     model-wide fp64 BatchNorm accumulator buffer, carved per layer.  The
     accumulators are re-zeroed by the optimizer launch at the end of a step."""
 
-    def __init__(self):
+    def __init__(self, dtype: torch.dtype = torch.bfloat16):
+        self.dtype = dtype  # activation / compute dtype of the model
         self.split_floats = 0
         self.split: torch.Tensor | None = None
         self.acc_len = 0
@@ -90,7 +91,8 @@ class Layer:
 
 
 class ConvBN(Layer):
-    """conv(k x k, stride) -> BatchNorm -> [+ residual] -> [ReLU], NHWC bf16."""
+    """conv(k x k, stride) -> BatchNorm -> [+ residual] -> [ReLU], NHWC in the
+    model's compute dtype (fp32: reference precision, or bf16)."""
 
     def __init__(self, name: str, N: int, H: int, W: int, cin: int, cout: int, k: int,
                  stride: int, relu: bool = True, residual: bool = False, momentum: float = 0.1,
@@ -130,7 +132,7 @@ class ConvBN(Layer):
         s, n = self.shp, self.name
         self.st = st
         self.ws = ws
-        self.w16 = st.bf16(f"{n}.conv.weight")
+        self.w16 = st.compute(f"{n}.conv.weight")
         self.dw = st.grad(f"{n}.conv.weight")
         self.gamma = st.view(f"{n}.bn.gamma")
         self.beta = st.view(f"{n}.bn.beta")
@@ -138,7 +140,7 @@ class ConvBN(Layer):
         self.dbeta = st.grad(f"{n}.bn.beta")
         self.rmean = st.view(f"{n}.bn.moving_mean")
         self.rvar = st.view(f"{n}.bn.moving_variance")
-        bf = dict(dtype=torch.bfloat16, device=device)
+        bf = dict(dtype=ws.dtype, device=device)
         f32 = dict(dtype=torch.float32, device=device)
         self.z = torch.zeros(self.out_shape, **bf)      # conv output (pre-BN)
         self.y = torch.zeros(self.out_shape, **bf)      # layer output
@@ -150,9 +152,9 @@ class ConvBN(Layer):
         self.acc_f = ws.take_acc(2 * s.Co)
         self.acc_b = ws.take_acc(2 * s.Co)
         dev = torch.device(device)
-        self.pf = K.conv_plan(0, s, dev)
-        self.pd = K.conv_plan(1, s, dev)
-        self.pw = K.conv_plan(2, s, dev)
+        self.pf = K.conv_plan(0, s, dev, ws.dtype)
+        self.pd = K.conv_plan(1, s, dev, ws.dtype)
+        self.pw = K.conv_plan(2, s, dev, ws.dtype)
         ws.need_split(self.pf.workspace)
         ws.need_split(self.pd.workspace)
 
@@ -227,10 +229,10 @@ class BasicBlock(Layer):
     def bind(self, st, ws, device):
         for l in self.sublayers():
             l.bind(st, ws, device)
-        self.da = torch.zeros(self.c1.out_shape, dtype=torch.bfloat16, device=device)
+        self.da = torch.zeros(self.c1.out_shape, dtype=ws.dtype, device=device)
         self.dres = None
         if self.sc is not None:
-            self.dres = torch.zeros(self.out_shape, dtype=torch.bfloat16, device=device)
+            self.dres = torch.zeros(self.out_shape, dtype=ws.dtype, device=device)
 
     def prepare_backward(self):
         for l in self.sublayers():
@@ -240,7 +242,8 @@ class BasicBlock(Layer):
         if self.sc is None:
             a = self.c1.forward(x, train=train)
             return self.c2.forward(a, residual=x, train=train)
-        if not self.c1.ws.overlap and self.c1.shp.R == 3 and self.c1.shp.stride == 2:
+        if (not self.c1.ws.overlap and self.c1.shp.R == 3 and self.c1.shp.stride == 2
+                and self.c1.ws.dtype == torch.bfloat16):
             # conv1 and the projection shortcut in one paired launch
             c1, sc = self.c1, self.sc
             c1.x = sc.x = x
@@ -300,7 +303,7 @@ class ClassifierHead(Layer):
         f32 = dict(dtype=torch.float32, device=device)
         self.feat = torch.zeros(self.N * self.C, **f32)
         self.dlogits = torch.zeros(self.N * self.K, **f32)
-        self.dx = torch.zeros((self.N, self.HW, self.C), dtype=torch.bfloat16, device=device)
+        self.dx = torch.zeros((self.N, self.HW, self.C), dtype=ws.dtype, device=device)
 
     def forward_backward(self, x, labels, stats, train=True):
         # the weight gradient rides in the same launch (atomics into the

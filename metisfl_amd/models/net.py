@@ -23,9 +23,9 @@ from metisfl_amd.ops.optim import OptimizerSpec
 
 
 class DeviceDataset:
-    """A learner's shard resident in device memory (bf16 NHWC rows, int32
-    labels) plus a per-epoch permutation buffer.  Rows are padded so each is a
-    multiple of 8 elements (16-B vector gathers)."""
+    """A learner's shard resident in device memory (NHWC rows in the model's
+    compute dtype, int32 labels) plus a per-epoch permutation buffer.  Rows
+    are padded so each is a multiple of 8 elements (16-B vector gathers)."""
 
     def __init__(self, x: torch.Tensor, y: torch.Tensor, batch_size: int, seed: int = 0,
                  shuffle: bool = True, drop_last: bool = True):
@@ -62,6 +62,9 @@ class StaticNet:
 
     input_channels_padded: int = 8
     num_classes: int = 10
+    # activation / compute dtype: bf16 (mixed precision, the default of the
+    # example models) or fp32 (reference precision -- ResNet18's default)
+    compute_dtype: torch.dtype = torch.bfloat16
 
     def __init__(self, batch_size: int, device="cpu", optimizer: OptimizerSpec | None = None,
                  seed: int = 0):
@@ -71,14 +74,15 @@ class StaticNet:
         specs: list[VarSpec] = []
         for l in self.all_layers():
             specs.extend(l.specs())
-        self.state = FlatState(specs, self.device, optimizer or OptimizerSpec(), seed=seed)
-        self.ws = Workspace()
+        self.state = FlatState(specs, self.device, optimizer or OptimizerSpec(), seed=seed,
+                               compute_dtype=self.compute_dtype)
+        self.ws = Workspace(self.compute_dtype)
         for l in self.all_layers():
             l.bind(self.state, self.ws, self.device)
         self.ws.allocate(self.device)
         self.post_bind()
         dev = self.device
-        self.xb = torch.zeros((self.B,) + self.input_shape, dtype=torch.bfloat16, device=dev)
+        self.xb = torch.zeros((self.B,) + self.input_shape, dtype=self.compute_dtype, device=dev)
         self.yb = torch.zeros(self.B, dtype=torch.int32, device=dev)
         self.stats = torch.zeros(4, dtype=torch.float32, device=dev)
         self.eval_step_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -204,14 +208,15 @@ class StaticNet:
     # -- data helpers ----------------------------------------------------------
     def make_dataset(self, x_nhwc: np.ndarray | torch.Tensor, y: np.ndarray | torch.Tensor,
                      seed: int = 0, shuffle: bool = True, batch_size: int | None = None) -> DeviceDataset:
-        """Upload a shard: pads channels to the model's input width, casts to bf16."""
+        """Upload a shard: pads channels to the model's input width, casts to
+        the compute dtype."""
         x = torch.as_tensor(x_nhwc)
         if x.dim() > 2 and len(self.input_shape) == 1:
             x = x.reshape(x.shape[0], -1)  # (N, H, W[, 1]) images into a flat MLP input
         if x.shape[-1] < self.input_shape[-1]:
             pad = self.input_shape[-1] - x.shape[-1]
             x = torch.nn.functional.pad(x, (0, pad))  # zero channels / features up to the 8-wide rows
-        x = x.to(torch.bfloat16).to(self.device)
+        x = x.to(self.compute_dtype).to(self.device)
         y = torch.as_tensor(y)
         if y.is_floating_point():  # regression targets: fp32 bits in the int32 label slots
             y = y.to(torch.float32).contiguous().view(torch.int32)

@@ -10,6 +10,12 @@ variables including BatchNorm moving statistics.
 
 The 3 input channels are zero-padded to 8 once, at shard upload, so the stem
 conv runs on the same 16-B-vectorised MFMA path as every other conv.
+
+Precision: ``dtype="fp32"`` (default) trains at the reference's precision --
+Keras trains fp32 (examples/keras/models/cifar_cnn.py:19-41, no
+mixed-precision policy; keras_model_ops.py:117-197) -- on the exact fp32 MFMA
+kernels (conv32.hip / bn32.hip).  ``dtype="bf16"`` is the mixed-precision
+option (bf16 activations and weights, fp32 master / accumulation).
 """
 from __future__ import annotations
 
@@ -18,6 +24,8 @@ import torch
 from metisfl_amd.models.layers import BasicBlock, ClassifierHead, ConvBN
 from metisfl_amd.models.net import StaticNet
 
+DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16}
+
 
 class ResNet18(StaticNet):
     input_shape = (32, 32, 8)
@@ -25,7 +33,8 @@ class ResNet18(StaticNet):
     widths = (64, 128, 256, 512)
 
     def __init__(self, batch_size: int = 32, device="cpu", optimizer=None, seed: int = 0,
-                 width_mult: float = 1.0, num_classes: int = 10):
+                 width_mult: float = 1.0, num_classes: int = 10, dtype: str = "fp32"):
+        self.compute_dtype = DTYPES[dtype]
         self.width_mult = width_mult
         self.num_classes = num_classes
         super().__init__(batch_size, device, optimizer, seed)
@@ -53,7 +62,7 @@ class ResNet18(StaticNet):
     def post_bind(self):
         dev = self.device
         # gradient buffers at block boundaries: dx of block i is dout of block i-1
-        self.dacts = [torch.zeros(b.in_shape, dtype=torch.bfloat16, device=dev) for b in self.blocks]
+        self.dacts = [torch.zeros(b.in_shape, dtype=self.compute_dtype, device=dev) for b in self.blocks]
 
     def forward(self, x, train):
         h = self.stem.forward(x, train=train)

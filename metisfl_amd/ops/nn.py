@@ -6,9 +6,15 @@ batch gather).  CPU tensors use plain-PyTorch references with identical
 semantics; they power the host-only test suite and are what the GPU numerics
 tests compare the kernels against.
 
-Tensor conventions: activations NHWC bf16 ``[N, H, W, C]``; conv weights KRSC
-bf16 ``[Cout, R, S, Cin]`` (compute copy) with an fp32 master elsewhere; all
-per-channel BatchNorm state is fp32.
+Tensor conventions: activations NHWC ``[N, H, W, C]``; conv weights KRSC
+``[Cout, R, S, Cin]``; all per-channel BatchNorm state is fp32.  Two compute
+precisions share these ops and dispatch on the activation dtype:
+
+* fp32 -- the reference precision (Keras trains fp32): conv32.hip on the exact
+  fp32 MFMA (v_mfma_f32_32x32x2_f32), bn32.hip, the fp32 head; weights are the
+  fp32 master itself.
+* bf16 -- the explicit mixed-precision option: conv.hip on bf16 MFMA with a
+  bf16 compute copy of the weights.
 """
 from __future__ import annotations
 
@@ -58,11 +64,12 @@ class ConvPlan:
     workspace: int
 
 
-def conv_plan(mode: int, shp: ConvShape, device: torch.device) -> ConvPlan:
+def conv_plan(mode: int, shp: ConvShape, device: torch.device, dtype=torch.bfloat16) -> ConvPlan:
     """mode 0 fwd / 1 dgrad / 2 wgrad (tile sizes, split-K factor, fp32 split-K
     workspace floats).  CPU path: no workspace."""
     if device.type == "cuda":
-        return ConvPlan(*ops().conv_plan(mode, *shp.args()))
+        fn = ops().conv32_plan if dtype == torch.float32 else ops().conv_plan
+        return ConvPlan(*fn(mode, *shp.args()))
     return ConvPlan(0, 0, 1, 0, 1, 0)
 
 
@@ -87,10 +94,13 @@ def conv_forward(x, w, y, shp: ConvShape, ws=None, stats=None) -> None:
     """y = conv(x, w); ``stats`` (fp64 [2*Cout]) accumulates the per-channel
     sum / sum-of-squares of the bf16 output for the following BatchNorm."""
     if x.is_cuda:
-        ops().conv_forward(x, w, y, ws, stats, *shp.args())
+        if x.dtype == torch.float32:
+            ops().conv32_forward(x, w, y, ws, stats, *shp.args())
+        else:
+            ops().conv_forward(x, w, y, ws, stats, *shp.args())
         return
     out = F.conv2d(_nchw(x), _wt(w), stride=shp.stride, padding=shp.pad)
-    y.copy_(out.permute(0, 2, 3, 1).to(torch.bfloat16))
+    y.copy_(out.permute(0, 2, 3, 1).to(y.dtype))
     if stats is not None:
         _acc_stats_cpu(y, stats)
 
@@ -124,11 +134,11 @@ def conv_dgrad(dy, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
     (the kernel forms W^T fragments with transposing LDS reads).  ``bnb``:
     fuse the consumer BatchNorm-backward reductions into the epilogue."""
     if dy.is_cuda:
+        fn = ops().conv32_dgrad if dy.dtype == torch.float32 else ops().conv_dgrad
         if bnb is None:
-            ops().conv_dgrad(dy, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None)
+            fn(dy, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None)
         else:
-            ops().conv_dgrad(dy, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean, bnb.invstd,
-                             bnb.acc)
+            fn(dy, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean, bnb.invstd, bnb.acc)
         return
     _conv_dgrad_cpu(dy, w, dx, shp, accumulate)
     if bnb is not None:
@@ -142,14 +152,15 @@ def _conv_dgrad_cpu(dy, w, dx, shp: ConvShape, accumulate: bool) -> None:
     g = g.permute(0, 2, 3, 1)
     if accumulate:
         g = g + dx.float()
-    dx.copy_(g.to(torch.bfloat16))
+    dx.copy_(g.to(dx.dtype))
 
 
 def conv_wgrad(x, dy, dw, shp: ConvShape, accumulate: bool = False) -> None:
     """dw (fp32 [Cout][R][S][Cin]) = sum over pixels of dy x im2col(x).
     accumulate=True promises dw is already zero (split-K slices add into it)."""
     if x.is_cuda:
-        ops().conv_wgrad(x, dy, dw, *shp.args(), accumulate)
+        fn = ops().conv32_wgrad if x.dtype == torch.float32 else ops().conv_wgrad
+        fn(x, dy, dw, *shp.args(), accumulate)
         return
     # contiguous NCHW: torch's CPU weight-gradient kernel corrupts the heap on
     # channels-last views for strided 1x1 convs with few channels (observed
@@ -163,7 +174,7 @@ def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShap
     """A downsampling block's conv1 (3x3, stride 2; ``shp``) and its 1x1 / stride-2
     projection shortcut of the same x -- one paired launch on the GPU."""
     assert shp.R == 3 and shp.stride == 2
-    if x.is_cuda:
+    if x.is_cuda and x.dtype != torch.float32:
         ops().conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp.N, shp.H, shp.W, shp.C, shp.Co)
         return
     conv_forward(x, w1, y1, shp, ws1, stats1)
@@ -175,8 +186,9 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
     """A layer's weight gradient (dw += ..., dw zero on entry) and input
     gradient (as conv_dgrad) -- on the GPU in ONE paired launch, so the two
     independent, latency-bound GEMMs share the CUs (conv.hip
-    conv_bwd_pair_kernel; MFL_CONV_PAIR=0 for two launches)."""
-    if dy.is_cuda:
+    conv_bwd_pair_kernel; MFL_CONV_PAIR=0 for two launches).  fp32: two
+    launches (the fp32 GEMMs are compute-bound; pairing buys nothing)."""
+    if dy.is_cuda and dy.dtype != torch.float32:
         if bnb is None:
             ops().conv_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None,
                                      None)
@@ -199,7 +211,7 @@ def transpose_krsc(w, wt, Co: int, RS: int, Ci: int) -> None:
 def bn_stats(x, C: int, acc) -> None:
     """acc[0:C] += sum x, acc[C:2C] += sum x^2 (fp64) over the rows of NHWC x."""
     if x.is_cuda:
-        ops().bn_stats(x, C, acc)
+        (ops().bn32_stats if x.dtype == torch.float32 else ops().bn_stats)(x, C, acc)
         return
     _acc_stats_cpu(x, acc)
 
@@ -211,8 +223,8 @@ def bn_apply(x, C: int, acc, gamma, beta, mean, invstd, run_mean, run_var, y, re
     over the M rows), publishes mean/invstd, updates running stats; eval:
     running statistics."""
     if x.is_cuda:
-        ops().bn_apply(x, C, acc, gamma, beta, mean, invstd, run_mean, run_var, residual, y, relu,
-                       train, momentum, eps)
+        fn = ops().bn32_apply if x.dtype == torch.float32 else ops().bn_apply
+        fn(x, C, acc, gamma, beta, mean, invstd, run_mean, run_var, residual, y, relu, train, momentum, eps)
         return
     M = x.numel() // C
     if train:
@@ -235,7 +247,7 @@ def bn_apply(x, C: int, acc, gamma, beta, mean, invstd, run_mean, run_var, y, re
         v = v + residual.float()
     if relu:
         v = v.clamp_min(0)
-    y.copy_(v.to(torch.bfloat16))
+    y.copy_(v.to(y.dtype))
 
 
 def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
@@ -245,13 +257,14 @@ def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
     residual-shortcut gradient of an add+ReLU).  ``acc`` (fp64 [2C]) must be
     zero on entry."""
     if dy.is_cuda:
-        ops().bn_backward(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked, presummed)
+        fn = ops().bn32_backward if dy.dtype == torch.float32 else ops().bn_backward
+        fn(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked, presummed)
         return
     g = dy.float()
     if y is not None:
         g = torch.where(y.float() > 0, g, torch.zeros_like(g))
         if dy_masked is not None:
-            dy_masked.copy_(g.to(torch.bfloat16))
+            dy_masked.copy_(g.to(dy_masked.dtype))
     xf = x.float()
     xh = (xf - mean) * invstd
     gm = g.reshape(-1, C)
@@ -265,7 +278,7 @@ def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
         dbeta.copy_(acc[:C].float())
     k1 = gamma * invstd
     out = k1 * (g - (acc[:C] / M).float() - xh * (acc[C:2 * C] / M).float())
-    dx.copy_(out.to(torch.bfloat16))
+    dx.copy_(out.to(dx.dtype))
 
 
 # ---------------------------------------------------------------------------
@@ -276,8 +289,8 @@ def head_forward_backward(x, B: int, HW: int, C: int, W, bias, labels, feat, dlo
     the weight / bias gradients are ADDED in the same launch (fused
     head_wgrad; the buffers must hold zeros or a running sum)."""
     if x.is_cuda:
-        ops().head_forward_backward(x, B, HW, C, W, bias, labels, feat, dlogits, dx, stats,
-                                    backward, dW, db)
+        fn = ops().head32_forward_backward if x.dtype == torch.float32 else ops().head_forward_backward
+        fn(x, B, HW, C, W, bias, labels, feat, dlogits, dx, stats, backward, dW, db)
         return
     xf = x.float().reshape(B, HW, C)
     f = xf.mean(1)
@@ -298,7 +311,7 @@ def head_forward_backward(x, B: int, HW: int, C: int, W, bias, labels, feat, dlo
     feat.view(-1)[: B * C].copy_(f.reshape(-1))
     dlogits.view(-1)[: B * K].copy_(d.reshape(-1))
     dfeat = d @ W.reshape(K, C)
-    dx.copy_((dfeat / HW)[:, None, :].expand(B, HW, C).reshape(dx.shape).to(torch.bfloat16))
+    dx.copy_((dfeat / HW)[:, None, :].expand(B, HW, C).reshape(dx.shape).to(dx.dtype))
     if dW is not None:
         dW.add_((d.t() @ f).reshape(dW.shape))
         if db is not None:
@@ -318,7 +331,8 @@ def head_wgrad(feat, dlogits, B: int, C: int, K: int, dW, db) -> None:
 
 def gather_batch(shard, labels, perm, step, steps_per_epoch: int, B: int, xb, yb) -> None:
     if shard.is_cuda:
-        ops().gather_batch(shard, labels, perm, step, steps_per_epoch, B, xb, yb)
+        fn = ops().gather_batch32 if shard.dtype == torch.float32 else ops().gather_batch
+        fn(shard, labels, perm, step, steps_per_epoch, B, xb, yb)
         return
     s = int(step[0]) % steps_per_epoch
     idx = perm[s * B:(s + 1) * B].long()

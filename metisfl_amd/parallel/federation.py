@@ -272,7 +272,9 @@ class CollectiveFederation:
         ceil(lambda * max_i(ms_per_epoch_i) / ms_per_batch_self) updates."""
         if self.cfg.protocol != "semi_synchronous":
             return
-        if not (self.global_iteration == 2 or self.cfg.semi_sync_recompute):
+        # called at the end of round ``global_iteration``: the end of round 1
+        # sets the budgets round 2 runs with (controller.cc:527-532)
+        if not (self.global_iteration == 1 or self.cfg.semi_sync_recompute):
             return
         t_max = self.cfg.semi_sync_lambda * float(meta[:, 3].max())
         self.num_local_updates = [max(1, int(math.ceil(t_max / max(1e-6, float(mpb)))))

@@ -64,8 +64,11 @@ def tensor_spec_to_numpy(spec: model_pb2.TensorSpec) -> np.ndarray:
         dt = dt.newbyteorder("<")
     arr = np.frombuffer(spec.value, dtype=dt, count=spec.length)
     shape = tuple(spec.dimensions) if len(spec.dimensions) else (spec.length,)
-    order = "F" if spec.type.fortran_order else "C"
-    return arr.reshape(shape, order=order)
+    # ``value`` always holds the elements in logical (C) order -- the encoder
+    # above and the reference (proto_messages_factory.py:462 ``arr.flatten()``,
+    # :492 plain reshape) both write it so; ``fortran_order`` only records the
+    # source array's memory layout and must not re-order the decode.
+    return arr.reshape(shape)
 
 
 def model_from_arrays(names, arrays, trainables=None, he_scheme=None) -> model_pb2.Model:

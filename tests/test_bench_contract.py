@@ -68,3 +68,22 @@ def test_async_bench_json_contract():
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
     assert REQUIRED <= set(d) and d["updates"] == 1
+
+
+def test_bench_spawns_its_own_ranks():
+    """``bench.py --gpus 2`` with no launcher runs 2 learners by itself."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *TINY,
+                        "--width-mult", "0.125"], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["learners"] == 2
+    assert d["collective"]["world_size"] == 2 and d["collective"]["backend"] == "gloo"
+    assert d["dtype"] == "fp32"
+
+
+def test_bench_world_size_mismatch_fails():
+    env = _env()
+    env.update({"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *TINY], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0

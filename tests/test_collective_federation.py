@@ -57,7 +57,7 @@ def _worker(rank, world, port, out_dir, mode):
         np.save(os.path.join(out_dir, f"community_r{rec.global_iteration}_rank{rank}.npy"),
                 net.state.model32.numpy())
         res["rounds"].append({"gi": rec.global_iteration, "weights": rec.weights,
-                              "updates": list(fed.num_local_updates)})
+                              "updates": list(rec.num_local_updates), "next": list(fed.num_local_updates)})
         if mode == "ckpt" and r == 0:
             fed.save_checkpoint(os.path.join(out_dir, "ckpt"))
     if rank == 0:
@@ -113,9 +113,11 @@ def test_secure_ckks_aggregation_two_ranks(tmp_path):
 def test_semi_sync_step_budgets(tmp_path):
     res = _run(tmp_path, "semi")
     r0 = res[0]["rounds"]
-    # round 1 uses epochs * ceil(n / batch); after round 2 the budgets are
-    # recomputed from lambda * slowest epoch time (controller.cc:520-569)
+    # round 1 uses epochs * ceil(n / batch); the end of round 1 recomputes
+    # the budgets from lambda * slowest epoch time, so round 2 already runs
+    # with them (controller.cc:520-569, as the native engine does)
     assert r0[0]["updates"] == [2, 3]
+    assert r0[1]["updates"] == r0[0]["next"]  # round 2 ran the recomputed budgets
     assert all(u >= 1 for u in r0[1]["updates"])
     assert res[0]["rounds"][1]["updates"] == res[1]["rounds"][1]["updates"]
 

@@ -1,0 +1,315 @@
+"""Reference-precision (fp32) learner path on the GPU.
+
+Kernel level: every fp32 conv (fwd / dgrad / wgrad, all ResNet-18 CIFAR
+shapes at batch 32 -- i.e. the real launch plans incl. split-K and the
+parity-decomposed stride-2 dgrad -- plus ragged odd shapes) is pinned against
+plain PyTorch F.conv2d / conv2d_input / conv2d_weight computed in fp64 on the
+host, at relative error <= 1e-5; BatchNorm, head and gather against the
+host reference ops.
+
+Model level: the fp32 ResNet-18 training step vs an independent torch.nn
+ResNet-18 (tests/torch_resnet_ref.py) -- loss and EVERY per-tensor gradient
+at relative error <= 1e-4, BN running statistics after the step -- and a
+300-step loss trajectory where bf16 must land within 3% of fp32.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double().cpu().flatten(), b.double().cpu().flatten()
+    return float((a - b).norm() / (b.norm() + 1e-300))
+
+
+RESNET_SHAPES = [  # N, H, W, C, Co, k, stride
+    (32, 32, 32, 8, 64, 3, 1),      # stem
+    (32, 32, 32, 64, 64, 3, 1),
+    (32, 32, 32, 64, 128, 3, 2),
+    (32, 32, 32, 64, 128, 1, 2),
+    (32, 16, 16, 128, 128, 3, 1),
+    (32, 16, 16, 128, 256, 3, 2),
+    (32, 16, 16, 128, 256, 1, 2),
+    (32, 8, 8, 256, 256, 3, 1),
+    (32, 8, 8, 256, 512, 3, 2),
+    (32, 8, 8, 256, 512, 1, 2),
+    (32, 4, 4, 512, 512, 3, 1),
+]
+ODD_SHAPES = [
+    (3, 7, 7, 12, 20, 3, 1),
+    (2, 9, 9, 8, 16, 3, 2),    # odd dX dims: masked (non-parity) stride-2 dgrad
+    (5, 6, 10, 4, 36, 1, 1),
+    (4, 10, 6, 16, 8, 1, 2),
+]
+
+
+def _shape(t):
+    from metisfl_amd.ops.nn import ConvShape
+    N, H, W, C, Co, k, s = t
+    return ConvShape(N, H, W, C, Co, k, k, s, k // 2)
+
+
+def _ws(shp):
+    from metisfl_amd.ops import nn as K
+    n = max(K.conv_plan(m, shp, torch.device(DEV), torch.float32).workspace for m in (0, 1))
+    return torch.zeros(max(4, n), dtype=torch.float32, device=DEV)
+
+
+@pytest.mark.parametrize("t", RESNET_SHAPES + ODD_SHAPES, ids=lambda t: "x".join(map(str, t)))
+def test_conv32_forward_matches_fp64(t):
+    from metisfl_amd.ops import nn as K
+    shp = _shape(t)
+    g = torch.Generator().manual_seed(hash(t) & 0xFFFF)
+    x = torch.randn(shp.N, shp.H, shp.W, shp.C, generator=g)
+    w = torch.randn(shp.Co, shp.R, shp.S, shp.C, generator=g) / (shp.R * shp.S * shp.C) ** 0.5
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), stride=shp.stride,
+                   padding=shp.pad).permute(0, 2, 3, 1)
+    y = torch.zeros(ref.shape, dtype=torch.float32, device=DEV)
+    stats = torch.zeros(2 * shp.Co, dtype=torch.float64, device=DEV)
+    ws = _ws(shp)
+    K.conv_forward(x.to(DEV), w.to(DEV), y, shp, ws, stats)
+    torch.cuda.synchronize()
+    assert _rel(y, ref) <= 1e-5
+    r2 = ref.reshape(-1, shp.Co)
+    assert _rel(stats[:shp.Co], r2.sum(0)) <= 1e-5
+    assert _rel(stats[shp.Co:], (r2 * r2).sum(0)) <= 1e-5
+    # the split-K counters re-arm: a second launch gives the same bits
+    y2 = torch.zeros_like(y)
+    K.conv_forward(x.to(DEV), w.to(DEV), y2, shp, ws, None)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("t", RESNET_SHAPES + ODD_SHAPES, ids=lambda t: "x".join(map(str, t)))
+def test_conv32_dgrad_matches_fp64(t):
+    from metisfl_amd.ops import nn as K
+    shp = _shape(t)
+    g = torch.Generator().manual_seed(7 + (hash(t) & 0xFFFF))
+    dy = torch.randn(shp.N, shp.P, shp.Q, shp.Co, generator=g)
+    w = torch.randn(shp.Co, shp.R, shp.S, shp.C, generator=g) / (shp.R * shp.S * shp.Co) ** 0.5
+    ref = torch.nn.grad.conv2d_input((shp.N, shp.C, shp.H, shp.W), w.double().permute(0, 3, 1, 2),
+                                     dy.double().permute(0, 3, 1, 2), stride=shp.stride,
+                                     padding=shp.pad).permute(0, 2, 3, 1)
+    ws = _ws(shp)
+    dx = torch.zeros(ref.shape, dtype=torch.float32, device=DEV)
+    K.conv_dgrad(dy.to(DEV), w.to(DEV), dx, shp, ws, accumulate=False)
+    torch.cuda.synchronize()
+    assert _rel(dx, ref) <= 1e-5
+    # accumulate: dx += dgrad
+    base = torch.randn(ref.shape, generator=g)
+    dx2 = base.to(DEV)
+    K.conv_dgrad(dy.to(DEV), w.to(DEV), dx2, shp, ws, accumulate=True)
+    torch.cuda.synchronize()
+    assert _rel(dx2, ref + base.double()) <= 1e-5
+
+
+def test_conv32_dgrad_fused_bn_reductions():
+    from metisfl_amd.ops import nn as K
+    shp = _shape((32, 16, 16, 128, 128, 3, 1))
+    g = torch.Generator().manual_seed(11)
+    dy = torch.randn(shp.N, shp.P, shp.Q, shp.Co, generator=g)
+    w = torch.randn(shp.Co, 3, 3, shp.C, generator=g) / (9 * shp.Co) ** 0.5
+    z = torch.randn(shp.N, shp.H, shp.W, shp.C, generator=g)
+    yv = torch.relu(torch.randn(shp.N, shp.H, shp.W, shp.C, generator=g))
+    mean = torch.randn(shp.C, generator=g)
+    invstd = torch.rand(shp.C, generator=g) + 0.5
+    acc_c = torch.zeros(2 * shp.C, dtype=torch.float64)
+    dx_c = torch.zeros(shp.N, shp.H, shp.W, shp.C)
+    K.conv_dgrad(dy, w, dx_c, shp, None, False, K.BnBwdTarget(z, yv, mean, invstd, acc_c))
+    acc_g = torch.zeros(2 * shp.C, dtype=torch.float64, device=DEV)
+    dx_g = torch.zeros(shp.N, shp.H, shp.W, shp.C, device=DEV)
+    K.conv_dgrad(dy.to(DEV), w.to(DEV), dx_g, shp, _ws(shp), False,
+                 K.BnBwdTarget(z.to(DEV), yv.to(DEV), mean.to(DEV), invstd.to(DEV), acc_g))
+    torch.cuda.synchronize()
+    assert _rel(dx_g, dx_c) <= 1e-5
+    assert _rel(acc_g, acc_c) <= 1e-5
+
+
+@pytest.mark.parametrize("t", RESNET_SHAPES + ODD_SHAPES, ids=lambda t: "x".join(map(str, t)))
+def test_conv32_wgrad_matches_fp64(t):
+    from metisfl_amd.ops import nn as K
+    shp = _shape(t)
+    g = torch.Generator().manual_seed(3 + (hash(t) & 0xFFFF))
+    x = torch.randn(shp.N, shp.H, shp.W, shp.C, generator=g)
+    dy = torch.randn(shp.N, shp.P, shp.Q, shp.Co, generator=g)
+    ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2).contiguous(),
+                                      (shp.Co, shp.C, shp.R, shp.S),
+                                      dy.double().permute(0, 3, 1, 2).contiguous(), stride=shp.stride,
+                                      padding=shp.pad).permute(0, 2, 3, 1)
+    dw = torch.full(ref.shape, 123.0, dtype=torch.float32, device=DEV)  # overwritten
+    K.conv_wgrad(x.to(DEV), dy.to(DEV), dw, shp, accumulate=False)
+    torch.cuda.synchronize()
+    assert _rel(dw, ref) <= 1e-5
+    dw2 = torch.ones(ref.shape, dtype=torch.float32, device=DEV)  # accumulate onto 1
+    K.conv_wgrad(x.to(DEV), dy.to(DEV), dw2, shp, accumulate=True)
+    torch.cuda.synchronize()
+    assert _rel(dw2, ref + 1.0) <= 1e-5
+
+
+@pytest.mark.parametrize("res,relu,train", [(False, True, True), (True, True, True), (False, False, True),
+                                            (True, True, False)])
+def test_bn32_apply_and_backward_match_host(res, relu, train):
+    from metisfl_amd.ops import nn as K
+    g = torch.Generator().manual_seed(5)
+    M, C = 4096, 128
+    x = torch.randn(M, C, generator=g) * 2 + 0.5
+    r = torch.randn(M, C, generator=g) if res else None
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g)
+    out = {}
+    for dev in ("cpu", DEV):
+        acc = torch.zeros(2 * C, dtype=torch.float64, device=dev)
+        K.bn_stats(x.to(dev), C, acc)
+        mean = torch.zeros(C, device=dev)
+        invstd = torch.zeros(C, device=dev)
+        rm = torch.full((C,), 0.1, device=dev)
+        rv = torch.full((C,), 1.5, device=dev)
+        y = torch.zeros(M, C, device=dev)
+        K.bn_apply(x.to(dev), C, acc, gamma.to(dev), beta.to(dev), mean, invstd, rm, rv, y,
+                   r.to(dev) if res else None, relu, train)
+        dy = torch.randn(M, C, generator=torch.Generator().manual_seed(9)).to(dev)
+        accb = torch.zeros(2 * C, dtype=torch.float64, device=dev)
+        dg = torch.zeros(C, device=dev)
+        db = torch.zeros(C, device=dev)
+        dx = torch.zeros(M, C, device=dev)
+        dym = torch.zeros(M, C, device=dev) if relu else None
+        if train:
+            K.bn_backward(dy, x.to(dev), y if relu else None, C, gamma.to(dev), mean, invstd, accb, dg, db,
+                          dx, dym)
+        out[dev] = [t.cpu() for t in (acc, mean, invstd, rm, rv, y, dg, db, dx) + ((dym,) if relu else ())]
+    for a, b in zip(out["cpu"], out[DEV]):
+        assert _rel(b, a) <= 1e-5
+
+
+def test_head32_and_gather32_match_host():
+    from metisfl_amd.ops import nn as K
+    g = torch.Generator().manual_seed(1)
+    B, HW, C, NC = 32, 16, 512, 10
+    x = torch.randn(B, HW, C, generator=g)
+    W = torch.randn(NC, C, generator=g) * 0.05
+    b = torch.randn(NC, generator=g) * 0.1
+    lab = torch.randint(0, NC, (B,), generator=g, dtype=torch.int32)
+    res = {}
+    for dev in ("cpu", DEV):
+        feat = torch.zeros(B * C, device=dev)
+        dl = torch.zeros(B * NC, device=dev)
+        dx = torch.zeros(B, HW, C, device=dev)
+        st = torch.zeros(4, device=dev)
+        dW = torch.zeros(NC, C, device=dev)
+        db = torch.zeros(NC, device=dev)
+        K.head_forward_backward(x.to(dev), B, HW, C, W.to(dev), b.to(dev), lab.to(dev), feat, dl, dx, st,
+                                True, dW, db)
+        res[dev] = [t.cpu() for t in (feat, dl, dx, st[:3], dW, db)]
+    for a, c in zip(res["cpu"], res[DEV]):
+        assert _rel(c, a) <= 1e-5
+    # gather: fp32 rows through the permutation at the device step counter
+    shard = torch.randn(64, 32, 32, 8, generator=g)
+    labels = torch.randint(0, 10, (64,), generator=g, dtype=torch.int32)
+    perm = torch.randperm(64, generator=g).to(torch.int32)
+    step = torch.tensor([3], dtype=torch.int32)
+    xb = torch.zeros(16, 32, 32, 8, device=DEV)
+    yb = torch.zeros(16, dtype=torch.int32, device=DEV)
+    K.gather_batch(shard.to(DEV), labels.to(DEV), perm.to(DEV), step.to(DEV), 4, 16, xb, yb)
+    torch.cuda.synchronize()
+    idx = perm[(3 % 4) * 16:(3 % 4 + 1) * 16].long()
+    assert torch.equal(xb.cpu(), shard[idx]) and torch.equal(yb.cpu(), labels[idx])
+
+
+# ---------------------------------------------------------------------------
+def _x8(x):
+    return F.pad(torch.as_tensor(x), (0, 5))
+
+
+def test_fp32_resnet18_step_matches_torch_nn():
+    """The whole fp32 training step (gather -> 20 conv/BN layers -> head ->
+    backward) vs an independent torch.nn ResNet-18 in fp64."""
+    from metisfl_amd.models.resnet import ResNet18
+    from metisfl_amd.ops.optim import OptimizerSpec
+    from tests.torch_resnet_ref import reference_step
+    rng = np.random.default_rng(0)
+    B = 32
+    x = rng.standard_normal((B, 32, 32, 3)).astype(np.float32)
+    y = rng.integers(0, 10, B)
+    net = ResNet18(batch_size=B, device=DEV, optimizer=OptimizerSpec("vanilla_sgd", 0.0), seed=4)
+    assert net.compute_dtype == torch.float32
+    values = net.state.to_numpy()
+    ds = net.make_dataset(x, y, shuffle=False)
+    net.zero_grad_in_optimizer = False
+    net.reset_train_stats()
+    net._train_body(ds)
+    torch.cuda.synchronize()
+    loss = net.train_stats()["loss"]
+    ref_loss, ref_g, ref_run = reference_step(values, _x8(x), torch.as_tensor(y))
+    assert abs(loss - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss)), (loss, ref_loss)
+    worst = []
+    for name, rg in ref_g.items():
+        err = _rel(net.state.grad(name), rg)
+        worst.append((err, name))
+        assert err <= 1e-4, (name, err)
+    worst.sort(reverse=True)
+    print("worst per-tensor gradient rel err:", worst[:4])
+    for name, rv in ref_run.items():
+        assert _rel(net.state.view(name), rv) <= 1e-5, name
+
+
+def test_bf16_resnet18_step_tracks_torch_nn():
+    """The mixed-precision option against the same fp32-exact oracle: cosine
+    of the whole gradient and of every conv weight gradient."""
+    from metisfl_amd.models.resnet import ResNet18
+    from metisfl_amd.ops.optim import OptimizerSpec
+    from tests.torch_resnet_ref import reference_step
+    rng = np.random.default_rng(1)
+    B = 32
+    x = rng.standard_normal((B, 32, 32, 3)).astype(np.float32)
+    y = rng.integers(0, 10, B)
+    net = ResNet18(batch_size=B, device=DEV, optimizer=OptimizerSpec("vanilla_sgd", 0.0), seed=4, dtype="bf16")
+    values = net.state.to_numpy()
+    ds = net.make_dataset(x, y, shuffle=False)
+    net.zero_grad_in_optimizer = False
+    net._train_body(ds)
+    torch.cuda.synchronize()
+    _, ref_g, _ = reference_step(values, _x8(x), torch.as_tensor(y))
+
+    def cos(a, b):
+        a, b = a.double().cpu().flatten(), b.double().cpu().flatten()
+        return float(a @ b / (a.norm() * b.norm() + 1e-300))
+
+    allg = torch.cat([net.state.grad(n).flatten().cpu() for n in ref_g])
+    allr = torch.cat([ref_g[n].flatten() for n in ref_g])
+    c_all = cos(allg, allr)
+    per = sorted((cos(net.state.grad(n), ref_g[n]), n) for n in ref_g if n.endswith("conv.weight"))
+    print(f"bf16 gradient cosine {c_all:.5f}; lowest conv tensors {per[:3]}")
+    assert c_all >= 0.99
+    assert per[0][0] >= 0.95
+
+
+def test_loss_trajectory_bf16_within_3pct_of_fp32():
+    """300 local updates on a learnable synthetic task: the bf16 final loss
+    lands within 3% (or 0.02 absolute) of the fp32 one."""
+    from metisfl_amd.models.resnet import ResNet18
+    from metisfl_amd.ops.optim import OptimizerSpec
+    rng = np.random.default_rng(0)
+    n = 960
+    x = rng.standard_normal((n, 32, 32, 3)).astype(np.float32)
+    y = rng.integers(0, 10, n)
+    x[np.arange(n), :, :, y % 3] += ((y[:, None, None] // 3) - 1.5) * 0.6
+    final = {}
+    for dt in ("fp32", "bf16"):
+        net = ResNet18(batch_size=32, device=DEV, optimizer=OptimizerSpec("momentum_sgd", 0.01, momentum=0.75),
+                       seed=7, dtype=dt)
+        ds = net.make_dataset(x, y, seed=1)
+        spe = ds.steps_per_epoch
+        curve = []
+        for ep in range(10):  # 10 x 30 = 300 updates
+            net.reset_train_stats()
+            net.train_steps(ds, spe, ep * spe)
+            curve.append(net.train_stats()["loss"])
+        final[dt] = curve[-1]
+        print(dt, [round(c, 4) for c in curve])
+    assert final["fp32"] < 1.0  # the task was learned
+    assert abs(final["bf16"] - final["fp32"]) <= max(0.03 * final["fp32"], 0.02), final

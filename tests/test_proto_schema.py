@@ -98,3 +98,18 @@ def test_all_services_present():
     assert service_common_pb2.Ack().DESCRIPTOR.fields_by_name["timestamp"].number == 2
     assert metis_pb2.FederatedTaskRuntimeMetadata.DESCRIPTOR.fields_by_name[
         "model_tensor_quantifiers"].number == 18
+
+
+def test_fortran_ordered_array_round_trips():
+    """A transposed (F-contiguous) weight keeps its values: the bytes are in
+    logical C order and the fortran_order flag only records the layout, as
+    in the reference (proto_messages_factory.py:462,492)."""
+    import numpy as np
+    from metisfl_amd.utils.tensor_codec import numpy_to_tensor_spec, tensor_spec_to_numpy
+    a = np.asfortranarray(np.arange(6, dtype=np.float32).reshape(2, 3))
+    spec = numpy_to_tensor_spec(a)
+    assert spec.type.fortran_order
+    assert spec.value == np.arange(6, dtype=np.float32).tobytes()
+    np.testing.assert_array_equal(tensor_spec_to_numpy(spec), a)
+    t = np.arange(12, dtype=np.float64).reshape(3, 4).T  # a view, F-contiguous
+    np.testing.assert_array_equal(tensor_spec_to_numpy(numpy_to_tensor_spec(t)), t)
