@@ -5,6 +5,17 @@
 
 namespace mfl {
 
+// Branch-free division by a runtime divisor d >= 1 for 0 <= x < 2^31:
+// q = (umulhi(x, m) >> sh) + (x & id), with m = ceil(2^(31+s) / d),
+// s = ceil(log2 d), sh = s - 1 (d = 1: m = 0, id = ~0).  Replaces the
+// shift-or-divide branches in the DMA address math, which split the k-loop
+// into basic blocks the scheduler could not interleave with the MFMAs.
+struct FastDiv {
+  uint32_t m;
+  int sh;
+  uint32_t id;
+};
+
 struct Conv32Args {
   ConvGeom g;          // fwd geometry, or the role-swapped dgrad geometry (conv.h)
   const float* src;    // fwd: X; dgrad: dY
@@ -23,7 +34,7 @@ struct Conv32Args {
   int kchunk;
   int accum;
   int par_mc;
-  int c_shift, q_shift, pq_shift;
+  FastDiv dc, dq, dpq;  // / C, / Q, / (P*Q)
 };
 
 struct BnBwdFusion32 {

@@ -53,11 +53,19 @@ constexpr int kTiles = kStages - 1;  // k-tiles in flight
 __device__ __forceinline__ f32x16 mfma_f32(float a, float b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ int sdiv(int x, int d, int shift) { return shift >= 0 ? x >> shift : x / d; }
+__device__ __forceinline__ int fdiv(int x, const FastDiv& f) {
+  return (int)((__umulhi((uint32_t)x, f.m) >> f.sh) + ((uint32_t)x & f.id));
+}
 
 // fp32 [row][32] tile, 128-B rows: 16-B chunk ch of `row`
 __device__ __forceinline__ int rk_off(int row, int ch) { return row * 128 + ((ch ^ swz_b128<128>(row)) << 4); }
 
+// k-loop over the LDS ring.  compute(stage, mid) runs the MFMAs of the tile
+// in `stage` and calls mid() once its first k-group is issued: the DMA of
+// tile kt+2 (address math included) is placed there, so its VALU/SALU work
+// issues while the matrix pipe is busy instead of in front of it.  Stage
+// (kt+2)%3 is free: every wave passed this iteration's barrier, i.e. finished
+// reading it in iteration kt-1.
 template <int L, typename Issue, typename Compute>
 __device__ __forceinline__ void ring_loop(int nk, Issue& issue, Compute& compute) {
 #pragma unroll
@@ -69,8 +77,11 @@ __device__ __forceinline__ void ring_loop(int nk, Issue& issue, Compute& compute
     if (kt + 1 < nk) wait_vmcnt<L>();
     else wait_vmcnt<0>();
     lds_barrier();  // every wave's tile kt landed, every wave left stage (kt-1)%3
-    if (kt + kTiles < nk) issue(kt + kTiles, stage == 0 ? kStages - 1 : stage - 1);
-    compute(stage);
+    const int nxt = kt + kTiles;
+    const int nst = stage == 0 ? kStages - 1 : stage - 1;
+    compute(stage, [&] {
+      if (nxt < nk) issue(nxt, nst);
+    });
     stage = stage == kStages - 1 ? 0 : stage + 1;
   }
 }
@@ -223,9 +234,9 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
       a_y0[i] = y + dh;
       a_x0[i] = rem - y * q2 + dw;
     } else {
-      const int n = sdiv(mm, g.P * g.Q, a.pq_shift);
+      const int n = fdiv(mm, a.dpq);
       const int rem = mm - n * g.P * g.Q;
-      const int oy = sdiv(rem, g.Q, a.q_shift);
+      const int oy = fdiv(rem, a.dq);
       const int ox = rem - oy * g.Q;
       a_nb[i] = n * HWC;
       a_y0[i] = DGRAD ? oy + g.pad : oy * ST - g.pad;
@@ -239,7 +250,7 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
     const int kb = kbeg + kt * kBK;
     {
       const int k = kb + a_kc;
-      const int rs = sdiv(k, g.C, a.c_shift);
+      const int rs = fdiv(k, a.dc);
       const int c = k - rs * g.C;
       const int r = PAR ? (ns == 2 ? rs >> 1 : rs) : rs / KS;
       const int s = PAR ? rs - r * ns : rs - r * KS;
@@ -275,7 +286,7 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
         const int row = (wave + 4 * i) * B_RPI + lane / B_CPR;  // k within the tile
         const int n = n0 + (lane % B_CPR) * 4;
         const int kr = kb + row;
-        int rs = sdiv(kr, g.C, a.c_shift);
+        int rs = fdiv(kr, a.dc);
         const int ko = kr - rs * g.C;
         if (PAR) {  // class tap index -> kernel tap (r0 + 2 j_r, s0 + 2 j_s)
           const int jr = ns == 2 ? rs >> 1 : rs;
@@ -300,34 +311,47 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int li = lane & 31, lh = lane >> 5;
-  auto compute = [&](int stage) {
+  // fragments of k-group grp (8 k): A as one ds_read_b128 per 32-row tile,
+  // B likewise (fwd) or as 4 ds_read_b32 of the [k][n] tile (dgrad)
+  auto load = [&](const uint8_t* As, const uint8_t* Bs, int grp, f32x4* af, f32x4* bfr) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * (BM / 2) + 32 * i + li;
+      af[i] = *reinterpret_cast<const f32x4*>(As + rk_off(row, 2 * grp + lh));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * (BN / 2) + 32 * j + li;
+      if constexpr (DGRAD) {
+        const float* Bf = reinterpret_cast<const float*>(Bs);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bfr[j][e] = Bf[(8 * grp + 4 * lh + e) * BN + col];
+      } else {
+        bfr[j] = *reinterpret_cast<const f32x4*>(Bs + rk_off(col, 2 * grp + lh));
+      }
+    }
+  };
+  // every fragment of the k-tile is requested up front (TM+TN registers x4
+  // per group): the reads of groups 1-3 are in flight while group 0's MFMAs
+  // run, and the scheduler barrier keeps hipcc from sinking them back behind
+  // the MFMAs (it otherwise re-uses one register set per group and re-exposes
+  // the LDS latency before every group)
+  auto compute = [&](int stage, auto&& mid) {
     const uint8_t* As = smem + stage * STAGE;
     const uint8_t* Bs = As + A_BYTES;
+    f32x4 af[kBK / 8][TM], bfr[kBK / 8][TN];
+#pragma unroll
+    for (int grp = 0; grp < kBK / 8; ++grp) load(As, Bs, grp, af[grp], bfr[grp]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int grp = 0; grp < kBK / 8; ++grp) {
-      f32x4 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * (BM / 2) + 32 * i + li;
-        af[i] = *reinterpret_cast<const f32x4*>(As + rk_off(row, 2 * grp + lh));
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = wn * (BN / 2) + 32 * j + li;
-        if constexpr (DGRAD) {
-          const float* Bf = reinterpret_cast<const float*>(Bs);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bfr[j][e] = Bf[(8 * grp + 4 * lh + e) * BN + col];
-        } else {
-          bfr[j] = *reinterpret_cast<const f32x4*>(Bs + rk_off(col, 2 * grp + lh));
-        }
-      }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(af[i][e], bfr[j][e], acc[i][j]);
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(af[grp][i][e], bfr[grp][j][e], acc[i][j]);
+      if (grp == 0) mid();
     }
   };
   ring_loop<ACH + BCH>(nk, issue, compute);
@@ -436,7 +460,7 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
   const bool a_ok = a_co < g.Ng;
   const int jcol = j0 + (lane % B_CPR) * 4;
   const bool jok = jcol < g.K;
-  const int rs = sdiv(jcol, g.C, a.c_shift);
+  const int rs = fdiv(jcol, a.dc);
   const int jc = jcol - rs * g.C;
   const int jr = rs / KS, js = rs - (rs / KS) * KS;
   const int PQ = g.P * g.Q;
@@ -453,9 +477,9 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int m = kb + (wave + 4 * i) * B_RPI + lane / B_CPR;
-      const int n = sdiv(m, PQ, a.pq_shift);
+      const int n = fdiv(m, a.dpq);
       const int rem = m - n * PQ;
-      const int oy = sdiv(rem, g.Q, a.q_shift);
+      const int oy = fdiv(rem, a.dq);
       const int ox = rem - oy * g.Q;
       const int iy = oy * ST - g.pad + jr, ix = ox * ST - g.pad + js;
       const bool ok = (m < kend) & jok & (iy >= 0) & (iy < g.H) & (ix >= 0) & (ix < g.W);
@@ -472,26 +496,32 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
   const int li = lane & 31, lh = lane >> 5;
-  auto compute = [&](int stage) {
+  auto load = [&](const float* As, const float* Bs, int grp, f32x4* af, f32x4* bfr) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int kr = 8 * grp + 4 * lh + e;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i][e] = As[kr * BM + wm * (BM / 2) + 32 * i + li];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j][e] = Bs[kr * BN + wn * (BN / 2) + 32 * j + li];
+    }
+  };
+  auto compute = [&](int stage, auto&& mid) {
     const float* As = reinterpret_cast<const float*>(smem + stage * STAGE);
     const float* Bs = reinterpret_cast<const float*>(smem + stage * STAGE + A_BYTES);
+    f32x4 af[kBK / 8][TM], bfr[kBK / 8][TN];
+#pragma unroll
+    for (int grp = 0; grp < kBK / 8; ++grp) load(As, Bs, grp, af[grp], bfr[grp]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int grp = 0; grp < kBK / 8; ++grp) {
-      f32x4 af[TM], bfr[TN];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int kr = 8 * grp + 4 * lh + e;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) af[i][e] = As[kr * BM + wm * (BM / 2) + 32 * i + li];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j][e] = Bs[kr * BN + wn * (BN / 2) + 32 * j + li];
-      }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(af[i][e], bfr[j][e], acc[i][j]);
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(af[grp][i][e], bfr[grp][j][e], acc[i][j]);
+      if (grp == 0) mid();
     }
   };
   ring_loop<ACH + BCH>(nk, issue, compute);
@@ -517,12 +547,6 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
 
 // ---------------------------------------------------------------------------
 // host side
-int log2_exact(int v) {
-  if (v <= 0 || (v & (v - 1))) return -1;
-  int s = 0;
-  while ((1 << s) < v) ++s;
-  return s;
-}
 uint32_t range_bytes(int64_t elems) {
   const int64_t b = elems * 4;
   return b >= 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)b;
@@ -647,10 +671,23 @@ ConvPlan plan_conv32(const ConvGeom& g, int mode) {
   return p;
 }
 
+static FastDiv make_fdiv(int d) {
+  FastDiv f{0u, 0, 0u};
+  if (d <= 1) {
+    f.id = 0xFFFFFFFFu;
+    return f;
+  }
+  int s = 0;
+  while ((1LL << s) < d) ++s;
+  f.m = (uint32_t)(((1ULL << (31 + s)) + (uint64_t)d - 1) / (uint64_t)d);
+  f.sh = s - 1;
+  return f;
+}
+
 static void fill_shifts(Conv32Args& a) {
-  a.c_shift = log2_exact(a.g.C);
-  a.q_shift = log2_exact(a.g.Q);
-  a.pq_shift = log2_exact(a.g.P * a.g.Q);
+  a.dc = make_fdiv(a.g.C);
+  a.dq = make_fdiv(a.g.Q);
+  a.dpq = make_fdiv(a.g.P * a.g.Q);
 }
 
 void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const float* src, const float* wgt,

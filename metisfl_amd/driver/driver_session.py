@@ -15,8 +15,10 @@ MI355X-first differences:
     through the ``ssh`` CLI for remote hosts;
   * the model is shipped as a small JSON definition of a built-in family
     (or a cloudpickled TorchModelDef), not a tarred SavedModel;
-  * for the on-node data plane (RCCL all-reduce instead of gRPC model
-    transfer) see ``FederationDriver.run_collective`` in driver/collective.py.
+  * the on-node data plane (RCCL all-reduce instead of gRPC model
+    transfer) is ``DriverSession.run_collective`` below: one learner process
+    per GPU under one process group, rank 0 reporting rounds to the
+    controller.
 """
 from __future__ import annotations
 

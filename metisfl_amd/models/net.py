@@ -25,10 +25,16 @@ from metisfl_amd.ops.optim import OptimizerSpec
 class DeviceDataset:
     """A learner's shard resident in device memory (NHWC rows in the model's
     compute dtype, int32 labels) plus a per-epoch permutation buffer.  Rows
-    are padded so each is a multiple of 8 elements (16-B vector gathers)."""
+    are padded so each is a multiple of 8 elements (16-B vector gathers).
+
+    An epoch is ceil(n / batch) steps, as in Keras ``fit`` -- the count the
+    controller budgets with (epochs * ceil(n / batch), controller.cc:148-153).
+    The graph has a static batch shape, so the last batch of an epoch is
+    completed with the first samples of the same epoch's permutation instead
+    of running short (``drop_last=True``: floor(n / batch) full batches)."""
 
     def __init__(self, x: torch.Tensor, y: torch.Tensor, batch_size: int, seed: int = 0,
-                 shuffle: bool = True, drop_last: bool = True):
+                 shuffle: bool = True, drop_last: bool = False):
         assert x.shape[0] == y.shape[0]
         self.x = x.contiguous()
         self.y = y.to(torch.int32).contiguous()
@@ -207,7 +213,8 @@ class StaticNet:
 
     # -- data helpers ----------------------------------------------------------
     def make_dataset(self, x_nhwc: np.ndarray | torch.Tensor, y: np.ndarray | torch.Tensor,
-                     seed: int = 0, shuffle: bool = True, batch_size: int | None = None) -> DeviceDataset:
+                     seed: int = 0, shuffle: bool = True, batch_size: int | None = None,
+                     drop_last: bool | None = None) -> DeviceDataset:
         """Upload a shard: pads channels to the model's input width, casts to
         the compute dtype."""
         x = torch.as_tensor(x_nhwc)
@@ -221,7 +228,10 @@ class StaticNet:
         if y.is_floating_point():  # regression targets: fp32 bits in the int32 label slots
             y = y.to(torch.float32).contiguous().view(torch.int32)
         y = y.to(torch.int32).to(self.device)
-        return DeviceDataset(x, y, batch_size or self.B, seed=seed, shuffle=shuffle)
+        # training shards: ceil(n / B) steps per epoch (wrapped last batch);
+        # evaluation shards (unshuffled): full batches only, no sample twice
+        return DeviceDataset(x, y, batch_size or self.B, seed=seed, shuffle=shuffle,
+                             drop_last=(not shuffle) if drop_last is None else drop_last)
 
     @staticmethod
     def timer():

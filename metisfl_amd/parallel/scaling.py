@@ -1,6 +1,6 @@
 """Scaling-factor semantics of the reference's controller scalers.
 
-Canonical implementation lives in the C++ engine (csrc/engine/scaling.cc);
+Canonical implementation lives in the C++ engine (csrc/engine/policies.h);
 this host mirror exists for engine-less use and for cross-checking in tests.
 Reference: scaling/batches_scaler.cc:7-50, participants_scaler.cc:7-43,
 train_dataset_size_scaler.cc:7-50.  Quirk kept: a
