@@ -5,6 +5,8 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
+#include <cstring>
+
 #include "kernels/ckks.h"
 
 namespace {
@@ -69,15 +71,22 @@ void check_u64(const torch::Tensor& t, int64_t numel, const char* nm) {
 
 int64_t num_ct(int64_t n, int64_t S) { return std::max<int64_t>(1, (n + S - 1) / S); }
 
+mfl::CkksKey key_from(const std::string& k) {
+  TORCH_CHECK(k.size() == 32, "ckks: the encryption key must be 32 bytes");
+  mfl::CkksKey key;
+  std::memcpy(key.w, k.data(), 32);
+  return key;
+}
+
 void ckks_encrypt_dev(std::vector<torch::Tensor> tabs, int64_t N, int64_t L, torch::Tensor x,
-                      torch::Tensor ct, torch::Tensor u, double delta, int64_t seed) {
+                      torch::Tensor ct, torch::Tensor u, double delta, pybind11::bytes key32) {
   auto T = tables(tabs, N, L);
   TORCH_CHECK(T.pk_a && T.pk_b && T.pk_a_sh && T.pk_b_sh, "ckks encrypt: public key not loaded");
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == torch::kFloat32, "x fp32");
   const int64_t nct = num_ct(x.numel(), T.S);
   check_u64(ct, nct * 2 * L * N, "ct");
   check_u64(u, nct * L * N, "u scratch");
-  mfl::launch_ckks_encrypt(T, x.data_ptr<float>(), x.numel(), nct, delta, (uint64_t)seed,
+  mfl::launch_ckks_encrypt(T, x.data_ptr<float>(), x.numel(), nct, delta, key_from(key32),
                            reinterpret_cast<uint64_t*>(ct.data_ptr()),
                            reinterpret_cast<uint64_t*>(u.data_ptr()), cur_stream(x));
 }
@@ -125,7 +134,28 @@ void ckks_reduce_dev(std::vector<torch::Tensor> tabs, int64_t N, int64_t L, torc
 
 }  // namespace
 
+// RFC 8439 known-answer / stream checks on the device
+torch::Tensor chacha20_blocks_dev(pybind11::bytes key32, int64_t counter0, pybind11::bytes nonce12, int64_t nblocks,
+                                  torch::Tensor like) {
+  const std::string n = nonce12;
+  TORCH_CHECK(n.size() == 12 && nblocks > 0 && nblocks < (1 << 24), "nonce 12 bytes, 0 < nblocks < 2^24");
+  uint32_t nw[3];
+  std::memcpy(nw, n.data(), 12);
+  auto out = torch::empty({nblocks * 16}, like.options().dtype(torch::kInt32));
+  mfl::launch_chacha_blocks(key_from(key32), (uint32_t)counter0, nw, (int)nblocks,
+                            reinterpret_cast<uint32_t*>(out.data_ptr()), cur_stream(like));
+  return out;
+}
+torch::Tensor ckks_noise_dump_dev(pybind11::bytes key32, int64_t c, int64_t n, torch::Tensor like) {
+  TORCH_CHECK(n > 0 && n < (1 << 26), "0 < n < 2^26");
+  auto out = torch::empty({3 * n}, like.options().dtype(torch::kInt64));
+  mfl::launch_ckks_noise_dump(key_from(key32), c, (int)n, out.data_ptr<int64_t>(), cur_stream(like));
+  return out;
+}
+
 void register_ckks(pybind11::module& m) {
+  m.def("chacha20_blocks", &chacha20_blocks_dev);
+  m.def("ckks_noise_dump", &ckks_noise_dump_dev);
   m.def("ckks_encrypt", &ckks_encrypt_dev);
   m.def("ckks_decrypt", &ckks_decrypt_dev);
   m.def("ckks_ntt", &ckks_ntt_dev);

@@ -11,6 +11,8 @@
 #include "engine/controller.h"
 #include "engine/policies.h"
 #include "he/ckks.h"
+#include "common/chacha20.h"
+#include <cstring>
 
 namespace py = pybind11;
 using namespace mfl;
@@ -228,6 +230,16 @@ PYBIND11_MODULE(_engine, m) {
     return B(serialize_model(parse_model(std::string(model))));
   });
 
+  // RFC 8439 block function (known-answer tests; same code as the device side)
+  m.def("chacha20_block", [](py::bytes key, uint32_t counter, py::bytes nonce) {
+    const std::string k = key, n = nonce;
+    if (k.size() != 32 || n.size() != 12) throw std::invalid_argument("key 32 bytes, nonce 12 bytes");
+    uint32_t kw[8], nw[3], out[16];
+    std::memcpy(kw, k.data(), 32);
+    std::memcpy(nw, n.data(), 12);
+    chacha20_block(kw, counter, nw, out);
+    return py::bytes(reinterpret_cast<const char*>(out), 64);
+  });
   py::class_<CKKS>(m, "CKKS")
       .def(py::init<uint32_t, uint32_t>(), py::arg("batch_size"), py::arg("scaling_factor_bits"))
       .def("gen_crypto_context_and_keys", &CKKS::gen_crypto_context_and_keys,
@@ -279,6 +291,8 @@ PYBIND11_MODULE(_engine, m) {
              return py::array_t<double>(v.size(), v.data());
            })
       .def("encode_decode_roundtrip", &CKKS::encode_decode_roundtrip)
+      .def("debug_sample", &CKKS::debug_sample, py::arg("kind"), py::arg("n"),
+           "sampler output for statistical tests: 0 ternary secret, 1 Gaussian error, 2 uniform mod q_0")
       .def_property_readonly("ring_dim", &CKKS::ring_dim)
       .def_property_readonly("slots", &CKKS::slots)
       .def_property_readonly("moduli", &CKKS::moduli)

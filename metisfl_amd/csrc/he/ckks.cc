@@ -1,5 +1,12 @@
 #include "he/ckks.h"
 
+#include <sys/random.h>
+
+#include <cerrno>
+#include <cmath>
+
+#include "common/chacha20.h"
+
 #include <omp.h>
 #include <sys/stat.h>
 
@@ -174,8 +181,89 @@ struct Crt {
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// ChaCha20Rng
+void ChaCha20Rng::os_random(void* buf, size_t n) {
+  uint8_t* p = static_cast<uint8_t*>(buf);
+  while (n) {
+    const ssize_t r = getrandom(p, n, 0);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      throw std::runtime_error("getrandom failed");
+    }
+    p += r;
+    n -= (size_t)r;
+  }
+}
+
+ChaCha20Rng::ChaCha20Rng() {
+  os_random(key_, sizeof(key_));
+  nonce_[0] = nonce_[1] = 0;
+  nonce_[2] = kChaKeygen;
+}
+
+ChaCha20Rng::ChaCha20Rng(const uint32_t key[8], uint64_t stream, uint32_t domain) {
+  for (int i = 0; i < 8; ++i) key_[i] = key[i];
+  nonce_[0] = (uint32_t)stream;
+  nonce_[1] = (uint32_t)(stream >> 32);
+  nonce_[2] = domain;
+}
+
+void ChaCha20Rng::refill() {
+  chacha20_block(key_, ctr_, nonce_, buf_);
+  if (++ctr_ == 0) {  // 2^32 blocks (256 GiB) on one nonce: move to the next
+    if (++nonce_[0] == 0) ++nonce_[1];
+  }
+  pos_ = 0;
+}
+
+uint64_t ChaCha20Rng::next_u64() {
+  if (pos_ > 14) refill();
+  const uint64_t v = chacha_u64(buf_ + pos_);
+  pos_ += 2;
+  return v;
+}
+
+uint64_t ChaCha20Rng::below(uint64_t q) {
+  const uint64_t lim = (~0ULL / q) * q;  // largest multiple of q <= 2^64 - 1
+  for (;;) {
+    const uint64_t v = next_u64();
+    if (v < lim) return v % q;
+  }
+}
+
+int ChaCha20Rng::ternary() {
+  for (;;) {  // exact: reject 3 of a 2-bit draw
+    const uint64_t v = next_u64();
+    for (int i = 0; i < 32; ++i) {
+      const int t = (int)((v >> (2 * i)) & 3u);
+      if (t != 3) return t - 1;
+    }
+  }
+}
+
+double ChaCha20Rng::gauss(double sigma) {
+  if (has_spare_) {
+    has_spare_ = false;
+    return spare_ * sigma;
+  }
+  const double u1 = chacha_unit_open0(next_u64()), u2 = chacha_unit(next_u64());
+  const double r = std::sqrt(-2.0 * std::log(u1));
+  spare_ = r * std::sin(2.0 * M_PI * u2);
+  has_spare_ = true;
+  return r * std::cos(2.0 * M_PI * u2) * sigma;
+}
+
+void ChaCha20Rng::derive_key(uint32_t out[8]) {
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t v = next_u64();
+    out[2 * i] = (uint32_t)v;
+    out[2 * i + 1] = (uint32_t)(v >> 32);
+  }
+}
+
 CKKS::CKKS(uint32_t batch_size, uint32_t scaling_bits)
-    : batch_(batch_size), bits_(scaling_bits), rng_(std::random_device{}()) {
+    : batch_(batch_size), bits_(scaling_bits) {
   if (batch_size == 0 || (batch_size & (batch_size - 1)))
     throw std::runtime_error("CKKS batch_size must be a power of two");
   if (scaling_bits < 20 || scaling_bits > 58) throw std::runtime_error("CKKS scaling bits in [20,58]");
@@ -381,18 +469,24 @@ uint64_t CKKS::reduce_signed(long double x, int l) const {
 }
 
 void CKKS::sample_ternary(std::vector<int64_t>& v) {
-  std::uniform_int_distribution<int> d(-1, 1);
-  for (auto& x : v) x = d(rng_);
+  for (auto& x : v) x = rng_.ternary();
+}
+
+static int64_t clip_round(double g) {
+  g = g > 19.2 ? 19.2 : (g < -19.2 ? -19.2 : g);  // 6 sigma
+  return (int64_t)llround(g);
 }
 
 void CKKS::sample_gauss(std::vector<int64_t>& v) {
-  std::normal_distribution<double> d(0.0, 3.2);
-  for (auto& x : v) {
-    double g = d(rng_);
-    if (g > 19.2) g = 19.2;
-    if (g < -19.2) g = -19.2;
-    x = llround(g);
-  }
+  for (auto& x : v) x = clip_round(rng_.gauss(3.2));
+}
+
+std::vector<int64_t> CKKS::debug_sample(int kind, size_t n) {
+  std::vector<int64_t> v(n);
+  if (kind == 0) sample_ternary(v);
+  else if (kind == 1) sample_gauss(v);
+  else for (auto& x : v) x = (int64_t)rng_.below(q_.empty() ? 1000003ULL : q_[0]) ;
+  return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -411,11 +505,10 @@ void CKKS::gen_crypto_context_and_keys(const std::string& dir) {
     uint64_t* al = &pk_a_[(size_t)l * N_];
     uint64_t* bl = &pk_b_[(size_t)l * N_];
     std::vector<uint64_t> el(N_);
-    std::uniform_int_distribution<uint64_t> du(0, q - 1);
     for (uint32_t i = 0; i < N_; ++i) {
       sl[i] = s[i] < 0 ? q - 1 : (uint64_t)s[i];
       el[i] = e[i] < 0 ? q - (uint64_t)(-e[i]) : (uint64_t)e[i];
-      al[i] = du(rng_);
+      al[i] = rng_.below(q);
     }
     ntt(sl, l);
     ntt(el.data(), l);
@@ -513,25 +606,19 @@ std::string CKKS::encrypt(const std::vector<double>& values) {
   const size_t per_ct = (size_t)2 * L * N_;
   out.resize(hdr + nct * per_ct * 8);
   uint64_t* body = reinterpret_cast<uint64_t*>(&out[hdr]);
-  std::vector<uint64_t> seeds(nct);
-  for (auto& s : seeds) s = rng_();
+  uint32_t ekey[8];  // fresh per encryption; one ChaCha20 stream per ciphertext
+  rng_.derive_key(ekey);
   const long double delta = ldexpl(1.0L, (int)bits_);
 #pragma omp parallel for schedule(dynamic, 1)
   for (size_t c = 0; c < nct; ++c) {
-    std::mt19937_64 rng(seeds[c]);
-    std::uniform_int_distribution<int> dt(-1, 1);
-    std::normal_distribution<double> dg(0.0, 3.2);
-    auto gauss = [&]() {
-      double g = dg(rng);
-      g = g > 19.2 ? 19.2 : (g < -19.2 ? -19.2 : g);
-      return (int64_t)llround(g);
-    };
+    ChaCha20Rng rng(ekey, (uint64_t)c, kChaEncrypt);
+    auto gauss = [&]() { return clip_round(rng.gauss(3.2)); };
     const size_t off = c * slots_;
     const size_t n = std::min<size_t>(slots_, values.size() > off ? values.size() - off : 0);
     std::vector<double> coeffs;
     encode(values.data() + off, n, coeffs);
     std::vector<int64_t> u(N_), e0(N_), e1(N_);
-    for (auto& x : u) x = dt(rng);
+    for (auto& x : u) x = rng.ternary();
     for (auto& x : e0) x = gauss();
     for (auto& x : e1) x = gauss();
     uint64_t* c0 = body + c * per_ct;

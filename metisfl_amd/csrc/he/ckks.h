@@ -19,7 +19,9 @@
 //   | nct x { c0[nlimbs][N], c1[nlimbs][N] }  (u64, little endian)
 // Security note: secrets are ternary, errors discrete Gaussian (sigma 3.2),
 // log2(Q) ~ 60 + 2*scaling_bits <= 218 at N = 8192 (128-bit HE-standard bound);
-// randomness comes from std::random_device-seeded mt19937_64 (not a CSPRNG).
+// randomness is ChaCha20 (RFC 8439, common/chacha20.h) keyed from getrandom():
+// a context generator for key generation, and a fresh 256-bit key per
+// encryption with one counter-mode stream per ciphertext.
 #pragma once
 #include <cstdint>
 #include <random>
@@ -28,6 +30,31 @@
 #include <vector>
 
 namespace mfl {
+
+// Host CSPRNG: ChaCha20 in counter mode.  Default-constructed: a 256-bit key
+// from the kernel entropy pool (getrandom); or an explicit (key, stream,
+// domain) for the per-ciphertext encryption streams.
+class ChaCha20Rng {
+ public:
+  ChaCha20Rng();
+  ChaCha20Rng(const uint32_t key[8], uint64_t stream, uint32_t domain);
+  uint64_t next_u64();
+  uint64_t below(uint64_t q);     // uniform in [0, q), rejection sampled
+  int ternary();                  // uniform in {-1, 0, 1}
+  double gauss(double sigma);     // Box-Muller
+  void derive_key(uint32_t out[8]);  // 256 fresh bits for a sub-stream key
+  static void os_random(void* buf, size_t n);
+
+ private:
+  void refill();
+  uint32_t key_[8];
+  uint32_t nonce_[3];
+  uint32_t ctr_ = 0;
+  uint32_t buf_[16];
+  int pos_ = 16;
+  bool has_spare_ = false;
+  double spare_ = 0.0;
+};
 
 class CKKS {
  public:
@@ -85,6 +112,12 @@ class CKKS {
   void decode(const std::vector<long double>& coeffs, double scale, double* out, size_t n) const;
   void sample_ternary(std::vector<int64_t>& v);
   void sample_gauss(std::vector<int64_t>& v);
+
+ public:
+  // statistical tests of the samplers (tests/test_ckks_rng.py)
+  std::vector<int64_t> debug_sample(int kind, size_t n);
+
+ private:
   uint64_t reduce_signed(long double x, int limb) const;
 
   uint32_t batch_, bits_, N_, slots_;
@@ -94,7 +127,7 @@ class CKKS {
   std::vector<uint64_t> pk_b_, pk_a_, sk_;  // [limb][N] NTT form
   bool has_pk_ = false, has_sk_ = false;
   Files files_;
-  std::mt19937_64 rng_;
+  ChaCha20Rng rng_;
   // canonical-embedding FFT tables
   std::vector<uint64_t> rot_;
   std::vector<double> ksi_re_, ksi_im_;

@@ -31,9 +31,19 @@ struct CkksTables {
   const double* ksi_im;        // [2N + 1] sin(2 pi k / 2N)
 };
 
+// 256-bit ChaCha20 key of one encryption (secret; fresh per call)
+struct CkksKey {
+  uint32_t w[8];
+};
+
 // x: fp32 [n] -> ct: u64 [nct][2][L][N] (nct = ceil(n / S)); u_scratch: u64 [nct][L][N]
 void launch_ckks_encrypt(const CkksTables& T, const float* x, int64_t n, int64_t nct, double delta,
-                         uint64_t seed, uint64_t* ct, uint64_t* u_scratch, hipStream_t s);
+                         const CkksKey& key, uint64_t* ct, uint64_t* u_scratch, hipStream_t s);
+// tests: RFC 8439 blocks counter0.. on the device; the (u, e0, e1) noise of
+// ciphertext c's first n coefficients -> out [3][n]
+void launch_chacha_blocks(const CkksKey& key, uint32_t counter0, const uint32_t nonce[3], int nblocks, uint32_t* out,
+                          hipStream_t s);
+void launch_ckks_noise_dump(const CkksKey& key, int64_t c, int n, int64_t* out, hipStream_t s);
 // ct [nct][2][L][N] -> out fp32 [n] (or fp64 into out64 when non-null); m_scratch: u64 [nct][L][N]
 void launch_ckks_decrypt(const CkksTables& T, const uint64_t* ct, int64_t nct, double inv_scale,
                          uint64_t* m_scratch, float* out, double* out64, int64_t n, hipStream_t s);

@@ -26,10 +26,16 @@
 //            ckks_reduce (x mod q after an int64 sum all-reduce of <= 16
 //            pre-scaled ciphertexts: every residue is < 2^60, so the sum of
 //            16 stays below 2^64).
-// Randomness: splitmix64 of (seed, ciphertext, coefficient) -- statistically
-// fine, NOT a CSPRNG (the host path's mt19937_64 is not one either; ckks.h).
+// Randomness: ChaCha20 (RFC 8439, common/chacha20.h) in counter mode under a
+// secret 256-bit key drawn from the OS entropy pool for every encryption:
+// ciphertext c is stream (nonce c, domain "encr"), coefficient k reads block
+// k, so every (c, k) samples independently.  One 64-byte block gives u
+// (ternary, 64-bit uniform mod 3: bias < 2^-62) and e0 / e1 (Box-Muller of
+// two 53-bit uniforms, sigma 3.2 clipped at 6 sigma).
 #include "kernels/ckks.h"
 #include "kernels/common.h"
+// after the HIP headers: chacha20.h marks its functions __host__ __device__
+#include "common/chacha20.h"
 
 namespace mfl {
 namespace {
@@ -51,11 +57,20 @@ __device__ __forceinline__ uint64_t smod(int64_t x, uint64_t q) {
   int64_t r = x % (int64_t)q;
   return (uint64_t)(r < 0 ? r + (int64_t)q : r);
 }
-__device__ __forceinline__ uint64_t splitmix(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
+// K11: the noise of coefficient k of ciphertext c
+__device__ __forceinline__ void sample_noise(const CkksKey& key, int64_t c, int k, int64_t& u, int64_t& e0,
+                                             int64_t& e1) {
+  const uint32_t nonce[3] = {(uint32_t)c, (uint32_t)((uint64_t)c >> 32), kChaEncrypt};
+  uint32_t w[16];
+  chacha20_block(key.w, (uint32_t)k, nonce, w);
+  u = chacha_ternary(chacha_u64(w));
+  const double u1 = chacha_unit_open0(chacha_u64(w + 2)), u2 = chacha_unit(chacha_u64(w + 4));
+  const double r = 3.2 * sqrt(-2.0 * log(u1));
+  double g0 = r * cospi(2.0 * u2), g1 = r * sinpi(2.0 * u2);
+  g0 = fmin(19.2, fmax(-19.2, g0));
+  g1 = fmin(19.2, fmax(-19.2, g1));
+  e0 = llrint(g0);
+  e1 = llrint(g1);
 }
 __device__ __forceinline__ int log2u(uint32_t x) { return 31 - __clz(x); }
 __device__ __forceinline__ uint32_t bitrev(uint32_t x, int bits) { return __brev(x) >> (32 - bits); }
@@ -69,7 +84,7 @@ __device__ __forceinline__ cplx cmul(cplx a, cplx b) {
 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(512) void ckks_encode_sample_kernel(CkksTables T, const float* __restrict__ x,
-                                                                 int64_t n, double delta, uint64_t seed,
+                                                                 int64_t n, double delta, CkksKey key,
                                                                  uint64_t* __restrict__ ct,
                                                                  uint64_t* __restrict__ u_out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -105,17 +120,8 @@ __global__ __launch_bounds__(512) void ckks_encode_sample_kernel(CkksTables T, c
     const cplx z = v[bitrev((uint32_t)(k < S ? k : k - S), sbits)];
     const double coeff = (k < S ? z.re : z.im) * inv_s;
     const int64_t m = (int64_t)round(coeff * delta);
-    // K11: u ternary, e0 / e1 Box-Muller Gaussians (sigma 3.2, clipped at 6 sigma)
-    const uint64_t ctr = seed ^ ((uint64_t)c * (uint64_t)N + (uint64_t)k) * 0xD1B54A32D192ED03ull;
-    const uint64_t h1 = splitmix(ctr), h2 = splitmix(ctr ^ 0xA0761D6478BD642Full);
-    const int64_t u = (int64_t)((h2 >> 32) % 3u) - 1;
-    const double u1 = ((double)(h1 >> 40) + 1.0) * (1.0 / 16777217.0);  // (0, 1]
-    const double u2 = (double)(h1 & 0xFFFFFFull) * (1.0 / 16777216.0);
-    const double r = 3.2 * sqrt(-2.0 * log(u1));
-    double g0 = r * cospi(2.0 * u2), g1 = r * sinpi(2.0 * u2);
-    g0 = fmin(19.2, fmax(-19.2, g0));
-    g1 = fmin(19.2, fmax(-19.2, g1));
-    const int64_t e0 = llrint(g0), e1 = llrint(g1);
+    int64_t u, e0, e1;
+    sample_noise(key, c, k, u, e0, e1);
     for (int l = 0; l < L; ++l) {
       const uint64_t q = T.q[l];
       c0[(int64_t)l * N + k] = addmod(smod(m, q), smod(e0, q), q);
@@ -296,9 +302,9 @@ __global__ __launch_bounds__(256) void ckks_reduce_kernel(CkksTables T, uint64_t
 }  // namespace
 
 void launch_ckks_encrypt(const CkksTables& T, const float* x, int64_t n, int64_t nct, double delta,
-                         uint64_t seed, uint64_t* ct, uint64_t* u_scratch, hipStream_t s) {
+                         const CkksKey& key, uint64_t* ct, uint64_t* u_scratch, hipStream_t s) {
   const size_t lds = (size_t)T.N * 8;  // S complex doubles == N u64
-  ckks_encode_sample_kernel<<<(unsigned)nct, 512, lds, s>>>(T, x, n, delta, seed, ct, u_scratch);
+  ckks_encode_sample_kernel<<<(unsigned)nct, 512, lds, s>>>(T, x, n, delta, key, ct, u_scratch);
   ckks_ntt_fwd_kernel<<<(unsigned)(nct * 2 * T.L), 512, lds, s>>>(T, ct);
   ckks_ntt_fwd_kernel<<<(unsigned)(nct * T.L), 512, lds, s>>>(T, u_scratch);
   ckks_pk_combine_kernel<<<stream_grid(nct * T.L * T.N, 256, 8192), 256, 0, s>>>(T, ct, u_scratch, nct);
@@ -324,6 +330,36 @@ void launch_ckks_scale(const CkksTables& T, uint64_t* x, const uint64_t* wq, int
 
 void launch_ckks_reduce(const CkksTables& T, uint64_t* x, int64_t total, hipStream_t s) {
   ckks_reduce_kernel<<<stream_grid(total, 256, 8192), 256, 0, s>>>(T, x, total);
+}
+
+namespace {
+__global__ void chacha_blocks_kernel(CkksKey key, uint32_t counter0, uint32_t n0, uint32_t n1, uint32_t n2,
+                                     int nblocks, uint32_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nblocks) return;
+  const uint32_t nonce[3] = {n0, n1, n2};
+  uint32_t w[16];
+  chacha20_block(key.w, counter0 + (uint32_t)i, nonce, w);
+  for (int j = 0; j < 16; ++j) out[(int64_t)i * 16 + j] = w[j];
+}
+__global__ void noise_dump_kernel(CkksKey key, int64_t c, int n, int64_t* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  int64_t u, e0, e1;
+  sample_noise(key, c, k, u, e0, e1);
+  out[k] = u;
+  out[n + k] = e0;
+  out[2 * (int64_t)n + k] = e1;
+}
+}  // namespace
+
+void launch_chacha_blocks(const CkksKey& key, uint32_t counter0, const uint32_t nonce[3], int nblocks, uint32_t* out,
+                          hipStream_t s) {
+  chacha_blocks_kernel<<<(nblocks + 255) / 256, 256, 0, s>>>(key, counter0, nonce[0], nonce[1], nonce[2], nblocks,
+                                                             out);
+}
+void launch_ckks_noise_dump(const CkksKey& key, int64_t c, int n, int64_t* out, hipStream_t s) {
+  noise_dump_kernel<<<(n + 255) / 256, 256, 0, s>>>(key, c, n, out);
 }
 
 }  // namespace mfl

@@ -109,8 +109,10 @@ class DeviceCKKS:
             self._scratch = torch.empty(need, dtype=torch.int64, device=self.device)
         return self._scratch[:need]
 
-    def encrypt(self, x: torch.Tensor, out: torch.Tensor | None = None, seed: int | None = None) -> torch.Tensor:
-        """fp32 [n] (device) -> ciphertext limbs int64 [nct*2*L*N] at scale 2^bits."""
+    def encrypt(self, x: torch.Tensor, out: torch.Tensor | None = None, key: bytes | None = None) -> torch.Tensor:
+        """fp32 [n] (device) -> ciphertext limbs int64 [nct*2*L*N] at scale 2^bits.
+        The noise is ChaCha20 under a fresh secret 256-bit key from the OS
+        CSPRNG (``key`` only for reproducibility tests)."""
         x = x.reshape(-1)
         if x.dtype != torch.float32:
             x = x.float()
@@ -118,9 +120,9 @@ class DeviceCKKS:
         n = x.numel()
         if out is None:
             out = torch.empty(self.ct_numel(n), dtype=torch.int64, device=self.device)
-        s = secrets.randbits(63) if seed is None else int(seed) & ((1 << 63) - 1)
+        k = secrets.token_bytes(32) if key is None else bytes(key)
         _ops().ckks_encrypt(self.tables, self.N, self.L, x, out, self._scratch_for(n),
-                            float(2.0 ** self.bits), s)
+                            float(2.0 ** self.bits), k)
         return out
 
     def decrypt(self, ct: torch.Tensor, n: int, log2_scale: float | None = None,
