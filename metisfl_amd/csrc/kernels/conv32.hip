@@ -57,32 +57,49 @@ __device__ __forceinline__ int fdiv(int x, const FastDiv& f) {
   return (int)((__umulhi((uint32_t)x, f.m) >> f.sh) + ((uint32_t)x & f.id));
 }
 
+// DMA offset, or past every buffer range when !ok -- bitwise, so hipcc keeps
+// the address math branch-free (a ?: here became an exec-masked branch that
+// split the k-loop body)
+__device__ __forceinline__ uint32_t oob_or(bool ok, uint32_t off) { return off | (kOOB & (0u - (uint32_t)!ok)); }
+
 // fp32 [row][32] tile, 128-B rows: 16-B chunk ch of `row`
 __device__ __forceinline__ int rk_off(int row, int ch) { return row * 128 + ((ch ^ swz_b128<128>(row)) << 4); }
 
-// k-loop over the LDS ring.  compute(stage, mid) runs the MFMAs of the tile
-// in `stage` and calls mid() once its first k-group is issued: the DMA of
-// tile kt+2 (address math included) is placed there, so its VALU/SALU work
-// issues while the matrix pipe is busy instead of in front of it.  Stage
-// (kt+2)%3 is free: every wave passed this iteration's barrier, i.e. finished
-// reading it in iteration kt-1.
+// k-loop over the LDS ring, branch-free: the DMA of tile kt+2 is issued in
+// every iteration (past the end its offsets are all out of range: the
+// hardware fills the free stage with zeros and reads no memory), so the loop
+// body is ONE basic block and compute() can interleave the issue's address
+// math with its MFMAs (sched_group_barrier).  In-order issue otherwise runs
+// the ~60-90 VALU instructions of the issue between two dependent MFMAs with
+// the matrix pipe idle (measured: 45-50% of fp32 MFMA peak).  Stage
+// (kt+2)%3 is free: every wave passed this iteration's barrier, i.e.
+// finished reading it in iteration kt-1.
 template <int L, typename Issue, typename Compute>
 __device__ __forceinline__ void ring_loop(int nk, Issue& issue, Compute& compute) {
 #pragma unroll
-  for (int u = 0; u < kTiles; ++u)
-    if (u < nk) issue(u, u);
+  for (int u = 0; u < kTiles; ++u) issue(u, u);
   int stage = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    // own DMA of tile kt landed; the next one may still be in flight
-    if (kt + 1 < nk) wait_vmcnt<L>();
-    else wait_vmcnt<0>();
-    lds_barrier();  // every wave's tile kt landed, every wave left stage (kt-1)%3
+    wait_vmcnt<L>();  // own DMA of tile kt landed; tile kt+1's may still fly
+    lds_barrier();    // every wave's tile kt landed, every wave left stage (kt-1)%3
     const int nxt = kt + kTiles;
     const int nst = stage == 0 ? kStages - 1 : stage - 1;
-    compute(stage, [&] {
-      if (nxt < nk) issue(nxt, nst);
-    });
+    compute(stage, [&] { issue(nxt, nst); });
     stage = stage == kStages - 1 ? 0 : stage + 1;
+  }
+  wait_vmcnt<0>();  // the trailing (zero-fill) DMAs land before smem is reused
+}
+
+// Interleave pattern for one k-tile: per MFMA, up to V VALU, 2 SALU and one
+// VMEM instruction of the DMA issue slot in behind it.
+template <int NMFMA, int V>
+__device__ __forceinline__ void interleave_mfma() {
+#pragma unroll
+  for (int i = 0; i < NMFMA; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x002, V, 0);  // VALU
+    __builtin_amdgcn_sched_group_barrier(0x004, 2, 0);  // SALU
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
   }
 }
 
@@ -275,7 +292,7 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
           ok = kv & (iy >= 0) & (ix >= 0);
         }
         ok = ok & (iy < g.H) & (ix < g.W);
-        const uint32_t off = ok ? (uint32_t)(a_nb[i] + (iy * g.W + ix) * g.C + c) * 4u : kOOB;
+        const uint32_t off = oob_or(ok, (uint32_t)(a_nb[i] + (iy * g.W + ix) * g.C + c) * 4u);
         dma16(rsA, off, st + (wave + 4 * i) * 1024);
       }
     }
@@ -292,11 +309,11 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
           const int jr = ns == 2 ? rs >> 1 : rs;
           rs = (r0 + 2 * jr) * KS + s0 + 2 * (rs - jr * ns);
         }
-        off = ((kr < kend) & (n < g.Ng)) ? (uint32_t)((ko * KS * KS + rs) * g.Ng + n) * 4u : kOOB;
+        off = oob_or((kr < kend) & (n < g.Ng), (uint32_t)((ko * KS * KS + rs) * g.Ng + n) * 4u);
       } else {
         const int n = n0 + lrow + 32 * i;
         const int k = kb + a_kc;
-        off = ((k < kend) & (n < g.Ng)) ? (uint32_t)(n * g.K + k) * 4u : kOOB;
+        off = oob_or((k < kend) & (n < g.Ng), (uint32_t)(n * g.K + k) * 4u);
       }
       dma16(rsB, off, st + A_BYTES + (wave + 4 * i) * 1024);
     }
@@ -336,23 +353,24 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
   // run, and the scheduler barrier keeps hipcc from sinking them back behind
   // the MFMAs (it otherwise re-uses one register set per group and re-exposes
   // the LDS latency before every group)
-  auto compute = [&](int stage, auto&& mid) {
+  auto compute = [&](int stage, auto&& issue_next) {
     const uint8_t* As = smem + stage * STAGE;
     const uint8_t* Bs = As + A_BYTES;
     f32x4 af[kBK / 8][TM], bfr[kBK / 8][TN];
 #pragma unroll
     for (int grp = 0; grp < kBK / 8; ++grp) load(As, Bs, grp, af[grp], bfr[grp]);
-    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);  // all fragment reads first
+    issue_next();
 #pragma unroll
-    for (int grp = 0; grp < kBK / 8; ++grp) {
+    for (int grp = 0; grp < kBK / 8; ++grp)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(af[grp][i][e], bfr[grp][j][e], acc[i][j]);
-      if (grp == 0) mid();
-    }
+    interleave_mfma<4 * kBK / 8 * TM * TN, 8>();
+    __builtin_amdgcn_sched_barrier(0);
   };
   ring_loop<ACH + BCH>(nk, issue, compute);
   __syncthreads();  // every wave done with the ring before smem is reused
@@ -471,7 +489,7 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const int m = kb + (wave + 4 * i) * A_RPI + lane / A_CPR;
-      const uint32_t off = ((m < kend) & a_ok) ? (uint32_t)(m * g.Ng + a_co) * 4u : kOOB;
+      const uint32_t off = oob_or((m < kend) & a_ok, (uint32_t)(m * g.Ng + a_co) * 4u);
       dma16(rsA, off, st + (wave + 4 * i) * 1024);
     }
 #pragma unroll
@@ -483,7 +501,7 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
       const int ox = rem - oy * g.Q;
       const int iy = oy * ST - g.pad + jr, ix = ox * ST - g.pad + js;
       const bool ok = (m < kend) & jok & (iy >= 0) & (iy < g.H) & (ix >= 0) & (ix < g.W);
-      const uint32_t off = ok ? (uint32_t)(((n * g.H + iy) * g.W + ix) * g.C + jc) * 4u : kOOB;
+      const uint32_t off = oob_or(ok, (uint32_t)(((n * g.H + iy) * g.W + ix) * g.C + jc) * 4u);
       dma16(rsB, off, st + A_BYTES + (wave + 4 * i) * 1024);
     }
   };
@@ -506,23 +524,24 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
       for (int j = 0; j < TN; ++j) bfr[j][e] = Bs[kr * BN + wn * (BN / 2) + 32 * j + li];
     }
   };
-  auto compute = [&](int stage, auto&& mid) {
+  auto compute = [&](int stage, auto&& issue_next) {
     const float* As = reinterpret_cast<const float*>(smem + stage * STAGE);
     const float* Bs = reinterpret_cast<const float*>(smem + stage * STAGE + A_BYTES);
     f32x4 af[kBK / 8][TM], bfr[kBK / 8][TN];
 #pragma unroll
     for (int grp = 0; grp < kBK / 8; ++grp) load(As, Bs, grp, af[grp], bfr[grp]);
     __builtin_amdgcn_sched_barrier(0);
+    issue_next();
 #pragma unroll
-    for (int grp = 0; grp < kBK / 8; ++grp) {
+    for (int grp = 0; grp < kBK / 8; ++grp)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(af[grp][i][e], bfr[grp][j][e], acc[i][j]);
-      if (grp == 0) mid();
-    }
+    interleave_mfma<4 * kBK / 8 * TM * TN, 8>();
+    __builtin_amdgcn_sched_barrier(0);
   };
   ring_loop<ACH + BCH>(nk, issue, compute);
 

@@ -45,7 +45,7 @@ from metisfl_amd.utils import tracing
 
 META_FIELDS = ("num_training_examples", "completed_batches", "ms_per_batch", "ms_per_epoch",
                "train_loss", "train_accuracy", "completed_epochs", "global_iteration",
-               "test_loss", "test_accuracy")
+               "test_loss", "test_accuracy", "participated")
 
 
 @dataclass
@@ -74,6 +74,18 @@ class FederationConfig:
     secure_aggregation: bool = False
     he_batch_size: int = 4096
     he_scaling_bits: int = 52
+    # Straggler handling (the reference carries
+    # GlobalModelSpecs.learners_participation_ratio, metis.proto:307, but
+    # never acts on it).  A synchronous round closes once
+    # ceil(participation_ratio * N) learners finished their budget, or at
+    # round_deadline_s: learners still training then stop, contribute weight
+    # 0 (their partial work is discarded) and receive the community model.
+    # Progress is polled every poll_steps local updates (host-side, over the
+    # process group's key-value store -- no collective, no GPU sync beyond
+    # the chunk boundary).
+    participation_ratio: float = 1.0
+    round_deadline_s: float | None = None
+    poll_steps: int = 64
     extra: dict = field(default_factory=dict)
 
 
@@ -153,32 +165,80 @@ class CollectiveFederation:
         if self.comm.device.type == "cuda":
             torch.cuda.synchronize(self.comm.device)
 
+    @property
+    def elastic(self) -> bool:
+        """Straggler drop active (participation ratio < 1 or a round deadline)."""
+        return self.world > 1 and (self.cfg.participation_ratio < 1.0 or self.cfg.round_deadline_s is not None)
+
+    def quorum(self) -> int:
+        return max(1, min(self.world, math.ceil(self.cfg.participation_ratio * self.world - 1e-9)))
+
+    def _store(self):
+        import torch.distributed as dist
+        return dist.distributed_c10d._get_default_store()
+
+    def _train_elastic(self, nsteps: int, t0: float) -> tuple[int, bool]:
+        """Chunked local training that stops early once the round's quorum
+        has finished or the deadline passed -> (steps run, participated)."""
+        store, key = self._store(), f"metisfl/round{self.global_iteration}/done"
+        q = self.quorum()
+        deadline = self.cfg.round_deadline_s
+        slow = float(self.cfg.extra.get("debug_slow_s", {}).get(str(self.rank), 0.0))
+        done = 0
+        while done < nsteps:
+            k = min(self.cfg.poll_steps, nsteps - done)
+            self.net.train_steps(self.train_ds, k, step_offset=self.steps_done + done)
+            self._sync()
+            if slow:
+                time.sleep(slow)  # test hook: a deliberately slow learner
+            done += k
+            if done >= nsteps:
+                break
+            if int(store.add(key, 0)) >= q or (deadline is not None and time.perf_counter() - t0 > deadline):
+                return done, False  # dropped from this round
+        store.add(key, 1)
+        return done, True
+
     def local_train(self, nsteps: int) -> dict:
         net = self.net
         net.reset_train_stats()
         t0 = time.perf_counter()
+        participated = True
+        ran = nsteps
         with tracing.range("metisfl.local_train"):
             if self._ev0 is not None:
                 self._ev0.record()
-            net.train_steps(self.train_ds, nsteps, step_offset=self.steps_done)
+            if self.elastic:
+                ran, participated = self._train_elastic(nsteps, t0)
+            else:
+                net.train_steps(self.train_ds, nsteps, step_offset=self.steps_done)
             if self._ev1 is not None:
                 self._ev1.record()
                 self._ev1.synchronize()
                 ms = self._ev0.elapsed_time(self._ev1)
             else:
                 ms = (time.perf_counter() - t0) * 1e3
-        self.steps_done += nsteps
+        self.steps_done += ran
         tr = net.train_stats()
-        out = {"ms": ms, "ms_per_batch": ms / max(1, nsteps),
-               "ms_per_epoch": ms / max(1, nsteps) * self._spe,
-               "completed_batches": nsteps, "completed_epochs": nsteps / self._spe,
-               "train_loss": tr["loss"], "train_accuracy": tr["accuracy"]}
+        out = {"ms": ms, "ms_per_batch": ms / max(1, ran),
+               "ms_per_epoch": ms / max(1, ran) * self._spe,
+               "completed_batches": ran, "completed_epochs": ran / self._spe,
+               "train_loss": tr["loss"], "train_accuracy": tr["accuracy"],
+               "participated": participated}
         if self.cfg.evaluate_test and self.test_ds is not None:
             with tracing.range("metisfl.evaluate"):
                 out["test"] = net.evaluate(self.test_ds, self.cfg.eval_max_steps)
         return out
 
     def aggregation_weights(self, meta: np.ndarray) -> list[float]:
+        part = meta[:, 10] > 0.5
+        if not part.all():  # stragglers dropped: scale over the participants only
+            idx = np.flatnonzero(part)
+            ws = scaling.compute(self.cfg.scaling_factor, meta[idx, 0], meta[idx, 1], len(idx))
+            w = [0.0] * self.world
+            for i, x in zip(idx, ws):
+                w[int(i)] = float(x)
+            return w
         w = scaling.compute(self.cfg.scaling_factor, meta[:, 0], meta[:, 1], self.world)
         if self.engine is not None:
             we = self.engine.weights(meta[:, 0], meta[:, 1])
@@ -297,7 +357,8 @@ class CollectiveFederation:
         row = torch.tensor([self.train_ds.n, res["completed_batches"], res["ms_per_batch"],
                             res["ms_per_epoch"], res["train_loss"], res["train_accuracy"],
                             res["completed_epochs"], self.global_iteration,
-                            test.get("loss", float("nan")), test.get("accuracy", float("nan"))],
+                            test.get("loss", float("nan")), test.get("accuracy", float("nan")),
+                            1.0 if res["participated"] else 0.0],
                            dtype=torch.float64, device=self.comm.device)
         meta = self.comm.all_gather_rows(row).cpu().numpy()
         completed = time.time()
@@ -324,10 +385,30 @@ class CollectiveFederation:
         return rec
 
     # -- checkpoint / resume ------------------------------------------
+    COMMUNITY_FILE = "community_model.pb"
+
+    def community_model_proto(self):
+        """The community model as the reference's wire message
+        ``metisfl.FederatedModel`` (model.proto:48-52): one Variable per
+        tensor, in FlatState order, plaintext fp32."""
+        from metisfl_amd.proto import model_pb2
+        from metisfl_amd.utils.tensor_codec import model_from_arrays
+        st = self.net.state
+        vals = st.to_numpy()
+        names = [s.name for s in st.specs]
+        fm = model_pb2.FederatedModel()
+        fm.num_contributors = self.world
+        fm.global_iteration = self.global_iteration
+        fm.model.CopyFrom(model_from_arrays(names, [vals[n] for n in names], [s.trainable for s in st.specs]))
+        return fm
+
     def save_checkpoint(self, path: str) -> None:
-        """Collective: every rank writes its optimizer state; rank 0 also writes
-        the community model and the federation state.  The layout is plain
-        tensors + JSON (loadable with torch.load(weights_only=True))."""
+        """Collective.  Rank 0 writes the community model as a serialized
+        ``FederatedModel`` proto (the layout the gRPC controller exchanges:
+        ``ReplaceCommunityModel`` / ``GetCommunityModelLineage`` carry the
+        same message) plus federation.json; every rank writes its learner-
+        local optimizer state (torch.save of plain tensors, loadable with
+        weights_only=True)."""
         os.makedirs(path, exist_ok=True)
         st = self.net.state
         self._sync()
@@ -339,32 +420,59 @@ class CollectiveFederation:
                 per_rank[k] = t.cpu()
         torch.save(per_rank, os.path.join(path, f"rank{self.rank}.pt"))
         if self.rank == 0:
-            torch.save({"model32": st.model32.cpu()}, os.path.join(path, "community.pt"))
+            with open(os.path.join(path, self.COMMUNITY_FILE), "wb") as f:
+                f.write(self.community_model_proto().SerializeToString())
             with open(os.path.join(path, "federation.json"), "w") as f:
                 json.dump({"global_iteration": self.global_iteration,
                            "num_local_updates": self.num_local_updates,
                            "world": self.world, "learner_ids": self.learner_ids,
+                           "dataset_sizes": self.dataset_sizes,
                            "config": {k: v for k, v in asdict(self.cfg).items() if k != "extra"},
                            "variables": [[s.name, list(s.shape), s.trainable] for s in st.specs],
                            "history": [r.to_json() for r in self.history]}, f)
         self.comm.barrier()
 
+    def load_community_model(self, fm) -> None:
+        """Install a ``FederatedModel`` (proto or serialized bytes) as the
+        community model, matching variables by name."""
+        from metisfl_amd.proto import model_pb2
+        from metisfl_amd.utils.tensor_codec import model_to_arrays
+        if isinstance(fm, (bytes, bytearray)):
+            m = model_pb2.FederatedModel()
+            m.ParseFromString(bytes(fm))
+            fm = m
+        names, arrays, _ = model_to_arrays(fm.model)
+        st = self.net.state
+        st.load_numpy(dict(zip(names, arrays)))
+        st.set_anchor()
+
     def resume(self, path: str) -> None:
-        """Reload a checkpoint written by ``save_checkpoint`` (same world size)."""
+        """Reload a checkpoint written by ``save_checkpoint``.  The world size
+        may differ (learners joined or left, SURVEY §5.3 / the reference's
+        join-leave semantics, controller.cc:99-199): the community model is
+        restored on every rank, learner-local state (optimizer slots, step
+        counter, epoch permutation) only on ranks that existed before, and
+        the step budgets / aggregation weights follow the CURRENT shards
+        (computed at construction from the new dataset sizes)."""
         with open(os.path.join(path, "federation.json")) as f:
             meta = json.load(f)
-        if meta["world"] != self.world:
-            raise ValueError(f"checkpoint has {meta['world']} learners, running {self.world}")
+        with open(os.path.join(path, self.COMMUNITY_FILE), "rb") as f:
+            self.load_community_model(f.read())
         st = self.net.state
         dev = st.model32.device
-        st.model32.copy_(torch.load(os.path.join(path, "community.pt"), weights_only=True)["model32"].to(dev))
-        st.refresh_bf16()
-        per_rank = torch.load(os.path.join(path, f"rank{self.rank}.pt"), weights_only=True)
-        st.step.copy_(per_rank["step"].to(dev))
-        for k in ("m", "v", "anchor"):
-            if k in per_rank and getattr(st, k) is not None:
-                getattr(st, k).copy_(per_rank[k].to(dev))
-        self.train_ds.perm.copy_(per_rank["perm"].to(self.train_ds.perm.device))
-        self.steps_done = int(per_rank["steps_done"])
+        same_world = meta["world"] == self.world
+        rank_file = os.path.join(path, f"rank{self.rank}.pt")
+        if os.path.exists(rank_file) and self.rank < meta["world"]:
+            per_rank = torch.load(rank_file, weights_only=True)
+            st.step.copy_(per_rank["step"].to(dev))
+            for k in ("m", "v"):
+                if k in per_rank and getattr(st, k) is not None and per_rank[k].numel() == getattr(st, k).numel():
+                    getattr(st, k).copy_(per_rank[k].to(dev))
+            if same_world and per_rank["perm"].numel() == self.train_ds.perm.numel():
+                self.train_ds.perm.copy_(per_rank["perm"].to(self.train_ds.perm.device))
+                self.steps_done = int(per_rank["steps_done"])
+        st.set_anchor()  # FedProx anchors at the restored community model
         self.global_iteration = int(meta["global_iteration"])
-        self.num_local_updates = list(meta["num_local_updates"])
+        if same_world:
+            self.num_local_updates = list(meta["num_local_updates"])
+        self.resumed_from_world = int(meta["world"])
