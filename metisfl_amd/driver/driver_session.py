@@ -237,6 +237,62 @@ class DriverSessionBase:
             model = model_from_arrays(names, arrays, tr, self._he_scheme)
         return self._driver_controller_grpc_client.replace_community_model(1, model, request_retries=3)
 
+    # -- on-node collective data plane (DataPlane: rccl) ----------------------------------------
+    @property
+    def collective(self) -> bool:
+        return self.federation_environment.data_plane == "rccl"
+
+    def _collective_job(self, rounds: int) -> str:
+        """The JSON job description every collective rank reads."""
+        env = self.federation_environment
+        lm, cp = env.local_model_config, env.communication_protocol
+        rule = env.global_model_config.aggregation_rule
+        if self.neural_engine != "static":
+            raise RuntimeError("the collective data plane runs static-graph models (StaticModelDef)")
+        opt = MM.construct_optimizer_config_pb_from_kwargs(lm.optimizer_config.optimizer_pb_kwargs)
+        fed = {"protocol": "semi_synchronous" if cp.is_semi_synchronous else "synchronous",
+               "scaling_factor": {"NumTrainingExamples": "NUM_TRAINING_EXAMPLES",
+                                  "NumCompletedBatches": "NUM_COMPLETED_BATCHES",
+                                  "NumParticipants": "NUM_PARTICIPANTS"}.get(
+                   rule.aggregation_rule_scaling_factor or "NumTrainingExamples", "NUM_TRAINING_EXAMPLES"),
+               "batch_size": lm.batch_size, "local_epochs": lm.local_epochs,
+               "semi_sync_lambda": float(cp.semi_synchronous_lambda or 2.0),
+               "semi_sync_recompute": bool(cp.semi_sync_recompute_num_updates),
+               "participation_ratio": float(env.global_model_config.participation_ratio or 1.0),
+               "secure_aggregation": self._he_scheme is not None}
+        job = {"model_dir": self._model_dir, "batch_size": lm.batch_size, "seed": self.seed,
+               "optimizer_hex": opt.SerializeToString().hex(),
+               "controller_hex": self._controller_entity.SerializeToString().hex(),
+               "train_recipe": self.train_dataset_recipe_fp, "test_recipe": self.test_dataset_recipe_fp,
+               "rounds": rounds, "federation": fed,
+               "backend": "gloo" if self.device == "cpu" else None,
+               "learners": [{"id": l.learner_id, "hostname": l.grpc_servicer.hostname or "localhost",
+                             "port": int(l.grpc_servicer.port or 0) or 1 + i,
+                             "train_path": l.dataset_configs.train_dataset_path,
+                             "test_path": l.dataset_configs.test_dataset_path, "devices": l.devices}
+                            for i, l in enumerate(env.learners)]}
+        p = os.path.join(self.working_dir, "collective_job.json")
+        with open(p, "w") as f:
+            json.dump(job, f)
+        return p
+
+    def _init_collective_learners(self, rounds: int):
+        """One process per learner (= per GPU) under one process group; the
+        torch.distributed env is set here, before any of them touches a GPU
+        (reference counterpart: driver_session.py:529-582)."""
+        import sys
+        job = self._collective_job(rounds)
+        learners = list(self.federation_environment.learners)
+        port = free_port()
+        for rank, l in enumerate(learners):
+            extra = {"RANK": str(rank), "WORLD_SIZE": str(len(learners)), "MASTER_ADDR": "127.0.0.1",
+                     "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+                     "LOCAL_RANK": str(l.devices[0] if l.devices else rank)}
+            if self.device == "cpu":
+                extra.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+            self._spawn(f"learner_{l.learner_id}", [sys.executable, "-m", "metisfl_amd.learner.collective", job],
+                        extra)
+
     # -- public API -----------------------------------------------------------------------------------
     def initialize_federation(self):
         self._init_controller()
@@ -244,9 +300,24 @@ class DriverSessionBase:
         if not ok:
             raise RuntimeError("controller did not come up; see controller.log")
         self._ship_model_to_controller()
+        if self.collective:
+            self._init_collective_learners(self.federation_environment.termination_signals.federation_rounds)
+            return
         for l in self.federation_environment.learners:
             self._init_learner(l, self.federation_environment.controller)
             time.sleep(0.1)
+
+    def run_collective(self, request_every_secs: float = 1.0) -> dict:
+        """Whole collective federation: controller up, one rank per GPU,
+        wait for the configured rounds, statistics, shutdown."""
+        if not self.collective:
+            raise RuntimeError("run_collective needs DataPlane: rccl in the federation environment")
+        self.initialize_federation()
+        try:
+            self.monitor_federation(request_every_secs)
+        finally:
+            self.shutdown_federation()
+        return self.get_federation_statistics()
 
     def monitor_federation(self, request_every_secs: float = 10):
         env = self.federation_environment
@@ -261,6 +332,9 @@ class DriverSessionBase:
             for name, p in self._procs.items():
                 if p.poll() is not None and p.returncode != 0:
                     raise RuntimeError(f"{name} exited with {p.returncode}; see {name}.log")
+            if self.collective and all(p.poll() == 0 for n, p in self._procs.items() if n.startswith("learner_")):
+                MetisLogger.info("Collective learners completed their rounds. Exiting ...")
+                return "rounds"
             md = self._driver_controller_grpc_client.get_runtime_metadata(num_backtracks=0).metadata
             if (cp.is_synchronous or cp.is_semi_synchronous) and rounds and len(md) > 0:
                 if max(m.global_iteration for m in md) > rounds:
@@ -302,7 +376,8 @@ class DriverSessionBase:
     def shutdown_federation(self, timeout: float = 60):
         try:
             self._collect_local_statistics()
-            for c in self._driver_learner_grpc_clients.values():
+            # collective learners have no gRPC server: they exit after their rounds
+            for c in ([] if self.collective else self._driver_learner_grpc_clients.values()):
                 try:
                     c.shutdown_learner(request_retries=1, request_timeout=30, block=True)
                 except Exception as e:  # noqa: BLE001 - a dead learner must not block shutdown

@@ -210,6 +210,10 @@ class FederationEnvironment:
         fe = config.get("FederationEnvironment")
         self.docker = DockerImage(fe.get("DockerImage"))
         self.launcher = fe.get("Launcher", "local")
+        # "grpc" (the reference's: models travel through the controller) or
+        # "rccl" (one process per GPU on this node, models averaged by an
+        # RCCL all-reduce; the controller keeps the bookkeeping)
+        self.data_plane = str(fe.get("DataPlane", "grpc")).lower()
         self.termination_signals = TerminationSignals(fe.get("TerminationSignals"))
         self.evaluation_metric = fe.get("EvaluationMetric", "accuracy")
         self.communication_protocol = CommunicationProtocol(fe.get("CommunicationProtocol"))

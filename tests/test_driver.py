@@ -92,3 +92,30 @@ def test_driver_session_end_to_end(tmp_path, engine):
     if engine == "static":
         res = stats["community_model_results"]["community_evaluation"]
         assert any(e.get("evaluations") for e in res)
+
+
+def test_driver_runs_rccl_data_plane_collective(tmp_path):
+    """DataPlane: rccl -- the driver launches one collective learner process
+    per learner (gloo on the CPU; RCCL on GPUs), rank 0 reports every round
+    to the gRPC controller, and the reference's four statistics keys come
+    back through the usual controller queries."""
+    import json
+    from metisfl_amd.driver.driver_session import DriverSession, free_port
+    from metisfl_amd.models.model_def import StaticModelDef
+    from metisfl_amd.utils.fedenv_parser import FederationEnvironment
+    d = env_dict([free_port(), free_port()], rounds=2)
+    d["FederationEnvironment"]["DataPlane"] = "rccl"
+    fe = FederationEnvironment(config=d)
+    assert fe.data_plane == "rccl"
+    sess = DriverSession(fe, StaticModelDef("resnet18", width_mult=0.125), train_recipe, None, eval_recipe,
+                         working_dir=str(tmp_path / "w"), device="cpu")
+    stats = sess.run_collective(request_every_secs=0.3)
+    assert set(stats) == {"learners_descriptor", "learners_models_results", "federation_runtime_metadata",
+                          "community_model_results"}
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert sorted({int(m["global_iteration"]) for m in md}) == [1, 2]
+    assert len(stats["learners_descriptor"]["learner"]) == 2
+    lineages = stats["learners_models_results"]["learner_task"]
+    assert len(lineages) == 2 and all(len(v["task_metadata"]) == 2 for v in lineages.values())
+    sess.save_statistics(str(tmp_path / "experiment.json"))
+    assert json.load(open(tmp_path / "experiment.json"))["federation_runtime_metadata"]
