@@ -83,7 +83,8 @@ std::vector<int64_t> conv32_plan(int64_t mode, int64_t N, int64_t H, int64_t W, 
 }
 
 void run(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const torch::Tensor& w, const torch::Tensor& y,
-         const c10::optional<torch::Tensor>& ws, double* stats, bool accum, const mfl::BnBwdFusion32* bnb) {
+         const c10::optional<torch::Tensor>& ws, double* stats, bool accum, const mfl::BnBwdFusion32* bnb,
+         int stats_reps = 1) {
   const auto p = mfl::plan_conv32(g, dgrad ? 1 : 0);
   float* slab = nullptr;
   int* counters = nullptr;
@@ -93,8 +94,12 @@ void run(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const tor
     counters = reinterpret_cast<int*>(ws->data_ptr<float>());
     slab = ws->data_ptr<float>() + kCounterWords;
   }
-  mfl::launch_conv32_gemm(g, dgrad, p, fp(src), fp(w), fp(y), slab, counters, stats, accum, bnb, cur_stream(y));
+  mfl::launch_conv32_gemm(g, dgrad, p, fp(src), fp(w), fp(y), slab, counters, stats, accum, bnb, cur_stream(y),
+                          stats_reps);
 }
+
+// BN accumulators may hold R replicas [R][2][C] (R = numel / 2C)
+int reps_of(const torch::Tensor& acc, int64_t C) { return (int)std::max<int64_t>(1, acc.numel() / (2 * C)); }
 
 double* stats_ptr(const c10::optional<torch::Tensor>& st, int64_t C) {
   if (!st.has_value() || !st->defined()) return nullptr;
@@ -110,7 +115,8 @@ void conv32_forward(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::opti
   check_f32(x, (int64_t)N * H * W * C, "x");
   check_f32(w, (int64_t)Co * R * S * C, "w");
   check_f32(y, (int64_t)g.M * Co, "y");
-  run(g, false, x, w, y, ws, stats_ptr(stats, Co), false, nullptr);
+  run(g, false, x, w, y, ws, stats_ptr(stats, Co), false, nullptr,
+      stats.has_value() && stats->defined() ? reps_of(*stats, Co) : 1);
 }
 
 void conv32_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, c10::optional<torch::Tensor> ws, int64_t N,
@@ -135,6 +141,7 @@ void conv32_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, c10::opti
     f.mean = fp(*bn_mean);
     f.invstd = fp(*bn_invstd);
     f.acc = stats_ptr(bn_acc, C);
+    f.reps = reps_of(*bn_acc, C);
   }
   run(g, true, dy, w, dx, ws, nullptr, accumulate, fuse ? &f : nullptr);
 }
@@ -166,7 +173,7 @@ const double* acc_ptr(const torch::Tensor& acc, int64_t C) {
 void bn32_stats(torch::Tensor x, int64_t C, torch::Tensor acc) {
   check_nhwc32(x, C);
   acc_ptr(acc, C);
-  mfl::launch_bn32_stats(fp(x), x.numel() / C, (int)C, acc.data_ptr<double>(), cur_stream(x));
+  mfl::launch_bn32_stats(fp(x), x.numel() / C, (int)C, acc.data_ptr<double>(), cur_stream(x), reps_of(acc, C));
 }
 
 void bn32_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torch::Tensor gamma, torch::Tensor beta,
@@ -188,6 +195,7 @@ void bn32_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, to
   if (train) {
     TORCH_CHECK(acc.has_value() && acc->defined(), "train-mode BN needs the statistics accumulator");
     a.acc = acc_ptr(*acc, C);
+    a.reps = reps_of(*acc, C);
   }
   a.gamma = fp(gamma);
   a.beta = fp(beta);
@@ -229,6 +237,7 @@ void bn32_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tenso
   if (dgamma.has_value() && dgamma->defined()) { check_pc(*dgamma, C, "dgamma"); a.dgamma = fp(*dgamma); }
   if (dbeta.has_value() && dbeta->defined()) { check_pc(*dbeta, C, "dbeta"); a.dbeta = fp(*dbeta); }
   a.acc = acc_ptr(acc, C);
+  a.reps = reps_of(acc, C);
   a.gamma = fp(gamma);
   a.mean = fp(mean);
   a.invstd = fp(invstd);
@@ -237,7 +246,7 @@ void bn32_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tenso
   a.C = (int)C;
   auto s = cur_stream(x);
   if (!presummed)
-    mfl::launch_bn32_bwd_reduce(a.dy, a.x, a.y, a.mean, a.invstd, a.M, a.C, acc.data_ptr<double>(), s);
+    mfl::launch_bn32_bwd_reduce(a.dy, a.x, a.y, a.mean, a.invstd, a.M, a.C, acc.data_ptr<double>(), s, a.reps);
   mfl::launch_bn32_bwd_apply(a, s);
 }
 

@@ -46,7 +46,7 @@ __device__ __forceinline__ void channel_atomic4(float4 s, float4 q, int C, int t
 }  // namespace
 
 __global__ __launch_bounds__(256) void bn32_stats_kernel(const float* __restrict__ x, int64_t M, int C,
-                                                         double* __restrict__ acc) {
+                                                         double* __restrict__ acc, int reps) {
   // channel groups beyond 256 threads: grid.y slices the channels
   const int tpr_all = C / 4;
   const int tpr = min(tpr_all - (int)blockIdx.y * 256, 256);
@@ -62,13 +62,13 @@ __global__ __launch_bounds__(256) void bn32_stats_kernel(const float* __restrict
       q.x += v.x * v.x; q.y += v.y * v.y; q.z += v.z * v.z; q.w += v.w * v.w;
     }
   }
-  channel_atomic4(s, q, C, tpr, rpp, acc + cbase);
+  channel_atomic4(s, q, C, tpr, rpp, acc + (int64_t)(blockIdx.x % reps) * 2 * C + cbase);
 }
 
-void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_t s) {
+void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_t s, int reps) {
   // acc + cbase: the [C] halves stay at stride C, so pass the base and C
   const int gy = (C / 4 + 255) / 256;
-  bn32_stats_kernel<<<dim3(blocks_for(M, C), gy), 256, 0, s>>>(x, M, C, acc);
+  bn32_stats_kernel<<<dim3(blocks_for(M, C), gy), 256, 0, s>>>(x, M, C, acc, reps > 0 ? reps : 1);
 }
 
 template <bool RES, bool RELU>
@@ -88,8 +88,13 @@ __global__ __launch_bounds__(256) void bn32_apply_kernel(BnFwdArgs32 a, int64_t 
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     double mu, var;
     if (a.train) {
-      mu = a.acc[c] * inv_m;
-      var = a.acc[C + c] * inv_m - mu * mu;
+      double s0 = 0.0, s1 = 0.0;
+      for (int r = 0; r < a.reps; ++r) {
+        s0 += a.acc[(int64_t)r * 2 * C + c];
+        s1 += a.acc[(int64_t)r * 2 * C + C + c];
+      }
+      mu = s0 * inv_m;
+      var = s1 * inv_m - mu * mu;
       if (var < 0.0) var = 0.0;
     } else {
       mu = a.run_mean[c];
@@ -151,7 +156,7 @@ __global__ __launch_bounds__(256) void bn32_bwd_reduce_kernel(const float* __res
                                                               const float* __restrict__ y,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd, int64_t M,
-                                                              int C, double* __restrict__ acc) {
+                                                              int C, double* __restrict__ acc, int reps) {
   const int tpr_all = C / 4;
   const int tpr = min(tpr_all - (int)blockIdx.y * 256, 256);
   const int rpp = 256 / tpr;
@@ -180,13 +185,14 @@ __global__ __launch_bounds__(256) void bn32_bwd_reduce_kernel(const float* __res
       q.w += g.w * ((xv.w - mu.w) * is.w);
     }
   }
-  channel_atomic4(s, q, C, tpr, rpp, acc + blockIdx.y * 1024);
+  channel_atomic4(s, q, C, tpr, rpp, acc + (int64_t)(blockIdx.x % reps) * 2 * C + blockIdx.y * 1024);
 }
 
 void launch_bn32_bwd_reduce(const float* dy, const float* x, const float* y, const float* mean,
-                            const float* invstd, int64_t M, int C, double* acc, hipStream_t s) {
+                            const float* invstd, int64_t M, int C, double* acc, hipStream_t s, int reps) {
   const int gy = (C / 4 + 255) / 256;
-  bn32_bwd_reduce_kernel<<<dim3(blocks_for(M, C), gy), 256, 0, s>>>(dy, x, y, mean, invstd, M, C, acc);
+  bn32_bwd_reduce_kernel<<<dim3(blocks_for(M, C), gy), 256, 0, s>>>(dy, x, y, mean, invstd, M, C, acc,
+                                                                      reps > 0 ? reps : 1);
 }
 
 // Backward apply: dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat))
@@ -207,7 +213,11 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
   }
   const double inv_m = 1.0 / (double)a.M;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const double s = a.acc[c], q = a.acc[C + c];
+    double s = 0.0, q = 0.0;
+    for (int r = 0; r < a.reps; ++r) {
+      s += a.acc[(int64_t)r * 2 * C + c];
+      q += a.acc[(int64_t)r * 2 * C + C + c];
+    }
     sc[c] = a.gamma[c] * a.invstd[c];
     sc[C + c] = (float)(s * inv_m);
     sc[2 * C + c] = (float)(q * inv_m);

@@ -27,6 +27,7 @@ struct ConvPlan {
   int stats_rows = 0;  // 1 = the epilogue accumulates BN statistics
   int bk = 64;         // k-tile depth (64 or 128)
   int par_mc = 0;      // stride-2 dgrad parity decomposition: rows per class (0 = off)
+  int stages = 3;      // LDS ring depth (conv32.hip)
 };
 
 // Kernel argument block.  *_shift = log2 of the divisor when it is a power of

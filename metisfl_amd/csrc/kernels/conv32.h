@@ -35,6 +35,8 @@ struct Conv32Args {
   int accum;
   int par_mc;
   FastDiv dc, dq, dpq;  // / C, / Q, / (P*Q)
+  int reps;             // BN accumulator replicas ([reps][2][Ng]; workgroup b adds into replica b % reps)
+  int dbg;              // timing experiments only (MFL_C32_DBG): bit0 skip MFMAs, bit1 skip operand DMA
 };
 
 struct BnBwdFusion32 {
@@ -43,15 +45,18 @@ struct BnBwdFusion32 {
   const float* mean = nullptr;
   const float* invstd = nullptr;
   double* acc = nullptr;
+  int reps = 1;
 };
 
 // mode 0 fwd, 1 dgrad, 2 wgrad.  kchunk in k elements (multiple of 32).
 ConvPlan plan_conv32(const ConvGeom& g, int mode);
 int conv32_counter_slots(const ConvGeom& g, const ConvPlan& p);
 
+// stats: [stats_reps][2][Ng] fp64 BN sums of the forward output (replicated
+// so that hundreds of workgroups do not serialise on the same 2*Ng addresses)
 void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const float* src, const float* wgt,
                         float* y, float* ysplit, int* counters, double* stats, bool accum,
-                        const BnBwdFusion32* bnb, hipStream_t s);
+                        const BnBwdFusion32* bnb, hipStream_t s, int stats_reps = 1);
 // dw (fp32 OHWI); accumulate: dw holds a running sum (zero for a fresh step)
 // and every slice adds atomically; otherwise the split-1 plan stores and a
 // split plan requires dw zeroed by the caller.

@@ -38,6 +38,8 @@
 //    with fp64 atomics.  Split-K slices reduce in-launch (last arriver sums
 //    the write-through slabs in slice order: bitwise deterministic).
 //  * Stride-2 dgrad runs parity-class decomposed (PAR), as in conv.hip.
+#include <type_traits>
+
 #include "kernels/common.h"
 #include "kernels/conv32.h"
 #include "kernels/lds_tiles.h"
@@ -46,9 +48,10 @@ namespace mfl {
 
 namespace {
 
-constexpr int kBK = 32;      // fp32 k-elements per tile = 128-B rows
-constexpr int kStages = 3;   // LDS ring
-constexpr int kTiles = kStages - 1;  // k-tiles in flight
+constexpr int kBK = 64;      // fp32 k-elements per tile
+constexpr int kRowB = kBK * 4;       // [row][k] tiles: 256-B rows
+constexpr int kRPI = 1024 / kRowB;   // rows per 1-KiB LDS-DMA instruction
+constexpr int kCPR = kRowB / 16;     // 16-B chunks per row
 
 __device__ __forceinline__ f32x16 mfma_f32(float a, float b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
@@ -62,41 +65,60 @@ __device__ __forceinline__ int fdiv(int x, const FastDiv& f) {
 // split the k-loop body)
 __device__ __forceinline__ uint32_t oob_or(bool ok, uint32_t off) { return off | (kOOB & (0u - (uint32_t)!ok)); }
 
-// fp32 [row][32] tile, 128-B rows: 16-B chunk ch of `row`
-__device__ __forceinline__ int rk_off(int row, int ch) { return row * 128 + ((ch ^ swz_b128<128>(row)) << 4); }
+// fp32 [row][kBK] tile: 16-B chunk ch of `row` (swizzled)
+__device__ __forceinline__ int rk_off(int row, int ch) { return row * kRowB + ((ch ^ swz_b128<kRowB>(row)) << 4); }
 
-// k-loop over the LDS ring, branch-free: the DMA of tile kt+2 is issued in
-// every iteration (past the end its offsets are all out of range: the
-// hardware fills the free stage with zeros and reads no memory), so the loop
-// body is ONE basic block and compute() can interleave the issue's address
-// math with its MFMAs (sched_group_barrier).  In-order issue otherwise runs
-// the ~60-90 VALU instructions of the issue between two dependent MFMAs with
-// the matrix pipe idle (measured: 45-50% of fp32 MFMA peak).  Stage
-// (kt+2)%3 is free: every wave passed this iteration's barrier, i.e.
-// finished reading it in iteration kt-1.
-template <int L, typename Issue, typename Compute>
-__device__ __forceinline__ void ring_loop(int nk, Issue& issue, Compute& compute) {
+// k-loop: LDS ring of 3 stages (DMA 2-3 tiles ahead) + register double
+// buffer of MFMA fragments (LDS reads 1 tile ahead).  Iteration kt:
+//   wait own DMA of tile kt+1, wait own fragment reads of tile kt, barrier
+//   (=> every wave's tile kt+1 landed AND every wave holds tile kt's
+//   fragments in registers, so stage kt%3 is free) -> issue the DMA of tile
+//   kt+3 into stage kt%3 -> issue the fragment reads of tile kt+1 -> MFMAs of
+//   tile kt.  The reads and the DMA address math then run UNDER the MFMAs of
+//   the same wave (sched_group_barrier interleave) instead of in front of
+//   them: with one wave per SIMD the LDS read latency before each tile's first
+//   MFMA was the largest exposed stall of the straight loop (45-50% of the
+//   fp32 MFMA peak).  The loop is unrolled by two so each register set is
+//   static.  DMAs past the last tile use out-of-range offsets (zero fill, no
+//   memory traffic): the body stays one basic block.
+template <int NS, int L, typename Issue, typename Read, typename Mma>
+__device__ __forceinline__ void ring_loop(int nk, Issue& issue, Read& read, Mma& mma) {
+  static_assert((NS - 1) * L <= 63, "vmcnt is a 6-bit counter");
 #pragma unroll
-  for (int u = 0; u < kTiles; ++u) issue(u, u);
-  int stage = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    wait_vmcnt<L>();  // own DMA of tile kt landed; tile kt+1's may still fly
-    lds_barrier();    // every wave's tile kt landed, every wave left stage (kt-1)%3
-    const int nxt = kt + kTiles;
-    const int nst = stage == 0 ? kStages - 1 : stage - 1;
-    compute(stage, [&] { issue(nxt, nst); });
-    stage = stage == kStages - 1 ? 0 : stage + 1;
+  for (int u = 0; u < NS; ++u) issue(u, u);
+  wait_vmcnt<(NS - 1) * L>();  // tile 0
+  lds_barrier();
+  read(0, std::integral_constant<int, 0>{});
+  int st = 0;  // stage of tile kt
+  auto step = [&](int kt, auto cur) {
+    constexpr int C = decltype(cur)::value;
+    wait_vmcnt<(NS - 2) * L>();            // tile kt+1 landed (kt+2.. may fly)
+    __builtin_amdgcn_s_waitcnt(0xC07F);    // lgkmcnt(0): tile kt's fragments in registers
+    lds_barrier();
+    const int nst = st == NS - 1 ? 0 : st + 1;
+    issue(kt + NS, st);
+    read(nst, std::integral_constant<int, 1 - C>{});
+    mma(cur);
+    st = nst;
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, std::integral_constant<int, 0>{});
+    step(kt + 1, std::integral_constant<int, 1>{});
   }
+  if (kt < nk) step(kt, std::integral_constant<int, 0>{});
   wait_vmcnt<0>();  // the trailing (zero-fill) DMAs land before smem is reused
+  __builtin_amdgcn_s_waitcnt(0xC07F);
 }
 
-// Interleave pattern for one k-tile: per MFMA, up to V VALU, 2 SALU and one
-// VMEM instruction of the DMA issue slot in behind it.
+// Interleave pattern for one k-tile: per MFMA, one LDS read, up to V VALU,
+// 2 SALU and one VMEM (LDS-DMA) instruction slot in behind it.
 template <int NMFMA, int V>
 __device__ __forceinline__ void interleave_mfma() {
 #pragma unroll
   for (int i = 0; i < NMFMA; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
     __builtin_amdgcn_sched_group_barrier(0x002, V, 0);  // VALU
     __builtin_amdgcn_sched_group_barrier(0x004, 2, 0);  // SALU
     __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
@@ -171,6 +193,8 @@ __device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, int m0, int
     }
   }
   if (!stats) return;
+  // replica of this workgroup (b % 8 = the XCD under round-robin placement)
+  stats += (int64_t)((blockIdx.x + blockIdx.y * gridDim.x + blockIdx.z * gridDim.x * gridDim.y) % a.reps) * 2 * g.Ng;
   reinterpret_cast<float4*>(red)[2 * t] = s;
   reinterpret_cast<float4*>(red)[2 * t + 1] = q;
   __syncthreads();
@@ -195,13 +219,13 @@ __device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, int m0, int
 //   fwd:   A = im2col(X) [M][R*S*C],  B[k][n] = W[n][k]   (both [row][k] tiles)
 //   dgrad: A = stride-aware gather of dY [M = N*H*W][R*S*Co],
 //          B[k = (r,s,co)][n = ci] = W[co][r][s][ci]      ([k][n] tile, b32 reads)
-template <int BM, int BN, bool DGRAD, int KS, int ST, bool PAR>
-__global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
+template <int BM, int BN, bool DGRAD, int KS, int ST, bool PAR, int NS>
+__global__ __launch_bounds__(256, 1) void conv32_gemm_kernel(Conv32Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr int A_BYTES = BM * 128;
-  constexpr int STAGE = A_BYTES + BN * 128;
-  constexpr int ACH = BM / 32;  // DMA instructions per wave per k-tile (1 KiB each)
-  constexpr int BCH = BN / 32;
+  constexpr int A_BYTES = BM * kRowB;
+  constexpr int STAGE = A_BYTES + BN * kRowB;
+  constexpr int ACH = BM * kBK / 1024;  // DMA instructions per wave per k-tile (1 KiB each)
+  constexpr int BCH = BN * kBK / 1024;
   constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 MFMA tiles per wave
   constexpr int BRB = BN * 4;                // dgrad B row bytes
   constexpr int B_RPI = 1024 / BRB, B_CPR = BRB / 16;
@@ -233,12 +257,12 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
 
   // [row][k] DMA: instruction i of wave w fills rows 32i + 8w + lane/8,
   // physical chunk lane%8 <- logical chunk (k offset) a_kc (i-independent).
-  const int lrow = wave * 8 + (lane >> 3);
-  const int a_kc = ((lane & 7) ^ swz_b128<128>(lrow)) * 4;
+  const int lrow = wave * kRPI + lane / kCPR;
+  const int a_kc = ((lane % kCPR) ^ swz_b128<kRowB>(lrow)) * 4;  // same for every i: rows step by 4*kRPI
   int a_nb[ACH], a_y0[ACH], a_x0[ACH];
 #pragma unroll
   for (int i = 0; i < ACH; ++i) {
-    const int m = m0 + lrow + 32 * i;
+    const int m = m0 + lrow + 4 * kRPI * i;
     const int mm = m < g.M ? m : 0;
     if constexpr (PAR) {
       const int q2 = g.Q >> 1;
@@ -263,6 +287,7 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
   }
 
   auto issue = [&](int kt, int stage) {
+    if (a.dbg & 2) return;
     uint8_t* st = smem + stage * STAGE;
     const int kb = kbeg + kt * kBK;
     {
@@ -311,7 +336,7 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
         }
         off = oob_or((kr < kend) & (n < g.Ng), (uint32_t)((ko * KS * KS + rs) * g.Ng + n) * 4u);
       } else {
-        const int n = n0 + lrow + 32 * i;
+        const int n = n0 + lrow + 4 * kRPI * i;
         const int k = kb + a_kc;
         off = oob_or((k < kend) & (n < g.Ng), (uint32_t)(n * g.K + k) * 4u);
       }
@@ -353,14 +378,17 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
   // run, and the scheduler barrier keeps hipcc from sinking them back behind
   // the MFMAs (it otherwise re-uses one register set per group and re-exposes
   // the LDS latency before every group)
-  auto compute = [&](int stage, auto&& issue_next) {
+  f32x4 fa[2][kBK / 8][TM], fb[2][kBK / 8][TN];  // fragment double buffer
+  auto read = [&](int stage, auto set) {
+    constexpr int S = decltype(set)::value;
     const uint8_t* As = smem + stage * STAGE;
     const uint8_t* Bs = As + A_BYTES;
-    f32x4 af[kBK / 8][TM], bfr[kBK / 8][TN];
 #pragma unroll
-    for (int grp = 0; grp < kBK / 8; ++grp) load(As, Bs, grp, af[grp], bfr[grp]);
-    __builtin_amdgcn_sched_barrier(0);  // all fragment reads first
-    issue_next();
+    for (int grp = 0; grp < kBK / 8; ++grp) load(As, Bs, grp, fa[S][grp], fb[S][grp]);
+  };
+  auto mma = [&](auto set) {
+    constexpr int S = decltype(set)::value;
+    if (a.dbg & 1) return;
 #pragma unroll
     for (int grp = 0; grp < kBK / 8; ++grp)
 #pragma unroll
@@ -368,11 +396,11 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(af[grp][i][e], bfr[grp][j][e], acc[i][j]);
-    interleave_mfma<4 * kBK / 8 * TM * TN, 8>();
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(fa[S][grp][i][e], fb[S][grp][j][e], acc[i][j]);
+    interleave_mfma<4 * kBK / 8 * TM * TN, 6>();
     __builtin_amdgcn_sched_barrier(0);
   };
-  ring_loop<ACH + BCH>(nk, issue, compute);
+  ring_loop<NS, ACH + BCH>(nk, issue, read, mma);
   __syncthreads();  // every wave done with the ring before smem is reused
 
   // ---- epilogue -----------------------------------------------------------
@@ -452,14 +480,14 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
 // wgrad:  dW[co][j] = sum_m dY[m][co] * im2col(X)[m][j],  j = (r, s, c)
 // Both operands are row-contiguous in memory: tiles [32 m][BM co] and
 // [32 m][BN j], b32 fragment reads, MFMA (g, e) slot h reduces m = 8g + 4h + e.
-template <int BM, int BN, int KS, int ST>
-__global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, float* __restrict__ dw, int atomic) {
+template <int BM, int BN, int KS, int ST, int NS>
+__global__ __launch_bounds__(256, 1) void conv32_wgrad_kernel(Conv32Args a, float* __restrict__ dw, int atomic) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int A_BYTES = kBK * BM * 4;
   constexpr int STAGE = A_BYTES + kBK * BN * 4;
   constexpr int ARB = BM * 4, A_RPI = 1024 / ARB, A_CPR = ARB / 16;
   constexpr int BRB = BN * 4, B_RPI = 1024 / BRB, B_CPR = BRB / 16;
-  constexpr int ACH = BM / 32, BCH = BN / 32;
+  constexpr int ACH = BM * kBK / 1024, BCH = BN * kBK / 1024;
   constexpr int TM = BM / 64, TN = BN / 64;
   const ConvGeom& g = a.g;  // H,W,C = X; P,Q = dY spatial; Ng = Cout; K = R*S*C; M = N*P*Q
   const auto rsA = make_rsrc(a.src, a.src_bytes);  // dY
@@ -484,6 +512,7 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
   const int PQ = g.P * g.Q;
 
   auto issue = [&](int kt, int stage) {
+    if (a.dbg & 2) return;
     uint8_t* st = smem + stage * STAGE;
     const int kb = kbeg + kt * kBK;
 #pragma unroll
@@ -524,14 +553,17 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
       for (int j = 0; j < TN; ++j) bfr[j][e] = Bs[kr * BN + wn * (BN / 2) + 32 * j + li];
     }
   };
-  auto compute = [&](int stage, auto&& issue_next) {
+  f32x4 fa[2][kBK / 8][TM], fb[2][kBK / 8][TN];
+  auto read = [&](int stage, auto set) {
+    constexpr int S = decltype(set)::value;
     const float* As = reinterpret_cast<const float*>(smem + stage * STAGE);
     const float* Bs = reinterpret_cast<const float*>(smem + stage * STAGE + A_BYTES);
-    f32x4 af[kBK / 8][TM], bfr[kBK / 8][TN];
 #pragma unroll
-    for (int grp = 0; grp < kBK / 8; ++grp) load(As, Bs, grp, af[grp], bfr[grp]);
-    __builtin_amdgcn_sched_barrier(0);
-    issue_next();
+    for (int grp = 0; grp < kBK / 8; ++grp) load(As, Bs, grp, fa[S][grp], fb[S][grp]);
+  };
+  auto mma = [&](auto set) {
+    constexpr int S = decltype(set)::value;
+    if (a.dbg & 1) return;
 #pragma unroll
     for (int grp = 0; grp < kBK / 8; ++grp)
 #pragma unroll
@@ -539,11 +571,11 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(af[grp][i][e], bfr[grp][j][e], acc[i][j]);
-    interleave_mfma<4 * kBK / 8 * TM * TN, 8>();
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(fa[S][grp][i][e], fb[S][grp][j][e], acc[i][j]);
+    interleave_mfma<4 * kBK / 8 * TM * TN, 6>();
     __builtin_amdgcn_sched_barrier(0);
   };
-  ring_loop<ACH + BCH>(nk, issue, compute);
+  ring_loop<NS, ACH + BCH>(nk, issue, read, mma);
 
   // epilogue straight from the accumulators: each register store covers two
   // 128-B row segments (the full-rate atomic shape, MI355X_MICROARCH.md)
@@ -583,21 +615,31 @@ void set_lds(K* kernel, size_t lds) {
                               (int)lds);
 }
 
+// LDS ring depth per tile shape: 64x64 workgroups run two per CU (4 stages =
+// 64 KiB each), the larger tiles one per CU with the deepest ring that fits
+// 160 KiB.  Measured: with 3 stages every conv ran at ~45% of the fp32 MFMA
+// peak -- the k-tiles waited for their LDS-DMA (latency-bound: 2 x 16 KiB in
+// flight per workgroup cannot cover ~1-2 us at 38 GB/s per CU).
+constexpr int stages_for(int bm, int bn) {
+  return (156 * 1024) / ((bm + bn) * kRowB) > 4 ? 4 : (156 * 1024) / ((bm + bn) * kRowB);
+}
+
 size_t gemm_lds(int bm, int bn) {
-  const size_t ring = (size_t)kStages * (bm + bn) * 128;
+  const size_t ring = (size_t)stages_for(bm, bn) * (bm + bn) * kRowB;
   const size_t epi = (size_t)bm * (bn + 4) * 4 + 256 * 8 * 4 + 16;
   return ring > epi ? ring : epi;
 }
 
 template <int BM, int BN, bool DG, int KS, int ST, bool PAR>
 void launch_t(const Conv32Args& a, dim3 grid, hipStream_t s) {
+  constexpr int NS = stages_for(BM, BN);
   static bool init = false;
   const size_t lds = gemm_lds(BM, BN);
   if (!init) {
-    set_lds(&conv32_gemm_kernel<BM, BN, DG, KS, ST, PAR>, lds);
+    set_lds(&conv32_gemm_kernel<BM, BN, DG, KS, ST, PAR, NS>, lds);
     init = true;
   }
-  conv32_gemm_kernel<BM, BN, DG, KS, ST, PAR><<<grid, 256, lds, s>>>(a);
+  conv32_gemm_kernel<BM, BN, DG, KS, ST, PAR, NS><<<grid, 256, lds, s>>>(a);
 }
 
 template <int BM, int BN, bool DG>
@@ -623,7 +665,9 @@ void launch_geom(const Conv32Args& a, dim3 grid, hipStream_t s) {
 struct Cand {
   int bm, bn;
 };
-constexpr Cand kCands[] = {{64, 64}, {128, 64}, {64, 128}, {128, 128}};
+// (128x128 needs 2 x 8 x 4 fragment registers per operand and tile row at
+// kBK = 64 -- beyond the register budget of the double-buffered loop)
+constexpr Cand kCands[] = {{64, 64}, {128, 64}, {64, 128}};
 
 }  // namespace
 
@@ -650,7 +694,7 @@ static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
     if (fn && c.bn != fn) continue;
     if (par && ((g.N * (g.P / 2) * (g.Q / 2)) % c.bm)) continue;
     const int tiles = cdiv(rows, c.bm) * cdiv(cols, c.bn);
-    const int occ = c.bm * c.bn <= 4096 ? 2 : 1;
+    const int occ = 1;  // a 64-deep ring of >= 3 stages fills most of a CU's LDS
     const int slots = 256 * occ;
     for (int sp = 1; sp <= 64 && sp <= nkt_all; ++sp) {
       if (fs && sp != fs) continue;
@@ -677,6 +721,7 @@ static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
   }
   best.stats_rows = mode == 0 ? 1 : 0;
   best.bk = kBK;
+  best.stages = stages_for(best.bm, best.bn);
   best.par_mc = par && mode == 1 ? g.N * (g.P / 2) * (g.Q / 2) : 0;
   if (best_t >= 1e30) best.kchunk = 0;  // no feasible tile
   return best;
@@ -711,7 +756,7 @@ static void fill_shifts(Conv32Args& a) {
 
 void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const float* src, const float* wgt,
                         float* y, float* ysplit, int* counters, double* stats, bool accum,
-                        const BnBwdFusion32* bnb, hipStream_t s) {
+                        const BnBwdFusion32* bnb, hipStream_t s, int stats_reps) {
   Conv32Args a{};
   a.g = g;
   a.src = src;
@@ -727,32 +772,34 @@ void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const 
     a.bn_invstd = bnb->invstd;
     a.bn_acc = bnb->acc;
   }
+  a.reps = (bnb && bnb->acc) ? (bnb->reps > 0 ? bnb->reps : 1) : (stats_reps > 0 ? stats_reps : 1);
   a.src_bytes = range_bytes((int64_t)g.N * g.H * g.W * g.C);
   a.wgt_bytes = range_bytes((int64_t)g.K * g.Ng);
   a.kchunk = p.kchunk;
   a.accum = accum ? 1 : 0;
   a.par_mc = dgrad ? p.par_mc : 0;
   fill_shifts(a);
+  a.dbg = env_int("MFL_C32_DBG", 0);
   const dim3 grid(cdiv(g.M, p.bm), cdiv(g.Ng, p.bn), p.splits);
   const int key = p.bm * 1000 + p.bn;
   switch (key) {
     case 64064: dgrad ? launch_geom<64, 64, true>(a, grid, s) : launch_geom<64, 64, false>(a, grid, s); break;
     case 128064: dgrad ? launch_geom<128, 64, true>(a, grid, s) : launch_geom<128, 64, false>(a, grid, s); break;
-    case 64128: dgrad ? launch_geom<64, 128, true>(a, grid, s) : launch_geom<64, 128, false>(a, grid, s); break;
-    default: dgrad ? launch_geom<128, 128, true>(a, grid, s) : launch_geom<128, 128, false>(a, grid, s); break;
+    default: dgrad ? launch_geom<64, 128, true>(a, grid, s) : launch_geom<64, 128, false>(a, grid, s); break;
   }
 }
 
 namespace {
 template <int BM, int BN, int KS, int ST>
 void launch_w(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStream_t s) {
+  constexpr int NS = stages_for(BM, BN);
   static bool init = false;
-  const size_t lds = (size_t)kStages * kBK * (BM + BN) * 4;
+  const size_t lds = (size_t)NS * kBK * (BM + BN) * 4;
   if (!init) {
-    set_lds(&conv32_wgrad_kernel<BM, BN, KS, ST>, lds);
+    set_lds(&conv32_wgrad_kernel<BM, BN, KS, ST, NS>, lds);
     init = true;
   }
-  conv32_wgrad_kernel<BM, BN, KS, ST><<<grid, 256, lds, s>>>(a, dw, atomic);
+  conv32_wgrad_kernel<BM, BN, KS, ST, NS><<<grid, 256, lds, s>>>(a, dw, atomic);
 }
 template <int BM, int BN>
 void launch_w_geom(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStream_t s) {
@@ -774,14 +821,14 @@ void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, c
   a.wgt_bytes = range_bytes((int64_t)g.N * g.H * g.W * g.C);
   a.kchunk = p.kchunk;
   fill_shifts(a);
+  a.dbg = env_int("MFL_C32_DBG", 0);
   const dim3 grid(cdiv(g.Ng, p.bm), cdiv(g.K, p.bn), p.splits);
   const int atomic = (accumulate || p.splits > 1) ? 1 : 0;
   const int key = p.bm * 1000 + p.bn;
   switch (key) {
     case 64064: launch_w_geom<64, 64>(a, grid, dw, atomic, s); break;
     case 128064: launch_w_geom<128, 64>(a, grid, dw, atomic, s); break;
-    case 64128: launch_w_geom<64, 128>(a, grid, dw, atomic, s); break;
-    default: launch_w_geom<128, 128>(a, grid, dw, atomic, s); break;
+    default: launch_w_geom<64, 128>(a, grid, dw, atomic, s); break;
   }
 }
 

@@ -41,6 +41,13 @@ __device__ __forceinline__ void store8(float* d, const Pack8& p) {
   reinterpret_cast<float4*>(d)[1] = p.b;
 }
 
+// softmax transcendentals: the fast forms for the bf16 path, full-precision
+// libm for the fp32 (reference-precision) path -- only K per sample
+template <typename T>
+__device__ __forceinline__ float hexp(float x) { return sizeof(T) == 4 ? expf(x) : __expf(x); }
+template <typename T>
+__device__ __forceinline__ float hlog(float x) { return sizeof(T) == 4 ? logf(x) : __logf(x); }
+
 template <typename T>
 __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int HW, int C,
                                                    const float* __restrict__ W,
@@ -106,7 +113,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
     for (int k = lane; k < K; k += 64) mx = fmaxf(mx, lg[k]);
     mx = wave_max(mx);
     float se = 0.f;
-    for (int k = lane; k < K; k += 64) se += __expf(lg[k] - mx);
+    for (int k = lane; k < K; k += 64) se += hexp<T>(lg[k] - mx);
     se = wave_sum(se);
     const int y = labels[b];
     // argmax (first max wins)
@@ -121,7 +128,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
       const int oi = __shfl_xor(bi, o, 64);
       if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
     }
-    const float lse = mx + __logf(se);
+    const float lse = mx + hlog<T>(se);
     if (lane == 0 && stats) {
       atomicAdd(&stats[0], lse - lg[y]);
       atomicAdd(&stats[1], bi == y ? 1.f : 0.f);
@@ -130,7 +137,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
     if (backward) {
       const float invB = 1.f / (float)B;
       for (int k = lane; k < K; k += 64) {
-        const float p = __expf(lg[k] - lse);
+        const float p = hexp<T>(lg[k] - lse);
         const float d = (p - (k == y ? 1.f : 0.f)) * invB;
         lg[k] = d;
         dlog[(int64_t)b * K + k] = d;

@@ -109,6 +109,7 @@ struct BnFwdArgs32 {
   int C;
   float momentum, eps;
   int train, relu;
+  int reps;  // acc holds [reps][2][C] replicas, summed here
 };
 struct BnBwdArgs32 {
   const float* dy;
@@ -124,11 +125,12 @@ struct BnBwdArgs32 {
   float* dy_masked;
   int64_t M;
   int C;
+  int reps;  // acc replicas, as BnFwdArgs32
 };
-void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_t s);
+void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_t s, int reps = 1);
 void launch_bn32_apply(const BnFwdArgs32& a, hipStream_t s);
 void launch_bn32_bwd_reduce(const float* dy, const float* x, const float* y, const float* mean,
-                            const float* invstd, int64_t M, int C, double* acc, hipStream_t s);
+                            const float* invstd, int64_t M, int C, double* acc, hipStream_t s, int reps = 1);
 void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s);
 
 // ---- head.hip ------------------------------------------------------------

@@ -149,8 +149,12 @@ class ConvBN(Layer):
         self.invstd = torch.zeros(s.Co, **f32)
         # fp64 [2C] statistics accumulators (forward sums, backward sums),
         # carved from the model-wide buffer the optimizer launch re-zeroes
-        self.acc_f = ws.take_acc(2 * s.Co)
-        self.acc_b = ws.take_acc(2 * s.Co)
+        # fp32 kernels spread their fp64 atomics over 8 replicas (one per
+        # XCD under round-robin placement): 256+ workgroups adding into the
+        # same 2*C addresses serialised at the memory side (~5 us per conv)
+        reps = 8 if ws.dtype == torch.float32 and torch.device(device).type == "cuda" else 1
+        self.acc_f = ws.take_acc(2 * s.Co * reps)
+        self.acc_b = ws.take_acc(2 * s.Co * reps)
         dev = torch.device(device)
         self.pf = K.conv_plan(0, s, dev, ws.dtype)
         self.pd = K.conv_plan(1, s, dev, ws.dtype)

@@ -83,6 +83,12 @@ def _wt(w: torch.Tensor) -> torch.Tensor:
     return w.float().permute(0, 3, 1, 2)
 
 
+def _acc_total(acc: torch.Tensor, C: int) -> torch.Tensor:
+    """BN accumulators may hold R replicas [R][2][C] (the fp32 kernels spread
+    their fp64 atomics over them); the statistics are their sum."""
+    return acc[: acc.numel() // (2 * C) * 2 * C].reshape(-1, 2 * C).sum(0)
+
+
 def _acc_stats_cpu(y: torch.Tensor, acc: torch.Tensor) -> None:
     yf = y.float().reshape(-1, y.shape[-1]).double()
     C = yf.shape[1]
@@ -228,8 +234,9 @@ def bn_apply(x, C: int, acc, gamma, beta, mean, invstd, run_mean, run_var, y, re
         return
     M = x.numel() // C
     if train:
-        mu = acc[:C] / M
-        var = (acc[C:2 * C] / M - mu * mu).clamp_min(0)
+        tot = _acc_total(acc, C)
+        mu = tot[:C] / M
+        var = (tot[C:2 * C] / M - mu * mu).clamp_min(0)
         mean.copy_(mu.float())
         invstd.copy_((1.0 / torch.sqrt(var + eps)).float())
         unb = var * M / (M - 1) if M > 1 else var
@@ -272,12 +279,13 @@ def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
     if not presummed:  # else the producer of dy already added the sums
         acc[:C] += gm.double().sum(0)
         acc[C:2 * C] += (gm.double() * xh.reshape(-1, C).double()).sum(0)
+    tot = _acc_total(acc, C)
     if dgamma is not None:
-        dgamma.copy_(acc[C:2 * C].float())
+        dgamma.copy_(tot[C:2 * C].float())
     if dbeta is not None:
-        dbeta.copy_(acc[:C].float())
+        dbeta.copy_(tot[:C].float())
     k1 = gamma * invstd
-    out = k1 * (g - (acc[:C] / M).float() - xh * (acc[C:2 * C] / M).float())
+    out = k1 * (g - (tot[:C] / M).float() - xh * (tot[C:2 * C] / M).float())
     dx.copy_(out.to(dx.dtype))
 
 

@@ -13,7 +13,7 @@ for f in files:
         name = r["Kernel_Name"]
         if flt and flt not in name:
             continue
-        key = (name.split("(")[0].replace("(anonymous namespace)::", "")[-60:], r["Grid_Size"])
+        key = (name.replace("(anonymous namespace)::", "").split("(")[0][-60:], r["Grid_Size"])
         per[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for (name, g), cs in sorted(per.items()):
     avg = {k: sum(v) / len(v) for k, v in cs.items()}
