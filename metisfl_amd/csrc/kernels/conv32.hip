@@ -48,7 +48,10 @@ namespace mfl {
 
 namespace {
 
-constexpr int kBK = 64;      // fp32 k-elements per tile
+#ifndef MFL_C32_BK
+#define MFL_C32_BK 32
+#endif
+constexpr int kBK = MFL_C32_BK;  // fp32 k-elements per tile (32: 128-B rows)
 constexpr int kRowB = kBK * 4;       // [row][k] tiles: 256-B rows
 constexpr int kRPI = 1024 / kRowB;   // rows per 1-KiB LDS-DMA instruction
 constexpr int kCPR = kRowB / 16;     // 16-B chunks per row
@@ -220,7 +223,7 @@ __device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, int m0, int
 //   dgrad: A = stride-aware gather of dY [M = N*H*W][R*S*Co],
 //          B[k = (r,s,co)][n = ci] = W[co][r][s][ci]      ([k][n] tile, b32 reads)
 template <int BM, int BN, bool DGRAD, int KS, int ST, bool PAR, int NS>
-__global__ __launch_bounds__(256, 1) void conv32_gemm_kernel(Conv32Args a) {
+__global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int A_BYTES = BM * kRowB;
   constexpr int STAGE = A_BYTES + BN * kRowB;
@@ -481,7 +484,7 @@ __global__ __launch_bounds__(256, 1) void conv32_gemm_kernel(Conv32Args a) {
 // Both operands are row-contiguous in memory: tiles [32 m][BM co] and
 // [32 m][BN j], b32 fragment reads, MFMA (g, e) slot h reduces m = 8g + 4h + e.
 template <int BM, int BN, int KS, int ST, int NS>
-__global__ __launch_bounds__(256, 1) void conv32_wgrad_kernel(Conv32Args a, float* __restrict__ dw, int atomic) {
+__global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, float* __restrict__ dw, int atomic) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int A_BYTES = kBK * BM * 4;
   constexpr int STAGE = A_BYTES + kBK * BN * 4;
@@ -620,8 +623,11 @@ void set_lds(K* kernel, size_t lds) {
 // 160 KiB.  Measured: with 3 stages every conv ran at ~45% of the fp32 MFMA
 // peak -- the k-tiles waited for their LDS-DMA (latency-bound: 2 x 16 KiB in
 // flight per workgroup cannot cover ~1-2 us at 38 GB/s per CU).
+#ifndef MFL_C32_NS
+#define MFL_C32_NS 3
+#endif
 constexpr int stages_for(int bm, int bn) {
-  return (156 * 1024) / ((bm + bn) * kRowB) > 4 ? 4 : (156 * 1024) / ((bm + bn) * kRowB);
+  return (156 * 1024) / ((bm + bn) * kRowB) > MFL_C32_NS ? MFL_C32_NS : (156 * 1024) / ((bm + bn) * kRowB);
 }
 
 size_t gemm_lds(int bm, int bn) {

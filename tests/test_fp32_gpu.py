@@ -244,23 +244,24 @@ def test_fp32_resnet18_step_matches_torch_nn():
     net._train_body(ds)
     torch.cuda.synchronize()
     loss = net.train_stats()["loss"]
-    ref_loss, ref_g, ref_run = reference_step(values, _x8(x), torch.as_tensor(y))
-    # PyTorch's own fp32 evaluation of the same step: the fp32 noise floor.
-    # Gradients that are sums with heavy cancellation (BN beta = sum of the
-    # masked upstream gradient over 2,048-32,768 rows) lose relative accuracy
-    # in ANY fp32 evaluation; the bound is 1e-4 or 2x what torch fp32 itself
-    # reaches on that tensor, whichever is larger.
-    _, t32_g, _ = reference_step(values, _x8(x), torch.as_tensor(y), dtype=torch.float32)
+    # ReLU masks pinned to the executor's own (tests/torch_resnet_ref._relu):
+    # with 2.5M ReLU'd elements per step a handful sit within fp32 rounding of
+    # zero, and a flipped mask element moves its whole upstream gradient --
+    # e.g. ONE flipped element of layer3.1's output put 1e-4 into every
+    # gradient below it.  The flip count itself is bounded.
+    masks = {n: (l.y > 0).permute(0, 3, 1, 2).cpu()
+             for n, l in [("stem", net.stem)] + [(c.name, c) for b in net.blocks for c in (b.c1, b.c2)]}
+    flips = [0]
+    ref_loss, ref_g, ref_run = reference_step(values, _x8(x), torch.as_tensor(y), relu_masks=masks, flips=flips)
+    assert flips[0] <= 8, flips
     assert abs(loss - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss)), (loss, ref_loss)
     worst = []
     for name, rg in ref_g.items():
         err = _rel(net.state.grad(name), rg)
-        floor = _rel(t32_g[name], rg)
-        worst.append((err, floor, name))
-        assert err <= max(1e-4, 2 * floor), (name, err, floor)
+        worst.append((err, name))
+        assert err <= 1e-4, (name, err)
     worst.sort(reverse=True)
-    print("worst per-tensor gradient rel err (ours, torch fp32, name):", worst[:4])
-    assert sum(e <= 1e-4 for e, _, _ in worst) >= len(worst) - 3
+    print(f"mask flips {flips[0]}; worst per-tensor gradient rel err:", worst[:4])
     for name, rv in ref_run.items():
         assert _rel(net.state.view(name), rv) <= 1e-5, name
 

@@ -10,9 +10,25 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 
+def _relu(t, masks, key, flips=None):
+    """ReLU, or -- with ``masks`` -- multiplication by a given 0/1 mask (the
+    same function wherever the mask agrees with the sign of ``t``).  Pinning
+    the masks to the candidate's own removes ReLU's measure-zero derivative
+    jump from a gradient comparison: an element whose pre-activation is
+    within rounding of 0 can land on either side in two correct fp32
+    evaluations, and its whole upstream gradient then flips in or out."""
+    if masks is None or key not in masks:
+        return F.relu(t)
+    mk = masks[key].to(t.dtype)
+    if flips is not None:
+        flips[0] += int(((t > 0).to(t.dtype) != mk).sum())
+    return t * mk
+
+
 class _Block(nn.Module):
     def __init__(self, cin, cout, stride):
         super().__init__()
+        self.masks, self.key, self.flips = None, "", None
         self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
         self.bn1 = nn.BatchNorm2d(cout, eps=1e-5, momentum=0.1)
         self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
@@ -23,9 +39,9 @@ class _Block(nn.Module):
                                     nn.BatchNorm2d(cout, eps=1e-5, momentum=0.1))
 
     def forward(self, x):
-        o = F.relu(self.bn1(self.conv1(x)))
+        o = _relu(self.bn1(self.conv1(x)), self.masks, f"{self.key}.conv1", self.flips)
         o = self.bn2(self.conv2(o))
-        return F.relu(o + (self.sc(x) if self.sc is not None else x))
+        return _relu(o + (self.sc(x) if self.sc is not None else x), self.masks, f"{self.key}.conv2", self.flips)
 
 
 class TorchResNet18(nn.Module):
@@ -39,9 +55,18 @@ class TorchResNet18(nn.Module):
             c = w
         self.blocks = nn.ModuleList(blocks)
         self.fc = nn.Linear(c, num_classes)
+        self.masks = None
+        self.flips = [0]  # pinned mask elements that disagree with the sign
+
+    def pin_relu_masks(self, masks: dict | None) -> None:
+        """``masks``: framework ConvBN name -> NCHW 0/1 tensor of that layer's
+        ReLU output sign (see ``_relu``)."""
+        self.masks = masks
+        for i, b in enumerate(self.blocks):
+            b.masks, b.key, b.flips = masks, f"layer{i // 2 + 1}.{i % 2}", self.flips
 
     def forward(self, x):
-        h = F.relu(self.stem_bn(self.stem(x)))
+        h = _relu(self.stem_bn(self.stem(x)), self.masks, "stem", self.flips)
         for b in self.blocks:
             h = b(h)
         return self.fc(h.mean((2, 3)))
@@ -88,14 +113,20 @@ class TorchResNet18(nn.Module):
         return r
 
 
-def reference_step(values: dict, x_nhwc8: torch.Tensor, labels: torch.Tensor, dtype=torch.float64):
+def reference_step(values: dict, x_nhwc8: torch.Tensor, labels: torch.Tensor, dtype=torch.float64,
+                   relu_masks: dict | None = None, flips: list | None = None):
     """One training-mode forward/backward of the oracle: returns (loss, grads,
-    running stats after the step)."""
+    running stats after the step).  ``relu_masks``: see ``pin_relu_masks``;
+    ``flips`` (a one-element list) receives how many pinned mask elements
+    disagreed with the oracle's own pre-activation signs."""
     m = TorchResNet18().to(dtype)
     m.load_from(values)
+    m.pin_relu_masks(relu_masks)
     m.train()
     x = x_nhwc8.to(dtype).permute(0, 3, 1, 2).contiguous()
     logits = m(x)
     loss = F.cross_entropy(logits, labels.long())
     loss.backward()
+    if flips is not None:
+        flips[0] = m.flips[0]
     return float(loss.detach()), m.grads(), m.running_stats()
