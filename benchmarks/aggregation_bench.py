@@ -6,6 +6,11 @@ T tensors x V values, FedStride, in-memory store).
 Measures, for N learner models of T tensors x V fp32 values:
   * host   -- the native engine's FedAvg / FedStride over serialized Model
               protos (the reference controller's CPU path, OpenMP),
+  * engine_device -- the same engine call with the controller's device
+              backend (engine/device_agg.*): models staged into HBM on arrival
+              (as Controller::learner_completed_task does), one multi-tensor
+              launch, result copied back into the engine's model; plus the
+              cold variant that uploads inside the call,
   * device -- the HIP multi-tensor weighted sum K1 over device-resident flat
               models (one launch for all tensors),
   * rccl   -- scale + all-reduce of the flat model when launched with
@@ -59,14 +64,41 @@ def main() -> int:
     weights = [w / sum(weights) for w in weights]
     out = {"learners": N, "tensors": T, "values_per_tensor": V, "model_mb": T * V * 4 / 2 ** 20}
 
+    names = [f"t{i}" for i in range(T)]
+    models = [model_from_arrays(names, [rng.standard_normal(V).astype(np.float32) for _ in range(T)])
+              .SerializeToString() for _ in range(N)]
+    dev_ok = E.device_aggregation_available()
+    E.set_device_aggregation(False)
+    # the engine's aggregation as the controller runs it: over parsed models,
+    # (serialize the result included, parse of the inputs excluded)
+    staged_host = E.StagedModels([f"L{i}" for i in range(N)], models)
     if not a.no_host:
-        names = [f"t{i}" for i in range(T)]
-        models = [model_from_arrays(names, [rng.standard_normal(V).astype(np.float32) for _ in range(T)])
-                  .SerializeToString() for _ in range(N)]
-        out["host_fedavg_ms"] = _timeit(lambda: E.aggregate_models("fed_avg", models, weights), a.reps)
-        out["host_fedstride_ms"] = _timeit(
-            lambda: E.aggregate_models("fed_stride", models, weights, a.stride), a.reps)
-        del models
+        out["host_fedavg_ms"] = _timeit(lambda: staged_host.aggregate("fed_avg", weights), a.reps)
+        out["host_fedstride_ms"] = _timeit(lambda: staged_host.aggregate("fed_stride", weights, a.stride),
+                                           a.reps)
+    del staged_host
+    if dev_ok:
+        E.set_device_aggregation(True, 0)
+        host_bytes = E.aggregate_models("fed_avg", models, weights) if a.no_host else None
+        # controller path with residency: models staged on arrival, aggregated from HBM
+        staged = E.StagedModels([f"L{i}" for i in range(N)], models)
+        out["engine_device_fedavg_ms"] = _timeit(lambda: staged.aggregate("fed_avg", weights), a.reps)
+        st = E.device_aggregation_stats()
+        out["engine_device_fedavg_kernel_ms"] = st["last_kernel_ms"]
+        out["engine_device_fedavg_download_ms"] = st["last_download_ms"]
+        out["engine_device_stage_ms_per_model"] = st["last_upload_ms"]
+        out["engine_device_fedstride_ms"] = _timeit(lambda: staged.aggregate("fed_stride", weights, a.stride),
+                                                    a.reps)
+        E.set_device_aggregation(False)
+        ref = staged.aggregate("fed_avg", weights)
+        E.set_device_aggregation(True, 0)
+        out["engine_device_byte_identical"] = staged.aggregate("fed_avg", weights) == ref
+        # cold: the inputs are uploaded inside the call (no residency)
+        out["engine_device_cold_fedavg_ms"] = _timeit(lambda: E.aggregate_models("fed_avg", models, weights),
+                                                      max(1, a.reps // 2))
+        out["device"] = E.device_aggregation_stats().get("device_name")
+        del staged, host_bytes
+    del models
 
     if torch.cuda.is_available():
         dev = torch.device("cuda")

@@ -9,6 +9,7 @@
 #include "common/model.h"
 #include "engine/aggregation.h"
 #include "engine/controller.h"
+#include "engine/device_agg.h"
 #include "engine/policies.h"
 #include "he/ckks.h"
 #include "common/chacha20.h"
@@ -21,11 +22,18 @@ namespace {
 
 py::bytes B(const std::string& s) { return py::bytes(s); }
 
+// Shared payloads become ONE Python bytes object referenced by every task.
 py::dict dispatch_to_py(const Dispatch& d) {
   py::list runs, evals;
-  for (auto& [id, req] : d.run_tasks) runs.append(py::make_tuple(id, B(req)));
+  std::map<const std::string*, py::bytes> objs;
+  auto obj = [&](const Payload& p) {
+    auto it = objs.find(p.get());
+    if (it == objs.end()) it = objs.emplace(p.get(), B(*p)).first;
+    return it->second;
+  };
+  for (auto& [id, req] : d.run_tasks) runs.append(py::make_tuple(id, obj(req)));
   for (auto& e : d.eval_tasks)
-    evals.append(py::make_tuple(e.learner_id, B(e.request), e.comm_eval_index, e.metadata_index));
+    evals.append(py::make_tuple(e.learner_id, obj(e.request), e.comm_eval_index, e.metadata_index));
   py::dict out;
   out["run_tasks"] = runs;
   out["eval_tasks"] = evals;
@@ -59,6 +67,33 @@ py::bytes aggregate_models(const std::string& rule, const std::vector<std::strin
   }
   return B(serialize_federated_model(out));
 }
+
+struct StagedModels {
+  std::vector<ModelT> ms;
+  StagedModels(const std::vector<std::string>& ids, const std::vector<std::string>& models) {
+    for (auto& s : models) ms.push_back(parse_model(s));
+    py::gil_scoped_release nogil;
+    if (DeviceAggregator::enabled_for(ms.empty() ? 0 : ms[0].byte_size()))
+      for (size_t i = 0; i < ms.size(); ++i) DeviceAggregator::get()->stage(ids.at(i), ms[i], 1);
+  }
+  py::bytes aggregate(const std::string& rule, const std::vector<double>& weights, int stride) {
+    std::unique_ptr<AggregationFunction> agg;
+    if (rule == "fed_avg") agg.reset(new FederatedAverage());
+    else if (rule == "fed_stride") agg.reset(new FederatedStride());
+    else throw std::runtime_error("unknown rule " + rule);
+    FederatedModelT out;
+    {
+      py::gil_scoped_release nogil;
+      const size_t s = (rule == "fed_stride" && stride > 0) ? (size_t)stride : ms.size();
+      for (size_t b = 0; b < ms.size(); b += s) {
+        AggInput in;
+        for (size_t i = b; i < std::min(ms.size(), b + s); ++i) in.push_back({{&ms[i], weights[i]}});
+        out = agg->aggregate(in);
+      }
+    }
+    return B(serialize_federated_model(out));
+  }
+};
 
 class PyRecency {
  public:
@@ -214,6 +249,42 @@ PYBIND11_MODULE(_engine, m) {
           for (size_t i = 0; i < ids.size(); ++i) parts.push_back({ids[i], ntrain[i], batches[i]});
           return compute_scaling_factors(kind, n_all, parts);
         });
+  m.def("set_device_aggregation", &DeviceAggregator::set_enabled, py::arg("enabled"),
+        py::arg("min_bytes") = -1,
+        "Process-wide switch of the controller's device aggregation backend.");
+  m.def("device_aggregation_available", [] {
+    py::gil_scoped_release nogil;
+    return DeviceAggregator::get() != nullptr;
+  });
+  m.def("device_aggregation_stats", [] {
+    py::dict d;
+    auto* a = DeviceAggregator::peek();
+    d["available"] = a != nullptr;
+    if (!a) return d;
+    const DeviceAggStats s = a->stats();
+    d["device"] = s.device;
+    d["device_name"] = s.device_name;
+    d["staged_models"] = s.staged_models;
+    d["staged_bytes"] = s.staged_bytes;
+    d["resident_bytes"] = s.resident_bytes;
+    d["resident_hits"] = s.resident_hits;
+    d["cold_uploads"] = s.cold_uploads;
+    d["fedavg_calls"] = s.fedavg_calls;
+    d["rolling_calls"] = s.rolling_calls;
+    d["pwa_calls"] = s.pwa_calls;
+    d["last_kernel_ms"] = s.last_kernel_ms;
+    d["last_total_ms"] = s.last_total_ms;
+    d["last_upload_ms"] = s.last_upload_ms;
+    d["last_download_ms"] = s.last_download_ms;
+    return d;
+  });
+  // Benchmark / test helper: models parsed and staged exactly like
+  // Controller::learner_completed_task does, then aggregated in place.
+  py::class_<StagedModels>(m, "StagedModels")
+      .def(py::init<const std::vector<std::string>&, const std::vector<std::string>&>(),
+           py::arg("ids"), py::arg("models"))
+      .def("aggregate", &StagedModels::aggregate, py::arg("rule"), py::arg("weights"),
+           py::arg("stride") = 0);
   m.def("aggregate_models", &aggregate_models, py::arg("rule"), py::arg("models"),
         py::arg("weights"), py::arg("stride") = 0);
   py::class_<PyRecency>(m, "FedRec").def(py::init<>()).def("aggregate", &PyRecency::aggregate);

@@ -2,9 +2,11 @@
 
 Two shared objects are produced next to the Python package:
 
-* ``metisfl_amd/_engine*.so`` -- the host-side federation controller engine
+* ``metisfl_amd/_engine*.so`` -- the federation controller engine
   (scheduler / selector / scalers / aggregators / model store / runtime
-  metadata / RNS-CKKS), plain C++17 + OpenMP + pybind11.  It is the native
+  metadata / RNS-CKKS), C++17 + OpenMP + pybind11, plus the device
+  aggregation backend (engine/device_agg*, HIP runtime + gfx950 kernels)
+  that takes over FedAvg / FedStride / FedRec / PWA when a GPU is visible.  It is the native
   equivalent of the reference's Bazel-built ``controller.so`` and ``fhe.so``
   (reference: setup.py:21-45, metisfl/controller/pybind/controller_pybind.cc,
   metisfl/encryption/pybind/ckks_pybind.cc).
@@ -68,6 +70,7 @@ def write_ninja() -> str:
                          + glob.glob(os.path.join(csrc, "engine", "*.cc"))
                          + glob.glob(os.path.join(csrc, "he", "*.cc"))
                          + [os.path.join(csrc, "bindings", "engine_pybind.cc")])
+    engine_hip = sorted(glob.glob(os.path.join(csrc, "engine", "*.hip")))
     hip_srcs = sorted(glob.glob(os.path.join(csrc, "kernels", "*.hip")))
     ops_bind = sorted(glob.glob(os.path.join(csrc, "bindings", "*.cpp")))
 
@@ -75,8 +78,9 @@ def write_ninja() -> str:
         "ninja_required_version = 1.3",
         f"cxx = g++",
         f"hipcc = {ROCM}/bin/hipcc",
-        f"engine_cflags = -O3 -fPIC -std=c++17 -fopenmp -Wall -Wno-sign-compare -fvisibility=hidden "
-        f"-I{csrc} {pyinc}",
+        f"engine_cflags = -O3 -fPIC -std=c++17 -fopenmp -Wall -Wno-sign-compare -Wno-unused-result -fvisibility=hidden "
+        f"-D__HIP_PLATFORM_AMD__ -I{csrc} -I{ROCM}/include {pyinc}",
+        f"engine_ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64",
         f"hip_cflags = --offload-arch={ARCH} -O3 -fPIC -std=c++17 -munsafe-fp-atomics -I{csrc} "
         f"-Wno-unused-result",
         f"bind_cflags = -O2 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__ -DUSE_ROCM "
@@ -91,7 +95,7 @@ def write_ninja() -> str:
         "  deps = gcc",
         "  description = CXX $in",
         "rule link_engine",
-        "  command = $cxx -shared -fopenmp $in -o $out",
+        "  command = $cxx -shared -fopenmp $in -o $out $engine_ldflags",
         "  description = LINK $out",
         "rule hipcc",
         "  command = $hipcc -MMD -MF $out.d $hip_cflags -c $in -o $out",
@@ -113,6 +117,10 @@ def write_ninja() -> str:
         o = os.path.join(BUILD_DIR, "engine", os.path.relpath(s, csrc).replace("/", "__") + ".o")
         eng_objs.append(o)
         lines.append(f"build {_rel(o)}: cxx_engine {_rel(s)}")
+    for s in engine_hip:  # the controller's device-aggregation kernels
+        o = os.path.join(BUILD_DIR, "engine", os.path.basename(s) + ".o")
+        eng_objs.append(o)
+        lines.append(f"build {_rel(o)}: hipcc {_rel(s)}")
     eng_so = os.path.join(PKG, "_engine" + suffix)
     lines.append(f"build {_rel(eng_so)}: link_engine " + " ".join(_rel(o) for o in eng_objs))
 

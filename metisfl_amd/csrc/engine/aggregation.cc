@@ -6,6 +6,7 @@
 #include <stdexcept>
 #include <type_traits>
 
+#include "engine/device_agg.h"
 #include "he/ckks.h"
 
 namespace mfl {
@@ -57,6 +58,17 @@ void dispatch(int dt, F&& f) {
 struct Chunk {
   size_t var, beg, end;
 };
+// Small models stay on one thread: an OpenMP team's barrier costs more than
+// the whole loop there (and, on oversubscribed or CPU-quota'd hosts, a
+// spinning team was measured at 30-60 ms for a 0.4 MB model vs 0.5 ms serial).
+constexpr size_t kParallelMinElems = size_t(1) << 20;
+
+size_t total_elems(const ModelT& m) {
+  size_t n = 0;
+  for (auto& v : m.vars) n += v.t.length;
+  return n;
+}
+
 std::vector<Chunk> make_chunks(const ModelT& m, size_t grain = 1 << 16) {
   std::vector<Chunk> out;
   for (size_t v = 0; v < m.vars.size(); ++v) {
@@ -73,6 +85,17 @@ void weighted_sum_into(ModelT& out, const std::vector<const ModelT*>& models,
                        const std::vector<double>& weights) {
   if (models.empty()) return;
   const ModelT& sample = *models.front();
+  for (size_t v = 0; v < sample.vars.size(); ++v) {
+    const auto& sv = sample.vars[v];
+    if (sv.ciphertext) throw std::runtime_error("Only Plaintext variables are supported.");
+    for (auto* m : models)
+      if (m->vars.size() != sample.vars.size() || m->vars[v].t.value.size() != sv.t.value.size())
+        throw std::runtime_error("models have mismatching structure");
+  }
+  // K1 on the device when the controller has one (byte-identical result)
+  if (DeviceAggregator::enabled_for(sample.byte_size()) &&
+      DeviceAggregator::get()->weighted_sum(out, models, weights))
+    return;
   out.vars.resize(sample.vars.size());
   for (size_t v = 0; v < sample.vars.size(); ++v) {
     auto& ov = out.vars[v];
@@ -86,13 +109,10 @@ void weighted_sum_into(ModelT& out, const std::vector<const ModelT*>& models,
     ov.t.byte_order = sv.t.byte_order;
     ov.t.fortran_order = sv.t.fortran_order;
     ov.t.value.assign((size_t)sv.t.length * dtype_size(sv.t.dtype), '\0');
-    if (sv.ciphertext) throw std::runtime_error("Only Plaintext variables are supported.");
-    for (auto* m : models)
-      if (m->vars.size() != sample.vars.size() || m->vars[v].t.value.size() != ov.t.value.size())
-        throw std::runtime_error("models have mismatching structure");
   }
   const auto chunks = make_chunks(out);
-#pragma omp parallel for schedule(dynamic, 1)
+  const bool par = total_elems(out) * models.size() >= kParallelMinElems;
+#pragma omp parallel for schedule(dynamic, 1) if (par)
   for (size_t c = 0; c < chunks.size(); ++c) {
     const Chunk ch = chunks[c];
     auto& ov = out.vars[ch.var];
@@ -111,7 +131,8 @@ void weighted_sum_into(ModelT& out, const std::vector<const ModelT*>& models,
 void merge_models(ModelT& y, const ModelT& x, double w, int op) {
   if (!same_structure(y, x)) throw std::runtime_error("merge: mismatching structure");
   const auto chunks = make_chunks(y);
-#pragma omp parallel for schedule(dynamic, 1)
+  const bool par = total_elems(y) >= kParallelMinElems;
+#pragma omp parallel for schedule(dynamic, 1) if (par)
   for (size_t c = 0; c < chunks.size(); ++c) {
     const Chunk ch = chunks[c];
     auto& yv = y.vars[ch.var];
@@ -129,7 +150,8 @@ void merge_models(ModelT& y, const ModelT& x, double w, int op) {
 
 void scale_model(ModelT& y, double z, int op) {
   const auto chunks = make_chunks(y);
-#pragma omp parallel for schedule(dynamic, 1)
+  const bool par = total_elems(y) >= kParallelMinElems;
+#pragma omp parallel for schedule(dynamic, 1) if (par)
   for (size_t c = 0; c < chunks.size(); ++c) {
     const Chunk ch = chunks[c];
     auto& yv = y.vars[ch.var];
@@ -161,23 +183,60 @@ FederatedModelT FederatedAverage::aggregate(const AggInput& pairs) {
 }
 
 // ---------------------------------------------------------------------------
+// With a device the `scaled` state lives in HBM (dev_ = its handle) and the
+// community model is materialised once per aggregate() call (fetch_pending),
+// since intermediate community values are overwritten before anyone sees them.
+RollingAverageBase::~RollingAverageBase() { release_device(); }
+
+void RollingAverageBase::release_device() {
+  if (dev_ >= 0) DeviceAggregator::get()->roll_free(dev_);
+  dev_ = -1;
+  pending_ = PENDING_NONE;
+}
+
 void RollingAverageBase::initialize(const ModelT* m, double w) {
-  scaled_ = *m;
+  release_device();
   z_ = w;
+  community_.num_contributors = 1;
+  if (DeviceAggregator::enabled_for(m->byte_size())) {
+    dev_ = DeviceAggregator::get()->roll_init(*m, w);
+    if (dev_ >= 0) {
+      scaled_ = ModelT();
+      pending_ = PENDING_COPY;  // reference keeps the *scaled* model here
+      return;
+    }
+  }
+  scaled_ = *m;
   scale_model(scaled_, w, 2);
   community_.model = scaled_;  // reference keeps the *scaled* model here
-  community_.num_contributors = 1;
 }
 
 void RollingAverageBase::update_scaled(const ModelT* existing, const ModelT* latest,
                                        double w_existing, double w_new) {
+  if (dev_ >= 0) {
+    auto* d = DeviceAggregator::get();
+    if (existing && !existing->empty()) d->roll_merge(dev_, *existing, w_existing, 1);
+    d->roll_merge(dev_, *latest, w_new, 0);
+    return;
+  }
   if (existing && !existing->empty()) merge_models(scaled_, *existing, w_existing, 1);
   merge_models(scaled_, *latest, w_new, 0);
 }
 
 void RollingAverageBase::update_community() {
+  if (dev_ >= 0) {
+    pending_ = PENDING_DIV;
+    return;
+  }
   community_.model = scaled_;
   scale_model(community_.model, z_, 3);
+}
+
+void RollingAverageBase::fetch_pending() {
+  if (dev_ < 0 || pending_ == PENDING_NONE) return;
+  DeviceAggregator::get()->roll_fetch(dev_, community_.model, pending_ == PENDING_COPY ? 1.0 : z_,
+                                      pending_ == PENDING_COPY ? 4 : 3);
+  pending_ = PENDING_NONE;
 }
 
 FederatedModelT FederatedStride::aggregate(const AggInput& pairs) {
@@ -194,10 +253,12 @@ FederatedModelT FederatedStride::aggregate(const AggInput& pairs) {
       community_.num_contributors += 1;
     }
   }
+  fetch_pending();
   return community_;
 }
 
 void FederatedStride::reset() {
+  release_device();
   z_ = 0.0;
   community_ = FederatedModelT();
   scaled_ = ModelT();
@@ -223,6 +284,7 @@ FederatedModelT FederatedRecency::aggregate(const AggInput& pairs) {
     update_scaled(existing, latest, w_old, w_new);
     update_community();
   }
+  fetch_pending();
   return community_;
 }
 

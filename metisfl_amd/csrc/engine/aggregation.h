@@ -54,13 +54,21 @@ class FederatedAverage : public AggregationFunction {
 };
 
 class RollingAverageBase : public AggregationFunction {
+ public:
+  ~RollingAverageBase() override;
+
  protected:
+  enum Pending { PENDING_NONE, PENDING_COPY, PENDING_DIV };
+  void release_device();
+  void fetch_pending();
   void initialize(const ModelT* m, double w);
   void update_scaled(const ModelT* existing, const ModelT* latest, double w_existing, double w_new);
   void update_community();
   ModelT scaled_;
   FederatedModelT community_;
   double z_ = 0.0;
+  int dev_ = -1;  // device-resident `scaled` state (DeviceAggregator handle)
+  Pending pending_ = PENDING_NONE;
 };
 
 class FederatedStride : public RollingAverageBase {

@@ -204,8 +204,10 @@ Dispatch Controller::resume_dispatch() {
   std::lock_guard<std::mutex> g(mu_);
   Dispatch d;
   if (!community_set_) return d;
+  const std::string fm = serialize_federated_model(community_);
+  std::map<uint32_t, Payload> cache;
   for (auto& kv : learners_)
-    d.run_tasks.emplace_back(kv.first, make_run_task(kv.first, community_, global_iteration_));
+    d.run_tasks.emplace_back(kv.first, make_run_task(kv.first, fm, global_iteration_, cache));
   return d;
 }
 

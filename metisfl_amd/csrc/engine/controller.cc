@@ -1,5 +1,7 @@
 #include "engine/controller.h"
 
+#include "engine/device_agg.h"
+
 #include <sys/resource.h>
 
 #include <chrono>
@@ -212,6 +214,7 @@ void Controller::remove_learner(const std::string& id, const std::string& token)
   std::lock_guard<std::mutex> g(mu_);
   validate(id, token);
   store_->erase({id});
+  if (auto* d = DeviceAggregator::peek()) d->drop(id);
   learners_.erase(id);
   templates_.erase(id);
 }
@@ -230,21 +233,26 @@ std::string Controller::community_model() const {
 }
 
 // ---------------------------------------------------------------------------
-std::string Controller::make_run_task(const std::string& id, const FederatedModelT& model,
-                                      uint32_t global_iteration) const {
+Payload Controller::make_run_task(const std::string& id, const std::string& fm_bytes,
+                                  uint32_t global_iteration, std::map<uint32_t, Payload>& cache) const {
+  auto it = templates_.find(id);
+  const uint32_t steps = it == templates_.end() ? 0 : it->second;
+  auto hit = cache.find(steps);
+  if (hit != cache.end()) return hit->second;
   Writer task;
   task.u64(1, global_iteration);
-  auto it = templates_.find(id);
-  task.u64(2, it == templates_.end() ? 0 : it->second);
+  task.u64(2, steps);
   task.f32(3, cfg_.percent_validation);
   Writer hp;
   hp.u64(1, cfg_.batch_size);
   if (!cfg_.optimizer_bytes.empty()) hp.bytes(2, cfg_.optimizer_bytes, true);
   Writer req;
-  req.bytes(1, serialize_federated_model(model), true);
+  req.bytes(1, fm_bytes, true);
   req.msg(2, task);
   req.msg(3, hp);
-  return req.take();
+  auto p = std::make_shared<const std::string>(req.take());
+  cache.emplace(steps, p);
+  return p;
 }
 
 std::string Controller::make_eval_task(const FederatedModelT& model) const {
@@ -269,7 +277,9 @@ void Controller::schedule_initial_task_locked(const std::string& id, Dispatch* d
   }
   auto& meta = metadata_.back();
   meta.assigned.push_back(id);
-  d->run_tasks.emplace_back(id, make_run_task(id, community_, meta.global_iteration));
+  std::map<uint32_t, Payload> cache;
+  d->run_tasks.emplace_back(
+      id, make_run_task(id, serialize_federated_model(community_), meta.global_iteration, cache));
   meta.train_submitted[id] = now_ns();
 }
 
@@ -299,6 +309,12 @@ Dispatch Controller::learner_completed_task(const std::string& id, const std::st
     metadata_[idx].train_received[id] = t0;
   }
   ModelT m = parse_model(task.bytes(1));
+  // Device residency: upload now, while the other learners are still
+  // training, so the round's aggregation reads HBM only (engine/device_agg.h).
+  // The in-memory store keeps `m`'s buffers alive at the same addresses
+  // (vector move); the Redis store re-parses on select, so it is not staged.
+  if (store_->name() == "InMemoryStore" && DeviceAggregator::enabled_for(m.byte_size()))
+    DeviceAggregator::get()->stage(id, m, cfg_.lineage);
   store_->insert(id, std::move(m));
   if (!metadata_.empty() && idx < metadata_.size())
     metadata_[idx].insertion_ms[id] = (double)(now_ns() - t0) / 1e6;
@@ -321,6 +337,7 @@ Dispatch Controller::evict_learner(const std::string& id) {
   std::lock_guard<std::mutex> g(mu_);
   if (!learners_.count(id)) throw StatusError(NOT_FOUND, "learner " + id + " not found");
   store_->erase({id});
+  if (auto* d = DeviceAggregator::peek()) d->drop(id);
   learners_.erase(id);
   templates_.erase(id);
   ++evicted_;
@@ -346,13 +363,14 @@ Dispatch Controller::run_scheduled_locked(const std::vector<std::string>& to_sch
   cm.global_iteration = task_iteration;
   community_ = cm;
   community_set_ = true;
-  community_lineage_.push_front(serialize_federated_model(cm));
+  const std::string cm_bytes = serialize_federated_model(cm);
+  community_lineage_.push_front(cm_bytes);
   while (community_lineage_.size() > cfg_.community_lineage) community_lineage_.pop_back();
   CommEval ce;
   ce.global_iteration = task_iteration;
   evaluations_.push_back(ce);
   const uint32_t ce_idx = (uint32_t)evaluations_.size() - 1;
-  const std::string eval_req = make_eval_task(cm);
+  const Payload eval_req = std::make_shared<const std::string>(make_eval_task(cm));
   for (auto& lid : to_schedule) {
     if (idx < metadata_.size()) metadata_[idx].eval_submitted[lid] = now_ns();
     d.eval_tasks.push_back({lid, eval_req, ce_idx, idx});
@@ -362,9 +380,10 @@ Dispatch Controller::run_scheduled_locked(const std::vector<std::string>& to_sch
   RoundMeta nm;
   nm.global_iteration = global_iteration_;
   nm.started_at = now_ns();
+  std::map<uint32_t, Payload> cache;
   for (auto& lid : to_schedule) {
     nm.assigned.push_back(lid);
-    d.run_tasks.emplace_back(lid, make_run_task(lid, cm, global_iteration_));
+    d.run_tasks.emplace_back(lid, make_run_task(lid, cm_bytes, global_iteration_, cache));
     nm.train_submitted[lid] = now_ns();
   }
   metadata_.push_back(nm);

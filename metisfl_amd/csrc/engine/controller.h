@@ -64,14 +64,20 @@ struct ControllerConfig {
   static ControllerConfig from_params(std::string_view controller_params_bytes);
 };
 
+// Request payloads are shared: every learner of a round receives the same
+// serialized community model, so identical requests are built ONCE and the
+// dispatch holds N references (the reference serialises one copy per learner,
+// controller.cc:594-604 -- O(N x model) host work per round).
+using Payload = std::shared_ptr<const std::string>;
+
 struct EvalTask {
   std::string learner_id;
-  std::string request;  // EvaluateModelRequest
+  Payload request;  // EvaluateModelRequest
   uint32_t comm_eval_index;
   uint32_t metadata_index;
 };
 struct Dispatch {
-  std::vector<std::pair<std::string, std::string>> run_tasks;  // (learner, RunTaskRequest)
+  std::vector<std::pair<std::string, Payload>> run_tasks;  // (learner, RunTaskRequest)
   std::vector<EvalTask> eval_tasks;
 };
 
@@ -155,8 +161,10 @@ class Controller {
 
  private:
   void validate(const std::string& id, const std::string& token) const;
-  std::string make_run_task(const std::string& id, const FederatedModelT& model,
-                            uint32_t global_iteration) const;
+  // Run-task request for learner `id`; requests that come out identical
+  // (same local-step template) share one payload through `cache`.
+  Payload make_run_task(const std::string& id, const std::string& fm_bytes, uint32_t global_iteration,
+                        std::map<uint32_t, Payload>& cache) const;
   std::string make_eval_task(const FederatedModelT& model) const;
   void schedule_initial_task_locked(const std::string& id, Dispatch* d);
   Dispatch schedule_tasks_locked(const std::string& id, uint32_t task_iteration);

@@ -1,5 +1,7 @@
 #include "he/ckks.h"
 
+#include "engine/device_agg.h"
+
 #include <sys/random.h>
 
 #include <cerrno>
@@ -714,6 +716,12 @@ std::string CKKS::weighted_average(const std::vector<std::string_view>& cts,
       wq[i * h.L + l] = (uint64_t)r;
       wqs[i * h.L + l] = shoup(wq[i * h.L + l], h.q[l]);
     }
+  }
+  // K9 on the controller's device (residency: limbs of staged models are read in place)
+  if (DeviceAggregator::enabled_for(total * 8 * v.size())) {
+    std::vector<const uint64_t*> bodies;
+    for (auto& x : v) bodies.push_back(x.body);
+    if (DeviceAggregator::get()->ckks_pwa(bodies, wq, wqs, h.q, h.L, h.N, total, o)) return out;
   }
 #pragma omp parallel for schedule(static)
   for (size_t k = 0; k < total; k += h.N) {

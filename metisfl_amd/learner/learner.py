@@ -76,6 +76,7 @@ class Learner:
         self._train_future: futures.Future | None = None
         self._cancel = threading.Event()
         self._lock = threading.Lock()
+        self._joined = threading.Event()
         self.completed_tasks = 0
 
     def host_port_identifier(self) -> str:
@@ -93,6 +94,7 @@ class Learner:
         self.learner_id, self.auth_token, status = self._client.join_federation(
             self.learner_server_entity, self._id_fp, self._token_fp, tr[0], tr[1], va[0], va[1], te[0], te[1],
             is_cls, is_reg, request_retries=3)
+        self._joined.set()
         return status
 
     def leave_federation(self):
@@ -121,6 +123,13 @@ class Learner:
             MetisLogger.error("learner %s: training task failed: %r", self.host_port_identifier(), exc)
             return
         self.completed_tasks += 1
+        # The controller dispatches a joining learner's first task from inside
+        # JoinFederation, so a fast task can finish before the join response
+        # (our id / token) has arrived: report only once it has.
+        if not self._joined.wait(timeout=120.0):
+            MetisLogger.error("learner %s: completed a task but never joined; result dropped",
+                              self.host_port_identifier())
+            return
         self._client.mark_task_completed(self.learner_id, self.auth_token, fut.result(), block=False)
 
     def run_learning_task(self, learning_task_pb, hyperparameters_pb, model_pb,

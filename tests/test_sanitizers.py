@@ -40,8 +40,15 @@ def _build(kind):
     os.makedirs(os.path.dirname(exe), exist_ok=True)
     flags = {"tsan": ["-fsanitize=thread"],
              "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fopenmp"]}[kind]
+    # the controller's device-aggregation kernels come from the in-tree native
+    # build (hipcc object); with no GPU visible the engine stays on its host rules
+    from metisfl_amd.csrc import build as native_build
+    native_build.build(["_engine"])
+    kobj = glob.glob(os.path.join(ROOT, "build", "native", "engine", "*.hip.o"))
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-pthread", f"-I{CSRC}",
-           *flags, *srcs, "-o", exe]
+           "-D__HIP_PLATFORM_AMD__", f"-I{rocm}/include", *flags, *srcs, *kobj, "-o", exe,
+           f"-L{rocm}/lib", f"-Wl,-rpath,{rocm}/lib", "-lamdhip64"]
     subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=900)
     return exe
 
