@@ -13,6 +13,7 @@
 #include "engine/policies.h"
 #include "he/ckks.h"
 #include "common/chacha20.h"
+#include <chrono>
 #include <cstring>
 
 namespace py = pybind11;
@@ -70,6 +71,7 @@ py::bytes aggregate_models(const std::string& rule, const std::vector<std::strin
 
 struct StagedModels {
   std::vector<ModelT> ms;
+  double last_aggregate_ms = 0;  // the engine call alone (no serialization)
   StagedModels(const std::vector<std::string>& ids, const std::vector<std::string>& models) {
     for (auto& s : models) ms.push_back(parse_model(s));
     py::gil_scoped_release nogil;
@@ -84,12 +86,16 @@ struct StagedModels {
     FederatedModelT out;
     {
       py::gil_scoped_release nogil;
+      const auto t0 = std::chrono::steady_clock::now();
       const size_t s = (rule == "fed_stride" && stride > 0) ? (size_t)stride : ms.size();
       for (size_t b = 0; b < ms.size(); b += s) {
         AggInput in;
         for (size_t i = b; i < std::min(ms.size(), b + s); ++i) in.push_back({{&ms[i], weights[i]}});
         out = agg->aggregate(in);
       }
+      agg->reset();
+      last_aggregate_ms =
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return B(serialize_federated_model(out));
   }
@@ -284,7 +290,8 @@ PYBIND11_MODULE(_engine, m) {
       .def(py::init<const std::vector<std::string>&, const std::vector<std::string>&>(),
            py::arg("ids"), py::arg("models"))
       .def("aggregate", &StagedModels::aggregate, py::arg("rule"), py::arg("weights"),
-           py::arg("stride") = 0);
+           py::arg("stride") = 0)
+      .def_readonly("last_aggregate_ms", &StagedModels::last_aggregate_ms);
   m.def("aggregate_models", &aggregate_models, py::arg("rule"), py::arg("models"),
         py::arg("weights"), py::arg("stride") = 0);
   py::class_<PyRecency>(m, "FedRec").def(py::init<>()).def("aggregate", &PyRecency::aggregate);

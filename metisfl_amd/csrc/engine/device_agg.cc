@@ -100,10 +100,10 @@ class Impl final : public DeviceAggregator {
  public:
   explicit Impl(int dev) : dev_(dev) {
     hip_check(hipSetDevice(dev_), "hipSetDevice");
-    hipDeviceProp_t p;
-    hip_check(hipGetDeviceProperties(&p, dev_), "hipGetDeviceProperties");
+    char name[256] = {0};
+    hip_check(hipDeviceGetName(name, sizeof(name) - 1, dev_), "hipDeviceGetName");
     stats_.device = dev_;
-    stats_.device_name = p.name;
+    stats_.device_name = name;
     hip_check(hipStreamCreateWithFlags(&upload_, hipStreamNonBlocking), "stream");
     hip_check(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking), "stream");
     for (auto& r : ring_) {
@@ -334,7 +334,7 @@ class Impl final : public DeviceAggregator {
   }
 
  private:
-  static constexpr uint64_t kChunk = 32ull << 20;
+  static constexpr uint64_t kChunk = 8ull << 20;  // small enough to pipeline copy-out with D2H
   struct Ring {
     char* host = nullptr;
     hipEvent_t done = nullptr;
@@ -488,6 +488,11 @@ class Impl final : public DeviceAggregator {
   }
 
   void upload_tiles(const Layout& lay) {
+    // the tile table of the previous call is reused when the layout repeats
+    // (every op of a round, every rolling merge)
+    if (tiles_dev_ && lay.bytes == tiles_bytes_ && lay.dtype == tiles_dtype_) return;
+    tiles_bytes_ = lay.bytes;
+    tiles_dtype_ = lay.dtype;
     std::vector<Tile> t = make_tiles(lay);
     ntiles_ = (int)t.size();
     const size_t b = std::max<size_t>(1, t.size()) * sizeof(Tile);
@@ -553,7 +558,7 @@ class Impl final : public DeviceAggregator {
     stats_.last_download_ms = ms_since(t0);
   }
 
-  static constexpr int kRing = 3;
+  static constexpr int kRing = 4;
   mutable std::mutex mu_;
   int dev_;
   hipStream_t upload_ = nullptr, compute_ = nullptr;
@@ -565,6 +570,8 @@ class Impl final : public DeviceAggregator {
   char* scratch_ = nullptr;
   uint64_t scratch_cap_ = 0;
   Tile* tiles_dev_ = nullptr;
+  std::vector<uint64_t> tiles_bytes_;
+  std::vector<int> tiles_dtype_;
   size_t tiles_cap_ = 0;
   int ntiles_ = 0;
   struct Roll {
