@@ -13,8 +13,13 @@ Reference architectures (studied, not copied):
     a sigmoid classification head.
   * ImdbLSTM -- imdb_lstm.py: embedding + LSTM + dense sigmoid.
   * IonosphereMLP -- examples/pytorch/models/mlp.py: MLP 34-10-8-1 (sigmoid).
-MelanomaFC (melanoma_fc.py) needs ImageNet-pretrained Xception weights,
-which cannot be fetched here; it is not provided.
+  * MelanomaFC -- melanoma_fc.py: a FROZEN Xception trunk (entry / 8x middle
+    / exit flow of depthwise-separable convolutions with residual 1x1
+    projections), global average pooling, Dense 8 + ReLU, Dropout 0.7,
+    Dense 1 + sigmoid, binary cross-entropy.  The reference loads
+    ImageNet weights into the trunk; none can be fetched here, so the trunk
+    is random-init unless ``trunk_weights`` names a local state dict
+    (loaded with ``torch.load(weights_only=True)``) -- parity unpinned.
 """
 from __future__ import annotations
 
@@ -119,3 +124,82 @@ def synthetic_volumes(n: int, shape, seed: int = 0, classes: int | None = None):
     else:
         y = 62.68 + 10 * x.mean(dim=tuple(range(1, x.dim()))) * 30
     return x.numpy(), y.numpy()
+
+
+# ---------------------------------------------------------------------------
+class _SepConv(nn.Sequential):
+    """Depthwise 3x3 + pointwise 1x1 (Keras SeparableConv2D, no bias) + BN."""
+
+    def __init__(self, cin, cout, relu_first=True):
+        layers = [nn.ReLU(inplace=False)] if relu_first else []
+        layers += [nn.Conv2d(cin, cin, 3, padding=1, groups=cin, bias=False),
+                   nn.Conv2d(cin, cout, 1, bias=False), nn.BatchNorm2d(cout)]
+        super().__init__(*layers)
+
+
+class _XBlock(nn.Module):
+    """Residual block: [sepconv]*reps (+ maxpool s2) + 1x1 s2 projection."""
+
+    def __init__(self, cin, cout, reps, stride, relu_first=True, grow_first=True):
+        super().__init__()
+        chans = [cin] + ([cout] * reps if grow_first else [cin] * (reps - 1) + [cout])
+        seq = [_SepConv(chans[i], chans[i + 1], relu_first=(i > 0 or relu_first)) for i in range(reps)]
+        if stride != 1:
+            seq.append(nn.MaxPool2d(3, stride, padding=1))
+        self.body = nn.Sequential(*seq)
+        self.skip = None if (cin == cout and stride == 1) else nn.Sequential(
+            nn.Conv2d(cin, cout, 1, stride=stride, bias=False), nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        return self.body(x) + (x if self.skip is None else self.skip(x))
+
+
+class Xception(nn.Module):
+    """Xception feature extractor (Chollet 2017; keras.applications.Xception
+    with include_top=False): 2048 channels at 1/32 resolution."""
+
+    def __init__(self):
+        super().__init__()
+        self.stem = nn.Sequential(nn.Conv2d(3, 32, 3, 2, bias=False), nn.BatchNorm2d(32), nn.ReLU(),
+                                  nn.Conv2d(32, 64, 3, bias=False), nn.BatchNorm2d(64), nn.ReLU())
+        blocks = [_XBlock(64, 128, 2, 2, relu_first=False), _XBlock(128, 256, 2, 2), _XBlock(256, 728, 2, 2)]
+        blocks += [_XBlock(728, 728, 3, 1) for _ in range(8)]
+        blocks += [_XBlock(728, 1024, 2, 2, grow_first=False)]
+        self.blocks = nn.Sequential(*blocks)
+        self.exit = nn.Sequential(_SepConv(1024, 1536, relu_first=False), nn.ReLU(),
+                                  _SepConv(1536, 2048, relu_first=False), nn.ReLU())
+
+    def forward(self, x):
+        return self.exit(self.blocks(self.stem(x)))
+
+
+class _MelanomaNet(nn.Module):
+    def __init__(self, trunk_weights: str | None):
+        super().__init__()
+        self.trunk = Xception()
+        if trunk_weights:
+            self.trunk.load_state_dict(torch.load(trunk_weights, map_location="cpu", weights_only=True))
+        for p in self.trunk.parameters():  # base_model.trainable = False
+            p.requires_grad_(False)
+        self.head = nn.Sequential(nn.Linear(2048, 8), nn.ReLU(), nn.Dropout(0.7), nn.Linear(8, 1))
+
+    def forward(self, x):
+        # preprocess_input: [0, 255] -> [-1, 1]; the frozen trunk keeps its BN statistics
+        self.trunk.eval()
+        f = self.trunk(x / 127.5 - 1.0)
+        return self.head(f.mean(dim=(2, 3))).squeeze(-1)
+
+
+class MelanomaFC(TorchModelDef):
+    """Binary melanoma classifier: frozen Xception + small dense head
+    (logit output; the loss applies the sigmoid)."""
+
+    def __init__(self, image_size=(1024, 1024), trunk_weights: str | None = None):
+        self.image_size = tuple(image_size)
+        self.trunk_weights = trunk_weights
+
+    def get_model(self):
+        return _MelanomaNet(self.trunk_weights)
+
+    def loss(self, outputs, targets):
+        return F.binary_cross_entropy_with_logits(outputs, targets.float())

@@ -6,9 +6,15 @@ processes through the driver with the fused HIP optimizer.
     python examples/neuroimaging.py --learners 2 --rounds 3 [--device cpu] [--dims 2]
 
 Volumes are synthetic with MRI-like shapes (no network / UK Biobank access);
---shape 91 109 91 gives the reference's full resolution.
+--shape 91 109 91 gives the reference's full resolution.  As in the
+reference (MRIScanGen.generate_tfrecord / load_dataset), every learner's
+shard is serialized once to a TFRecord file of tf.train.Example rows
+(image + label as raw bytes features) and the dataset recipe decodes it --
+here through the framework's native TFRecord reader (datasets/tfrecord.py),
+with ``--npz`` as the plain-numpy alternative.
 """
 import argparse
+import collections
 import json
 import os
 import sys
@@ -20,12 +26,29 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 from examples.models.torch_models import BrainAge2DCNN, BrainAge3DCNN, synthetic_volumes  # noqa: E402
 from examples.utils.environment_generator import EnvGen  # noqa: E402
 from metisfl_amd.driver.driver_session import DriverSession, free_port  # noqa: E402
+from metisfl_amd.datasets import tfrecord  # noqa: E402
 from metisfl_amd.models.model_dataset import ModelDatasetRegression  # noqa: E402
+
+IMAGE_COLUMN, LABEL_COLUMN = "9dof_2mm_vol", "age_at_scan"  # the reference's BrainAge columns
 
 
 def dataset_recipe(path):
+    if path.endswith(".tfrecord"):
+        cols = tfrecord.read_examples(path)
+        return ModelDatasetRegression(cols[IMAGE_COLUMN], cols[LABEL_COLUMN])
     with np.load(path, allow_pickle=False) as z:
         return ModelDatasetRegression(z["x"], z["y"])
+
+
+def save_shard(path_base: str, x, y, use_tfrecord: bool) -> str:
+    if use_tfrecord:
+        p = path_base + ".tfrecord"
+        tfrecord.write_examples(p, collections.OrderedDict(
+            [(IMAGE_COLUMN, x.astype(np.float32)), (LABEL_COLUMN, y.astype(np.float64))]))
+        return p
+    p = path_base + ".npz"
+    np.savez(p, x=x, y=y)
+    return p
 
 
 def main():
@@ -38,6 +61,7 @@ def main():
     ap.add_argument("--device", default=None)
     ap.add_argument("--gpus", type=int, default=8)
     ap.add_argument("--workdir", default="/tmp/metis_amd_neuroimaging")
+    ap.add_argument("--npz", action="store_true", help="plain .npz shards instead of TFRecords")
     a = ap.parse_args()
     shape = tuple(a.shape or ((32, 32, 32) if a.dims == 3 else (96, 96)))
     model = BrainAge3DCNN() if a.dims == 3 else BrainAge2DCNN()
@@ -50,12 +74,10 @@ def main():
     d = a.workdir + "_data"
     os.makedirs(d, exist_ok=True)
     xte, yte = synthetic_volumes(16, shape, seed=999)
-    test_p = os.path.join(d, "test.npz")
-    np.savez(test_p, x=xte, y=yte)
+    test_p = save_shard(os.path.join(d, "test"), xte, yte, not a.npz)
     for i, l in enumerate(env.learners):
         x, y = synthetic_volumes(a.samples, shape, seed=i)
-        p = os.path.join(d, f"train_{i}.npz")
-        np.savez(p, x=x, y=y)
+        p = save_shard(os.path.join(d, f"train_{i}"), x, y, not a.npz)
         l.dataset_configs.train_dataset_path = p
         l.dataset_configs.test_dataset_path = test_p
         l.grpc_servicer.port = free_port()

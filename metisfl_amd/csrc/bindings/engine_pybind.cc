@@ -7,6 +7,7 @@
 #include <pybind11/stl.h>
 
 #include "common/model.h"
+#include "common/tfrecord.h"
 #include "engine/aggregation.h"
 #include "engine/controller.h"
 #include "engine/device_agg.h"
@@ -284,6 +285,27 @@ PYBIND11_MODULE(_engine, m) {
     d["last_download_ms"] = s.last_download_ms;
     return d;
   });
+  // TFRecord container I/O (datasets/tfrecord.py builds tf.train.Example on top)
+  m.def("crc32c", [](py::bytes b) {
+    std::string_view s = b;
+    return crc32c(s.data(), s.size());
+  });
+  m.def("tfrecord_read", [](const std::string& path, bool verify) {
+    std::vector<std::string> recs;
+    {
+      py::gil_scoped_release nogil;
+      recs = tfrecord_read(path, verify);
+    }
+    py::list out;
+    for (auto& r : recs) out.append(py::bytes(r));
+    return out;
+  }, py::arg("path"), py::arg("verify") = true);
+  m.def("tfrecord_write", [](const std::string& path, const std::vector<py::bytes>& records, bool append) {
+    std::vector<std::string_view> v;
+    for (auto& r : records) v.emplace_back(r);  // views into the caller's bytes objects
+    py::gil_scoped_release nogil;
+    tfrecord_write(path, v, append);
+  }, py::arg("path"), py::arg("records"), py::arg("append") = false);
   // Benchmark / test helper: models parsed and staged exactly like
   // Controller::learner_completed_task does, then aggregated in place.
   py::class_<StagedModels>(m, "StagedModels")

@@ -326,13 +326,19 @@ SCHEMA_FILES = ["model.proto", "service_common.proto", "metis.proto", "controlle
                 "learner.proto"]
 
 
-def build_file_protos(schema_dir: str = SCHEMA_DIR) -> list[descriptor_pb2.FileDescriptorProto]:
+# Non-metisfl schemas read or written by the framework (registered under their
+# upstream file names): tf.train.Example for TFRecord datasets.
+EXTRA_FILES = {"tf_example.proto": "tensorflow/core/example/example.proto"}
+
+
+def build_file_protos(schema_dir: str = SCHEMA_DIR, files=None) -> list[descriptor_pb2.FileDescriptorProto]:
     ctxs = []
     symbols: dict[str, str] = {}
     _wkt_symbols(symbols)
-    for fn in SCHEMA_FILES:
+    files = files or {fn: f"metisfl/proto/{fn}" for fn in SCHEMA_FILES}
+    for fn, registered in files.items():
         with open(os.path.join(schema_dir, fn)) as f:
-            ctx = parse_proto(f.read(), f"metisfl/proto/{fn}")
+            ctx = parse_proto(f.read(), registered)
         _collect_types(ctx.proto, symbols)
         ctxs.append(ctx)
     for ctx in ctxs:
@@ -356,7 +362,7 @@ def load() -> descriptor_pool.DescriptorPool:
     pool = descriptor_pool.Default()
     if _LOADED:
         return pool
-    for fdp in build_file_protos():
+    for fdp in build_file_protos() + build_file_protos(files=EXTRA_FILES):
         try:
             pool.FindFileByName(fdp.name)
         except KeyError:

@@ -16,8 +16,9 @@ import tempfile
 from metisfl_amd.proto import metis_pb2
 from metisfl_amd.utils.metis_logger import MetisLogger
 
-_DEFAULT_DIR = os.environ.get("METISFL_AMD_SSL_DIR",
-                              os.path.join(tempfile.gettempdir(), "metisfl_amd_ssl_default"))
+def _default_dir() -> str:
+    return os.environ.get("METISFL_AMD_SSL_DIR",
+                          os.path.join(tempfile.gettempdir(), "metisfl_amd_ssl_default"))
 
 
 def generate_self_signed(out_dir: str, common_name: str = "localhost", days: int = 3650):
@@ -44,7 +45,7 @@ class SSLConfigurator:
 
     @classmethod
     def gen_default_certificates(cls, as_stream: bool = False):
-        cert, key = generate_self_signed(_DEFAULT_DIR)
+        cert, key = generate_self_signed(_default_dir())
         if as_stream:
             return cls.load_file_as_stream(cert), cls.load_file_as_stream(key)
         return cert, key

@@ -119,3 +119,33 @@ def test_driver_runs_rccl_data_plane_collective(tmp_path):
     assert len(lineages) == 2 and all(len(v["task_metadata"]) == 2 for v in lineages.values())
     sess.save_statistics(str(tmp_path / "experiment.json"))
     assert json.load(open(tmp_path / "experiment.json"))["federation_runtime_metadata"]
+
+
+def test_driver_session_over_tls(tmp_path, monkeypatch):
+    """EnableSSL: the controller and every learner serve TLS (self-signed
+    certificate generated on first use, reference ssl_configurator.py:16-77);
+    learners verify the controller with its public certificate, the
+    controller reaches learners with theirs; a plaintext client is refused."""
+    import grpc
+    from metisfl_amd.driver.driver_session import DriverSession, free_port
+    from metisfl_amd.proto.grpc_api import CONTROLLER_SERVICE, raw_unary
+    from metisfl_amd.utils.fedenv_parser import FederationEnvironment
+    monkeypatch.setenv("METISFL_AMD_SSL_DIR", str(tmp_path / "ssl"))
+    fe = FederationEnvironment(config=env_dict([free_port(), free_port()], ssl=True))
+    sess = DriverSession(fe, "fake", train_recipe, None, eval_recipe, working_dir=str(tmp_path / "w"),
+                         device="cpu", fake_train_delay=0.5)
+    try:
+        sess.initialize_federation()
+        assert (tmp_path / "ssl" / "server-cert.pem").exists()
+        reason = sess.monitor_federation(request_every_secs=0.3)
+        assert reason == "rounds"
+        c = fe.controller.grpc_servicer
+        ch = grpc.insecure_channel(f"{c.hostname}:{c.port}")
+        with pytest.raises(grpc.RpcError):
+            raw_unary(ch, CONTROLLER_SERVICE, "GetServicesHealthStatus")(b"", timeout=5)
+        ch.close()
+    finally:
+        sess.shutdown_federation(timeout=60)
+    stats = sess.get_federation_statistics()
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert max(int(m.get("global_iteration", 0)) for m in md) >= 3

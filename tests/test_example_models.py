@@ -68,3 +68,25 @@ def test_convergence_plots_from_experiment(tmp_path):
     rows = main([str(p), "--out", str(tmp_path / "plots")])
     assert rows[0]["round_s"] == 2.5 and abs(rows[0]["test_accuracy_mean"] - 0.6) < 1e-9
     assert (tmp_path / "plots" / "rounds.csv").exists()
+
+
+def test_melanoma_fc_frozen_trunk_trains_head(tmp_path):
+    """MelanomaFC (melanoma_fc.py): only the dense head trains; the Xception
+    trunk is frozen and can be loaded from a local state dict."""
+    import torch
+
+    import examples.models.torch_models as TM
+    from metisfl_amd.models.torch_ops import TorchModelOps
+    trunk = TM.Xception()
+    torch.save(trunk.state_dict(), tmp_path / "xception.pt")
+    d = TM.MelanomaFC((64, 64), trunk_weights=str(tmp_path / "xception.pt"))
+    rng = np.random.default_rng(0)
+    x = (rng.random((8, 3, 64, 64)) * 255).astype(np.float32)
+    y = rng.integers(0, 2, 8)
+    ops = TorchModelOps(d, device="cpu")
+    before = {n: p.detach().clone() for n, p in ops.model.named_parameters()}
+    task, hp = _task(2, lr=0.1)
+    assert ops.train_model(ModelDataset(x=x, y=y, size=len(x)), task, hp) is not None
+    changed = {n for n, p in ops.model.named_parameters() if not torch.equal(p, before[n])}
+    assert changed and all(n.startswith("head.") for n in changed)
+    assert sum(p.numel() for p in ops.model.trunk.parameters()) > 20_000_000
