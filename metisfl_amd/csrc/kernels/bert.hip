@@ -27,6 +27,10 @@
 
 #include "kernels/bert.h"
 
+#ifndef MFL_BERT_DBG
+#define MFL_BERT_DBG 0  // timing experiments only (compile-time)
+#endif
+
 namespace mfl {
 
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -184,7 +188,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
       }
     }
   }
-  if (a.dbg & 2) return;
+  if constexpr (MFL_BERT_DBG & 2) return;
   // Block reduction of the column partials.  The two half-waves of a wave own
   // the same columns: fold them with one cross-half shuffle, write the wave's
   // row of red[w] with 16-B stores, then every thread sums its columns over
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
     for (int c = threadIdx.x; c < H; c += 256)
       red[0][q][c] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
   __syncthreads();
-  if (a.dbg & 1) return;
+  if constexpr (MFL_BERT_DBG & 1) return;
   for (int c = threadIdx.x; c < H; c += 256) {
     atomicAdd(a.dgamma + c, red[0][0][c]);
     atomicAdd(a.dbeta + c, red[0][1][c]);

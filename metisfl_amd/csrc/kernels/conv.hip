@@ -49,6 +49,10 @@
 #include "kernels/conv.h"
 #include "kernels/lds_tiles.h"
 
+#ifndef MFL_CONV_DBG
+#define MFL_CONV_DBG 0  // timing experiments only: bit0 skip MFMAs, bit1 skip operand DMA (compile-time: a runtime test split the k-loop into basic blocks)
+#endif
+
 namespace mfl {
 
 constexpr int kBK = 64;      // k-tile (elements); one 128-byte bf16 row per operand row
@@ -316,7 +320,7 @@ __device__ __forceinline__ void conv_gemm_body(const ConvArgs& a, const BlkCoord
   const int b_pch = lane % B_CPR;
 
   auto issue = [&](int kt, int stage) {
-    if (a.dbg & 2) return;
+    if constexpr (MFL_CONV_DBG & 2) return;
     uint8_t* st = smem + stage * STAGE;
     const int kb = kbeg + kt * BK;
     {
@@ -382,7 +386,7 @@ __device__ __forceinline__ void conv_gemm_body(const ConvArgs& a, const BlkCoord
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int stage) {
-    if (a.dbg & 1) return;
+    if constexpr (MFL_CONV_DBG & 1) return;
     const uint8_t* As = smem + stage * STAGE;
     const uint8_t* Bs = As + A_BYTES;
 #pragma unroll
@@ -550,7 +554,7 @@ __device__ __forceinline__ void conv_wgrad_body(const ConvArgs& a, float* __rest
   const int PQ = g.P * g.Q;
 
   auto issue = [&](int kt, int stage) {
-    if (a.dbg & 2) return;
+    if constexpr (MFL_CONV_DBG & 2) return;
     uint8_t* st = smem + stage * STAGE;
     const int mb = mbeg + kt * BK;
 #pragma unroll
@@ -576,7 +580,7 @@ __device__ __forceinline__ void conv_wgrad_body(const ConvArgs& a, float* __rest
 #pragma unroll
     for (int jj = 0; jj < TN; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int stage) {
-    if (a.dbg & 1) return;
+    if constexpr (MFL_CONV_DBG & 1) return;
     const uint8_t* As = smem + stage * STAGE;
     const uint8_t* Bs = As + T_BYTES;
 #pragma unroll

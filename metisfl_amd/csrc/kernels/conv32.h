@@ -36,7 +36,6 @@ struct Conv32Args {
   int par_mc;
   FastDiv dc, dq, dpq;  // / C, / Q, / (P*Q)
   int reps;             // BN accumulator replicas ([reps][2][Ng]; workgroup b adds into replica b % reps)
-  int dbg;              // timing experiments only (MFL_C32_DBG): bit0 skip MFMAs, bit1 skip operand DMA
 };
 
 struct BnBwdFusion32 {

@@ -39,6 +39,7 @@
 //    the write-through slabs in slice order: bitwise deterministic).
 //  * Stride-2 dgrad runs parity-class decomposed (PAR), as in conv.hip.
 #include <type_traits>
+#include <utility>
 
 #include "kernels/common.h"
 #include "kernels/conv32.h"
@@ -71,45 +72,70 @@ __device__ __forceinline__ uint32_t oob_or(bool ok, uint32_t off) { return off |
 // fp32 [row][kBK] tile: 16-B chunk ch of `row` (swizzled)
 __device__ __forceinline__ int rk_off(int row, int ch) { return row * kRowB + ((ch ^ swz_b128<kRowB>(row)) << 4); }
 
-// k-loop: LDS ring of 3 stages (DMA 2-3 tiles ahead) + register double
+#ifndef MFL_C32_DBG
+#define MFL_C32_DBG 0  // timing experiments only: bit0 skip MFMAs, bit1 skip operand DMA
+#endif
+#ifndef MFL_C32_GENERIC
+#define MFL_C32_GENERIC 0  // 1: every shape on the generic address path (A/B experiments)
+#endif
+
+template <int V>
+using IC = std::integral_constant<int, V>;
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(IC<I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// k-loop: LDS ring of NS stages (DMA 2-3 tiles ahead) + register double
 // buffer of MFMA fragments (LDS reads 1 tile ahead).  Iteration kt:
 //   wait own DMA of tile kt+1, wait own fragment reads of tile kt, barrier
 //   (=> every wave's tile kt+1 landed AND every wave holds tile kt's
-//   fragments in registers, so stage kt%3 is free) -> issue the DMA of tile
-//   kt+3 into stage kt%3 -> issue the fragment reads of tile kt+1 -> MFMAs of
-//   tile kt.  The reads and the DMA address math then run UNDER the MFMAs of
-//   the same wave (sched_group_barrier interleave) instead of in front of
-//   them: with one wave per SIMD the LDS read latency before each tile's first
-//   MFMA was the largest exposed stall of the straight loop (45-50% of the
-//   fp32 MFMA peak).  The loop is unrolled by two so each register set is
-//   static.  DMAs past the last tile use out-of-range offsets (zero fill, no
-//   memory traffic): the body stays one basic block.
+//   fragments in registers, so stage kt%NS is free) -> issue the DMA of tile
+//   kt+NS into stage kt%NS -> issue the fragment reads of tile kt+1 -> MFMAs
+//   of tile kt.  The reads and the DMA address math run UNDER the MFMAs of the
+//   same wave (sched_group_barrier interleave).
+// The loop is unrolled by lcm(NS, 2) so that the ring stage AND the fragment
+// register set of every step are compile-time constants: LDS addresses fold
+// into ds_read / M0 immediates and the loop carries no per-tile VALU address
+// math.  That matters more for fp32 than for bf16: the f32 MFMA shares the
+// VALU datapath (measured: a VALU wave beside an MFMA wave on one SIMD runs
+// no faster than both serialised, profiles/r2/mfma_valu_coissue_probe.log),
+// so every VALU instruction in the loop is MFMA time lost.  DMAs past the
+// last tile use out-of-range offsets (zero fill, no memory traffic).
+// `issue` must be called for tiles 0, 1, 2, ... in order (it may carry
+// scalar iterator state).
 template <int NS, int L, typename Issue, typename Read, typename Mma>
 __device__ __forceinline__ void ring_loop(int nk, Issue& issue, Read& read, Mma& mma) {
   static_assert((NS - 1) * L <= 63, "vmcnt is a 6-bit counter");
-#pragma unroll
-  for (int u = 0; u < NS; ++u) issue(u, u);
+  static_for<NS>([&](auto u) { issue(decltype(u)::value, u); });
   wait_vmcnt<(NS - 1) * L>();  // tile 0
   lds_barrier();
-  read(0, std::integral_constant<int, 0>{});
-  int st = 0;  // stage of tile kt
-  auto step = [&](int kt, auto cur) {
-    constexpr int C = decltype(cur)::value;
+  read(IC<0>{}, IC<0>{});
+  auto step = [&](int kt, auto stc, auto setc) {
+    constexpr int S = decltype(stc)::value, C = decltype(setc)::value;
+    constexpr int NXT = S == NS - 1 ? 0 : S + 1;
     wait_vmcnt<(NS - 2) * L>();            // tile kt+1 landed (kt+2.. may fly)
     __builtin_amdgcn_s_waitcnt(0xC07F);    // lgkmcnt(0): tile kt's fragments in registers
     lds_barrier();
-    const int nst = st == NS - 1 ? 0 : st + 1;
-    issue(kt + NS, st);
-    read(nst, std::integral_constant<int, 1 - C>{});
-    mma(cur);
-    st = nst;
+    issue(kt + NS, stc);
+    read(IC<NXT>{}, IC<1 - C>{});
+    mma(setc);
   };
+  constexpr int P = NS % 2 == 0 ? NS : 2 * NS;
   int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    step(kt, std::integral_constant<int, 0>{});
-    step(kt + 1, std::integral_constant<int, 1>{});
-  }
-  if (kt < nk) step(kt, std::integral_constant<int, 0>{});
+  for (; kt + P <= nk; kt += P)
+    static_for<P>([&](auto j) {
+      constexpr int J = decltype(j)::value;
+      step(kt + J, IC<J % NS>{}, IC<J % 2>{});
+    });
+  static_for<P - 1>([&](auto j) {
+    constexpr int J = decltype(j)::value;
+    if (kt + J < nk) step(kt + J, IC<J % NS>{}, IC<J % 2>{});
+  });
   wait_vmcnt<0>();  // the trailing (zero-fill) DMAs land before smem is reused
   __builtin_amdgcn_s_waitcnt(0xC07F);
 }
@@ -222,7 +248,14 @@ __device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, int m0, int
 //   fwd:   A = im2col(X) [M][R*S*C],  B[k][n] = W[n][k]   (both [row][k] tiles)
 //   dgrad: A = stride-aware gather of dY [M = N*H*W][R*S*Co],
 //          B[k = (r,s,co)][n = ci] = W[co][r][s][ci]      ([k][n] tile, b32 reads)
-template <int BM, int BN, bool DGRAD, int KS, int ST, bool PAR, int NS>
+// GEN selects the generic per-element address path (channel counts that are
+// not a multiple of the k-tile -- the 8-channel stem -- and the masked
+// stride-2 dgrad gather); otherwise a k-tile lies inside ONE filter tap, so
+// the tap (r, s) and channel offset are scalar per-tile state, each DMA row
+// keeps its tap-(0,0) address and a 9-bit tap-validity mask from the
+// prologue, and a DMA costs ~4 VALU (bit test, add, select) instead of ~20
+// including quarter-rate integer multiplies.
+template <int BM, int BN, bool DGRAD, int KS, int ST, bool PAR, int NS, bool GEN>
 __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int A_BYTES = BM * kRowB;
@@ -232,6 +265,7 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
   constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 MFMA tiles per wave
   constexpr int BRB = BN * 4;                // dgrad B row bytes
   constexpr int B_RPI = 1024 / BRB, B_CPR = BRB / 16;
+  static_assert(GEN || !(DGRAD && ST > 1 && !PAR), "masked stride-2 dgrad needs the generic path");
   const ConvGeom& g = a.g;
   const auto rsA = make_rsrc(a.src, a.src_bytes);
   const auto rsB = make_rsrc(a.wgt, a.wgt_bytes);
@@ -242,13 +276,13 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
   const int kbeg = blockIdx.z * a.kchunk;
-  int cls = 0, r0 = 0, s0 = 0, ns = 1, dh = 0, dw = 0, kc_end = g.K;
+  int cls = 0, r0 = 0, s0 = 0, nr = KS, ns = KS, dh = 0, dw = 0, kc_end = g.K;
   if constexpr (PAR) {
     cls = m0 / a.par_mc;
     const int qh = cls >> 1, qw = cls & 1;
     r0 = (qh + g.pad) & 1;
     s0 = (qw + g.pad) & 1;
-    const int nr = (KS - r0 + 1) >> 1;
+    nr = (KS - r0 + 1) >> 1;
     ns = (KS - s0 + 1) >> 1;
     dh = (qh + g.pad - r0) >> 1;
     dw = (qw + g.pad - s0) >> 1;
@@ -289,61 +323,139 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
     if (m >= g.M) a_y0[i] = -(1 << 28);  // forces the OOB offset
   }
 
-  auto issue = [&](int kt, int stage) {
-    if (a.dbg & 2) return;
-    uint8_t* st = smem + stage * STAGE;
-    const int kb = kbeg + kt * kBK;
-    {
-      const int k = kb + a_kc;
-      const int rs = fdiv(k, a.dc);
-      const int c = k - rs * g.C;
-      const int r = PAR ? (ns == 2 ? rs >> 1 : rs) : rs / KS;
-      const int s = PAR ? rs - r * ns : rs - r * KS;
-      const bool kv = k < kend;
+  // ---- fast path state (GEN == false) ----
+  // per DMA row: byte address of tap (0,0) + this lane's k chunk, and the
+  // validity of every tap (bit r*ns + s; fwd reads (y0 + r, x0 + s), dgrad
+  // (y0 - r, x0 - s))
+  int a_base[ACH];
+  uint32_t a_vm[ACH];
+  // B operand: fwd W[n][k] rows (per lane n, k chunk a_kc); dgrad W^T [k][n]
+  int b_base[BCH];
+  bool b_ok[BCH];
+  // scalar per-tile iterator: tap (tr, ts) of the tile, channel offset c0
+  int tr = 0, ts = 0, c0 = 0;
+  if constexpr (!GEN) {
+    const int sgn = DGRAD ? -1 : 1;
 #pragma unroll
-      for (int i = 0; i < ACH; ++i) {
-        int iy, ix;
-        bool ok;
-        if (PAR) {
-          iy = a_y0[i] - r;
-          ix = a_x0[i] - s;
-          ok = kv & (iy >= 0) & (ix >= 0);
-        } else if (DGRAD) {
-          const int ty = a_y0[i] - r, tx = a_x0[i] - s;
-          ok = kv & (ty >= 0) & (tx >= 0);
-          if (ST > 1) ok = ok & ((ty % ST) == 0) & ((tx % ST) == 0);
-          iy = ty / ST;
-          ix = tx / ST;
-        } else {
-          iy = a_y0[i] + r;
-          ix = a_x0[i] + s;
-          ok = kv & (iy >= 0) & (ix >= 0);
+    for (int i = 0; i < ACH; ++i) {
+      a_base[i] = (int)(((uint32_t)a_nb[i] + ((uint32_t)a_y0[i] * g.W + (uint32_t)a_x0[i]) * g.C + a_kc) * 4u);
+      uint32_t vm = 0;
+      for (int r = 0; r < nr; ++r)
+        for (int s2 = 0; s2 < ns; ++s2) {
+          const int iy = a_y0[i] + sgn * r, ix = a_x0[i] + sgn * s2;
+          const bool ok = (iy >= 0) & (iy < g.H) & (ix >= 0) & (ix < g.W);
+          vm |= (uint32_t)ok << (r * ns + s2);
         }
-        ok = ok & (iy < g.H) & (ix < g.W);
-        const uint32_t off = oob_or(ok, (uint32_t)(a_nb[i] + (iy * g.W + ix) * g.C + c) * 4u);
-        dma16(rsA, off, st + (wave + 4 * i) * 1024);
-      }
+      a_vm[i] = vm;
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
-      uint32_t off;
       if constexpr (DGRAD) {
         const int row = (wave + 4 * i) * B_RPI + lane / B_CPR;  // k within the tile
         const int n = n0 + (lane % B_CPR) * 4;
-        const int kr = kb + row;
-        int rs = fdiv(kr, a.dc);
-        const int ko = kr - rs * g.C;
-        if (PAR) {  // class tap index -> kernel tap (r0 + 2 j_r, s0 + 2 j_s)
-          const int jr = ns == 2 ? rs >> 1 : rs;
-          rs = (r0 + 2 * jr) * KS + s0 + 2 * (rs - jr * ns);
-        }
-        off = oob_or((kr < kend) & (n < g.Ng), (uint32_t)((ko * KS * KS + rs) * g.Ng + n) * 4u);
+        b_base[i] = (row * KS * KS * g.Ng + n) * 4;
+        b_ok[i] = n < g.Ng;
       } else {
         const int n = n0 + lrow + 4 * kRPI * i;
-        const int k = kb + a_kc;
-        off = oob_or((k < kend) & (n < g.Ng), (uint32_t)(n * g.K + k) * 4u);
+        b_base[i] = (n * g.K + a_kc) * 4;
+        b_ok[i] = n < g.Ng;
       }
-      dma16(rsB, off, st + A_BYTES + (wave + 4 * i) * 1024);
+    }
+    const int rs0 = kbeg / g.C;  // scalar, once
+    c0 = kbeg - rs0 * g.C;
+    tr = rs0 / ns;
+    ts = rs0 - tr * ns;
+  }
+
+  auto issue = [&](int kt, auto stc) {
+    if constexpr (MFL_C32_DBG & 2) return;
+    constexpr int S = decltype(stc)::value;
+    uint8_t* st = smem + S * STAGE;
+    const int kb = kbeg + kt * kBK;
+    if constexpr (!GEN) {
+      const bool kv = kb < kend;
+      const int tap = kv ? tr * ns + ts : 31;  // bit 31 is never set: every row OOB
+      const int sp = (tr * g.W + ts) * g.C;   // tap offset (elements)
+      const int aoff = ((DGRAD ? -sp : sp) + c0) * 4;
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        const bool ok = (a_vm[i] >> tap) & 1u;
+        dma16(rsA, ok ? (uint32_t)a_base[i] + (uint32_t)aoff : kOOB, st + (wave + 4 * i) * 1024);
+      }
+      int boff;
+      if constexpr (DGRAD) {
+        const int rsk = PAR ? (r0 + 2 * tr) * KS + s0 + 2 * ts : tr * KS + ts;  // kernel tap
+        boff = (c0 * KS * KS + rsk) * g.Ng * 4;
+      } else {
+        boff = kb * 4;
+      }
+#pragma unroll
+      for (int i = 0; i < BCH; ++i)
+        dma16(rsB, (b_ok[i] & kv) ? (uint32_t)(b_base[i] + boff) : kOOB, st + A_BYTES + (wave + 4 * i) * 1024);
+      // advance the scalar iterator by one k-tile (a tile never straddles a
+      // tap); selects, not branches: a branch here would cut the step into
+      // basic blocks the MFMA interleave cannot cross
+      c0 += kBK;
+      const int wrap = c0 == g.C;
+      c0 = wrap ? 0 : c0;
+      ts += wrap;
+      const int wrap2 = ts == ns;
+      ts = wrap2 ? 0 : ts;
+      tr += wrap2;
+      return;
+    } else {
+      {
+        const int k = kb + a_kc;
+        const int rs = fdiv(k, a.dc);
+        const int c = k - rs * g.C;
+        const int r = PAR ? (ns == 2 ? rs >> 1 : rs) : rs / KS;
+        const int s = PAR ? rs - r * ns : rs - r * KS;
+        const bool kv = k < kend;
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) {
+          int iy, ix;
+          bool ok;
+          if (PAR) {
+            iy = a_y0[i] - r;
+            ix = a_x0[i] - s;
+            ok = kv & (iy >= 0) & (ix >= 0);
+          } else if (DGRAD) {
+            const int ty = a_y0[i] - r, tx = a_x0[i] - s;
+            ok = kv & (ty >= 0) & (tx >= 0);
+            if (ST > 1) ok = ok & ((ty % ST) == 0) & ((tx % ST) == 0);
+            iy = ty / ST;
+            ix = tx / ST;
+          } else {
+            iy = a_y0[i] + r;
+            ix = a_x0[i] + s;
+            ok = kv & (iy >= 0) & (ix >= 0);
+          }
+          ok = ok & (iy < g.H) & (ix < g.W);
+          const uint32_t off = oob_or(ok, (uint32_t)(a_nb[i] + (iy * g.W + ix) * g.C + c) * 4u);
+          dma16(rsA, off, st + (wave + 4 * i) * 1024);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < BCH; ++i) {
+        uint32_t off;
+        if constexpr (DGRAD) {
+          const int row = (wave + 4 * i) * B_RPI + lane / B_CPR;  // k within the tile
+          const int n = n0 + (lane % B_CPR) * 4;
+          const int kr = kb + row;
+          int rs = fdiv(kr, a.dc);
+          const int ko = kr - rs * g.C;
+          if (PAR) {  // class tap index -> kernel tap (r0 + 2 j_r, s0 + 2 j_s)
+            const int jr = ns == 2 ? rs >> 1 : rs;
+            rs = (r0 + 2 * jr) * KS + s0 + 2 * (rs - jr * ns);
+          }
+          off = oob_or((kr < kend) & (n < g.Ng), (uint32_t)((ko * KS * KS + rs) * g.Ng + n) * 4u);
+        } else {
+          const int n = n0 + lrow + 4 * kRPI * i;
+          const int k = kb + a_kc;
+          off = oob_or((k < kend) & (n < g.Ng), (uint32_t)(n * g.K + k) * 4u);
+        }
+        dma16(rsB, off, st + A_BYTES + (wave + 4 * i) * 1024);
+      }
     }
   };
 
@@ -382,16 +494,16 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
   // the MFMAs (it otherwise re-uses one register set per group and re-exposes
   // the LDS latency before every group)
   f32x4 fa[2][kBK / 8][TM], fb[2][kBK / 8][TN];  // fragment double buffer
-  auto read = [&](int stage, auto set) {
+  auto read = [&](auto stc, auto set) {
     constexpr int S = decltype(set)::value;
-    const uint8_t* As = smem + stage * STAGE;
+    const uint8_t* As = smem + decltype(stc)::value * STAGE;
     const uint8_t* Bs = As + A_BYTES;
 #pragma unroll
     for (int grp = 0; grp < kBK / 8; ++grp) load(As, Bs, grp, fa[S][grp], fb[S][grp]);
   };
   auto mma = [&](auto set) {
     constexpr int S = decltype(set)::value;
-    if (a.dbg & 1) return;
+    if constexpr (MFL_C32_DBG & 1) return;
 #pragma unroll
     for (int grp = 0; grp < kBK / 8; ++grp)
 #pragma unroll
@@ -483,7 +595,13 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
 // wgrad:  dW[co][j] = sum_m dY[m][co] * im2col(X)[m][j],  j = (r, s, c)
 // Both operands are row-contiguous in memory: tiles [32 m][BM co] and
 // [32 m][BN j], b32 fragment reads, MFMA (g, e) slot h reduces m = 8g + 4h + e.
-template <int BM, int BN, int KS, int ST, int NS>
+// GEN: generic per-element pixel decomposition.  Fast path (Q divides 32 and
+// the 32-pixel k-tile either divides P*Q or is a multiple of it, M % 32 == 0
+// -- every ResNet-18 CIFAR layer): a k-tile's pixel m = kb + row splits into a
+// scalar part (image n_s, output row oy_s: per-tile iterator) and a per-lane
+// constant (row within the tile), so the im2col address of X is one add and
+// its bounds test one compare per DMA.
+template <int BM, int BN, int KS, int ST, int NS, bool GEN>
 __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, float* __restrict__ dw, int atomic) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int A_BYTES = kBK * BM * 4;
@@ -514,27 +632,73 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
   const int jr = rs / KS, js = rs - (rs / KS) * KS;
   const int PQ = g.P * g.Q;
 
-  auto issue = [&](int kt, int stage) {
-    if (a.dbg & 2) return;
-    uint8_t* st = smem + stage * STAGE;
-    const int kb = kbeg + kt * kBK;
+  // fast path: lane-constant parts of both operand addresses
+  int a_base[ACH], b_base[BCH], b_iy[BCH];
+  bool b_ok[BCH];
+  int n_s = 0, oy_s = 0;  // scalar pixel iterator of the tile start
+  if constexpr (!GEN) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      const int m = kb + (wave + 4 * i) * A_RPI + lane / A_CPR;
-      const uint32_t off = oob_or((m < kend) & a_ok, (uint32_t)(m * g.Ng + a_co) * 4u);
-      dma16(rsA, off, st + (wave + 4 * i) * 1024);
+      const int row = (wave + 4 * i) * A_RPI + lane / A_CPR;
+      a_base[i] = (row * g.Ng + a_co) * 4;
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
-      const int m = kb + (wave + 4 * i) * B_RPI + lane / B_CPR;
-      const int n = fdiv(m, a.dpq);
-      const int rem = m - n * PQ;
-      const int oy = fdiv(rem, a.dq);
-      const int ox = rem - oy * g.Q;
-      const int iy = oy * ST - g.pad + jr, ix = ox * ST - g.pad + js;
-      const bool ok = (m < kend) & jok & (iy >= 0) & (iy < g.H) & (ix >= 0) & (ix < g.W);
-      const uint32_t off = oob_or(ok, (uint32_t)(((n * g.H + iy) * g.W + ix) * g.C + jc) * 4u);
-      dma16(rsB, off, st + A_BYTES + (wave + 4 * i) * 1024);
+      const int row = (wave + 4 * i) * B_RPI + lane / B_CPR;
+      const int n_l = PQ >= kBK ? 0 : row / PQ;
+      const int oy_l = (row % PQ) / g.Q, ox_l = row % g.Q;
+      const int iy_l = oy_l * ST - g.pad + jr, ix = ox_l * ST - g.pad + js;
+      b_iy[i] = iy_l;
+      b_ok[i] = jok & (ix >= 0) & (ix < g.W);
+      b_base[i] = (int)((((uint32_t)n_l * g.H + (uint32_t)iy_l) * g.W + (uint32_t)ix) * g.C + jc) * 4;
+    }
+    n_s = kbeg / PQ;  // scalar, once
+    oy_s = (kbeg - n_s * PQ) / g.Q;
+  }
+
+  auto issue = [&](int kt, auto stc) {
+    if constexpr (MFL_C32_DBG & 2) return;
+    uint8_t* st = smem + decltype(stc)::value * STAGE;
+    const int kb = kbeg + kt * kBK;
+    if constexpr (!GEN) {
+      const bool kv = kb < kend;
+      const int aoff = kb * g.Ng * 4;
+#pragma unroll
+      for (int i = 0; i < ACH; ++i)
+        dma16(rsA, (a_ok & kv) ? (uint32_t)(a_base[i] + aoff) : kOOB, st + (wave + 4 * i) * 1024);
+      const int oys = oy_s * ST;
+      const int boff = (n_s * g.H + oys) * g.W * g.C * 4;
+#pragma unroll
+      for (int i = 0; i < BCH; ++i) {
+        const bool ok = b_ok[i] & kv & ((uint32_t)(b_iy[i] + oys) < (uint32_t)g.H);
+        dma16(rsB, ok ? (uint32_t)b_base[i] + (uint32_t)boff : kOOB, st + A_BYTES + (wave + 4 * i) * 1024);
+      }
+      // advance 32 pixels (selects, see the gemm kernel)
+      const int big = PQ >= kBK;
+      const int oy_n = oy_s + (big ? kBK / g.Q : 0);
+      const int wrap = oy_n == g.P;
+      oy_s = wrap ? 0 : oy_n;
+      n_s += big ? wrap : kBK / PQ;
+      return;
+    } else {
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        const int m = kb + (wave + 4 * i) * A_RPI + lane / A_CPR;
+        const uint32_t off = oob_or((m < kend) & a_ok, (uint32_t)(m * g.Ng + a_co) * 4u);
+        dma16(rsA, off, st + (wave + 4 * i) * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < BCH; ++i) {
+        const int m = kb + (wave + 4 * i) * B_RPI + lane / B_CPR;
+        const int n = fdiv(m, a.dpq);
+        const int rem = m - n * PQ;
+        const int oy = fdiv(rem, a.dq);
+        const int ox = rem - oy * g.Q;
+        const int iy = oy * ST - g.pad + jr, ix = ox * ST - g.pad + js;
+        const bool ok = (m < kend) & jok & (iy >= 0) & (iy < g.H) & (ix >= 0) & (ix < g.W);
+        const uint32_t off = oob_or(ok, (uint32_t)(((n * g.H + iy) * g.W + ix) * g.C + jc) * 4u);
+        dma16(rsB, off, st + A_BYTES + (wave + 4 * i) * 1024);
+      }
     }
   };
 
@@ -557,16 +721,16 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
     }
   };
   f32x4 fa[2][kBK / 8][TM], fb[2][kBK / 8][TN];
-  auto read = [&](int stage, auto set) {
+  auto read = [&](auto stc, auto set) {
     constexpr int S = decltype(set)::value;
-    const float* As = reinterpret_cast<const float*>(smem + stage * STAGE);
-    const float* Bs = reinterpret_cast<const float*>(smem + stage * STAGE + A_BYTES);
+    const float* As = reinterpret_cast<const float*>(smem + decltype(stc)::value * STAGE);
+    const float* Bs = reinterpret_cast<const float*>(smem + decltype(stc)::value * STAGE + A_BYTES);
 #pragma unroll
     for (int grp = 0; grp < kBK / 8; ++grp) load(As, Bs, grp, fa[S][grp], fb[S][grp]);
   };
   auto mma = [&](auto set) {
     constexpr int S = decltype(set)::value;
-    if (a.dbg & 1) return;
+    if constexpr (MFL_C32_DBG & 1) return;
 #pragma unroll
     for (int grp = 0; grp < kBK / 8; ++grp)
 #pragma unroll
@@ -636,16 +800,28 @@ size_t gemm_lds(int bm, int bn) {
   return ring > epi ? ring : epi;
 }
 
-template <int BM, int BN, bool DG, int KS, int ST, bool PAR>
-void launch_t(const Conv32Args& a, dim3 grid, hipStream_t s) {
+template <int BM, int BN, bool DG, int KS, int ST, bool PAR, bool GEN>
+void launch_t2(const Conv32Args& a, dim3 grid, hipStream_t s) {
   constexpr int NS = stages_for(BM, BN);
   static bool init = false;
   const size_t lds = gemm_lds(BM, BN);
   if (!init) {
-    set_lds(&conv32_gemm_kernel<BM, BN, DG, KS, ST, PAR, NS>, lds);
+    set_lds(&conv32_gemm_kernel<BM, BN, DG, KS, ST, PAR, NS, GEN>, lds);
     init = true;
   }
-  conv32_gemm_kernel<BM, BN, DG, KS, ST, PAR, NS><<<grid, 256, lds, s>>>(a);
+  conv32_gemm_kernel<BM, BN, DG, KS, ST, PAR, NS, GEN><<<grid, 256, lds, s>>>(a);
+}
+// the fast address path needs every k-tile inside one filter tap
+template <int BM, int BN, bool DG, int KS, int ST, bool PAR>
+void launch_t(const Conv32Args& a, dim3 grid, hipStream_t s) {
+  if constexpr (DG && ST > 1 && !PAR) {
+    launch_t2<BM, BN, DG, KS, ST, PAR, true>(a, grid, s);
+  } else {
+    if (a.g.C % kBK == 0 && a.kchunk % kBK == 0 && !(MFL_C32_GENERIC))
+      launch_t2<BM, BN, DG, KS, ST, PAR, false>(a, grid, s);
+    else
+      launch_t2<BM, BN, DG, KS, ST, PAR, true>(a, grid, s);
+  }
 }
 
 template <int BM, int BN, bool DG>
@@ -785,7 +961,6 @@ void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const 
   a.accum = accum ? 1 : 0;
   a.par_mc = dgrad ? p.par_mc : 0;
   fill_shifts(a);
-  a.dbg = env_int("MFL_C32_DBG", 0);
   const dim3 grid(cdiv(g.M, p.bm), cdiv(g.Ng, p.bn), p.splits);
   const int key = p.bm * 1000 + p.bn;
   switch (key) {
@@ -796,16 +971,26 @@ void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const 
 }
 
 namespace {
-template <int BM, int BN, int KS, int ST>
-void launch_w(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStream_t s) {
+template <int BM, int BN, int KS, int ST, bool GEN>
+void launch_w2(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStream_t s) {
   constexpr int NS = stages_for(BM, BN);
   static bool init = false;
   const size_t lds = (size_t)NS * kBK * (BM + BN) * 4;
   if (!init) {
-    set_lds(&conv32_wgrad_kernel<BM, BN, KS, ST, NS>, lds);
+    set_lds(&conv32_wgrad_kernel<BM, BN, KS, ST, NS, GEN>, lds);
     init = true;
   }
-  conv32_wgrad_kernel<BM, BN, KS, ST, NS><<<grid, 256, lds, s>>>(a, dw, atomic);
+  conv32_wgrad_kernel<BM, BN, KS, ST, NS, GEN><<<grid, 256, lds, s>>>(a, dw, atomic);
+}
+// fast path: Q | 32, the 32-pixel k-tile divides P*Q or is a multiple of it
+template <int BM, int BN, int KS, int ST>
+void launch_w(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStream_t s) {
+  const ConvGeom& g = a.g;
+  const int pq = g.P * g.Q;
+  const bool fast = g.Q > 0 && kBK % g.Q == 0 && (pq % kBK == 0 || kBK % pq == 0) && g.M % kBK == 0 &&
+                    a.kchunk % kBK == 0 && !(MFL_C32_GENERIC);
+  if (fast) launch_w2<BM, BN, KS, ST, false>(a, grid, dw, atomic, s);
+  else launch_w2<BM, BN, KS, ST, true>(a, grid, dw, atomic, s);
 }
 template <int BM, int BN>
 void launch_w_geom(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStream_t s) {
@@ -827,7 +1012,6 @@ void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, c
   a.wgt_bytes = range_bytes((int64_t)g.N * g.H * g.W * g.C);
   a.kchunk = p.kchunk;
   fill_shifts(a);
-  a.dbg = env_int("MFL_C32_DBG", 0);
   const dim3 grid(cdiv(g.Ng, p.bm), cdiv(g.K, p.bn), p.splits);
   const int atomic = (accumulate || p.splits > 1) ? 1 : 0;
   const int key = p.bm * 1000 + p.bn;

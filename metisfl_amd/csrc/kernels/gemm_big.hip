@@ -32,6 +32,10 @@
 #include "kernels/gemm.h"
 #include "kernels/lds_tiles.h"
 
+#ifndef MFL_GB_DBG
+#define MFL_GB_DBG 0  // timing experiments only: bit0 skip MFMAs, bit1 skip operand DMA, bit2 skip the output stage (compile-time)
+#endif
+
 namespace mfl {
 
 struct BigGemmArgs {
@@ -275,13 +279,13 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto issue = [&](int kt, int stage) {
-    if (p.dbg & 2) return;
+    if constexpr (MFL_GB_DBG & 2) return;
     uint8_t* st = smem + stage * C::STAGE;
     stage_operand<AT, BK>(rsA, p.lda, m0, (kt0 + kt) * BK, st, wave, lane);
     stage_operand<BT, BK>(rsB, p.ldb, n0, (kt0 + kt) * BK, st + C::TILE, wave, lane);
   };
   auto compute = [&](int stage) {
-    if (p.dbg & 1) return;
+    if constexpr (MFL_GB_DBG & 1) return;
     const uint8_t* As = smem + stage * C::STAGE;
     const uint8_t* Bs = As + C::TILE;
     if constexpr (kGbPinOrder && BK == 64 && !AT && !BT) {
@@ -470,7 +474,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
 
   // half-tile h (0 A0, 1 B0, 2 B1, 3 A1) of k-tile kt into ring slot kt & 1
   auto stage = [&](int h, int kt) {
-    if (p.dbg & 2) return;
+    if constexpr (MFL_GB_DBG & 2) return;
     uint8_t* dst = smem + ((kt & 1) * 4 + h) * PP_HALF;
     const bool v = kt < nk;
     const int k0 = (kt0 + (v ? kt : 0)) * 64;
@@ -528,7 +532,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
   auto mfma_section = [&](int mi, int ni) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    if (!(p.dbg & 1)) mfma_quadrant(mi, ni);
+    if constexpr (!(MFL_GB_DBG & 1)) mfma_quadrant(mi, ni);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     lds_barrier();
@@ -579,7 +583,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
   wait_vm<0>();                // trailing out-of-range half-tiles land before the LDS is reused
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   lds_barrier();
-  if (p.dbg & 4) {  // timing experiment: no output stage (keep the accumulators live)
+  if constexpr (MFL_GB_DBG & 4) {  // timing experiment: no output stage (keep the accumulators live)
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll

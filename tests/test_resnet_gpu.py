@@ -63,26 +63,32 @@ def test_resnet_gradients_gpu_vs_cpu_reference():
 
 
 def test_graph_replay_equals_eager():
+    """One captured-hipGraph update equals the eager update up to the
+    summation-order noise of the atomics (BN statistics, split-K wgrad); over
+    several lr-0.05 updates of this tiny model that noise is amplified
+    chaotically (ReLU masks flip: 2e-7 -> 8e-5 -> 2e-3 measured in BOTH
+    graph-vs-graph and eager-vs-eager pairs, scripts/graph_diag.py), so the
+    multi-step check only bounds the divergence."""
     x, y = _data(64, 1)
     a = _make("cuda", lr=0.05)
     b = _make("cuda", lr=0.05)
-    c = _make("cuda", lr=0.05)
     da = a.make_dataset(x, y, shuffle=False)
     db = b.make_dataset(x, y, shuffle=False)
-    dc = c.make_dataset(x, y, shuffle=False)
-    for _ in range(3):
+    a._train_body(da)
+    b.train_steps(db, 1)  # captured hipGraph
+    torch.cuda.synchronize()
+    assert int(a.state.step.cpu()) == int(b.state.step.cpu()) == 1
+    diff1 = float((a.state.model32 - b.state.model32).abs().max())
+    scale = float(a.state.model32.abs().max())
+    for _ in range(2):
         a._train_body(da)
-        c._train_body(dc)
-    b.train_steps(db, 3)  # captured hipGraph
+    b.train_steps(db, 2, 1)
     torch.cuda.synchronize()
     assert int(a.state.step.cpu()) == int(b.state.step.cpu()) == 3
-    # atomics (BN statistics, split-K wgrad) make the summation order vary
-    # run to run, and three lr-0.05 steps amplify it: the graph must agree
-    # with eager as well as eager agrees with itself (calibrated, floor 1e-3)
-    noise = float((a.state.model32 - c.state.model32).abs().max())
-    diff = float((a.state.model32 - b.state.model32).abs().max())
-    print(f"graph-vs-eager max |diff| {diff:.2e}, eager-vs-eager {noise:.2e}")
-    assert diff <= max(1e-3, 8 * noise), (diff, noise)
+    diff3 = float((a.state.model32 - b.state.model32).abs().max())
+    print(f"graph-vs-eager max |diff| after 1 step {diff1:.2e}, after 3 steps {diff3:.2e} (|w| max {scale:.2f})")
+    assert diff1 <= 1e-5 * max(1.0, scale), diff1
+    assert diff3 <= 2e-2 * max(1.0, scale), diff3
 
 
 def test_full_width_resnet18_trains():
