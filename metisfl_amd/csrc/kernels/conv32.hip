@@ -857,6 +857,35 @@ int conv32_counter_slots(const ConvGeom& g, const ConvPlan& p) {
   return cdiv(g.M, p.bm) * cdiv(g.Ng, p.bn);
 }
 
+// Measured plans (scripts/conv32_bench.py --sweep, profiles/r2/c32_sweep_v2.log)
+// for the flagship shapes -- ResNet-18 on CIFAR-10 at batch 32 -- where the
+// throughput model below picks a plan >= 5% slower than the best one (it
+// over-prefers 128x64 tiles for dgrad / wgrad and splits 1x1 convs that are
+// latency-bound).  Keyed on the ORIGINAL convolution (dgrad geometry is role
+// swapped), like a vendor library's performance database.
+struct TunedPlan {
+  int mode, n, h, w, c, co, r, stride, bm, bn, splits;
+};
+constexpr TunedPlan kTuned[] = {
+    {0, 32, 8, 8, 256, 256, 3, 1, 64, 64, 4},   {0, 32, 8, 8, 256, 512, 1, 2, 64, 64, 1},
+    {1, 32, 32, 32, 64, 64, 3, 1, 64, 64, 1},   {1, 32, 32, 32, 64, 128, 3, 2, 64, 64, 1},
+    {1, 32, 32, 32, 64, 128, 1, 2, 64, 64, 1},  {1, 32, 8, 8, 256, 256, 3, 1, 64, 64, 4},
+    {2, 32, 8, 8, 256, 256, 3, 1, 64, 64, 3},   {2, 32, 8, 8, 256, 512, 3, 2, 64, 64, 2},
+    {2, 32, 4, 4, 512, 512, 3, 1, 64, 64, 2},
+};
+static void tuned_plan(const ConvGeom& g, int mode, int& bm, int& bn, int& sp) {
+  const bool dg = mode == 1;
+  const int h = dg ? g.P : g.H, w = dg ? g.Q : g.W, c = dg ? g.Ng : g.C, co = dg ? g.C : g.Ng;
+  for (const TunedPlan& t : kTuned)
+    if (t.mode == mode && t.n == g.N && t.h == h && t.w == w && t.c == c && t.co == co && t.r == g.R &&
+        t.stride == g.stride) {
+      bm = t.bm;
+      bn = t.bn;
+      sp = t.splits;
+      return;
+    }
+}
+
 static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
   const int rows = mode == 2 ? g.Ng : g.M;
   const int cols = mode == 2 ? g.K : g.Ng;
@@ -866,7 +895,8 @@ static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
     par = true;
     kred = ((g.R + 1) / 2) * ((g.S + 1) / 2) * g.C;  // the largest parity class
   }
-  const int fb = env_int("MFL_C32_BM", 0), fn = env_int("MFL_C32_BN", 0), fs = env_int("MFL_C32_SPLIT", 0);
+  int fb = env_int("MFL_C32_BM", 0), fn = env_int("MFL_C32_BN", 0), fs = env_int("MFL_C32_SPLIT", 0);
+  if (!fb && !fn && !fs) tuned_plan(g, mode, fb, fn, fs);
   const double clk = 2.4e3;  // cycles per us
   ConvPlan best;
   double best_t = 1e30;

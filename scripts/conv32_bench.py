@@ -76,7 +76,7 @@ def main():
                     f"{us:7.1f} us {flop / us / 1e6:6.1f} TF")
             if a.sweep:
                 best = (us, p.bm, p.bn, p.splits)
-                for bm, bn, sp in itertools.product((64, 128), (64, 128), (1, 2, 3, 4, 6, 8, 12, 16, 24, 32)):
+                for bm, bn, sp in itertools.product((64, 128), (64, 128), (1, 2, 3, 4, 6, 7, 8, 12, 14, 16, 24, 28, 32, 48, 64)):
                     set_plan(bm, bn, sp)
                     q = K.conv_plan(mode, shp, dev, torch.float32)
                     if q.kchunk == 0 or q.splits != sp or q.bm != bm or q.bn != bn:
