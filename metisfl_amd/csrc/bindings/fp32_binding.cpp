@@ -196,6 +196,7 @@ void bn32_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, to
     TORCH_CHECK(acc.has_value() && acc->defined(), "train-mode BN needs the statistics accumulator");
     a.acc = acc_ptr(*acc, C);
     a.reps = reps_of(*acc, C);
+    TORCH_CHECK(a.reps <= 8, "at most 8 BN accumulator replicas");
   }
   a.gamma = fp(gamma);
   a.beta = fp(beta);
@@ -238,6 +239,7 @@ void bn32_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tenso
   if (dbeta.has_value() && dbeta->defined()) { check_pc(*dbeta, C, "dbeta"); a.dbeta = fp(*dbeta); }
   a.acc = acc_ptr(acc, C);
   a.reps = reps_of(acc, C);
+  TORCH_CHECK(a.reps <= 8, "at most 8 BN accumulator replicas");
   a.gamma = fp(gamma);
   a.mean = fp(mean);
   a.invstd = fp(invstd);

@@ -71,6 +71,29 @@ void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_
   bn32_stats_kernel<<<dim3(blocks_for(M, C), gy), 256, 0, s>>>(x, M, C, acc, reps > 0 ? reps : 1);
 }
 
+constexpr int kMaxReps = 8;  // replicas summed per channel (layers.py uses 8 on the fp32 GPU path)
+
+// Sum of a channel's replicas: every load issued before the first add (a
+// runtime-bound loop serialised one memory round trip per replica).
+__device__ __forceinline__ void rep_sums(const double* acc, int reps, int C, int c, double& s0, double& s1) {
+  double a[kMaxReps], b[kMaxReps];
+#pragma unroll
+  for (int r = 0; r < kMaxReps; ++r) {
+    a[r] = r < reps ? acc[(int64_t)r * 2 * C + c] : 0.0;
+    b[r] = r < reps ? acc[(int64_t)r * 2 * C + C + c] : 0.0;
+  }
+  s0 = 0.0;
+  s1 = 0.0;
+#pragma unroll
+  for (int r = 0; r < kMaxReps; ++r) {
+    s0 += a[r];
+    s1 += b[r];
+  }
+}
+
+// Main loops: when C / 4 divides 256 the grid stride is a multiple of C / 4,
+// so a lane's channels never change -- its coefficients live in registers
+// (no LDS read and no 64-bit modulo per vector).
 template <bool RES, bool RELU>
 __global__ __launch_bounds__(256) void bn32_apply_kernel(BnFwdArgs32 a, int64_t nvec) {
   extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
@@ -88,11 +111,8 @@ __global__ __launch_bounds__(256) void bn32_apply_kernel(BnFwdArgs32 a, int64_t 
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     double mu, var;
     if (a.train) {
-      double s0 = 0.0, s1 = 0.0;
-      for (int r = 0; r < a.reps; ++r) {
-        s0 += a.acc[(int64_t)r * 2 * C + c];
-        s1 += a.acc[(int64_t)r * 2 * C + C + c];
-      }
+      double s0, s1;
+      rep_sums(a.acc, a.reps, C, c, s0, s1);
       mu = s0 * inv_m;
       var = s1 * inv_m - mu * mu;
       if (var < 0.0) var = 0.0;
@@ -116,15 +136,21 @@ __global__ __launch_bounds__(256) void bn32_apply_kernel(BnFwdArgs32 a, int64_t 
   }
   __syncthreads();
   const int tpr = C / 4;
+  const bool fixed = (256 % tpr) == 0;  // lane channels constant over the grid stride
+  int cb = fixed ? (int)(threadIdx.x % (unsigned)tpr) * 4 : 0;
+  float4 sc = *reinterpret_cast<const float4*>(coef + cb);
+  float4 sh = *reinterpret_cast<const float4*>(coef + C + cb);
   for (; i < nvec; i += stride) {
     const float4 xc = xv, rc = rv;
     if (i + stride < nvec) {
       xv = X[i + stride];
       if (RES) rv = R[i + stride];
     }
-    const int cb = (int)(i % tpr) * 4;
-    const float4 sc = *reinterpret_cast<const float4*>(coef + cb);
-    const float4 sh = *reinterpret_cast<const float4*>(coef + C + cb);
+    if (!fixed) {
+      cb = (int)(i % tpr) * 4;
+      sc = *reinterpret_cast<const float4*>(coef + cb);
+      sh = *reinterpret_cast<const float4*>(coef + C + cb);
+    }
     float4 v = make_float4(fmaf(xc.x, sc.x, sh.x), fmaf(xc.y, sc.y, sh.y), fmaf(xc.z, sc.z, sh.z),
                            fmaf(xc.w, sc.w, sh.w));
     if (RES) {
@@ -213,11 +239,8 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
   }
   const double inv_m = 1.0 / (double)a.M;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    double s = 0.0, q = 0.0;
-    for (int r = 0; r < a.reps; ++r) {
-      s += a.acc[(int64_t)r * 2 * C + c];
-      q += a.acc[(int64_t)r * 2 * C + C + c];
-    }
+    double s, q;
+    rep_sums(a.acc, a.reps, C, c, s, q);
     sc[c] = a.gamma[c] * a.invstd[c];
     sc[C + c] = (float)(s * inv_m);
     sc[2 * C + c] = (float)(q * inv_m);
@@ -230,6 +253,17 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
   }
   __syncthreads();
   const int tpr = C / 4;
+  const bool fixed = (256 % tpr) == 0;
+  int cb = fixed ? (int)(threadIdx.x % (unsigned)tpr) * 4 : 0;
+  float4 k1, mg, mx, mu, is;
+  auto load_coef = [&]() {
+    k1 = *reinterpret_cast<const float4*>(sc + cb);
+    mg = *reinterpret_cast<const float4*>(sc + C + cb);
+    mx = *reinterpret_cast<const float4*>(sc + 2 * C + cb);
+    mu = *reinterpret_cast<const float4*>(sc + 3 * C + cb);
+    is = *reinterpret_cast<const float4*>(sc + 4 * C + cb);
+  };
+  load_coef();
   for (; i < nvec; i += stride) {
     float4 g = gv;
     const float4 xc = xv, yc = yv;
@@ -238,7 +272,10 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
       xv = X[i + stride];
       if (MASK) yv = Y[i + stride];
     }
-    const int cb = (int)(i % tpr) * 4;
+    if (!fixed) {
+      cb = (int)(i % tpr) * 4;
+      load_coef();
+    }
     if (MASK) {
       g.x = yc.x > 0.f ? g.x : 0.f;
       g.y = yc.y > 0.f ? g.y : 0.f;
@@ -246,16 +283,12 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
       g.w = yc.w > 0.f ? g.w : 0.f;
       if (WRITE_DYM) reinterpret_cast<float4*>(a.dy_masked)[i] = g;
     }
-    const float gg[4] = {g.x, g.y, g.z, g.w};
-    const float xx[4] = {xc.x, xc.y, xc.z, xc.w};
-    float o[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c = cb + k;
-      const float xh = (xx[k] - sc[3 * C + c]) * sc[4 * C + c];
-      o[k] = sc[c] * (gg[k] - sc[C + c] - xh * sc[2 * C + c]);
-    }
-    reinterpret_cast<float4*>(a.dx)[i] = make_float4(o[0], o[1], o[2], o[3]);
+    float4 o;
+    o.x = k1.x * (g.x - mg.x - ((xc.x - mu.x) * is.x) * mx.x);
+    o.y = k1.y * (g.y - mg.y - ((xc.y - mu.y) * is.y) * mx.y);
+    o.z = k1.z * (g.z - mg.z - ((xc.z - mu.z) * is.z) * mx.z);
+    o.w = k1.w * (g.w - mg.w - ((xc.w - mu.w) * is.w) * mx.w);
+    reinterpret_cast<float4*>(a.dx)[i] = o;
   }
 }
 
