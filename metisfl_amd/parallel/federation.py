@@ -51,7 +51,15 @@ META_FIELDS = ("num_training_examples", "completed_batches", "ms_per_batch", "ms
 @dataclass
 class FederationConfig:
     protocol: str = "synchronous"          # synchronous | semi_synchronous
-    aggregation: str = "fed_avg"           # fed_avg (fed_stride == fed_avg on one all-reduce)
+    # fed_avg | fed_stride.  FedStride (federated_stride.cc:6-64) exists to bound
+    # the AGGREGATOR's memory: the reference controller folds `stride_length`
+    # learner models at a time into a rolling scaled sum instead of holding
+    # all N.  On the collective data plane no process ever holds more than its
+    # own model plus ring chunks (reduce-scatter + all-gather), so the bound
+    # holds for any N and the rolling sum sum_i(w_i x_i) / sum_i(w_i) is ONE
+    # scale + all-reduce; the result equals the engine's FedStride up to fp32
+    # summation order (tests/test_collective_federation.py::test_fed_stride_*).
+    aggregation: str = "fed_avg"
     scaling_factor: str = "NUM_TRAINING_EXAMPLES"
     stride_length: int = 0
     batch_size: int = 32

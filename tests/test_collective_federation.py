@@ -37,7 +37,9 @@ def _worker(rank, world, port, out_dir, mode):
                           seed=rank)
     cfg = FederationConfig(protocol="semi_synchronous" if mode == "semi" else "synchronous", batch_size=4,
                            local_epochs=1, semi_sync_lambda=2.0, evaluate_test=False,
-                           secure_aggregation=mode == "secure")
+                           secure_aggregation=mode == "secure",
+                           aggregation="fed_stride" if mode == "stride" else "fed_avg",
+                           stride_length=1 if mode == "stride" else 0)
     sizes = [8 + 4 * r for r in range(world)]
     engine = CollectiveController(cfg, sizes) if rank == 0 else None
     fed = CollectiveFederation(comm, net, ds, cfg, engine=engine)
@@ -93,6 +95,28 @@ def test_sync_fedavg_two_ranks_matches_host_reference(tmp_path):
     eng = res[0]["engine"]
     assert eng["rounds"] == 2 and eng["learners"] == 2 and eng["quantifiers"] > 0
     assert sorted(eng["lineage"].values()) == [2, 2]
+
+
+def test_fed_stride_three_ranks_matches_engine_fedstride(tmp_path):
+    """FedStride (stride 1: the most memory-bounded rolling fold) on the
+    collective path equals the native engine's host FedStride over the same
+    local models and weights (up to fp32 summation order)."""
+    from metisfl_amd import _engine as E
+    from metisfl_amd.proto import model_pb2
+    from metisfl_amd.utils.tensor_codec import model_from_arrays, model_to_arrays
+    res = _run(tmp_path, "stride", world=3)
+    w = res[0]["rounds"][0]["weights"]
+    assert np.allclose(w, np.array([8, 12, 16]) / 36)
+    for r in (0, 1):
+        gi = r + 1
+        comm = [np.load(tmp_path / f"community_r{gi}_rank{k}.npy") for k in range(3)]
+        assert all(np.array_equal(comm[0], c) for c in comm[1:])
+        locs = [np.load(tmp_path / f"local_r{r}_rank{k}.npy") for k in range(3)]
+        models = [model_from_arrays(["flat"], [l]).SerializeToString() for l in locs]
+        fm = model_pb2.FederatedModel()
+        fm.ParseFromString(E.aggregate_models("fed_stride", models, [float(x) for x in w], 1))
+        ref = model_to_arrays(fm.model)[1][0]
+        assert np.allclose(comm[0], ref, rtol=1e-5, atol=1e-6)
 
 
 def test_secure_ckks_aggregation_two_ranks(tmp_path):
