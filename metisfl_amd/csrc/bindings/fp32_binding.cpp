@@ -146,6 +146,54 @@ void conv32_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, c10::opti
   run(g, true, dy, w, dx, ws, nullptr, accumulate, fuse ? &f : nullptr);
 }
 
+// A layer's dgrad (+ fused consumer-BN reductions) and wgrad (dw zero on
+// entry or a running sum) -- one paired launch when both plans allow it.
+void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, torch::Tensor w, torch::Tensor dx,
+                          c10::optional<torch::Tensor> ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co,
+                          int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate,
+                          c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
+                          c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
+                          c10::optional<torch::Tensor> bn_acc) {
+  const auto gf = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
+  const auto gd = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
+  check_f32(x, (int64_t)N * H * W * C, "x");
+  check_f32(dy, (int64_t)gf.M * Co, "dy");
+  check_f32(dw, (int64_t)Co * R * S * C, "dw");
+  check_f32(w, (int64_t)Co * R * S * C, "w");
+  check_f32(dx, (int64_t)N * H * W * C, "dx");
+  mfl::BnBwdFusion32 f;
+  const bool fuse = bn_acc.has_value() && bn_acc->defined();
+  if (fuse) {
+    TORCH_CHECK(bn_z.has_value() && bn_mean.has_value() && bn_invstd.has_value(), "bn fusion operands");
+    check_f32(*bn_z, dx.numel(), "bn_z");
+    if (bn_y.has_value() && bn_y->defined()) check_f32(*bn_y, dx.numel(), "bn_y");
+    check_f32(*bn_mean, C, "bn_mean");
+    check_f32(*bn_invstd, C, "bn_invstd");
+    f.z = fp(*bn_z);
+    f.y = opt_ptr<float>(bn_y);
+    f.mean = fp(*bn_mean);
+    f.invstd = fp(*bn_invstd);
+    f.acc = stats_ptr(bn_acc, C);
+    f.reps = reps_of(*bn_acc, C);
+  }
+  const auto pd = mfl::plan_conv32(gd, 1);
+  const auto pw = mfl::plan_conv32(gf, 2);
+  float* slab = nullptr;
+  int* counters = nullptr;
+  if (pd.splits > 1) {
+    TORCH_CHECK(ws.has_value() && ws->defined(), "split-K workspace required");
+    check_f32(*ws, ws_floats(gd, pd), "workspace", false);
+    counters = reinterpret_cast<int*>(ws->data_ptr<float>());
+    slab = ws->data_ptr<float>() + kCounterWords;
+  }
+  if (mfl::launch_conv32_bwd_pair(gd, pd, gf, pw, fp(dy), fp(w), fp(dx), slab, counters, accumulate,
+                                  fuse ? &f : nullptr, fp(x), fp(dw), cur_stream(dx)))
+    return;
+  mfl::launch_conv32_wgrad(gf, pw, fp(x), fp(dy), fp(dw), true, cur_stream(dw));
+  mfl::launch_conv32_gemm(gd, true, pd, fp(dy), fp(w), fp(dx), slab, counters, nullptr, accumulate,
+                          fuse ? &f : nullptr, cur_stream(dx));
+}
+
 void conv32_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t N, int64_t H, int64_t W, int64_t C,
                   int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate) {
   const auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
@@ -306,6 +354,7 @@ void register_fp32(pybind11::module& m) {
   m.def("conv32_forward", &conv32_forward);
   m.def("conv32_dgrad", &conv32_dgrad);
   m.def("conv32_wgrad", &conv32_wgrad);
+  m.def("conv32_backward_pair", &conv32_backward_pair);
   m.def("bn32_stats", &bn32_stats);
   m.def("bn32_apply", &bn32_apply);
   m.def("bn32_backward", &bn32_backward);

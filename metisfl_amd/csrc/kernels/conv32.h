@@ -61,5 +61,12 @@ void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const 
 // split plan requires dw zeroed by the caller.
 void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, const float* dy, float* dw,
                          bool accumulate, hipStream_t s);
+// dgrad (gd, pd; role-swapped geometry) + wgrad (gf = the forward geometry,
+// pw; dw must hold zeros or a running sum: slices add atomically) of one
+// layer in one launch.  Returns false (nothing launched) when the two plans
+// do not both run 64x64 tiles on the fast address paths.
+bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGeom& gf, const ConvPlan& pw,
+                            const float* dy, const float* w, float* dx, float* ysplit, int* counters, bool accum,
+                            const BnBwdFusion32* bnb, const float* x, float* dw, hipStream_t s);
 
 }  // namespace mfl

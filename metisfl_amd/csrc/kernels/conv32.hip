@@ -38,6 +38,7 @@
 //    with fp64 atomics.  Split-K slices reduce in-launch (last arriver sums
 //    the write-through slabs in slice order: bitwise deterministic).
 //  * Stride-2 dgrad runs parity-class decomposed (PAR), as in conv.hip.
+#include <algorithm>
 #include <type_traits>
 #include <utility>
 
@@ -62,6 +63,16 @@ __device__ __forceinline__ f32x16 mfma_f32(float a, float b, const f32x16& c) {
 }
 __device__ __forceinline__ int fdiv(int x, const FastDiv& f) {
   return (int)((__umulhi((uint32_t)x, f.m) >> f.sh) + ((uint32_t)x & f.id));
+}
+
+// A workgroup's coordinates in its own GEMM's grid.  The stand-alone kernels
+// take them from the hardware; the paired dgrad+wgrad launch maps one
+// hardware grid onto the two GEMMs' grids.
+struct Blk {
+  int x, y, z, gx, gy, gz;
+};
+__device__ __forceinline__ Blk hw_blk() {
+  return Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z};
 }
 
 // DMA offset, or past every buffer range when !ok -- bitwise, so hipcc keeps
@@ -172,8 +183,8 @@ __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
 
 // Output tile [BM][BN + 4] fp32 in LDS -> y (float4 rows), + fused channel sums.
 template <int BM, int BN>
-__device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, int m0, int n0, const float* tile,
-                                                float* red) {
+__device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, const Blk& b, int m0, int n0,
+                                                const float* tile, float* red) {
   constexpr int TST = BN + 4;
   constexpr int CPR = BN / 4;      // float4 per row
   constexpr int RPP = 256 / CPR;   // rows per pass
@@ -223,7 +234,7 @@ __device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, int m0, int
   }
   if (!stats) return;
   // replica of this workgroup (b % 8 = the XCD under round-robin placement)
-  stats += (int64_t)((blockIdx.x + blockIdx.y * gridDim.x + blockIdx.z * gridDim.x * gridDim.y) % a.reps) * 2 * g.Ng;
+  stats += (int64_t)((b.x + b.y * b.gx + b.z * b.gx * b.gy) % a.reps) * 2 * g.Ng;
   reinterpret_cast<float4*>(red)[2 * t] = s;
   reinterpret_cast<float4*>(red)[2 * t + 1] = q;
   __syncthreads();
@@ -256,8 +267,7 @@ __device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, int m0, int
 // prologue, and a DMA costs ~4 VALU (bit test, add, select) instead of ~20
 // including quarter-rate integer multiplies.
 template <int BM, int BN, bool DGRAD, int KS, int ST, bool PAR, int NS, bool GEN>
-__global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+__device__ __forceinline__ void conv32_gemm_body(const Conv32Args& a, const Blk& blk, uint8_t* smem) {
   constexpr int A_BYTES = BM * kRowB;
   constexpr int STAGE = A_BYTES + BN * kRowB;
   constexpr int ACH = BM * kBK / 1024;  // DMA instructions per wave per k-tile (1 KiB each)
@@ -273,9 +283,9 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  const int kbeg = blockIdx.z * a.kchunk;
+  const int m0 = blk.x * BM;
+  const int n0 = blk.y * BN;
+  const int kbeg = blk.z * a.kchunk;
   int cls = 0, r0 = 0, s0 = 0, nr = KS, ns = KS, dh = 0, dw = 0, kc_end = g.K;
   if constexpr (PAR) {
     cls = m0 / a.par_mc;
@@ -532,16 +542,16 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
         tile[rl * TST + wn * (BN / 2) + 32 * j + li] = acc[i][j][e];
       }
   __syncthreads();
-  const int splits = gridDim.z;
+  const int splits = blk.gz;
   if (splits > 1) {
     // in-launch split-K (write-through slabs + arrival ticket; conv.hip)
     constexpr int F = BM * BN / 1024;  // float4 per thread
     constexpr int C4 = BN / 4;
-    const int tile_id = blockIdx.y * gridDim.x + blockIdx.x;
-    const int ntiles = gridDim.x * gridDim.y;
+    const int tile_id = blk.y * blk.gx + blk.x;
+    const int ntiles = blk.gx * blk.gy;
     const int64_t zstride = (int64_t)ntiles * BM * BN * 4;
     const auto rsS = make_rsrc(a.ysplit + (int64_t)tile_id * (BM * BN), 0x7FFFFFF0u);
-    const uint32_t zoff = (uint32_t)(blockIdx.z * zstride);
+    const uint32_t zoff = (uint32_t)(blk.z * zstride);
 #pragma unroll
     for (int u = 0; u < F; ++u) {
       const int f = t + 256 * u;
@@ -570,7 +580,7 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
       for (int u = 0; u < F; ++u) {
         const int f = t + 256 * u;
         float4 r;
-        if (z == (int)blockIdx.z) {
+        if (z == blk.z) {
           r = *reinterpret_cast<const float4*>(tile + (f / C4) * TST + (f % C4) * 4);
         } else {
           const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rsS, (int)(z * zstride + f * 16), 0, 16);
@@ -588,7 +598,13 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
     }
     __syncthreads();
   }
-  tile_epilogue32<BM, BN>(a, m0, n0, tile, red);
+  tile_epilogue32<BM, BN>(a, blk, m0, n0, tile, red);
+}
+
+template <int BM, int BN, bool DGRAD, int KS, int ST, bool PAR, int NS, bool GEN>
+__global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  conv32_gemm_body<BM, BN, DGRAD, KS, ST, PAR, NS, GEN>(a, hw_blk(), smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -602,8 +618,8 @@ __global__ __launch_bounds__(256, 2) void conv32_gemm_kernel(Conv32Args a) {
 // constant (row within the tile), so the im2col address of X is one add and
 // its bounds test one compare per DMA.
 template <int BM, int BN, int KS, int ST, int NS, bool GEN>
-__global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, float* __restrict__ dw, int atomic) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+__device__ __forceinline__ void conv32_wgrad_body(const Conv32Args& a, const Blk& blk, uint8_t* smem,
+                                                  float* __restrict__ dw, int atomic) {
   constexpr int A_BYTES = kBK * BM * 4;
   constexpr int STAGE = A_BYTES + kBK * BN * 4;
   constexpr int ARB = BM * 4, A_RPI = 1024 / ARB, A_CPR = ARB / 16;
@@ -617,9 +633,9 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int i0 = blockIdx.x * BM;
-  const int j0 = blockIdx.y * BN;
-  const int kbeg = blockIdx.z * a.kchunk;
+  const int i0 = blk.x * BM;
+  const int j0 = blk.y * BN;
+  const int kbeg = blk.z * a.kchunk;
   const int kend = min(g.M, kbeg + a.kchunk);
   const int nk = max(0, (kend - kbeg + kBK - 1) / kBK);
 
@@ -761,6 +777,34 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
         else *p = acc[i][j][e];
       }
     }
+}
+
+template <int BM, int BN, int KS, int ST, int NS, bool GEN>
+__global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, float* __restrict__ dw, int atomic) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  conv32_wgrad_body<BM, BN, KS, ST, NS, GEN>(a, hw_blk(), smem, dw, atomic);
+}
+
+// A layer's backward in ONE launch: blocks [0, nd) run the dgrad GEMM (with
+// its fused consumer-BN reductions), the rest the wgrad GEMM.  Both read dY,
+// neither waits for the other; as two launches each is a few hundred
+// workgroups whose tail waves leave CUs idle and the second pays a launch
+// boundary.  dgrad blocks first: it is on the critical path (the bf16
+// twin measured dgrad-first / wgrad-first / alternating 502 / 551 / 508 ms).
+template <int KS, int ST, bool PAR, int NS>
+__global__ __launch_bounds__(256, 2) void conv32_bwd_pair_kernel(Conv32Args ad, Conv32Args aw, float* __restrict__ dw,
+                                                                 int atomic, int nd, int gdx, int gdy, int gwx,
+                                                                 int gwy, int gwz) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int b = blockIdx.x;
+  if (b < nd) {
+    const Blk k{b % gdx, (b / gdx) % gdy, b / (gdx * gdy), gdx, gdy, nd / (gdx * gdy)};
+    conv32_gemm_body<64, 64, true, KS, ST, PAR, NS, false>(ad, k, smem);
+  } else {
+    const int w = b - nd;
+    const Blk k{w % gwx, (w / gwx) % gwy, w / (gwx * gwy), gwx, gwy, gwz};
+    conv32_wgrad_body<64, 64, KS, ST, NS, false>(aw, k, smem, dw, atomic);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -966,9 +1010,9 @@ static void fill_shifts(Conv32Args& a) {
   a.dpq = make_fdiv(a.g.P * a.g.Q);
 }
 
-void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const float* src, const float* wgt,
-                        float* y, float* ysplit, int* counters, double* stats, bool accum,
-                        const BnBwdFusion32* bnb, hipStream_t s, int stats_reps) {
+static Conv32Args gemm_args(const ConvGeom& g, bool dgrad, const ConvPlan& p, const float* src, const float* wgt,
+                            float* y, float* ysplit, int* counters, double* stats, bool accum,
+                            const BnBwdFusion32* bnb, int stats_reps) {
   Conv32Args a{};
   a.g = g;
   a.src = src;
@@ -991,6 +1035,13 @@ void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const 
   a.accum = accum ? 1 : 0;
   a.par_mc = dgrad ? p.par_mc : 0;
   fill_shifts(a);
+  return a;
+}
+
+void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const float* src, const float* wgt,
+                        float* y, float* ysplit, int* counters, double* stats, bool accum,
+                        const BnBwdFusion32* bnb, hipStream_t s, int stats_reps) {
+  const Conv32Args a = gemm_args(g, dgrad, p, src, wgt, y, ysplit, counters, stats, accum, bnb, stats_reps);
   const dim3 grid(cdiv(g.M, p.bm), cdiv(g.Ng, p.bn), p.splits);
   const int key = p.bm * 1000 + p.bn;
   switch (key) {
@@ -1001,6 +1052,12 @@ void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const 
 }
 
 namespace {
+bool wgrad_fast(const ConvGeom& g, int kchunk) {
+  const int pq = g.P * g.Q;
+  return g.Q > 0 && kBK % g.Q == 0 && (pq % kBK == 0 || kBK % pq == 0) && g.M % kBK == 0 && kchunk % kBK == 0 &&
+         !(MFL_C32_GENERIC);
+}
+
 template <int BM, int BN, int KS, int ST, bool GEN>
 void launch_w2(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStream_t s) {
   constexpr int NS = stages_for(BM, BN);
@@ -1015,11 +1072,7 @@ void launch_w2(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStream_
 // fast path: Q | 32, the 32-pixel k-tile divides P*Q or is a multiple of it
 template <int BM, int BN, int KS, int ST>
 void launch_w(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStream_t s) {
-  const ConvGeom& g = a.g;
-  const int pq = g.P * g.Q;
-  const bool fast = g.Q > 0 && kBK % g.Q == 0 && (pq % kBK == 0 || kBK % pq == 0) && g.M % kBK == 0 &&
-                    a.kchunk % kBK == 0 && !(MFL_C32_GENERIC);
-  if (fast) launch_w2<BM, BN, KS, ST, false>(a, grid, dw, atomic, s);
+  if (wgrad_fast(a.g, a.kchunk)) launch_w2<BM, BN, KS, ST, false>(a, grid, dw, atomic, s);
   else launch_w2<BM, BN, KS, ST, true>(a, grid, dw, atomic, s);
 }
 template <int BM, int BN>
@@ -1032,8 +1085,7 @@ void launch_w_geom(const Conv32Args& a, dim3 grid, float* dw, int atomic, hipStr
 }
 }  // namespace
 
-void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, const float* dy, float* dw,
-                         bool accumulate, hipStream_t s) {
+static Conv32Args wgrad_args(const ConvGeom& g, const ConvPlan& p, const float* x, const float* dy) {
   Conv32Args a{};
   a.g = g;
   a.src = dy;
@@ -1042,6 +1094,12 @@ void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, c
   a.wgt_bytes = range_bytes((int64_t)g.N * g.H * g.W * g.C);
   a.kchunk = p.kchunk;
   fill_shifts(a);
+  return a;
+}
+
+void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, const float* dy, float* dw,
+                         bool accumulate, hipStream_t s) {
+  const Conv32Args a = wgrad_args(g, p, x, dy);
   const dim3 grid(cdiv(g.Ng, p.bm), cdiv(g.K, p.bn), p.splits);
   const int atomic = (accumulate || p.splits > 1) ? 1 : 0;
   const int key = p.bm * 1000 + p.bn;
@@ -1050,6 +1108,36 @@ void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, c
     case 128064: launch_w_geom<128, 64>(a, grid, dw, atomic, s); break;
     default: launch_w_geom<64, 128>(a, grid, dw, atomic, s); break;
   }
+}
+
+bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGeom& gf, const ConvPlan& pw,
+                            const float* dy, const float* w, float* dx, float* ysplit, int* counters, bool accum,
+                            const BnBwdFusion32* bnb, const float* x, float* dw, hipStream_t s) {
+  if (env_int("MFL_C32_PAIR", 1) == 0) return false;
+  const bool par = pd.par_mc != 0;
+  if (pd.bm != 64 || pd.bn != 64 || pw.bm != 64 || pw.bn != 64) return false;
+  if (gd.C % kBK != 0 || pd.kchunk % kBK != 0 || (MFL_C32_GENERIC)) return false;  // dgrad fast path
+  if (gd.stride > 1 && !par) return false;
+  if (!wgrad_fast(gf, pw.kchunk)) return false;
+  const Conv32Args ad = gemm_args(gd, true, pd, dy, w, dx, ysplit, counters, nullptr, accum, bnb, 1);
+  const Conv32Args aw = wgrad_args(gf, pw, x, dy);
+  const int gdx = cdiv(gd.M, 64), gdy = cdiv(gd.Ng, 64), nd = gdx * gdy * pd.splits;
+  const int gwx = cdiv(gf.Ng, 64), gwy = cdiv(gf.K, 64), gwz = pw.splits;
+  const int nblk = nd + gwx * gwy * gwz;
+  const size_t lds = std::max(gemm_lds(64, 64), (size_t)stages_for(64, 64) * kBK * (64 + 64) * 4);
+  constexpr int NS = stages_for(64, 64);
+  auto go = [&](auto kern) {
+    static_assert(NS >= 2, "ring");
+    if (lds > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    kern<<<nblk, 256, lds, s>>>(ad, aw, dw, 1, nd, gdx, gdy, gwx, gwy, gwz);
+  };
+  if (gd.R == 3 && gd.stride == 1) go(conv32_bwd_pair_kernel<3, 1, false, NS>);
+  else if (gd.R == 1 && gd.stride == 1) go(conv32_bwd_pair_kernel<1, 1, false, NS>);
+  else if (gd.R == 3 && gd.stride == 2) go(conv32_bwd_pair_kernel<3, 2, true, NS>);
+  else if (gd.R == 1 && gd.stride == 2) go(conv32_bwd_pair_kernel<1, 2, true, NS>);
+  else return false;
+  return true;
 }
 
 }  // namespace mfl

@@ -192,9 +192,17 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
     """A layer's weight gradient (dw += ..., dw zero on entry) and input
     gradient (as conv_dgrad) -- on the GPU in ONE paired launch, so the two
     independent, latency-bound GEMMs share the CUs (conv.hip
-    conv_bwd_pair_kernel; MFL_CONV_PAIR=0 for two launches).  fp32: two
-    launches (the fp32 GEMMs are compute-bound; pairing buys nothing)."""
-    if dy.is_cuda and dy.dtype != torch.float32:
+    conv_bwd_pair_kernel; MFL_CONV_PAIR=0 for two launches).  fp32: one
+    launch too (conv32.hip conv32_bwd_pair_kernel, when both plans run 64x64
+    tiles on the fast address paths; MFL_C32_PAIR=0 for two launches)."""
+    if dy.is_cuda and dy.dtype == torch.float32:
+        if bnb is None:
+            ops().conv32_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None)
+        else:
+            ops().conv32_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
+                                       bnb.invstd, bnb.acc)
+        return
+    if dy.is_cuda:
         if bnb is None:
             ops().conv_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None,
                                      None)

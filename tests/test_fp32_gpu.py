@@ -85,6 +85,31 @@ def test_conv32_forward_matches_fp64(t):
     assert torch.equal(y, y2)
 
 
+@pytest.mark.parametrize("t", [s for s in RESNET_SHAPES if s[3] != 8] + ODD_SHAPES,
+                         ids=lambda t: "x".join(map(str, t)))
+def test_conv32_backward_pair_matches_fp64(t):
+    """The paired dgrad + wgrad launch (conv32_bwd_pair_kernel, or its
+    two-launch fallback for shapes that do not pair) vs fp64 references."""
+    from metisfl_amd.ops import nn as K
+    shp = _shape(t)
+    g = torch.Generator().manual_seed(11 + (hash(t) & 0xFFFF))
+    x = torch.randn(shp.N, shp.H, shp.W, shp.C, generator=g)
+    dy = torch.randn(shp.N, shp.P, shp.Q, shp.Co, generator=g)
+    w = torch.randn(shp.Co, shp.R, shp.S, shp.C, generator=g) / (shp.R * shp.S * shp.C) ** 0.5
+    ref_dx = torch.nn.grad.conv2d_input((shp.N, shp.C, shp.H, shp.W), w.double().permute(0, 3, 1, 2),
+                                        dy.double().permute(0, 3, 1, 2), stride=shp.stride,
+                                        padding=shp.pad).permute(0, 2, 3, 1)
+    ref_dw = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (shp.Co, shp.C, shp.R, shp.S),
+                                         dy.double().permute(0, 3, 1, 2), stride=shp.stride,
+                                         padding=shp.pad).permute(0, 2, 3, 1)
+    dx = torch.zeros(ref_dx.shape, dtype=torch.float32, device=DEV)
+    dw = torch.zeros(ref_dw.shape, dtype=torch.float32, device=DEV)
+    K.conv_backward_pair(x.to(DEV), dy.to(DEV), dw, w.to(DEV), dx, shp, _ws(shp), accumulate=False)
+    torch.cuda.synchronize()
+    assert _rel(dx, ref_dx) <= 1e-5
+    assert _rel(dw, ref_dw) <= 1e-5
+
+
 @pytest.mark.parametrize("t", RESNET_SHAPES + ODD_SHAPES, ids=lambda t: "x".join(map(str, t)))
 def test_conv32_dgrad_matches_fp64(t):
     from metisfl_amd.ops import nn as K
