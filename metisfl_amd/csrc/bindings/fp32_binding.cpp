@@ -224,10 +224,10 @@ void bn32_stats(torch::Tensor x, int64_t C, torch::Tensor acc) {
   mfl::launch_bn32_stats(fp(x), x.numel() / C, (int)C, acc.data_ptr<double>(), cur_stream(x), reps_of(acc, C));
 }
 
-void bn32_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torch::Tensor gamma, torch::Tensor beta,
-                torch::Tensor mean, torch::Tensor invstd, torch::Tensor run_mean, torch::Tensor run_var,
-                c10::optional<torch::Tensor> residual, torch::Tensor y, bool relu, bool train, double momentum,
-                double eps) {
+mfl::BnFwdArgs32 bn32_args(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torch::Tensor gamma,
+                           torch::Tensor beta, torch::Tensor mean, torch::Tensor invstd, torch::Tensor run_mean,
+                           torch::Tensor run_var, c10::optional<torch::Tensor> residual, torch::Tensor y, bool relu,
+                           bool train, double momentum, double eps) {
   check_nhwc32(x, C);
   check_nhwc32(y, C);
   TORCH_CHECK(y.numel() == x.numel(), "bn y size");
@@ -258,7 +258,69 @@ void bn32_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, to
   a.eps = (float)eps;
   a.train = train ? 1 : 0;
   a.relu = relu ? 1 : 0;
-  mfl::launch_bn32_apply(a, cur_stream(x));
+  return a;
+}
+
+void bn32_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torch::Tensor gamma, torch::Tensor beta,
+                torch::Tensor mean, torch::Tensor invstd, torch::Tensor run_mean, torch::Tensor run_var,
+                c10::optional<torch::Tensor> residual, torch::Tensor y, bool relu, bool train, double momentum,
+                double eps) {
+  mfl::launch_bn32_apply(
+      bn32_args(x, C, acc, gamma, beta, mean, invstd, run_mean, run_var, residual, y, relu, train, momentum, eps),
+      cur_stream(x));
+}
+
+// shortcut BN (no ReLU) + conv1 BN (ReLU) of a downsampling block in one launch
+void bn32_apply_pair(torch::Tensor x1, torch::Tensor gamma1, torch::Tensor beta1, torch::Tensor mean1,
+                     torch::Tensor invstd1, torch::Tensor rm1, torch::Tensor rv1, c10::optional<torch::Tensor> acc1,
+                     torch::Tensor y1, torch::Tensor x2, torch::Tensor gamma2, torch::Tensor beta2,
+                     torch::Tensor mean2, torch::Tensor invstd2, torch::Tensor rm2, torch::Tensor rv2,
+                     c10::optional<torch::Tensor> acc2, torch::Tensor y2, int64_t C, bool train, double momentum,
+                     double eps) {
+  const auto a1 = bn32_args(x1, C, acc1, gamma1, beta1, mean1, invstd1, rm1, rv1, c10::nullopt, y1, false, train,
+                            momentum, eps);
+  const auto a2 = bn32_args(x2, C, acc2, gamma2, beta2, mean2, invstd2, rm2, rv2, c10::nullopt, y2, true, train,
+                            momentum, eps);
+  mfl::launch_bn32_apply_pair(a1, a2, cur_stream(x1));
+}
+
+// conv1 (3x3 / s2) + projection shortcut (1x1 / s2) of one x: one launch when both plans pair
+void conv32_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c10::optional<torch::Tensor> ws1,
+                         c10::optional<torch::Tensor> stats1, torch::Tensor w2, torch::Tensor y2,
+                         c10::optional<torch::Tensor> ws2, c10::optional<torch::Tensor> stats2, int64_t N, int64_t H,
+                         int64_t W, int64_t C, int64_t Co) {
+  const auto g1 = fwd_geom(N, H, W, C, Co, 3, 3, 2, 1);
+  const auto g2 = fwd_geom(N, H, W, C, Co, 1, 1, 2, 0);
+  TORCH_CHECK(g1.M == g2.M, "conv1 / shortcut output sizes differ");
+  check_f32(x, N * H * W * C, "x");
+  check_f32(w1, Co * 9 * C, "w1");
+  check_f32(w2, Co * C, "w2");
+  check_f32(y1, (int64_t)g1.M * Co, "y1");
+  check_f32(y2, (int64_t)g2.M * Co, "y2");
+  const auto p1 = mfl::plan_conv32(g1, 0), p2 = mfl::plan_conv32(g2, 0);
+  auto slab = [&](const mfl::ConvGeom& g, const mfl::ConvPlan& p, const c10::optional<torch::Tensor>& ws,
+                  float*& ys, int*& cn) {
+    ys = nullptr;
+    cn = nullptr;
+    if (p.splits > 1) {
+      TORCH_CHECK(ws.has_value() && ws->defined(), "split-K workspace required");
+      check_f32(*ws, ws_floats(g, p), "workspace", false);
+      cn = reinterpret_cast<int*>(ws->data_ptr<float>());
+      ys = ws->data_ptr<float>() + kCounterWords;
+    }
+  };
+  float *ys1, *ys2;
+  int *c1, *c2;
+  slab(g1, p1, ws1, ys1, c1);
+  slab(g2, p2, ws2, ys2, c2);
+  double* st1 = stats_ptr(stats1, Co);
+  double* st2 = stats_ptr(stats2, Co);
+  const int r1 = st1 ? reps_of(*stats1, Co) : 1, r2 = st2 ? reps_of(*stats2, Co) : 1;
+  if (mfl::launch_conv32_fwd_pair(g1, p1, fp(w1), fp(y1), ys1, c1, st1, r1, g2, p2, fp(w2), fp(y2), ys2, c2, st2, r2,
+                                  fp(x), cur_stream(x)))
+    return;
+  run(g1, false, x, w1, y1, ws1, st1, false, nullptr, r1);
+  run(g2, false, x, w2, y2, ws2, st2, false, nullptr, r2);
 }
 
 void bn32_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C, torch::Tensor gamma,
@@ -357,6 +419,8 @@ void register_fp32(pybind11::module& m) {
   m.def("conv32_backward_pair", &conv32_backward_pair);
   m.def("bn32_stats", &bn32_stats);
   m.def("bn32_apply", &bn32_apply);
+  m.def("bn32_apply_pair", &bn32_apply_pair);
+  m.def("conv32_forward_pair", &conv32_forward_pair);
   m.def("bn32_backward", &bn32_backward);
   m.def("head32_forward_backward", &head32_forward_backward);
   m.def("gather_batch32", &gather_batch32);

@@ -94,14 +94,16 @@ __device__ __forceinline__ void rep_sums(const double* acc, int reps, int C, int
 // Main loops: when C / 4 divides 256 the grid stride is a multiple of C / 4,
 // so a lane's channels never change -- its coefficients live in registers
 // (no LDS read and no 64-bit modulo per vector).
+// (bid, nblk): this block's index in the apply's own grid (the paired launch
+// maps one hardware grid onto two applies)
 template <bool RES, bool RELU>
-__global__ __launch_bounds__(256) void bn32_apply_kernel(BnFwdArgs32 a, int64_t nvec) {
-  extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
+__device__ __forceinline__ void bn32_apply_body(const BnFwdArgs32& a, int64_t nvec, int bid, int nblk,
+                                                float* coef) {
   const int C = a.C;
   const float4* X = reinterpret_cast<const float4*>(a.x);
   const float4* R = reinterpret_cast<const float4*>(a.residual);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)nblk * blockDim.x;
+  int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
   float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), rv = xv;
   if (i < nvec) {  // first vectors in flight across the prologue
     xv = X[i];
@@ -124,7 +126,7 @@ __global__ __launch_bounds__(256) void bn32_apply_kernel(BnFwdArgs32 a, int64_t 
     const float sc = (float)((double)a.gamma[c] * isd);
     coef[c] = sc;
     coef[C + c] = (float)((double)a.beta[c] - mu * (double)a.gamma[c] * isd);
-    if (a.train && blockIdx.x == 0) {
+    if (a.train && bid == 0) {
       a.mean[c] = (float)mu;
       a.invstd[c] = (float)isd;
       if (a.run_mean) {
@@ -161,6 +163,28 @@ __global__ __launch_bounds__(256) void bn32_apply_kernel(BnFwdArgs32 a, int64_t 
     }
     reinterpret_cast<float4*>(a.y)[i] = v;
   }
+}
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(256) void bn32_apply_kernel(BnFwdArgs32 a, int64_t nvec) {
+  extern __shared__ __attribute__((aligned(16))) float coef[];  // [2][C]
+  bn32_apply_body<RES, RELU>(a, nvec, blockIdx.x, gridDim.x, coef);
+}
+
+// A downsampling block's two BatchNorms (shortcut: no ReLU; conv1: ReLU) in
+// one launch (the bf16 twin: bn.hip bn_apply_pair_kernel).
+__global__ __launch_bounds__(256) void bn32_apply_pair_kernel(BnFwdArgs32 a1, int64_t n1, int g1, BnFwdArgs32 a2,
+                                                              int64_t n2) {
+  extern __shared__ __attribute__((aligned(16))) float coef[];
+  if ((int)blockIdx.x < g1) bn32_apply_body<false, false>(a1, n1, blockIdx.x, g1, coef);
+  else bn32_apply_body<false, true>(a2, n2, blockIdx.x - g1, gridDim.x - g1, coef);
+}
+
+void launch_bn32_apply_pair(const BnFwdArgs32& a1, const BnFwdArgs32& a2, hipStream_t s) {
+  const int64_t n1 = a1.M * a1.C / 4, n2 = a2.M * a2.C / 4;
+  const unsigned g1 = stream_grid(n1, 256, 2048), g2 = stream_grid(n2, 256, 2048);
+  const size_t sm = 2 * (size_t)(a1.C > a2.C ? a1.C : a2.C) * sizeof(float);
+  bn32_apply_pair_kernel<<<g1 + g2, 256, sm, s>>>(a1, n1, (int)g1, a2, n2);
 }
 
 void launch_bn32_apply(const BnFwdArgs32& a, hipStream_t s) {

@@ -65,6 +65,12 @@ void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, c
 // pw; dw must hold zeros or a running sum: slices add atomically) of one
 // layer in one launch.  Returns false (nothing launched) when the two plans
 // do not both run 64x64 tiles on the fast address paths.
+// conv1 (3x3/s2, g1) + projection shortcut (1x1/s2, g2) of one x in one
+// launch; false (nothing launched) when the plans do not pair.
+bool launch_conv32_fwd_pair(const ConvGeom& g1, const ConvPlan& p1, const float* w1, float* y1, float* ys1,
+                            int* c1, double* st1, int reps1, const ConvGeom& g2, const ConvPlan& p2,
+                            const float* w2, float* y2, float* ys2, int* c2, double* st2, int reps2,
+                            const float* x, hipStream_t s);
 bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGeom& gf, const ConvPlan& pw,
                             const float* dy, const float* w, float* dx, float* ysplit, int* counters, bool accum,
                             const BnBwdFusion32* bnb, const float* x, float* dw, hipStream_t s);

@@ -791,6 +791,23 @@ __global__ __launch_bounds__(256, 2) void conv32_wgrad_kernel(Conv32Args a, floa
 // workgroups whose tail waves leave CUs idle and the second pays a launch
 // boundary.  dgrad blocks first: it is on the critical path (the bf16
 // twin measured dgrad-first / wgrad-first / alternating 502 / 551 / 508 ms).
+// A downsampling block's conv1 (3x3 / stride 2) and projection shortcut
+// (1x1 / stride 2) read the same x: one launch, blocks [0, n1) conv1.
+template <int NS>
+__global__ __launch_bounds__(256, 2) void conv32_fwd_pair_kernel(Conv32Args a1, Conv32Args a2, int n1, int g1x,
+                                                                 int g1y, int g2x, int g2y, int g2z) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int b = blockIdx.x;
+  if (b < n1) {
+    const Blk k{b % g1x, (b / g1x) % g1y, b / (g1x * g1y), g1x, g1y, n1 / (g1x * g1y)};
+    conv32_gemm_body<64, 64, false, 3, 2, false, NS, false>(a1, k, smem);
+  } else {
+    const int w = b - n1;
+    const Blk k{w % g2x, (w / g2x) % g2y, w / (g2x * g2y), g2x, g2y, g2z};
+    conv32_gemm_body<64, 64, false, 1, 2, false, NS, false>(a2, k, smem);
+  }
+}
+
 template <int KS, int ST, bool PAR, int NS>
 __global__ __launch_bounds__(256, 2) void conv32_bwd_pair_kernel(Conv32Args ad, Conv32Args aw, float* __restrict__ dw,
                                                                  int atomic, int nd, int gdx, int gdy, int gwx,
@@ -1137,6 +1154,27 @@ bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGe
   else if (gd.R == 3 && gd.stride == 2) go(conv32_bwd_pair_kernel<3, 2, true, NS>);
   else if (gd.R == 1 && gd.stride == 2) go(conv32_bwd_pair_kernel<1, 2, true, NS>);
   else return false;
+  return true;
+}
+
+bool launch_conv32_fwd_pair(const ConvGeom& g1, const ConvPlan& p1, const float* w1, float* y1, float* ys1,
+                            int* c1, double* st1, int reps1, const ConvGeom& g2, const ConvPlan& p2,
+                            const float* w2, float* y2, float* ys2, int* c2, double* st2, int reps2,
+                            const float* x, hipStream_t s) {
+  if (env_int("MFL_C32_PAIR", 1) == 0) return false;
+  if (p1.bm != 64 || p1.bn != 64 || p2.bm != 64 || p2.bn != 64) return false;
+  if (g1.R != 3 || g1.stride != 2 || g2.R != 1 || g2.stride != 2) return false;
+  if (g1.C % kBK != 0 || p1.kchunk % kBK != 0 || p2.kchunk % kBK != 0 || (MFL_C32_GENERIC)) return false;
+  const Conv32Args a1 = gemm_args(g1, false, p1, x, w1, y1, ys1, c1, st1, false, nullptr, reps1);
+  const Conv32Args a2 = gemm_args(g2, false, p2, x, w2, y2, ys2, c2, st2, false, nullptr, reps2);
+  const int g1x = cdiv(g1.M, 64), g1y = cdiv(g1.Ng, 64), n1 = g1x * g1y * p1.splits;
+  const int g2x = cdiv(g2.M, 64), g2y = cdiv(g2.Ng, 64), g2z = p2.splits;
+  constexpr int NS = stages_for(64, 64);
+  const size_t lds = gemm_lds(64, 64);
+  if (lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv32_fwd_pair_kernel<NS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  conv32_fwd_pair_kernel<NS><<<n1 + g2x * g2y * g2z, 256, lds, s>>>(a1, a2, n1, g1x, g1y, g2x, g2y, g2z);
   return true;
 }
 

@@ -246,20 +246,20 @@ class BasicBlock(Layer):
         if self.sc is None:
             a = self.c1.forward(x, train=train)
             return self.c2.forward(a, residual=x, train=train)
-        if (not self.c1.ws.overlap and self.c1.shp.R == 3 and self.c1.shp.stride == 2
-                and self.c1.ws.dtype == torch.bfloat16):
+        if not self.c1.ws.overlap and self.c1.shp.R == 3 and self.c1.shp.stride == 2:
             # conv1 and the projection shortcut in one paired launch
             c1, sc = self.c1, self.sc
             c1.x = sc.x = x
             K.conv_forward_pair(x, c1.w16, c1.z, c1._split(), c1.ws.acc(c1.acc_f) if train else None,
                                 sc.w16, sc.z, sc._split(), sc.ws.acc(sc.acc_f) if train else None, c1.shp)
-            if x.is_cuda and hasattr(K.ops(), "bn_apply_pair") and not sc.relu and c1.relu:
+            if x.is_cuda and not sc.relu and c1.relu:
                 # ... and their two BatchNorms in one launch
-                K.ops().bn_apply_pair(sc.z, sc.gamma, sc.beta, sc.mean, sc.invstd, sc.rmean, sc.rvar,
-                                      sc.ws.acc(sc.acc_f) if train else None, sc.y,
-                                      c1.z, c1.gamma, c1.beta, c1.mean, c1.invstd, c1.rmean, c1.rvar,
-                                      c1.ws.acc(c1.acc_f) if train else None, c1.y,
-                                      c1.shp.Co, train, c1.momentum, c1.eps)
+                pair = K.ops().bn32_apply_pair if x.dtype == torch.float32 else K.ops().bn_apply_pair
+                pair(sc.z, sc.gamma, sc.beta, sc.mean, sc.invstd, sc.rmean, sc.rvar,
+                     sc.ws.acc(sc.acc_f) if train else None, sc.y,
+                     c1.z, c1.gamma, c1.beta, c1.mean, c1.invstd, c1.rmean, c1.rvar,
+                     c1.ws.acc(c1.acc_f) if train else None, c1.y,
+                     c1.shp.Co, train, c1.momentum, c1.eps)
                 r, a = sc.y, c1.y
             else:
                 r = sc.bn_forward(train=train)

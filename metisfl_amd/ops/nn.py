@@ -180,8 +180,9 @@ def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShap
     """A downsampling block's conv1 (3x3, stride 2; ``shp``) and its 1x1 / stride-2
     projection shortcut of the same x -- one paired launch on the GPU."""
     assert shp.R == 3 and shp.stride == 2
-    if x.is_cuda and x.dtype != torch.float32:
-        ops().conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp.N, shp.H, shp.W, shp.C, shp.Co)
+    if x.is_cuda:
+        fn = ops().conv32_forward_pair if x.dtype == torch.float32 else ops().conv_forward_pair
+        fn(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp.N, shp.H, shp.W, shp.C, shp.Co)
         return
     conv_forward(x, w1, y1, shp, ws1, stats1)
     conv_forward(x, w2, y2, ConvShape(shp.N, shp.H, shp.W, shp.C, shp.Co, 1, 1, 2, 0), ws2, stats2)
