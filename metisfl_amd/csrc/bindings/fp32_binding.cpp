@@ -323,10 +323,12 @@ void conv32_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c1
   run(g2, false, x, w2, y2, ws2, st2, false, nullptr, r2);
 }
 
-void bn32_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C, torch::Tensor gamma,
-                   torch::Tensor mean, torch::Tensor invstd, torch::Tensor acc, c10::optional<torch::Tensor> dgamma,
-                   c10::optional<torch::Tensor> dbeta, torch::Tensor dx, c10::optional<torch::Tensor> dy_masked,
-                   bool presummed) {
+void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,
+                        torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd, torch::Tensor acc,
+                        c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor dx,
+                        c10::optional<torch::Tensor> dy_masked, bool presummed, c10::optional<torch::Tensor> z2,
+                        c10::optional<torch::Tensor> mean2, c10::optional<torch::Tensor> invstd2,
+                        c10::optional<torch::Tensor> acc2) {
   check_nhwc32(dy, C);
   check_nhwc32(x, C);
   check_nhwc32(dx, C);
@@ -356,10 +358,32 @@ void bn32_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tenso
   a.dx = fp(dx);
   a.M = x.numel() / C;
   a.C = (int)C;
+  if (acc2.has_value() && acc2->defined()) {
+    TORCH_CHECK(a.dy_masked != nullptr, "the side reduction runs over dy_masked");
+    TORCH_CHECK(C / 4 <= 256 && 256 % (C / 4) == 0, "side reduction needs C / 4 dividing 256");
+    TORCH_CHECK(z2.has_value() && mean2.has_value() && invstd2.has_value(), "side reduction operands");
+    check_nhwc32(*z2, C);
+    TORCH_CHECK(z2->numel() == x.numel(), "side z size");
+    check_pc(*mean2, C, "mean2");
+    check_pc(*invstd2, C, "invstd2");
+    a.z2 = fp(*z2);
+    a.mean2 = fp(*mean2);
+    a.invstd2 = fp(*invstd2);
+    a.acc2 = const_cast<double*>(acc_ptr(*acc2, C));
+    a.reps2 = reps_of(*acc2, C);
+  }
   auto s = cur_stream(x);
   if (!presummed)
     mfl::launch_bn32_bwd_reduce(a.dy, a.x, a.y, a.mean, a.invstd, a.M, a.C, acc.data_ptr<double>(), s, a.reps);
   mfl::launch_bn32_bwd_apply(a, s);
+}
+
+void bn32_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C, torch::Tensor gamma,
+                   torch::Tensor mean, torch::Tensor invstd, torch::Tensor acc, c10::optional<torch::Tensor> dgamma,
+                   c10::optional<torch::Tensor> dbeta, torch::Tensor dx, c10::optional<torch::Tensor> dy_masked,
+                   bool presummed) {
+  bn32_backward_side(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked, presummed, c10::nullopt,
+                     c10::nullopt, c10::nullopt, c10::nullopt);
 }
 
 // ---- head / data ---------------------------------------------------------
@@ -422,6 +446,7 @@ void register_fp32(pybind11::module& m) {
   m.def("bn32_apply_pair", &bn32_apply_pair);
   m.def("conv32_forward_pair", &conv32_forward_pair);
   m.def("bn32_backward", &bn32_backward);
+  m.def("bn32_backward_side", &bn32_backward_side);
   m.def("head32_forward_backward", &head32_forward_backward);
   m.def("gather_batch32", &gather_batch32);
 }

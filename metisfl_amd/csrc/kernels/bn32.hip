@@ -288,6 +288,13 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
     is = *reinterpret_cast<const float4*>(sc + 4 * C + cb);
   };
   load_coef();
+  // side reduction (fixed channels only: the binding checks)
+  const bool side = WRITE_DYM && a.acc2 != nullptr;
+  float4 s2 = make_float4(0.f, 0.f, 0.f, 0.f), q2 = s2, mu2 = s2, is2 = s2;
+  if (side) {
+    mu2 = *reinterpret_cast<const float4*>(a.mean2 + cb);
+    is2 = *reinterpret_cast<const float4*>(a.invstd2 + cb);
+  }
   for (; i < nvec; i += stride) {
     float4 g = gv;
     const float4 xc = xv, yc = yv;
@@ -306,6 +313,14 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
       g.z = yc.z > 0.f ? g.z : 0.f;
       g.w = yc.w > 0.f ? g.w : 0.f;
       if (WRITE_DYM) reinterpret_cast<float4*>(a.dy_masked)[i] = g;
+      if (WRITE_DYM && side) {
+        const float4 z2 = reinterpret_cast<const float4*>(a.z2)[i];
+        s2.x += g.x; s2.y += g.y; s2.z += g.z; s2.w += g.w;
+        q2.x += g.x * ((z2.x - mu2.x) * is2.x);
+        q2.y += g.y * ((z2.y - mu2.y) * is2.y);
+        q2.z += g.z * ((z2.z - mu2.z) * is2.z);
+        q2.w += g.w * ((z2.w - mu2.w) * is2.w);
+      }
     }
     float4 o;
     o.x = k1.x * (g.x - mg.x - ((xc.x - mu.x) * is.x) * mx.x);
@@ -313,6 +328,10 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
     o.z = k1.z * (g.z - mg.z - ((xc.z - mu.z) * is.z) * mx.z);
     o.w = k1.w * (g.w - mg.w - ((xc.w - mu.w) * is.w) * mx.w);
     reinterpret_cast<float4*>(a.dx)[i] = o;
+  }
+  if (side) {
+    __syncthreads();  // sc[] reads done before channel_atomic4's LDS staging
+    channel_atomic4(s2, q2, C, tpr, 256 / tpr, a.acc2 + (int64_t)(blockIdx.x % a.reps2) * 2 * C);
   }
 }
 

@@ -126,6 +126,14 @@ struct BnBwdArgs32 {
   int64_t M;
   int C;
   int reps;  // acc replicas, as BnFwdArgs32
+  // optional side reduction over the masked gradient written to dy_masked:
+  // acc2 += (sum g, sum g * (z2 - mean2) * invstd2) -- the BN backward sums
+  // of a projection shortcut whose upstream gradient IS dy_masked
+  const float* z2;
+  const float* mean2;
+  const float* invstd2;
+  double* acc2;
+  int reps2;
 };
 void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_t s, int reps = 1);
 void launch_bn32_apply(const BnFwdArgs32& a, hipStream_t s);

@@ -182,9 +182,17 @@ class ConvBN(Layer):
         return K.BnBwdTarget(self.z, self.y if self.relu else None, self.mean, self.invstd,
                              self.ws.acc(self.acc_b))
 
+    def bn_side(self) -> K.BnSide | None:
+        """This (shortcut) layer's BN backward sums as a side reduction of the
+        launch that writes its upstream gradient (fp32 GPU path)."""
+        if (self.ws.dtype == torch.float32 and self.z.is_cuda and 256 % (self.shp.Co // 4) == 0
+                and self.shp.Co % 4 == 0):
+            return K.BnSide(self.z, self.mean, self.invstd, self.ws.acc(self.acc_b))
+        return None
+
     def backward(self, dy: torch.Tensor, dx: torch.Tensor | None, accumulate: bool = False,
                  dres: torch.Tensor | None = None, presummed: bool = False,
-                 bnb: K.BnBwdTarget | None = None) -> None:
+                 bnb: K.BnBwdTarget | None = None, side: K.BnSide | None = None) -> None:
         """dy: gradient w.r.t. this layer's output.  Writes dgamma/dbeta/dW into
         the flat gradient buffer and (if dx is given) d input into dx; ``dres``
         receives the ReLU-masked dy that the residual branch needs.
@@ -194,7 +202,7 @@ class ConvBN(Layer):
         s = self.shp
         K.bn_backward(dy, self.z, self.y if self.relu else None, s.Co, self.gamma, self.mean,
                       self.invstd, self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz, dres,
-                      presummed=presummed)
+                      presummed=presummed, side=side)
         # weight gradient: off the critical path -> side stream (joined before
         # the optimizer); the gradient buffer is zero on entry (re-zeroed by
         # the optimizer launch), so split-K slices accumulate atomically
@@ -283,8 +291,12 @@ class BasicBlock(Layer):
             self.c2.backward(dout, self.da, dres=dx, presummed=presummed, bnb=self.c1.bn_target())
             self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev)
         else:
-            self.c2.backward(dout, self.da, dres=self.dres, presummed=presummed, bnb=self.c1.bn_target())
-            self.sc.backward(self.dres, dx)
+            # the shortcut BN's backward sums ride in conv2's BN-backward launch
+            # (it writes dres, the shortcut's upstream gradient)
+            side = self.sc.bn_side()
+            self.c2.backward(dout, self.da, dres=self.dres, presummed=presummed, bnb=self.c1.bn_target(),
+                             side=side)
+            self.sc.backward(self.dres, dx, presummed=side is not None)
             self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev)
 
 

@@ -266,13 +266,28 @@ def bn_apply(x, C: int, acc, gamma, beta, mean, invstd, run_mean, run_var, y, re
     y.copy_(v.to(y.dtype))
 
 
+@dataclass
+class BnSide:
+    """A second BatchNorm whose upstream gradient is ``dy_masked`` (a
+    downsampling block's projection shortcut): its backward sums are added
+    into ``acc`` by the same launch (fp32 GPU path; C / 4 must divide 256)."""
+    z: torch.Tensor
+    mean: torch.Tensor
+    invstd: torch.Tensor
+    acc: torch.Tensor
+
+
 def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
-                dy_masked=None, presummed: bool = False) -> None:
+                dy_masked=None, presummed: bool = False, side: BnSide | None = None) -> None:
     """BN(+ReLU) backward.  ``y`` (the post-activation output) gives the ReLU
     mask; ``dy_masked`` optionally receives the masked upstream gradient (the
     residual-shortcut gradient of an add+ReLU).  ``acc`` (fp64 [2C]) must be
     zero on entry."""
     if dy.is_cuda:
+        if side is not None:
+            ops().bn32_backward_side(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked, presummed,
+                                     side.z, side.mean, side.invstd, side.acc)
+            return
         fn = ops().bn32_backward if dy.dtype == torch.float32 else ops().bn_backward
         fn(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked, presummed)
         return
@@ -281,6 +296,11 @@ def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
         g = torch.where(y.float() > 0, g, torch.zeros_like(g))
         if dy_masked is not None:
             dy_masked.copy_(g.to(dy_masked.dtype))
+    if side is not None:
+        gs = g.reshape(-1, C).double()
+        xs = ((side.z.float() - side.mean) * side.invstd).reshape(-1, C).double()
+        side.acc[:C] += gs.sum(0)
+        side.acc[C:2 * C] += (gs * xs).sum(0)
     xf = x.float()
     xh = (xf - mean) * invstd
     gm = g.reshape(-1, C)
