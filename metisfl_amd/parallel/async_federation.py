@@ -29,14 +29,19 @@ learner's next submission carries the version it trained from, and its
 FedRec weight is multiplied by cfg.staleness's discount of
 t = version_now - version_base (``staleness_discount``).
 
-Rank 0 trains its own shard in chunks of ``poll_every`` local steps and
-serves pending submissions between chunks, so a finisher waits at most one
-chunk.  The weights are the NUM_TRAINING_EXAMPLES (or batch / participant)
-scaling inputs, un-normalised, as FedRec consumes them.
+Rank 0's aggregator runs in a service thread with its own process group
+(point-to-point transfers) and its own HIP stream, so a finisher is served
+the moment it posts -- rank 0's own training never blocks it (and is not
+chunked).  ``serve_in_thread=False`` keeps the single-threaded variant: rank
+0 trains in chunks of ``poll_every`` local steps and serves between chunks,
+so a finisher waits up to one chunk.  The weights are the
+NUM_TRAINING_EXAMPLES (or batch / participant) scaling inputs,
+un-normalised, as FedRec consumes them.
 """
 from __future__ import annotations
 
 import json
+import threading
 import time
 from dataclasses import dataclass
 
@@ -80,13 +85,21 @@ class AsyncUpdate:
 
 class AsyncCollectiveFederation:
     def __init__(self, comm: Comm, net, train_ds, cfg: FederationConfig, tasks_per_learner: int = 2,
-                 poll_every: int = 16, store=None, broadcast_initial: bool = True):
+                 poll_every: int = 16, store=None, broadcast_initial: bool = True,
+                 serve_in_thread: bool = True):
         self.comm, self.net, self.train_ds, self.cfg = comm, net, train_ds, cfg
         self.rank, self.world = comm.rank, comm.world
         _INSTANCES[0] += 1
         self.tag = _INSTANCES[0]  # store-key namespace: repeated federations never see old keys
         self.tasks = tasks_per_learner
         self.poll_every = max(1, poll_every)
+        self.threaded = bool(serve_in_thread) and comm.distributed
+        # point-to-point model transfers on their own group (created on every
+        # rank, a collective call): the service thread's sends / receives never
+        # interleave with the default group's collectives
+        self.p2p = dist.new_group(backend=comm.backend) if comm.distributed else None
+        self._lock = threading.Lock()     # rank 0: FedRec state (S, Z, last, version)
+        self._svc_error: BaseException | None = None
         self.store = store if store is not None else (
             dist.distributed_c10d._get_default_store() if comm.distributed else None)
         n = int(train_ds.n)
@@ -122,37 +135,74 @@ class AsyncCollectiveFederation:
         self.net.train_steps(self.train_ds, nsteps, step_offset=self.steps_done)
         self.steps_done += nsteps
 
+    def _pending(self) -> bool:
+        return any(self.next_task[r] < self.tasks for r in range(1, self.world))
+
+    def _serve_loop(self) -> None:
+        """Rank 0 service thread: serve submissions as they arrive."""
+        try:
+            st = self.net.state
+            if st.model32.is_cuda:
+                torch.cuda.set_device(st.model32.device)
+                stream = torch.cuda.Stream(device=st.model32.device)
+                ctx = torch.cuda.stream(stream)
+            else:
+                import contextlib
+                ctx = contextlib.nullcontext()
+            with ctx:
+                while self._pending():
+                    if not self.serve(block=False):
+                        time.sleep(0.0005)
+        except BaseException as e:  # noqa: BLE001 - re-raised on the main thread
+            self._svc_error = e
+
     def run(self) -> list[AsyncUpdate]:
         """Run ``tasks_per_learner`` asynchronous tasks on this learner; rank 0
         also serves every other learner's submissions until all are done."""
+        svc = None
+        if self.rank == 0 and self.threaded:
+            svc = threading.Thread(target=self._serve_loop, name="metisfl-async-aggregator", daemon=True)
+            svc.start()
         for task in range(self.tasks):
             self.net.reset_train_stats()
             left = self.num_local_updates
             while left > 0:
-                k = min(left, self.poll_every) if self.rank == 0 else left
+                k = min(left, self.poll_every) if (self.rank == 0 and not self.threaded) else left
                 self._train(k)
                 left -= k
-                if self.rank == 0:
+                if self.rank == 0 and not self.threaded:
                     self.serve(block=False)
             meta = {"task": task, "weight": self._weight(self.num_local_updates),
                     "loss": self.net.train_stats()["loss"], "batches": self.num_local_updates,
                     "base_version": self.base_version}
             if self.rank == 0:
-                self._fedrec(0, self.net.state.model32, meta)
-                self.net.state.model32.copy_(self._community())
-                self.base_version = self.version
+                with self._lock:
+                    self._fedrec(0, self.net.state.model32, meta)
+                    self.net.state.model32.copy_(self._community())
+                    self._sync_stream()
+                    self.base_version = self.version
                 self._install()
             else:
                 self.store.set(_KEY.format(self.tag, self.rank, task), json.dumps(meta))
-                dist.send(self.net.state.model32, dst=0)
-                dist.recv(self.net.state.model32, src=0)
+                dist.send(self.net.state.model32, dst=0, group=self.p2p)
+                dist.recv(self.net.state.model32, src=0, group=self.p2p)
                 self.base_version = int(self.store.get(_VER.format(self.tag, self.rank, task)))
                 self._install()
         if self.rank == 0:
-            while any(self.next_task[r] < self.tasks for r in range(1, self.world)):
-                if not self.serve(block=False):
-                    time.sleep(0.001)
+            if svc is not None:
+                svc.join()
+                if self._svc_error is not None:
+                    raise RuntimeError("async aggregator thread failed") from self._svc_error
+            else:
+                while self._pending():
+                    if not self.serve(block=False):
+                        time.sleep(0.001)
         return self.updates
+
+    def _sync_stream(self) -> None:
+        t = self.net.state.model32
+        if t.is_cuda:
+            torch.cuda.current_stream(t.device).synchronize()
 
     def _install(self) -> None:
         st = self.net.state
@@ -172,10 +222,14 @@ class AsyncCollectiveFederation:
             if not block and not self.store.check([key]):
                 continue
             meta = json.loads(self.store.get(key))
-            dist.recv(self.rbuf, src=r)
-            self._fedrec(r, self.rbuf, meta)
-            self.store.set(_VER.format(self.tag, r, t), str(self.version))
-            dist.send(self._community(), dst=r)
+            dist.recv(self.rbuf, src=r, group=self.p2p)
+            with self._lock:
+                self._fedrec(r, self.rbuf, meta)
+                comm_model = self._community()
+                ver = self.version
+                self._sync_stream()
+            self.store.set(_VER.format(self.tag, r, t), str(ver))
+            dist.send(comm_model, dst=r, group=self.p2p)
             self.next_task[r] = t + 1
             served += 1
         return served
@@ -195,8 +249,8 @@ class AsyncCollectiveFederation:
         self.last[r].copy_(theta)
         self.last_w[r] = w
         self.version += 1
-        if theta.is_cuda:
-            torch.cuda.synchronize(theta.device)
+        if theta.is_cuda:  # this stream only: rank 0's training keeps running on its own
+            torch.cuda.current_stream(theta.device).synchronize()
         self.updates.append(AsyncUpdate(r, int(meta["task"]), w, time.time(),
                                         (time.perf_counter() - t0) * 1e3, float(meta["loss"]),
                                         int(meta["batches"]), stale, w0))

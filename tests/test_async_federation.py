@@ -17,7 +17,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, staleness="none"):
+def _worker(rank, world, port, out_dir, staleness="none", threaded=True):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
@@ -34,7 +34,8 @@ def _worker(rank, world, port, out_dir, staleness="none"):
     ds = net.make_dataset(rng.standard_normal((n, 13)).astype(np.float32),
                           rng.standard_normal(n).astype(np.float32), seed=rank)
     cfg = FederationConfig(batch_size=4, local_epochs=1, evaluate_test=False, staleness=staleness)
-    fed = AsyncCollectiveFederation(comm, net, ds, cfg, tasks_per_learner=3, poll_every=1)
+    fed = AsyncCollectiveFederation(comm, net, ds, cfg, tasks_per_learner=3, poll_every=1,
+                                    serve_in_thread=threaded)
     ups = fed.run()
     res = {"rank": rank, "final": net.state.model32.numpy().tolist()}
     if rank == 0:
@@ -49,10 +50,14 @@ def _worker(rank, world, port, out_dir, staleness="none"):
     comm.close()
 
 
-def test_async_fedrec_three_learners(tmp_path):
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("threaded", [True, False], ids=["service-thread", "chunked"])
+def test_async_fedrec_three_learners(tmp_path, threaded):
     world = 3
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
-                       start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), "none", threaded), nprocs=world,
+                       join=True, start_method="spawn")
     res = [json.load(open(tmp_path / f"async_none_{r}.json")) for r in range(world)]
     ups = res[0]["updates"]
     assert len(ups) == world * 3
