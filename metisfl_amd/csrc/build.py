@@ -43,6 +43,14 @@ def _py_includes() -> list[str]:
     return [sysconfig.get_paths()["include"], pybind11.get_include()]
 
 
+def _py_embed_ldflags() -> str:
+    """Link flags for an executable embedding this interpreter (controller_main)."""
+    libdir = sysconfig.get_config_var("LIBDIR") or ""
+    ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
+    extra = sysconfig.get_config_var("LIBS") or ""
+    return f"-L{libdir} -Wl,-rpath,{libdir} -lpython{ver} {extra} -lm"
+
+
 def _torch_paths():
     import torch
     from torch.utils import cpp_extension as ce
@@ -86,6 +94,8 @@ def write_ninja() -> str:
         f"bind_cflags = -O2 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__ -DUSE_ROCM "
         f"-DTORCH_EXTENSION_NAME=_ops -DTORCH_API_INCLUDE_EXTENSION_H -D_GLIBCXX_USE_CXX11_ABI={abi} "
         f"-I{csrc} {tincs} -I{ROCM}/include {pyinc} -Wno-deprecated-declarations",
+        f"tool_cflags = {pyinc} -DMETISFL_AMD_DEFAULT_ROOT=\\\"{ROOT}\\\"",
+        f"tool_ldflags = {_py_embed_ldflags()}",
         f"ops_ldflags = -shared -fPIC --offload-arch={ARCH} -L{tlib} -Wl,-rpath,{tlib} "
         f"-lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip -ltorch_python -lamdhip64",
         "",
@@ -107,6 +117,14 @@ def write_ninja() -> str:
         "  depfile = $out.d",
         "  deps = gcc",
         "  description = CXX(torch) $in",
+        "rule cxx_tool",
+        "  command = $cxx -MMD -MF $out.d -O2 -std=c++17 -fvisibility=hidden $tool_cflags -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = CXX(tool) $in",
+        "rule link_tool",
+        "  command = $cxx $in -o $out $tool_ldflags",
+        "  description = LINK $out",
         "rule link_ops",
         "  command = $hipcc $in -o $out $ops_ldflags",
         "  description = LINK $out",
@@ -135,6 +153,11 @@ def write_ninja() -> str:
         lines.append(f"build {_rel(o)}: cxx_bind {_rel(s)}")
     ops_so = os.path.join(PKG, "_ops" + suffix)
     lines.append(f"build {_rel(ops_so)}: link_ops " + " ".join(_rel(o) for o in ops_objs))
+    # standalone controller executable (reference controller_main.cc)
+    tool_src = os.path.join(csrc, "tools", "controller_main.cc")
+    tool_obj = os.path.join(BUILD_DIR, "tools", "controller_main.o")
+    lines.append(f"build {_rel(tool_obj)}: cxx_tool {_rel(tool_src)}")
+    lines.append(f"build metisfl_controller: link_tool {_rel(tool_obj)}")
     lines.append("")
     path = os.path.join(BUILD_DIR, "build.ninja")
     with open(path, "w") as f:
