@@ -1,6 +1,7 @@
 """BERT-path HIP kernels (bert.hip, gemm.hip) vs the fp32 CPU reference ops,
 and the BERT-tiny training step GPU vs CPU."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -196,6 +197,52 @@ def test_bert_tiny_step_gpu_vs_cpu():
     la = float(nets["cpu"].stats[0]) / float(nets["cpu"].stats[2])
     lb = float(nets[DEV].stats[0].cpu()) / float(nets[DEV].stats[2].cpu())
     assert abs(la - lb) < 0.02 * la
+
+
+def test_bert_tiny_step_tracks_torch_nn_oracle():
+    """The bf16 HIP BERT step vs an independent fp32 torch.nn BERT
+    (tests/torch_bert_ref.py) on the same master weights and records: loss
+    and the gradient of EVERY parameter tensor (cosine similarity; bf16
+    activations / GEMM operands bound the agreement)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from torch_bert_ref import TorchBertMLM
+
+    from metisfl_amd.datasets import synthetic_mlm
+    from metisfl_amd.models.bert import BERT_TINY, BertMLM
+    from metisfl_amd.ops.optim import OptimizerSpec
+    _native()
+    c = BERT_TINY
+    rec = synthetic_mlm(8, c.seq, c.max_pred, c.vocab, seed=5, rec_stride=c.rec_stride)
+    net = BertMLM(batch_size=8, device=DEV, seed=4, config=c, optimizer=OptimizerSpec("vanilla_sgd", 0.0))
+    net.zero_grad_in_optimizer = False
+    net._train_body(net.make_dataset(rec, shuffle=False))
+    torch.cuda.synchronize()
+    loss_gpu = float(net.stats[0].cpu()) / float(net.stats[2].cpu())
+    ref = TorchBertMLM(c)
+    ref.load_from_flat(net.state)
+    loss_ref = ref(torch.as_tensor(rec[:8]))
+    loss_ref.backward()
+    g_ref = ref.grads_like_flat()
+    num = den_a = den_b = 0.0
+    worst = []
+    for name, gr in g_ref.items():
+        gg = net.state.grad(name).detach().double().cpu().reshape(gr.shape)
+        gr = gr.double()
+        if name == "emb.word":  # rows of tokens that never occur get zero in both
+            gr, gg = gr[: c.vocab], gg[: c.vocab]
+        num += float((gg * gr).sum())
+        den_a += float((gg * gg).sum())
+        den_b += float((gr * gr).sum())
+        cs = float((gg * gr).sum() / (gg.norm() * gr.norm() + 1e-30))
+        worst.append((cs, name))
+    worst.sort()
+    cos = num / (den_a ** 0.5 * den_b ** 0.5)
+    print(f"bf16 BERT-tiny: loss {loss_gpu:.5f} vs torch.nn fp32 {float(loss_ref):.5f}; "
+          f"gradient cosine {cos:.5f}; lowest {worst[:3]}")
+    assert abs(loss_gpu - float(loss_ref)) < 0.01 * float(loss_ref)
+    assert cos > 0.99, (cos, worst[:5])
+    assert worst[0][0] > 0.95, worst[:5]
 
 
 def test_bert_base_graph_step_runs():
