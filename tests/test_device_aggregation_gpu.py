@@ -114,3 +114,23 @@ def test_pwa_device_is_byte_identical(tmp_path):
     assert host == dev
     out = c.decrypt(dev, 20_000)
     assert np.abs(out - sum(w * x for w, x in zip(ws, xs))).max() < 1e-6
+
+
+def test_grpc_controller_stages_and_aggregates_on_device(tmp_path):
+    """End to end: a gRPC controller with 6 echo learners (worker processes,
+    benchmarks/scalability.py) and a 4 MB model -- every learner's model is
+    staged into HBM on arrival and the rounds aggregate from there."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "benchmarks"))
+    import scalability
+    E.set_device_aggregation(True, 1 << 20)
+    s0 = E.device_aggregation_stats()
+    r = scalability.run_case(6, 4.0, rounds=2, workers=3, tmpdir=str(tmp_path))
+    s1 = r["device_aggregation"]
+    assert r["rounds_measured"] >= 2, r
+    assert s1["available"]
+    assert s1["staged_models"] - s0.get("staged_models", 0) >= 6 * 2
+    assert s1["fedavg_calls"] - s0.get("fedavg_calls", 0) >= 2
+    assert s1["resident_hits"] - s0.get("resident_hits", 0) >= 6 * 2
+    assert s1["cold_uploads"] == s0.get("cold_uploads", 0)
