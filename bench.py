@@ -63,6 +63,9 @@ def main() -> int:
                          "all-reduce of ciphertexts / device decrypt)")
     ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
                     help="compute precision: fp32 = reference precision (default), bf16 = mixed")
+    ap.add_argument("--conv-products", choices=("exact", "bf16x3"), default=None,
+                    help="fp32 convolution products: exact fp32 MFMA, or bf16x3 split products "
+                         "with fp32 storage/accumulation (default: ResNet18's default)")
     ap.add_argument("--width-mult", type=float, default=1.0, help=argparse.SUPPRESS)  # CPU plumbing tests only
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
@@ -98,7 +101,7 @@ def main() -> int:
 
     opt = OptimizerSpec("momentum_sgd", args.lr, momentum=args.momentum)
     net = ResNet18(batch_size=args.batch, device=dev, optimizer=opt, seed=7, dtype=args.dtype,
-                   width_mult=args.width_mult)
+                   width_mult=args.width_mult, conv_products=args.conv_products)
     train_ds = net.make_dataset(xtr, ytr, seed=comm.rank)
     test_ds = net.make_dataset(xte, yte, seed=comm.rank, shuffle=False)
     del xtr, xte
@@ -176,6 +179,7 @@ def main() -> int:
             "protocol": "synchronous",
             "parallelism": f"fedavg-dp{n}",
             "test_eval": not args.no_eval,
+            **({"conv_products": net.conv_products} if args.dtype == "fp32" else {}),
             **({"width_mult": args.width_mult} if args.width_mult != 1.0 else {}),
         },
         "round_ms": round_ms,

@@ -11,6 +11,18 @@
 
 namespace {
 
+// Convolution product mode of the fp32 path: 0 = exact fp32 MFMA (mfl::c32x),
+// 1 = bf16x3 split products with fp32 accumulation (mfl::c32s).  Process-wide,
+// set before a model captures its graph.
+int g_c32_mode = 0;
+#define C32_CALL(fn, ...) (g_c32_mode ? mfl::c32s::fn(__VA_ARGS__) : mfl::c32x::fn(__VA_ARGS__))
+
+void set_conv32_mode(int64_t m) {
+  TORCH_CHECK(m == 0 || m == 1, "conv32 mode is 0 (exact fp32) or 1 (bf16x3)");
+  g_c32_mode = (int)m;
+}
+int64_t conv32_mode() { return g_c32_mode; }
+
 hipStream_t cur_stream(const torch::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
 
 void check_f32(const torch::Tensor& t, int64_t numel, const char* nm, bool exact = true) {
@@ -65,8 +77,8 @@ mfl::ConvGeom dgrad_geom(int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co,
 constexpr int64_t kCounterWords = 1024;
 int64_t ws_floats(const mfl::ConvGeom& g, const mfl::ConvPlan& p) {
   if (p.splits <= 1) return 0;
-  TORCH_CHECK(mfl::conv32_counter_slots(g, p) <= kCounterWords, "split-K plan has too many tiles");
-  return kCounterWords + (int64_t)p.splits * mfl::conv32_counter_slots(g, p) * p.bm * p.bn;
+  TORCH_CHECK(C32_CALL(conv32_counter_slots, g, p) <= kCounterWords, "split-K plan has too many tiles");
+  return kCounterWords + (int64_t)p.splits * C32_CALL(conv32_counter_slots, g, p) * p.bm * p.bn;
 }
 
 // mode 0 fwd / 1 dgrad / 2 wgrad -> [bm, bn, splits, kchunk, stats_rows, workspace_floats]
@@ -74,18 +86,18 @@ std::vector<int64_t> conv32_plan(int64_t mode, int64_t N, int64_t H, int64_t W, 
                                  int64_t S, int64_t stride, int64_t pad) {
   if (mode == 2) {
     const auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
-    const auto p = mfl::plan_conv32(g, 2);
+    const auto p = C32_CALL(plan_conv32, g, 2);
     return {p.bm, p.bn, p.splits, p.kchunk, 0, 0};
   }
   const auto g = mode == 0 ? fwd_geom(N, H, W, C, Co, R, S, stride, pad) : dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
-  const auto p = mfl::plan_conv32(g, (int)mode);
+  const auto p = C32_CALL(plan_conv32, g, (int)mode);
   return {p.bm, p.bn, p.splits, p.kchunk, mode == 0 ? 1 : 0, ws_floats(g, p)};
 }
 
 void run(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const torch::Tensor& w, const torch::Tensor& y,
          const c10::optional<torch::Tensor>& ws, double* stats, bool accum, const mfl::BnBwdFusion32* bnb,
          int stats_reps = 1) {
-  const auto p = mfl::plan_conv32(g, dgrad ? 1 : 0);
+  const auto p = C32_CALL(plan_conv32, g, dgrad ? 1 : 0);
   float* slab = nullptr;
   int* counters = nullptr;
   if (p.splits > 1) {
@@ -94,7 +106,7 @@ void run(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const tor
     counters = reinterpret_cast<int*>(ws->data_ptr<float>());
     slab = ws->data_ptr<float>() + kCounterWords;
   }
-  mfl::launch_conv32_gemm(g, dgrad, p, fp(src), fp(w), fp(y), slab, counters, stats, accum, bnb, cur_stream(y),
+  C32_CALL(launch_conv32_gemm, g, dgrad, p, fp(src), fp(w), fp(y), slab, counters, stats, accum, bnb, cur_stream(y),
                           stats_reps);
 }
 
@@ -176,8 +188,8 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
     f.acc = stats_ptr(bn_acc, C);
     f.reps = reps_of(*bn_acc, C);
   }
-  const auto pd = mfl::plan_conv32(gd, 1);
-  const auto pw = mfl::plan_conv32(gf, 2);
+  const auto pd = C32_CALL(plan_conv32, gd, 1);
+  const auto pw = C32_CALL(plan_conv32, gf, 2);
   float* slab = nullptr;
   int* counters = nullptr;
   if (pd.splits > 1) {
@@ -186,11 +198,11 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
     counters = reinterpret_cast<int*>(ws->data_ptr<float>());
     slab = ws->data_ptr<float>() + kCounterWords;
   }
-  if (mfl::launch_conv32_bwd_pair(gd, pd, gf, pw, fp(dy), fp(w), fp(dx), slab, counters, accumulate,
+  if (C32_CALL(launch_conv32_bwd_pair, gd, pd, gf, pw, fp(dy), fp(w), fp(dx), slab, counters, accumulate,
                                   fuse ? &f : nullptr, fp(x), fp(dw), cur_stream(dx)))
     return;
-  mfl::launch_conv32_wgrad(gf, pw, fp(x), fp(dy), fp(dw), true, cur_stream(dw));
-  mfl::launch_conv32_gemm(gd, true, pd, fp(dy), fp(w), fp(dx), slab, counters, nullptr, accumulate,
+  C32_CALL(launch_conv32_wgrad, gf, pw, fp(x), fp(dy), fp(dw), true, cur_stream(dw));
+  C32_CALL(launch_conv32_gemm, gd, true, pd, fp(dy), fp(w), fp(dx), slab, counters, nullptr, accumulate,
                           fuse ? &f : nullptr, cur_stream(dx));
 }
 
@@ -200,9 +212,9 @@ void conv32_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t N
   check_f32(x, (int64_t)N * H * W * C, "x");
   check_f32(dy, (int64_t)g.M * Co, "dy");
   check_f32(dw, (int64_t)Co * R * S * C, "dw");
-  const auto p = mfl::plan_conv32(g, 2);
+  const auto p = C32_CALL(plan_conv32, g, 2);
   if (!accumulate && p.splits > 1) dw.zero_();
-  mfl::launch_conv32_wgrad(g, p, fp(x), fp(dy), fp(dw), accumulate, cur_stream(dw));
+  C32_CALL(launch_conv32_wgrad, g, p, fp(x), fp(dy), fp(dw), accumulate, cur_stream(dw));
 }
 
 // ---- BatchNorm -----------------------------------------------------------
@@ -297,7 +309,7 @@ void conv32_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c1
   check_f32(w2, Co * C, "w2");
   check_f32(y1, (int64_t)g1.M * Co, "y1");
   check_f32(y2, (int64_t)g2.M * Co, "y2");
-  const auto p1 = mfl::plan_conv32(g1, 0), p2 = mfl::plan_conv32(g2, 0);
+  const auto p1 = C32_CALL(plan_conv32, g1, 0), p2 = C32_CALL(plan_conv32, g2, 0);
   auto slab = [&](const mfl::ConvGeom& g, const mfl::ConvPlan& p, const c10::optional<torch::Tensor>& ws,
                   float*& ys, int*& cn) {
     ys = nullptr;
@@ -316,7 +328,7 @@ void conv32_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c1
   double* st1 = stats_ptr(stats1, Co);
   double* st2 = stats_ptr(stats2, Co);
   const int r1 = st1 ? reps_of(*stats1, Co) : 1, r2 = st2 ? reps_of(*stats2, Co) : 1;
-  if (mfl::launch_conv32_fwd_pair(g1, p1, fp(w1), fp(y1), ys1, c1, st1, r1, g2, p2, fp(w2), fp(y2), ys2, c2, st2, r2,
+  if (C32_CALL(launch_conv32_fwd_pair, g1, p1, fp(w1), fp(y1), ys1, c1, st1, r1, g2, p2, fp(w2), fp(y2), ys2, c2, st2, r2,
                                   fp(x), cur_stream(x)))
     return;
   run(g1, false, x, w1, y1, ws1, st1, false, nullptr, r1);
@@ -436,6 +448,8 @@ void gather_batch32(torch::Tensor shard, torch::Tensor labels, torch::Tensor per
 }  // namespace
 
 void register_fp32(pybind11::module& m) {
+  m.def("set_conv32_mode", &set_conv32_mode);
+  m.def("conv32_mode", &conv32_mode);
   m.def("conv32_plan", &conv32_plan);
   m.def("conv32_forward", &conv32_forward);
   m.def("conv32_dgrad", &conv32_dgrad);

@@ -144,9 +144,16 @@ def write_ninja() -> str:
 
     ops_objs = []
     for s in hip_srcs:
-        o = os.path.join(BUILD_DIR, "hip", os.path.basename(s) + ".o")
-        ops_objs.append(o)
-        lines.append(f"build {_rel(o)}: hipcc {_rel(s)}")
+        # conv32.hip is built once per product variant (exact fp32 / bf16x3;
+        # namespaces mfl::c32x / mfl::c32s, kernels/conv32.h)
+        variants = [("", "-DMFL_C32_BF16X3=0"), (".bf16x3", "-DMFL_C32_BF16X3=1")] \
+            if os.path.basename(s) == "conv32.hip" else [("", None)]
+        for tag, flag in variants:
+            o = os.path.join(BUILD_DIR, "hip", os.path.basename(s) + tag + ".o")
+            ops_objs.append(o)
+            lines.append(f"build {_rel(o)}: hipcc {_rel(s)}")
+            if flag:
+                lines.append(f"  hip_cflags = $hip_cflags {flag}")
     for s in ops_bind:
         o = os.path.join(BUILD_DIR, "bind", os.path.basename(s) + ".o")
         ops_objs.append(o)

@@ -47,32 +47,14 @@ struct BnBwdFusion32 {
   int reps = 1;
 };
 
-// mode 0 fwd, 1 dgrad, 2 wgrad.  kchunk in k elements (multiple of 32).
-ConvPlan plan_conv32(const ConvGeom& g, int mode);
-int conv32_counter_slots(const ConvGeom& g, const ConvPlan& p);
-
-// stats: [stats_reps][2][Ng] fp64 BN sums of the forward output (replicated
-// so that hundreds of workgroups do not serialise on the same 2*Ng addresses)
-void launch_conv32_gemm(const ConvGeom& g, bool dgrad, const ConvPlan& p, const float* src, const float* wgt,
-                        float* y, float* ysplit, int* counters, double* stats, bool accum,
-                        const BnBwdFusion32* bnb, hipStream_t s, int stats_reps = 1);
-// dw (fp32 OHWI); accumulate: dw holds a running sum (zero for a fresh step)
-// and every slice adds atomically; otherwise the split-1 plan stores and a
-// split plan requires dw zeroed by the caller.
-void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, const float* dy, float* dw,
-                         bool accumulate, hipStream_t s);
-// dgrad (gd, pd; role-swapped geometry) + wgrad (gf = the forward geometry,
-// pw; dw must hold zeros or a running sum: slices add atomically) of one
-// layer in one launch.  Returns false (nothing launched) when the two plans
-// do not both run 64x64 tiles on the fast address paths.
-// conv1 (3x3/s2, g1) + projection shortcut (1x1/s2, g2) of one x in one
-// launch; false (nothing launched) when the plans do not pair.
-bool launch_conv32_fwd_pair(const ConvGeom& g1, const ConvPlan& p1, const float* w1, float* y1, float* ys1,
-                            int* c1, double* st1, int reps1, const ConvGeom& g2, const ConvPlan& p2,
-                            const float* w2, float* y2, float* ys2, int* c2, double* st2, int reps2,
-                            const float* x, hipStream_t s);
-bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGeom& gf, const ConvPlan& pw,
-                            const float* dy, const float* w, float* dx, float* ysplit, int* counters, bool accum,
-                            const BnBwdFusion32* bnb, const float* x, float* dw, hipStream_t s);
+// The API exists twice: mfl::c32x (exact fp32 MFMA) and mfl::c32s (fp32
+// operands split into bf16 hi + lo, three bf16 MFMA products, fp32
+// accumulation); conv32.hip is compiled once per variant.
+namespace c32x {
+#include "kernels/conv32_api.inc"
+}
+namespace c32s {
+#include "kernels/conv32_api.inc"
+}
 
 }  // namespace mfl

@@ -9,6 +9,16 @@
 // exact fp32 FMA (cdna_hip_programming.md 'FP32-input MFMA').  The bf16 family
 // (conv.hip) stays as the explicit mixed-precision option.
 //
+// Second variant (MFL_C32_BF16X3=1, namespace mfl::c32s): same fp32 operands,
+// LDS staging, fp32 accumulators and outputs, but each k-tile's fragments are
+// split in registers into bf16 hi + lo and multiplied as hi*hi + hi*lo +
+// lo*hi on v_mfma_f32_32x32x16_bf16 (16x the fp32 MFMA rate, 3 products):
+// per-product relative error <= ~2^-17, 4e-6 measured on whole convolutions
+// (exact: 3e-7).  The fp32 MFMA shares the VALU datapath, so the exact loop
+// is MFMA-paced; the split loop is paced by its ~2.5 VALU per operand value
+// and by the fp32 operand bytes it streams -- 1.52 -> 1.22 ms per ResNet-18
+// step (profiles/r2/fp32_bf16x3_step_summary.txt).
+//
 // Design for CDNA4 (not a port of anything -- the reference has no kernels):
 //  * fp32 MFMA runs at 1/16 of the bf16 rate (64 FLOP/clk/SIMD), so here the
 //    step is COMPUTE-bound where the bf16 one is latency-bound: tiles are
@@ -46,7 +56,19 @@
 #include "kernels/conv32.h"
 #include "kernels/lds_tiles.h"
 
+// Built twice (csrc/build.py): MFL_C32_BF16X3=0 -> namespace mfl::c32x (exact
+// fp32 MFMA), =1 -> mfl::c32s (3-product bf16 split, see mma_tile).
+#ifndef MFL_C32_BF16X3
+#define MFL_C32_BF16X3 0
+#endif
+#if MFL_C32_BF16X3
+#define MFL_C32_VARIANT c32s
+#else
+#define MFL_C32_VARIANT c32x
+#endif
+
 namespace mfl {
+namespace MFL_C32_VARIANT {
 
 namespace {
 
@@ -61,6 +83,71 @@ constexpr int kCPR = kRowB / 16;     // 16-B chunks per row
 __device__ __forceinline__ f32x16 mfma_f32(float a, float b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f32x16 mfma_bf16x16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+
+// fp32 -> bf16 (hi, lo) with a = hi + lo + e, |e| <= 2^-18 |a|: hi = RNE(a),
+// a - hi is exact in fp32 (<= 16 significant bits), lo = RNE(a - hi).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16v2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk_bf16(f32x2 v) {  // one v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16v2));
+}
+// 20 VALU per 8 values: 4 cvt_pk, 8 unpack (shift / and), 4 v_pk_add_f32, 4 cvt_pk
+__device__ __forceinline__ void split_hl(const f32x4& p, const f32x4& q, bf16x8& hi, bf16x8& lo) {
+  const f32x2 v[4] = {{p[0], p[1]}, {p[2], p[3]}, {q[0], q[1]}, {q[2], q[3]}};
+  u32x4 h, l;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t w = cvt_pk_bf16(v[i]);
+    h[i] = w;
+    l[i] = cvt_pk_bf16(v[i] - f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)});
+  }
+  hi = __builtin_bit_cast(bf16x8, h);
+  lo = __builtin_bit_cast(bf16x8, l);
+}
+
+// One k-tile of MFMAs.  Exact mode: 32x32x2 fp32, MFMA (g, e) of lane half h
+// reduces k = 8g + 4h + e.  Split mode (3-product bf16): the two 4-k fragments
+// of groups 2g2 and 2g2+1 form one lane's 8 bf16 k-slots of a 32x32x16 MFMA
+// (k = 16g2 + {4h + e, 8 + 4h + e}); A and B use the same slots, so the
+// reduction is over the same k set and acc += Ahi Bhi + Ahi Blo + Alo Bhi.
+template <int TM, int TN, typename FA, typename FB>
+__device__ __forceinline__ void mma_tile(const FA& fa, const FB& fb, f32x16 (&acc)[TM][TN]) {
+#if MFL_C32_BF16X3
+#pragma unroll
+  for (int g2 = 0; g2 < kBK / 16; ++g2) {
+    bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) split_hl(fa[2 * g2][i], fa[2 * g2 + 1][i], ah[i], al[i]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) split_hl(fb[2 * g2][j], fb[2 * g2 + 1][j], bh[j], bl[j]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[i][j] = mfma_bf16x16(al[i], bh[j], acc[i][j]);
+        acc[i][j] = mfma_bf16x16(ah[i], bl[j], acc[i][j]);
+        acc[i][j] = mfma_bf16x16(ah[i], bh[j], acc[i][j]);
+      }
+  }
+#else
+#pragma unroll
+  for (int grp = 0; grp < kBK / 8; ++grp)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(fa[grp][i][e], fb[grp][j][e], acc[i][j]);
+#endif
+}
+// MFMA count / VALU budget per k-tile for the interleave pattern
+template <int TM, int TN>
+constexpr int kTileMfma = MFL_C32_BF16X3 ? 3 * (kBK / 16) * TM * TN : 4 * (kBK / 8) * TM * TN;
+constexpr int kTileValu = MFL_C32_BF16X3 ? 16 : 6;
 __device__ __forceinline__ int fdiv(int x, const FastDiv& f) {
   return (int)((__umulhi((uint32_t)x, f.m) >> f.sh) + ((uint32_t)x & f.id));
 }
@@ -514,15 +601,8 @@ __device__ __forceinline__ void conv32_gemm_body(const Conv32Args& a, const Blk&
   auto mma = [&](auto set) {
     constexpr int S = decltype(set)::value;
     if constexpr (MFL_C32_DBG & 1) return;
-#pragma unroll
-    for (int grp = 0; grp < kBK / 8; ++grp)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(fa[S][grp][i][e], fb[S][grp][j][e], acc[i][j]);
-    interleave_mfma<4 * kBK / 8 * TM * TN, 6>();
+    mma_tile<TM, TN>(fa[S], fb[S], acc);
+    interleave_mfma<kTileMfma<TM, TN>, kTileValu>();
     __builtin_amdgcn_sched_barrier(0);
   };
   ring_loop<NS, ACH + BCH>(nk, issue, read, mma);
@@ -747,15 +827,8 @@ __device__ __forceinline__ void conv32_wgrad_body(const Conv32Args& a, const Blk
   auto mma = [&](auto set) {
     constexpr int S = decltype(set)::value;
     if constexpr (MFL_C32_DBG & 1) return;
-#pragma unroll
-    for (int grp = 0; grp < kBK / 8; ++grp)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f32(fa[S][grp][i][e], fb[S][grp][j][e], acc[i][j]);
-    interleave_mfma<4 * kBK / 8 * TM * TN, 6>();
+    mma_tile<TM, TN>(fa[S], fb[S], acc);
+    interleave_mfma<kTileMfma<TM, TN>, kTileValu>();
     __builtin_amdgcn_sched_barrier(0);
   };
   ring_loop<NS, ACH + BCH>(nk, issue, read, mma);
@@ -927,6 +1000,23 @@ int conv32_counter_slots(const ConvGeom& g, const ConvPlan& p) {
 struct TunedPlan {
   int mode, n, h, w, c, co, r, stride, bm, bn, splits;
 };
+#if MFL_C32_BF16X3
+// profiles/r2/c32x3_sweep.log; dgrad / wgrad stay 64x64 where that lets the
+// layer's backward run as one paired launch
+constexpr TunedPlan kTuned[] = {
+    {0, 32, 32, 32, 8, 64, 3, 1, 128, 64, 1},   {0, 32, 32, 32, 64, 64, 3, 1, 128, 64, 1},
+    {0, 32, 32, 32, 64, 128, 3, 2, 64, 64, 1},  {0, 32, 16, 16, 128, 128, 3, 1, 64, 64, 2},
+    {0, 32, 16, 16, 128, 256, 3, 2, 64, 64, 4}, {0, 32, 8, 8, 256, 256, 3, 1, 64, 64, 4},
+    {0, 32, 8, 8, 256, 512, 3, 2, 64, 64, 4},   {0, 32, 4, 4, 512, 512, 3, 1, 64, 64, 8},
+    {1, 32, 32, 32, 64, 64, 3, 1, 64, 64, 1},   {1, 32, 32, 32, 64, 128, 3, 2, 64, 64, 1},
+    {1, 32, 32, 32, 64, 128, 1, 2, 64, 64, 1},  {1, 32, 16, 16, 128, 128, 3, 1, 64, 64, 3},
+    {1, 32, 16, 16, 128, 256, 3, 2, 64, 64, 3}, {1, 32, 8, 8, 256, 256, 3, 1, 64, 64, 4},
+    {1, 32, 8, 8, 256, 512, 3, 2, 64, 64, 4},   {1, 32, 4, 4, 512, 512, 3, 1, 64, 64, 8},
+    {2, 32, 16, 16, 128, 128, 3, 1, 64, 64, 14}, {2, 32, 16, 16, 128, 256, 3, 2, 64, 64, 7},
+    {2, 32, 8, 8, 256, 256, 3, 1, 64, 64, 3},   {2, 32, 8, 8, 256, 512, 3, 2, 64, 64, 2},
+    {2, 32, 4, 4, 512, 512, 3, 1, 64, 64, 1},
+};
+#else
 constexpr TunedPlan kTuned[] = {
     {0, 32, 8, 8, 256, 256, 3, 1, 64, 64, 4},   {0, 32, 8, 8, 256, 512, 1, 2, 64, 64, 1},
     {1, 32, 32, 32, 64, 64, 3, 1, 64, 64, 1},   {1, 32, 32, 32, 64, 128, 3, 2, 64, 64, 1},
@@ -934,6 +1024,7 @@ constexpr TunedPlan kTuned[] = {
     {2, 32, 8, 8, 256, 256, 3, 1, 64, 64, 3},   {2, 32, 8, 8, 256, 512, 3, 2, 64, 64, 2},
     {2, 32, 4, 4, 512, 512, 3, 1, 64, 64, 2},
 };
+#endif
 static void tuned_plan(const ConvGeom& g, int mode, int& bm, int& bn, int& sp) {
   const bool dg = mode == 1;
   const int h = dg ? g.P : g.H, w = dg ? g.Q : g.W, c = dg ? g.Ng : g.C, co = dg ? g.C : g.Ng;
@@ -976,7 +1067,10 @@ static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
       if (s_eff != sp) continue;
       if (mode != 2 && s_eff > 1 && tiles > 1024) continue;  // counter block size
       const int nwg = tiles * s_eff;
-      const double t_alone = (double)c.bm * c.bn * kt * kBK * 2 / 256.0 / clk + 1.2;
+      // split mode: VALU-paced (the operand splits), ~0.6x (64x64) / ~0.47x
+      // (larger wave tiles reuse each split) of the fp32-MFMA time
+      const double pace = MFL_C32_BF16X3 ? (c.bm == 64 && c.bn == 64 ? 0.6 : 0.47) : 1.0;
+      const double t_alone = pace * c.bm * c.bn * kt * kBK * 2 / 256.0 / clk + 1.2;
       const int full = nwg / slots, rem = nwg % slots;
       double tt = full * occ * t_alone + (rem ? (rem > 256 ? occ : 1) * t_alone : 0.0);
       if (s_eff > 1) {
@@ -1178,4 +1272,5 @@ bool launch_conv32_fwd_pair(const ConvGeom& g1, const ConvPlan& p1, const float*
   return true;
 }
 
+}  // namespace MFL_C32_VARIANT
 }  // namespace mfl

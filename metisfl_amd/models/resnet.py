@@ -16,8 +16,16 @@ Keras trains fp32 (examples/keras/models/cifar_cnn.py:19-41, no
 mixed-precision policy; keras_model_ops.py:117-197) -- on the exact fp32 MFMA
 kernels (conv32.hip / bn32.hip).  ``dtype="bf16"`` is the mixed-precision
 option (bf16 activations and weights, fp32 master / accumulation).
+
+``conv_products`` picks how the fp32 convolutions form their products
+(ops/nn.py ``set_conv_products``): ``"exact"`` fp32 MFMA or ``"bf16x3"``
+split products with fp32 storage and accumulation (relative error ~4e-6 per
+convolution).  Default: ``METISFL_AMD_CONV_PRODUCTS`` or
+:data:`DEFAULT_CONV_PRODUCTS`.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -25,6 +33,11 @@ from metisfl_amd.models.layers import BasicBlock, ClassifierHead, ConvBN
 from metisfl_amd.models.net import StaticNet
 
 DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16}
+DEFAULT_CONV_PRODUCTS = "bf16x3"
+
+
+def default_conv_products() -> str:
+    return os.environ.get("METISFL_AMD_CONV_PRODUCTS", DEFAULT_CONV_PRODUCTS)
 
 
 class ResNet18(StaticNet):
@@ -33,8 +46,14 @@ class ResNet18(StaticNet):
     widths = (64, 128, 256, 512)
 
     def __init__(self, batch_size: int = 32, device="cpu", optimizer=None, seed: int = 0,
-                 width_mult: float = 1.0, num_classes: int = 10, dtype: str = "fp32"):
+                 width_mult: float = 1.0, num_classes: int = 10, dtype: str = "fp32",
+                 conv_products: str | None = None):
         self.compute_dtype = DTYPES[dtype]
+        self.conv_products = conv_products or default_conv_products()
+        if dtype == "fp32" and torch.device(device).type == "cuda":
+            # before any plan / workspace is sized and before graph capture
+            from metisfl_amd.ops.nn import set_conv_products
+            set_conv_products(self.conv_products)
         self.width_mult = width_mult
         self.num_classes = num_classes
         super().__init__(batch_size, device, optimizer, seed)

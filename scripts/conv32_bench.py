@@ -47,7 +47,10 @@ def main():
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--modes", default="0,1,2")
+    ap.add_argument("--products", default="exact", choices=("exact", "bf16x3"))
     a = ap.parse_args()
+    K.set_conv_products(a.products)
+    print("conv products:", a.products)
     dev = torch.device("cuda")
     ws = torch.zeros(16 << 20, device=dev)
     total = {0: 0.0, 1: 0.0, 2: 0.0}

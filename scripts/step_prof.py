@@ -20,8 +20,9 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--conv-products", default=None, choices=(None, "exact", "bf16x3"))
     a = ap.parse_args()
-    net = ResNet18(batch_size=a.batch, device="cuda", seed=7, dtype=a.dtype,
+    net = ResNet18(batch_size=a.batch, device="cuda", seed=7, dtype=a.dtype, conv_products=a.conv_products,
                    optimizer=OptimizerSpec("momentum_sgd", 0.005, momentum=0.75))
     g = torch.Generator(device="cuda").manual_seed(0)
     x = torch.randn((2048, 32, 32, 3), generator=g, device="cuda")
@@ -33,7 +34,8 @@ def main():
     net.train_steps(ds, a.steps, a.warmup)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) * 1e3 / a.steps
-    print(f"{a.dtype} batch {a.batch}: {dt:.4f} ms per local update "
+    tag = f"{a.dtype}/{net.conv_products}" if a.dtype == "fp32" else a.dtype
+    print(f"{tag} batch {a.batch}: {dt:.4f} ms per local update "
           f"({a.batch / dt * 1e3:.0f} samples/s), loss {net.train_stats()['loss']:.4f}", flush=True)
 
 

@@ -48,6 +48,22 @@ ODD_SHAPES = [
 ]
 
 
+@pytest.fixture(autouse=True)
+def _exact_after():
+    yield
+    from metisfl_amd.ops import nn as K
+    K.set_conv_products("exact")
+
+
+@pytest.fixture(params=["exact", "bf16x3"])
+def products(request):
+    """Both fp32 convolution product modes (ops/nn.py set_conv_products)."""
+    from metisfl_amd.ops import nn as K
+    K.set_conv_products(request.param)
+    yield request.param
+    K.set_conv_products("exact")
+
+
 def _shape(t):
     from metisfl_amd.ops.nn import ConvShape
     N, H, W, C, Co, k, s = t
@@ -61,7 +77,7 @@ def _ws(shp):
 
 
 @pytest.mark.parametrize("t", RESNET_SHAPES + ODD_SHAPES, ids=lambda t: "x".join(map(str, t)))
-def test_conv32_forward_matches_fp64(t):
+def test_conv32_forward_matches_fp64(t, products):
     from metisfl_amd.ops import nn as K
     shp = _shape(t)
     g = torch.Generator().manual_seed(hash(t) & 0xFFFF)
@@ -76,7 +92,11 @@ def test_conv32_forward_matches_fp64(t):
     torch.cuda.synchronize()
     assert _rel(y, ref) <= 1e-5
     r2 = ref.reshape(-1, shp.Co)
-    assert _rel(stats[:shp.Co], r2.sum(0)) <= 1e-5
+    if products == "exact":
+        assert _rel(stats[:shp.Co], r2.sum(0)) <= 1e-5
+    else:  # a channel sum cancels: bound the error by the sum of magnitudes
+        err = (stats[:shp.Co].cpu() - r2.sum(0)).norm() / r2.abs().sum(0).norm()
+        assert err <= 1e-5, float(err)
     assert _rel(stats[shp.Co:], (r2 * r2).sum(0)) <= 1e-5
     # the split-K counters re-arm: a second launch gives the same bits
     y2 = torch.zeros_like(y)
@@ -87,7 +107,7 @@ def test_conv32_forward_matches_fp64(t):
 
 @pytest.mark.parametrize("t", [s for s in RESNET_SHAPES if s[3] != 8] + ODD_SHAPES,
                          ids=lambda t: "x".join(map(str, t)))
-def test_conv32_backward_pair_matches_fp64(t):
+def test_conv32_backward_pair_matches_fp64(t, products):
     """The paired dgrad + wgrad launch (conv32_bwd_pair_kernel, or its
     two-launch fallback for shapes that do not pair) vs fp64 references."""
     from metisfl_amd.ops import nn as K
@@ -111,7 +131,7 @@ def test_conv32_backward_pair_matches_fp64(t):
 
 
 @pytest.mark.parametrize("t", RESNET_SHAPES + ODD_SHAPES, ids=lambda t: "x".join(map(str, t)))
-def test_conv32_dgrad_matches_fp64(t):
+def test_conv32_dgrad_matches_fp64(t, products):
     from metisfl_amd.ops import nn as K
     shp = _shape(t)
     g = torch.Generator().manual_seed(7 + (hash(t) & 0xFFFF))
@@ -133,7 +153,7 @@ def test_conv32_dgrad_matches_fp64(t):
     assert _rel(dx2, ref + base.double()) <= 1e-5
 
 
-def test_conv32_dgrad_fused_bn_reductions():
+def test_conv32_dgrad_fused_bn_reductions(products):
     from metisfl_amd.ops import nn as K
     shp = _shape((32, 16, 16, 128, 128, 3, 1))
     g = torch.Generator().manual_seed(11)
@@ -156,7 +176,7 @@ def test_conv32_dgrad_fused_bn_reductions():
 
 
 @pytest.mark.parametrize("t", RESNET_SHAPES + ODD_SHAPES, ids=lambda t: "x".join(map(str, t)))
-def test_conv32_wgrad_matches_fp64(t):
+def test_conv32_wgrad_matches_fp64(t, products):
     from metisfl_amd.ops import nn as K
     shp = _shape(t)
     g = torch.Generator().manual_seed(3 + (hash(t) & 0xFFFF))
@@ -250,9 +270,11 @@ def _x8(x):
     return F.pad(torch.as_tensor(x), (0, 5))
 
 
-def test_fp32_resnet18_step_matches_torch_nn():
+@pytest.mark.parametrize("conv_products", ["exact", "bf16x3"])
+def test_fp32_resnet18_step_matches_torch_nn(conv_products):
     """The whole fp32 training step (gather -> 20 conv/BN layers -> head ->
-    backward) vs an independent torch.nn ResNet-18 in fp64."""
+    backward) vs an independent torch.nn ResNet-18 in fp64, for both fp32
+    convolution product modes."""
     from metisfl_amd.models.resnet import ResNet18
     from metisfl_amd.ops.optim import OptimizerSpec
     from tests.torch_resnet_ref import reference_step
@@ -260,7 +282,8 @@ def test_fp32_resnet18_step_matches_torch_nn():
     B = 32
     x = rng.standard_normal((B, 32, 32, 3)).astype(np.float32)
     y = rng.integers(0, 10, B)
-    net = ResNet18(batch_size=B, device=DEV, optimizer=OptimizerSpec("vanilla_sgd", 0.0), seed=4)
+    net = ResNet18(batch_size=B, device=DEV, optimizer=OptimizerSpec("vanilla_sgd", 0.0), seed=4,
+                   conv_products=conv_products)
     assert net.compute_dtype == torch.float32
     values = net.state.to_numpy()
     ds = net.make_dataset(x, y, shuffle=False)
@@ -278,7 +301,9 @@ def test_fp32_resnet18_step_matches_torch_nn():
              for n, l in [("stem", net.stem)] + [(c.name, c) for b in net.blocks for c in (b.c1, b.c2)]}
     flips = [0]
     ref_loss, ref_g, ref_run = reference_step(values, _x8(x), torch.as_tensor(y), relu_masks=masks, flips=flips)
-    assert flips[0] <= 8, flips
+    # bf16x3 products carry ~15x the exact mode's per-element error, so
+    # proportionally more near-zero pre-activations flip sign
+    assert flips[0] <= (8 if conv_products == "exact" else 160), flips
     assert abs(loss - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss)), (loss, ref_loss)
     worst = []
     for name, rg in ref_g.items():
