@@ -158,8 +158,23 @@ __device__ __forceinline__ int fdiv(int x, const FastDiv& f) {
 struct Blk {
   int x, y, z, gx, gy, gz;
 };
+// XCD-grouped block order.  The hardware deals workgroups round-robin over the
+// 8 XCDs (b % 8), so the 8 tiles dispatched together -- neighbouring output
+// rows that share their 3x3 halo rows -- land on 8 different L2s (measured L2
+// hit rate of the bf16x3 forward: 62 %).  Within each chunk of 64 dispatched
+// blocks, XCD x takes the 8 consecutive virtual tiles [8x, 8x + 8): the
+// dispatch order (dgrad-before-wgrad in the paired launches, split-K slices
+// 256 apart on one XCD) is kept at 64-block granularity.  (A global
+// XCD-contiguous order lost that ordering: 1.22 -> 1.30 ms.)
+__device__ __forceinline__ int xcd_group(int b, int n) {
+  const int base = b & ~63;
+  if (base + 64 > n) return b;  // ragged last chunk: hardware order
+  return base + ((b & 7) << 3) + ((b >> 3) & 7);
+}
 __device__ __forceinline__ Blk hw_blk() {
-  return Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z};
+  const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+  const int v = xcd_group(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gz);
+  return Blk{v % gx, (v / gx) % gy, v / (gx * gy), gx, gy, gz};
 }
 
 // DMA offset, or past every buffer range when !ok -- bitwise, so hipcc keeps
@@ -870,7 +885,7 @@ template <int NS>
 __global__ __launch_bounds__(256, 2) void conv32_fwd_pair_kernel(Conv32Args a1, Conv32Args a2, int n1, int g1x,
                                                                  int g1y, int g2x, int g2y, int g2z) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int b = blockIdx.x;
+  const int b = xcd_group(blockIdx.x, gridDim.x);
   if (b < n1) {
     const Blk k{b % g1x, (b / g1x) % g1y, b / (g1x * g1y), g1x, g1y, n1 / (g1x * g1y)};
     conv32_gemm_body<64, 64, false, 3, 2, false, NS, false>(a1, k, smem);
@@ -886,7 +901,7 @@ __global__ __launch_bounds__(256, 2) void conv32_bwd_pair_kernel(Conv32Args ad, 
                                                                  int atomic, int nd, int gdx, int gdy, int gwx,
                                                                  int gwy, int gwz) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int b = blockIdx.x;
+  const int b = xcd_group(blockIdx.x, gridDim.x);
   if (b < nd) {
     const Blk k{b % gdx, (b / gdx) % gdy, b / (gdx * gdy), gdx, gdy, nd / (gdx * gdy)};
     conv32_gemm_body<64, 64, true, KS, ST, PAR, NS, false>(ad, k, smem);
