@@ -64,6 +64,8 @@ class Learner:
         self.validation_dataset = resolve_dataset(validation_dataset, paths.get("validation"), cls)
         self.test_dataset = resolve_dataset(test_dataset, paths.get("test"), cls)
         self._client = GRPCControllerClient(controller_server_entity, max_workers=1)
+        self._client.retry_sleep_s = 1.0
+        self.completion_retries = 60
         cred = learner_credentials_fp or os.path.join(
             "/tmp/metis_amd", f"learner_{learner_server_entity.port}_credentials")
         os.makedirs(cred, exist_ok=True)
@@ -130,7 +132,11 @@ class Learner:
             MetisLogger.error("learner %s: completed a task but never joined; result dropped",
                               self.host_port_identifier())
             return
-        self._client.mark_task_completed(self.learner_id, self.auth_token, fut.result(), block=False)
+        # A completed task must survive a controller restart (the
+        # restored controller waits for this round's results): retry while the
+        # controller is UNAVAILABLE, for up to ~1 minute.
+        self._client.mark_task_completed(self.learner_id, self.auth_token, fut.result(),
+                                         request_retries=self.completion_retries, block=False)
 
     def run_learning_task(self, learning_task_pb, hyperparameters_pb, model_pb,
                           cancel_running_tasks=True, block=False, verbose=False) -> bool:
@@ -183,6 +189,7 @@ class Learner:
                  cancel_infer_running_tasks=True):
         if cancel_train_running_tasks:
             self._cancel.set()
+        self._client.cancel_retries()
         self._train_pool.shutdown(wait=True, cancel_futures=cancel_train_running_tasks)
         self._eval_pool.shutdown(wait=not cancel_eval_running_tasks, cancel_futures=cancel_eval_running_tasks)
         self.model_ops.cleanup()

@@ -15,7 +15,7 @@
 from __future__ import annotations
 
 import queue
-import time
+import threading
 from concurrent import futures
 
 import grpc
@@ -25,6 +25,12 @@ from metisfl_amd.utils.ssl_configurator import SSLConfigurator
 
 MAX_MSG_OPTIONS = [("grpc.max_send_message_length", -1),
                    ("grpc.max_receive_message_length", -1)]
+# Client channels reconnect within ~2 s of a peer coming back (gRPC's default
+# back-off grows to 120 s, so after a controller restart a learner's channel
+# could stay in TRANSIENT_FAILURE long after the new controller listens).
+CLIENT_OPTIONS = MAX_MSG_OPTIONS + [("grpc.initial_reconnect_backoff_ms", 200),
+                                    ("grpc.min_reconnect_backoff_ms", 200),
+                                    ("grpc.max_reconnect_backoff_ms", 2000)]
 
 
 class GRPCEndpoint:
@@ -37,8 +43,8 @@ def make_channel(server_entity) -> grpc.Channel:
     endpoint = GRPCEndpoint(server_entity).listening_endpoint
     cert, _ = SSLConfigurator.load_certificates_from_ssl_config_pb(server_entity.ssl_config, as_stream=True)
     if cert:
-        return grpc.secure_channel(endpoint, grpc.ssl_channel_credentials(cert), options=MAX_MSG_OPTIONS)
-    return grpc.insecure_channel(endpoint, options=MAX_MSG_OPTIONS)
+        return grpc.secure_channel(endpoint, grpc.ssl_channel_credentials(cert), options=CLIENT_OPTIONS)
+    return grpc.insecure_channel(endpoint, options=CLIENT_OPTIONS)
 
 
 class GRPCChannelMaxMsgLength:
@@ -56,21 +62,31 @@ class GRPCServerClient:
         self.grpc_endpoint = GRPCEndpoint(server_entity)
         self.executor = futures.ThreadPoolExecutor(max_workers=max_workers)
         self.executor_pool: "queue.Queue[futures.Future]" = queue.Queue()
+        self._closing = threading.Event()
         self._channel = make_channel(server_entity)
 
     def get_channel(self):
         return self._channel
 
+    # a retry cannot change these answers
+    FINAL_CODES = (grpc.StatusCode.INVALID_ARGUMENT, grpc.StatusCode.NOT_FOUND, grpc.StatusCode.ALREADY_EXISTS,
+                   grpc.StatusCode.PERMISSION_DENIED, grpc.StatusCode.UNAUTHENTICATED,
+                   grpc.StatusCode.UNIMPLEMENTED)
+
     def request_with_timeout(self, request_fn, request_timeout, request_retries):
         response = None
         for attempt in range(max(1, request_retries)):
+            if self._closing.is_set():
+                break
             try:
                 return request_fn(request_timeout)
             except grpc.RpcError as err:
                 MetisLogger.info("Exception raised: %s, retrying (%d/%d)...", err.code(), attempt + 1,
                                  request_retries)
+                if err.code() in self.FINAL_CODES:
+                    break
                 if err.code() == grpc.StatusCode.UNAVAILABLE and attempt + 1 < request_retries:
-                    time.sleep(self.retry_sleep_s)
+                    self._closing.wait(self.retry_sleep_s)  # shutdown() cuts the back-off short
         return response
 
     def _schedule(self, request_fn, request_retries, request_timeout, block):
@@ -83,7 +99,12 @@ class GRPCServerClient:
         self.executor_pool.put(fut)
         return fut
 
+    def cancel_retries(self):
+        """Pending and future retry loops give up (no new back-off sleeps)."""
+        self._closing.set()
+
     def shutdown(self):
+        self._closing.set()
         self.executor.shutdown(wait=True)
         self._channel.close()
 
