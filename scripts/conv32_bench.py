@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--modes", default="0,1,2")
     ap.add_argument("--products", default="exact", choices=("exact", "bf16x3"))
+    ap.add_argument("--stats-reps", type=int, default=1,
+                    help="forward BN-statistics accumulator replicas (0: no statistics)")
     a = ap.parse_args()
     K.set_conv_products(a.products)
     print("conv products:", a.products)
@@ -60,7 +62,7 @@ def main():
         x = torch.randn(N, H, W, C, device=dev)
         w = torch.randn(Co, k, k, C, device=dev) * 0.05
         y = torch.zeros(N, shp.P, shp.Q, Co, device=dev)
-        st = torch.zeros(2 * Co, dtype=torch.float64, device=dev)
+        st = torch.zeros(2 * Co * max(1, a.stats_reps), dtype=torch.float64, device=dev) if a.stats_reps else None
         dy = torch.randn(N, shp.P, shp.Q, Co, device=dev)
         dx = torch.zeros(N, H, W, C, device=dev)
         dw = torch.zeros(Co, k, k, C, device=dev)
