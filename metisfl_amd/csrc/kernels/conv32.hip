@@ -1019,7 +1019,7 @@ struct TunedPlan {
 // profiles/r2/c32x3_sweep.log; dgrad / wgrad stay 64x64 where that lets the
 // layer's backward run as one paired launch
 constexpr TunedPlan kTuned[] = {
-    {0, 32, 32, 32, 8, 64, 3, 1, 128, 64, 1},   {0, 32, 32, 32, 64, 64, 3, 1, 128, 64, 1},
+    {0, 32, 32, 32, 8, 64, 3, 1, 64, 64, 1},    {0, 32, 32, 32, 64, 64, 3, 1, 128, 64, 1},
     {0, 32, 32, 32, 64, 128, 3, 2, 64, 64, 1},  {0, 32, 16, 16, 128, 128, 3, 1, 64, 64, 2},
     {0, 32, 16, 16, 128, 256, 3, 2, 64, 64, 4}, {0, 32, 8, 8, 256, 256, 3, 1, 64, 64, 4},
     {0, 32, 8, 8, 256, 512, 3, 2, 64, 64, 4},   {0, 32, 4, 4, 512, 512, 3, 1, 64, 64, 8},
