@@ -73,6 +73,16 @@ void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_
 
 constexpr int kMaxReps = 8;  // replicas summed per channel (layers.py uses 8 on the fp32 GPU path)
 
+// Grid of the apply kernels.  Every block's prologue re-derives all C
+// channels' coefficients from the 8 fp64 replica pairs (16 loads per
+// channel): at one float4 per thread (2,048 blocks) that is 2,048 x C x 128 B
+// of L2 reads -- 67 MB for a C = 512 layer whose payload is 4 MB.  Capping the
+// grid amortises the prologue over several vectors per thread.
+#ifndef MFL_BN32_GRID
+#define MFL_BN32_GRID 512
+#endif
+inline unsigned apply_grid(int64_t nvec) { return stream_grid(nvec, 256, MFL_BN32_GRID); }
+
 // Sum of a channel's replicas: every load issued before the first add (a
 // runtime-bound loop serialised one memory round trip per replica).
 __device__ __forceinline__ void rep_sums(const double* acc, int reps, int C, int c, double& s0, double& s1) {
@@ -182,14 +192,14 @@ __global__ __launch_bounds__(256) void bn32_apply_pair_kernel(BnFwdArgs32 a1, in
 
 void launch_bn32_apply_pair(const BnFwdArgs32& a1, const BnFwdArgs32& a2, hipStream_t s) {
   const int64_t n1 = a1.M * a1.C / 4, n2 = a2.M * a2.C / 4;
-  const unsigned g1 = stream_grid(n1, 256, 2048), g2 = stream_grid(n2, 256, 2048);
+  const unsigned g1 = apply_grid(n1), g2 = apply_grid(n2);
   const size_t sm = 2 * (size_t)(a1.C > a2.C ? a1.C : a2.C) * sizeof(float);
   bn32_apply_pair_kernel<<<g1 + g2, 256, sm, s>>>(a1, n1, (int)g1, a2, n2);
 }
 
 void launch_bn32_apply(const BnFwdArgs32& a, hipStream_t s) {
   const int64_t nvec = a.M * a.C / 4;
-  const unsigned g = stream_grid(nvec, 256, 2048);
+  const unsigned g = apply_grid(nvec);
   const size_t sm = 2 * a.C * sizeof(float);
   if (a.residual) {
     if (a.relu) bn32_apply_kernel<true, true><<<g, 256, sm, s>>>(a, nvec);
@@ -337,7 +347,7 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
 
 void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s) {
   const int64_t nvec = a.M * a.C / 4;
-  const unsigned g = stream_grid(nvec, 256, 2048);
+  const unsigned g = apply_grid(nvec);
   const size_t sm = 5 * a.C * sizeof(float);
   if (a.y) {
     if (a.dy_masked) bn32_bwd_apply_kernel<true, true><<<g, 256, sm, s>>>(a, nvec);
