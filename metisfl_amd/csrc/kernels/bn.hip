@@ -174,14 +174,14 @@ __global__ __launch_bounds__(256) void bn_apply_pair_kernel(BnFwdArgs a1, int64_
 
 void launch_bn_apply_pair(const BnFwdArgs& a1, const BnFwdArgs& a2, hipStream_t s) {
   const int64_t n1 = a1.M * a1.C / 8, n2 = a2.M * a2.C / 8;
-  const unsigned g1 = stream_grid(n1, 256, 2048), g2 = stream_grid(n2, 256, 2048);
+  const unsigned g1 = stream_grid(n1, 256, 512), g2 = stream_grid(n2, 256, 512);
   const size_t sm = 2 * (size_t)(a1.C > a2.C ? a1.C : a2.C) * sizeof(float);
   bn_apply_pair_kernel<<<g1 + g2, 256, sm, s>>>(a1, n1, (int)g1, a2, n2);
 }
 
 void launch_bn_apply(const BnFwdArgs& a, hipStream_t s) {
   const int64_t nvec = a.M * a.C / 8;
-  const unsigned g = stream_grid(nvec, 256, 2048);
+  const unsigned g = stream_grid(nvec, 256, 512);  // see bn32.hip apply_grid
   const size_t sm = 2 * a.C * sizeof(float);
   if (a.residual) {
     if (a.relu) bn_apply_kernel<true, true><<<g, 256, sm, s>>>(a, nvec);
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a, int64_t 
 
 void launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t s) {
   const int64_t nvec = a.M * a.C / 8;
-  const unsigned g = stream_grid(nvec, 256, 2048);
+  const unsigned g = stream_grid(nvec, 256, 512);  // see bn32.hip apply_grid
   const size_t sm = 5 * a.C * sizeof(float);
   if (a.y) {
     if (a.dy_masked) bn_bwd_apply_kernel<true, true><<<g, 256, sm, s>>>(a, nvec);
