@@ -94,7 +94,24 @@ std::vector<int64_t> conv32_plan(int64_t mode, int64_t N, int64_t H, int64_t W, 
   return {p.bm, p.bn, p.splits, p.kchunk, mode == 0 ? 1 : 0, ws_floats(g, p)};
 }
 
-void run(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const torch::Tensor& w, const torch::Tensor& y,
+// fwd / dgrad B operand: the fp32 weights (exact mode), or in bf16x3 mode their
+// packed hi|lo split -- the model's optimizer-maintained mirror when given
+// (wp, int32), else packed here into a temporary (stream-ordered lifetime)
+const float* wsrc(const torch::Tensor& w, const c10::optional<torch::Tensor>& wp, torch::Tensor& tmp) {
+  if (!g_c32_mode) return fp(w);
+  if (wp.has_value() && wp->defined()) {
+    TORCH_CHECK(wp->is_cuda() && wp->is_contiguous() && wp->scalar_type() == torch::kInt32 &&
+                    wp->numel() == w.numel(),
+                "packed weights: contiguous int32 device tensor of the weights' size");
+    return reinterpret_cast<const float*>(wp->data_ptr());
+  }
+  TORCH_CHECK(w.numel() % 4 == 0, "weights are packed in groups of 4");
+  tmp = torch::empty({w.numel()}, w.options().dtype(torch::kInt32));
+  mfl::launch_split_pack(fp(w), reinterpret_cast<uint32_t*>(tmp.data_ptr()), w.numel(), cur_stream(w));
+  return reinterpret_cast<const float*>(tmp.data_ptr());
+}
+
+void run(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const float* wptr, const torch::Tensor& y,
          const c10::optional<torch::Tensor>& ws, double* stats, bool accum, const mfl::BnBwdFusion32* bnb,
          int stats_reps = 1) {
   const auto p = C32_CALL(plan_conv32, g, dgrad ? 1 : 0);
@@ -106,7 +123,7 @@ void run(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const tor
     counters = reinterpret_cast<int*>(ws->data_ptr<float>());
     slab = ws->data_ptr<float>() + kCounterWords;
   }
-  C32_CALL(launch_conv32_gemm, g, dgrad, p, fp(src), fp(w), fp(y), slab, counters, stats, accum, bnb, cur_stream(y),
+  C32_CALL(launch_conv32_gemm, g, dgrad, p, fp(src), wptr, fp(y), slab, counters, stats, accum, bnb, cur_stream(y),
                           stats_reps);
 }
 
@@ -122,12 +139,13 @@ double* stats_ptr(const c10::optional<torch::Tensor>& st, int64_t C) {
 
 void conv32_forward(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::optional<torch::Tensor> ws,
                     c10::optional<torch::Tensor> stats, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co,
-                    int64_t R, int64_t S, int64_t stride, int64_t pad) {
+                    int64_t R, int64_t S, int64_t stride, int64_t pad, c10::optional<torch::Tensor> wp) {
   const auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
   check_f32(x, (int64_t)N * H * W * C, "x");
   check_f32(w, (int64_t)Co * R * S * C, "w");
   check_f32(y, (int64_t)g.M * Co, "y");
-  run(g, false, x, w, y, ws, stats_ptr(stats, Co), false, nullptr,
+  torch::Tensor tmp;
+  run(g, false, x, wsrc(w, wp, tmp), y, ws, stats_ptr(stats, Co), false, nullptr,
       stats.has_value() && stats->defined() ? reps_of(*stats, Co) : 1);
 }
 
@@ -135,7 +153,7 @@ void conv32_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, c10::opti
                   int64_t H, int64_t W, int64_t C, int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad,
                   bool accumulate, c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
                   c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
-                  c10::optional<torch::Tensor> bn_acc) {
+                  c10::optional<torch::Tensor> bn_acc, c10::optional<torch::Tensor> wp) {
   const auto g = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
   check_f32(dy, (int64_t)N * g.H * g.W * Co, "dy");
   check_f32(w, (int64_t)Co * R * S * C, "w");
@@ -155,7 +173,8 @@ void conv32_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, c10::opti
     f.acc = stats_ptr(bn_acc, C);
     f.reps = reps_of(*bn_acc, C);
   }
-  run(g, true, dy, w, dx, ws, nullptr, accumulate, fuse ? &f : nullptr);
+  torch::Tensor tmp;
+  run(g, true, dy, wsrc(w, wp, tmp), dx, ws, nullptr, accumulate, fuse ? &f : nullptr);
 }
 
 // A layer's dgrad (+ fused consumer-BN reductions) and wgrad (dw zero on
@@ -165,7 +184,7 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
                           int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate,
                           c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
                           c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
-                          c10::optional<torch::Tensor> bn_acc) {
+                          c10::optional<torch::Tensor> bn_acc, c10::optional<torch::Tensor> wp) {
   const auto gf = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
   const auto gd = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
   check_f32(x, (int64_t)N * H * W * C, "x");
@@ -198,11 +217,13 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
     counters = reinterpret_cast<int*>(ws->data_ptr<float>());
     slab = ws->data_ptr<float>() + kCounterWords;
   }
-  if (C32_CALL(launch_conv32_bwd_pair, gd, pd, gf, pw, fp(dy), fp(w), fp(dx), slab, counters, accumulate,
+  torch::Tensor tmp;
+  const float* wb = wsrc(w, wp, tmp);
+  if (C32_CALL(launch_conv32_bwd_pair, gd, pd, gf, pw, fp(dy), wb, fp(dx), slab, counters, accumulate,
                                   fuse ? &f : nullptr, fp(x), fp(dw), cur_stream(dx)))
     return;
   C32_CALL(launch_conv32_wgrad, gf, pw, fp(x), fp(dy), fp(dw), true, cur_stream(dw));
-  C32_CALL(launch_conv32_gemm, gd, true, pd, fp(dy), fp(w), fp(dx), slab, counters, nullptr, accumulate,
+  C32_CALL(launch_conv32_gemm, gd, true, pd, fp(dy), wb, fp(dx), slab, counters, nullptr, accumulate,
                           fuse ? &f : nullptr, cur_stream(dx));
 }
 
@@ -300,7 +321,8 @@ void bn32_apply_pair(torch::Tensor x1, torch::Tensor gamma1, torch::Tensor beta1
 void conv32_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c10::optional<torch::Tensor> ws1,
                          c10::optional<torch::Tensor> stats1, torch::Tensor w2, torch::Tensor y2,
                          c10::optional<torch::Tensor> ws2, c10::optional<torch::Tensor> stats2, int64_t N, int64_t H,
-                         int64_t W, int64_t C, int64_t Co) {
+                         int64_t W, int64_t C, int64_t Co, c10::optional<torch::Tensor> wp1,
+                         c10::optional<torch::Tensor> wp2) {
   const auto g1 = fwd_geom(N, H, W, C, Co, 3, 3, 2, 1);
   const auto g2 = fwd_geom(N, H, W, C, Co, 1, 1, 2, 0);
   TORCH_CHECK(g1.M == g2.M, "conv1 / shortcut output sizes differ");
@@ -328,11 +350,14 @@ void conv32_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c1
   double* st1 = stats_ptr(stats1, Co);
   double* st2 = stats_ptr(stats2, Co);
   const int r1 = st1 ? reps_of(*stats1, Co) : 1, r2 = st2 ? reps_of(*stats2, Co) : 1;
-  if (C32_CALL(launch_conv32_fwd_pair, g1, p1, fp(w1), fp(y1), ys1, c1, st1, r1, g2, p2, fp(w2), fp(y2), ys2, c2, st2, r2,
+  torch::Tensor t1, t2;
+  const float* wb1 = wsrc(w1, wp1, t1);
+  const float* wb2 = wsrc(w2, wp2, t2);
+  if (C32_CALL(launch_conv32_fwd_pair, g1, p1, wb1, fp(y1), ys1, c1, st1, r1, g2, p2, wb2, fp(y2), ys2, c2, st2, r2,
                                   fp(x), cur_stream(x)))
     return;
-  run(g1, false, x, w1, y1, ws1, st1, false, nullptr, r1);
-  run(g2, false, x, w2, y2, ws2, st2, false, nullptr, r2);
+  run(g1, false, x, wb1, y1, ws1, st1, false, nullptr, r1);
+  run(g2, false, x, wb2, y2, ws2, st2, false, nullptr, r2);
 }
 
 void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,

@@ -62,9 +62,13 @@ void fused_optimizer(int64_t mode, torch::Tensor p, torch::Tensor g,
     need(m, "m");
     need(v, "v");
   }
-  if (p16.has_value() && p16->defined()) {
-    CHECK_IN((*p16), torch::kBFloat16);
-    TORCH_CHECK(p16->numel() == n, "bf16 copy size mismatch");
+  int mirror = 0;
+  if (p16.has_value() && p16->defined()) {  // bf16 compute copy, or the int32 packed bf16x3 split
+    TORCH_CHECK(p16->is_cuda() && p16->is_contiguous(), "weight mirror must be a contiguous device tensor");
+    TORCH_CHECK(p16->scalar_type() == torch::kBFloat16 || p16->scalar_type() == torch::kInt32,
+                "weight mirror is bf16 or int32 (packed split)");
+    TORCH_CHECK(p16->numel() == n, "weight mirror size mismatch");
+    mirror = p16->scalar_type() == torch::kInt32 ? 2 : 1;
   }
   if (lr_scale.has_value() && lr_scale->defined()) CHECK_IN((*lr_scale), torch::kFloat32);
   if (step.has_value() && step->defined()) CHECK_IN((*step), torch::kInt32);
@@ -75,13 +79,20 @@ void fused_optimizer(int64_t mode, torch::Tensor p, torch::Tensor g,
   h.wd = (float)wd;
   mfl::launch_fused_optimizer((int)mode, p.data_ptr<float>(), g.data_ptr<float>(),
                               ptr_or_null<float>(m), ptr_or_null<float>(v),
-                              ptr_or_null<float>(anchor), ptr_or_null<uint16_t>(p16), n, h,
+                              ptr_or_null<float>(anchor), mirror ? p16->data_ptr() : nullptr, n, h,
                               ptr_or_null<float>(lr_scale), ptr_or_null<int>(step), zero_grad,
                               zero_region.has_value() && zero_region->defined() ? zero_region->data_ptr() : nullptr,
                               zero_region.has_value() && zero_region->defined()
                                   ? (int64_t)(zero_region->numel() * zero_region->element_size()) / 16 * 16
                                   : 0,
-                              cur_stream(p), tick ? step->data_ptr<int>() : nullptr);
+                              cur_stream(p), tick ? step->data_ptr<int>() : nullptr, mirror);
+}
+
+void split_pack_f32(torch::Tensor x, torch::Tensor y) {
+  CHECK_IN(x, torch::kFloat32);
+  CHECK_IN(y, torch::kInt32);
+  TORCH_CHECK(x.numel() == y.numel() && x.numel() % 4 == 0, "split pack size");
+  mfl::launch_split_pack(x.data_ptr<float>(), reinterpret_cast<uint32_t*>(y.data_ptr()), x.numel(), cur_stream(x));
 }
 
 void cast_f32_bf16(torch::Tensor x, torch::Tensor y) {
@@ -404,6 +415,7 @@ void register_fp32(pybind11::module& m);
 PYBIND11_MODULE(_ops, m) {
   m.doc() = "metisfl_amd hand-written HIP (gfx950) kernels";
   m.def("fused_optimizer", &fused_optimizer);
+  m.def("split_pack_f32", &split_pack_f32);
   m.def("bn_apply_pair", &bn_apply_pair);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("scale_f32", &scale_f32);

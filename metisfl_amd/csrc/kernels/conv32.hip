@@ -61,6 +61,7 @@
 #ifndef MFL_C32_BF16X3
 #define MFL_C32_BF16X3 0
 #endif
+
 #if MFL_C32_BF16X3
 #define MFL_C32_VARIANT c32s
 #else
@@ -114,7 +115,24 @@ __device__ __forceinline__ void split_hl(const f32x4& p, const f32x4& q, bf16x8&
 // of groups 2g2 and 2g2+1 form one lane's 8 bf16 k-slots of a 32x32x16 MFMA
 // (k = 16g2 + {4h + e, 8 + 4h + e}); A and B use the same slots, so the
 // reduction is over the same k set and acc += Ahi Bhi + Ahi Blo + Alo Bhi.
-template <int TM, int TN, typename FA, typename FB>
+// B operand already packed by the producer (the optimizer's weight mirror:
+// dword = hi << 16 | lo, the same hi / lo split_hl computes): 8 v_perm per 8
+// values instead of 20 VALU
+__device__ __forceinline__ void unpack_hl(const f32x4& p, const f32x4& q, bf16x8& hi, bf16x8& lo) {
+  const uint32_t d[8] = {__float_as_uint(p[0]), __float_as_uint(p[1]), __float_as_uint(p[2]), __float_as_uint(p[3]),
+                         __float_as_uint(q[0]), __float_as_uint(q[1]), __float_as_uint(q[2]), __float_as_uint(q[3])};
+  u32x4 h, l;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    h[i] = __builtin_amdgcn_perm(d[2 * i + 1], d[2 * i], 0x07060302u);  // high halves: hi(2i), hi(2i+1)
+    l[i] = __builtin_amdgcn_perm(d[2 * i + 1], d[2 * i], 0x05040100u);  // low halves: lo(2i), lo(2i+1)
+  }
+  hi = __builtin_bit_cast(bf16x8, h);
+  lo = __builtin_bit_cast(bf16x8, l);
+}
+
+// BPACK (bf16x3 only): the B fragments hold packed hi|lo dwords.
+template <int TM, int TN, bool BPACK = false, typename FA, typename FB>
 __device__ __forceinline__ void mma_tile(const FA& fa, const FB& fb, f32x16 (&acc)[TM][TN]) {
 #if MFL_C32_BF16X3
 #pragma unroll
@@ -123,7 +141,10 @@ __device__ __forceinline__ void mma_tile(const FA& fa, const FB& fb, f32x16 (&ac
 #pragma unroll
     for (int i = 0; i < TM; ++i) split_hl(fa[2 * g2][i], fa[2 * g2 + 1][i], ah[i], al[i]);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) split_hl(fb[2 * g2][j], fb[2 * g2 + 1][j], bh[j], bl[j]);
+    for (int j = 0; j < TN; ++j) {
+      if constexpr (BPACK) unpack_hl(fb[2 * g2][j], fb[2 * g2 + 1][j], bh[j], bl[j]);
+      else split_hl(fb[2 * g2][j], fb[2 * g2 + 1][j], bh[j], bl[j]);
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -616,7 +637,7 @@ __device__ __forceinline__ void conv32_gemm_body(const Conv32Args& a, const Blk&
   auto mma = [&](auto set) {
     constexpr int S = decltype(set)::value;
     if constexpr (MFL_C32_DBG & 1) return;
-    mma_tile<TM, TN>(fa[S], fb[S], acc);
+    mma_tile<TM, TN, MFL_C32_BF16X3 != 0>(fa[S], fb[S], acc);  // fwd / dgrad: B = the weight mirror
     interleave_mfma<kTileMfma<TM, TN>, kTileValu>();
     __builtin_amdgcn_sched_barrier(0);
   };

@@ -21,10 +21,13 @@ struct OptHyper {
 // ---- optim.hip -----------------------------------------------------------
 // zero_grad: write 0 back into g after use (next step's atomics start from 0);
 // zero/zero_bytes: an extra region (BN accumulators) zeroed by the same launch.
+// p16: the weight mirror written from the updated fp32 values -- bf16 (mirror
+// 1) or the packed bf16x3 split (mirror 2, conv32.hip c32s); nullptr: none
 void launch_fused_optimizer(int mode, float* p, float* g, float* m, float* v,
-                            const float* anchor, uint16_t* p16, int64_t n, const OptHyper& h,
+                            const float* anchor, void* p16, int64_t n, const OptHyper& h,
                             const float* lr_ptr, const int* step_ptr, bool zero_grad, void* zero,
-                            int64_t zero_bytes, hipStream_t s, int* tick_step = nullptr);
+                            int64_t zero_bytes, hipStream_t s, int* tick_step = nullptr, int mirror = 1);
+void launch_split_pack(const float* x, uint32_t* y, int64_t n, hipStream_t s);
 // tick_step: also increment *tick_step once, after the optimizer's reads of
 // step_ptr (in the same launch for the modes that never read it)
 void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);

@@ -16,10 +16,20 @@
 
 namespace mfl {
 
-template <int MODE, bool W16>
+// fp32 -> packed (hi << 16 | lo) bf16 pair, a = hi + lo + O(2^-18 |a|): the
+// weight mirror of the bf16x3 convolutions (conv32.hip c32s decodes it with
+// two v_perm per pair instead of splitting in the k-loop)
+__device__ __forceinline__ uint32_t split_pack(float a) {
+  const uint16_t h = f2bf(a);
+  const uint16_t l = f2bf(a - bf2f(h));
+  return ((uint32_t)h << 16) | l;
+}
+
+// MIRROR: 0 none, 1 bf16 compute copy (p16), 2 packed bf16x3 split (ps)
+template <int MODE, int MIRROR>
 __global__ __launch_bounds__(256) void fused_opt_kernel(
     float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
-    const float* __restrict__ anchor, uint16_t* __restrict__ p16, int64_t n4, OptHyper h,
+    const float* __restrict__ anchor, void* __restrict__ mirror, int64_t n4, OptHyper h,
     const float* __restrict__ lr_ptr, const int* __restrict__ step_ptr, int zero_grad,
     uint4* __restrict__ zero, int64_t zero16, int* __restrict__ tick_step) {
   const float lr = lr_ptr ? lr_ptr[0] * h.lr : h.lr;
@@ -79,11 +89,14 @@ __global__ __launch_bounds__(256) void fused_opt_kernel(
       reinterpret_cast<float4*>(v)[i] = vv;
     }
     reinterpret_cast<float4*>(p)[i] = pv;
-    if (W16) {
+    if (MIRROR == 1) {
       uint2 o;
       o.x = pack2bf(pp[0], pp[1]);
       o.y = pack2bf(pp[2], pp[3]);
-      reinterpret_cast<uint2*>(p16)[i] = o;
+      reinterpret_cast<uint2*>(mirror)[i] = o;
+    } else if (MIRROR == 2) {
+      reinterpret_cast<uint4*>(mirror)[i] = make_uint4(split_pack(pp[0]), split_pack(pp[1]), split_pack(pp[2]),
+                                                       split_pack(pp[3]));
     }
   }
   // the step-counter increment that used to be its own launch; these modes
@@ -96,27 +109,31 @@ __global__ __launch_bounds__(256) void fused_opt_kernel(
 
 template <int MODE>
 static void launch_mode(float* p, float* g, float* m, float* v, const float* anchor,
-                        uint16_t* p16, int64_t n, const OptHyper& h, const float* lr_ptr,
+                        void* p16, int mirror, int64_t n, const OptHyper& h, const float* lr_ptr,
                         const int* step_ptr, bool zg, void* zero, int64_t zero_bytes,
                         hipStream_t s, int* tick_step) {
   const int64_t n4 = n / 4;
   const int64_t z16 = zero ? zero_bytes / 16 : 0;
   const unsigned grid = stream_grid(n4 > z16 ? n4 : z16, 256, 2048);
   uint4* z = reinterpret_cast<uint4*>(zero);
-  if (p16)
-    fused_opt_kernel<MODE, true><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr,
-                                                      step_ptr, zg ? 1 : 0, z, z16, tick_step);
+  if (p16 && mirror == 2)
+    fused_opt_kernel<MODE, 2><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr, step_ptr, zg ? 1 : 0,
+                                                   z, z16, tick_step);
+  else if (p16)
+    fused_opt_kernel<MODE, 1><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr, step_ptr, zg ? 1 : 0,
+                                                   z, z16, tick_step);
   else
-    fused_opt_kernel<MODE, false><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr,
-                                                       step_ptr, zg ? 1 : 0, z, z16, tick_step);
+    fused_opt_kernel<MODE, 0><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr, step_ptr, zg ? 1 : 0,
+                                                   z, z16, tick_step);
 }
 
 void launch_fused_optimizer(int mode, float* p, float* g, float* m, float* v,
-                            const float* anchor, uint16_t* p16, int64_t n, const OptHyper& h,
+                            const float* anchor, void* p16, int64_t n, const OptHyper& h,
                             const float* lr_ptr, const int* step_ptr, bool zero_grad, void* zero,
-                            int64_t zero_bytes, hipStream_t s, int* tick_step) {
+                            int64_t zero_bytes, hipStream_t s, int* tick_step, int mirror) {
 #define MFL_OPT_CASE(M_) \
-  case M_: launch_mode<M_>(p, g, m, v, anchor, p16, n, h, lr_ptr, step_ptr, zero_grad, zero, zero_bytes, s, tick_step); break;
+  case M_: launch_mode<M_>(p, g, m, v, anchor, p16, mirror, n, h, lr_ptr, step_ptr, zero_grad, zero, zero_bytes, \
+                           s, tick_step); break;
   switch (mode) {
     MFL_OPT_CASE(OPT_SGD)
     MFL_OPT_CASE(OPT_MOMENTUM)
@@ -127,6 +144,22 @@ void launch_fused_optimizer(int mode, float* p, float* g, float* m, float* v,
   }
 #undef MFL_OPT_CASE
   if (tick_step && (mode == OPT_ADAM || mode == OPT_ADAMW)) launch_tick(tick_step, 1, s);
+}
+
+// fp32 -> packed bf16x3 split mirror of a flat buffer (initial weights, a
+// received community model)
+__global__ __launch_bounds__(256) void split_pack_kernel(const float4* __restrict__ x, uint4* __restrict__ y,
+                                                         int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = x[i];
+    y[i] = make_uint4(split_pack(v.x), split_pack(v.y), split_pack(v.z), split_pack(v.w));
+  }
+}
+void launch_split_pack(const float* x, uint32_t* y, int64_t n, hipStream_t s) {
+  const int64_t n4 = n / 4;
+  split_pack_kernel<<<stream_grid(n4), 256, 0, s>>>(reinterpret_cast<const float4*>(x), reinterpret_cast<uint4*>(y),
+                                                    n4);
 }
 
 // ---------------------------------------------------------------------------

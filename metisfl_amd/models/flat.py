@@ -78,6 +78,15 @@ class FlatState:
         self.grad32 = torch.zeros(max(self.n_params, ALIGN), dtype=torch.float32, device=dev)[: self.n_params]
         self.p16 = (torch.zeros(self.n_params, dtype=torch.bfloat16, device=dev)
                     if compute_dtype == torch.bfloat16 else None)
+        # fp32 GPU models whose convolutions run bf16x3 products keep a packed
+        # (hi << 16 | lo) bf16 split of the weights, written by the optimizer
+        # launch like the bf16 mirror (conv32.hip decodes it with v_perm
+        # instead of splitting every weight fragment in every k-loop)
+        self.psplit = None
+        if compute_dtype == torch.float32 and dev.type == "cuda" and self.n_params:
+            from metisfl_amd.ops.nn import conv_products
+            if conv_products() == "bf16x3":
+                self.psplit = torch.zeros(self.n_params, dtype=torch.int32, device=dev)
         self.anchor: torch.Tensor | None = None
         self.m: torch.Tensor | None = None
         self.v: torch.Tensor | None = None
@@ -102,6 +111,14 @@ class FlatState:
         s = self.by_name[name]
         assert s.trainable and self.p16 is not None
         return self.p16[s.offset: s.offset + s.numel].view(s.shape)
+
+    def packed(self, name: str) -> torch.Tensor | None:
+        """The packed bf16x3 split of a weight (int32 view), or None."""
+        if self.psplit is None:
+            return None
+        s = self.by_name[name]
+        assert s.trainable
+        return self.psplit[s.offset: s.offset + s.numel]
 
     def compute(self, name: str) -> torch.Tensor:
         """The weight view the kernels read: the bf16 mirror, or the fp32
@@ -135,8 +152,12 @@ class FlatState:
         self.refresh_bf16()
 
     def refresh_bf16(self) -> None:
+        """Re-derive the weight mirror (bf16 copy or packed bf16x3 split) from
+        the fp32 master after it was written outside the optimizer."""
         if self.n_params and self.p16 is not None:
             opt_ops.cast_bf16(self.params32, self.p16)
+        if self.n_params and self.psplit is not None:
+            opt_ops.split_pack(self.params32, self.psplit)
 
     # ---- optimizer ----------------------------------------------------------
     def set_optimizer(self, spec: OptimizerSpec, reset_state: bool = False) -> None:
@@ -157,8 +178,8 @@ class FlatState:
         if self.n_params == 0 or self.optimizer is None:
             return False
         opt_ops.fused_step(self.optimizer, self.params32, self.grad32, self.m, self.v, self.anchor,
-                           self.p16, self.lr_scale, self.step, zero_grad, zero_region,
-                           tick)
+                           self.p16 if self.p16 is not None else self.psplit, self.lr_scale, self.step,
+                           zero_grad, zero_region, tick)
         return True
 
     def set_anchor(self) -> None:

@@ -133,6 +133,7 @@ class ConvBN(Layer):
         self.st = st
         self.ws = ws
         self.w16 = st.compute(f"{n}.conv.weight")
+        self.wp = st.packed(f"{n}.conv.weight")  # bf16x3 weight mirror (fp32 GPU path), else None
         self.dw = st.grad(f"{n}.conv.weight")
         self.gamma = st.view(f"{n}.bn.gamma")
         self.beta = st.view(f"{n}.bn.beta")
@@ -165,7 +166,8 @@ class ConvBN(Layer):
     def forward(self, x: torch.Tensor, residual: torch.Tensor | None = None, train: bool = True):
         s = self.shp
         self.x = x
-        K.conv_forward(x, self.w16, self.z, s, self._split(), self.ws.acc(self.acc_f) if train else None)
+        K.conv_forward(x, self.w16, self.z, s, self._split(), self.ws.acc(self.acc_f) if train else None,
+                       wp=self.wp)
         return self.bn_forward(residual, train)
 
     def bn_forward(self, residual: torch.Tensor | None = None, train: bool = True):
@@ -209,12 +211,12 @@ class ConvBN(Layer):
         if dx is not None and not self.ws.overlap:
             # both GEMMs in one launch (their workgroups share the CUs)
             K.conv_backward_pair(self.x, self.dz, self.dw, self.w16, dx, s, self._split(), accumulate,
-                                 bnb=bnb)
+                                 bnb=bnb, wp=self.wp)
             return
         with self.ws.fork():
             K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True)
         if dx is not None:
-            K.conv_dgrad(self.dz, self.w16, dx, s, self._split(), accumulate, bnb=bnb)
+            K.conv_dgrad(self.dz, self.w16, dx, s, self._split(), accumulate, bnb=bnb, wp=self.wp)
 
 
 class BasicBlock(Layer):
@@ -259,7 +261,8 @@ class BasicBlock(Layer):
             c1, sc = self.c1, self.sc
             c1.x = sc.x = x
             K.conv_forward_pair(x, c1.w16, c1.z, c1._split(), c1.ws.acc(c1.acc_f) if train else None,
-                                sc.w16, sc.z, sc._split(), sc.ws.acc(sc.acc_f) if train else None, c1.shp)
+                                sc.w16, sc.z, sc._split(), sc.ws.acc(sc.acc_f) if train else None, c1.shp,
+                                wp1=c1.wp, wp2=sc.wp)
             if x.is_cuda and not sc.relu and c1.relu:
                 # ... and their two BatchNorms in one launch
                 pair = K.ops().bn32_apply_pair if x.dtype == torch.float32 else K.ops().bn_apply_pair

@@ -122,12 +122,14 @@ def _acc_stats_cpu(y: torch.Tensor, acc: torch.Tensor) -> None:
     acc[C:2 * C] += (yf * yf).sum(0)
 
 
-def conv_forward(x, w, y, shp: ConvShape, ws=None, stats=None) -> None:
+def conv_forward(x, w, y, shp: ConvShape, ws=None, stats=None, wp=None) -> None:
     """y = conv(x, w); ``stats`` (fp64 [2*Cout]) accumulates the per-channel
-    sum / sum-of-squares of the bf16 output for the following BatchNorm."""
+    sum / sum-of-squares of the bf16 output for the following BatchNorm.
+    ``wp``: the packed bf16x3 mirror of ``w`` (fp32 / bf16x3 mode; packed on
+    the fly when omitted)."""
     if x.is_cuda:
         if x.dtype == torch.float32:
-            ops().conv32_forward(x, w, y, ws, stats, *shp.args())
+            ops().conv32_forward(x, w, y, ws, stats, *shp.args(), wp)
         else:
             ops().conv_forward(x, w, y, ws, stats, *shp.args())
         return
@@ -161,16 +163,18 @@ def _bnb_sums_cpu(dx: torch.Tensor, t: BnBwdTarget) -> None:
 
 
 def conv_dgrad(dy, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
-               bnb: BnBwdTarget | None = None) -> None:
+               bnb: BnBwdTarget | None = None, wp=None) -> None:
     """dx (+)= conv_transpose(dy, W); ``w`` is the KRSC weight [Cout][R][S][Cin]
     (the kernel forms W^T fragments with transposing LDS reads).  ``bnb``:
     fuse the consumer BatchNorm-backward reductions into the epilogue."""
     if dy.is_cuda:
-        fn = ops().conv32_dgrad if dy.dtype == torch.float32 else ops().conv_dgrad
+        f32 = dy.dtype == torch.float32
+        fn = ops().conv32_dgrad if f32 else ops().conv_dgrad
+        extra = (wp,) if f32 else ()
         if bnb is None:
-            fn(dy, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None)
+            fn(dy, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None, *extra)
         else:
-            fn(dy, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean, bnb.invstd, bnb.acc)
+            fn(dy, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean, bnb.invstd, bnb.acc, *extra)
         return
     _conv_dgrad_cpu(dy, w, dx, shp, accumulate)
     if bnb is not None:
@@ -202,20 +206,23 @@ def conv_wgrad(x, dy, dw, shp: ConvShape, accumulate: bool = False) -> None:
     dw.copy_(g.permute(0, 2, 3, 1).reshape(dw.shape))
 
 
-def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShape) -> None:
+def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShape, wp1=None, wp2=None) -> None:
     """A downsampling block's conv1 (3x3, stride 2; ``shp``) and its 1x1 / stride-2
     projection shortcut of the same x -- one paired launch on the GPU."""
     assert shp.R == 3 and shp.stride == 2
     if x.is_cuda:
-        fn = ops().conv32_forward_pair if x.dtype == torch.float32 else ops().conv_forward_pair
-        fn(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp.N, shp.H, shp.W, shp.C, shp.Co)
+        if x.dtype == torch.float32:
+            ops().conv32_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp.N, shp.H, shp.W, shp.C,
+                                      shp.Co, wp1, wp2)
+        else:
+            ops().conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp.N, shp.H, shp.W, shp.C, shp.Co)
         return
     conv_forward(x, w1, y1, shp, ws1, stats1)
     conv_forward(x, w2, y2, ConvShape(shp.N, shp.H, shp.W, shp.C, shp.Co, 1, 1, 2, 0), ws2, stats2)
 
 
 def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
-                       bnb: BnBwdTarget | None = None) -> None:
+                       bnb: BnBwdTarget | None = None, wp=None) -> None:
     """A layer's weight gradient (dw += ..., dw zero on entry) and input
     gradient (as conv_dgrad) -- on the GPU in ONE paired launch, so the two
     independent, latency-bound GEMMs share the CUs (conv.hip
@@ -224,10 +231,11 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
     tiles on the fast address paths; MFL_C32_PAIR=0 for two launches)."""
     if dy.is_cuda and dy.dtype == torch.float32:
         if bnb is None:
-            ops().conv32_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None)
+            ops().conv32_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None,
+                                       wp)
         else:
             ops().conv32_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
-                                       bnb.invstd, bnb.acc)
+                                       bnb.invstd, bnb.acc, wp)
         return
     if dy.is_cuda:
         if bnb is None:
@@ -238,7 +246,7 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
                                      bnb.invstd, bnb.acc)
         return
     conv_wgrad(x, dy, dw, shp, accumulate=True)
-    conv_dgrad(dy, w, dx, shp, ws, accumulate, bnb=bnb)
+    conv_dgrad(dy, w, dx, shp, ws, accumulate, bnb=bnb, wp=wp)
 
 
 def transpose_krsc(w, wt, Co: int, RS: int, Ci: int) -> None:

@@ -140,6 +140,18 @@ def _reference_step(spec, p, g, m, v, anchor, p16, lr_scale, step):
         p16.copy_(p.to(torch.bfloat16))
 
 
+def split_pack(x: torch.Tensor, y: torch.Tensor) -> None:
+    """y (int32) = packed (hi << 16 | lo) bf16 split of the fp32 x."""
+    if x.is_cuda:
+        ops().split_pack_f32(x, y)
+        return
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    h = hi.view(torch.int16).to(torch.int32) & 0xFFFF
+    lw = lo.view(torch.int16).to(torch.int32) & 0xFFFF
+    y.copy_((h << 16) | lw)
+
+
 def cast_bf16(x: torch.Tensor, y: torch.Tensor) -> None:
     if x.is_cuda:
         ops().cast_f32_bf16(x, y)

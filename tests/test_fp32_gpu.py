@@ -380,3 +380,31 @@ def test_loss_trajectory_bf16_within_3pct_of_fp32():
         print(dt, [round(c, 4) for c in curve])
     assert final["fp32"] < 1.0  # the task was learned
     assert abs(final["bf16"] - final["fp32"]) <= max(0.03 * final["fp32"], 0.02), final
+
+
+def test_bf16x3_weight_mirror_tracks_master():
+    """The packed bf16x3 weight mirror (hi << 16 | lo, written by the fused
+    optimizer and read by the fwd / dgrad convolutions) equals the split of
+    the fp32 master after training steps, bit for bit, and after an external
+    write of the master (refresh_bf16)."""
+    from metisfl_amd.models.resnet import ResNet18
+    from metisfl_amd.ops import optim as opt_ops
+    from metisfl_amd.ops.optim import OptimizerSpec
+    net = ResNet18(batch_size=8, device=DEV, seed=3, conv_products="bf16x3",
+                   optimizer=OptimizerSpec("momentum_sgd", 0.01, momentum=0.9))
+    assert net.state.psplit is not None
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn((64, 32, 32, 3), generator=g, device=DEV)
+    y = torch.randint(0, 10, (64,), generator=g, device=DEV)
+    net.train_steps(net.make_dataset(x, y), 3)
+    torch.cuda.synchronize()
+
+    def ref():
+        r = torch.zeros(net.state.n_params, dtype=torch.int32)
+        opt_ops.split_pack(net.state.params32.cpu(), r)
+        return r
+    assert torch.equal(net.state.psplit.cpu(), ref())
+    net.state.params32.mul_(0.5)
+    net.state.refresh_bf16()
+    torch.cuda.synchronize()
+    assert torch.equal(net.state.psplit.cpu(), ref())
