@@ -22,8 +22,10 @@ ResNet-18 architecture (no network for datasets/checkpoints).
 
 Precision: ``--dtype fp32`` (default) is the reference's precision -- the
 reference trains fp32 Keras models (examples/keras/models/cifar_cnn.py:19-41,
-keras_model_ops.py:117-197) -- on the exact fp32 MFMA kernels (conv32.hip);
-``--dtype bf16`` is the mixed-precision option, reported separately.
+keras_model_ops.py:117-197) -- on the fp32 convolution kernels (conv32.hip:
+fp32 storage and accumulation, bf16x3 split products by default, exact fp32
+MFMA products with ``--conv-products exact``); ``--dtype bf16`` is the
+mixed-precision option, reported separately.
 
 Launch: ``python bench.py`` (1 GPU), ``python bench.py --gpus N`` (spawns its
 own N rank processes before touching any GPU), or under
