@@ -111,7 +111,26 @@ const float* wsrc(const torch::Tensor& w, const c10::optional<torch::Tensor>& wp
   return reinterpret_cast<const float*>(tmp.data_ptr());
 }
 
-void run(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const float* wptr, const torch::Tensor& y,
+// dgrad / wgrad dY operand: fp32 (exact mode); in bf16x3 mode its packed hi|lo
+// split -- as the layer's fp32 BN backward wrote it when dy is an int32 view of
+// that buffer (bn32_backward with an int32 dx), else packed here into a
+// temporary (stream-ordered lifetime)
+const float* dysrc(const torch::Tensor& dy, int64_t n, torch::Tensor& tmp) {
+  if (dy.scalar_type() == torch::kInt32) {
+    TORCH_CHECK(g_c32_mode, "a packed (int32) dY needs the bf16x3 conv product mode");
+    TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.numel() == n,
+                "packed dY: contiguous int32 device tensor of dY's size");
+    return reinterpret_cast<const float*>(dy.data_ptr());
+  }
+  check_f32(dy, n, "dy");
+  if (!g_c32_mode) return fp(dy);
+  TORCH_CHECK(n % 4 == 0, "dY is packed in groups of 4");
+  tmp = torch::empty({n}, dy.options().dtype(torch::kInt32));
+  mfl::launch_split_pack(fp(dy), reinterpret_cast<uint32_t*>(tmp.data_ptr()), n, cur_stream(dy));
+  return reinterpret_cast<const float*>(tmp.data_ptr());
+}
+
+void run(const mfl::ConvGeom& g, bool dgrad, const float* src, const float* wptr, const torch::Tensor& y,
          const c10::optional<torch::Tensor>& ws, double* stats, bool accum, const mfl::BnBwdFusion32* bnb,
          int stats_reps = 1) {
   const auto p = C32_CALL(plan_conv32, g, dgrad ? 1 : 0);
@@ -123,7 +142,7 @@ void run(const mfl::ConvGeom& g, bool dgrad, const torch::Tensor& src, const flo
     counters = reinterpret_cast<int*>(ws->data_ptr<float>());
     slab = ws->data_ptr<float>() + kCounterWords;
   }
-  C32_CALL(launch_conv32_gemm, g, dgrad, p, fp(src), wptr, fp(y), slab, counters, stats, accum, bnb, cur_stream(y),
+  C32_CALL(launch_conv32_gemm, g, dgrad, p, src, wptr, fp(y), slab, counters, stats, accum, bnb, cur_stream(y),
                           stats_reps);
 }
 
@@ -145,7 +164,7 @@ void conv32_forward(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::opti
   check_f32(w, (int64_t)Co * R * S * C, "w");
   check_f32(y, (int64_t)g.M * Co, "y");
   torch::Tensor tmp;
-  run(g, false, x, wsrc(w, wp, tmp), y, ws, stats_ptr(stats, Co), false, nullptr,
+  run(g, false, fp(x), wsrc(w, wp, tmp), y, ws, stats_ptr(stats, Co), false, nullptr,
       stats.has_value() && stats->defined() ? reps_of(*stats, Co) : 1);
 }
 
@@ -155,7 +174,8 @@ void conv32_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, c10::opti
                   c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
                   c10::optional<torch::Tensor> bn_acc, c10::optional<torch::Tensor> wp) {
   const auto g = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
-  check_f32(dy, (int64_t)N * g.H * g.W * Co, "dy");
+  torch::Tensor dtmp;
+  const float* dyp = dysrc(dy, (int64_t)N * g.H * g.W * Co, dtmp);
   check_f32(w, (int64_t)Co * R * S * C, "w");
   check_f32(dx, (int64_t)N * H * W * C, "dx");
   mfl::BnBwdFusion32 f;
@@ -174,7 +194,7 @@ void conv32_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, c10::opti
     f.reps = reps_of(*bn_acc, C);
   }
   torch::Tensor tmp;
-  run(g, true, dy, wsrc(w, wp, tmp), dx, ws, nullptr, accumulate, fuse ? &f : nullptr);
+  run(g, true, dyp, wsrc(w, wp, tmp), dx, ws, nullptr, accumulate, fuse ? &f : nullptr);
 }
 
 // A layer's dgrad (+ fused consumer-BN reductions) and wgrad (dw zero on
@@ -188,7 +208,8 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
   const auto gf = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
   const auto gd = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
   check_f32(x, (int64_t)N * H * W * C, "x");
-  check_f32(dy, (int64_t)gf.M * Co, "dy");
+  torch::Tensor dtmp;
+  const float* dyp = dysrc(dy, (int64_t)gf.M * Co, dtmp);
   check_f32(dw, (int64_t)Co * R * S * C, "dw");
   check_f32(w, (int64_t)Co * R * S * C, "w");
   check_f32(dx, (int64_t)N * H * W * C, "dx");
@@ -219,11 +240,11 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
   }
   torch::Tensor tmp;
   const float* wb = wsrc(w, wp, tmp);
-  if (C32_CALL(launch_conv32_bwd_pair, gd, pd, gf, pw, fp(dy), wb, fp(dx), slab, counters, accumulate,
+  if (C32_CALL(launch_conv32_bwd_pair, gd, pd, gf, pw, dyp, wb, fp(dx), slab, counters, accumulate,
                                   fuse ? &f : nullptr, fp(x), fp(dw), cur_stream(dx)))
     return;
-  C32_CALL(launch_conv32_wgrad, gf, pw, fp(x), fp(dy), fp(dw), true, cur_stream(dw));
-  C32_CALL(launch_conv32_gemm, gd, true, pd, fp(dy), wb, fp(dx), slab, counters, nullptr, accumulate,
+  C32_CALL(launch_conv32_wgrad, gf, pw, fp(x), dyp, fp(dw), true, cur_stream(dw));
+  C32_CALL(launch_conv32_gemm, gd, true, pd, dyp, wb, fp(dx), slab, counters, nullptr, accumulate,
                           fuse ? &f : nullptr, cur_stream(dx));
 }
 
@@ -231,11 +252,12 @@ void conv32_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t N
                   int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate) {
   const auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
   check_f32(x, (int64_t)N * H * W * C, "x");
-  check_f32(dy, (int64_t)g.M * Co, "dy");
+  torch::Tensor dtmp;
+  const float* dyp = dysrc(dy, (int64_t)g.M * Co, dtmp);
   check_f32(dw, (int64_t)Co * R * S * C, "dw");
   const auto p = C32_CALL(plan_conv32, g, 2);
   if (!accumulate && p.splits > 1) dw.zero_();
-  C32_CALL(launch_conv32_wgrad, g, p, fp(x), fp(dy), fp(dw), accumulate, cur_stream(dw));
+  C32_CALL(launch_conv32_wgrad, g, p, fp(x), dyp, fp(dw), accumulate, cur_stream(dw));
 }
 
 // ---- BatchNorm -----------------------------------------------------------
@@ -356,8 +378,8 @@ void conv32_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c1
   if (C32_CALL(launch_conv32_fwd_pair, g1, p1, wb1, fp(y1), ys1, c1, st1, r1, g2, p2, wb2, fp(y2), ys2, c2, st2, r2,
                                   fp(x), cur_stream(x)))
     return;
-  run(g1, false, x, wb1, y1, ws1, st1, false, nullptr, r1);
-  run(g2, false, x, wb2, y2, ws2, st2, false, nullptr, r2);
+  run(g1, false, fp(x), wb1, y1, ws1, st1, false, nullptr, r1);
+  run(g2, false, fp(x), wb2, y2, ws2, st2, false, nullptr, r2);
 }
 
 void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,
@@ -368,7 +390,14 @@ void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::
                         c10::optional<torch::Tensor> acc2) {
   check_nhwc32(dy, C);
   check_nhwc32(x, C);
-  check_nhwc32(dx, C);
+  // an int32 dx receives the packed bf16x3 split of the gradient: the dY
+  // operand of the layer's bf16x3 dgrad / wgrad (see dysrc)
+  const bool pack_dx = dx.scalar_type() == torch::kInt32;
+  if (pack_dx) {
+    TORCH_CHECK(dx.is_cuda() && dx.is_contiguous(), "packed dx: contiguous int32 device tensor");
+  } else {
+    check_nhwc32(dx, C);
+  }
   TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel(), "bn bwd sizes");
   for (auto* t : {&gamma, &mean, &invstd}) check_pc(*t, C, "bn param");
   mfl::BnBwdArgs32 a{};
@@ -392,7 +421,8 @@ void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::
   a.gamma = fp(gamma);
   a.mean = fp(mean);
   a.invstd = fp(invstd);
-  a.dx = fp(dx);
+  a.dx = reinterpret_cast<float*>(dx.data_ptr());
+  a.pack_dx = pack_dx ? 1 : 0;
   a.M = x.numel() / C;
   a.C = (int)C;
   if (acc2.has_value() && acc2->defined()) {

@@ -337,7 +337,10 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
     o.y = k1.y * (g.y - mg.y - ((xc.y - mu.y) * is.y) * mx.y);
     o.z = k1.z * (g.z - mg.z - ((xc.z - mu.z) * is.z) * mx.z);
     o.w = k1.w * (g.w - mg.w - ((xc.w - mu.w) * is.w) * mx.w);
-    reinterpret_cast<float4*>(a.dx)[i] = o;
+    if (a.pack_dx)  // uniform: the bf16x3 convolutions' dY encoding
+      reinterpret_cast<uint4*>(a.dx)[i] = make_uint4(split_pack(o.x), split_pack(o.y), split_pack(o.z), split_pack(o.w));
+    else
+      reinterpret_cast<float4*>(a.dx)[i] = o;
   }
   if (side) {
     __syncthreads();  // sc[] reads done before channel_atomic4's LDS staging

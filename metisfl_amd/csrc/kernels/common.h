@@ -31,6 +31,16 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return *reinterpret_cast<uint16_t*>(&b);
 }
 
+// fp32 -> packed (hi << 16 | lo) bf16 pair, a = hi + lo + O(2^-18 |a|): the
+// operand encoding of the bf16x3 fp32 convolutions (conv32.hip c32s decodes it
+// with two v_perm per pair instead of splitting in the k-loop).  Written by the
+// fused optimizer (weight mirror) and by the fp32 BN backward (the conv's dY).
+__device__ __forceinline__ uint32_t split_pack(float a) {
+  const uint16_t h = f2bf(a);
+  const uint16_t l = f2bf(a - bf2f(h));
+  return ((uint32_t)h << 16) | l;
+}
+
 // Packs two floats into two bf16 (RNE) in one dword.
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);

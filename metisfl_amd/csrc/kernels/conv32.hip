@@ -131,15 +131,19 @@ __device__ __forceinline__ void unpack_hl(const f32x4& p, const f32x4& q, bf16x8
   lo = __builtin_bit_cast(bf16x8, l);
 }
 
-// BPACK (bf16x3 only): the B fragments hold packed hi|lo dwords.
-template <int TM, int TN, bool BPACK = false, typename FA, typename FB>
+// BPACK / APACK (bf16x3 only): the B / A fragments hold packed hi|lo dwords
+// (B: the optimizer's weight mirror; A: dY as the fp32 BN backward wrote it).
+template <int TM, int TN, bool BPACK = false, bool APACK = false, typename FA, typename FB>
 __device__ __forceinline__ void mma_tile(const FA& fa, const FB& fb, f32x16 (&acc)[TM][TN]) {
 #if MFL_C32_BF16X3
 #pragma unroll
   for (int g2 = 0; g2 < kBK / 16; ++g2) {
     bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) split_hl(fa[2 * g2][i], fa[2 * g2 + 1][i], ah[i], al[i]);
+    for (int i = 0; i < TM; ++i) {
+      if constexpr (APACK) unpack_hl(fa[2 * g2][i], fa[2 * g2 + 1][i], ah[i], al[i]);
+      else split_hl(fa[2 * g2][i], fa[2 * g2 + 1][i], ah[i], al[i]);
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       if constexpr (BPACK) unpack_hl(fb[2 * g2][j], fb[2 * g2 + 1][j], bh[j], bl[j]);
@@ -637,7 +641,8 @@ __device__ __forceinline__ void conv32_gemm_body(const Conv32Args& a, const Blk&
   auto mma = [&](auto set) {
     constexpr int S = decltype(set)::value;
     if constexpr (MFL_C32_DBG & 1) return;
-    mma_tile<TM, TN, MFL_C32_BF16X3 != 0>(fa[S], fb[S], acc);  // fwd / dgrad: B = the weight mirror
+    // fwd / dgrad: B = the weight mirror; dgrad: A = dY, packed by its producer
+    mma_tile<TM, TN, MFL_C32_BF16X3 != 0, MFL_C32_BF16X3 != 0 && DGRAD>(fa[S], fb[S], acc);
     interleave_mfma<kTileMfma<TM, TN>, kTileValu>();
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -863,7 +868,7 @@ __device__ __forceinline__ void conv32_wgrad_body(const Conv32Args& a, const Blk
   auto mma = [&](auto set) {
     constexpr int S = decltype(set)::value;
     if constexpr (MFL_C32_DBG & 1) return;
-    mma_tile<TM, TN>(fa[S], fb[S], acc);
+    mma_tile<TM, TN, false, MFL_C32_BF16X3 != 0>(fa[S], fb[S], acc);  // A = dY (packed), B = X
     interleave_mfma<kTileMfma<TM, TN>, kTileValu>();
     __builtin_amdgcn_sched_barrier(0);
   };

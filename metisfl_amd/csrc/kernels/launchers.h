@@ -137,6 +137,9 @@ struct BnBwdArgs32 {
   const float* invstd2;
   double* acc2;
   int reps2;
+  // 1: dx is written as packed bf16x3 splits (split_pack, common.h) -- the
+  // dY operand the bf16x3 dgrad / wgrad kernels decode without splitting
+  int pack_dx;
 };
 void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_t s, int reps = 1);
 void launch_bn32_apply(const BnFwdArgs32& a, hipStream_t s);

@@ -16,14 +16,7 @@
 
 namespace mfl {
 
-// fp32 -> packed (hi << 16 | lo) bf16 pair, a = hi + lo + O(2^-18 |a|): the
-// weight mirror of the bf16x3 convolutions (conv32.hip c32s decodes it with
-// two v_perm per pair instead of splitting in the k-loop)
-__device__ __forceinline__ uint32_t split_pack(float a) {
-  const uint16_t h = f2bf(a);
-  const uint16_t l = f2bf(a - bf2f(h));
-  return ((uint32_t)h << 16) | l;
-}
+// split_pack (common.h): the packed bf16x3 weight mirror
 
 // MIRROR: 0 none, 1 bf16 compute copy (p16), 2 packed bf16x3 split (ps)
 template <int MODE, int MIRROR>

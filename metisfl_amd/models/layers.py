@@ -202,21 +202,24 @@ class ConvBN(Layer):
         reductions; ``bnb``: the BN whose upstream gradient ``dx`` is (its
         reductions are fused into this layer's dgrad epilogue)."""
         s = self.shp
+        # bf16x3 conv products: dz is only ever read by this layer's dgrad and
+        # wgrad, so the BN backward writes it as their packed operand encoding
+        pk = self.dz.is_cuda and self.dz.dtype == torch.float32 and K.conv_products() == "bf16x3"
         K.bn_backward(dy, self.z, self.y if self.relu else None, s.Co, self.gamma, self.mean,
                       self.invstd, self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz, dres,
-                      presummed=presummed, side=side)
+                      presummed=presummed, side=side, dx_packed=pk)
         # weight gradient: off the critical path -> side stream (joined before
         # the optimizer); the gradient buffer is zero on entry (re-zeroed by
         # the optimizer launch), so split-K slices accumulate atomically
         if dx is not None and not self.ws.overlap:
             # both GEMMs in one launch (their workgroups share the CUs)
             K.conv_backward_pair(self.x, self.dz, self.dw, self.w16, dx, s, self._split(), accumulate,
-                                 bnb=bnb, wp=self.wp)
+                                 bnb=bnb, wp=self.wp, dy_packed=pk)
             return
         with self.ws.fork():
-            K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True)
+            K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True, dy_packed=pk)
         if dx is not None:
-            K.conv_dgrad(self.dz, self.w16, dx, s, self._split(), accumulate, bnb=bnb, wp=self.wp)
+            K.conv_dgrad(self.dz, self.w16, dx, s, self._split(), accumulate, bnb=bnb, wp=self.wp, dy_packed=pk)
 
 
 class BasicBlock(Layer):

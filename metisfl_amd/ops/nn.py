@@ -162,8 +162,14 @@ def _bnb_sums_cpu(dx: torch.Tensor, t: BnBwdTarget) -> None:
     t.acc[C:2 * C] += (g.double() * xh.double()).sum(0)
 
 
+def _dy_arg(dy, dy_packed: bool):
+    """``dy_packed``: the fp32 buffer holds packed bf16x3 splits (written by
+    :func:`bn_backward` with ``dx_packed``); the binding takes it as int32."""
+    return dy.view(torch.int32) if dy_packed else dy
+
+
 def conv_dgrad(dy, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
-               bnb: BnBwdTarget | None = None, wp=None) -> None:
+               bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False) -> None:
     """dx (+)= conv_transpose(dy, W); ``w`` is the KRSC weight [Cout][R][S][Cin]
     (the kernel forms W^T fragments with transposing LDS reads).  ``bnb``:
     fuse the consumer BatchNorm-backward reductions into the epilogue."""
@@ -171,6 +177,8 @@ def conv_dgrad(dy, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
         f32 = dy.dtype == torch.float32
         fn = ops().conv32_dgrad if f32 else ops().conv_dgrad
         extra = (wp,) if f32 else ()
+        if f32:
+            dy = _dy_arg(dy, dy_packed)
         if bnb is None:
             fn(dy, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None, *extra)
         else:
@@ -191,12 +199,14 @@ def _conv_dgrad_cpu(dy, w, dx, shp: ConvShape, accumulate: bool) -> None:
     dx.copy_(g.to(dx.dtype))
 
 
-def conv_wgrad(x, dy, dw, shp: ConvShape, accumulate: bool = False) -> None:
+def conv_wgrad(x, dy, dw, shp: ConvShape, accumulate: bool = False, dy_packed: bool = False) -> None:
     """dw (fp32 [Cout][R][S][Cin]) = sum over pixels of dy x im2col(x).
     accumulate=True promises dw is already zero (split-K slices add into it)."""
     if x.is_cuda:
-        fn = ops().conv32_wgrad if x.dtype == torch.float32 else ops().conv_wgrad
-        fn(x, dy, dw, *shp.args(), accumulate)
+        if x.dtype == torch.float32:
+            ops().conv32_wgrad(x, _dy_arg(dy, dy_packed), dw, *shp.args(), accumulate)
+        else:
+            ops().conv_wgrad(x, dy, dw, *shp.args(), accumulate)
         return
     # contiguous NCHW: torch's CPU weight-gradient kernel corrupts the heap on
     # channels-last views for strided 1x1 convs with few channels (observed
@@ -222,7 +232,7 @@ def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShap
 
 
 def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
-                       bnb: BnBwdTarget | None = None, wp=None) -> None:
+                       bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False) -> None:
     """A layer's weight gradient (dw += ..., dw zero on entry) and input
     gradient (as conv_dgrad) -- on the GPU in ONE paired launch, so the two
     independent, latency-bound GEMMs share the CUs (conv.hip
@@ -230,6 +240,7 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
     launch too (conv32.hip conv32_bwd_pair_kernel, when both plans run 64x64
     tiles on the fast address paths; MFL_C32_PAIR=0 for two launches)."""
     if dy.is_cuda and dy.dtype == torch.float32:
+        dy = _dy_arg(dy, dy_packed)
         if bnb is None:
             ops().conv32_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None,
                                        wp)
@@ -312,12 +323,19 @@ class BnSide:
 
 
 def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
-                dy_masked=None, presummed: bool = False, side: BnSide | None = None) -> None:
+                dy_masked=None, presummed: bool = False, side: BnSide | None = None,
+                dx_packed: bool = False) -> None:
     """BN(+ReLU) backward.  ``y`` (the post-activation output) gives the ReLU
     mask; ``dy_masked`` optionally receives the masked upstream gradient (the
     residual-shortcut gradient of an add+ReLU).  ``acc`` (fp64 [2C]) must be
-    zero on entry."""
+    zero on entry.  ``dx_packed`` (fp32 GPU path, bf16x3 conv products): dx
+    receives the packed (hi << 16 | lo) bf16 split of the gradient instead of
+    fp32 -- the dY operand encoding of the layer's dgrad / wgrad kernels, which
+    then decode it with two v_perm per pair instead of splitting it per k-tile."""
     if dy.is_cuda:
+        if dx_packed:
+            assert dy.dtype == torch.float32, "packed dx is an fp32-path encoding"
+            dx = dx.view(torch.int32)
         if side is not None:
             ops().bn32_backward_side(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked, presummed,
                                      side.z, side.mean, side.invstd, side.acc)

@@ -231,6 +231,63 @@ def test_bn32_apply_and_backward_match_host(res, relu, train):
         assert _rel(b, a) <= 1e-5
 
 
+@pytest.mark.parametrize("t", [(8, 16, 16, 128, 128, 3, 1), (8, 16, 16, 64, 128, 3, 2), (8, 16, 16, 64, 128, 1, 2),
+                               (8, 32, 32, 8, 64, 3, 1)], ids=lambda t: "x".join(map(str, t)))
+def test_packed_dy_path_is_bit_identical(t):
+    """bf16x3: the BN backward writes dz as packed hi|lo splits (dx_packed)
+    and the layer's dgrad / wgrad / paired launch decode it (dy_packed) -- the
+    same products as splitting an fp32 dY in the k-loop, so bit-identical
+    outputs; and the packed BN output is exactly split_pack of the fp32 one."""
+    from metisfl_amd.ops import nn as K
+    from metisfl_amd.ops import optim as O
+    prev = K.conv_products()
+    K.set_conv_products("bf16x3")
+    try:
+        N, H, W_, C, Co, R, st = t
+        shp = K.ConvShape(N, H, W_, C, Co, R, R, st, R // 2)
+        g = torch.Generator().manual_seed(21)
+        x = torch.randn(N, H, W_, C, generator=g).to(DEV)
+        w = (torch.randn(Co, R, R, C, generator=g) / (R * R * C) ** 0.5).to(DEV)
+        M = N * shp.P * shp.Q
+        # the BN backward producing dz, fp32 and packed
+        z = torch.randn(M, Co, generator=g).to(DEV)
+        yv = torch.relu(torch.randn(M, Co, generator=g)).to(DEV)
+        dout = torch.randn(M, Co, generator=g).to(DEV)
+        gamma = (torch.rand(Co, generator=g) + 0.5).to(DEV)
+        mean = z.mean(0)
+        invstd = 1.0 / z.var(0, unbiased=False).add(1e-5).sqrt()
+        dz32 = torch.zeros(M, Co, device=DEV)
+        dzp = torch.zeros(M, Co, device=DEV)
+        for out, pk in ((dz32, False), (dzp, True)):
+            acc = torch.zeros(2 * Co, dtype=torch.float64, device=DEV)
+            K.bn_backward(dout, z, yv, Co, gamma, mean, invstd, acc, None, None, out, dx_packed=pk)
+        ref_pack = torch.zeros(M * Co, dtype=torch.int32, device=DEV)
+        O.split_pack(dz32.reshape(-1), ref_pack)
+        torch.cuda.synchronize()
+        assert torch.equal(dzp.view(torch.int32).reshape(-1), ref_pack)
+        dz32 = dz32.reshape(N, shp.P, shp.Q, Co)
+        dzp = dzp.reshape(N, shp.P, shp.Q, Co)
+        res = {}
+        for pk, dz in ((False, dz32), (True, dzp)):
+            dx = torch.zeros(N, H, W_, C, device=DEV)
+            dw = torch.zeros(Co, R, R, C, device=DEV)
+            dx2 = torch.zeros_like(dx)
+            dw2 = torch.zeros_like(dw)
+            if C % 32 == 0:
+                K.conv_backward_pair(x, dz, dw, w, dx, shp, _ws(shp), accumulate=False, dy_packed=pk)
+                K.conv_dgrad(dz, w, dx2, shp, _ws(shp), accumulate=False, dy_packed=pk)
+            K.conv_wgrad(x, dz, dw2, shp, accumulate=False, dy_packed=pk)
+            torch.cuda.synchronize()
+            res[pk] = (dx, dw, dx2, dw2)
+        # dx: deterministic split-K (slices summed in order) -> bit-identical;
+        # dw: split-K slices meet in fp32 atomics, whose order varies run to run
+        assert torch.equal(res[False][0], res[True][0]) and torch.equal(res[False][2], res[True][2])
+        for a, b in ((res[False][1], res[True][1]), (res[False][3], res[True][3])):
+            assert _rel(b, a) <= 1e-6
+    finally:
+        K.set_conv_products(prev)
+
+
 def test_head32_and_gather32_match_host():
     from metisfl_amd.ops import nn as K
     g = torch.Generator().manual_seed(1)
