@@ -115,14 +115,16 @@ const float* wsrc(const torch::Tensor& w, const c10::optional<torch::Tensor>& wp
 // split -- as the layer's fp32 BN backward wrote it when dy is an int32 view of
 // that buffer (bn32_backward with an int32 dx), else packed here into a
 // temporary (stream-ordered lifetime)
-const float* dysrc(const torch::Tensor& dy, int64_t n, torch::Tensor& tmp) {
+// The same holds for the activation operand X of fwd / wgrad (int32: the
+// packed mirror the fp32 BN apply wrote next to its output).
+const float* dysrc(const torch::Tensor& dy, int64_t n, torch::Tensor& tmp, const char* nm = "dy") {
   if (dy.scalar_type() == torch::kInt32) {
-    TORCH_CHECK(g_c32_mode, "a packed (int32) dY needs the bf16x3 conv product mode");
+    TORCH_CHECK(g_c32_mode, "a packed (int32) conv operand needs the bf16x3 conv product mode: ", nm);
     TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.numel() == n,
-                "packed dY: contiguous int32 device tensor of dY's size");
+                "packed operand: contiguous int32 device tensor of the operand's size: ", nm);
     return reinterpret_cast<const float*>(dy.data_ptr());
   }
-  check_f32(dy, n, "dy");
+  check_f32(dy, n, nm);
   if (!g_c32_mode) return fp(dy);
   TORCH_CHECK(n % 4 == 0, "dY is packed in groups of 4");
   tmp = torch::empty({n}, dy.options().dtype(torch::kInt32));
@@ -160,11 +162,12 @@ void conv32_forward(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::opti
                     c10::optional<torch::Tensor> stats, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co,
                     int64_t R, int64_t S, int64_t stride, int64_t pad, c10::optional<torch::Tensor> wp) {
   const auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
-  check_f32(x, (int64_t)N * H * W * C, "x");
+  torch::Tensor xtmp;
+  const float* xs = dysrc(x, (int64_t)N * H * W * C, xtmp, "x");
   check_f32(w, (int64_t)Co * R * S * C, "w");
   check_f32(y, (int64_t)g.M * Co, "y");
   torch::Tensor tmp;
-  run(g, false, fp(x), wsrc(w, wp, tmp), y, ws, stats_ptr(stats, Co), false, nullptr,
+  run(g, false, xs, wsrc(w, wp, tmp), y, ws, stats_ptr(stats, Co), false, nullptr,
       stats.has_value() && stats->defined() ? reps_of(*stats, Co) : 1);
 }
 
@@ -207,8 +210,8 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
                           c10::optional<torch::Tensor> bn_acc, c10::optional<torch::Tensor> wp) {
   const auto gf = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
   const auto gd = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
-  check_f32(x, (int64_t)N * H * W * C, "x");
-  torch::Tensor dtmp;
+  torch::Tensor xtmp, dtmp;
+  const float* xs = dysrc(x, (int64_t)N * H * W * C, xtmp, "x");
   const float* dyp = dysrc(dy, (int64_t)gf.M * Co, dtmp);
   check_f32(dw, (int64_t)Co * R * S * C, "dw");
   check_f32(w, (int64_t)Co * R * S * C, "w");
@@ -241,9 +244,9 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
   torch::Tensor tmp;
   const float* wb = wsrc(w, wp, tmp);
   if (C32_CALL(launch_conv32_bwd_pair, gd, pd, gf, pw, dyp, wb, fp(dx), slab, counters, accumulate,
-                                  fuse ? &f : nullptr, fp(x), fp(dw), cur_stream(dx)))
+                                  fuse ? &f : nullptr, xs, fp(dw), cur_stream(dx)))
     return;
-  C32_CALL(launch_conv32_wgrad, gf, pw, fp(x), dyp, fp(dw), true, cur_stream(dw));
+  C32_CALL(launch_conv32_wgrad, gf, pw, xs, dyp, fp(dw), true, cur_stream(dw));
   C32_CALL(launch_conv32_gemm, gd, true, pd, dyp, wb, fp(dx), slab, counters, nullptr, accumulate,
                           fuse ? &f : nullptr, cur_stream(dx));
 }
@@ -251,13 +254,13 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
 void conv32_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t N, int64_t H, int64_t W, int64_t C,
                   int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate) {
   const auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
-  check_f32(x, (int64_t)N * H * W * C, "x");
-  torch::Tensor dtmp;
+  torch::Tensor xtmp, dtmp;
+  const float* xs = dysrc(x, (int64_t)N * H * W * C, xtmp, "x");
   const float* dyp = dysrc(dy, (int64_t)g.M * Co, dtmp);
   check_f32(dw, (int64_t)Co * R * S * C, "dw");
   const auto p = C32_CALL(plan_conv32, g, 2);
   if (!accumulate && p.splits > 1) dw.zero_();
-  C32_CALL(launch_conv32_wgrad, g, p, fp(x), dyp, fp(dw), accumulate, cur_stream(dw));
+  C32_CALL(launch_conv32_wgrad, g, p, xs, dyp, fp(dw), accumulate, cur_stream(dw));
 }
 
 // ---- BatchNorm -----------------------------------------------------------
@@ -316,13 +319,21 @@ mfl::BnFwdArgs32 bn32_args(torch::Tensor x, int64_t C, c10::optional<torch::Tens
   return a;
 }
 
+// yp (optional, int32 of y's size): also write y's packed bf16x3 split
+uint32_t* yp_ptr(const c10::optional<torch::Tensor>& yp, const torch::Tensor& y) {
+  if (!yp.has_value() || !yp->defined()) return nullptr;
+  TORCH_CHECK(yp->is_cuda() && yp->is_contiguous() && yp->scalar_type() == torch::kInt32 && yp->numel() == y.numel(),
+              "yp: contiguous int32 device tensor of y's size");
+  return reinterpret_cast<uint32_t*>(yp->data_ptr());
+}
+
 void bn32_apply(torch::Tensor x, int64_t C, c10::optional<torch::Tensor> acc, torch::Tensor gamma, torch::Tensor beta,
                 torch::Tensor mean, torch::Tensor invstd, torch::Tensor run_mean, torch::Tensor run_var,
                 c10::optional<torch::Tensor> residual, torch::Tensor y, bool relu, bool train, double momentum,
-                double eps) {
-  mfl::launch_bn32_apply(
-      bn32_args(x, C, acc, gamma, beta, mean, invstd, run_mean, run_var, residual, y, relu, train, momentum, eps),
-      cur_stream(x));
+                double eps, c10::optional<torch::Tensor> yp) {
+  auto a = bn32_args(x, C, acc, gamma, beta, mean, invstd, run_mean, run_var, residual, y, relu, train, momentum, eps);
+  a.yp = yp_ptr(yp, y);
+  mfl::launch_bn32_apply(a, cur_stream(x));
 }
 
 // shortcut BN (no ReLU) + conv1 BN (ReLU) of a downsampling block in one launch
@@ -331,11 +342,12 @@ void bn32_apply_pair(torch::Tensor x1, torch::Tensor gamma1, torch::Tensor beta1
                      torch::Tensor y1, torch::Tensor x2, torch::Tensor gamma2, torch::Tensor beta2,
                      torch::Tensor mean2, torch::Tensor invstd2, torch::Tensor rm2, torch::Tensor rv2,
                      c10::optional<torch::Tensor> acc2, torch::Tensor y2, int64_t C, bool train, double momentum,
-                     double eps) {
+                     double eps, c10::optional<torch::Tensor> yp2) {
   const auto a1 = bn32_args(x1, C, acc1, gamma1, beta1, mean1, invstd1, rm1, rv1, c10::nullopt, y1, false, train,
                             momentum, eps);
-  const auto a2 = bn32_args(x2, C, acc2, gamma2, beta2, mean2, invstd2, rm2, rv2, c10::nullopt, y2, true, train,
-                            momentum, eps);
+  auto a2 = bn32_args(x2, C, acc2, gamma2, beta2, mean2, invstd2, rm2, rv2, c10::nullopt, y2, true, train,
+                      momentum, eps);
+  a2.yp = yp_ptr(yp2, y2);
   mfl::launch_bn32_apply_pair(a1, a2, cur_stream(x1));
 }
 
@@ -348,7 +360,8 @@ void conv32_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c1
   const auto g1 = fwd_geom(N, H, W, C, Co, 3, 3, 2, 1);
   const auto g2 = fwd_geom(N, H, W, C, Co, 1, 1, 2, 0);
   TORCH_CHECK(g1.M == g2.M, "conv1 / shortcut output sizes differ");
-  check_f32(x, N * H * W * C, "x");
+  torch::Tensor xtmp;
+  const float* xs = dysrc(x, N * H * W * C, xtmp, "x");
   check_f32(w1, Co * 9 * C, "w1");
   check_f32(w2, Co * C, "w2");
   check_f32(y1, (int64_t)g1.M * Co, "y1");
@@ -376,10 +389,10 @@ void conv32_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c1
   const float* wb1 = wsrc(w1, wp1, t1);
   const float* wb2 = wsrc(w2, wp2, t2);
   if (C32_CALL(launch_conv32_fwd_pair, g1, p1, wb1, fp(y1), ys1, c1, st1, r1, g2, p2, wb2, fp(y2), ys2, c2, st2, r2,
-                                  fp(x), cur_stream(x)))
+                                  xs, cur_stream(y1)))
     return;
-  run(g1, false, fp(x), wb1, y1, ws1, st1, false, nullptr, r1);
-  run(g2, false, fp(x), wb2, y2, ws2, st2, false, nullptr, r2);
+  run(g1, false, xs, wb1, y1, ws1, st1, false, nullptr, r1);
+  run(g2, false, xs, wb2, y2, ws2, st2, false, nullptr, r2);
 }
 
 void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,

@@ -172,6 +172,8 @@ __device__ __forceinline__ void bn32_apply_body(const BnFwdArgs32& a, int64_t nv
       v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
     }
     reinterpret_cast<float4*>(a.y)[i] = v;
+    if (a.yp)  // uniform
+      reinterpret_cast<uint4*>(a.yp)[i] = make_uint4(split_pack(v.x), split_pack(v.y), split_pack(v.z), split_pack(v.w));
   }
 }
 

@@ -132,7 +132,9 @@ __device__ __forceinline__ void unpack_hl(const f32x4& p, const f32x4& q, bf16x8
 }
 
 // BPACK / APACK (bf16x3 only): the B / A fragments hold packed hi|lo dwords
-// (B: the optimizer's weight mirror; A: dY as the fp32 BN backward wrote it).
+// (the optimizer's weight mirror; activations as the fp32 BN apply wrote their
+// mirror; dY as the fp32 BN backward wrote it).  Every c32s operand arrives
+// packed, so the k-loop never splits.
 template <int TM, int TN, bool BPACK = false, bool APACK = false, typename FA, typename FB>
 __device__ __forceinline__ void mma_tile(const FA& fa, const FB& fb, f32x16 (&acc)[TM][TN]) {
 #if MFL_C32_BF16X3
@@ -641,8 +643,8 @@ __device__ __forceinline__ void conv32_gemm_body(const Conv32Args& a, const Blk&
   auto mma = [&](auto set) {
     constexpr int S = decltype(set)::value;
     if constexpr (MFL_C32_DBG & 1) return;
-    // fwd / dgrad: B = the weight mirror; dgrad: A = dY, packed by its producer
-    mma_tile<TM, TN, MFL_C32_BF16X3 != 0, MFL_C32_BF16X3 != 0 && DGRAD>(fa[S], fb[S], acc);
+    // B = the weight mirror; A = X (fwd) or dY (dgrad), packed by its producer
+    mma_tile<TM, TN, MFL_C32_BF16X3 != 0, MFL_C32_BF16X3 != 0>(fa[S], fb[S], acc);
     interleave_mfma<kTileMfma<TM, TN>, kTileValu>();
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -868,7 +870,7 @@ __device__ __forceinline__ void conv32_wgrad_body(const Conv32Args& a, const Blk
   auto mma = [&](auto set) {
     constexpr int S = decltype(set)::value;
     if constexpr (MFL_C32_DBG & 1) return;
-    mma_tile<TM, TN, false, MFL_C32_BF16X3 != 0>(fa[S], fb[S], acc);  // A = dY (packed), B = X
+    mma_tile<TM, TN, MFL_C32_BF16X3 != 0, MFL_C32_BF16X3 != 0>(fa[S], fb[S], acc);  // A = dY, B = X (both packed)
     interleave_mfma<kTileMfma<TM, TN>, kTileValu>();
     __builtin_amdgcn_sched_barrier(0);
   };

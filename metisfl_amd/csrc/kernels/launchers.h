@@ -101,6 +101,9 @@ struct BnFwdArgs32 {
   const float* x;
   const float* residual;  // optional
   float* y;
+  // optional: y's packed bf16x3 split (split_pack, common.h) -- the activation
+  // operand the bf16x3 forward / wgrad convolutions decode without splitting
+  uint32_t* yp;
   const double* acc;
   const float* gamma;
   const float* beta;

@@ -146,6 +146,12 @@ class ConvBN(Layer):
         self.z = torch.zeros(self.out_shape, **bf)      # conv output (pre-BN)
         self.y = torch.zeros(self.out_shape, **bf)      # layer output
         self.dz = torch.zeros(self.out_shape, **bf)
+        # fp32 GPU path, bf16x3 conv products: the BN apply also writes y's
+        # packed (hi << 16 | lo) split, the operand the consuming convolutions
+        # (forward and wgrad) decode instead of splitting per k-tile
+        self.yp = (torch.zeros(self.out_shape, dtype=torch.int32, device=device)
+                   if ws.dtype == torch.float32 and torch.device(device).type == "cuda" else None)
+        self.xp = None
         self.mean = torch.zeros(s.Co, **f32)
         self.invstd = torch.zeros(s.Co, **f32)
         # fp64 [2C] statistics accumulators (forward sums, backward sums),
@@ -163,11 +169,19 @@ class ConvBN(Layer):
         ws.need_split(self.pf.workspace)
         ws.need_split(self.pd.workspace)
 
-    def forward(self, x: torch.Tensor, residual: torch.Tensor | None = None, train: bool = True):
+    def out_p(self) -> torch.Tensor | None:
+        """The packed mirror of this layer's output (None unless the fp32 GPU
+        path runs bf16x3 conv products)."""
+        return self.yp if self.yp is not None and K.conv_products() == "bf16x3" else None
+
+    def forward(self, x: torch.Tensor, residual: torch.Tensor | None = None, train: bool = True,
+                xp: torch.Tensor | None = None):
+        """``xp``: the packed mirror of ``x`` its producer wrote (or None)."""
         s = self.shp
         self.x = x
+        self.xp = xp
         K.conv_forward(x, self.w16, self.z, s, self._split(), self.ws.acc(self.acc_f) if train else None,
-                       wp=self.wp)
+                       wp=self.wp, xp=xp)
         return self.bn_forward(residual, train)
 
     def bn_forward(self, residual: torch.Tensor | None = None, train: bool = True):
@@ -175,7 +189,7 @@ class ConvBN(Layer):
         s = self.shp
         K.bn_apply(self.z, s.Co, self.ws.acc(self.acc_f), self.gamma, self.beta, self.mean,
                    self.invstd, self.rmean, self.rvar, self.y, residual, self.relu, train,
-                   self.momentum, self.eps)
+                   self.momentum, self.eps, yp=self.out_p())
         return self.y
 
     def bn_target(self) -> K.BnBwdTarget:
@@ -214,10 +228,10 @@ class ConvBN(Layer):
         if dx is not None and not self.ws.overlap:
             # both GEMMs in one launch (their workgroups share the CUs)
             K.conv_backward_pair(self.x, self.dz, self.dw, self.w16, dx, s, self._split(), accumulate,
-                                 bnb=bnb, wp=self.wp, dy_packed=pk)
+                                 bnb=bnb, wp=self.wp, dy_packed=pk, xp=self.xp)
             return
         with self.ws.fork():
-            K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True, dy_packed=pk)
+            K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True, dy_packed=pk, xp=self.xp)
         if dx is not None:
             K.conv_dgrad(self.dz, self.w16, dx, s, self._split(), accumulate, bnb=bnb, wp=self.wp, dy_packed=pk)
 
@@ -255,37 +269,44 @@ class BasicBlock(Layer):
         for l in self.sublayers():
             l.prepare_backward()
 
-    def forward(self, x, train=True):
+    def out_p(self):
+        return self.c2.out_p()
+
+    def forward(self, x, train=True, xp=None):
+        """``xp``: the packed mirror of ``x`` (bf16x3 fp32 path) or None."""
         if self.sc is None:
-            a = self.c1.forward(x, train=train)
-            return self.c2.forward(a, residual=x, train=train)
+            a = self.c1.forward(x, train=train, xp=xp)
+            return self.c2.forward(a, residual=x, train=train, xp=self.c1.out_p())
         if not self.c1.ws.overlap and self.c1.shp.R == 3 and self.c1.shp.stride == 2:
             # conv1 and the projection shortcut in one paired launch
             c1, sc = self.c1, self.sc
             c1.x = sc.x = x
+            c1.xp = sc.xp = xp
             K.conv_forward_pair(x, c1.w16, c1.z, c1._split(), c1.ws.acc(c1.acc_f) if train else None,
                                 sc.w16, sc.z, sc._split(), sc.ws.acc(sc.acc_f) if train else None, c1.shp,
-                                wp1=c1.wp, wp2=sc.wp)
+                                wp1=c1.wp, wp2=sc.wp, xp=xp)
             if x.is_cuda and not sc.relu and c1.relu:
-                # ... and their two BatchNorms in one launch
-                pair = K.ops().bn32_apply_pair if x.dtype == torch.float32 else K.ops().bn_apply_pair
+                # ... and their two BatchNorms in one launch (the shortcut's
+                # output only feeds the residual add: no packed mirror)
+                f32 = x.dtype == torch.float32
+                pair = K.ops().bn32_apply_pair if f32 else K.ops().bn_apply_pair
                 pair(sc.z, sc.gamma, sc.beta, sc.mean, sc.invstd, sc.rmean, sc.rvar,
                      sc.ws.acc(sc.acc_f) if train else None, sc.y,
                      c1.z, c1.gamma, c1.beta, c1.mean, c1.invstd, c1.rmean, c1.rvar,
                      c1.ws.acc(c1.acc_f) if train else None, c1.y,
-                     c1.shp.Co, train, c1.momentum, c1.eps)
+                     c1.shp.Co, train, c1.momentum, c1.eps, *((c1.out_p(),) if f32 else ()))
                 r, a = sc.y, c1.y
             else:
                 r = sc.bn_forward(train=train)
                 a = c1.bn_forward(train=train)
-            return self.c2.forward(a, residual=r, train=train)
+            return self.c2.forward(a, residual=r, train=train, xp=c1.out_p())
         # projection shortcut runs concurrently with conv1 (side stream, own
         # split-K workspace); conv2 consumes both after the join
         with self.c1.ws.fork():
-            r = self.sc.forward(x, train=train)
-        a = self.c1.forward(x, train=train)
+            r = self.sc.forward(x, train=train, xp=xp)
+        a = self.c1.forward(x, train=train, xp=xp)
         self.c1.ws.join()
-        return self.c2.forward(a, residual=r, train=train)
+        return self.c2.forward(a, residual=r, train=train, xp=self.c1.out_p())
 
     def backward(self, dout, dx, presummed: bool = False, prev: K.BnBwdTarget | None = None):
         """``presummed``: conv2's BN reductions were fused into dout's producer;

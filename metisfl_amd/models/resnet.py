@@ -31,6 +31,7 @@ import torch
 
 from metisfl_amd.models.layers import BasicBlock, ClassifierHead, ConvBN
 from metisfl_amd.models.net import StaticNet
+from metisfl_amd.ops.optim import split_pack
 
 DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16}
 DEFAULT_CONV_PRODUCTS = "bf16x3"
@@ -82,11 +83,25 @@ class ResNet18(StaticNet):
         dev = self.device
         # gradient buffers at block boundaries: dx of block i is dout of block i-1
         self.dacts = [torch.zeros(b.in_shape, dtype=self.compute_dtype, device=dev) for b in self.blocks]
+        self._xbp = None  # packed input batch (bf16x3 fp32 path), sized on first use
+        if self.stem.yp is not None:
+            self._xbp = torch.zeros((self.B,) + self.input_shape, dtype=torch.int32, device=dev)
 
     def forward(self, x, train):
-        h = self.stem.forward(x, train=train)
+        xp = None
+        if self.stem.out_p() is not None:
+            # bf16x3 fp32 path: every conv operand arrives packed (hi << 16 |
+            # lo); the gathered input batch is packed once for the stem's
+            # forward and wgrad, the BN applies write the rest
+            if self._xbp is None or self._xbp.shape != x.shape:
+                self._xbp = torch.zeros(x.shape, dtype=torch.int32, device=x.device)
+            split_pack(x.reshape(-1), self._xbp.view(-1))
+            xp = self._xbp
+        h = self.stem.forward(x, train=train, xp=xp)
+        hp = self.stem.out_p()
         for b in self.blocks:
-            h = b.forward(h, train=train)
+            h = b.forward(h, train=train, xp=hp)
+            hp = b.out_p()
         return h
 
     def backward(self, dlast):

@@ -122,14 +122,14 @@ def _acc_stats_cpu(y: torch.Tensor, acc: torch.Tensor) -> None:
     acc[C:2 * C] += (yf * yf).sum(0)
 
 
-def conv_forward(x, w, y, shp: ConvShape, ws=None, stats=None, wp=None) -> None:
+def conv_forward(x, w, y, shp: ConvShape, ws=None, stats=None, wp=None, xp=None) -> None:
     """y = conv(x, w); ``stats`` (fp64 [2*Cout]) accumulates the per-channel
     sum / sum-of-squares of the bf16 output for the following BatchNorm.
-    ``wp``: the packed bf16x3 mirror of ``w`` (fp32 / bf16x3 mode; packed on
-    the fly when omitted)."""
+    ``wp`` / ``xp``: the packed bf16x3 mirrors (int32) of ``w`` / ``x`` (fp32 /
+    bf16x3 mode; packed on the fly when omitted)."""
     if x.is_cuda:
         if x.dtype == torch.float32:
-            ops().conv32_forward(x, w, y, ws, stats, *shp.args(), wp)
+            ops().conv32_forward(x if xp is None else xp, w, y, ws, stats, *shp.args(), wp)
         else:
             ops().conv_forward(x, w, y, ws, stats, *shp.args())
         return
@@ -199,12 +199,13 @@ def _conv_dgrad_cpu(dy, w, dx, shp: ConvShape, accumulate: bool) -> None:
     dx.copy_(g.to(dx.dtype))
 
 
-def conv_wgrad(x, dy, dw, shp: ConvShape, accumulate: bool = False, dy_packed: bool = False) -> None:
+def conv_wgrad(x, dy, dw, shp: ConvShape, accumulate: bool = False, dy_packed: bool = False,
+               xp=None) -> None:
     """dw (fp32 [Cout][R][S][Cin]) = sum over pixels of dy x im2col(x).
     accumulate=True promises dw is already zero (split-K slices add into it)."""
     if x.is_cuda:
         if x.dtype == torch.float32:
-            ops().conv32_wgrad(x, _dy_arg(dy, dy_packed), dw, *shp.args(), accumulate)
+            ops().conv32_wgrad(x if xp is None else xp, _dy_arg(dy, dy_packed), dw, *shp.args(), accumulate)
         else:
             ops().conv_wgrad(x, dy, dw, *shp.args(), accumulate)
         return
@@ -216,14 +217,15 @@ def conv_wgrad(x, dy, dw, shp: ConvShape, accumulate: bool = False, dy_packed: b
     dw.copy_(g.permute(0, 2, 3, 1).reshape(dw.shape))
 
 
-def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShape, wp1=None, wp2=None) -> None:
+def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShape, wp1=None, wp2=None,
+                      xp=None) -> None:
     """A downsampling block's conv1 (3x3, stride 2; ``shp``) and its 1x1 / stride-2
     projection shortcut of the same x -- one paired launch on the GPU."""
     assert shp.R == 3 and shp.stride == 2
     if x.is_cuda:
         if x.dtype == torch.float32:
-            ops().conv32_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp.N, shp.H, shp.W, shp.C,
-                                      shp.Co, wp1, wp2)
+            ops().conv32_forward_pair(x if xp is None else xp, w1, y1, ws1, stats1, w2, y2, ws2, stats2,
+                                      shp.N, shp.H, shp.W, shp.C, shp.Co, wp1, wp2)
         else:
             ops().conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp.N, shp.H, shp.W, shp.C, shp.Co)
         return
@@ -232,7 +234,7 @@ def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShap
 
 
 def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
-                       bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False) -> None:
+                       bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False, xp=None) -> None:
     """A layer's weight gradient (dw += ..., dw zero on entry) and input
     gradient (as conv_dgrad) -- on the GPU in ONE paired launch, so the two
     independent, latency-bound GEMMs share the CUs (conv.hip
@@ -241,11 +243,12 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
     tiles on the fast address paths; MFL_C32_PAIR=0 for two launches)."""
     if dy.is_cuda and dy.dtype == torch.float32:
         dy = _dy_arg(dy, dy_packed)
+        xa = x if xp is None else xp
         if bnb is None:
-            ops().conv32_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None,
+            ops().conv32_backward_pair(xa, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None,
                                        wp)
         else:
-            ops().conv32_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
+            ops().conv32_backward_pair(xa, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
                                        bnb.invstd, bnb.acc, wp)
         return
     if dy.is_cuda:
@@ -278,13 +281,18 @@ def bn_stats(x, C: int, acc) -> None:
 
 def bn_apply(x, C: int, acc, gamma, beta, mean, invstd, run_mean, run_var, y, residual=None,
              relu: bool = False, train: bool = True, momentum: float = 0.1,
-             eps: float = 1e-5) -> None:
+             eps: float = 1e-5, yp=None) -> None:
     """y = relu?(BN(x) + residual).  train: batch statistics from ``acc`` (sums
     over the M rows), publishes mean/invstd, updates running stats; eval:
-    running statistics."""
+    running statistics.  ``yp`` (fp32 GPU path): also write y's packed bf16x3
+    split (int32) -- the operand the next convolutions read."""
     if x.is_cuda:
-        fn = ops().bn32_apply if x.dtype == torch.float32 else ops().bn_apply
-        fn(x, C, acc, gamma, beta, mean, invstd, run_mean, run_var, residual, y, relu, train, momentum, eps)
+        if x.dtype == torch.float32:
+            ops().bn32_apply(x, C, acc, gamma, beta, mean, invstd, run_mean, run_var, residual, y, relu, train,
+                             momentum, eps, yp)
+        else:
+            ops().bn_apply(x, C, acc, gamma, beta, mean, invstd, run_mean, run_var, residual, y, relu, train,
+                           momentum, eps)
         return
     M = x.numel() // C
     if train:

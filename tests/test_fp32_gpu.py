@@ -284,6 +284,32 @@ def test_packed_dy_path_is_bit_identical(t):
         assert torch.equal(res[False][0], res[True][0]) and torch.equal(res[False][2], res[True][2])
         for a, b in ((res[False][1], res[True][1]), (res[False][3], res[True][3])):
             assert _rel(b, a) <= 1e-6
+        # activations: the packed mirror a BN apply writes (yp) feeds the
+        # forward / wgrad as xp -- same bits as packing x on the fly
+        xp = torch.zeros(x.shape, dtype=torch.int32, device=DEV)
+        O.split_pack(x.reshape(-1), xp.view(-1))
+        y1 = torch.zeros(N, shp.P, shp.Q, Co, device=DEV)
+        y2 = torch.zeros_like(y1)
+        K.conv_forward(x, w, y1, shp, _ws(shp))
+        K.conv_forward(x, w, y2, shp, _ws(shp), xp=xp)
+        dwa = torch.zeros(Co, R, R, C, device=DEV)
+        dwb = torch.zeros_like(dwa)
+        K.conv_wgrad(x, dzp, dwa, shp, accumulate=False, dy_packed=True)
+        K.conv_wgrad(x, dzp, dwb, shp, accumulate=False, dy_packed=True, xp=xp)
+        C2 = Co
+        zz = torch.randn(M, C2, generator=g).to(DEV)
+        acc = torch.zeros(2 * C2, dtype=torch.float64, device=DEV)
+        K.bn_stats(zz, C2, acc)
+        yb = torch.zeros(M, C2, device=DEV)
+        ybp = torch.zeros(M, C2, dtype=torch.int32, device=DEV)
+        K.bn_apply(zz, C2, acc, gamma, gamma - 1, torch.zeros(C2, device=DEV), torch.zeros(C2, device=DEV),
+                   torch.zeros(C2, device=DEV), torch.ones(C2, device=DEV), yb, relu=True, yp=ybp)
+        ref_y = torch.zeros(M * C2, dtype=torch.int32, device=DEV)
+        O.split_pack(yb.reshape(-1), ref_y)
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y2)
+        assert _rel(dwb, dwa) <= 1e-6
+        assert torch.equal(ybp.reshape(-1), ref_y)
     finally:
         K.set_conv_products(prev)
 
