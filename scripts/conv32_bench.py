@@ -67,9 +67,24 @@ def main():
         dx = torch.zeros(N, H, W, C, device=dev)
         dw = torch.zeros(Co, k, k, C, device=dev)
         flop = 2.0 * N * shp.P * shp.Q * Co * k * k * C
-        runs = {0: lambda: K.conv_forward(x, w, y, shp, ws, st),
-                1: lambda: K.conv_dgrad(dy, w, dx, shp, ws, False),
-                2: lambda: K.conv_wgrad(x, dy, dw, shp, accumulate=True)}
+        if a.products == "bf16x3":
+            # as in the model: operands arrive as packed hi|lo mirrors written
+            # by their producers (no per-call packing inside the timing)
+            from metisfl_amd.ops.optim import split_pack
+            wp = torch.zeros(w.shape, dtype=torch.int32, device=dev)
+            split_pack(w.reshape(-1), wp.view(-1))
+            xp = torch.zeros(x.shape, dtype=torch.int32, device=dev)
+            split_pack(x.reshape(-1), xp.view(-1))
+            dyp = torch.zeros(dy.shape, dtype=torch.int32, device=dev)
+            split_pack(dy.reshape(-1), dyp.view(-1))
+            dyv = dyp.view(torch.float32)
+            runs = {0: lambda: K.conv_forward(x, w, y, shp, ws, st, wp=wp, xp=xp),
+                    1: lambda: K.conv_dgrad(dyv, w, dx, shp, ws, False, wp=wp, dy_packed=True),
+                    2: lambda: K.conv_wgrad(x, dyv, dw, shp, accumulate=True, dy_packed=True, xp=xp)}
+        else:
+            runs = {0: lambda: K.conv_forward(x, w, y, shp, ws, st),
+                    1: lambda: K.conv_dgrad(dy, w, dx, shp, ws, False),
+                    2: lambda: K.conv_wgrad(x, dy, dw, shp, accumulate=True)}
         for mode in map(int, a.modes.split(",")):
             if mode == 1 and C == 8:
                 continue
