@@ -1045,7 +1045,11 @@ struct TunedPlan {
 };
 #if MFL_C32_BF16X3
 // profiles/r2/c32x3_sweep.log; dgrad / wgrad stay 64x64 where that lets the
-// layer's backward run as one paired launch
+// layer's backward run as one paired launch.  Re-swept with pre-split (packed)
+// operands (profiles/r2/xpack/c32x3_packed_sweep.log): stand-alone, the 32x32
+// forward then prefers 64x64 tiles (15.8 vs 17.4 us) and one wgrad 1 split,
+// but inside the step neither moved (forward 17.2 vs 17.35 us per call,
+// profiles/r2/xpack/retune_negative/), so the table is unchanged.
 constexpr TunedPlan kTuned[] = {
     {0, 32, 32, 32, 8, 64, 3, 1, 64, 64, 1},    {0, 32, 32, 32, 64, 64, 3, 1, 128, 64, 1},
     {0, 32, 32, 32, 64, 128, 3, 2, 64, 64, 1},  {0, 32, 16, 16, 128, 128, 3, 1, 64, 64, 2},
