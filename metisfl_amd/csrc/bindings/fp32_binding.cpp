@@ -497,7 +497,8 @@ void head32_forward_backward(torch::Tensor x, int64_t B, int64_t HW, int64_t C, 
 
 // fp32 rows are gathered as 16-B units, like the bf16 ones
 void gather_batch32(torch::Tensor shard, torch::Tensor labels, torch::Tensor perm, torch::Tensor step,
-                    int64_t steps_per_epoch, int64_t B, torch::Tensor xb, torch::Tensor yb) {
+                    int64_t steps_per_epoch, int64_t B, torch::Tensor xb, torch::Tensor yb,
+                    c10::optional<torch::Tensor> xp) {
   check_f32(shard, 0, "shard", false);
   check_f32(xb, 0, "xb", false);
   for (auto* t : {&labels, &perm, &step, &yb})
@@ -510,7 +511,8 @@ void gather_batch32(torch::Tensor shard, torch::Tensor labels, torch::Tensor per
   TORCH_CHECK(perm.numel() >= steps_per_epoch * B, "permutation too short");
   mfl::launch_gather_batch(reinterpret_cast<const uint16_t*>(shard.data_ptr()), labels.data_ptr<int>(),
                            perm.data_ptr<int>(), step.data_ptr<int>(), (int)steps_per_epoch, (int)B, row * 2,
-                           reinterpret_cast<uint16_t*>(xb.data_ptr()), yb.data_ptr<int>(), cur_stream(shard));
+                           reinterpret_cast<uint16_t*>(xb.data_ptr()), yb.data_ptr<int>(), cur_stream(shard),
+                           yp_ptr(xp, xb));
 }
 
 }  // namespace

@@ -165,7 +165,7 @@ void launch_head_wgrad(const float* feat, const float* dlogits, int B, int C, in
 // ---- data.hip ------------------------------------------------------------
 void launch_gather_batch(const uint16_t* shard, const int* labels, const int* perm,
                          const int* step, int steps_per_epoch, int B, int64_t row_elems,
-                         uint16_t* xb, int* yb, hipStream_t s);
+                         uint16_t* xb, int* yb, hipStream_t s, uint32_t* xp = nullptr);
 
 // ---- layers.hip (example-model layers) -------------------------------------
 void launch_bias_act_fwd(uint16_t* y, const float* bias, int64_t M, int N, int act, hipStream_t s);

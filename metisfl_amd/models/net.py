@@ -106,6 +106,11 @@ class StaticNet:
     def post_bind(self) -> None:
         """Allocate model-level buffers once layers are bound."""
 
+    def packed_input(self) -> torch.Tensor | None:
+        """A buffer the batch gather also fills with the packed bf16x3 split of
+        ``xb`` (models whose first conv reads packed operands), else None."""
+        return None
+
     def all_layers(self) -> list[Layer]:
         raise NotImplementedError
 
@@ -124,7 +129,8 @@ class StaticNet:
         st = self.state
         if not self.zero_grad_in_optimizer:
             st.grad32.zero_()
-        K.gather_batch(ds.x, ds.y, ds.perm, st.step, ds.steps_per_epoch, self.B, self.xb, self.yb)
+        K.gather_batch(ds.x, ds.y, ds.perm, st.step, ds.steps_per_epoch, self.B, self.xb, self.yb,
+                       xp=self.packed_input())
         out = self.forward(self.xb, train=True)
         dlast = self.head.forward_backward(out, self.yb, self.stats, train=True)
         for l in self.all_layers():
@@ -138,7 +144,7 @@ class StaticNet:
 
     def _eval_body(self, ds: DeviceDataset) -> None:
         K.gather_batch(ds.x, ds.y, ds.perm, self.eval_step_ctr, ds.steps_per_epoch, self.B,
-                       self.xb, self.yb)
+                       self.xb, self.yb, xp=self.packed_input())
         out = self.forward(self.xb, train=False)
         self.head.forward_backward(out, self.yb, self.stats, train=False)
         opt_ops.tick(self.eval_step_ctr, 1)

@@ -87,15 +87,20 @@ class ResNet18(StaticNet):
         if self.stem.yp is not None:
             self._xbp = torch.zeros((self.B,) + self.input_shape, dtype=torch.int32, device=dev)
 
+    def packed_input(self):
+        return self._xbp if self.stem.out_p() is not None else None
+
     def forward(self, x, train):
         xp = None
         if self.stem.out_p() is not None:
             # bf16x3 fp32 path: every conv operand arrives packed (hi << 16 |
-            # lo); the gathered input batch is packed once for the stem's
-            # forward and wgrad, the BN applies write the rest
+            # lo); the batch gather packs the input for the stem's forward and
+            # wgrad (other callers' inputs are packed here), the BN applies
+            # write the rest
             if self._xbp is None or self._xbp.shape != x.shape:
                 self._xbp = torch.zeros(x.shape, dtype=torch.int32, device=x.device)
-            split_pack(x.reshape(-1), self._xbp.view(-1))
+            if x is not getattr(self, "xb", None):
+                split_pack(x.reshape(-1), self._xbp.view(-1))
             xp = self._xbp
         h = self.stem.forward(x, train=train, xp=xp)
         hp = self.stem.out_p()

@@ -426,11 +426,17 @@ def head_wgrad(feat, dlogits, B: int, C: int, K: int, dW, db) -> None:
         db.copy_(d.sum(0))
 
 
-def gather_batch(shard, labels, perm, step, steps_per_epoch: int, B: int, xb, yb) -> None:
+def gather_batch(shard, labels, perm, step, steps_per_epoch: int, B: int, xb, yb, xp=None) -> None:
+    """xb / yb <- the step's mini-batch.  ``xp`` (fp32 shards on the GPU): also
+    write the batch's packed bf16x3 split (int32), the stem conv's operand."""
     if shard.is_cuda:
-        fn = ops().gather_batch32 if shard.dtype == torch.float32 else ops().gather_batch
-        fn(shard, labels, perm, step, steps_per_epoch, B, xb, yb)
+        if shard.dtype == torch.float32:
+            ops().gather_batch32(shard, labels, perm, step, steps_per_epoch, B, xb, yb, xp)
+        else:
+            ops().gather_batch(shard, labels, perm, step, steps_per_epoch, B, xb, yb)
         return
+    if xp is not None:
+        raise ValueError("packed input batches exist on the fp32 GPU path only")
     s = int(step[0]) % steps_per_epoch
     idx = perm[s * B:(s + 1) * B].long()
     xb.copy_(shard.view(labels.numel(), -1)[idx].reshape(xb.shape))
