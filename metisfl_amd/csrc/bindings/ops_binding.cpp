@@ -411,6 +411,7 @@ void register_layers(pybind11::module& m);
 void register_bert(pybind11::module& m);
 void register_ckks(pybind11::module& m);
 void register_fp32(pybind11::module& m);
+void register_hconv(pybind11::module& m);
 
 PYBIND11_MODULE(_ops, m) {
   m.doc() = "metisfl_amd hand-written HIP (gfx950) kernels";
@@ -440,4 +441,5 @@ PYBIND11_MODULE(_ops, m) {
   register_bert(m);
   register_ckks(m);
   register_fp32(m);
+  register_hconv(m);
 }

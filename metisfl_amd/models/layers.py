@@ -79,6 +79,42 @@ class Workspace:
             torch.cuda.current_stream(self.side.device).wait_stream(self.side)
 
 
+# Host-side tests run the fused-fill orchestration on the CPU references.
+FUSED_FILL_CPU = os.environ.get("METISFL_AMD_FUSED_FILL_CPU", "0") == "1"
+
+
+class Pending:
+    """An activation that has not been materialised yet:
+    T = relu?(BN_src(z) [+ res | + BN_r(zr)]).  Its consumer applies T in the
+    operand fill (halo conv) and writes it into ``y`` / ``yp`` (the owning
+    layer's output buffers); ``materialize`` runs it as a BatchNorm apply
+    instead, for consumers without a fused fill (stride-2 convs, the head)."""
+
+    def __init__(self, layer: "ConvBN", res: torch.Tensor | None = None, res_layer: "ConvBN | None" = None):
+        self.layer = layer
+        self.z = layer.z
+        self.bn = layer.bn_params()
+        self.relu = layer.relu
+        self.res = res
+        self.res_layer = res_layer  # residual = BN of this (projection shortcut) layer's z
+        self.zr = res_layer.z if res_layer is not None else None
+        self.bnr = res_layer.bn_params() if res_layer is not None else None
+        self.y = layer.y
+        self.yp = layer.out_p()
+
+    @staticmethod
+    def of(layer: "ConvBN") -> "Pending":
+        return Pending(layer)
+
+    def materialize(self, train: bool) -> torch.Tensor:
+        """BatchNorm apply(s) writing y (+ yp); returns y."""
+        res = self.res
+        if self.res_layer is not None:
+            res = self.res_layer.bn_forward(train=train)
+        self.layer.bn_forward(res, train)
+        return self.y
+
+
 class Layer:
     def specs(self) -> list[VarSpec]:
         return []
@@ -168,20 +204,52 @@ class ConvBN(Layer):
         self.pw = K.conv_plan(2, s, dev, ws.dtype)
         ws.need_split(self.pf.workspace)
         ws.need_split(self.pd.workspace)
+        # halo conv with the fused BN fill: fp32 activations with bf16x3
+        # products on the GPU (or FUSED_FILL_CPU for the host-side tests)
+        self._hconv_ws = -1
+        if ws.dtype == torch.float32 and (
+                (dev.type == "cuda" and K.conv_products() == "bf16x3") or (dev.type == "cpu" and FUSED_FILL_CPU)):
+            self._hconv_ws = K.hconv_workspace(s, dev)
+            if self._hconv_ws > 0:
+                ws.need_split(self._hconv_ws)
 
     def out_p(self) -> torch.Tensor | None:
         """The packed mirror of this layer's output (None unless the fp32 GPU
         path runs bf16x3 conv products)."""
         return self.yp if self.yp is not None and K.conv_products() == "bf16x3" else None
 
+    def bn_params(self) -> K.BnParams:
+        return K.BnParams(self.ws.acc(self.acc_f), self.gamma, self.beta, self.mean, self.invstd,
+                          self.rmean, self.rvar, self.momentum, self.eps)
+
+    def hconv_ok(self) -> bool:
+        """Whether this conv runs as a halo-tiled conv with its input's BN
+        fused into the operand fill (fp32 activations, bf16x3 products)."""
+        return self._hconv_ws >= 0
+
+    def forward_fused(self, src: "Pending", train: bool = True) -> "Pending":
+        """z = conv(T(src)) with the producer's BatchNorm (+ residual, + ReLU)
+        applied in this conv's operand fill; the owner tiles materialise T(src)
+        into src's y / yp.  Returns this layer's output as the next Pending."""
+        s = self.shp
+        self.x, self.xp = src.y, src.yp
+        K.hconv_forward(src.z, self.wp, self.w16, self.z, s, src.bn, train, src.relu, ws=self._split(),
+                        stats=self.ws.acc(self.acc_f) if train else None, res=src.res, zr=src.zr,
+                        bnr=src.bnr, y=src.y, yp=src.yp)
+        return Pending.of(self)
+
     def forward(self, x: torch.Tensor, residual: torch.Tensor | None = None, train: bool = True,
-                xp: torch.Tensor | None = None):
-        """``xp``: the packed mirror of ``x`` its producer wrote (or None)."""
+                xp: torch.Tensor | None = None, bn: bool = True):
+        """``xp``: the packed mirror of ``x`` its producer wrote (or None).
+        ``bn=False``: the convolution only (its BatchNorm is applied by the
+        consumer, see forward_fused); returns None."""
         s = self.shp
         self.x = x
         self.xp = xp
         K.conv_forward(x, self.w16, self.z, s, self._split(), self.ws.acc(self.acc_f) if train else None,
                        wp=self.wp, xp=xp)
+        if not bn:
+            return None
         return self.bn_forward(residual, train)
 
     def bn_forward(self, residual: torch.Tensor | None = None, train: bool = True):
@@ -307,6 +375,36 @@ class BasicBlock(Layer):
         a = self.c1.forward(x, train=train, xp=xp)
         self.c1.ws.join()
         return self.c2.forward(a, residual=r, train=train, xp=self.c1.out_p())
+
+    def forward_fused(self, src: Pending, train: bool = True) -> Pending:
+        """Forward with every BatchNorm apply deferred into its consumer's
+        operand fill: ``src`` is this block's (not yet materialised) input; the
+        returned Pending is its output relu(BN2(z2) + shortcut)."""
+        c1, c2, sc = self.c1, self.c2, self.sc
+        if sc is None:
+            # identity block: conv1's fill materialises x (the residual)
+            a = c1.forward_fused(src, train) if c1.hconv_ok() else self._plain(c1, src, train)
+            out = c2.forward_fused(a, train) if c2.hconv_ok() else self._plain(c2, a, train)
+            out.res = src.y
+            return out
+        # downsampling block: the paired stride-2 conv1 + 1x1 shortcut read x
+        # packed, so x is materialised by a BatchNorm apply first
+        x = src.materialize(train)
+        c1.x = sc.x = x
+        c1.xp = sc.xp = src.yp
+        K.conv_forward_pair(x, c1.w16, c1.z, c1._split(), c1.ws.acc(c1.acc_f) if train else None,
+                            sc.w16, sc.z, sc._split(), sc.ws.acc(sc.acc_f) if train else None, c1.shp,
+                            wp1=c1.wp, wp2=sc.wp, xp=src.yp)
+        a = Pending.of(c1)
+        out = c2.forward_fused(a, train) if c2.hconv_ok() else self._plain(c2, a, train)
+        # the shortcut's BatchNorm rides in the consumer of z2 (residual BN_r(z_sc))
+        return Pending(c2, res_layer=sc)
+
+    @staticmethod
+    def _plain(layer: ConvBN, src: Pending, train: bool) -> Pending:
+        x = src.materialize(train)
+        layer.forward(x, train=train, xp=src.yp, bn=False)
+        return Pending.of(layer)
 
     def backward(self, dout, dx, presummed: bool = False, prev: K.BnBwdTarget | None = None):
         """``presummed``: conv2's BN reductions were fused into dout's producer;

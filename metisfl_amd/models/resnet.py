@@ -29,7 +29,7 @@ import os
 
 import torch
 
-from metisfl_amd.models.layers import BasicBlock, ClassifierHead, ConvBN
+from metisfl_amd.models.layers import BasicBlock, ClassifierHead, ConvBN, Pending
 from metisfl_amd.models.net import StaticNet
 from metisfl_amd.ops.optim import split_pack
 
@@ -90,6 +90,11 @@ class ResNet18(StaticNet):
     def packed_input(self):
         return self._xbp if self.stem.out_p() is not None else None
 
+    def fused_fill(self) -> bool:
+        """Every BatchNorm apply rides in its consumer's operand fill where the
+        consumer is a halo conv (models/layers.py forward_fused)."""
+        return any(c.hconv_ok() for b in self.blocks for c in b.sublayers())
+
     def forward(self, x, train):
         xp = None
         if self.stem.out_p() is not None:
@@ -102,6 +107,12 @@ class ResNet18(StaticNet):
             if x is not getattr(self, "xb", None):
                 split_pack(x.reshape(-1), self._xbp.view(-1))
             xp = self._xbp
+        if self.fused_fill():
+            self.stem.forward(x, train=train, xp=xp, bn=False)
+            p = Pending.of(self.stem)
+            for b in self.blocks:
+                p = b.forward_fused(p, train)
+            return p.materialize(train)
         h = self.stem.forward(x, train=train, xp=xp)
         hp = self.stem.out_p()
         for b in self.blocks:

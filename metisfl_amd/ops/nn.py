@@ -271,6 +271,66 @@ def transpose_krsc(w, wt, Co: int, RS: int, Ci: int) -> None:
 
 
 # ---------------------------------------------------------------------------
+# Halo-tiled convolution with the producer's BatchNorm fused into the operand
+# fill (hconv.hip; fp32 activations, bf16x3 products)
+@dataclass
+class BnParams:
+    """One BatchNorm's parameters and statistics buffers: ``acc`` holds the
+    fp64 sums of its input [reps][2][C] (train); ``mean`` / ``invstd`` are
+    published and the running averages updated by the launch that applies it."""
+    acc: torch.Tensor | None
+    gamma: torch.Tensor
+    beta: torch.Tensor
+    mean: torch.Tensor
+    invstd: torch.Tensor
+    run_mean: torch.Tensor
+    run_var: torch.Tensor
+    momentum: float = 0.1
+    eps: float = 1e-5
+
+
+def hconv_workspace(shp: ConvShape, device: torch.device) -> int:
+    """Split-K workspace floats of the halo conv for ``shp``, or -1 when the
+    geometry is not covered (3x3 / stride 1 CIFAR-ResNet stages)."""
+    if shp.R != 3 or shp.stride != 1 or shp.pad != 1 or shp.C != shp.Co:
+        return -1
+    if device.type == "cuda":
+        return int(ops().hconv_fwd_workspace(shp.N, shp.H, shp.W, shp.C, shp.Co))
+    ok = (shp.H == shp.W and (shp.H, shp.C) in ((32, 64), (16, 128), (8, 256), (4, 512))
+          and shp.N % {32: 1, 16: 1, 8: 2, 4: 8}[shp.H] == 0)
+    return 0 if ok else -1
+
+
+def hconv_forward(z, wp, w, out, shp: ConvShape, bn: BnParams, train: bool, relu: bool, ws=None, stats=None,
+                  res=None, zr=None, bnr: BnParams | None = None, y=None, yp=None) -> None:
+    """out = conv3x3(T(z), w) with T(z) = relu?(BN(z) [+ res | + BN_r(zr)]) applied
+    as the operand enters LDS (one launch: no separate BatchNorm apply).
+    ``y`` / ``yp`` receive T(z) and its packed bf16x3 split (the activation
+    the backward pass and later residual adds read); ``stats`` accumulates the
+    output's BN sums (train).  Publishes ``bn`` (and ``bnr``) in train mode.
+    ``wp``: the packed weight mirror (GPU), ``w``: the fp32 weights (CPU)."""
+    C = shp.C
+    if z.is_cuda:
+        b2 = bnr if bnr is not None else None
+        ops().hconv_forward(z, wp, out, ws, stats, shp.N, shp.H, shp.W, C, shp.Co, train, relu,
+                            bn.acc if train else None, bn.gamma, bn.beta, bn.mean, bn.invstd, bn.run_mean,
+                            bn.run_var, bn.momentum, bn.eps, res, zr,
+                            (b2.acc if train else None) if b2 else None, b2.gamma if b2 else None,
+                            b2.beta if b2 else None, b2.mean if b2 else None, b2.invstd if b2 else None,
+                            b2.run_mean if b2 else None, b2.run_var if b2 else None, y, yp)
+        return
+    # reference: the BatchNorm apply(s) the fill replaces, then the conv
+    r = res
+    if zr is not None:
+        r = torch.empty_like(zr)
+        bn_apply(zr, C, bnr.acc, bnr.gamma, bnr.beta, bnr.mean, bnr.invstd, bnr.run_mean, bnr.run_var, r,
+                 relu=False, train=train, momentum=bnr.momentum, eps=bnr.eps)
+    v = y if y is not None else torch.empty_like(z)
+    bn_apply(z, C, bn.acc, bn.gamma, bn.beta, bn.mean, bn.invstd, bn.run_mean, bn.run_var, v, residual=r,
+             relu=relu, train=train, momentum=bn.momentum, eps=bn.eps)
+    conv_forward(v, w, out, shp, stats=stats)
+
+
 def bn_stats(x, C: int, acc) -> None:
     """acc[0:C] += sum x, acc[C:2C] += sum x^2 (fp64) over the rows of NHWC x."""
     if x.is_cuda:
