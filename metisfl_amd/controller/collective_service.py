@@ -27,21 +27,38 @@ from metisfl_amd.utils.metis_logger import MetisLogger
 from metisfl_amd.utils.proto_messages_factory import MetisProtoMessages as M
 
 SERVICE = "metisfl_amd.CollectiveService"
-METHODS = ("RegisterLearners", "ScalingFactors", "RecordRound")
+METHODS = ("RegisterLearners", "ScalingFactors", "RecordRound", "RecordAsyncUpdate", "RecordEvaluation",
+           "RequestStop", "ShouldStop")
 
 
 def add_collective_service(servicer, server: grpc.Server) -> None:
     eng = servicer.engine
 
+    registered: list[str] = []  # the current collective membership
+
     def register(req: bytes, ctx) -> bytes:
+        """(Re-)register the collective ranks.  A relaunch after a lost rank
+        (driver_session.py) registers the surviving membership: learners of
+        the previous membership that are not in it leave the federation (the
+        reference's LeaveFederation, controller.cc:171-199), the survivors
+        re-join with fresh tokens."""
         d = json.loads(req)
+        want = {f"{l.get('hostname', 'localhost')}:{int(l.get('port', 0))}" for l in d["learners"]}
+        current = set(eng.learner_ids())
+        for lid in list(registered):
+            if lid in current:  # leaving, or re-joining with fresh specs / token
+                eng.evict_learner(lid)
+                if lid not in want:
+                    MetisLogger.info("Collective learner %s left the federation.", lid)
+        registered.clear()
         ids, toks = [], []
         for l in d["learners"]:
             se = M.construct_server_entity_pb(l.get("hostname", "localhost"), int(l.get("port", 0)))
             ds = M.construct_dataset_spec_pb(int(l["num_training_examples"]), 0, int(l.get("num_test_examples", 0)))
-            lid, tok, _ = eng.add_learner(se.SerializeToString(), ds.SerializeToString())
+            lid, tok, _ = eng.add_learner(se.SerializeToString(), ds.SerializeToString(), False)
             ids.append(lid)
             toks.append(tok)
+            registered.append(lid)
         MetisLogger.info("Collective federation registered %d learners.", len(ids))
         servicer.checkpoint(force=True)
         return json.dumps({"ids": ids, "tokens": toks}).encode()
@@ -51,16 +68,48 @@ def add_collective_service(servicer, server: grpc.Server) -> None:
         f = eng.scaling_factors(d["ids"], [float(x) for x in d["num_train"]], [float(x) for x in d["batches"]])
         return json.dumps({"factors": [float(f[i]) for i in d["ids"]]}).encode()
 
+    state = {"stop": False}
+
     def record(req: bytes, ctx) -> bytes:
         d = json.loads(req)
         metas = [base64.b64decode(m) for m in d["metas"]]
         eng.record_collective_round(int(d["global_iteration"]), d["ids"], int(d["started_ns"]),
                                     int(d["completed_ns"]), int(d["agg_started_ns"]), int(d["agg_completed_ns"]),
                                     metas, d.get("zeros", []), d.get("sizes", []), d.get("lengths", []))
+        if d.get("eval_ids"):  # the learners' evaluations of the new community model
+            eng.record_community_evaluation(int(d["global_iteration"]), d["eval_ids"],
+                                            [base64.b64decode(e) for e in d["evaluations"]])
         servicer.checkpoint()
+        return json.dumps({"stop": state["stop"]}).encode()
+
+    def record_async(req: bytes, ctx) -> bytes:
+        """One FedRec update of an asynchronous collective federation: the
+        finisher's task metadata (local task lineage) and the update's
+        FederatedTaskRuntimeMetadata (one community version)."""
+        d = json.loads(req)
+        eng.record_collective_round(int(d["global_iteration"]), [d["id"]], int(d["started_ns"]),
+                                    int(d["completed_ns"]), int(d["agg_started_ns"]), int(d["agg_completed_ns"]),
+                                    [base64.b64decode(d["meta"])], [], [], [])
+        servicer.checkpoint()
+        return json.dumps({"stop": state["stop"]}).encode()
+
+    def record_eval(req: bytes, ctx) -> bytes:
+        d = json.loads(req)
+        eng.record_community_evaluation(int(d["global_iteration"]), d["ids"],
+                                        [base64.b64decode(e) for e in d["evaluations"]])
+        return json.dumps({"stop": state["stop"]}).encode()
+
+    def request_stop(req: bytes, ctx) -> bytes:
+        state["stop"] = True
+        MetisLogger.info("Collective federation: stop requested.")
         return b"{}"
 
-    fns = {"RegisterLearners": register, "ScalingFactors": scaling, "RecordRound": record}
+    def should_stop(req: bytes, ctx) -> bytes:
+        return json.dumps({"stop": state["stop"]}).encode()
+
+    fns = {"RegisterLearners": register, "ScalingFactors": scaling, "RecordRound": record,
+           "RecordAsyncUpdate": record_async, "RecordEvaluation": record_eval, "RequestStop": request_stop,
+           "ShouldStop": should_stop}
     handlers = {name: grpc.unary_unary_rpc_method_handler(fn) for name, fn in fns.items()}
     server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(SERVICE, handlers),))
 

@@ -141,11 +141,14 @@ PYBIND11_MODULE(_engine, m) {
         return new Controller(p);
       }))
       .def("add_learner",
-           [](Controller& c, py::bytes se, py::bytes ds) {
+           [](Controller& c, py::bytes se, py::bytes ds, bool schedule) {
+             // schedule=false: a collective (RCCL data plane) rank -- no
+             // RunTask is scheduled and no round is opened for it
              Dispatch d;
-             auto r = c.add_learner(std::string(se), std::string(ds), &d);
+             auto r = c.add_learner(std::string(se), std::string(ds), schedule ? &d : nullptr);
              return py::make_tuple(r.first, r.second, dispatch_to_py(d));
-           })
+           },
+           py::arg("server_entity"), py::arg("dataset_spec"), py::arg("schedule") = true)
       .def("remove_learner", &Controller::remove_learner, py::call_guard<py::gil_scoped_release>())
       .def("evict_learner",
            [](Controller& c, const std::string& id) {
@@ -205,6 +208,12 @@ PYBIND11_MODULE(_engine, m) {
              std::vector<std::string> mm;
              for (auto& b : meta) mm.emplace_back(b);
              c.record_collective_round(gi, ids, s, e, as, ae, mm, zeros, sizes, lengths);
+           })
+      .def("record_community_evaluation",
+           [](Controller& c, uint32_t gi, const std::vector<std::string>& ids, const std::vector<py::bytes>& evs) {
+             std::vector<std::string> ee;
+             for (auto& b : evs) ee.emplace_back(b);
+             c.record_community_evaluation(gi, ids, ee);
            })
       .def("community_model", [](const Controller& c) { return B(c.community_model()); })
       .def("participating_learners", [](const Controller& c) { return B(c.participating_learners()); })

@@ -57,7 +57,8 @@ void hconv_forward(torch::Tensor z, torch::Tensor wp, torch::Tensor out, OptT ws
                    int64_t W, int64_t C, int64_t Co, bool train, bool relu, OptT acc, torch::Tensor gamma,
                    torch::Tensor beta, torch::Tensor mean, torch::Tensor invstd, torch::Tensor run_mean,
                    torch::Tensor run_var, double momentum, double eps, OptT res, OptT zr, OptT acc2, OptT gamma2,
-                   OptT beta2, OptT mean2, OptT invstd2, OptT run_mean2, OptT run_var2, OptT y, OptT yp) {
+                   OptT beta2, OptT mean2, OptT invstd2, OptT run_mean2, OptT run_var2, OptT y, OptT yp,
+                   OptT stamps) {
   const int64_t ws_need = mfl::hc::hconv_fwd_workspace((int)N, (int)H, (int)W, (int)C, (int)Co);
   TORCH_CHECK(ws_need >= 0, "halo conv: unsupported geometry N=", N, " H=", H, " W=", W, " C=", C, " Co=", Co);
   const int64_t nin = N * H * W * C, nout = N * H * W * Co;
@@ -111,6 +112,12 @@ void hconv_forward(torch::Tensor z, torch::Tensor wp, torch::Tensor out, OptT ws
     a.counters = reinterpret_cast<int*>(ws->data_ptr<float>());
     a.slab = ws->data_ptr<float>() + 1024;
   }
+  if (has(stamps)) {  // profiling: [grid][16] int64 phase stamps
+    check(*stamps, torch::kInt64, -1, "stamps");
+    TORCH_CHECK(stamps->numel() >= 16 * 2048, "stamps: at least 16 x 2048 slots");
+    a.stamps = reinterpret_cast<long long*>(stamps->data_ptr<int64_t>());
+  }
+  if (const char* e = getenv("MFL_HC_DBG")) a.dbg = atoi(e);  // timing ablations only
   mfl::hc::launch_hconv_fwd(a, cur_stream(out));
 }
 

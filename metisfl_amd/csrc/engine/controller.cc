@@ -124,7 +124,7 @@ std::string RoundMeta::serialize() const {
 
 // ---------------------------------------------------------------------------
 Controller::Controller(const std::string& params_bytes)
-    : cfg_(ControllerConfig::from_params(params_bytes)), rng_(std::random_device{}()) {
+    : cfg_(ControllerConfig::from_params(params_bytes)) {
   if (cfg_.batch_size == 0) throw StatusError(INVALID_ARGUMENT, "batch size cannot be zero");
   if (cfg_.epochs == 0) throw StatusError(INVALID_ARGUMENT, "epochs cannot be zero");
   if (cfg_.protocol == PROTO_ASYNC)
@@ -146,10 +146,16 @@ Controller::Controller(const std::string& params_bytes)
     store_.reset(new HashMapModelStore(cfg_.lineage));
 }
 
+// 128 bits from the ChaCha20 stream (keyed with 256 bits of getrandom): an
+// observer of other tokens learns nothing about the next one (a 32-bit seeded
+// mt19937 could be brute-forced from one token)
 std::string Controller::random_token() {
   static const char* hex = "0123456789abcdef";
-  std::string t(64, '0');
-  for (auto& ch : t) ch = hex[rng_() & 15];
+  std::string t(32, '0');
+  for (int w = 0; w < 2; ++w) {
+    uint64_t v = rng_.next_u64();
+    for (int i = 0; i < 16; ++i, v >>= 4) t[16 * w + i] = hex[v & 15];
+  }
   return t;
 }
 
@@ -549,6 +555,22 @@ void Controller::record_collective_round(uint32_t global_iteration, const std::v
   }
   metadata_.push_back(m);
   global_iteration_ = std::max(global_iteration_, global_iteration);
+}
+
+void Controller::record_community_evaluation(uint32_t global_iteration, const std::vector<std::string>& ids,
+                                             const std::vector<std::string>& model_evaluations) {
+  std::lock_guard<std::mutex> g(mu_);
+  CommEval ce;
+  ce.global_iteration = global_iteration;
+  for (size_t i = 0; i < ids.size() && i < model_evaluations.size(); ++i) ce.evals[ids[i]] = model_evaluations[i];
+  const int64_t t = now_ns();
+  for (auto& m : metadata_)
+    if (m.global_iteration == global_iteration)
+      for (auto& id : ids) {
+        m.eval_submitted[id] = t;
+        m.eval_received[id] = t;
+      }
+  evaluations_.push_back(std::move(ce));
 }
 
 // ---------------------------------------------------------------------------

@@ -9,7 +9,8 @@
 //    network; the on-node collective engine needs no model transfer at all.
 //  * Single mutex, no detached threads: the reference's data races on
 //    `metadata_` / `community_evaluations_` cannot occur.
-//  * Auth tokens are random 64-hex strings (the reference uses "#learners+1",
+//  * Auth tokens are 128-bit random 32-hex strings from a ChaCha20 CSPRNG keyed
+//    by getrandom (the reference uses "#learners+1",
 //    controller.cc:130; its own proto comment asks for a random token).
 //  * GetCommunityModelLineage / GetLearnerLocalModelLineage are implemented
 //    (declared but missing in the reference servicer, controller.proto:15,19).
@@ -20,6 +21,8 @@
 #include <memory>
 #include <mutex>
 #include <random>
+
+#include "he/ckks.h"
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -147,6 +150,11 @@ class Controller {
   std::string community_model() const;  // FederatedModel
   std::string participating_learners() const;               // GetParticipatingLearnersResponse
   std::string runtime_metadata_lineage(int n) const;        // GetRuntimeMetadataLineageResponse
+  // Collective (RCCL) data plane: the learners evaluated the community model
+  // of `global_iteration` in place; model_evaluations[i] is learner ids[i]'s
+  // serialized ModelEvaluations (controller.cc:469-485 in the reference).
+  void record_community_evaluation(uint32_t global_iteration, const std::vector<std::string>& ids,
+                                   const std::vector<std::string>& model_evaluations);
   std::string community_evaluation_lineage(int n) const;    // GetCommunityModelEvaluationLineageResponse
   std::string local_task_lineage(int n, const std::vector<std::string>& ids) const;
   std::string community_model_lineage(int n) const;         // GetCommunityModelLineageResponse
@@ -196,7 +204,7 @@ class Controller {
   std::vector<CommEval> evaluations_;
   uint32_t global_iteration_ = 0;
   uint32_t evicted_ = 0;
-  std::mt19937_64 rng_;
+  ChaCha20Rng rng_;  // auth tokens: ChaCha20 keyed from getrandom (he/ckks.h)
 };
 
 int64_t now_ns();

@@ -54,6 +54,8 @@ struct FwdArgs {
   int reps;
   float* slab;         // split-K slabs
   int* counters;       // split-K arrival tickets (zero between launches)
+  long long* stamps = nullptr;  // profiling: per-workgroup phase timestamps [grid][16] (core clock)
+  int dbg = 0;                  // ablation (timing only): 1 skip MFMAs, 2 skip fragment reads, 4 skip fills
 };
 
 // Geometry supported by the halo kernels (3x3, stride 1, pad 1, square

@@ -78,12 +78,14 @@ struct Cfg {
   static constexpr int WM = MT / WGM, WN = NT / WGN;
   static constexpr int TM = WM / 32, TN = WN / 32;  // 32x32 MFMA tiles per wave
   static constexpr int CC = 16;                     // channels per k chunk
+  static constexpr int KCH = 64;                    // input channels per workgroup (split-K slice)
+  static constexpr int NCH = KCH / CC;              // chunks: every one's input loads issued up front
   static constexpr int PH = TH + 2, PW = TW + 2, PIX = IMGS * PH * PW;
   static constexpr int PS = PS_, ROWB = ROWB_, IMGB = IMGB_;
   static constexpr int A_BYTES = ((IMGS - 1) * IMGB + (PH - 1) * ROWB + PW * PS + 15) / 16 * 16;
   static constexpr int BPS = 80;
   static constexpr int B_BYTES = 9 * NT * BPS;
-  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int STAGE = A_BYTES + B_BYTES + 64;  // + a dummy slot for padding items
   static constexpr int NA = (PIX * 4 + 255) / 256;  // A float4 items per thread per chunk
   static constexpr int NB = (NT * 36 + 255) / 256;  // B uint4 items per thread per chunk
   static constexpr int TST = NT + 4;                // epilogue tile row (floats)
@@ -143,6 +145,15 @@ __device__ __forceinline__ float4 as_f4(const u32x4& v) {
   return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
 
+// In-kernel phase stamps (profiling only, a.stamps != nullptr): lane 0 of
+// wave 0 records the core clock at phase boundaries with a vector store.
+__device__ __forceinline__ void stamp(const FwdArgs& a, int k) {
+  if (a.stamps && threadIdx.x == 0) {
+    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    a.stamps[(int64_t)b * 16 + k] = (long long)__builtin_readcyclecounter();
+  }
+}
+
 // RK: residual kind of the input transform (0 none, 1 fp32 tensor, 2 BN of a
 // projection shortcut's pre-BN output).  Grid: x = spatial tiles, y = output
 // channel tiles, z = input-channel slices (split-K; kchunk channels each).
@@ -163,26 +174,9 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
   const int y0 = ty * K::TH, x0 = tx * K::TW;
   const int n0 = blockIdx.y * K::NT;
   const int kbeg = blockIdx.z * kchunk;
-  const int nch = kchunk / K::CC;  // even (host check)
   float* coef = reinterpret_cast<float*>(smem + K::LDS_MAIN);  // [4][kchunk]: sc, sh, sc2, sh2
   const FwdXform& X = a.x;
-
-  // ---- coefficients of this slice's input channels ----
-  {
-    const bool publish = X.train && blockIdx.x == 0 && blockIdx.y == 0;
-    for (int c = t; c < kchunk; c += 256) {
-      float sc = 1.f, sh = 0.f;
-      if (X.has_bn) bn_coef(X.bn, C, kbeg + c, X.M, X.train, publish, sc, sh);
-      coef[c] = sc;
-      coef[kchunk + c] = sh;
-      if constexpr (RK == 2) {
-        float s2, h2;
-        bn_coef(X.bnr, C, kbeg + c, X.M, X.train, publish, s2, h2);
-        coef[2 * kchunk + c] = s2;
-        coef[3 * kchunk + c] = h2;
-      }
-    }
-  }
+  stamp(a, 0);
 
   // ---- per-thread fill geometry (fixed over the chunks) ----
   const int q = t & 3;  // float4 within the 16-channel chunk (256 % 4 == 0)
@@ -201,7 +195,7 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
     const bool item = i < K::PIX * 4;
     const bool in = item && (img0 + img < a.N) && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
     a_off[u] = in ? (uint32_t)(((((img0 + img) * a.H + iy) * a.W + ix) * C + 4 * q) * 4) : kOOB;
-    a_lds[u] = item ? img * K::IMGB + py * K::ROWB + px * K::PS + 8 * q : -1;
+    a_lds[u] = item ? img * K::IMGB + py * K::ROWB + px * K::PS + 8 * q : K::A_BYTES + K::B_BYTES + 8 * q;
     a_own[u] = own_tile && in && py >= 1 && py <= K::TH && px >= 1 && px <= K::TW;
   }
   uint32_t b_off[K::NB];
@@ -213,29 +207,40 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
     const int tap = r >> 2, bq = r & 3;
     const bool item = i < K::NT * 36;
     b_off[u] = item ? (uint32_t)((((n0 + co) * 9 + tap) * C + 4 * bq) * 4) : kOOB;
-    b_lds[u] = item ? K::A_BYTES + tap * (K::NT * K::BPS) + co * K::BPS + 8 * bq : -1;
+    b_lds[u] = item ? K::A_BYTES + tap * (K::NT * K::BPS) + co * K::BPS + 8 * bq : K::A_BYTES + K::B_BYTES + 8 * bq;
   }
   const uint32_t in_bytes = (uint32_t)((int64_t)a.N * a.H * a.W * C * 4);
   const auto rsZ = make_rsrc(X.z, in_bytes);
   const auto rsR = make_rsrc(RK == 1 ? X.res : X.zr, in_bytes);
   const auto rsW = make_rsrc(a.wp, (uint32_t)((int64_t)a.Co * 9 * C * 4));
 
-  u32x4 az[K::NA], ar[K::NA], bw[K::NB];
-  auto load = [&](int k) {
+  // The input patch of EVERY chunk is requested at kernel start (its latency
+  // -- the producer's output comes from the Infinity Cache / HBM, ~2 us -- is
+  // paid once, under the BatchNorm coefficient prologue); the weights (L2-
+  // resident) stream one chunk ahead through a single register set.
+  u32x4 az[K::NCH][K::NA], ar[K::NCH][K::NA], bw[K::NB];
+  auto load_a = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    if (a.dbg & 4) return;
     const uint32_t cb = (uint32_t)((kbeg + k * K::CC) * 4);
 #pragma unroll
     for (int u = 0; u < K::NA; ++u) {
       const uint32_t off = a_off[u] == kOOB ? kOOB : a_off[u] + cb;
-      az[u] = __builtin_amdgcn_raw_buffer_load_b128(rsZ, (int)off, 0, 0);
-      if constexpr (RK != 0) ar[u] = __builtin_amdgcn_raw_buffer_load_b128(rsR, (int)off, 0, 0);
+      az[k][u] = __builtin_amdgcn_raw_buffer_load_b128(rsZ, (int)off, 0, 0);
+      if constexpr (RK != 0) ar[k][u] = __builtin_amdgcn_raw_buffer_load_b128(rsR, (int)off, 0, 0);
     }
+  };
+  auto load_b = [&](int k) {
+    if (a.dbg & 4) return;
+    const uint32_t cb = (uint32_t)((kbeg + k * K::CC) * 4);
 #pragma unroll
     for (int u = 0; u < K::NB; ++u) {
       const uint32_t off = b_off[u] == kOOB ? kOOB : b_off[u] + cb;
       bw[u] = __builtin_amdgcn_raw_buffer_load_b128(rsW, (int)off, 0, 0);
     }
   };
-  auto store = [&](int k, uint8_t* stage) {
+  auto store = [&](auto kc, uint8_t* stage) {
+    constexpr int k = decltype(kc)::value;
     const int cl = k * K::CC + 4 * q;  // channel within the slice
     const float4 sc = *reinterpret_cast<const float4*>(coef + cl);
     const float4 sh = *reinterpret_cast<const float4*>(coef + kchunk + cl);
@@ -247,24 +252,23 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
     const int gch = (kbeg + k * K::CC) * 4;  // byte offset of the chunk
 #pragma unroll
     for (int u = 0; u < K::NA; ++u) {
-      if (a_lds[u] < 0) continue;
-      const float4 zv = as_f4(az[u]);
+      const float4 zv = as_f4(az[k][u]);
       float4 v = make_float4(fmaf(zv.x, sc.x, sh.x), fmaf(zv.y, sc.y, sh.y), fmaf(zv.z, sc.z, sh.z),
                              fmaf(zv.w, sc.w, sh.w));
       if constexpr (RK == 1) {
-        const float4 r = as_f4(ar[u]);
+        const float4 r = as_f4(ar[k][u]);
         v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
       } else if constexpr (RK == 2) {
-        const float4 r = as_f4(ar[u]);
+        const float4 r = as_f4(ar[k][u]);
         v.x += fmaf(r.x, s2.x, h2.x);
         v.y += fmaf(r.y, s2.y, h2.y);
         v.z += fmaf(r.z, s2.z, h2.z);
         v.w += fmaf(r.w, s2.w, h2.w);
       }
-      if (X.relu) {
-        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-      }
-      if (a_off[u] == kOOB) v = make_float4(0.f, 0.f, 0.f, 0.f);  // padding is post-activation zero
+      const float lo = X.relu ? 0.f : -__builtin_inff();
+      v.x = fmaxf(v.x, lo); v.y = fmaxf(v.y, lo); v.z = fmaxf(v.z, lo); v.w = fmaxf(v.w, lo);
+      const bool oob = a_off[u] == kOOB;  // padding is post-activation zero
+      v.x = oob ? 0.f : v.x; v.y = oob ? 0.f : v.y; v.z = oob ? 0.f : v.z; v.w = oob ? 0.f : v.w;
       uint32_t h01, l01, h23, l23;
       split2(v.x, v.y, h01, l01);
       split2(v.z, v.w, h23, l23);
@@ -282,7 +286,6 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
     }
 #pragma unroll
     for (int u = 0; u < K::NB; ++u) {
-      if (b_lds[u] < 0) continue;
       const u32x4 d = bw[u];
       const uint32_t h01 = __builtin_amdgcn_perm(d[1], d[0], 0x07060302u);
       const uint32_t h23 = __builtin_amdgcn_perm(d[3], d[2], 0x07060302u);
@@ -293,6 +296,25 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
       *reinterpret_cast<uint2*>(p + 32) = make_uint2(l01, l23);
     }
   };
+
+  static_for<K::NCH>([&](auto kc) { load_a(kc); });
+  load_b(0);
+  // ---- coefficients of this slice's input channels ----
+  {
+    const bool publish = X.train && blockIdx.x == 0 && blockIdx.y == 0;
+    for (int c = t; c < kchunk; c += 256) {
+      float sc = 1.f, sh = 0.f;
+      if (X.has_bn) bn_coef(X.bn, C, kbeg + c, X.M, X.train, publish, sc, sh);
+      coef[c] = sc;
+      coef[kchunk + c] = sh;
+      if constexpr (RK == 2) {
+        float s2, h2;
+        bn_coef(X.bnr, C, kbeg + c, X.M, X.train, publish, s2, h2);
+        coef[2 * kchunk + c] = s2;
+        coef[3 * kchunk + c] = h2;
+      }
+    }
+  }
 
   // ---- fragment addresses (tap (0,0), hi half; lo at +32) ----
   int fa_off[K::TM], fb_off[K::TN];
@@ -315,10 +337,13 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
+  // 9 taps, fragments read two taps ahead (three register sets): the MFMAs
+  // of tap t wait only for the reads issued before tap t-1's; sched_barrier
+  // keeps hipcc from sinking the reads back behind the MFMAs
   auto compute = [&](const uint8_t* st) {
-    bf16x8 ah[2][K::TM], al[2][K::TM], bh[2][K::TN], bl[2][K::TN];
-    auto rd = [&](auto tapc, auto sc) {
-      constexpr int TAP = decltype(tapc)::value, S = decltype(sc)::value;
+    bf16x8 ah[3][K::TM], al[3][K::TM], bh[3][K::TN], bl[3][K::TN];
+    auto rd = [&](auto tapc) {
+      constexpr int TAP = decltype(tapc)::value, S = TAP % 3;
       constexpr int AO = (TAP / 3) * K::ROWB + (TAP % 3) * K::PS;
       constexpr int BO = TAP * K::NT * K::BPS;
 #pragma unroll
@@ -332,37 +357,55 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
         bl[S][j] = *reinterpret_cast<const bf16x8*>(st + fb_off[j] + BO + 32);
       }
     };
-    rd(IC<0>{}, IC<0>{});
+    rd(IC<0>{});
+    rd(IC<1>{});
     static_for<9>([&](auto tapc) {
-      constexpr int TAP = decltype(tapc)::value, S = TAP & 1;
-      if constexpr (TAP < 8) rd(IC<TAP + 1>{}, IC<1 - S>{});
+      constexpr int TAP = decltype(tapc)::value, S = TAP % 3;
+      if constexpr (TAP + 2 < 9) {
+        if (!(a.dbg & 2)) rd(IC<TAP + 2>{});
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(a.dbg & 1)) {
 #pragma unroll
-      for (int i = 0; i < K::TM; ++i)
+        for (int i = 0; i < K::TM; ++i)
 #pragma unroll
-        for (int j = 0; j < K::TN; ++j) {
-          acc[i][j] = mfma_bf16x16(al[S][i], bh[S][j], acc[i][j]);
-          acc[i][j] = mfma_bf16x16(ah[S][i], bl[S][j], acc[i][j]);
-          acc[i][j] = mfma_bf16x16(ah[S][i], bh[S][j], acc[i][j]);
-        }
+          for (int j = 0; j < K::TN; ++j) {
+            acc[i][j] = mfma_bf16x16(al[S][i], bh[S][j], acc[i][j]);
+            acc[i][j] = mfma_bf16x16(ah[S][i], bl[S][j], acc[i][j]);
+            acc[i][j] = mfma_bf16x16(ah[S][i], bh[S][j], acc[i][j]);
+          }
+      }
+      __builtin_amdgcn_sched_barrier(0);
     });
+  };
+  // LDS-only barrier: the owner-write global stores and the next chunk's
+  // loads stay in flight (__syncthreads would drain vmcnt)
+  auto bar = [&]() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes / reads done
+    lds_barrier();
   };
 
   __syncthreads();  // coefficients visible
-  load(0);
-  store(0, smem);
+  stamp(a, 1);
+  store(IC<0>{}, smem);
+  load_b(1);
+  bar();
+  stamp(a, 2);
+  static_for<K::NCH>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    uint8_t* cur = smem + (k & 1) * K::STAGE;
+    uint8_t* nxt = smem + ((k + 1) & 1) * K::STAGE;
+    compute(cur);
+    if constexpr (k == 0) stamp(a, 3);
+    if constexpr (k + 1 < K::NCH) {
+      store(IC<k + 1>{}, nxt);
+      if constexpr (k + 2 < K::NCH) load_b(k + 2);
+    }
+    bar();
+    if constexpr (k == 0) stamp(a, 4);
+  });
   __syncthreads();
-  for (int k = 0; k < nch; k += 2) {
-    // chunk k from stage 0 (chunk k+1 loading), chunk k+1 from stage 1
-    load(k + 1);
-    compute(smem);
-    store(k + 1, smem + K::STAGE);
-    __syncthreads();
-    const bool more = k + 2 < nch;
-    if (more) load(k + 2);
-    compute(smem + K::STAGE);
-    if (more) store(k + 2, smem);
-    __syncthreads();
-  }
+  stamp(a, 5);
 
   // ---- epilogue: tile through LDS, split-K reduce, output + BN sums ----
   float* tile = reinterpret_cast<float*>(smem);
@@ -432,6 +475,7 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
     }
     __syncthreads();
   }
+  stamp(a, 6);
   // output rows: float4 per thread per pass
   constexpr int RPP = 256 / C4;
   const int cg = t % C4, r0 = t / C4;
@@ -447,6 +491,7 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     sq.x += v.x * v.x; sq.y += v.y * v.y; sq.z += v.z * v.z; sq.w += v.w * v.w;
   }
+  stamp(a, 7);
   if (!a.stats) return;
   double* stats = a.stats + (int64_t)((blockIdx.x + blockIdx.y * gridDim.x) % a.reps) * 2 * a.Co;
   reinterpret_cast<float4*>(red)[2 * t] = s;
@@ -462,11 +507,12 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
     atomicAdd(&stats[n0 + t], sa);
     atomicAdd(&stats[a.Co + n0 + t], sb);
   }
+  stamp(a, 8);
 }
 
 // Stage configurations for the CIFAR ResNet-18 shapes at any batch (3x3, s1):
 // S1 32x32x64: 8x16-pixel tiles x 64 channels, waves 2x2 (64x32 each)
-// S2 16x16x128: 8x16 x 32 channels, waves 4x1
+// S2 16x16x128: 8x16 x 32 channels, waves 4x1, 2 input-channel slices
 // S3 8x8x256: 2 images x 64 channels, waves 2x2, 4 input-channel slices
 // S4 4x4x512: 8 images x 64 channels, waves 2x2, 8 slices
 // (pitches from scripts/hconv_banks.py: conflict-free A reads for every tap)
@@ -496,10 +542,11 @@ Plan plan_fwd(int N, int H, int W, int C, int Co) {
     p.nt = nt;
   };
   if (H == 32 && C == 64) fill(1, 8, 16, 1, 64, 1);
-  else if (H == 16 && C == 128) fill(2, 8, 16, 1, 32, 1);
+  else if (H == 16 && C == 128) fill(2, 8, 16, 1, 32, 2);
   else if (H == 8 && C == 256) fill(3, 8, 8, 2, 64, 4);
   else if (H == 4 && C == 512) fill(4, 4, 4, 8, 64, 8);
   if (p.stage && p.grid.x * p.grid.y > 1024) p.stage = 0;  // counter block
+  if (p.stage && p.kchunk != 64) p.stage = 0;               // Cfg::KCH
   return p;
 }
 

@@ -129,7 +129,9 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
       if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
     }
     const float lse = mx + hlog<T>(se);
-    if (lane == 0 && stats) {
+    // y < 0: a padding row of the last evaluation batch (DeviceDataset
+    // pad_tail) -- excluded from the statistics
+    if (lane == 0 && stats && y >= 0) {
       atomicAdd(&stats[0], lse - lg[y]);
       atomicAdd(&stats[1], bi == y ? 1.f : 0.f);
       atomicAdd(&stats[2], 1.f);

@@ -238,8 +238,8 @@ __global__ __launch_bounds__(64) void xent_kernel(const uint16_t* __restrict__ l
       dlogits[(int64_t)b * Kp + k] = f2bf(g);
     }
   }
-  if (l == 0) {
-    const float zy = (y >= 0 && y < K) ? bf2f(z[y]) : mx;
+  if (l == 0 && y >= 0) {  // y < 0: evaluation padding row
+    const float zy = y < K ? bf2f(z[y]) : mx;
     atomicAdd(&stats[0], __logf(se) + mx - zy);
     atomicAdd(&stats[1], am == y ? 1.f : 0.f);
     atomicAdd(&stats[2], 1.f);
@@ -260,7 +260,8 @@ __global__ __launch_bounds__(256) void mse_kernel(const uint16_t* __restrict__ p
                                                   int backward) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   float se = 0.f, cnt = 0.f;
-  if (b < B) {
+  // a NaN target (the int32 -1 label of an evaluation padding row) is skipped
+  if (b < B && !__builtin_isnan(target[b])) {
     const float d = bf2f(pred[(int64_t)b * Kp]) - target[b];
     se = d * d;
     cnt = 1.f;

@@ -63,7 +63,7 @@ class DriverSessionBase:
 
     def __init__(self, fed_env, model, train_dataset_recipe_fn, validation_dataset_recipe_fn=None,
                  test_dataset_recipe_fn=None, working_dir: str = "/tmp/metis_amd/", device: str | None = None,
-                 seed: int = 0, fake_train_delay: float = 0.0):
+                 seed: int = 0, fake_train_delay: float = 0.0, collective_options: dict | None = None):
         MetisASCIIArt.print()
         self.federation_environment = fed_env if isinstance(fed_env, fedenv_parser.FederationEnvironment) \
             else fedenv_parser.FederationEnvironment(fed_env)
@@ -75,6 +75,12 @@ class DriverSessionBase:
         os.makedirs(working_dir)
         self.device = device
         self.seed = seed
+        # collective data plane knobs: checkpoint_every (rounds, default 1),
+        # max_recoveries (lost-rank relaunches, default 2), heartbeat_timeout_s,
+        # fault ({"rank", "round"}: fault injection for tests), extra
+        # (FederationConfig.extra: test hooks such as uneven learner delays)
+        self.collective_options = dict(collective_options or {})
+        self.recoveries: list[dict] = []
         self.fake_train_delay = fake_train_delay  # echo learners only
         self._model_dir = os.path.join(working_dir, "model_definition")
         self.neural_engine = self._save_model(model)
@@ -242,48 +248,92 @@ class DriverSessionBase:
     def collective(self) -> bool:
         return self.federation_environment.data_plane == "rccl"
 
-    def _collective_job(self, rounds: int) -> str:
-        """The JSON job description every collective rank reads."""
+    _RULES = {"FEDAVG": "fed_avg", "FEDSTRIDE": "fed_stride", "FEDREC": "fed_rec", "PWA": "fed_avg"}
+
+    def _collective_federation(self) -> dict:
+        """FederationConfig of the collective ranks from the YAML: protocol,
+        aggregation rule, scaling factor, stride, semi-sync knobs, secure
+        aggregation.  Combinations the collective data plane does not run
+        raise instead of silently falling back to synchronous FedAvg."""
         env = self.federation_environment
         lm, cp = env.local_model_config, env.communication_protocol
         rule = env.global_model_config.aggregation_rule
+        rname = (rule.aggregation_rule_name or "FedAvg").upper()
+        if rname not in self._RULES:
+            raise RuntimeError(f"aggregation rule {rule.aggregation_rule_name!r} is not supported on DataPlane: rccl")
+        if cp.is_asynchronous:
+            protocol = "asynchronous"
+            if self._he_scheme is not None:
+                raise RuntimeError("DataPlane: rccl runs CKKS secure aggregation (PWA) on synchronous / "
+                                   "semi-synchronous rounds only; use DataPlane: grpc for asynchronous PWA")
+        elif cp.is_semi_synchronous:
+            protocol = "semi_synchronous"
+        elif cp.is_synchronous:
+            protocol = "synchronous"
+        else:
+            raise RuntimeError(f"unknown communication protocol {cp.name!r}")
+        return {"protocol": protocol, "aggregation": self._RULES[rname],
+                "stride_length": int(rule.aggregation_rule_stride_length or 0),
+                "scaling_factor": {"NumTrainingExamples": "NUM_TRAINING_EXAMPLES",
+                                   "NumCompletedBatches": "NUM_COMPLETED_BATCHES",
+                                   "NumParticipants": "NUM_PARTICIPANTS"}.get(
+                    rule.aggregation_rule_scaling_factor or "NumTrainingExamples", "NUM_TRAINING_EXAMPLES"),
+                "batch_size": lm.batch_size, "local_epochs": lm.local_epochs,
+                "semi_sync_lambda": float(cp.semi_synchronous_lambda or 2.0),
+                "semi_sync_recompute": bool(cp.semi_sync_recompute_num_updates),
+                "participation_ratio": float(env.global_model_config.participation_ratio or 1.0),
+                "secure_aggregation": self._he_scheme is not None,
+                "extra": dict(self.collective_options.get("extra", {}))}
+
+    def _collective_job(self, rounds: int, learners=None, resume_dir: str | None = None,
+                        prev_ranks: list[int] | None = None, fault: dict | None = None, tag: str = "") -> str:
+        """The JSON job description every collective rank reads."""
+        env = self.federation_environment
+        lm = env.local_model_config
         if self.neural_engine != "static":
             raise RuntimeError("the collective data plane runs static-graph models (StaticModelDef)")
+        learners = list(env.learners) if learners is None else learners
         opt = MM.construct_optimizer_config_pb_from_kwargs(lm.optimizer_config.optimizer_pb_kwargs)
-        fed = {"protocol": "semi_synchronous" if cp.is_semi_synchronous else "synchronous",
-               "scaling_factor": {"NumTrainingExamples": "NUM_TRAINING_EXAMPLES",
-                                  "NumCompletedBatches": "NUM_COMPLETED_BATCHES",
-                                  "NumParticipants": "NUM_PARTICIPANTS"}.get(
-                   rule.aggregation_rule_scaling_factor or "NumTrainingExamples", "NUM_TRAINING_EXAMPLES"),
-               "batch_size": lm.batch_size, "local_epochs": lm.local_epochs,
-               "semi_sync_lambda": float(cp.semi_synchronous_lambda or 2.0),
-               "semi_sync_recompute": bool(cp.semi_sync_recompute_num_updates),
-               "participation_ratio": float(env.global_model_config.participation_ratio or 1.0),
-               "secure_aggregation": self._he_scheme is not None}
+        ts = env.termination_signals
+        o = self.collective_options
         job = {"model_dir": self._model_dir, "batch_size": lm.batch_size, "seed": self.seed,
                "optimizer_hex": opt.SerializeToString().hex(),
                "controller_hex": self._controller_entity.SerializeToString().hex(),
                "train_recipe": self.train_dataset_recipe_fp, "test_recipe": self.test_dataset_recipe_fp,
-               "rounds": rounds, "federation": fed,
+               "rounds": rounds, "federation": self._collective_federation(),
+               "termination": {"cutoff_mins": ts.execution_time_cutoff_mins, "metric": env.evaluation_metric,
+                               "metric_cutoff": ts.metric_cutoff_score},
+               "checkpoint_dir": os.path.join(self.working_dir, "collective_checkpoint"),
+               "checkpoint_every": int(o.get("checkpoint_every", 1)),
+               "heartbeat_timeout_s": float(o.get("heartbeat_timeout_s", 20.0)),
+               "resume_dir": resume_dir, "fault": fault,
                "backend": "gloo" if self.device == "cpu" else None,
                "learners": [{"id": l.learner_id, "hostname": l.grpc_servicer.hostname or "localhost",
-                             "port": int(l.grpc_servicer.port or 0) or 1 + i,
+                             "port": int(l.grpc_servicer.port or 0) or 1 + self._learner_index(l),
                              "train_path": l.dataset_configs.train_dataset_path,
-                             "test_path": l.dataset_configs.test_dataset_path, "devices": l.devices}
-                            for i, l in enumerate(env.learners)]}
-        p = os.path.join(self.working_dir, "collective_job.json")
+                             "test_path": l.dataset_configs.test_dataset_path, "devices": l.devices,
+                             "seed": self._learner_index(l),
+                             "prev_rank": prev_ranks[i] if prev_ranks is not None else None}
+                            for i, l in enumerate(learners)]}
+        p = os.path.join(self.working_dir, f"collective_job{tag}.json")
         with open(p, "w") as f:
             json.dump(job, f)
         return p
 
-    def _init_collective_learners(self, rounds: int):
+    def _learner_index(self, learner) -> int:
+        return [l.learner_id for l in self.federation_environment.learners].index(learner.learner_id)
+
+    def _init_collective_learners(self, rounds: int, learners=None, resume_dir=None, prev_ranks=None,
+                                  fault=None, tag: str = ""):
         """One process per learner (= per GPU) under one process group; the
         torch.distributed env is set here, before any of them touches a GPU
-        (reference counterpart: driver_session.py:529-582)."""
+        (reference counterpart: driver_session.py:529-582).  Each launch is a
+        set of FRESH processes (never a re-exec of one that touched the GPU)."""
         import sys
-        job = self._collective_job(rounds)
-        learners = list(self.federation_environment.learners)
+        learners = list(self.federation_environment.learners) if learners is None else learners
+        job = self._collective_job(rounds, learners, resume_dir, prev_ranks, fault, tag)
         port = free_port()
+        self._collective_members = learners
         for rank, l in enumerate(learners):
             extra = {"RANK": str(rank), "WORLD_SIZE": str(len(learners)), "MASTER_ADDR": "127.0.0.1",
                      "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0",
@@ -293,15 +343,68 @@ class DriverSessionBase:
             self._spawn(f"learner_{l.learner_id}", [sys.executable, "-m", "metisfl_amd.learner.collective", job],
                         extra)
 
+    # a rank that lost a peer exits with this code (parallel/watchdog.py); the
+    # driver's own terminate gives -15 / -9
+    _PEER_EXIT = (75, -15, -9)
+
+    def _recover_collective(self, failed_name: str, code: int) -> None:
+        """A collective rank died: stop the survivors (blocked in a collective,
+        or already out on their watchdog), and relaunch them as fresh
+        processes on the smaller world from the last FederatedModel checkpoint
+        (the reference's learners may leave at any time,
+        controller.cc:171-199)."""
+        members = list(self._collective_members)
+        names = {f"learner_{l.learner_id}": l for l in members}
+        for name, p in self._procs.items():
+            if name in names and p.poll() is None:
+                p.terminate()
+        for name, p in self._procs.items():
+            if name in names:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait(10)
+        failed = {n for n in names if self._procs[n].returncode not in (0,) + self._PEER_EXIT}
+        if not failed and code not in self._PEER_EXIT:
+            failed.add(failed_name)
+        if not failed:
+            raise RuntimeError(f"collective learners left on a lost peer, but the failed rank is unknown "
+                               f"({failed_name} exited with {code})")
+        survivors = [l for l in members if f"learner_{l.learner_id}" not in failed]
+        if not survivors:
+            raise RuntimeError(f"every collective learner failed ({failed_name} exited with {code})")
+        ckpt = os.path.join(self.working_dir, "collective_checkpoint")
+        resume = ckpt if os.path.exists(os.path.join(ckpt, "federation.json")) else None
+        prev = [members.index(l) for l in survivors]
+        gi = None
+        if resume:
+            with open(os.path.join(ckpt, "federation.json")) as f:
+                gi = json.load(f)["global_iteration"]
+        self.recoveries.append({"failed": sorted(failed), "exit_code": code, "survivors": len(survivors),
+                                "resumed_from_round": gi, "at": time.time()})
+        MetisLogger.warning("collective learner(s) %s lost (exit %d): relaunching %d survivors from round %s",
+                            sorted(failed), code, len(survivors), gi)
+        for n in names:
+            log = os.path.join(self.working_dir, f"{n}.log")
+            if os.path.exists(log):
+                os.replace(log, log + f".attempt{len(self.recoveries)}")
+            self._procs.pop(n, None)
+        self._init_collective_learners(self.federation_environment.termination_signals.federation_rounds,
+                                       survivors, resume, prev, None, tag=f"_r{len(self.recoveries)}")
+
     # -- public API -----------------------------------------------------------------------------------
     def initialize_federation(self):
+        if self.collective:
+            self._collective_federation()  # unsupported combinations fail before anything starts
         self._init_controller()
         ok = self._driver_controller_grpc_client.check_health_status(request_retries=10, request_timeout=30)
         if not ok:
             raise RuntimeError("controller did not come up; see controller.log")
         self._ship_model_to_controller()
         if self.collective:
-            self._init_collective_learners(self.federation_environment.termination_signals.federation_rounds)
+            self._init_collective_learners(self.federation_environment.termination_signals.federation_rounds,
+                                           fault=self.collective_options.get("fault"))
             return
         for l in self.federation_environment.learners:
             self._init_learner(l, self.federation_environment.controller)
@@ -329,9 +432,20 @@ class DriverSessionBase:
         st = time.time()
         while True:
             time.sleep(request_every_secs)
-            for name, p in self._procs.items():
+            for name, p in list(self._procs.items()):
                 if p.poll() is not None and p.returncode != 0:
+                    if (self.collective and name.startswith("learner_")
+                            and len(self.recoveries) < int(self.collective_options.get("max_recoveries", 2))):
+                        self._recover_collective(name, p.returncode)
+                        break
                     raise RuntimeError(f"{name} exited with {p.returncode}; see {name}.log")
+            evals = self._driver_controller_grpc_client.get_community_model_evaluation_lineage(-1)
+            for res in evals.community_evaluation:
+                scores = [float(e.test_evaluation.metric_values[metric]) for e in res.evaluations.values()
+                          if metric in e.test_evaluation.metric_values]
+                if scores and sum(scores) / len(scores) >= metric_cutoff:
+                    MetisLogger.info("Exceeded evaluation metric cutoff score. Exiting ...")
+                    return "metric"
             if self.collective and all(p.poll() == 0 for n, p in self._procs.items() if n.startswith("learner_")):
                 MetisLogger.info("Collective learners completed their rounds. Exiting ...")
                 return "rounds"
@@ -340,13 +454,6 @@ class DriverSessionBase:
                 if max(m.global_iteration for m in md) > rounds:
                     MetisLogger.info("Exceeded federation rounds cutoff point. Exiting ...")
                     return "rounds"
-            evals = self._driver_controller_grpc_client.get_community_model_evaluation_lineage(-1)
-            for res in evals.community_evaluation:
-                scores = [float(e.test_evaluation.metric_values[metric]) for e in res.evaluations.values()
-                          if metric in e.test_evaluation.metric_values]
-                if scores and sum(scores) / len(scores) >= metric_cutoff:
-                    MetisLogger.info("Exceeded evaluation metric cutoff score. Exiting ...")
-                    return "metric"
             if (time.time() - st) / 60 > cutoff_mins:
                 MetisLogger.info("Exceeded execution time cutoff minutes. Exiting ...")
                 return "time"
@@ -373,8 +480,29 @@ class DriverSessionBase:
         with open(path, "w") as f:
             json.dump(self._federation_statistics, f, indent=1)
 
+    def _request_collective_stop(self) -> None:
+        """Ask running collective ranks to leave after their current round."""
+        from metisfl_amd.controller import collective_service as cs
+        from metisfl_amd.utils.grpc_services import make_channel
+        ch = make_channel(self._controller_entity)
+        try:
+            cs.call(ch, "RequestStop", {}, timeout=10)
+        except Exception as e:  # noqa: BLE001 - the controller may already be gone
+            MetisLogger.warning("collective stop request failed: %r", e)
+        finally:
+            ch.close()
+
     def shutdown_federation(self, timeout: float = 60):
         try:
+            if self.collective and any(p.poll() is None for n, p in self._procs.items() if n.startswith("learner_")):
+                self._request_collective_stop()
+                end = time.time() + timeout
+                for n, p in self._procs.items():
+                    if n.startswith("learner_"):
+                        try:
+                            p.wait(timeout=max(0.1, end - time.time()))
+                        except subprocess.TimeoutExpired:
+                            pass
             self._collect_local_statistics()
             # collective learners have no gRPC server: they exit after their rounds
             for c in ([] if self.collective else self._driver_learner_grpc_clients.values()):

@@ -4,11 +4,29 @@
 
 Rank 0 fetches the driver's initial community model from the controller and
 broadcasts it; every round the learners train their shards and average in
-place with one RCCL all-reduce (parallel/federation.py); rank 0 reports each
-round to the controller's collective bookkeeping service, so the driver's
-``monitor_federation`` / ``get_federation_statistics`` see the rounds.  The
-reference has no such data plane: its learners always ship models through
-the controller (driver_session.py:529-582 launches them with their GPUs).
+place with one RCCL all-reduce (parallel/federation.py), then evaluate the
+new community model on their test shards; rank 0 reports each round (runtime
+metadata, task lineages, the CommunityModelEvaluation) to the controller's
+collective bookkeeping service, so the driver's ``monitor_federation`` /
+``get_federation_statistics`` see the rounds.  The reference has no such data
+plane: its learners always ship models through the controller
+(driver_session.py:529-582 launches them with their GPUs).
+
+Protocols: synchronous / semi-synchronous rounds (CollectiveFederation), or
+the asynchronous protocol (AsyncCollectiveFederation.run_until: FedRec over
+point-to-point transfers, one community version per completed task).
+
+Termination (the driver's TerminationSignals, driver_session.py:423-467):
+FederationRounds (sync: rounds; async: community versions), the wall-clock
+cutoff, the mean community-model test metric, or the driver's stop request;
+rank 0 decides and the decision is broadcast, so every rank leaves after the
+same round.
+
+Failure handling: a ``FederatedModel`` checkpoint is written
+every ``checkpoint_every`` rounds, a RankWatchdog exits the survivors of a
+lost rank (exit code 75), and the driver relaunches them as FRESH processes
+with ``resume_dir`` and the new world size.  ``fault`` ({"rank", "round"})
+kills a rank at the start of a round (fault injection for tests).
 
     python -m metisfl_amd.learner.collective <job.json>
 """
@@ -17,6 +35,9 @@ from __future__ import annotations
 import json
 import os
 import sys
+import time
+
+EXIT_INJECTED_FAULT = 17
 
 
 def _load_recipe(path):
@@ -25,6 +46,14 @@ def _load_recipe(path):
     import cloudpickle  # the driver's own file (DriverSession._dump_recipe)
     with open(path, "rb") as f:
         return cloudpickle.load(f)
+
+
+def _stop_decision(comm, rank0_stop: bool) -> bool:
+    """Rank 0's stop decision, identical on every rank."""
+    import torch
+    t = torch.tensor([1.0 if rank0_stop else 0.0], dtype=torch.float64, device=comm.device)
+    comm.broadcast_(t, src=0)
+    return bool(t.item() > 0.5)
 
 
 def main(argv=None) -> int:
@@ -39,11 +68,14 @@ def main(argv=None) -> int:
     from metisfl_amd.parallel.comm import Comm
     from metisfl_amd.parallel.engine_bridge import RemoteCollectiveController
     from metisfl_amd.parallel.federation import CollectiveFederation, FederationConfig
+    from metisfl_amd.parallel.watchdog import RankWatchdog
     from metisfl_amd.proto import metis_pb2, model_pb2
     from metisfl_amd.utils.grpc_controller_client import GRPCControllerClient
 
     comm = Comm(backend=job.get("backend"))
     rank = comm.rank
+    if comm.world != len(job["learners"]):
+        raise RuntimeError(f"WORLD_SIZE {comm.world} != {len(job['learners'])} learners in the job")
     lcfg = job["learners"][rank]
     torch.manual_seed(job.get("seed", 0) + rank)
     opt = OptimizerSpec.from_proto(model_pb2.OptimizerConfig.FromString(bytes.fromhex(job["optimizer_hex"])))
@@ -52,38 +84,98 @@ def main(argv=None) -> int:
                               seed=job.get("seed", 0))
     train = resolve_dataset(_load_recipe(job.get("train_recipe")), lcfg.get("train_path"))
     test = resolve_dataset(_load_recipe(job.get("test_recipe")), lcfg.get("test_path"))
-    train_ds = net.make_dataset(train.get_x(), train.get_y(), seed=rank)
+    train_ds = net.make_dataset(train.get_x(), train.get_y(), seed=lcfg.get("seed", rank))
     test_ds = net.make_dataset(test.get_x(), test.get_y(), seed=rank, shuffle=False) if test is not None else None
     fcfg = FederationConfig(**job["federation"])
-    fed = CollectiveFederation(comm, net, train_ds, fcfg, test_ds=test_ds, broadcast_initial=False)
+    term = job.get("termination") or {}
+    rounds = int(job["rounds"])
+    cutoff_s = float(term["cutoff_mins"]) * 60.0 if term.get("cutoff_mins") else None
+    metric, metric_cutoff = term.get("metric"), term.get("metric_cutoff")
+    fault = job.get("fault") or {}
+    ckpt_dir, every = job.get("checkpoint_dir"), int(job.get("checkpoint_every", 1) or 0)
     entity = metis_pb2.ServerEntity.FromString(bytes.fromhex(job["controller_hex"]))
-    if rank == 0:
+    wd = None
+    if comm.world > 1 and job.get("watchdog", True):
+        wd = RankWatchdog(comm, interval_s=float(job.get("heartbeat_s", 1.0)),
+                          timeout_s=float(job.get("heartbeat_timeout_s", 20.0))).start()
+    t_start = time.time()
+
+    def initial_model(fed_load):
+        if rank != 0 or job.get("resume_dir"):
+            return
         client = GRPCControllerClient(entity, max_workers=1)
         try:
             lin = client.get_community_model_lineage(1)
             if len(lin.federated_models):
-                fed.load_community_model(lin.federated_models[-1])
+                fed_load(lin.federated_models[-1])
         finally:
             client.shutdown()
-        fed.engine = RemoteCollectiveController(entity, fed.dataset_sizes,
-                                                [(l["hostname"], l["port"]) for l in job["learners"]])
+
+    endpoints = [(l["hostname"], l["port"]) for l in job["learners"]]
+    if fcfg.protocol == "asynchronous":
+        from metisfl_amd.parallel.async_federation import AsyncCollectiveFederation
+        from metisfl_amd.parallel.federation import install_community_model
+        initial_model(lambda fm: install_community_model(net, fm))
+        engine = None
+        if rank == 0:
+            sizes = comm.all_gather_rows(torch.tensor([float(train_ds.n)], dtype=torch.float64,
+                                                      device=comm.device)).cpu().numpy()[:, 0]
+            engine = RemoteCollectiveController(entity, [int(x) for x in sizes], endpoints)
+        else:
+            comm.all_gather_rows(torch.tensor([float(train_ds.n)], dtype=torch.float64, device=comm.device))
+        fed = AsyncCollectiveFederation(comm, net, train_ds, fcfg, test_ds=test_ds, engine=engine,
+                                        broadcast_initial=True)
+        delay = float((fcfg.extra or {}).get("debug_delay_s", {}).get(str(rank), 0.0))
+        ups = fed.run_until(max_updates=rounds, cutoff_s=cutoff_s, metric=metric, metric_cutoff=metric_cutoff,
+                            debug_delay_s=delay)
+        if rank == 0:
+            print(f"[collective-async] {len(ups)} FedRec updates, stop: {fed.stop_reason}, staleness "
+                  f"{[u.staleness for u in ups]}", flush=True)
+            engine.close()
+        if wd is not None:
+            wd.stop()
+        comm.close()
+        return 0
+
+    fed = CollectiveFederation(comm, net, train_ds, fcfg, test_ds=test_ds, broadcast_initial=False)
+    initial_model(fed.load_community_model)
+    if rank == 0:
+        fed.engine = RemoteCollectiveController(entity, fed.dataset_sizes, endpoints)
     fed.broadcast_initial_model()
     if job.get("resume_dir"):
-        fed.resume(job["resume_dir"])
-    for _ in range(int(job["rounds"])):
+        fed.resume(job["resume_dir"], prev_rank=lcfg.get("prev_rank"))
+        if rank == 0:
+            print(f"[collective] resumed at round {fed.global_iteration} on {comm.world} learners "
+                  f"(checkpoint of {fed.resumed_from_world})", flush=True)
+    while fed.global_iteration < rounds:
+        if fault and int(fault.get("rank", -1)) == rank and fed.global_iteration + 1 == int(fault.get("round", 0)):
+            print(f"[collective] fault injection: rank {rank} exits at round {fed.global_iteration + 1}", flush=True)
+            sys.stdout.flush()
+            os._exit(EXIT_INJECTED_FAULT)
         rec = fed.run_round()
         if rank == 0:
             print(f"[collective] round {rec.global_iteration}: {rec.round_ms:.1f} ms "
-                  f"(train {rec.train_ms:.1f}, aggregate {rec.aggregation_ms:.2f}) weights {rec.weights}",
-                  flush=True)
-    if job.get("checkpoint_dir"):
-        fed.save_checkpoint(job["checkpoint_dir"])
+                  f"(train {rec.train_ms:.1f}, aggregate {rec.aggregation_ms:.2f}, community eval "
+                  f"{rec.community_eval_ms:.1f}) weights {rec.weights}", flush=True)
+        if ckpt_dir and every and (fed.global_iteration % every == 0 or fed.global_iteration >= rounds):
+            fed.save_checkpoint(ckpt_dir)
+        stop = False
+        if rank == 0:
+            m = fed.community_metric(rec, metric) if metric else None
+            stop = (fed.stop_requested or (metric_cutoff is not None and m is not None and m >= float(metric_cutoff))
+                    or (cutoff_s is not None and time.time() - t_start > cutoff_s))
+        if _stop_decision(comm, stop):
+            break
+    if ckpt_dir and not (every and fed.global_iteration % every == 0):
+        fed.save_checkpoint(ckpt_dir)
     if rank == 0:
         st = net.state
         vals = st.to_numpy()
         fed.engine.snapshot_community([s.name for s in st.specs], [vals[s.name] for s in st.specs],
                                       [s.trainable for s in st.specs], fed.global_iteration)
         fed.engine.close()
+    if wd is not None:
+        wd.stop()
     comm.close()
     return 0
 

@@ -34,11 +34,19 @@ class DeviceDataset:
     of running short (``drop_last=True``: floor(n / batch) full batches)."""
 
     def __init__(self, x: torch.Tensor, y: torch.Tensor, batch_size: int, seed: int = 0,
-                 shuffle: bool = True, drop_last: bool = False):
+                 shuffle: bool = True, drop_last: bool = False, pad_tail: bool = False):
         assert x.shape[0] == y.shape[0]
+        self.n = int(x.shape[0])
+        # pad_tail (evaluation): ceil(n / B) batches, the last one completed
+        # with a padding row (zeros, label -1) that the loss / accuracy
+        # kernels skip -- every sample is evaluated exactly once, as Keras
+        # ``evaluate`` does
+        self.pad_tail = bool(pad_tail) and not shuffle
+        if self.pad_tail:
+            x = torch.cat([x, torch.zeros((1,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)])
+            y = torch.cat([y.to(torch.int32), torch.full((1,), -1, dtype=torch.int32, device=y.device)])
         self.x = x.contiguous()
         self.y = y.to(torch.int32).contiguous()
-        self.n = int(x.shape[0])
         self.batch_size = batch_size
         self.steps_per_epoch = max(1, self.n // batch_size) if drop_last else max(1, -(-self.n // batch_size))
         self.shuffle = shuffle
@@ -53,6 +61,8 @@ class DeviceDataset:
             p = torch.randperm(self.n, generator=self.gen)
         else:
             p = torch.arange(self.n)
+        if p.numel() < need and self.pad_tail:  # the padding row
+            p = torch.cat([p, torch.full((need - p.numel(),), self.n, dtype=p.dtype)])
         if p.numel() < need:  # last partial batch wraps around
             p = torch.cat([p, p[: need - p.numel()]])
         self.perm.copy_(p[:need].to(torch.int32), non_blocking=True)
@@ -235,9 +245,10 @@ class StaticNet:
             y = y.to(torch.float32).contiguous().view(torch.int32)
         y = y.to(torch.int32).to(self.device)
         # training shards: ceil(n / B) steps per epoch (wrapped last batch);
-        # evaluation shards (unshuffled): full batches only, no sample twice
+        # evaluation shards (unshuffled): ceil(n / B) steps, the last batch's
+        # tail is padding the statistics skip (every sample exactly once)
         return DeviceDataset(x, y, batch_size or self.B, seed=seed, shuffle=shuffle,
-                             drop_last=(not shuffle) if drop_last is None else drop_last)
+                             drop_last=bool(drop_last), pad_tail=not shuffle and not drop_last)
 
     @staticmethod
     def timer():

@@ -302,7 +302,7 @@ def hconv_workspace(shp: ConvShape, device: torch.device) -> int:
 
 
 def hconv_forward(z, wp, w, out, shp: ConvShape, bn: BnParams, train: bool, relu: bool, ws=None, stats=None,
-                  res=None, zr=None, bnr: BnParams | None = None, y=None, yp=None) -> None:
+                  res=None, zr=None, bnr: BnParams | None = None, y=None, yp=None, stamps=None) -> None:
     """out = conv3x3(T(z), w) with T(z) = relu?(BN(z) [+ res | + BN_r(zr)]) applied
     as the operand enters LDS (one launch: no separate BatchNorm apply).
     ``y`` / ``yp`` receive T(z) and its packed bf16x3 split (the activation
@@ -317,7 +317,7 @@ def hconv_forward(z, wp, w, out, shp: ConvShape, bn: BnParams, train: bool, relu
                             bn.run_var, bn.momentum, bn.eps, res, zr,
                             (b2.acc if train else None) if b2 else None, b2.gamma if b2 else None,
                             b2.beta if b2 else None, b2.mean if b2 else None, b2.invstd if b2 else None,
-                            b2.run_mean if b2 else None, b2.run_var if b2 else None, y, yp)
+                            b2.run_mean if b2 else None, b2.run_var if b2 else None, y, yp, stamps)
         return
     # reference: the BatchNorm apply(s) the fill replaces, then the conv
     r = res
@@ -456,9 +456,11 @@ def head_forward_backward(x, B: int, HW: int, C: int, W, bias, labels, feat, dlo
     lab = labels[:B].long()
     lse = torch.logsumexp(logits, 1)
     if stats is not None:
-        stats[0] += (lse - logits.gather(1, lab[:, None])[:, 0]).sum()
-        stats[1] += (logits.argmax(1) == lab).float().sum()
-        stats[2] += B
+        ok = lab >= 0  # label -1: an evaluation padding row (not counted)
+        lv = lab.clamp_min(0)
+        stats[0] += torch.where(ok, lse - logits.gather(1, lv[:, None])[:, 0], torch.zeros(())).sum()
+        stats[1] += ((logits.argmax(1) == lab) & ok).float().sum()
+        stats[2] += ok.float().sum()
     if not backward:
         return
     p = torch.softmax(logits, 1)
@@ -607,9 +609,11 @@ def xent(logits, labels, B: int, Kp: int, K: int, dlogits, stats) -> None:
     z = logits.float().reshape(B, Kp)[:, :K]
     y = labels[:B].long()
     lse = torch.logsumexp(z, 1)
-    stats[0] += float((lse - z.gather(1, y[:, None])[:, 0]).sum())
-    stats[1] += float((z.argmax(1) == y).sum())
-    stats[2] += float(B)
+    ok = y >= 0  # label -1: an evaluation padding row
+    yv = y.clamp_min(0)
+    stats[0] += float(torch.where(ok, lse - z.gather(1, yv[:, None])[:, 0], torch.zeros(())).sum())
+    stats[1] += float(((z.argmax(1) == y) & ok).sum())
+    stats[2] += float(ok.sum())
     if dlogits is not None:
         g = torch.zeros(B, Kp)
         g[:, :K] = (torch.softmax(z, 1) - F.one_hot(y, K).float()) / B
@@ -623,8 +627,9 @@ def mse(pred, target, B: int, Kp: int, dpred, stats) -> None:
         return
     t = target[:B].view(torch.float32) if target.dtype == torch.int32 else target[:B].float()
     d = pred.float().reshape(B, Kp)[:, 0] - t
-    stats[0] += float((d * d).sum())
-    stats[2] += float(B)
+    ok = ~torch.isnan(t)  # the -1 label bits of an evaluation padding row
+    stats[0] += float(torch.where(ok, d * d, torch.zeros(())).sum())
+    stats[2] += float(ok.sum())
     if dpred is not None:
         g = torch.zeros(B, Kp)
         g[:, 0] = 2 * d / B

@@ -55,6 +55,8 @@ from metisfl_amd.parallel.federation import FederationConfig
 
 _KEY = "metisfl_async/{}/{}/{}"
 _VER = "metisfl_async/ver/{}/{}/{}"
+_STOP = "metisfl_async/stop/{}"
+_DONE = "metisfl_async/done/{}/{}"
 _INSTANCES = [0]  # federations built so far in this process (identical on every rank)
 
 
@@ -86,8 +88,16 @@ class AsyncUpdate:
 class AsyncCollectiveFederation:
     def __init__(self, comm: Comm, net, train_ds, cfg: FederationConfig, tasks_per_learner: int = 2,
                  poll_every: int = 16, store=None, broadcast_initial: bool = True,
-                 serve_in_thread: bool = True):
+                 serve_in_thread: bool = True, test_ds=None, engine=None):
         self.comm, self.net, self.train_ds, self.cfg = comm, net, train_ds, cfg
+        self.test_ds = test_ds
+        # rank 0: the controller bridge (engine_bridge.py) every FedRec update
+        # and community evaluation is recorded with (runtime metadata, local
+        # task lineage, community-model evaluations)
+        self.engine = engine if comm.rank == 0 else None
+        self.evaluations: list[dict] = []  # rank 0: {"version", "learner", "loss", "accuracy"}
+        self._stop_flag = False            # termination mode (run_until)
+        self._done: set[int] = set()
         self.rank, self.world = comm.rank, comm.world
         _INSTANCES[0] += 1
         self.tag = _INSTANCES[0]  # store-key namespace: repeated federations never see old keys
@@ -136,7 +146,11 @@ class AsyncCollectiveFederation:
         self.steps_done += nsteps
 
     def _pending(self) -> bool:
+        if self._until:
+            return len(self._done) < self.world - 1
         return any(self.next_task[r] < self.tasks for r in range(1, self.world))
+
+    _until = False
 
     def _serve_loop(self) -> None:
         """Rank 0 service thread: serve submissions as they arrive."""
@@ -216,12 +230,18 @@ class AsyncCollectiveFederation:
         served = 0
         for r in range(1, self.world):
             t = self.next_task[r]
-            if t >= self.tasks:
+            if (not self._until and t >= self.tasks) or r in self._done:
                 continue
             key = _KEY.format(self.tag, r, t)
             if not block and not self.store.check([key]):
+                if self._until:
+                    dkey = _DONE.format(self.tag, r)
+                    if self.store.check([dkey]):  # its last submission was served
+                        self._record_eval(r, json.loads(self.store.get(dkey)).get("eval"))
+                        self._done.add(r)
                 continue
             meta = json.loads(self.store.get(key))
+            self._record_eval(r, meta.get("eval"))
             dist.recv(self.rbuf, src=r, group=self.p2p)
             with self._lock:
                 self._fedrec(r, self.rbuf, meta)
@@ -232,6 +252,7 @@ class AsyncCollectiveFederation:
             dist.send(comm_model, dst=r, group=self.p2p)
             self.next_task[r] = t + 1
             served += 1
+            self._after_update()
         return served
 
     def _fedrec(self, r: int, theta: torch.Tensor, meta: dict) -> None:
@@ -251,9 +272,14 @@ class AsyncCollectiveFederation:
         self.version += 1
         if theta.is_cuda:  # this stream only: rank 0's training keeps running on its own
             torch.cuda.current_stream(theta.device).synchronize()
-        self.updates.append(AsyncUpdate(r, int(meta["task"]), w, time.time(),
-                                        (time.perf_counter() - t0) * 1e3, float(meta["loss"]),
-                                        int(meta["batches"]), stale, w0))
+        up = AsyncUpdate(r, int(meta["task"]), w, time.time(), (time.perf_counter() - t0) * 1e3,
+                         float(meta["loss"]), int(meta["batches"]), stale, w0)
+        self.updates.append(up)
+        if self.engine is not None:
+            # one FederatedTaskRuntimeMetadata per community version + the
+            # finisher's local task lineage (the reference's async controller
+            # records both per completion, controller.cc:201-259, 428-518)
+            self.engine.record_async_update(self.version, r, meta, up)
 
     def _community(self) -> torch.Tensor:
         c = self.S.clone()
@@ -266,3 +292,113 @@ class AsyncCollectiveFederation:
         xs = [x.double().cpu().numpy() for x in self.last if x is not None]
         ws = [w for x, w in zip(self.last, self.last_w) if x is not None]
         return sum(w * x for w, x in zip(ws, xs)) / sum(ws)
+
+
+    # ---- termination-driven mode (the driver-launched asynchronous protocol) ------------
+    def _record_eval(self, r: int, ev) -> None:
+        """A learner's evaluation of the community model version it received
+        (it rides in its next submission / its done message)."""
+        if not ev:
+            return
+        rec = {"version": int(ev["version"]), "learner": r, "loss": float(ev["loss"]),
+               "accuracy": float(ev["accuracy"]), "num_examples": int(ev.get("n", 0))}
+        self.evaluations.append(rec)
+        if self.engine is not None:
+            self.engine.record_async_evaluation(rec)
+
+    def _after_update(self) -> None:
+        """Rank 0, after every FedRec update: the termination signals."""
+        if not self._until or self._stop_flag:
+            return
+        why = None
+        if self._max_updates and self.version >= self._max_updates:
+            why = "rounds"
+        elif self._deadline is not None and time.time() > self._deadline:
+            why = "time"
+        elif self._metric_cutoff is not None and self.evaluations:
+            last = [e for e in self.evaluations if e["num_examples"]][-self.world:]
+            vals = [e.get(self._metric) for e in last if e.get(self._metric) is not None]
+            if vals and float(np.mean(vals)) >= self._metric_cutoff:
+                why = "metric"
+        if why is None and self.engine is not None and self.engine.should_stop():
+            why = "driver"
+        if why is not None:
+            self._stop_flag = True
+            self.stop_reason = why
+            self.store.set(_STOP.format(self.tag), why)
+
+    def _stopped(self) -> bool:
+        if self.rank == 0:
+            return self._stop_flag
+        return bool(self.store.check([_STOP.format(self.tag)]))
+
+    def _evaluate_received(self) -> dict | None:
+        if self.test_ds is None or not self.cfg.evaluate_community:
+            return None
+        ev = self.net.evaluate(self.test_ds, self.cfg.eval_max_steps)
+        return {"version": self.base_version, "loss": ev["loss"], "accuracy": ev["accuracy"], "n": self.test_ds.n}
+
+    def run_until(self, max_updates: int | None = None, cutoff_s: float | None = None,
+                  metric: str | None = None, metric_cutoff: float | None = None,
+                  debug_delay_s: float = 0.0) -> list[AsyncUpdate]:
+        """Asynchronous tasks until a termination signal: ``max_updates``
+        community versions (FedRec updates -- the reference's global
+        iterations), the wall-clock cutoff, the mean community-model test
+        metric of the learners' latest evaluations, or the driver's stop
+        request.  Every learner finishes the task it is running, is served,
+        and leaves; rank 0 serves until all have left."""
+        self._until = True
+        self._max_updates = max_updates
+        self._deadline = time.time() + cutoff_s if cutoff_s else None
+        self._metric, self._metric_cutoff = metric, metric_cutoff
+        self.stop_reason = None
+        svc = None
+        if self.rank == 0 and self.world > 1:
+            if not self.threaded:
+                raise RuntimeError("run_until needs the threaded aggregator (serve_in_thread=True)")
+            svc = threading.Thread(target=self._serve_loop, name="metisfl-async-aggregator", daemon=True)
+            svc.start()
+        task, last_eval = 0, None
+        spe = self.train_ds.steps_per_epoch
+        while not self._stopped():
+            self.net.reset_train_stats()
+            t_task = time.time()
+            self._train(self.num_local_updates)
+            self._sync_stream()
+            if debug_delay_s:
+                time.sleep(debug_delay_s)  # test hook: uneven learner speeds
+            ms_b = (time.time() - t_task) * 1e3 / max(1, self.num_local_updates)
+            tr = self.net.train_stats()
+            meta = {"task": task, "weight": self._weight(self.num_local_updates),
+                    "loss": tr["loss"], "accuracy": tr["accuracy"], "batches": self.num_local_updates,
+                    "base_version": self.base_version, "eval": last_eval, "started_at": t_task,
+                    "n_train": int(self.train_ds.n), "ms_per_batch": ms_b, "ms_per_epoch": ms_b * spe,
+                    "epochs": self.num_local_updates / spe}
+            if self.rank == 0:
+                with self._lock:
+                    self._record_eval(0, last_eval)
+                    self._fedrec(0, self.net.state.model32, meta)
+                    self.net.state.model32.copy_(self._community())
+                    self._sync_stream()
+                    self.base_version = self.version
+                    self._after_update()
+                self._install()
+            else:
+                self.store.set(_KEY.format(self.tag, self.rank, task), json.dumps(meta))
+                dist.send(self.net.state.model32, dst=0, group=self.p2p)
+                dist.recv(self.net.state.model32, src=0, group=self.p2p)
+                self.base_version = int(self.store.get(_VER.format(self.tag, self.rank, task)))
+                self._install()
+            last_eval = self._evaluate_received()
+            task += 1
+        if self.rank == 0:
+            with self._lock:
+                self._record_eval(0, last_eval)
+            if svc is not None:
+                svc.join()
+                if self._svc_error is not None:
+                    raise RuntimeError("async aggregator thread failed") from self._svc_error
+        else:
+            self.store.set(_DONE.format(self.tag, self.rank), json.dumps({"eval": last_eval}))
+        self.tasks_run = task
+        return self.updates

@@ -49,7 +49,7 @@ class CollectiveController:
         for r, n in enumerate(dataset_sizes):
             se = M.construct_server_entity_pb("localhost", 50052 + r).SerializeToString()
             ds = M.construct_dataset_spec_pb(int(n), 0, 0).SerializeToString()
-            lid, tok, _ = self.engine.add_learner(se, ds)
+            lid, tok, _ = self.engine.add_learner(se, ds, False)
             self.ids.append(lid)
             self.tokens.append(tok)
 
@@ -68,13 +68,58 @@ class CollectiveController:
         return M.construct_task_execution_metadata_pb(int(gi), ev, float(epochs), int(batches), batch_size,
                                                       float(ms_e), float(ms_b)).SerializeToString()
 
-    def record_round(self, rec, batch_size: int, quantifiers=None) -> None:
+    @staticmethod
+    def _model_evaluations(ev: dict) -> bytes:
+        """A learner's evaluation of the community model as the reference's
+        ModelEvaluations (test set; metric values are strings)."""
+        test = M.construct_model_evaluation_pb({"loss": ev["loss"], "accuracy": ev["accuracy"]})
+        return M.construct_model_evaluations_pb(M.construct_model_evaluation_pb({}),
+                                                M.construct_model_evaluation_pb({}), test).SerializeToString()
+
+    def _evals(self, rec):
+        if not rec.community_eval:
+            return [], []
+        ids = [self.ids[i] for i, e in enumerate(rec.community_eval) if e.get("num_examples") and i < len(self.ids)]
+        evs = [self._model_evaluations(e) for e in rec.community_eval if e.get("num_examples")]
+        return ids, evs
+
+    def record_round(self, rec, batch_size: int, quantifiers=None) -> bool:
         ns = lambda t: int(t * 1e9)
         zeros, sizes, lengths = quantifiers or ([], [], [])
         metas = [self._task_meta(rec.learner_meta[i], batch_size) for i in range(len(self.ids))]
         self.engine.record_collective_round(rec.global_iteration, self.ids, ns(rec.started_at),
                                             ns(rec.completed_at), ns(rec.aggregation_started_at),
                                             ns(rec.aggregation_completed_at), metas, zeros, sizes, lengths)
+        ids, evs = self._evals(rec)
+        if ids:
+            self.engine.record_community_evaluation(rec.global_iteration, ids, evs)
+        return False
+
+    # -- asynchronous collective federation (async_federation.run_until) ---------------
+    def _async_args(self, version: int, r: int, meta: dict, up):
+        row = [meta.get("n_train", 0), meta["batches"], meta.get("ms_per_batch", 0.0), meta.get("ms_per_epoch", 0.0),
+               meta["loss"], meta.get("accuracy", float("nan")), meta.get("epochs", 0.0), version]
+        agg_done = up.received_at
+        agg_start = agg_done - up.aggregation_ms / 1e3
+        return row, int(meta.get("started_at", agg_start) * 1e9), int(agg_start * 1e9), int(agg_done * 1e9)
+
+    def record_async_update(self, version: int, r: int, meta: dict, up, batch_size: int = 0) -> None:
+        """One FedRec update: the finisher's task metadata and one runtime
+        metadata record (global iteration = community version)."""
+        row, st, ag0, ag1 = self._async_args(version, r, meta, up)
+        self.engine.record_collective_round(version, [self.ids[r]], st, ag0, ag0, ag1,
+                                            [self._task_meta(row, batch_size)], [], [], [])
+
+    def record_async_evaluation(self, ev: dict) -> None:
+        self.engine.record_community_evaluation(ev["version"], [self.ids[ev["learner"]]],
+                                                [self._model_evaluations(ev)])
+
+    def should_stop(self) -> bool:
+        return False
+
+    def community_evaluation_lineage(self, n: int = 0):
+        return controller_pb2.GetCommunityModelEvaluationLineageResponse.FromString(
+            self.engine.community_evaluation_lineage(n))
 
     def snapshot_community(self, names, arrays, trainable, global_iteration: int) -> None:
         """Community-model lineage entry (an explicit D2H copy: done on
@@ -124,17 +169,42 @@ class RemoteCollectiveController(CollectiveController):
                                                         "batches": [float(x) for x in completed_batches]})
         return r["factors"]
 
-    def record_round(self, rec, batch_size: int, quantifiers=None) -> None:
+    def record_round(self, rec, batch_size: int, quantifiers=None) -> bool:
+        """-> True when the driver asked the federation to stop."""
         import base64
         ns = lambda t: int(t * 1e9)
         zeros, sizes, lengths = quantifiers or ([], [], [])
         metas = [base64.b64encode(self._task_meta(rec.learner_meta[i], batch_size)).decode()
                  for i in range(len(self.ids))]
-        self._cs.call(self._ch, "RecordRound", {
+        ids, evs = self._evals(rec)
+        r = self._cs.call(self._ch, "RecordRound", {
             "global_iteration": rec.global_iteration, "ids": self.ids, "started_ns": ns(rec.started_at),
             "completed_ns": ns(rec.completed_at), "agg_started_ns": ns(rec.aggregation_started_at),
             "agg_completed_ns": ns(rec.aggregation_completed_at), "metas": metas,
-            "zeros": [int(z) for z in zeros], "sizes": [int(z) for z in sizes], "lengths": [int(z) for z in lengths]})
+            "zeros": [int(z) for z in zeros], "sizes": [int(z) for z in sizes], "lengths": [int(z) for z in lengths],
+            "eval_ids": ids, "evaluations": [base64.b64encode(e).decode() for e in evs]})
+        return bool(r.get("stop", False))
+
+    def should_stop(self) -> bool:
+        if getattr(self, "_stop_seen", False):
+            return True
+        self._stop_seen = bool(self._cs.call(self._ch, "ShouldStop", {}).get("stop", False))
+        return self._stop_seen
+
+    def record_async_update(self, version: int, r: int, meta: dict, up, batch_size: int = 0) -> None:
+        import base64
+        row, st, ag0, ag1 = self._async_args(version, r, meta, up)
+        resp = self._cs.call(self._ch, "RecordAsyncUpdate", {
+            "global_iteration": version, "id": self.ids[r], "started_ns": st, "completed_ns": ag0,
+            "agg_started_ns": ag0, "agg_completed_ns": ag1,
+            "meta": base64.b64encode(self._task_meta(row, batch_size)).decode()})
+        self._stop_seen = getattr(self, "_stop_seen", False) or bool(resp.get("stop", False))
+
+    def record_async_evaluation(self, ev: dict) -> None:
+        import base64
+        self._cs.call(self._ch, "RecordEvaluation", {
+            "global_iteration": ev["version"], "ids": [self.ids[ev["learner"]]],
+            "evaluations": [base64.b64encode(self._model_evaluations(ev)).decode()]})
 
     def snapshot_community(self, names, arrays, trainable, global_iteration: int) -> None:
         from metisfl_amd.utils.grpc_controller_client import GRPCControllerClient

@@ -67,6 +67,10 @@ class FederationConfig:
     semi_sync_lambda: float = 2.0
     semi_sync_recompute: bool = False
     evaluate_test: bool = True             # learner test-set eval at task end
+    # every learner evaluates the NEW community model on its test shard after
+    # the all-reduce (the reference's SendEvaluationTasks, controller.cc:469-485,
+    # 571-587); rank 0 records the CommunityModelEvaluation with the round
+    evaluate_community: bool = True
     eval_max_steps: int | None = None
     quantify: bool = True                  # per-variable zero counts of each community model
     jsonl_log: str | None = None           # rank 0: one JSON line per round (utils/tracing.py)
@@ -115,11 +119,31 @@ class RoundRecord:
     allreduce_gbps: float = 0.0            # algorithm bandwidth: model bytes / all-reduce time
     hbm_used_bytes: int = 0
     he_stats: dict | None = None           # secure aggregation: encrypt / all-reduce / decrypt ms
+    # per-learner test metrics of the community model (rank order), and the
+    # time the evaluation took: after the barrier (outside completed_at -
+    # started_at, as in the reference) but inside round_ms
+    community_eval: list | None = None
+    community_eval_ms: float = 0.0
 
     def to_json(self) -> dict:
         d = asdict(self)
         d["learner_meta"] = self.learner_meta.tolist()
         return d
+
+
+def install_community_model(net, fm) -> None:
+    """Install a ``FederatedModel`` (proto or serialized bytes) into ``net``
+    as the community model, matching variables by name."""
+    from metisfl_amd.proto import model_pb2
+    from metisfl_amd.utils.tensor_codec import model_to_arrays
+    if isinstance(fm, (bytes, bytearray)):
+        m = model_pb2.FederatedModel()
+        m.ParseFromString(bytes(fm))
+        fm = m
+    names, arrays, _ = model_to_arrays(fm.model)
+    st = net.state
+    st.load_numpy(dict(zip(names, arrays)))
+    st.set_anchor()
 
 
 class CollectiveFederation:
@@ -240,6 +264,11 @@ class CollectiveFederation:
 
     def aggregation_weights(self, meta: np.ndarray) -> list[float]:
         part = meta[:, 10] > 0.5
+        if not part.any():
+            # every learner hit the deadline before finishing its budget: the
+            # ones that ran the most local updates stand in as participants
+            # (an all-zero weight vector would zero the community model)
+            part = meta[:, 1] >= meta[:, 1].max()
         if not part.all():  # stragglers dropped: scale over the participants only
             idx = np.flatnonzero(part)
             ws = scaling.compute(self.cfg.scaling_factor, meta[idx, 0], meta[idx, 1], len(idx))
@@ -356,6 +385,27 @@ class CollectiveFederation:
         lengths = [e - b for b, e in segs]
         return zeros, [n * 4 for n in lengths], lengths
 
+    def evaluate_community(self) -> tuple[list | None, float]:
+        """Every learner evaluates the community model (resident after the
+        all-reduce) on its test shard; the metrics are all-gathered (a few
+        scalars per learner).  -> ([{"loss", "accuracy", "num_examples"}] per
+        rank, ms)."""
+        if not self.cfg.evaluate_community:
+            return None, 0.0
+        t0 = time.perf_counter()
+        ev = {"loss": float("nan"), "accuracy": float("nan")}
+        n = 0
+        if self.test_ds is not None:
+            with tracing.range("metisfl.community_eval"):
+                ev = self.net.evaluate(self.test_ds, self.cfg.eval_max_steps)
+            n = self.test_ds.n
+        row = torch.tensor([ev["loss"], ev["accuracy"], float(n)], dtype=torch.float64, device=self.comm.device)
+        rows = self.comm.all_gather_rows(row).cpu().numpy()
+        out = [{"loss": float(r[0]), "accuracy": float(r[1]), "num_examples": int(r[2])} for r in rows]
+        if all(o["num_examples"] == 0 for o in out):
+            return None, (time.perf_counter() - t0) * 1e3
+        return out, (time.perf_counter() - t0) * 1e3
+
     def run_round(self) -> RoundRecord:
         self.global_iteration += 1
         started = time.time()
@@ -373,24 +423,35 @@ class CollectiveFederation:
         weights, agg_ms = self.aggregate(meta)
         agg_done = time.time()
         ar_ms = getattr(self, "last_allreduce_ms", 0.0)
+        community_eval, ce_ms = self.evaluate_community()
+        round_done = time.time()
         nbytes = self.net.state.model32.numel() * 4
         rec = RoundRecord(self.global_iteration, started, completed, completed, agg_done,
-                          (agg_done - started) * 1e3, res["ms"], agg_ms, meta, weights,
+                          (round_done - started) * 1e3, res["ms"], agg_ms, meta, weights,
                           list(self.num_local_updates), res.get("test"), ar_ms,
                           nbytes / (ar_ms * 1e6) if ar_ms > 0 else 0.0,
                           tracing.hbm_usage(self.comm.device).get("used_bytes", 0)
                           if self.comm.device.type == "cuda" else 0)
+        rec.community_eval, rec.community_eval_ms = community_eval, ce_ms
         if self.cfg.secure_aggregation:
             rec.he_stats = dict(self.last_he_stats)
         if self.rank == 0:
             self._log.write({"kind": "round", **rec.to_json(),
                              "rounds_per_s": 1e3 / rec.round_ms if rec.round_ms > 0 else 0.0})
+        self.stop_requested = False
         if self.engine is not None:
-            self.engine.record_round(rec, self.cfg.batch_size,
-                                     self._quantifiers() if self.cfg.quantify else None)
+            r = self.engine.record_round(rec, self.cfg.batch_size,
+                                         self._quantifiers() if self.cfg.quantify else None)
+            self.stop_requested = bool(r)  # the driver asked the federation to stop
         self.update_templates(meta)
         self.history.append(rec)
         return rec
+
+    def community_metric(self, rec: RoundRecord, metric: str) -> float | None:
+        """Mean over learners of a community-model test metric (the driver's
+        MetricCutoffScore statistic, driver_session.py:423-467)."""
+        vals = [e[metric] for e in (rec.community_eval or []) if e.get("num_examples") and metric in e]
+        return float(np.mean(vals)) if vals else None
 
     # -- checkpoint / resume (SURVEY §5.4) ------------------------------------------
     COMMUNITY_FILE = "community_model.pb"
@@ -443,25 +504,18 @@ class CollectiveFederation:
     def load_community_model(self, fm) -> None:
         """Install a ``FederatedModel`` (proto or serialized bytes) as the
         community model, matching variables by name."""
-        from metisfl_amd.proto import model_pb2
-        from metisfl_amd.utils.tensor_codec import model_to_arrays
-        if isinstance(fm, (bytes, bytearray)):
-            m = model_pb2.FederatedModel()
-            m.ParseFromString(bytes(fm))
-            fm = m
-        names, arrays, _ = model_to_arrays(fm.model)
-        st = self.net.state
-        st.load_numpy(dict(zip(names, arrays)))
-        st.set_anchor()
+        install_community_model(self.net, fm)
 
-    def resume(self, path: str) -> None:
+    def resume(self, path: str, prev_rank: int | None = None) -> None:
         """Reload a checkpoint written by ``save_checkpoint``.  The world size
         may differ (learners joined or left, SURVEY §5.3 / the reference's
         join-leave semantics, controller.cc:99-199): the community model is
         restored on every rank, learner-local state (optimizer slots, step
         counter, epoch permutation) only on ranks that existed before, and
         the step budgets / aggregation weights follow the CURRENT shards
-        (computed at construction from the new dataset sizes)."""
+        (computed at construction from the new dataset sizes).  ``prev_rank``:
+        this learner's rank in the checkpointed federation (a relaunch after a
+        lost rank renumbers the survivors); default: the same rank."""
         with open(os.path.join(path, "federation.json")) as f:
             meta = json.load(f)
         with open(os.path.join(path, self.COMMUNITY_FILE), "rb") as f:
@@ -469,14 +523,15 @@ class CollectiveFederation:
         st = self.net.state
         dev = st.model32.device
         same_world = meta["world"] == self.world
-        rank_file = os.path.join(path, f"rank{self.rank}.pt")
-        if os.path.exists(rank_file) and self.rank < meta["world"]:
+        old_rank = self.rank if prev_rank is None else int(prev_rank)
+        rank_file = os.path.join(path, f"rank{old_rank}.pt")
+        if os.path.exists(rank_file) and 0 <= old_rank < meta["world"]:
             per_rank = torch.load(rank_file, weights_only=True)
             st.step.copy_(per_rank["step"].to(dev))
             for k in ("m", "v"):
                 if k in per_rank and getattr(st, k) is not None and per_rank[k].numel() == getattr(st, k).numel():
                     getattr(st, k).copy_(per_rank[k].to(dev))
-            if same_world and per_rank["perm"].numel() == self.train_ds.perm.numel():
+            if same_world and old_rank == self.rank and per_rank["perm"].numel() == self.train_ds.perm.numel():
                 self.train_ds.perm.copy_(per_rank["perm"].to(self.train_ds.perm.device))
                 self.steps_done = int(per_rank["steps_done"])
         st.set_anchor()  # FedProx anchors at the restored community model

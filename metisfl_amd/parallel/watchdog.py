@@ -54,7 +54,12 @@ class RankWatchdog:
         return self
 
     def stop(self) -> None:
+        """Stop and join the heartbeat thread -- before the process group (and
+        its store) is destroyed: a store call racing the teardown aborts the
+        process (std::terminate)."""
         self._stop.set()
+        if self._thread.is_alive():
+            self._thread.join(timeout=5 * self.interval + 5)
 
     def pause(self) -> None:  # fault injection
         self._paused.set()

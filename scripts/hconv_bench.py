@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--eager", type=int, default=0,
+                    help="profiling: run only the halo conv, N eager calls per stage, no timing")
+    ap.add_argument("--stamps", action="store_true", help="in-kernel phase stamps of the halo conv")
     args = ap.parse_args()
     K.set_conv_products("bf16x3")
     dev = torch.device("cuda")
@@ -62,6 +65,29 @@ def main():
         def conv_only():
             K.conv_forward(y, w, out, shp, ws, stats, wp=wp, xp=yp)
 
+        if args.eager:
+            for _ in range(args.eager):
+                new()
+            torch.cuda.synchronize()
+            continue
+        if args.stamps:  # per-phase cycle stamps of every workgroup (median over workgroups)
+            st = torch.zeros(2048 * 16, dtype=torch.int64, device=dev)
+            for _ in range(3):
+                K.hconv_forward(z, wp, w, out, shp, bn, True, True, ws=ws, stats=stats, res=res, y=y, yp=yp,
+                                stamps=st)
+            torch.cuda.synchronize()
+            t = st.view(-1, 16)[:, :9].cpu().double()
+            t = t[t[:, 0] > 0]
+            base = t[:, 0].min()
+            rel = t - base
+            ph = ["coef", "fill0", "chunk0_mfma", "chunk0_store", "loop_rest", "epi_tile", "out_store",
+                  "stats"]
+            d = (t[:, 1:] - t[:, :-1]).median(0).values
+            print(json.dumps({"stage": f"{N}x{H}x{W}x{C}", "wg": int(t.shape[0]),
+                              "phase_cycles_median": {p: float(v) for p, v in zip(ph, d)},
+                              "start_spread": float(rel[:, 0].max()), "end_max": float(rel[:, 8].max())}),
+                  flush=True)
+            continue
         res_t = {}
         fns = (("bn+conv32", old), ("conv32", conv_only), ("hconv", new))
         graphs = {}

@@ -46,6 +46,9 @@ def _worker(rank, world, port, out_dir, mode):
     if mode == "straggler":
         cfg = FederationConfig(batch_size=4, local_epochs=4, evaluate_test=False, participation_ratio=2 / 3,
                                poll_steps=1, extra={"debug_slow_s": {"2": 0.4}})
+    elif mode == "deadline":  # every learner passes the deadline after one chunk
+        cfg = FederationConfig(batch_size=4, local_epochs=4, evaluate_test=False, round_deadline_s=1e-6,
+                               poll_steps=1, extra={"debug_slow_s": {"1": 0.2}})
     else:
         cfg = FederationConfig(batch_size=4, local_epochs=1, evaluate_test=False)
     fed = CollectiveFederation(comm, net, ds, cfg)
@@ -63,7 +66,7 @@ def _worker(rank, world, port, out_dir, mode):
         res["gi"] = rec.global_iteration
         res["weights"] = rec.weights
         res["updates"] = rec.num_local_updates
-    elif mode == "straggler":
+    elif mode in ("straggler", "deadline"):
         orig = fed.aggregate
 
         def spy(meta, _orig=orig):
@@ -119,3 +122,18 @@ def test_straggler_dropped_at_participation_ratio(tmp_path):
     l0 = np.load(tmp_path / "local_rank0.npy").astype(np.float64)
     l1 = np.load(tmp_path / "local_rank1.npy").astype(np.float64)
     assert np.allclose(comm[0], w[0] * l0 + w[1] * l1, rtol=1e-5, atol=1e-6)
+
+
+def test_deadline_with_no_finisher_keeps_a_community_model(tmp_path):
+    """when every learner passes the round deadline before finishing
+    its budget, the learners with the most local updates stand in as
+    participants instead of an all-zero weight vector zeroing the model."""
+    res = _run(tmp_path, "deadline", 3)
+    assert res[0]["participated"] == [0.0, 0.0, 0.0]
+    w, b = np.array(res[0]["weights"]), np.array(res[0]["batches"])
+    assert np.isclose(w.sum(), 1.0) and (w > 0).any()
+    assert np.all(w[b < b.max()] == 0.0)
+    comm = np.load(tmp_path / "community_rank0.npy").astype(np.float64)
+    assert np.abs(comm).sum() > 0
+    locs = [np.load(tmp_path / f"local_rank{r}.npy").astype(np.float64) for r in range(3)]
+    assert np.allclose(comm, sum(wi * l for wi, l in zip(w, locs)), rtol=1e-5, atol=1e-6)

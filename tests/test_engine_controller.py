@@ -54,7 +54,7 @@ def run_req(b):
 def test_join_dispatches_initial_task_and_validates():
     c = E.Controller(params())
     lid, tok, d = join(c, 1, 100)
-    assert lid == "learner-host:1" and len(tok) == 64
+    assert lid == "learner-host:1" and len(tok) == 32  # 128-bit token (32 hex digits)
     assert d["run_tasks"] == []  # no community model yet (controller.cc:394-397)
     c.replace_community_model(fed_model([1, 2, 3]))
     lid2, tok2, d2 = join(c, 2, 35)
@@ -291,3 +291,20 @@ def test_checkpoint_restore_resumes_the_federation():
     assert r.global_iteration() == 4 and len(d["run_tasks"]) == 2
     with pytest.raises(E.EngineStatusError):
         r.restore(b"garbage-not-a-checkpoint")
+
+
+def test_auth_tokens_are_128_bit_csprng_output():
+    """learner tokens are 128 bits from the ChaCha20 generator
+    keyed by getrandom (not a 32-bit seeded mt19937): 32 hex digits, all
+    distinct, and unbiased hex digits over many learners / controllers."""
+    toks = []
+    for k in range(4):
+        c = E.Controller(params())
+        toks += [join(c, p, 10)[1] for p in range(1, 257)]
+    assert all(len(t) == 32 and int(t, 16) >= 0 for t in toks)
+    assert len(set(toks)) == len(toks)
+    digits = np.array([int(ch, 16) for t in toks for ch in t])
+    counts = np.bincount(digits, minlength=16)
+    exp = len(digits) / 16
+    chi2 = float(((counts - exp) ** 2 / exp).sum())
+    assert chi2 < 45.0  # 15 dof: p ~ 1e-4
