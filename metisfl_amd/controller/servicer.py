@@ -317,13 +317,16 @@ class ControllerServicer(controller_pb2_grpc.ControllerServiceServicer):
     def LeaveFederation(self, request, context):
         if not request.learner_id or not request.auth_token:
             self._abort(context, 3, "Learner id and authentication token cannot be empty.")
+        dispatch = None
         try:
-            self.engine.remove_learner(request.learner_id, request.auth_token)
+            dispatch = self.engine.remove_learner(request.learner_id, request.auth_token)
         except E.EngineStatusError as e:
             self._abort(context, grpc.StatusCode.CANCELLED.value[0], e.args[1])
         self.dispatcher.forget(request.learner_id)
         MetisLogger.info("Learner %s left the federation.", request.learner_id)
         self.checkpoint(force=True)
+        if dispatch:  # the sync barrier was waiting only for the leaver
+            self.dispatcher.submit(dispatch)
         return controller_pb2.LeaveFederationResponse(ack=_ack(True))
 
     # -- task flow ---------------------------------------------------------------------------

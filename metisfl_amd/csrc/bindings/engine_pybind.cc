@@ -149,7 +149,15 @@ PYBIND11_MODULE(_engine, m) {
              return py::make_tuple(r.first, r.second, dispatch_to_py(d));
            },
            py::arg("server_entity"), py::arg("dataset_spec"), py::arg("schedule") = true)
-      .def("remove_learner", &Controller::remove_learner, py::call_guard<py::gil_scoped_release>())
+      .def("remove_learner",
+           [](Controller& c, const std::string& id, const std::string& tok) {
+             Dispatch d;
+             {
+               py::gil_scoped_release nogil;
+               d = c.remove_learner(id, tok);
+             }
+             return dispatch_to_py(d);
+           })
       .def("evict_learner",
            [](Controller& c, const std::string& id) {
              Dispatch d;

@@ -118,6 +118,7 @@ void hconv_forward(torch::Tensor z, torch::Tensor wp, torch::Tensor out, OptT ws
     a.stamps = reinterpret_cast<long long*>(stamps->data_ptr<int64_t>());
   }
   if (const char* e = getenv("MFL_HC_DBG")) a.dbg = atoi(e);  // timing ablations only
+  if (const char* e = getenv("MFL_HC_XCD")) a.xcd = atoi(e);
   mfl::hc::launch_hconv_fwd(a, cur_stream(out));
 }
 

@@ -1,5 +1,7 @@
 #include "common/model.h"
 
+#include <atomic>
+
 #include <algorithm>
 #include <stdexcept>
 
@@ -80,9 +82,11 @@ std::string serialize_variable(const VariableT& v) {
 }
 
 ModelT parse_model(std::string_view bytes) {
+  static std::atomic<uint64_t> next_uid{1};
   wire::WireMsg m(bytes);
   ModelT out;
   for (auto sv : m.strs(1)) out.vars.push_back(parse_variable(sv));
+  out.uid = next_uid.fetch_add(1, std::memory_order_relaxed);
   return out;
 }
 

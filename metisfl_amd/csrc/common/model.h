@@ -38,6 +38,10 @@ struct VariableT {
 
 struct ModelT {
   std::vector<VariableT> vars;
+  // process-unique identity, assigned when a model is parsed: a device-staged
+  // copy is matched by (uid, buffer addresses), so a later model that the
+  // allocator places at a freed model's addresses never aliases its slot
+  uint64_t uid = 0;
   size_t byte_size() const;
   bool empty() const { return vars.empty(); }
 };

@@ -216,13 +216,17 @@ std::pair<std::string, std::string> Controller::add_learner(const std::string& s
   return {id, rec.token};
 }
 
-void Controller::remove_learner(const std::string& id, const std::string& token) {
+Dispatch Controller::remove_learner(const std::string& id, const std::string& token) {
   std::lock_guard<std::mutex> g(mu_);
   validate(id, token);
   store_->erase({id});
   if (auto* d = DeviceAggregator::peek()) d->drop(id);
   learners_.erase(id);
   templates_.erase(id);
+  const auto active = active_ids_locked();
+  auto ready = scheduler_->poll(active);
+  if (ready.empty()) return Dispatch{};
+  return run_scheduled_locked(ready, active, global_iteration_);
 }
 
 void Controller::replace_community_model(const std::string& federated_model) {
@@ -310,6 +314,13 @@ Dispatch Controller::learner_completed_task(const std::string& id, const std::st
   tm.ms_per_batch = em.f32(7);
   const uint32_t idx = tm.global_iteration == 0 ? 0 : tm.global_iteration - 1;
   const int64_t t0 = now_ns();
+  // A duplicate completion (a client retry whose first reply was lost) of a
+  // task already recorded is acknowledged and ignored: (learner, global
+  // iteration) identifies a task under every protocol.
+  auto lm = local_meta_.find(id);
+  if (lm != local_meta_.end() && !lm->second.empty() && tm.global_iteration != 0 &&
+      lm->second.front().global_iteration == tm.global_iteration)
+    return Dispatch{};
   if (!metadata_.empty() && idx < metadata_.size()) {
     metadata_[idx].completed_by.push_back(id);
     metadata_[idx].train_received[id] = t0;

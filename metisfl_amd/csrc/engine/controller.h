@@ -120,7 +120,9 @@ class Controller {
   std::pair<std::string, std::string> add_learner(const std::string& server_entity,
                                                   const std::string& dataset_spec,
                                                   Dispatch* dispatch);
-  void remove_learner(const std::string& id, const std::string& token);
+  // LeaveFederation: a synchronous barrier that waited only for the leaver is
+  // released (the returned dispatch runs the round; the reference stalls)
+  Dispatch remove_learner(const std::string& id, const std::string& token);
   // failure detector: drop an unresponsive learner; may complete a pending
   // synchronous barrier (returns that round's dispatch)
   Dispatch evict_learner(const std::string& id);

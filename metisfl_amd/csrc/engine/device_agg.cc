@@ -88,11 +88,25 @@ struct Slot {
   hipEvent_t ready = nullptr;
   uint64_t stamp = 0;
   int pins = 0;  // > 0 while an aggregation reads it: never evicted
+  uint64_t uid = 0;  // ModelT::uid of the staged model
   bool matches(const ModelT& m) const {
-    if (m.vars.size() != ptrs.size()) return false;
+    if (m.uid != uid || m.vars.size() != ptrs.size()) return false;
     for (size_t i = 0; i < ptrs.size(); ++i)
       if (m.vars[i].t.value.data() != ptrs[i] || m.vars[i].t.value.size() != sizes[i]) return false;
     return true;
+  }
+};
+
+// Every entry point runs on the aggregation device and gives the caller's
+// thread its current device back (torch and the engine share one HIP runtime).
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    hip_check(hipSetDevice(dev), "hipSetDevice");
+  }
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
 
@@ -126,7 +140,7 @@ class Impl final : public DeviceAggregator {
 
   void stage(const std::string& learner, const ModelT& m, int keep) override {
     std::lock_guard<std::mutex> g(mu_);
-    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    DevGuard dg(dev_);
     if (m.vars.empty()) return;
     // a new model invalidates any slot that still names one of its buffers
     // (its previous owner was freed and the allocator reused the address)
@@ -157,21 +171,21 @@ class Impl final : public DeviceAggregator {
 
   void drop(const std::string& learner) override {
     std::lock_guard<std::mutex> g(mu_);
-    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    DevGuard dg(dev_);
     for (auto it = slots_.begin(); it != slots_.end();)
       it = (*it)->learner == learner ? release(it) : std::next(it);
   }
 
   void clear() override {
     std::lock_guard<std::mutex> g(mu_);
-    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    DevGuard dg(dev_);
     while (!slots_.empty()) release(slots_.begin());
   }
 
   bool weighted_sum(ModelT& out, const std::vector<const ModelT*>& models,
                     const std::vector<double>& weights) override {
     std::lock_guard<std::mutex> g(mu_);
-    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    DevGuard dg(dev_);
     const auto t0 = std::chrono::steady_clock::now();
     if (models.empty()) return false;
     const Layout lay = make_layout(*models.front());
@@ -202,7 +216,7 @@ class Impl final : public DeviceAggregator {
 
   int roll_init(const ModelT& m, double w) override {
     std::lock_guard<std::mutex> g(mu_);
-    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    DevGuard dg(dev_);
     Roll r;
     r.lay = make_layout(m);
     std::vector<Slot*> in, cold;
@@ -235,7 +249,7 @@ class Impl final : public DeviceAggregator {
 
   void roll_merge(int h, const ModelT& x, double w, int op) override {
     std::lock_guard<std::mutex> g(mu_);
-    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    DevGuard dg(dev_);
     Roll& r = roll_at(h);
     std::vector<Slot*> in, cold;
     if (!resolve({&x}, r.lay, in, cold))
@@ -248,7 +262,7 @@ class Impl final : public DeviceAggregator {
 
   void roll_fetch(int h, ModelT& out, double z, int op) override {
     std::lock_guard<std::mutex> g(mu_);
-    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    DevGuard dg(dev_);
     Roll& r = roll_at(h);
     char* o = scratch(r.lay.total);
     upload_tiles(r.lay);
@@ -258,7 +272,7 @@ class Impl final : public DeviceAggregator {
 
   void roll_free(int h) override {
     std::lock_guard<std::mutex> g(mu_);
-    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    DevGuard dg(dev_);
     auto it = rolls_.find(h);
     if (it == rolls_.end()) return;
     hipStreamSynchronize(compute_);
@@ -270,7 +284,7 @@ class Impl final : public DeviceAggregator {
                 const std::vector<uint64_t>& wqs, const std::vector<uint64_t>& q, uint32_t L,
                 uint32_t N, uint64_t total, uint64_t* out) override {
     std::lock_guard<std::mutex> g(mu_);
-    hip_check(hipSetDevice(dev_), "hipSetDevice");
+    DevGuard dg(dev_);
     const auto t0 = std::chrono::steady_clock::now();
     const uint64_t bytes = total * 8;
     // resident ciphertexts: a body that lies inside a staged variable is read in place
@@ -383,6 +397,7 @@ class Impl final : public DeviceAggregator {
     const auto t0 = std::chrono::steady_clock::now();
     auto s = std::make_unique<Slot>();
     s->learner = learner;
+    s->uid = m.uid;
     s->lay = make_layout(m);
     for (auto& v : m.vars) {
       s->ptrs.push_back(v.t.value.data());

@@ -56,6 +56,7 @@ struct FwdArgs {
   int* counters;       // split-K arrival tickets (zero between launches)
   long long* stamps = nullptr;  // profiling: per-workgroup phase timestamps [grid][16] (core clock)
   int dbg = 0;                  // ablation (timing only): 1 skip MFMAs, 2 skip fragment reads, 4 skip fills
+  int xcd = 1;                  // XCD-grouped tile order (MFL_HC_XCD=0: hardware order)
 };
 
 // Geometry supported by the halo kernels (3x3, stride 1, pad 1, square

@@ -71,9 +71,10 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-template <int TH_, int TW_, int IMGS_, int NT_, int WGM_, int PS_, int ROWB_, int IMGB_>
+template <int TH_, int TW_, int IMGS_, int NT_, int WGM_, int WGN_, int PS_, int ROWB_, int IMGB_>
 struct Cfg {
-  static constexpr int TH = TH_, TW = TW_, IMGS = IMGS_, NT = NT_, WGM = WGM_, WGN = 4 / WGM_;
+  static constexpr int TH = TH_, TW = TW_, IMGS = IMGS_, NT = NT_, WGM = WGM_, WGN = WGN_;
+  static constexpr int NTHR = 64 * WGM * WGN;  // 8 waves: two per SIMD hide each other's waits
   static constexpr int MT = IMGS * TH * TW;  // output pixels per workgroup
   static constexpr int WM = MT / WGM, WN = NT / WGN;
   static constexpr int TM = WM / 32, TN = WN / 32;  // 32x32 MFMA tiles per wave
@@ -86,12 +87,12 @@ struct Cfg {
   static constexpr int BPS = 80;
   static constexpr int B_BYTES = 9 * NT * BPS;
   static constexpr int STAGE = A_BYTES + B_BYTES + 64;  // + a dummy slot for padding items
-  static constexpr int NA = (PIX * 4 + 255) / 256;  // A float4 items per thread per chunk
-  static constexpr int NB = (NT * 36 + 255) / 256;  // B uint4 items per thread per chunk
+  static constexpr int NA = (PIX * 4 + NTHR - 1) / NTHR;  // A float4 items per thread per chunk
+  static constexpr int NB = (NT * 36 + NTHR - 1) / NTHR;  // B uint4 items per thread per chunk
   static constexpr int TST = NT + 4;                // epilogue tile row (floats)
-  static constexpr int EPI = MT * TST * 4 + 256 * 8 * 4 + 16;
+  static constexpr int EPI = MT * TST * 4 + NTHR * 8 * 4 + 16;
   static constexpr int LDS_MAIN = 2 * STAGE > EPI ? 2 * STAGE : EPI;
-  static_assert(WGM * WGN == 4 && TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "wave tiling");
+  static_assert((WGM * WGN == 4 || WGM * WGN == 8) && TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "wave tiling");
   static_assert(PS >= 64 && PS % 16 == 0 && ROWB % 16 == 0 && IMGB % 16 == 0, "16-B aligned fragments");
   static_assert(ROWB >= PW * PS && (IMGS == 1 || IMGB >= PH * ROWB), "patch pitches");
 };
@@ -157,36 +158,51 @@ __device__ __forceinline__ void stamp(const FwdArgs& a, int k) {
 // RK: residual kind of the input transform (0 none, 1 fp32 tensor, 2 BN of a
 // projection shortcut's pre-BN output).  Grid: x = spatial tiles, y = output
 // channel tiles, z = input-channel slices (split-K; kchunk channels each).
+// XCD-grouped workgroup order: the hardware deals workgroups round-robin
+// over the 8 XCDs (id % 8); logical tile L runs on group L / ceil(n / 8), so
+// consecutive spatial tiles of an image -- which share their halo rows --
+// read them through ONE XCD's L2 (bijective for any n, cdna_hip_programming
+// §5.5 T1).  All workgroups of a launch are co-resident (one per CU), so the
+// dispatch order itself does not matter.
+__device__ __forceinline__ int xcd_tile(int b, int n, bool on) {
+  if (!on || n < 16) return b;
+  const int q = n / 8, r = n % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 template <class K, int RK>
-__global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk) {
+__global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int nblk = gridDim.x * gridDim.y * gridDim.z;
+  const int lin = xcd_tile(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk, a.xcd);
+  const int bx = lin % gridDim.x, by = (lin / gridDim.x) % gridDim.y, bz = lin / (gridDim.x * gridDim.y);
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int li = lane & 31, lh = lane >> 5;
   const int wm = wave / K::WGN, wn = wave % K::WGN;
   const int C = a.C;
   const int txn = a.W / K::TW, tyn = a.H / K::TH;
-  int rem = blockIdx.x;
+  int rem = bx;
   const int tx = rem % txn;
   rem /= txn;
   const int ty = rem % tyn;
   const int img0 = (rem / tyn) * K::IMGS;
   const int y0 = ty * K::TH, x0 = tx * K::TW;
-  const int n0 = blockIdx.y * K::NT;
-  const int kbeg = blockIdx.z * kchunk;
+  const int n0 = by * K::NT;
+  const int kbeg = bz * kchunk;
   float* coef = reinterpret_cast<float*>(smem + K::LDS_MAIN);  // [4][kchunk]: sc, sh, sc2, sh2
   const FwdXform& X = a.x;
   stamp(a, 0);
 
   // ---- per-thread fill geometry (fixed over the chunks) ----
-  const int q = t & 3;  // float4 within the 16-channel chunk (256 % 4 == 0)
+  const int q = t & 3;  // float4 within the 16-channel chunk (NTHR % 4 == 0)
   uint32_t a_off[K::NA];  // byte offset of the item's pixel + 4q channels, kOOB outside
   int a_lds[K::NA];       // LDS byte offset of the item's hi half (-1: no item)
   bool a_own[K::NA];
-  const bool own_tile = blockIdx.y == 0 && (X.y != nullptr);
+  const bool own_tile = by == 0 && (X.y != nullptr);
 #pragma unroll
   for (int u = 0; u < K::NA; ++u) {
-    const int i = t + 256 * u;
+    const int i = t + K::NTHR * u;
     const int p = i >> 2;
     const int img = p / (K::PH * K::PW);
     const int r2 = p - img * (K::PH * K::PW);
@@ -202,7 +218,7 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
   int b_lds[K::NB];
 #pragma unroll
   for (int u = 0; u < K::NB; ++u) {
-    const int i = t + 256 * u;
+    const int i = t + K::NTHR * u;
     const int co = i / 36, r = i - co * 36;
     const int tap = r >> 2, bq = r & 3;
     const bool item = i < K::NT * 36;
@@ -239,31 +255,43 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
       bw[u] = __builtin_amdgcn_raw_buffer_load_b128(rsW, (int)off, 0, 0);
     }
   };
-  auto store = [&](auto kc, uint8_t* stage) {
-    constexpr int k = decltype(kc)::value;
+  // The fill of a chunk as NA + NB independent work units (unit u < NA: one
+  // float4 of the input patch -> BN / residual / ReLU -> bf16 hi + lo -> LDS
+  // and, for owner tiles, y / yp; unit NA + v: one packed weight float4 ->
+  // hi / lo -> LDS).  The units of chunk k+1 are spread over the taps of
+  // chunk k's MFMAs (their VALU / LDS writes issue under the matrix pipe).
+  struct Coef4 {
+    float4 sc, sh, s2, h2;
+  };
+  auto coef4 = [&](int k) {
     const int cl = k * K::CC + 4 * q;  // channel within the slice
-    const float4 sc = *reinterpret_cast<const float4*>(coef + cl);
-    const float4 sh = *reinterpret_cast<const float4*>(coef + kchunk + cl);
-    float4 s2 = sc, h2 = sh;
+    Coef4 c;
+    c.sc = *reinterpret_cast<const float4*>(coef + cl);
+    c.sh = *reinterpret_cast<const float4*>(coef + kchunk + cl);
+    c.s2 = c.sc;
+    c.h2 = c.sh;
     if constexpr (RK == 2) {
-      s2 = *reinterpret_cast<const float4*>(coef + 2 * kchunk + cl);
-      h2 = *reinterpret_cast<const float4*>(coef + 3 * kchunk + cl);
+      c.s2 = *reinterpret_cast<const float4*>(coef + 2 * kchunk + cl);
+      c.h2 = *reinterpret_cast<const float4*>(coef + 3 * kchunk + cl);
     }
-    const int gch = (kbeg + k * K::CC) * 4;  // byte offset of the chunk
-#pragma unroll
-    for (int u = 0; u < K::NA; ++u) {
+    return c;
+  };
+  auto store_unit = [&](auto kc, auto uc, uint8_t* stage, const Coef4& cf) {
+    constexpr int k = decltype(kc)::value, U = decltype(uc)::value;
+    if constexpr (U < K::NA) {
+      constexpr int u = U;
       const float4 zv = as_f4(az[k][u]);
-      float4 v = make_float4(fmaf(zv.x, sc.x, sh.x), fmaf(zv.y, sc.y, sh.y), fmaf(zv.z, sc.z, sh.z),
-                             fmaf(zv.w, sc.w, sh.w));
+      float4 v = make_float4(fmaf(zv.x, cf.sc.x, cf.sh.x), fmaf(zv.y, cf.sc.y, cf.sh.y),
+                             fmaf(zv.z, cf.sc.z, cf.sh.z), fmaf(zv.w, cf.sc.w, cf.sh.w));
       if constexpr (RK == 1) {
         const float4 r = as_f4(ar[k][u]);
         v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
       } else if constexpr (RK == 2) {
         const float4 r = as_f4(ar[k][u]);
-        v.x += fmaf(r.x, s2.x, h2.x);
-        v.y += fmaf(r.y, s2.y, h2.y);
-        v.z += fmaf(r.z, s2.z, h2.z);
-        v.w += fmaf(r.w, s2.w, h2.w);
+        v.x += fmaf(r.x, cf.s2.x, cf.h2.x);
+        v.y += fmaf(r.y, cf.s2.y, cf.h2.y);
+        v.z += fmaf(r.z, cf.s2.z, cf.h2.z);
+        v.w += fmaf(r.w, cf.s2.w, cf.h2.w);
       }
       const float lo = X.relu ? 0.f : -__builtin_inff();
       v.x = fmaxf(v.x, lo); v.y = fmaxf(v.y, lo); v.z = fmaxf(v.z, lo); v.w = fmaxf(v.w, lo);
@@ -276,16 +304,15 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
       *reinterpret_cast<uint2*>(d) = make_uint2(h01, h23);
       *reinterpret_cast<uint2*>(d + 32) = make_uint2(l01, l23);
       if (a_own[u]) {
-        const uint32_t go = a_off[u] + gch;  // pixel + chunk + 4q channels
+        const uint32_t go = a_off[u] + (uint32_t)((kbeg + k * K::CC) * 4);  // pixel + chunk + 4q channels
         *reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(X.y) + go) = v;
         if (X.yp)
           *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(X.yp) + go) =
               make_uint4((h01 << 16) | (l01 & 0xffffu), (h01 & 0xffff0000u) | (l01 >> 16),
                          (h23 << 16) | (l23 & 0xffffu), (h23 & 0xffff0000u) | (l23 >> 16));
       }
-    }
-#pragma unroll
-    for (int u = 0; u < K::NB; ++u) {
+    } else {
+      constexpr int u = U - K::NA;
       const u32x4 d = bw[u];
       const uint32_t h01 = __builtin_amdgcn_perm(d[1], d[0], 0x07060302u);
       const uint32_t h23 = __builtin_amdgcn_perm(d[3], d[2], 0x07060302u);
@@ -296,13 +323,18 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
       *reinterpret_cast<uint2*>(p + 32) = make_uint2(l01, l23);
     }
   };
+  constexpr int NU = K::NA + K::NB;
+  auto store = [&](auto kc, uint8_t* stage) {
+    const Coef4 cf = coef4(decltype(kc)::value);
+    static_for<NU>([&](auto uc) { store_unit(kc, uc, stage, cf); });
+  };
 
   static_for<K::NCH>([&](auto kc) { load_a(kc); });
   load_b(0);
   // ---- coefficients of this slice's input channels ----
   {
-    const bool publish = X.train && blockIdx.x == 0 && blockIdx.y == 0;
-    for (int c = t; c < kchunk; c += 256) {
+    const bool publish = X.train && bx == 0 && by == 0;
+    for (int c = t; c < kchunk; c += K::NTHR) {
       float sc = 1.f, sh = 0.f;
       if (X.has_bn) bn_coef(X.bn, C, kbeg + c, X.M, X.train, publish, sc, sh);
       coef[c] = sc;
@@ -340,7 +372,7 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
   // 9 taps, fragments read two taps ahead (three register sets): the MFMAs
   // of tap t wait only for the reads issued before tap t-1's; sched_barrier
   // keeps hipcc from sinking the reads back behind the MFMAs
-  auto compute = [&](const uint8_t* st) {
+  auto compute = [&](const uint8_t* st, auto&& side) {
     bf16x8 ah[3][K::TM], al[3][K::TM], bh[3][K::TN], bl[3][K::TN];
     auto rd = [&](auto tapc) {
       constexpr int TAP = decltype(tapc)::value, S = TAP % 3;
@@ -375,6 +407,7 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
             acc[i][j] = mfma_bf16x16(ah[S][i], bh[S][j], acc[i][j]);
           }
       }
+      side(tapc);  // fill units of the next chunk, behind this tap's MFMAs
       __builtin_amdgcn_sched_barrier(0);
     });
   };
@@ -395,12 +428,21 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
     constexpr int k = decltype(kc)::value;
     uint8_t* cur = smem + (k & 1) * K::STAGE;
     uint8_t* nxt = smem + ((k + 1) & 1) * K::STAGE;
-    compute(cur);
-    if constexpr (k == 0) stamp(a, 3);
     if constexpr (k + 1 < K::NCH) {
-      store(IC<k + 1>{}, nxt);
+      const Coef4 cf = coef4(k + 1);
+      // unit u of chunk k+1 rides behind tap (u * 9 / NU)
+      compute(cur, [&](auto tapc) {
+        constexpr int TAP = decltype(tapc)::value;
+        static_for<NU>([&](auto uc) {
+          constexpr int U = decltype(uc)::value;
+          if constexpr (U * 9 / NU == TAP) store_unit(IC<k + 1>{}, uc, nxt, cf);
+        });
+      });
       if constexpr (k + 2 < K::NCH) load_b(k + 2);
+    } else {
+      compute(cur, [](auto) {});
     }
+    if constexpr (k == 0) stamp(a, 3);
     bar();
     if constexpr (k == 0) stamp(a, 4);
   });
@@ -422,19 +464,19 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
   __syncthreads();
   const int splits = gridDim.z;
   constexpr int C4 = K::NT / 4;
-  constexpr int F = K::MT * K::NT / 1024;  // float4 per thread
-  static_assert(K::MT * K::NT % 1024 == 0, "epilogue vectors");
+  constexpr int F = K::MT * K::NT / (4 * K::NTHR);  // float4 per thread
+  static_assert(K::MT * K::NT % (4 * K::NTHR) == 0, "epilogue vectors");
   if (splits > 1) {
     // in-launch split-K (conv32.hip): write-through slabs + arrival ticket,
     // the last arriver sums the slices in slice order (deterministic)
-    const int tile_id = blockIdx.y * gridDim.x + blockIdx.x;
+    const int tile_id = by * gridDim.x + bx;
     const int ntiles = gridDim.x * gridDim.y;
     const int64_t zstride = (int64_t)ntiles * K::MT * K::NT * 4;
     const auto rsS = make_rsrc(a.slab + (int64_t)tile_id * (K::MT * K::NT), 0x7FFFFFF0u);
-    const uint32_t zoff = (uint32_t)(blockIdx.z * zstride);
+    const uint32_t zoff = (uint32_t)(bz * zstride);
 #pragma unroll
     for (int u = 0; u < F; ++u) {
-      const int f = t + 256 * u;
+      const int f = t + K::NTHR * u;
       const float4 v = *reinterpret_cast<const float4*>(tile + (f / C4) * K::TST + (f % C4) * 4);
       __builtin_amdgcn_raw_buffer_store_b128(
           u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)}, rsS,
@@ -442,7 +484,7 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    int* flag = reinterpret_cast<int*>(red + 256 * 8);
+    int* flag = reinterpret_cast<int*>(red + K::NTHR * 8);
     if (t == 0) {
       const int prev = __hip_atomic_fetch_add(&a.counters[tile_id], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = prev == splits - 1;
@@ -457,9 +499,9 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
     for (int z = 0; z < splits; ++z) {
 #pragma unroll
       for (int u = 0; u < F; ++u) {
-        const int f = t + 256 * u;
+        const int f = t + K::NTHR * u;
         float4 r;
-        if (z == (int)blockIdx.z) {
+        if (z == bz) {
           r = *reinterpret_cast<const float4*>(tile + (f / C4) * K::TST + (f % C4) * 4);
         } else {
           r = as_f4(__builtin_amdgcn_raw_buffer_load_b128(rsS, (int)(z * zstride + f * 16), 0, 16));
@@ -470,14 +512,14 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < F; ++u) {
-      const int f = t + 256 * u;
+      const int f = t + K::NTHR * u;
       *reinterpret_cast<float4*>(tile + (f / C4) * K::TST + (f % C4) * 4) = sum[u];
     }
     __syncthreads();
   }
   stamp(a, 6);
   // output rows: float4 per thread per pass
-  constexpr int RPP = 256 / C4;
+  constexpr int RPP = K::NTHR / C4;
   const int cg = t % C4, r0 = t / C4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f), sq = s;
   for (int rl = r0; rl < K::MT; rl += RPP) {
@@ -493,7 +535,7 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
   }
   stamp(a, 7);
   if (!a.stats) return;
-  double* stats = a.stats + (int64_t)((blockIdx.x + blockIdx.y * gridDim.x) % a.reps) * 2 * a.Co;
+  double* stats = a.stats + (int64_t)((bx + by * gridDim.x) % a.reps) * 2 * a.Co;
   reinterpret_cast<float4*>(red)[2 * t] = s;
   reinterpret_cast<float4*>(red)[2 * t + 1] = sq;
   __syncthreads();
@@ -511,15 +553,16 @@ __global__ __launch_bounds__(256, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk
 }
 
 // Stage configurations for the CIFAR ResNet-18 shapes at any batch (3x3, s1):
-// S1 32x32x64: 8x16-pixel tiles x 64 channels, waves 2x2 (64x32 each)
-// S2 16x16x128: 8x16 x 32 channels, waves 4x1, 2 input-channel slices
-// S3 8x8x256: 2 images x 64 channels, waves 2x2, 4 input-channel slices
-// S4 4x4x512: 8 images x 64 channels, waves 2x2, 8 slices
+// Every stage: 128 output pixels x 64 output channels per workgroup, 8 waves
+// as 4 (pixels) x 2 (channels) of 32x32 MFMA tiles, 64 input channels per
+// workgroup (split-K over the rest):
+// S1 32x32x64: 8x16-pixel tiles; S2 16x16x128: 8x16, 2 slices;
+// S3 8x8x256: 2 images, 4 slices; S4 4x4x512: 8 images, 8 slices
 // (pitches from scripts/hconv_banks.py: conflict-free A reads for every tap)
-using S1 = Cfg<8, 16, 1, 64, 2, 80, 1536, 15360>;
-using S2 = Cfg<8, 16, 1, 32, 4, 80, 1536, 15360>;
-using S3 = Cfg<8, 8, 2, 64, 2, 64, 784, 7936>;
-using S4 = Cfg<4, 4, 8, 64, 2, 64, 528, 3328>;
+using S1 = Cfg<8, 16, 1, 64, 4, 2, 80, 1536, 15360>;
+using S2 = Cfg<8, 16, 1, 64, 4, 2, 80, 1536, 15360>;
+using S3 = Cfg<8, 8, 2, 64, 4, 2, 64, 784, 7936>;
+using S4 = Cfg<4, 4, 8, 64, 4, 2, 64, 528, 3328>;
 
 struct Plan {
   int stage;  // 0: unsupported
@@ -542,7 +585,7 @@ Plan plan_fwd(int N, int H, int W, int C, int Co) {
     p.nt = nt;
   };
   if (H == 32 && C == 64) fill(1, 8, 16, 1, 64, 1);
-  else if (H == 16 && C == 128) fill(2, 8, 16, 1, 32, 2);
+  else if (H == 16 && C == 128) fill(2, 8, 16, 1, 64, 2);
   else if (H == 8 && C == 256) fill(3, 8, 8, 2, 64, 4);
   else if (H == 4 && C == 512) fill(4, 4, 4, 8, 64, 8);
   if (p.stage && p.grid.x * p.grid.y > 1024) p.stage = 0;  // counter block
@@ -559,7 +602,7 @@ void go(const FwdArgs& a, const Plan& p, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     init = true;
   }
-  hconv_fwd_kernel<K, RK><<<p.grid, 256, lds, s>>>(a, p.kchunk);
+  hconv_fwd_kernel<K, RK><<<p.grid, K::NTHR, lds, s>>>(a, p.kchunk);
 }
 
 template <class K>

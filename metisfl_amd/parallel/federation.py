@@ -518,8 +518,24 @@ class CollectiveFederation:
         lost rank renumbers the survivors); default: the same rank."""
         with open(os.path.join(path, "federation.json")) as f:
             meta = json.load(f)
-        with open(os.path.join(path, self.COMMUNITY_FILE), "rb") as f:
-            self.load_community_model(f.read())
+        pb = os.path.join(path, self.COMMUNITY_FILE)
+        legacy = os.path.join(path, "community.pt")
+        if os.path.exists(pb):
+            with open(pb, "rb") as f:
+                self.load_community_model(f.read())
+        elif os.path.exists(legacy):
+            # round-1 checkpoint layout: the flat fp32 community model as a
+            # plain tensor (loaded without unpickling code)
+            flat = torch.load(legacy, weights_only=True)
+            st = self.net.state
+            if flat.numel() != st.model32.numel():
+                raise RuntimeError(f"old-format checkpoint {legacy}: {flat.numel()} values, model has "
+                                   f"{st.model32.numel()}")
+            st.model32.copy_(flat.to(st.model32.device, st.model32.dtype).view_as(st.model32))
+            st.refresh_bf16()
+            st.set_anchor()
+        else:
+            raise FileNotFoundError(f"no community model in checkpoint {path} ({self.COMMUNITY_FILE})")
         st = self.net.state
         dev = st.model32.device
         same_world = meta["world"] == self.world

@@ -78,7 +78,9 @@ class GRPCControllerClient(GRPCServerClient):
         def _req(t=None):
             return self._stub.MarkTaskCompleted(
                 C.construct_mark_task_completed_request_pb(learner_id, auth_token, completed_task_pb), timeout=t)
-        return self._call(_req, request_retries, request_timeout, block)
+        # not idempotent: retried on transport failures only (the controller
+        # ignores a duplicate completion of a task it already recorded)
+        return self._schedule(_req, request_retries, request_timeout, block, retry_codes=self.TRANSIENT_CODES)
 
     def get_community_model_evaluation_lineage(self, num_backtracks, request_retries=1, request_timeout=None,
                                                block=True):

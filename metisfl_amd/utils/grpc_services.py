@@ -73,7 +73,12 @@ class GRPCServerClient:
                    grpc.StatusCode.PERMISSION_DENIED, grpc.StatusCode.UNAUTHENTICATED,
                    grpc.StatusCode.UNIMPLEMENTED)
 
-    def request_with_timeout(self, request_fn, request_timeout, request_retries):
+    # a non-idempotent request (MarkTaskCompleted: the controller inserts the
+    # model before it can fail) is retried only when it cannot have arrived,
+    # or arrived and timed out (the controller drops a duplicate completion)
+    TRANSIENT_CODES = (grpc.StatusCode.UNAVAILABLE, grpc.StatusCode.DEADLINE_EXCEEDED)
+
+    def request_with_timeout(self, request_fn, request_timeout, request_retries, retry_codes=None):
         response = None
         for attempt in range(max(1, request_retries)):
             if self._closing.is_set():
@@ -85,13 +90,16 @@ class GRPCServerClient:
                                  request_retries)
                 if err.code() in self.FINAL_CODES:
                     break
+                if retry_codes is not None and err.code() not in retry_codes:
+                    break
                 if err.code() == grpc.StatusCode.UNAVAILABLE and attempt + 1 < request_retries:
                     self._closing.wait(self.retry_sleep_s)  # shutdown() cuts the back-off short
         return response
 
-    def _schedule(self, request_fn, request_retries, request_timeout, block):
+    def _schedule(self, request_fn, request_retries, request_timeout, block, retry_codes=None):
         if request_retries > 1:
-            fut = self.executor.submit(self.request_with_timeout, request_fn, request_timeout, request_retries)
+            fut = self.executor.submit(self.request_with_timeout, request_fn, request_timeout, request_retries,
+                                       retry_codes)
         else:
             fut = self.executor.submit(request_fn, request_timeout)
         if block:

@@ -196,8 +196,7 @@ def test_learner_leaving_does_not_stall_sync_barrier():
     ls = _three_learners(c)
     c.learner_completed_task(ls[0][0], ls[0][1], completed([1, 1, 1], 1))
     c.learner_completed_task(ls[1][0], ls[1][1], completed([1, 1, 1], 1))
-    c.remove_learner(ls[2][0], ls[2][1])
-    d = c.learner_completed_task(ls[0][0], ls[0][1], completed([1, 1, 1], 1))
+    d = c.remove_learner(ls[2][0], ls[2][1])  # the barrier waited only for the leaver
     assert len(d["run_tasks"]) == 2
 
 
@@ -308,3 +307,58 @@ def test_auth_tokens_are_128_bit_csprng_output():
     exp = len(digits) / 16
     chi2 = float(((counts - exp) ** 2 / exp).sum())
     assert chi2 < 45.0  # 15 dof: p ~ 1e-4
+
+
+def test_duplicate_completion_is_ignored():
+    """a MarkTaskCompleted retried after its reply was lost does not
+    insert the model twice or count the learner twice at the barrier."""
+    c = E.Controller(params())
+    ls = _three_learners(c)
+    lid, tok = ls[0]
+    d1 = c.learner_completed_task(lid, tok, completed([1, 1, 1], 1))
+    d2 = c.learner_completed_task(lid, tok, completed([1, 1, 1], 1))  # the retry
+    assert d1["run_tasks"] == [] and d2["run_tasks"] == []
+    lt = controller_pb2.GetLocalTaskLineageResponse()
+    lt.ParseFromString(c.local_task_lineage(0, [lid]))
+    assert len(lt.learner_task[lid].task_metadata) == 1
+    # the barrier still needs the other two learners
+    assert c.learner_completed_task(ls[1][0], ls[1][1], completed([2, 2, 2], 1))["run_tasks"] == []
+    d = c.learner_completed_task(ls[2][0], ls[2][1], completed([4, 4, 4], 1))
+    assert len(d["run_tasks"]) == 3
+    resp = controller_pb2.GetRuntimeMetadataLineageResponse()
+    resp.ParseFromString(c.runtime_metadata_lineage(0))
+    assert sorted(resp.metadata[0].completed_by_learner_id) == sorted(l for l, _ in ls)
+
+
+def test_completion_retries_only_on_transient_codes():
+    import grpc
+
+    from metisfl_amd.utils.grpc_services import GRPCServerClient
+
+    class Err(grpc.RpcError):
+        def __init__(self, code):
+            self._c = code
+
+        def code(self):
+            return self._c
+
+    class Cli(GRPCServerClient):
+        retry_sleep_s = 0.0
+
+        def __init__(self):
+            import threading
+            self._closing = threading.Event()
+
+    calls = []
+
+    def fn(code):
+        def f(t):
+            calls.append(code)
+            raise Err(code)
+        return f
+    cli = Cli()
+    cli.request_with_timeout(fn(grpc.StatusCode.INTERNAL), None, 5, GRPCServerClient.TRANSIENT_CODES)
+    assert len(calls) == 1  # a server-side failure may have inserted the model: no retry
+    calls.clear()
+    cli.request_with_timeout(fn(grpc.StatusCode.UNAVAILABLE), None, 5, GRPCServerClient.TRANSIENT_CODES)
+    assert len(calls) == 5
