@@ -68,16 +68,17 @@ def main() -> int:
     ap.add_argument("--conv-products", choices=("exact", "bf16x3"), default=None,
                     help="fp32 convolution products: exact fp32 MFMA, or bf16x3 split products "
                          "with fp32 storage/accumulation (default: ResNet18's default)")
+    ap.add_argument("--exact-updates", type=int, default=300,
+                    help="fp32 bf16x3 runs: also time this many local updates with exact fp32 products "
+                         "(0: skip); reported as conv_products_exact")
     ap.add_argument("--width-mult", type=float, default=1.0, help=argparse.SUPPRESS)  # CPU plumbing tests only
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
 
-    env_world = os.environ.get("WORLD_SIZE")
-    if env_world is None and args.gpus > 1:
-        return _spawn_ranks(args.gpus)
-    if env_world is not None and int(env_world) != args.gpus:
-        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
-        return 2
+    from metisfl_amd.utils.launch import ensure_world
+    rc = ensure_world(args.gpus, __file__)
+    if rc is not None:
+        return rc
 
     import torch
 
@@ -109,6 +110,7 @@ def main() -> int:
     del xtr, xte
     cfg = FederationConfig(protocol="synchronous", batch_size=args.batch,
                            local_epochs=args.local_epochs, evaluate_test=not args.no_eval,
+                           evaluate_community=not args.no_eval,
                            secure_aggregation=args.secure_aggregation)
     engine = None
     if comm.rank == 0:  # the native controller keeps the round bookkeeping
@@ -195,6 +197,11 @@ def main() -> int:
                        if args.secure_aggregation and timed else None),
         "samples_per_s": (args.train_size * args.local_epochs) / (round_ms / 1e3) if round_ms else 0.0,
     }
+    out["community_eval_ms_mean"] = sum(r.community_eval_ms for r in timed) / max(1, len(timed))
+    out["aggregation_weights"] = [float(w) for w in timed[-1].weights] if timed and timed[-1].weights is not None else None
+    out["community_model"] = _community_digests(comm, net)
+    if args.dtype == "fp32" and net.conv_products == "bf16x3" and args.exact_updates > 0:
+        out["conv_products_exact"] = _exact_pass(args, comm, train_ds, opt, sync, out, updates)
     if comm.rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -205,20 +212,49 @@ def main() -> int:
     return 0
 
 
-def _spawn_ranks(n: int) -> int:
-    """``--gpus N`` without a launcher: start N rank processes with
-    torch.distributed.run (before this process touches any GPU) and relay
-    their output; rank 0 prints the JSON line."""
-    import socket
-    import subprocess
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.run(cmd, env=env).returncode
+def _community_digests(comm, net) -> dict:
+    """SHA-256 of every rank's resident community model (after the last
+    all-reduce the replicas must be bitwise identical)."""
+    import hashlib
+
+    import torch
+    h = hashlib.sha256(net.state.model32.detach().cpu().numpy().tobytes()).digest()
+    words = [int.from_bytes(h[4 * i:4 * i + 4], "little") for i in range(4)]  # 128 bits, exact in fp64
+    rows = comm.all_gather_rows(torch.tensor(words, dtype=torch.float64, device=comm.device)).cpu().numpy()
+    digests = ["".join(f"{int(w):08x}" for w in r) for r in rows]
+    return {"sha256_128": digests, "identical": len(set(digests)) == 1}
+
+
+def _exact_pass(args, comm, train_ds, opt, sync, out, updates) -> dict:
+    """The strict-IEEE alternative, timed after the headline rounds: a fresh
+    ResNet-18 whose convolutions multiply on the exact fp32 MFMA
+    (v_mfma_f32_32x32x2_f32) runs ``--exact-updates`` local updates (after
+    20 untimed ones that capture its step graph); the round-time estimate
+    swaps the measured bf16x3 training time for the exact one and keeps the
+    round's measured evaluation / aggregation time."""
+    import torch
+    from metisfl_amd.models.resnet import ResNet18
+    net = ResNet18(batch_size=args.batch, device=comm.device, optimizer=opt, seed=7, dtype="fp32",
+                   width_mult=args.width_mult, conv_products="exact")
+    k = args.exact_updates
+    net.train_steps(train_ds, 20, step_offset=0)
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    net.train_steps(train_ds, k, step_offset=20)
+    sync()
+    el = comm.all_max(time.perf_counter() - t0)
+    exact_upd = el * 1e3 / k
+    fast_upd = out["train_ms_mean"] / max(1, updates)
+    from metisfl_amd.ops.nn import set_conv_products
+    set_conv_products("bf16x3")
+    del net
+    if comm.device.type == "cuda":
+        torch.cuda.empty_cache()
+    return {"updates_timed": k, "ms_per_update": exact_upd, "bf16x3_ms_per_update": fast_upd,
+            "round_ms_est": out["round_ms"] + (exact_upd - fast_upd) * updates,
+            "method": "measured per-update time x local updates per round + the measured "
+                      "non-training part of the bf16x3 round"}
 
 
 if __name__ == "__main__":

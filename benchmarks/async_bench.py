@@ -44,8 +44,16 @@ def main() -> int:
     ap.add_argument("--staleness", default="polynomial")
     ap.add_argument("--poll-every", type=int, default=32)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--width-mult", type=float, default=1.0, help=argparse.SUPPRESS)  # CPU plumbing tests only
+    ap.add_argument("--delays-ms", default="",
+                    help="comma list: per-rank sleep after each task (uneven learner speeds; contention tests)")
     args = ap.parse_args()
+    from metisfl_amd.utils.launch import ensure_world
+    rc = ensure_world(args.gpus, __file__)
+    if rc is not None:
+        return rc
 
+    import numpy as np
     import torch
 
     from metisfl_amd.models.resnet import ResNet18
@@ -62,17 +70,23 @@ def main() -> int:
     g.manual_seed(2000 + comm.rank)
     x = torch.randn((n_train, 32, 32, 3), generator=g, device=dev)
     y = torch.randint(0, 10, (n_train,), generator=g, device=dev)
-    net = ResNet18(batch_size=args.batch, device=dev, seed=7,
+    net = ResNet18(batch_size=args.batch, device=dev, seed=7, width_mult=args.width_mult,
                    optimizer=OptimizerSpec("momentum_sgd", 0.005, momentum=0.75))
     ds = net.make_dataset(x, y, seed=comm.rank)
     del x
     cfg = FederationConfig(protocol="asynchronous", batch_size=args.batch, local_epochs=args.local_epochs,
                            evaluate_test=False, staleness=args.staleness)
 
+    delays = [float(v) for v in args.delays_ms.split(",") if v.strip()]
+    delay = delays[comm.rank % len(delays)] / 1e3 if delays else 0.0
+
+    fed_last = []
+
     def run(tasks):
         fed = AsyncCollectiveFederation(comm, net, ds, cfg, tasks_per_learner=tasks,
                                         poll_every=args.poll_every, broadcast_initial=False)
-        return fed.run()
+        fed_last[:] = [fed]
+        return fed.run(debug_delay_s=delay)
 
     if args.warmup:
         run(args.warmup)
@@ -91,7 +105,7 @@ def main() -> int:
             "metric": "async FedRec community updates/s (whole job), CIFAR-10 ResNet-18",
             "value": nup / elapsed, "unit": "updates/s", "n_gpus": n, "steps": args.tasks,
             "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / max(1, args.tasks),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32" if net.compute_dtype == torch.float32 else "bf16",
             "data": "synthetic (CIFAR-10 shapes, IID shards), random-init ResNet-18",
             "config": {"model": "resnet18-cifar", "learners": n, "per_learner_batch": args.batch,
                        "local_epochs_per_task": args.local_epochs, "protocol": "asynchronous",
@@ -100,6 +114,10 @@ def main() -> int:
             "fedrec_update_ms_mean": sum(u.aggregation_ms for u in ups) / max(1, nup),
             "staleness_mean": sum(u.staleness for u in ups) / max(1, nup),
             "staleness_max": max((u.staleness for u in ups), default=0),
+            "updates_per_learner": [sum(1 for u in ups if u.learner == r) for r in range(n)],
+            "community_model_matches_host": bool(np.allclose(fed_last[0].community_reference(),
+                                                             fed_last[0]._community().double().cpu().numpy(),
+                                                             rtol=1e-5, atol=1e-6)) if n > 1 else None,
         }
         line = json.dumps(out)
         print(line, flush=True)

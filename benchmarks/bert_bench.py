@@ -36,6 +36,10 @@ def main() -> int:
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
+    from metisfl_amd.utils.launch import ensure_world
+    rc = ensure_world(args.gpus, __file__)
+    if rc is not None:
+        return rc
 
     import torch
 

@@ -122,9 +122,93 @@ void hconv_forward(torch::Tensor z, torch::Tensor wp, torch::Tensor out, OptT ws
   mfl::hc::launch_hconv_fwd(a, cur_stream(out));
 }
 
+// dx (+)= conv3x3^T(dz, W), dz = BN_bwd(dy [* (ymask > 0)]) applied in the
+// operand fill from (acc: complete sums of g and g * xhat [reps][2][C],
+// gamma, mean, invstd); dgamma / dbeta published.  Owner tiles write dz's
+// packed split (dzp, the wgrad operand) and g (dres).  bnb_*: the consumer
+// BN-backward reductions of dx in the epilogue.
+void hconv_dgrad(torch::Tensor dy, OptT ymask, torch::Tensor z, torch::Tensor wp, torch::Tensor out, OptT ws,
+                 int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co, torch::Tensor acc, torch::Tensor gamma,
+                 torch::Tensor mean, torch::Tensor invstd, OptT dgamma, OptT dbeta, OptT dres, OptT dzp,
+                 bool accumulate, OptT bnb_z, OptT bnb_y, OptT bnb_mean, OptT bnb_invstd, OptT bnb_acc,
+                 OptT stamps) {
+  const int64_t ws_need = mfl::hc::hconv_fwd_workspace((int)N, (int)H, (int)W, (int)C, (int)Co);
+  TORCH_CHECK(ws_need >= 0, "halo dgrad: unsupported geometry N=", N, " H=", H, " W=", W, " C=", C, " Co=", Co);
+  const int64_t nin = N * H * W * C, nout = N * H * W * Co;
+  TORCH_CHECK(nin * 4 < (1LL << 31) && nout * 4 < (1LL << 31), "activation too large for 32-bit byte offsets");
+  check(dy, torch::kFloat32, nin, "dy");
+  check(z, torch::kFloat32, nin, "z");
+  check(wp, torch::kInt32, C * 9 * Co, "packed weights");
+  check(out, torch::kFloat32, nout, "out");
+  mfl::hc::DgArgs a{};
+  a.N = (int)N; a.H = (int)H; a.W = (int)W; a.C = (int)C; a.Co = (int)Co;
+  a.x.dy = dy.data_ptr<float>();
+  a.x.z = z.data_ptr<float>();
+  if (has(ymask)) {
+    check(*ymask, torch::kFloat32, nin, "ymask");
+    a.x.ymask = ymask->data_ptr<float>();
+  }
+  check(acc, torch::kFloat64, -1, "bn acc");
+  TORCH_CHECK(acc.numel() % (2 * C) == 0, "bn acc holds [reps][2][C]");
+  a.x.bn.acc = acc.data_ptr<double>();
+  a.x.bn.reps = (int)(acc.numel() / (2 * C));
+  TORCH_CHECK(a.x.bn.reps >= 1 && a.x.bn.reps <= 8, "1..8 BN accumulator replicas");
+  for (auto* p : {&gamma, &mean, &invstd}) check(*p, torch::kFloat32, C, "bn parameter");
+  a.x.bn.gamma = gamma.data_ptr<float>();
+  a.x.bn.mean = mean.data_ptr<float>();
+  a.x.bn.invstd = invstd.data_ptr<float>();
+  if (has(dgamma)) { check(*dgamma, torch::kFloat32, C, "dgamma"); a.x.bn.dgamma = dgamma->data_ptr<float>(); }
+  if (has(dbeta)) { check(*dbeta, torch::kFloat32, C, "dbeta"); a.x.bn.dbeta = dbeta->data_ptr<float>(); }
+  a.x.M = (int)(N * H * W);
+  if (has(dres)) {
+    check(*dres, torch::kFloat32, nin, "dres");
+    a.x.dres = dres->data_ptr<float>();
+  }
+  if (has(dzp)) {
+    check(*dzp, torch::kInt32, nin, "dzp");
+    a.x.dzp = reinterpret_cast<uint32_t*>(dzp->data_ptr());
+  }
+  a.wp = reinterpret_cast<const uint32_t*>(wp.data_ptr());
+  a.out = out.data_ptr<float>();
+  a.accumulate = accumulate ? 1 : 0;
+  if (has(bnb_acc)) {
+    TORCH_CHECK(has(bnb_z) && has(bnb_mean) && has(bnb_invstd), "consumer BN reductions need z, mean, invstd");
+    check(*bnb_z, torch::kFloat32, nout, "bnb z");
+    if (has(bnb_y)) {
+      check(*bnb_y, torch::kFloat32, nout, "bnb y");
+      a.bnb.y = bnb_y->data_ptr<float>();
+    }
+    check(*bnb_mean, torch::kFloat32, Co, "bnb mean");
+    check(*bnb_invstd, torch::kFloat32, Co, "bnb invstd");
+    check(*bnb_acc, torch::kFloat64, -1, "bnb acc");
+    TORCH_CHECK(bnb_acc->numel() % (2 * Co) == 0, "bnb acc holds [reps][2][Co]");
+    a.bnb.z = bnb_z->data_ptr<float>();
+    a.bnb.mean = bnb_mean->data_ptr<float>();
+    a.bnb.invstd = bnb_invstd->data_ptr<float>();
+    a.bnb.acc = bnb_acc->data_ptr<double>();
+    a.bnb.reps = (int)(bnb_acc->numel() / (2 * Co));
+  }
+  if (ws_need > 0) {
+    TORCH_CHECK(has(ws), "split-K workspace required");
+    check(*ws, torch::kFloat32, -1, "workspace");
+    TORCH_CHECK(ws->numel() >= ws_need, "workspace too small: ", ws->numel(), " < ", ws_need);
+    a.counters = reinterpret_cast<int*>(ws->data_ptr<float>());
+    a.slab = ws->data_ptr<float>() + 1024;
+  }
+  if (has(stamps)) {
+    check(*stamps, torch::kInt64, -1, "stamps");
+    TORCH_CHECK(stamps->numel() >= 16 * 2048, "stamps: at least 16 x 2048 slots");
+    a.stamps = reinterpret_cast<long long*>(stamps->data_ptr<int64_t>());
+  }
+  if (const char* e = getenv("MFL_HC_DBG")) a.dbg = atoi(e);
+  if (const char* e = getenv("MFL_HC_XCD")) a.xcd = atoi(e);
+  mfl::hc::launch_hconv_dgrad(a, cur_stream(out));
+}
+
 }  // namespace
 
 void register_hconv(pybind11::module& m) {
   m.def("hconv_fwd_workspace", &hconv_fwd_workspace);
   m.def("hconv_forward", &hconv_forward);
+  m.def("hconv_dgrad", &hconv_dgrad);
 }

@@ -141,8 +141,9 @@ __device__ __forceinline__ void bn32_apply_body(const BnFwdArgs32& a, int64_t nv
       a.invstd[c] = (float)isd;
       if (a.run_mean) {
         const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
-        a.run_mean[c] = (1.f - a.momentum) * a.run_mean[c] + a.momentum * (float)mu;
-        a.run_var[c] = (1.f - a.momentum) * a.run_var[c] + a.momentum * (float)unb;
+        // explicit fma: the halo conv's fill publishes the same bits (hconv.hip)
+        a.run_mean[c] = fmaf(1.f - a.momentum, a.run_mean[c], a.momentum * (float)mu);
+        a.run_var[c] = fmaf(1.f - a.momentum, a.run_var[c], a.momentum * (float)unb);
       }
     }
   }
@@ -335,10 +336,10 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
       }
     }
     float4 o;
-    o.x = k1.x * (g.x - mg.x - ((xc.x - mu.x) * is.x) * mx.x);
-    o.y = k1.y * (g.y - mg.y - ((xc.y - mu.y) * is.y) * mx.y);
-    o.z = k1.z * (g.z - mg.z - ((xc.z - mu.z) * is.z) * mx.z);
-    o.w = k1.w * (g.w - mg.w - ((xc.w - mu.w) * is.w) * mx.w);
+    o.x = k1.x * fmaf(-((xc.x - mu.x) * is.x), mx.x, g.x - mg.x);
+    o.y = k1.y * fmaf(-((xc.y - mu.y) * is.y), mx.y, g.y - mg.y);
+    o.z = k1.z * fmaf(-((xc.z - mu.z) * is.z), mx.z, g.z - mg.z);
+    o.w = k1.w * fmaf(-((xc.w - mu.w) * is.w), mx.w, g.w - mg.w);
     if (a.pack_dx)  // uniform: the bf16x3 convolutions' dY encoding
       reinterpret_cast<uint4*>(a.dx)[i] = make_uint4(split_pack(o.x), split_pack(o.y), split_pack(o.z), split_pack(o.w));
     else

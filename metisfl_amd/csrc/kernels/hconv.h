@@ -59,11 +59,67 @@ struct FwdArgs {
   int xcd = 1;                  // XCD-grouped tile order (MFL_HC_XCD=0: hardware order)
 };
 
+// ---- backward data (dgrad) -------------------------------------------------
+// The BatchNorm whose backward the dgrad's operand fill applies: the sums
+// [reps][2][C] of g and g * xhat are complete when the launch starts (the
+// producer of dy accumulated them); one block publishes dgamma / dbeta.
+struct BnBwdSrc {
+  const double* acc = nullptr;
+  int reps = 1;
+  const float* gamma = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  float* dgamma = nullptr;
+  float* dbeta = nullptr;
+};
+
+// Consumer BatchNorm-backward reductions in the dgrad epilogue (the BN whose
+// upstream gradient dx is): acc += (sum g, sum g * xhat), g = dx [* (y > 0)].
+struct BnSums {
+  const float* z = nullptr;
+  const float* y = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  double* acc = nullptr;
+  int reps = 1;
+};
+
+// dgrad input transform (once per element, as it enters LDS):
+//   g = dy [* (y > 0)],  dz = gamma * invstd * (g - mean(g) - xhat * mean(g * xhat))
+// zero outside the image.  Owner tiles write dz's packed split (dzp: the
+// layer's wgrad operand) and g (dres: the residual branch's gradient).
+struct DgXform {
+  const float* dy = nullptr;     // [N][H][W][C] gradient w.r.t. the layer output
+  const float* ymask = nullptr;  // post-activation output (ReLU mask) or nullptr
+  const float* z = nullptr;      // pre-BN conv output
+  BnBwdSrc bn;
+  int M = 0;
+  float* dres = nullptr;
+  uint32_t* dzp = nullptr;
+};
+
+// dx = conv3x3^T(dz, W) (+ dx when accumulate): C = dz channels (the layer's
+// output channels, the reduction), Co = dx channels (the layer's input).
+struct DgArgs {
+  int N, H, W, C, Co;
+  DgXform x;
+  const uint32_t* wp;  // the layer's packed weight mirror [C][3][3][Co]
+  float* out;
+  int accumulate = 0;
+  BnSums bnb;
+  float* slab;
+  int* counters;
+  long long* stamps = nullptr;
+  int dbg = 0;
+  int xcd = 1;
+};
+
 // Geometry supported by the halo kernels (3x3, stride 1, pad 1, square
 // CIFAR-ResNet stages); returns the split-K workspace floats (incl. 1024
 // counter words) or -1 when unsupported.
 int64_t hconv_fwd_workspace(int N, int H, int W, int C, int Co);
 void launch_hconv_fwd(const FwdArgs& a, hipStream_t s);
+void launch_hconv_dgrad(const DgArgs& a, hipStream_t s);
 
 }  // namespace hc
 }  // namespace mfl

@@ -97,47 +97,6 @@ struct Cfg {
   static_assert(ROWB >= PW * PS && (IMGS == 1 || IMGB >= PH * ROWB), "patch pitches");
 };
 
-// BatchNorm coefficients of channel c (bn32.hip bn32_apply_body, same fp64
-// math): scale / shift, publishing the batch statistics and running averages
-// when `publish`.
-__device__ __forceinline__ void bn_coef(const BnSrc& b, int C, int c, int M, bool train, bool publish, float& sc,
-                                        float& sh) {
-  double mu, var;
-  if (train) {
-    double a[8], q[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      a[r] = r < b.reps ? b.acc[(int64_t)r * 2 * C + c] : 0.0;
-      q[r] = r < b.reps ? b.acc[(int64_t)r * 2 * C + C + c] : 0.0;
-    }
-    double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      s0 += a[r];
-      s1 += q[r];
-    }
-    const double inv_m = 1.0 / (double)M;
-    mu = s0 * inv_m;
-    var = s1 * inv_m - mu * mu;
-    if (var < 0.0) var = 0.0;
-  } else {
-    mu = b.run_mean[c];
-    var = b.run_var[c];
-  }
-  const double isd = 1.0 / sqrt(var + (double)b.eps);
-  sc = (float)((double)b.gamma[c] * isd);
-  sh = (float)((double)b.beta[c] - mu * (double)b.gamma[c] * isd);
-  if (train && publish) {
-    b.mean[c] = (float)mu;
-    b.invstd[c] = (float)isd;
-    if (b.run_mean) {
-      const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
-      b.run_mean[c] = (1.f - b.momentum) * b.run_mean[c] + b.momentum * (float)mu;
-      b.run_var[c] = (1.f - b.momentum) * b.run_var[c] + b.momentum * (float)unb;
-    }
-  }
-}
-
 __device__ __forceinline__ f32x16 mfma_bf16x16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -148,16 +107,14 @@ __device__ __forceinline__ float4 as_f4(const u32x4& v) {
 
 // In-kernel phase stamps (profiling only, a.stamps != nullptr): lane 0 of
 // wave 0 records the core clock at phase boundaries with a vector store.
-__device__ __forceinline__ void stamp(const FwdArgs& a, int k) {
+template <class A>
+__device__ __forceinline__ void stamp(const A& a, int k) {
   if (a.stamps && threadIdx.x == 0) {
     const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
     a.stamps[(int64_t)b * 16 + k] = (long long)__builtin_readcyclecounter();
   }
 }
 
-// RK: residual kind of the input transform (0 none, 1 fp32 tensor, 2 BN of a
-// projection shortcut's pre-BN output).  Grid: x = spatial tiles, y = output
-// channel tiles, z = input-channel slices (split-K; kchunk channels each).
 // XCD-grouped workgroup order: the hardware deals workgroups round-robin
 // over the 8 XCDs (id % 8); logical tile L runs on group L / ceil(n / 8), so
 // consecutive spatial tiles of an image -- which share their halo rows --
@@ -170,9 +127,30 @@ __device__ __forceinline__ int xcd_tile(int b, int n, bool on) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-template <class K, int RK>
-__global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+// One BatchNorm replica row of the fp64 sums [reps][2][C]: (sum, sum2) of
+// channel c in replica r (zeros past `reps`).
+__device__ __forceinline__ void rep_load(const double* acc, int reps, int C, int r, int c, double& s0, double& s1) {
+  const bool ok = acc != nullptr && r < reps;
+  s0 = ok ? acc[(int64_t)r * 2 * C + c] : 0.0;
+  s1 = ok ? acc[(int64_t)r * 2 * C + C + c] : 0.0;
+}
+
+// MODE 0: forward, A = FwdArgs; the operand fill applies the producer's
+// BatchNorm (+ residual kind RK: 0 none, 1 fp32 tensor, 2 BN of a projection
+// shortcut's pre-BN output) and ReLU.
+// MODE 1: backward data, A = DgArgs; the fill applies the layer's BatchNorm
+// backward (RK = 1: with the ReLU mask of the layer output), the 9 taps of
+// the transposed weights are the forward's flipped (B slot 8 - tap).
+// Grid: x = spatial tiles, y = output channel tiles, z = input-channel
+// slices (split-K; kchunk channels each).
+template <class K, int MODE, int RK, class A>
+__device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem) {
+  constexpr bool DG = MODE == 1;
+  static_assert(K::NTHR == 512 && K::KCH == 64, "the coefficient prologue maps 8 waves onto 8 replicas x 64 channels");
+  // input chunks whose loads are in flight ahead of their fill: every chunk
+  // (forward, 1-2 inputs per element), or a ring of 2 (dgrad: 3 inputs)
+  constexpr int PF = DG ? 2 : K::NCH;
+  constexpr int NCOEF = DG ? 5 : 4;
   const int nblk = gridDim.x * gridDim.y * gridDim.z;
   const int lin = xcd_tile(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nblk, a.xcd);
   const int bx = lin % gridDim.x, by = (lin / gridDim.x) % gridDim.y, bz = lin / (gridDim.x * gridDim.y);
@@ -190,16 +168,49 @@ __global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kc
   const int y0 = ty * K::TH, x0 = tx * K::TW;
   const int n0 = by * K::NT;
   const int kbeg = bz * kchunk;
-  float* coef = reinterpret_cast<float*>(smem + K::LDS_MAIN);  // [4][kchunk]: sc, sh, sc2, sh2
-  const FwdXform& X = a.x;
+  float* coef = reinterpret_cast<float*>(smem + K::LDS_MAIN);  // [NCOEF][kchunk]
+  const auto& X = a.x;
   stamp(a, 0);
+
+  // ---- coefficient sources, requested BEFORE the operand loads: thread t
+  // holds channel cc = t % 64's sums of replica rr = t / 64 (the 8 waves
+  // cover the 8 replicas) and the channel's per-channel parameters, so the
+  // prologue waits only for these (counted vmcnt), never for the operands.
+  const int cc = t & 63, rr = t >> 6;
+  const int ch = kbeg + cc;
+  double p0 = 0.0, p1 = 0.0, q0 = 0.0, q1 = 0.0;
+  float g0 = 1.f, g1 = 0.f, g2 = 0.f, g3 = 0.f;  // per-channel parameters
+  float e0 = 1.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;  // RK == 2: the residual BN's
+  if constexpr (DG) {
+    rep_load(X.bn.acc, X.bn.reps, C, rr, ch, p0, p1);
+    g0 = X.bn.gamma[ch];
+    g1 = X.bn.mean[ch];
+    g2 = X.bn.invstd[ch];
+  } else {
+    if (X.has_bn) {
+      if (X.train) rep_load(X.bn.acc, X.bn.reps, C, rr, ch, p0, p1);
+      g0 = X.bn.gamma[ch];
+      g1 = X.bn.beta[ch];
+      g2 = X.bn.run_mean[ch];
+      g3 = X.bn.run_var[ch];
+    }
+    if constexpr (RK == 2) {
+      if (X.train) rep_load(X.bnr.acc, X.bnr.reps, C, rr, ch, q0, q1);
+      e0 = X.bnr.gamma[ch];
+      e1 = X.bnr.beta[ch];
+      e2 = X.bnr.run_mean[ch];
+      e3 = X.bnr.run_var[ch];
+    }
+  }
 
   // ---- per-thread fill geometry (fixed over the chunks) ----
   const int q = t & 3;  // float4 within the 16-channel chunk (NTHR % 4 == 0)
   uint32_t a_off[K::NA];  // byte offset of the item's pixel + 4q channels, kOOB outside
-  int a_lds[K::NA];       // LDS byte offset of the item's hi half (-1: no item)
+  int a_lds[K::NA];       // LDS byte offset of the item's hi half (dummy slot: no item)
   bool a_own[K::NA];
-  const bool own_tile = by == 0 && (X.y != nullptr);
+  bool own_tile;
+  if constexpr (DG) own_tile = by == 0 && (X.dzp != nullptr || X.dres != nullptr);
+  else own_tile = by == 0 && (X.y != nullptr);
 #pragma unroll
   for (int u = 0; u < K::NA; ++u) {
     const int i = t + K::NTHR * u;
@@ -214,88 +225,152 @@ __global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kc
     a_lds[u] = item ? img * K::IMGB + py * K::ROWB + px * K::PS + 8 * q : K::A_BYTES + K::B_BYTES + 8 * q;
     a_own[u] = own_tile && in && py >= 1 && py <= K::TH && px >= 1 && px <= K::TW;
   }
+  // B items.  Forward: (co, tap, channel quad) -> one b128 of the packed
+  // weight row W[n0 + co][tap][4 channels].  Dgrad: (tap, quad of 4 k =
+  // layer output channels, n = ci) -> four b32 W[k .. k+3][tap][n0 + ci]
+  // (each a coalesced 256-B row per wave), the transpose happens in the
+  // register pass.
   uint32_t b_off[K::NB];
   int b_lds[K::NB];
 #pragma unroll
   for (int u = 0; u < K::NB; ++u) {
     const int i = t + K::NTHR * u;
-    const int co = i / 36, r = i - co * 36;
-    const int tap = r >> 2, bq = r & 3;
     const bool item = i < K::NT * 36;
-    b_off[u] = item ? (uint32_t)((((n0 + co) * 9 + tap) * C + 4 * bq) * 4) : kOOB;
-    b_lds[u] = item ? K::A_BYTES + tap * (K::NT * K::BPS) + co * K::BPS + 8 * bq : K::A_BYTES + K::B_BYTES + 8 * bq;
+    if constexpr (DG) {
+      const int ci = i % K::NT, rs = i / K::NT;
+      const int tap = rs >> 2, kq = rs & 3;
+      b_off[u] = item ? (uint32_t)((((4 * kq) * 9 + tap) * a.Co + n0 + ci) * 4) : kOOB;
+      b_lds[u] = item ? K::A_BYTES + (8 - tap) * (K::NT * K::BPS) + ci * K::BPS + 8 * kq
+                      : K::A_BYTES + K::B_BYTES + 8 * kq;
+    } else {
+      const int co = i / 36, r = i - co * 36;
+      const int tap = r >> 2, bq = r & 3;
+      b_off[u] = item ? (uint32_t)((((n0 + co) * 9 + tap) * C + 4 * bq) * 4) : kOOB;
+      b_lds[u] = item ? K::A_BYTES + tap * (K::NT * K::BPS) + co * K::BPS + 8 * bq
+                      : K::A_BYTES + K::B_BYTES + 8 * bq;
+    }
   }
   const uint32_t in_bytes = (uint32_t)((int64_t)a.N * a.H * a.W * C * 4);
-  const auto rsZ = make_rsrc(X.z, in_bytes);
-  const auto rsR = make_rsrc(RK == 1 ? X.res : X.zr, in_bytes);
+  const float* src0;
+  const float* src1;
+  const float* src2 = nullptr;
+  if constexpr (DG) {
+    src0 = X.dy;
+    src1 = X.z;
+    src2 = X.ymask;
+  } else {
+    src0 = X.z;
+    src1 = RK == 1 ? X.res : X.zr;
+  }
+  const auto rs0 = make_rsrc(src0, in_bytes);
+  const auto rs1 = make_rsrc(src1, in_bytes);
+  const auto rs2 = make_rsrc(src2, in_bytes);
   const auto rsW = make_rsrc(a.wp, (uint32_t)((int64_t)a.Co * 9 * C * 4));
+  constexpr bool IN1 = DG || RK != 0;  // second input per element
+  constexpr bool IN2 = DG && RK == 1;  // third (dgrad ReLU mask)
 
-  // The input patch of EVERY chunk is requested at kernel start (its latency
-  // -- the producer's output comes from the Infinity Cache / HBM, ~2 us -- is
-  // paid once, under the BatchNorm coefficient prologue); the weights (L2-
-  // resident) stream one chunk ahead through a single register set.
-  u32x4 az[K::NCH][K::NA], ar[K::NCH][K::NA], bw[K::NB];
+  // Operand registers: a ring of PF chunks of the input patch (the
+  // producer's output comes from the Infinity Cache / HBM, ~2 us: its latency
+  // is paid once, under the coefficient prologue); the weights (L2-resident)
+  // stream one chunk ahead through a single register set.
+  u32x4 az[PF][K::NA], ar[PF][K::NA], am[PF][K::NA], bw[K::NB];
   auto load_a = [&](auto kc) {
-    constexpr int k = decltype(kc)::value;
+    constexpr int k = decltype(kc)::value, S = k % PF;
     if (a.dbg & 4) return;
     const uint32_t cb = (uint32_t)((kbeg + k * K::CC) * 4);
 #pragma unroll
     for (int u = 0; u < K::NA; ++u) {
       const uint32_t off = a_off[u] == kOOB ? kOOB : a_off[u] + cb;
-      az[k][u] = __builtin_amdgcn_raw_buffer_load_b128(rsZ, (int)off, 0, 0);
-      if constexpr (RK != 0) ar[k][u] = __builtin_amdgcn_raw_buffer_load_b128(rsR, (int)off, 0, 0);
+      az[S][u] = __builtin_amdgcn_raw_buffer_load_b128(rs0, (int)off, 0, 0);
+      if constexpr (IN1) ar[S][u] = __builtin_amdgcn_raw_buffer_load_b128(rs1, (int)off, 0, 0);
+      if constexpr (IN2) am[S][u] = __builtin_amdgcn_raw_buffer_load_b128(rs2, (int)off, 0, 0);
     }
   };
   auto load_b = [&](int k) {
     if (a.dbg & 4) return;
-    const uint32_t cb = (uint32_t)((kbeg + k * K::CC) * 4);
+    if constexpr (DG) {
+      const uint32_t kb = (uint32_t)((kbeg + k * K::CC) * 9 * a.Co * 4);  // first k row of the chunk
+      const uint32_t kst = (uint32_t)(9 * a.Co * 4);                       // next k
 #pragma unroll
-    for (int u = 0; u < K::NB; ++u) {
-      const uint32_t off = b_off[u] == kOOB ? kOOB : b_off[u] + cb;
-      bw[u] = __builtin_amdgcn_raw_buffer_load_b128(rsW, (int)off, 0, 0);
+      for (int u = 0; u < K::NB; ++u) {
+        const uint32_t off = b_off[u] == kOOB ? kOOB : b_off[u] + kb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          bw[u][e] = __builtin_amdgcn_raw_buffer_load_b32(rsW, (int)(off == kOOB ? kOOB : off + e * kst), 0, 0);
+      }
+    } else {
+      const uint32_t cb = (uint32_t)((kbeg + k * K::CC) * 4);
+#pragma unroll
+      for (int u = 0; u < K::NB; ++u) {
+        const uint32_t off = b_off[u] == kOOB ? kOOB : b_off[u] + cb;
+        bw[u] = __builtin_amdgcn_raw_buffer_load_b128(rsW, (int)off, 0, 0);
+      }
     }
   };
   // The fill of a chunk as NA + NB independent work units (unit u < NA: one
-  // float4 of the input patch -> BN / residual / ReLU -> bf16 hi + lo -> LDS
-  // and, for owner tiles, y / yp; unit NA + v: one packed weight float4 ->
-  // hi / lo -> LDS).  The units of chunk k+1 are spread over the taps of
-  // chunk k's MFMAs (their VALU / LDS writes issue under the matrix pipe).
+  // float4 of the input patch -> transform -> bf16 hi + lo -> LDS and, for
+  // owner tiles, the transform's global outputs; unit NA + v: one packed
+  // weight float4 -> hi / lo -> LDS).  The units of chunk k+1 are spread over
+  // the taps of chunk k's MFMAs (their VALU / LDS writes issue under the
+  // matrix pipe).
   struct Coef4 {
-    float4 sc, sh, s2, h2;
+    float4 c0, c1, c2, c3, c4;
   };
   auto coef4 = [&](int k) {
     const int cl = k * K::CC + 4 * q;  // channel within the slice
     Coef4 c;
-    c.sc = *reinterpret_cast<const float4*>(coef + cl);
-    c.sh = *reinterpret_cast<const float4*>(coef + kchunk + cl);
-    c.s2 = c.sc;
-    c.h2 = c.sh;
-    if constexpr (RK == 2) {
-      c.s2 = *reinterpret_cast<const float4*>(coef + 2 * kchunk + cl);
-      c.h2 = *reinterpret_cast<const float4*>(coef + 3 * kchunk + cl);
+    c.c0 = *reinterpret_cast<const float4*>(coef + cl);
+    c.c1 = *reinterpret_cast<const float4*>(coef + kchunk + cl);
+    c.c2 = c.c0;
+    c.c3 = c.c1;
+    c.c4 = c.c0;
+    if constexpr (DG || RK == 2) {
+      c.c2 = *reinterpret_cast<const float4*>(coef + 2 * kchunk + cl);
+      c.c3 = *reinterpret_cast<const float4*>(coef + 3 * kchunk + cl);
     }
+    if constexpr (DG) c.c4 = *reinterpret_cast<const float4*>(coef + 4 * kchunk + cl);
     return c;
   };
   auto store_unit = [&](auto kc, auto uc, uint8_t* stage, const Coef4& cf) {
-    constexpr int k = decltype(kc)::value, U = decltype(uc)::value;
+    constexpr int k = decltype(kc)::value, U = decltype(uc)::value, S = k % PF;
     if constexpr (U < K::NA) {
       constexpr int u = U;
-      const float4 zv = as_f4(az[k][u]);
-      float4 v = make_float4(fmaf(zv.x, cf.sc.x, cf.sh.x), fmaf(zv.y, cf.sc.y, cf.sh.y),
-                             fmaf(zv.z, cf.sc.z, cf.sh.z), fmaf(zv.w, cf.sc.w, cf.sh.w));
-      if constexpr (RK == 1) {
-        const float4 r = as_f4(ar[k][u]);
-        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
-      } else if constexpr (RK == 2) {
-        const float4 r = as_f4(ar[k][u]);
-        v.x += fmaf(r.x, cf.s2.x, cf.h2.x);
-        v.y += fmaf(r.y, cf.s2.y, cf.h2.y);
-        v.z += fmaf(r.z, cf.s2.z, cf.h2.z);
-        v.w += fmaf(r.w, cf.s2.w, cf.h2.w);
+      const bool oob = a_off[u] == kOOB;  // padding: zero after the transform
+      float4 v, gd;
+      if constexpr (DG) {
+        // bn32_bwd_apply's arithmetic (explicit fma: the same bits):
+        // dz = k1 (g - mg - ((z - mu) is) mx)
+        gd = as_f4(az[S][u]);
+        if constexpr (IN2) {
+          const float4 ym = as_f4(am[S][u]);
+          gd.x = ym.x > 0.f ? gd.x : 0.f;
+          gd.y = ym.y > 0.f ? gd.y : 0.f;
+          gd.z = ym.z > 0.f ? gd.z : 0.f;
+          gd.w = ym.w > 0.f ? gd.w : 0.f;
+        }
+        const float4 zv = as_f4(ar[S][u]);
+        const float4 &k1 = cf.c0, &mg = cf.c1, &mx = cf.c2, &mu = cf.c3, &is = cf.c4;
+        v.x = k1.x * fmaf(-((zv.x - mu.x) * is.x), mx.x, gd.x - mg.x);
+        v.y = k1.y * fmaf(-((zv.y - mu.y) * is.y), mx.y, gd.y - mg.y);
+        v.z = k1.z * fmaf(-((zv.z - mu.z) * is.z), mx.z, gd.z - mg.z);
+        v.w = k1.w * fmaf(-((zv.w - mu.w) * is.w), mx.w, gd.w - mg.w);
+      } else {
+        const float4 zv = as_f4(az[S][u]);
+        v = make_float4(fmaf(zv.x, cf.c0.x, cf.c1.x), fmaf(zv.y, cf.c0.y, cf.c1.y),
+                        fmaf(zv.z, cf.c0.z, cf.c1.z), fmaf(zv.w, cf.c0.w, cf.c1.w));
+        if constexpr (RK == 1) {
+          const float4 r = as_f4(ar[S][u]);
+          v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+        } else if constexpr (RK == 2) {
+          const float4 r = as_f4(ar[S][u]);
+          v.x += fmaf(r.x, cf.c2.x, cf.c3.x);
+          v.y += fmaf(r.y, cf.c2.y, cf.c3.y);
+          v.z += fmaf(r.z, cf.c2.z, cf.c3.z);
+          v.w += fmaf(r.w, cf.c2.w, cf.c3.w);
+        }
+        const float lo = X.relu ? 0.f : -__builtin_inff();
+        v.x = fmaxf(v.x, lo); v.y = fmaxf(v.y, lo); v.z = fmaxf(v.z, lo); v.w = fmaxf(v.w, lo);
       }
-      const float lo = X.relu ? 0.f : -__builtin_inff();
-      v.x = fmaxf(v.x, lo); v.y = fmaxf(v.y, lo); v.z = fmaxf(v.z, lo); v.w = fmaxf(v.w, lo);
-      const bool oob = a_off[u] == kOOB;  // padding is post-activation zero
       v.x = oob ? 0.f : v.x; v.y = oob ? 0.f : v.y; v.z = oob ? 0.f : v.z; v.w = oob ? 0.f : v.w;
       uint32_t h01, l01, h23, l23;
       split2(v.x, v.y, h01, l01);
@@ -305,11 +380,15 @@ __global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kc
       *reinterpret_cast<uint2*>(d + 32) = make_uint2(l01, l23);
       if (a_own[u]) {
         const uint32_t go = a_off[u] + (uint32_t)((kbeg + k * K::CC) * 4);  // pixel + chunk + 4q channels
-        *reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(X.y) + go) = v;
-        if (X.yp)
-          *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(X.yp) + go) =
-              make_uint4((h01 << 16) | (l01 & 0xffffu), (h01 & 0xffff0000u) | (l01 >> 16),
-                         (h23 << 16) | (l23 & 0xffffu), (h23 & 0xffff0000u) | (l23 >> 16));
+        const uint4 pk = make_uint4((h01 << 16) | (l01 & 0xffffu), (h01 & 0xffff0000u) | (l01 >> 16),
+                                    (h23 << 16) | (l23 & 0xffffu), (h23 & 0xffff0000u) | (l23 >> 16));
+        if constexpr (DG) {
+          if (X.dres) *reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(X.dres) + go) = gd;
+          if (X.dzp) *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(X.dzp) + go) = pk;
+        } else {
+          *reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(X.y) + go) = v;
+          if (X.yp) *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(X.yp) + go) = pk;
+        }
       }
     } else {
       constexpr int u = U - K::NA;
@@ -324,29 +403,94 @@ __global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kc
     }
   };
   constexpr int NU = K::NA + K::NB;
-  auto store = [&](auto kc, uint8_t* stage) {
-    const Coef4 cf = coef4(decltype(kc)::value);
-    static_for<NU>([&](auto uc) { store_unit(kc, uc, stage, cf); });
+  // LDS-only barrier: the owner-write global stores and the operand loads
+  // stay in flight (__syncthreads would drain vmcnt)
+  auto bar = [&]() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes / reads done
+    lds_barrier();
   };
 
-  static_for<K::NCH>([&](auto kc) { load_a(kc); });
+  static_for<PF>([&](auto kc) { load_a(kc); });
   load_b(0);
-  // ---- coefficients of this slice's input channels ----
-  {
-    const bool publish = X.train && bx == 0 && by == 0;
-    for (int c = t; c < kchunk; c += K::NTHR) {
+
+  // ---- coefficients of this slice's input channels: replica partials ->
+  // LDS (stage 1, free until chunk 1's fill) -> wave 0 sums them in replica
+  // order (bit-identical to bn32's rep_sums) -> coef[][]
+  double* part = reinterpret_cast<double*>(smem + K::STAGE);  // [2 sources][8][2][64]
+  part[(rr * 2 + 0) * 64 + cc] = p0;
+  part[(rr * 2 + 1) * 64 + cc] = p1;
+  if constexpr (!DG && RK == 2) {
+    part[1024 + (rr * 2 + 0) * 64 + cc] = q0;
+    part[1024 + (rr * 2 + 1) * 64 + cc] = q1;
+  }
+  bar();
+  if (wave == 0) {
+    const int c = cc;
+    auto sums = [&](int base, double& s0, double& s1) {
+      s0 = 0.0;
+      s1 = 0.0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        s0 += part[base + (r * 2 + 0) * 64 + c];
+        s1 += part[base + (r * 2 + 1) * 64 + c];
+      }
+    };
+    const double inv_m = 1.0 / (double)X.M;
+    const bool publish = bx == 0 && by == 0;
+    if constexpr (DG) {
+      double s, qq;
+      sums(0, s, qq);
+      coef[c] = g0 * g2;                    // gamma * invstd
+      coef[kchunk + c] = (float)(s * inv_m);  // mean g
+      coef[2 * kchunk + c] = (float)(qq * inv_m);  // mean g * xhat
+      coef[3 * kchunk + c] = g1;            // mean
+      coef[4 * kchunk + c] = g2;            // invstd
+      if (publish) {
+        if (X.bn.dgamma) X.bn.dgamma[ch] = (float)qq;
+        if (X.bn.dbeta) X.bn.dbeta[ch] = (float)s;
+      }
+    } else {
+      // bn32_apply's fp64 coefficient math; publishes the batch statistics
+      // and running averages once per channel
+      auto coefs = [&](const BnSrc& b, int base, float gm, float bt, float rm, float rv, float& sc, float& sh) {
+        double mu, var;
+        if (X.train) {
+          double s0, s1;
+          sums(base, s0, s1);
+          mu = s0 * inv_m;
+          var = s1 * inv_m - mu * mu;
+          if (var < 0.0) var = 0.0;
+        } else {
+          mu = rm;
+          var = rv;
+        }
+        const double isd = 1.0 / sqrt(var + (double)b.eps);
+        sc = (float)((double)gm * isd);
+        sh = (float)((double)bt - mu * (double)gm * isd);
+        if (X.train && publish) {
+          b.mean[ch] = (float)mu;
+          b.invstd[ch] = (float)isd;
+          if (b.run_mean) {
+            const int M = X.M;
+            const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+            b.run_mean[ch] = fmaf(1.f - b.momentum, rm, b.momentum * (float)mu);  // = bn32_apply's bits
+            b.run_var[ch] = fmaf(1.f - b.momentum, rv, b.momentum * (float)unb);
+          }
+        }
+      };
       float sc = 1.f, sh = 0.f;
-      if (X.has_bn) bn_coef(X.bn, C, kbeg + c, X.M, X.train, publish, sc, sh);
+      if (X.has_bn) coefs(X.bn, 0, g0, g1, g2, g3, sc, sh);
       coef[c] = sc;
       coef[kchunk + c] = sh;
       if constexpr (RK == 2) {
         float s2, h2;
-        bn_coef(X.bnr, C, kbeg + c, X.M, X.train, publish, s2, h2);
+        coefs(X.bnr, 1024, e0, e1, e2, e3, s2, h2);
         coef[2 * kchunk + c] = s2;
         coef[3 * kchunk + c] = h2;
       }
     }
   }
+  bar();  // coefficients visible; the operand loads are still in flight
 
   // ---- fragment addresses (tap (0,0), hi half; lo at +32) ----
   int fa_off[K::TM], fb_off[K::TN];
@@ -411,16 +555,13 @@ __global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kc
       __builtin_amdgcn_sched_barrier(0);
     });
   };
-  // LDS-only barrier: the owner-write global stores and the next chunk's
-  // loads stay in flight (__syncthreads would drain vmcnt)
-  auto bar = [&]() {
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes / reads done
-    lds_barrier();
-  };
 
-  __syncthreads();  // coefficients visible
   stamp(a, 1);
-  store(IC<0>{}, smem);
+  {
+    const Coef4 cf = coef4(0);
+    static_for<NU>([&](auto uc) { store_unit(IC<0>{}, uc, smem, cf); });
+  }
+  if constexpr (PF < K::NCH) load_a(IC<PF>{});  // chunk 0's registers are free
   load_b(1);
   bar();
   stamp(a, 2);
@@ -438,6 +579,7 @@ __global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kc
           if constexpr (U * 9 / NU == TAP) store_unit(IC<k + 1>{}, uc, nxt, cf);
         });
       });
+      if constexpr (k + 1 + PF < K::NCH) load_a(IC<k + 1 + PF>{});
       if constexpr (k + 2 < K::NCH) load_b(k + 2);
     } else {
       compute(cur, [](auto) {});
@@ -449,7 +591,7 @@ __global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kc
   __syncthreads();
   stamp(a, 5);
 
-  // ---- epilogue: tile through LDS, split-K reduce, output + BN sums ----
+  // ---- epilogue: tile through LDS, split-K reduce, output (+ reductions) ----
   float* tile = reinterpret_cast<float*>(smem);
   float* red = tile + K::MT * K::TST;
 #pragma unroll
@@ -518,24 +660,64 @@ __global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kc
     __syncthreads();
   }
   stamp(a, 6);
-  // output rows: float4 per thread per pass
+  // output rows: float4 per thread per pass, + the per-channel reductions
+  // (forward: this conv's BN statistics; dgrad: the consumer BN backward's)
   constexpr int RPP = K::NTHR / C4;
   const int cg = t % C4, r0 = t / C4;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), sq = s;
+  const int col = n0 + cg * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), sq = s, mu = s, is = s;
+  bool red_on;
+  if constexpr (DG) {
+    red_on = a.bnb.acc != nullptr;
+    if (red_on) {
+      mu = *reinterpret_cast<const float4*>(a.bnb.mean + col);
+      is = *reinterpret_cast<const float4*>(a.bnb.invstd + col);
+    }
+  } else {
+    red_on = a.stats != nullptr;
+  }
   for (int rl = r0; rl < K::MT; rl += RPP) {
     const int img = rl / (K::TH * K::TW);
     const int r2 = rl - img * (K::TH * K::TW);
     const int y = r2 / K::TW, x = r2 - y * K::TW;
     if (img0 + img >= a.N) continue;
-    const float4 v = *reinterpret_cast<const float4*>(tile + rl * K::TST + cg * 4);
-    const int64_t pix = ((int64_t)(img0 + img) * a.H + y0 + y) * a.W + x0 + x;
-    *reinterpret_cast<float4*>(a.out + pix * a.Co + n0 + cg * 4) = v;
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    sq.x += v.x * v.x; sq.y += v.y * v.y; sq.z += v.z * v.z; sq.w += v.w * v.w;
+    float4 v = *reinterpret_cast<const float4*>(tile + rl * K::TST + cg * 4);
+    const int64_t off = (((int64_t)(img0 + img) * a.H + y0 + y) * a.W + x0 + x) * a.Co + col;
+    float4* dst = reinterpret_cast<float4*>(a.out + off);
+    if constexpr (DG) {
+      if (a.accumulate) {
+        const float4 o = *dst;
+        v = make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w);
+      }
+      *dst = v;
+      if (red_on) {
+        // tile_epilogue32's consumer-BN reductions: g = dx [* (y > 0)]
+        const float4 z = *reinterpret_cast<const float4*>(a.bnb.z + off);
+        float4 gk = v;
+        if (a.bnb.y) {
+          const float4 ym = *reinterpret_cast<const float4*>(a.bnb.y + off);
+          gk.x = ym.x > 0.f ? gk.x : 0.f;
+          gk.y = ym.y > 0.f ? gk.y : 0.f;
+          gk.z = ym.z > 0.f ? gk.z : 0.f;
+          gk.w = ym.w > 0.f ? gk.w : 0.f;
+        }
+        s.x += gk.x; s.y += gk.y; s.z += gk.z; s.w += gk.w;
+        sq.x += gk.x * ((z.x - mu.x) * is.x);
+        sq.y += gk.y * ((z.y - mu.y) * is.y);
+        sq.z += gk.z * ((z.z - mu.z) * is.z);
+        sq.w += gk.w * ((z.w - mu.w) * is.w);
+      }
+    } else {
+      *dst = v;
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      sq.x += v.x * v.x; sq.y += v.y * v.y; sq.z += v.z * v.z; sq.w += v.w * v.w;
+    }
   }
   stamp(a, 7);
-  if (!a.stats) return;
-  double* stats = a.stats + (int64_t)((bx + by * gridDim.x) % a.reps) * 2 * a.Co;
+  if (!red_on) return;
+  double* stats;
+  if constexpr (DG) stats = a.bnb.acc + (int64_t)((bx + by * gridDim.x) % a.bnb.reps) * 2 * a.Co;
+  else stats = a.stats + (int64_t)((bx + by * gridDim.x) % a.reps) * 2 * a.Co;
   reinterpret_cast<float4*>(red)[2 * t] = s;
   reinterpret_cast<float4*>(red)[2 * t + 1] = sq;
   __syncthreads();
@@ -550,6 +732,18 @@ __global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kc
     atomicAdd(&stats[a.Co + n0 + t], sb);
   }
   stamp(a, 8);
+}
+
+template <class K, int RK>
+__global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  hconv_body<K, 0, RK>(a, kchunk, smem);
+}
+
+template <class K, int MASK>
+__global__ __launch_bounds__(K::NTHR, 1) void hconv_dgrad_kernel(DgArgs a, int kchunk) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  hconv_body<K, 1, MASK>(a, kchunk, smem);
 }
 
 // Stage configurations for the CIFAR ResNet-18 shapes at any batch (3x3, s1):
@@ -593,23 +787,35 @@ Plan plan_fwd(int N, int H, int W, int C, int Co) {
   return p;
 }
 
-template <class K, int RK>
-void go(const FwdArgs& a, const Plan& p, hipStream_t s) {
-  const size_t lds = (size_t)K::LDS_MAIN + 4 * (size_t)p.kchunk * sizeof(float);
-  static bool init = false;
+template <class Kern, class Args>
+void launch(Kern* kern, const Args& a, const Plan& p, size_t lds, int nthr, hipStream_t s) {
+  static bool init = false;  // one per kernel instantiation
   if (!init) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hconv_fwd_kernel<K, RK>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
     init = true;
   }
-  hconv_fwd_kernel<K, RK><<<p.grid, K::NTHR, lds, s>>>(a, p.kchunk);
+  kern<<<p.grid, nthr, lds, s>>>(a, p.kchunk);
+}
+
+template <class K>
+size_t lds_of(const Plan& p) {
+  return (size_t)K::LDS_MAIN + 5 * (size_t)p.kchunk * sizeof(float);  // + coef [5][kchunk]
 }
 
 template <class K>
 void go_rk(const FwdArgs& a, const Plan& p, hipStream_t s) {
-  if (a.x.zr) go<K, 2>(a, p, s);
-  else if (a.x.res) go<K, 1>(a, p, s);
-  else go<K, 0>(a, p, s);
+  const size_t lds = lds_of<K>(p);
+  if (a.x.zr) launch(&hconv_fwd_kernel<K, 2>, a, p, lds, K::NTHR, s);
+  else if (a.x.res) launch(&hconv_fwd_kernel<K, 1>, a, p, lds, K::NTHR, s);
+  else launch(&hconv_fwd_kernel<K, 0>, a, p, lds, K::NTHR, s);
+}
+
+template <class K>
+void go_dg(const DgArgs& a, const Plan& p, hipStream_t s) {
+  const size_t lds = lds_of<K>(p);
+  if (a.x.ymask) launch(&hconv_dgrad_kernel<K, 1>, a, p, lds, K::NTHR, s);
+  else launch(&hconv_dgrad_kernel<K, 0>, a, p, lds, K::NTHR, s);
 }
 
 }  // namespace
@@ -629,6 +835,17 @@ void launch_hconv_fwd(const FwdArgs& a, hipStream_t s) {
     case 3: go_rk<S3>(a, p, s); break;
     case 4: go_rk<S4>(a, p, s); break;
     default: break;  // the binding checked support
+  }
+}
+
+void launch_hconv_dgrad(const DgArgs& a, hipStream_t s) {
+  const Plan p = plan_fwd(a.N, a.H, a.W, a.C, a.Co);  // C == Co: the forward's tiling
+  switch (p.stage) {
+    case 1: go_dg<S1>(a, p, s); break;
+    case 2: go_dg<S2>(a, p, s); break;
+    case 3: go_dg<S3>(a, p, s); break;
+    case 4: go_dg<S4>(a, p, s); break;
+    default: break;
   }
 }
 

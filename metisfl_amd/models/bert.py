@@ -72,6 +72,8 @@ class BertMLM(StaticNet):
     """Masked-LM BERT learner.  ``make_dataset`` takes int32 records (see
     ``metisfl_amd.datasets.synthetic.synthetic_mlm``)."""
 
+    graph_steps = 1  # a ~15 ms step: one graph per update already hides the launch
+
     def __init__(self, batch_size: int, device="cpu", optimizer: OptimizerSpec | None = None, seed: int = 0,
                  config: BertConfig | dict | None = None):
         if isinstance(config, dict):
@@ -94,6 +96,7 @@ class BertMLM(StaticNet):
         self.stats = torch.zeros(4, dtype=torch.float32, device=dev)
         self.eval_step_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
         self._train_graph = None
+        self._train_graph_k = None
         self._train_graph_ds = None
         self._eval_graph = None
         self._eval_graph_ds = None

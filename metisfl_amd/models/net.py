@@ -10,6 +10,7 @@ a task.  Loss / accuracy are accumulated on device and read once per task.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import numpy as np
@@ -103,6 +104,7 @@ class StaticNet:
         self.stats = torch.zeros(4, dtype=torch.float32, device=dev)
         self.eval_step_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
         self._train_graph = None
+        self._train_graph_k = None
         self._train_graph_ds = None
         self._eval_graph = None
         self._eval_graph_ds = None
@@ -185,20 +187,38 @@ class StaticNet:
     def use_graphs(self) -> bool:
         return self.device.type == "cuda"
 
+    # Updates per captured train graph: a K-update graph replays K steps per
+    # host launch (the batch gather reads the device step counter, so the
+    # steps need nothing from the host); chunks never cross an epoch boundary,
+    # where the host reshuffles.  MFL_GRAPH_STEPS=1: one graph per update.
+    graph_steps: int = int(os.environ.get("MFL_GRAPH_STEPS", "8"))
+
     def train_steps(self, ds: DeviceDataset, nsteps: int, step_offset: int = 0) -> None:
         """Run ``nsteps`` local updates; reshuffles at epoch boundaries."""
-        if self.use_graphs() and (self._train_graph is None or self._train_graph_ds is not ds):
+        graphs = self.use_graphs()
+        if graphs and (self._train_graph is None or self._train_graph_ds is not ds):
             self._train_graph = self._capture(self._train_body, ds)
+            self._train_graph_k = None
             self._train_graph_ds = ds
         spe = ds.steps_per_epoch
-        for i in range(nsteps):
+        K = max(1, self.graph_steps)
+        i = 0
+        while i < nsteps:
             gstep = step_offset + i
             if gstep > 0 and gstep % spe == 0:
                 ds.reshuffle()
-            if self.use_graphs():
+            if graphs and K > 1 and nsteps - i >= K and spe - gstep % spe >= K:
+                if self._train_graph_k is None:
+                    body = self._train_body
+                    self._train_graph_k = self._capture(lambda d: [body(d) for _ in range(K)], ds)
+                self._train_graph_k.replay()
+                i += K
+                continue
+            if graphs:
                 self._train_graph.replay()
             else:
                 self._train_body(ds)
+            i += 1
 
     def evaluate(self, ds: DeviceDataset, max_steps: int | None = None) -> dict:
         """Loss / accuracy of the current model on ``ds`` (BN in inference mode)."""

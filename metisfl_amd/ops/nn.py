@@ -331,6 +331,32 @@ def hconv_forward(z, wp, w, out, shp: ConvShape, bn: BnParams, train: bool, relu
     conv_forward(v, w, out, shp, stats=stats)
 
 
+def hconv_dgrad(dy, ymask, z, wp, w, out, shp: ConvShape, bn: BnParams, dgamma=None, dbeta=None, ws=None,
+                dres=None, dzp=None, accumulate: bool = False, bnb: BnBwdTarget | None = None,
+                stamps=None) -> None:
+    """out (+)= conv3x3^T(dz, w) with dz = BN_backward(g), g = dy [* (ymask > 0)],
+    applied as the operand enters LDS (one launch: no separate BatchNorm
+    backward apply).  ``bn.acc`` holds the complete sums of g and g * xhat
+    (the producer of dy accumulated them); dgamma / dbeta are published.
+    ``dzp`` receives dz's packed bf16x3 split (the layer's wgrad operand),
+    ``dres`` g (the residual branch's gradient).  ``bnb``: the consumer
+    BatchNorm-backward reductions of ``out`` (as conv_dgrad)."""
+    C = shp.Co  # dz channels (the layer's output): the reduction
+    if dy.is_cuda:
+        ops().hconv_dgrad(dy, ymask, z, wp, out, ws, shp.N, shp.H, shp.W, C, shp.C, bn.acc, bn.gamma, bn.mean,
+                          bn.invstd, dgamma, dbeta, dres, dzp, accumulate,
+                          bnb.z if bnb else None, bnb.y if bnb else None, bnb.mean if bnb else None,
+                          bnb.invstd if bnb else None, bnb.acc if bnb else None, stamps)
+        return
+    # reference: the BatchNorm backward the fill replaces, then the dgrad
+    dz = torch.empty_like(z)
+    bn_backward(dy, z, ymask, C, bn.gamma, bn.mean, bn.invstd, bn.acc, dgamma, dbeta, dz, dy_masked=dres,
+                presummed=True)
+    if dzp is not None:
+        dzp.copy_(dz)
+    conv_dgrad(dz, w, out, shp, accumulate=accumulate, bnb=bnb)
+
+
 def bn_stats(x, C: int, acc) -> None:
     """acc[0:C] += sum x, acc[C:2C] += sum x^2 (fp64) over the rows of NHWC x."""
     if x.is_cuda:

@@ -170,9 +170,10 @@ class AsyncCollectiveFederation:
         except BaseException as e:  # noqa: BLE001 - re-raised on the main thread
             self._svc_error = e
 
-    def run(self) -> list[AsyncUpdate]:
+    def run(self, debug_delay_s: float = 0.0) -> list[AsyncUpdate]:
         """Run ``tasks_per_learner`` asynchronous tasks on this learner; rank 0
-        also serves every other learner's submissions until all are done."""
+        also serves every other learner's submissions until all are done.
+        ``debug_delay_s``: sleep after each task (uneven learner speeds)."""
         svc = None
         if self.rank == 0 and self.threaded:
             svc = threading.Thread(target=self._serve_loop, name="metisfl-async-aggregator", daemon=True)
@@ -186,6 +187,9 @@ class AsyncCollectiveFederation:
                 left -= k
                 if self.rank == 0 and not self.threaded:
                     self.serve(block=False)
+            if debug_delay_s:
+                self._sync_stream()
+                time.sleep(debug_delay_s)
             meta = {"task": task, "weight": self._weight(self.num_local_updates),
                     "loss": self.net.train_stats()["loss"], "batches": self.num_local_updates,
                     "base_version": self.base_version}

@@ -108,3 +108,80 @@ def test_hconv_forward_fused_bn(st, rk, train):
                     bnr=_clone(bnr) if bnr is not None else None)
     torch.cuda.synchronize()
     assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("mode", ["mask_bnb", "mask_accum_bnb", "plain"])
+@pytest.mark.parametrize("st", STAGES, ids=lambda s: f"{s[0]}x{s[1]}x{s[2]}")
+def test_hconv_dgrad_fused_bn_backward(st, mode):
+    """dx (+)= conv3x3^T(BN_bwd(dy [* mask]), W) in one launch vs the fp32
+    BatchNorm backward (bn32) it replaces + an fp64 transposed convolution:
+    dx <= 1e-5, the packed dz (wgrad operand), the masked gradient and
+    dgamma / dbeta bit-identical, the consumer-BN sums <= 1e-5."""
+    from metisfl_amd.ops import nn as K
+    from metisfl_amd.ops.optim import split_pack
+    H, W, C = st
+    N = 32
+    mask, accum, bnb_on = "mask" in mode, "accum" in mode, "bnb" in mode
+    shp = K.ConvShape(N, H, W, C, C, 3, 3, 1, 1)
+    ws_n = K.hconv_workspace(shp, torch.device(DEV))
+    g = torch.Generator().manual_seed(7 * H + len(mode))
+    dy = torch.randn(N, H, W, C, generator=g).to(DEV)
+    z = (torch.randn(N, H, W, C, generator=g) * 1.3 + 0.2).to(DEV)
+    ym = torch.randn(N, H, W, C, generator=g).clamp_min(0).to(DEV) if mask else None
+    w = (torch.randn(C, 3, 3, C, generator=g) / (9 * C) ** 0.5).to(DEV)
+    wp = torch.zeros(w.numel(), dtype=torch.int32, device=DEV)
+    split_pack(w.reshape(-1), wp)
+    mean = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    invstd = (0.5 + torch.rand(C, generator=g)).to(DEV)
+    gamma = (0.5 + torch.rand(C, generator=g)).to(DEV)
+    # complete sums of g and g * xhat, spread over two of 8 replicas
+    gd = (dy * (ym > 0) if mask else dy).reshape(-1, C).double().cpu()
+    xh = ((z - mean) * invstd).reshape(-1, C).double().cpu()
+    acc = torch.zeros(8, 2, C, dtype=torch.float64)
+    acc[0, 0], acc[0, 1] = gd[0::2].sum(0), (gd[0::2] * xh[0::2]).sum(0)
+    acc[7, 0], acc[7, 1] = gd[1::2].sum(0), (gd[1::2] * xh[1::2]).sum(0)
+    acc = acc.reshape(-1).to(DEV)
+    bn = K.BnParams(acc, gamma, torch.zeros(C, device=DEV), mean, invstd, None, None)
+    # reference: bn32's backward apply (fp32 dz, packed dz, masked g)
+    dz_ref = torch.empty_like(z)
+    dres_ref = torch.empty_like(z) if mask else None
+    dg_ref, db_ref = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    K.bn_backward(dy, z, ym, C, gamma, mean, invstd, acc, dg_ref, db_ref, dz_ref, dy_masked=dres_ref, presummed=True)
+    dzp_ref = torch.empty(z.shape, dtype=torch.int32, device=DEV)
+    K.bn_backward(dy, z, ym, C, gamma, mean, invstd, acc, None, None, dzp_ref, presummed=True, dx_packed=True)
+    out0 = torch.randn(N, H, W, C, generator=g).to(DEV) if accum else torch.zeros(N, H, W, C, device=DEV)
+    out_ref = F.conv_transpose2d(dz_ref.double().cpu().permute(0, 3, 1, 2), w.double().cpu().permute(0, 3, 1, 2),
+                                 padding=1).permute(0, 2, 3, 1) + out0.double().cpu()
+    bnb = None
+    if bnb_on:
+        zp = torch.randn(N, H, W, C, generator=g).to(DEV)
+        yp_ = torch.randn(N, H, W, C, generator=g).clamp_min(0).to(DEV)
+        bnb = K.BnBwdTarget(zp, yp_, (0.1 * torch.randn(C, generator=g)).to(DEV),
+                            (0.5 + torch.rand(C, generator=g)).to(DEV),
+                            torch.zeros(8 * 2 * C, dtype=torch.float64, device=DEV))
+    # the fused launch
+    out = out0.clone()
+    dzp = torch.zeros(z.shape, dtype=torch.int32, device=DEV)
+    dres = torch.zeros_like(z) if mask else None
+    dgam, dbet = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    ws = torch.zeros(max(4, ws_n), device=DEV)
+    K.hconv_dgrad(dy, ym, z, wp, w, out, shp, bn, dgamma=dgam, dbeta=dbet, ws=ws, dres=dres, dzp=dzp,
+                  accumulate=accum, bnb=bnb)
+    torch.cuda.synchronize()
+    assert _rel(out, out_ref) <= 1e-5
+    assert torch.equal(dzp, dzp_ref)
+    if mask:
+        assert torch.equal(dres, dres_ref)
+    assert torch.equal(dgam, dg_ref) and torch.equal(dbet, db_ref)
+    if bnb_on:
+        o2 = out_ref.reshape(-1, C)
+        gk = o2 * (bnb.y.double().cpu().reshape(-1, C) > 0)
+        xk = ((bnb.z.double().cpu() - bnb.mean.double().cpu()) * bnb.invstd.double().cpu()).reshape(-1, C)
+        s = bnb.acc.reshape(8, 2, C).sum(0).cpu()
+        assert (s[0] - gk.sum(0)).norm() / gk.abs().sum(0).norm() <= 1e-5
+        assert (s[1] - (gk * xk).sum(0)).norm() / (gk * xk).abs().sum(0).norm() <= 1e-5
+    # split-K tickets re-arm: a second launch gives the same bits
+    out2 = out0.clone()
+    K.hconv_dgrad(dy, ym, z, wp, w, out2, shp, bn, ws=ws, accumulate=accum)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
