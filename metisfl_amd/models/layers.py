@@ -81,6 +81,8 @@ class Workspace:
 
 # Host-side tests run the fused-fill orchestration on the CPU references.
 FUSED_FILL_CPU = os.environ.get("METISFL_AMD_FUSED_FILL_CPU", "0") == "1"
+# halo dgrad with the BatchNorm backward in its fill (see ConvBN.backward)
+HALO_DGRAD = os.environ.get("MFL_HALO_DGRAD", "0") == "1"
 
 
 class Pending:
@@ -284,6 +286,20 @@ class ConvBN(Layer):
         reductions; ``bnb``: the BN whose upstream gradient ``dx`` is (its
         reductions are fused into this layer's dgrad epilogue)."""
         s = self.shp
+        if HALO_DGRAD and dx is not None and presummed and side is None and self.hconv_ok():
+            # halo dgrad: the BN backward runs in its operand fill and its
+            # owner tiles write dz packed for the wgrad.  Opt-in: measured on
+            # MI355X (scripts/hdgrad_bench.py) the halo dgrad beats BN apply +
+            # im2col dgrad (19.9 vs 23.7 us at 32x32x64), but the wgrad then
+            # runs alone (19.4 us) instead of inside the paired launch, where
+            # dgrad + wgrad take 27.6 us: 38.9 vs 36.1 us per layer
+            bnp = K.BnParams(self.ws.acc(self.acc_b), self.gamma, self.beta, self.mean, self.invstd, None, None)
+            dzp = self.dz.view(torch.int32) if self.dz.is_cuda else self.dz
+            K.hconv_dgrad(dy, self.y if self.relu else None, self.z, self.wp, self.w16, dx, s, bnp,
+                          dgamma=self.dgamma, dbeta=self.dbeta, ws=self._split(), dres=dres, dzp=dzp,
+                          accumulate=accumulate, bnb=bnb)
+            K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True, dy_packed=self.dz.is_cuda, xp=self.xp)
+            return
         # bf16x3 conv products: dz is only ever read by this layer's dgrad and
         # wgrad, so the BN backward writes it as their packed operand encoding
         pk = self.dz.is_cuda and self.dz.dtype == torch.float32 and K.conv_products() == "bf16x3"

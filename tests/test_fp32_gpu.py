@@ -353,12 +353,16 @@ def _x8(x):
     return F.pad(torch.as_tensor(x), (0, 5))
 
 
-@pytest.mark.parametrize("conv_products", ["exact", "bf16x3"])
-def test_fp32_resnet18_step_matches_torch_nn(conv_products):
+@pytest.mark.parametrize("conv_products", ["exact", "bf16x3", "bf16x3_halo_dgrad"])
+def test_fp32_resnet18_step_matches_torch_nn(conv_products, monkeypatch):
     """The whole fp32 training step (gather -> 20 conv/BN layers -> head ->
     backward) vs an independent torch.nn ResNet-18 in fp64, for both fp32
-    convolution product modes."""
+    convolution product modes (and the opt-in halo dgrad backward)."""
+    from metisfl_amd.models import layers as L
     from metisfl_amd.models.resnet import ResNet18
+    if conv_products.endswith("_halo_dgrad"):
+        monkeypatch.setattr(L, "HALO_DGRAD", True)
+        conv_products = "bf16x3"
     from metisfl_amd.ops.optim import OptimizerSpec
     from tests.torch_resnet_ref import reference_step
     rng = np.random.default_rng(0)

@@ -12,9 +12,10 @@ from metisfl_amd.ops import nn as K
 from metisfl_amd.ops.optim import OptimizerSpec
 
 
-def _net(fused: bool, monkeypatch):
+def _net(fused: bool, monkeypatch, halo_dgrad: bool = False):
     from metisfl_amd.models.resnet import ResNet18
     monkeypatch.setattr(L, "FUSED_FILL_CPU", fused)
+    monkeypatch.setattr(L, "HALO_DGRAD", halo_dgrad)
     net = ResNet18(batch_size=8, optimizer=OptimizerSpec("momentum_sgd", 0.01, momentum=0.9), seed=5)
     net.zero_grad_in_optimizer = False
     return net
@@ -29,12 +30,13 @@ def test_hconv_workspace_covers_the_resnet_stages():
     assert K.hconv_workspace(K.ConvShape(4, 4, 4, 512, 512, 3, 3, 1, 1), dev) == -1  # 8-image tiles
 
 
-def test_fused_fill_matches_bn_apply_orchestration(monkeypatch):
+@pytest.mark.parametrize("halo_dgrad", [False, True], ids=["pair_bwd", "halo_dgrad"])
+def test_fused_fill_matches_bn_apply_orchestration(monkeypatch, halo_dgrad):
     rng = np.random.default_rng(3)
     x = rng.standard_normal((16, 32, 32, 3)).astype(np.float32)
     y = rng.integers(0, 10, 16)
     ref = _net(False, monkeypatch)
-    fus = _net(True, monkeypatch)
+    fus = _net(True, monkeypatch, halo_dgrad)
     assert not ref.fused_fill() and fus.fused_fill()
     assert torch.equal(ref.state.model32, fus.state.model32)
     for net in (ref, fus):
