@@ -70,7 +70,17 @@ def main():
         def hdgrad():
             K.hconv_dgrad(dy, ym, z, wp, w, dx, shp, bn, dgamma=dg, dbeta=db, ws=ws, dres=dres, dzp=dzp, bnb=bnb)
 
-        fns = (("bnbwd+pair", lambda: (bnbwd(), pair())), ("bnbwd", bnbwd), ("pair", pair), ("dgrad", dgrad),
+        side = torch.cuda.Stream()
+
+        def hdgrad_par_wgrad():  # the wgrad on a second stream, concurrent with the halo dgrad
+            cur = torch.cuda.current_stream()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                wgrad()
+            hdgrad()
+            cur.wait_stream(side)
+
+        fns = (("hdgrad||wgrad", hdgrad_par_wgrad), ("bnbwd+pair", lambda: (bnbwd(), pair())), ("bnbwd", bnbwd), ("pair", pair), ("dgrad", dgrad),
                ("wgrad", wgrad), ("hdgrad", hdgrad), ("hdgrad+wgrad", lambda: (hdgrad(), wgrad())))
         graphs = {}
         for name, fn in fns:
