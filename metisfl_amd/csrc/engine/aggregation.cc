@@ -213,13 +213,23 @@ void RollingAverageBase::initialize(const ModelT* m, double w) {
 
 void RollingAverageBase::update_scaled(const ModelT* existing, const ModelT* latest,
                                        double w_existing, double w_new) {
+  bool existing_done = !(existing && !existing->empty());
   if (dev_ >= 0) {
     auto* d = DeviceAggregator::get();
-    if (existing && !existing->empty()) d->roll_merge(dev_, *existing, w_existing, 1);
-    d->roll_merge(dev_, *latest, w_new, 0);
-    return;
+    try {
+      if (!existing_done) d->roll_merge(dev_, *existing, w_existing, 1);
+      existing_done = true;
+      d->roll_merge(dev_, *latest, w_new, 0);
+      return;
+    } catch (const std::runtime_error&) {
+      // no room on the device for this merge's operand: the rolling state
+      // continues on the host from the device's scaled sum (what the host
+      // path holds at this point), so the aggregation does not fail
+      d->roll_fetch(dev_, scaled_, 1.0, 4);
+      release_device();
+    }
   }
-  if (existing && !existing->empty()) merge_models(scaled_, *existing, w_existing, 1);
+  if (!existing_done) merge_models(scaled_, *existing, w_existing, 1);
   merge_models(scaled_, *latest, w_new, 0);
 }
 

@@ -226,6 +226,7 @@ class Impl final : public DeviceAggregator {
       finish(in, cold);
       return -1;
     }
+    resident_bytes_ += r.lay.total;  // the rolling state counts against the HBM budget
     r.meta.vars.resize(m.vars.size());
     for (size_t v = 0; v < m.vars.size(); ++v) {
       auto& mv = r.meta.vars[v];
@@ -277,6 +278,7 @@ class Impl final : public DeviceAggregator {
     if (it == rolls_.end()) return;
     hipStreamSynchronize(compute_);
     hipFree(it->second.dev);
+    resident_bytes_ -= it->second.lay.total;
     rolls_.erase(it);
   }
 

@@ -134,3 +134,36 @@ def test_grpc_controller_stages_and_aggregates_on_device(tmp_path):
     assert s1["fedavg_calls"] - s0.get("fedavg_calls", 0) >= 2
     assert s1["resident_hits"] - s0.get("resident_hits", 0) >= 6 * 2
     assert s1["cold_uploads"] == s0.get("cold_uploads", 0)
+
+
+def test_rolling_state_falls_back_to_host_when_hbm_budget_is_exhausted(tmp_path):
+    """FedStride with a device budget that holds the rolling state but not the
+    next operand: the merge continues on the host from the device's scaled
+    sum instead of failing, byte-identical to the host rule (own process: the
+    budget is read when the device aggregator starts)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"""
+import sys
+sys.path.insert(0, {root!r})
+import numpy as np
+from metisfl_amd import _engine as E
+from tests.test_device_aggregation_gpu import _rand_model
+rng = np.random.default_rng(11)
+ms = [_rand_model(rng) for _ in range(5)]
+ws = list(rng.random(5))
+E.set_device_aggregation(False)
+host = E.aggregate_models("fed_stride", ms, ws, 1)
+E.set_device_aggregation(True, 0)
+dev = E.aggregate_models("fed_stride", ms, ws, 1)
+st = E.device_aggregation_stats()
+print("RESULT", host == dev, st["rolling_calls"], flush=True)
+"""
+    env = dict(os.environ, METISFL_AMD_DEVICE_AGG_MAX_GB=str(2.2e6 / (1 << 30)), PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT")][0].split()
+    assert line[1] == "True"
+    assert int(line[2]) >= 1  # the rolling state did start on the device
