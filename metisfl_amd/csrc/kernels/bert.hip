@@ -552,10 +552,20 @@ __device__ __forceinline__ void colsum_tile(const f32x4 (&acc)[NI][4], float* cs
 // NW waves per workgroup, kT / NW query rows (and key rows) per wave.  The
 // K/V/Q/dO + P/dS tiles take 130 KiB of LDS (one workgroup per CU), so the
 // wave count is the only occupancy lever: NW = 8 runs two waves per SIMD.
+//
+// attn_bwd_body: one (sequence, head) item whose Q, K, V, dO tiles, D = rowsum
+// (dO * O) and lse are staged in LDS and whose bias-gradient partials cs are
+// zero.  Its barriers are LDS-only (lgkmcnt + s_barrier): the persistent
+// kernel keeps the NEXT item's operand loads and this item's output stores in
+// flight across them (__syncthreads would drain vmcnt).
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+}
+
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
-  constexpr int RW = kT / NW, NI = RW / 16, NT = 64 * NW;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+__device__ __forceinline__ void attn_bwd_body(const AttnArgs& a, int b, int h, uint8_t* smem, int tid) {
+  constexpr int RW = kT / NW, NI = RW / 16;
   constexpr int HT = kT * kD * 2;  // 16 KiB head tile
   uint8_t* Qs = smem;
   uint8_t* Ks = smem + HT;
@@ -566,37 +576,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
   float* Dd = reinterpret_cast<float*>(dSs + kT * kT * 2);
   float* Ls = Dd + kT;
   float* cs = Ls + kT;  // [3][64] bias-gradient partials
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int b = blockIdx.x / a.heads, h = blockIdx.x - b * a.heads;
+  const int lane = tid & 63, wave = tid >> 6;
   const int H = a.heads * kD, ld = 3 * H;
   const int64_t row0 = (int64_t)b * kT;
-  load_head<NT>(Qs, a.qkv, row0, ld, h * kD);
-  load_head<NT>(Ks, a.qkv, row0, ld, H + h * kD);
-  load_head<NT>(Vs, a.qkv, row0, ld, 2 * H + h * kD);
-  if (threadIdx.x < 2 * kT) {
-    // dO into LDS and D[t] = sum_d dO[t][d] * O[t][d]: thread -> row tid/2, half tid&1
-    const int r = threadIdx.x >> 1, half = threadIdx.x & 1;
-    float dsum = 0.f;
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
-      const int col = half * 32 + cc * 8;
-      const uint4 dov = *reinterpret_cast<const uint4*>(a.dctx + (row0 + r) * H + h * kD + col);
-      const uint4 ov = *reinterpret_cast<const uint4*>(a.ctx + (row0 + r) * H + h * kD + col);
-      *reinterpret_cast<uint4*>(dOs + toff<128>(r, col)) = dov;
-      float f1[8], f2[8];
-      unpack8(dov, f1);
-      unpack8(ov, f2);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) dsum += f1[k] * f2[k];
-    }
-    dsum += __shfl_xor(dsum, 1);
-    if (!half) {
-      Dd[r] = dsum;
-      Ls[r] = a.lse[((int64_t)b * a.heads + h) * kT + r];
-    }
-  }
-  if (threadIdx.x < 3 * kD) cs[threadIdx.x] = 0.f;
-  __syncthreads();
   const int t0 = wave * RW;
   const float c = a.scale * kLog2e;
   {
@@ -670,7 +652,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
         }
     colsum_tile(acc, cs, lane, a.scale);
   }
-  __syncthreads();  // every wave's P and dS rows are in LDS
+  lds_sync();  // every wave's P and dS rows are in LDS
   // dK = scale * dS^T Q and dV = P^T dO for key rows s0 .. s0+31
   {
     const int s0 = wave * RW;
@@ -712,11 +694,141 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
     colsum_tile(dk, cs + kD, lane, a.scale);
     colsum_tile(dv, cs + 2 * kD, lane, 1.f);
   }
-  __syncthreads();
-  if (a.dbias && threadIdx.x < 3 * kD) {
-    const int part = threadIdx.x / kD, d = threadIdx.x - part * kD;
-    atomicAdd(a.dbias + part * H + h * kD + d, cs[threadIdx.x]);
+  lds_sync();
+  if (a.dbias && tid < 3 * kD) {
+    const int part = tid / kD, d = tid - part * kD;
+    atomicAdd(a.dbias + part * H + h * kD + d, cs[tid]);
   }
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
+  constexpr int NT = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int HT = kT * kD * 2;
+  uint8_t* Qs = smem;
+  uint8_t* Ks = smem + HT;
+  uint8_t* Vs = smem + 2 * HT;
+  uint8_t* dOs = smem + 3 * HT;
+  float* Dd = reinterpret_cast<float*>(smem + 4 * HT + 2 * kT * kT * 2);
+  float* Ls = Dd + kT;
+  float* cs = Ls + kT;
+  const int b = blockIdx.x / a.heads, h = blockIdx.x - b * a.heads;
+  const int H = a.heads * kD, ld = 3 * H;
+  const int64_t row0 = (int64_t)b * kT;
+  load_head<NT>(Qs, a.qkv, row0, ld, h * kD);
+  load_head<NT>(Ks, a.qkv, row0, ld, H + h * kD);
+  load_head<NT>(Vs, a.qkv, row0, ld, 2 * H + h * kD);
+  if (threadIdx.x < 2 * kT) {
+    // dO into LDS and D[t] = sum_d dO[t][d] * O[t][d]: thread -> row tid/2, half tid&1
+    const int r = threadIdx.x >> 1, half = threadIdx.x & 1;
+    float dsum = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const int col = half * 32 + cc * 8;
+      const uint4 dov = *reinterpret_cast<const uint4*>(a.dctx + (row0 + r) * H + h * kD + col);
+      const uint4 ov = *reinterpret_cast<const uint4*>(a.ctx + (row0 + r) * H + h * kD + col);
+      *reinterpret_cast<uint4*>(dOs + toff<128>(r, col)) = dov;
+      float f1[8], f2[8];
+      unpack8(dov, f1);
+      unpack8(ov, f2);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dsum += f1[k] * f2[k];
+    }
+    dsum += __shfl_xor(dsum, 1);
+    if (!half) {
+      Dd[r] = dsum;
+      Ls[r] = a.lse[((int64_t)b * a.heads + h) * kT + r];
+    }
+  }
+  if (threadIdx.x < 3 * kD) cs[threadIdx.x] = 0.f;
+  __syncthreads();
+  attn_bwd_body<NW>(a, b, h, smem, threadIdx.x);
+}
+
+// Persistent variant (8 waves, one workgroup per CU, grid <= #CUs): each
+// workgroup walks items it, it + grid, ...; the NEXT item's Q, K, V, dO, O
+// tiles (80 KiB) are requested into registers (10 x 16 B per thread) right
+// after the current item's tiles were staged, so the operand latency of item
+// i + 1 hides under item i's MFMAs and stores instead of following them (the
+// per-item launch pays load -> compute -> store in series, 6 items per CU).
+// D = rowsum(dO * O) is reduced from the registers (8 lanes per row).
+__device__ __forceinline__ float dot8(const uint4& x, const uint4& y) {
+  float f1[8], f2[8];
+  unpack8(x, f1);
+  unpack8(y, f2);
+  float d = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d += f1[k] * f2[k];
+  return d;
+}
+
+__device__ __forceinline__ uint4 ldg16(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+__global__ __launch_bounds__(512) void attn_bwd_persist_kernel(AttnArgs a, int nitems) {
+  constexpr int HT = kT * kD * 2;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  float* Dd = reinterpret_cast<float*>(smem + 4 * HT + 2 * kT * kT * 2);
+  float* Ls = Dd + kT;
+  float* cs = Ls + kT;
+  const int H = a.heads * kD, ld = 3 * H;
+  // per thread: two 16-B chunks (rows r, r + 64; column chunk cc) of each of
+  // Q, K, V, dO, O of the next item, and one lse value
+  const int r = threadIdx.x >> 3, cc = (threadIdx.x & 7) * 8;
+  const int off0 = toff<128>(r, cc), off1 = toff<128>(r + 64, cc);
+  uint4 q0, q1, k0, k1, v0, v1, d0, d1, o0, o1;
+  float pl;
+#define MFL_ATTN_FETCH(ITEM)                                                              \
+  {                                                                                       \
+    const int b_ = (ITEM) / a.heads, h_ = (ITEM) - b_ * a.heads;                          \
+    const uint16_t* qp = a.qkv + ((int64_t)b_ * kT + r) * ld + h_ * kD + cc;              \
+    const int64_t q64 = (int64_t)64 * ld;                                                 \
+    q0 = ldg16(qp); q1 = ldg16(qp + q64);                                                 \
+    k0 = ldg16(qp + H); k1 = ldg16(qp + H + q64);                                         \
+    v0 = ldg16(qp + 2 * H); v1 = ldg16(qp + 2 * H + q64);                                 \
+    const int64_t o_ = ((int64_t)b_ * kT + r) * H + h_ * kD + cc, o64 = (int64_t)64 * H;  \
+    d0 = ldg16(a.dctx + o_); d1 = ldg16(a.dctx + o_ + o64);                               \
+    o0 = ldg16(a.ctx + o_); o1 = ldg16(a.ctx + o_ + o64);                                 \
+    pl = threadIdx.x < kT ? a.lse[((int64_t)b_ * a.heads + h_) * kT + threadIdx.x] : 0.f; \
+  }
+  int it = blockIdx.x;  // grid <= nitems
+  MFL_ATTN_FETCH(it)
+  for (; it < nitems; it += gridDim.x) {
+    // stage this item from the registers: Q K V dO tiles at smem + u * HT
+    *reinterpret_cast<uint4*>(smem + off0) = q0;
+    *reinterpret_cast<uint4*>(smem + off1) = q1;
+    *reinterpret_cast<uint4*>(smem + HT + off0) = k0;
+    *reinterpret_cast<uint4*>(smem + HT + off1) = k1;
+    *reinterpret_cast<uint4*>(smem + 2 * HT + off0) = v0;
+    *reinterpret_cast<uint4*>(smem + 2 * HT + off1) = v1;
+    *reinterpret_cast<uint4*>(smem + 3 * HT + off0) = d0;
+    *reinterpret_cast<uint4*>(smem + 3 * HT + off1) = d1;
+    float s0 = dot8(d0, o0), s1 = dot8(d1, o1);  // D = rowsum(dO * O): 8 lanes per row
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      s0 += __shfl_xor(s0, m);
+      s1 += __shfl_xor(s1, m);
+    }
+    if ((threadIdx.x & 7) == 0) {
+      Dd[r] = s0;
+      Dd[r + 64] = s1;
+    }
+    if (threadIdx.x < kT) Ls[threadIdx.x] = pl;
+    if (threadIdx.x < 3 * kD) cs[threadIdx.x] = 0.f;
+    lds_sync();
+    const int b = it / a.heads, h = it - b * a.heads;
+    // the next item's tiles fly under this item (the last round re-reads its
+    // own item: unconditional, so the prefetch stays in registers)
+    MFL_ATTN_FETCH(min(it + (int)gridDim.x, nitems - 1))
+    // the lane-derived fragment addresses are recomputed per item (an opaque
+    // thread id): hoisted out of the item loop they stayed live across the
+    // whole body (256 VGPRs + spills instead of ~100 + the prefetch)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    attn_bwd_body<8>(a, b, h, smem, tid);
+    lds_sync();  // every wave is done with this item's LDS before the next staging
+  }
+#undef MFL_ATTN_FETCH
 }
 
 static void lds_attr(const void* k, size_t bytes, bool& done) {
@@ -734,12 +846,26 @@ void launch_attn_fwd(const AttnArgs& a, hipStream_t s) {
 }
 
 void launch_attn_bwd(const AttnArgs& a, hipStream_t s) {
-  // 8 waves by default; MFL_ATTN_BWD_WAVES=4 for the one-wave-per-SIMD variant
+  // persistent 8-wave kernel by default; MFL_ATTN_BWD_PERSIST=0: one launch
+  // item per workgroup (MFL_ATTN_BWD_WAVES=4 for its one-wave-per-SIMD variant)
+  const char* pv = getenv("MFL_ATTN_BWD_PERSIST");  // read per launch (tests toggle it)
+  const int persist = pv && *pv == '0' ? 0 : 1;
   static const int nw = [] {
     const char* v = getenv("MFL_ATTN_BWD_WAVES");
     return v && *v == '4' ? 4 : 8;
   }();
-  static bool done4 = false, done8 = false;
+  static bool done4 = false, done8 = false, donep = false;
+  const int nitems = a.batch * a.heads;
+  if (persist) {
+    static const int ncu = [] {
+      int dev = 0, n = 256;
+      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      return n > 0 ? n : 256;
+    }();
+    lds_attr(reinterpret_cast<const void*>(&attn_bwd_persist_kernel), attn_bwd_lds(), donep);
+    attn_bwd_persist_kernel<<<std::min(nitems, ncu), 512, attn_bwd_lds(), s>>>(a, nitems);
+    return;
+  }
   if (nw == 4) {
     lds_attr(reinterpret_cast<const void*>(&attn_bwd_kernel<4>), attn_bwd_lds(), done4);
     attn_bwd_kernel<4><<<a.batch * a.heads, 256, attn_bwd_lds(), s>>>(a);

@@ -258,3 +258,34 @@ def test_bert_base_graph_step_runs():
     assert int(net.state.step.cpu()) == 3  # the optimizer launch's fused step tick
     s = net.train_stats()
     assert np.isfinite(s["loss"]) and abs(s["loss"] - math.log(c.vocab)) < 1.5, s
+
+
+def test_attention_bwd_persistent_matches_per_item_launch(monkeypatch):
+    """The persistent attention backward (next item's tiles prefetched into
+    registers, 576 items over <= 256 workgroups) computes exactly what the
+    one-item-per-workgroup launch does: D = rowsum(dO * O) is summed in a
+    different order (8-lane tree vs 2 x 32 sequential), so dq/dk/dv agree up
+    to that fp32 rounding (bf16 outputs: nearly all bits equal)."""
+    from metisfl_amd.ops import bert as BO
+    _native()
+    torch.manual_seed(9)
+    B, heads = 48, 12
+    T, H = 128, heads * 64
+    qkv = (torch.randn(B * T, 3 * H) * 1.5).to(BF).to(DEV)
+    dctx = torch.randn(B * T, H).to(BF).to(DEV)
+    scale = 1.0 / math.sqrt(64)
+    ctx = torch.empty(B * T, H, dtype=BF, device=DEV)
+    lse = torch.zeros(B * heads * T, device=DEV)
+    BO.attn_fwd(qkv, ctx, lse, B, heads, scale)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MFL_ATTN_BWD_PERSIST", mode)
+        dqkv = torch.empty(B * T, 3 * H, dtype=BF, device=DEV)
+        db = torch.zeros(3 * H, device=DEV)
+        BO.attn_bwd(qkv, ctx, lse, dctx, dqkv, B, heads, scale, dbias=db)
+        torch.cuda.synchronize()
+        out[mode] = (dqkv, db)
+    a, b = out["1"][0], out["0"][0]
+    assert rel(a, b) < 1e-3
+    assert (a == b).float().mean().item() > 0.99
+    assert rel(out["1"][1], out["0"][1]) < 1e-4
