@@ -368,6 +368,121 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(BigGemmArgs p) {
   big_epilogue<OUT32>(p, acc, smem, m0, n0, wm, wn, wave, lane);
 }
 
+// ---- half-height tiles, two workgroups per CU (MFL_GB_PIPE=3) -------------------
+// 128 x 256 output per workgroup, 4 waves (1 x 4, the same 128 x 64 per wave
+// and accumulator layout as the 256^2 kernels), BK = 32 through a 3-stage
+// ring: 72 KiB of LDS and <= 128 VGPRs... so TWO workgroups share a CU.  The
+// one-workgroup-per-CU kernels run their output stage (100-200 MB per call)
+// in lock step on every CU, with no MFMA work beside it (profiles/ANALYSIS.md,
+// BERT section: 8-31 us per call); here the two co-resident workgroups drift
+// apart, so one's epilogue overlaps the other's k-loop.  Costs 1.5x the
+// L2 -> LDS operand bytes of the 256^2 tile (A rows shared by half as many
+// columns).  Forward / dgrad (bf16 output) only.  Measured (negative, kept
+// opt-in): 15-30 % SLOWER than the ping-pong kernel on every BERT shape
+// (qkv fwd 96.0 vs 81.2 us, ffn2 fwd 93.3 vs 68.8;
+// profiles/r3/bert/gemm_sweep_h2_vs_pp.log) -- the extra operand traffic and
+// the BK = 32 barrier per k-step cost more than the overlap returns.
+template <bool T, int BK, int ROWS, int NW>
+__device__ __forceinline__ void stage_rows(__amdgpu_buffer_rsrc_t rs, int ld, int row0, int k0, uint8_t* dst,
+                                           int wave, int lane) {
+  constexpr int NI = ROWS * BK * 2 / 1024 / NW;
+  static_assert(!T || ROWS == 256, "[k][row] tiles: 512-B k-rows");
+#pragma unroll
+  for (int u = 0; u < NI; ++u) {
+    const int i = wave + NW * u;  // 1-KiB instruction index within the tile
+    uint32_t off;
+    if constexpr (!T) {
+      constexpr int RPI = 512 / BK, CPR = BK / 8;
+      const int row = RPI * i + lane / CPR;
+      const int lc = (lane % CPR) ^ swz_b128<2 * BK>(row);
+      off = (uint32_t)((row0 + row) * ld + k0 + 8 * lc) * 2u;
+    } else {
+      const int kr = 2 * i + (lane >> 5);
+      const int lc = (lane & 31) ^ swz_tr<512>(kr);
+      off = (uint32_t)((k0 + kr) * ld + row0 + 8 * lc) * 2u;
+    }
+    dma16(rs, off, dst + i * 1024);
+  }
+}
+
+template <bool BT>
+__global__ __launch_bounds__(256, 2) void gemm_h2_kernel(BigGemmArgs p) {
+  constexpr int BK = 32, NST = 3, BMH = 128;
+  constexpr int A_B = BMH * BK * 2, STG = A_B + GB_BN * BK * 2;  // 8 + 16 KiB per stage
+  constexpr int L = (A_B + GB_BN * BK * 2) / 1024 / 4;           // DMA instructions per wave per k-tile
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wn = wave;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int tiles_n = (p.N + GB_BN - 1) / GB_BN;
+  const int m0 = (wgid / tiles_n) * BMH;
+  const int n0 = (wgid - (wgid / tiles_n) * tiles_n) * GB_BN;
+  const auto rsA = make_rsrc(p.a, p.a_bytes);
+  const auto rsB = make_rsrc(p.b, p.b_bytes);
+  const int nk = p.K / BK;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](int kt, int stage) {
+    uint8_t* st = smem + stage * STG;
+    stage_rows<false, BK, BMH, 4>(rsA, p.lda, m0, kt * BK, st, wave, lane);
+    stage_rows<BT, BK, GB_BN, 4>(rsB, p.ldb, n0, kt * BK, st + A_B, wave, lane);
+  };
+  auto compute = [&](int stage) {
+    const uint8_t* As = smem + stage * STG;
+    const uint8_t* Bs = As + A_B;
+    bf16x8 bfr[4], af[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = frag<BT, BK>(Bs, 0, wn * 64 + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = frag<false, BK>(As, 0, 16 * i, lane);
+    if constexpr (BT) frags_ready(bfr);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  constexpr int D = NST - 1;
+#pragma unroll
+  for (int u = 0; u < D; ++u)
+    if (u < nk) issue(u, u);
+  int stage = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (nk - 1 - kt >= 1) wait_vm<L>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_barrier();  // everyone's tile kt landed; everyone done reading stage (kt-1)%NST
+    if (kt + D < nk) issue(kt + D, stage == 0 ? NST - 1 : stage - 1);
+    compute(stage);
+    stage = stage == NST - 1 ? 0 : stage + 1;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  lds_barrier();  // the ring is free for the epilogue staging
+  big_epilogue<false, 64>(p, acc, smem, m0, n0, 0, wn, wave, lane);
+}
+
+template <bool BT>
+void launch_h2_t(const BigGemmArgs& p, hipStream_t s) {
+  constexpr size_t kLds = 3 * (128 * 32 * 2 + 256 * 32 * 2);  // 72 KiB (>= the 4-wave epilogue staging)
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_h2_kernel<BT>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
+    attr = true;
+  }
+  const dim3 grid((unsigned)(((p.M + 127) / 128) * ((p.N + GB_BN - 1) / GB_BN)), 1);
+  gemm_h2_kernel<BT><<<grid, 256, kLds, s>>>(p);
+}
+
 // ---- ping-pong pipeline (MFL_GB_PIPE=2) ---------------------------------------
 // The same 256x256 tile and wave layout, scheduled after the guide's 256^2
 // 8-phase template (cdna_hip_programming.md §5): each k-tile is split into 4
@@ -679,11 +794,18 @@ void launch_big(BigGemmArgs p, int kdim, hipStream_t s) {
     return v && *v ? atoi(v) : 0;
   }();
   p.dbg = dbg;
-  const int bk = gb_pipe() == 1 ? 32 : 64;
+  const int bk = gb_pipe() == 1 ? 32 : 64;  // (the half-height kernel re-derives its own k-tiles)
   // p.kt_per_split arrives in units of GB_KQ (64) k-elements
   p.kt_per_split *= GB_KQ / bk;
   (void)kdim;
-  if (gb_pipe() == 2) {
+  if constexpr (!OUT32 && !AT) {
+    if (gb_pipe() == 3 && p.M % 128 == 0 && p.N % GB_BN == 0 && p.K % 32 == 0) {
+      p.kt_per_split = p.K / 32;
+      launch_h2_t<BT>(p, s);
+      return;
+    }
+  }
+  if (gb_pipe() == 2 || gb_pipe() == 3) {
     if (pp_width(p) == 192) launch_pp_t<AT, BT, OUT32, 192>(p, s);
     else launch_pp_t<AT, BT, OUT32, 256>(p, s);
   }
@@ -748,7 +870,7 @@ int64_t gemm_big_wgrad_workspace(int M, int N, int K) {
     return !(e && *e == '0');
   }();
   const int sp = wgrad_splits_env(M, N, K);
-  return (slabs && gb_pipe() == 2 && sp > 1) ? (int64_t)sp * N * K : 0;
+  return (slabs && (gb_pipe() == 2 || gb_pipe() == 3) && sp > 1) ? (int64_t)sp * N * K : 0;
 }
 
 void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,
