@@ -495,6 +495,69 @@ void head32_forward_backward(torch::Tensor x, int64_t B, int64_t HW, int64_t C, 
                              fuse ? fp(*dW) : nullptr, fuse ? opt_ptr<float>(db) : nullptr);
 }
 
+// The fp32 head with the last block's BatchNorm (+ residual, + ReLU) applied
+// in its pooling loop and, in train mode, the BN-backward sums of dx added
+// into acc_b (the caller then runs that BN's backward presummed).
+void head32_forward_backward_bn(int64_t B, int64_t HW, int64_t C, torch::Tensor W, c10::optional<torch::Tensor> bias,
+                                torch::Tensor labels, c10::optional<torch::Tensor> feat,
+                                c10::optional<torch::Tensor> dlogits, c10::optional<torch::Tensor> dx,
+                                c10::optional<torch::Tensor> stats, bool backward, c10::optional<torch::Tensor> dW,
+                                c10::optional<torch::Tensor> db, torch::Tensor z, torch::Tensor res,
+                                c10::optional<torch::Tensor> acc, torch::Tensor gamma, torch::Tensor beta,
+                                torch::Tensor mean, torch::Tensor invstd, torch::Tensor run_mean,
+                                torch::Tensor run_var, double momentum, double eps, bool train, torch::Tensor y,
+                                c10::optional<torch::Tensor> acc_b) {
+  const int64_t n = B * HW * C;
+  check_f32(z, n, "head z");
+  check_f32(res, n, "head res");
+  check_f32(y, n, "head y");
+  for (auto* t : {&gamma, &beta, &mean, &invstd, &run_mean, &run_var}) check_pc(*t, C, "head bn param");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "head: C must be a multiple of 8 (<= 2048)");
+  check_f32(W, 0, "head W", false);
+  TORCH_CHECK(W.numel() % C == 0, "head W");
+  const int64_t K = W.numel() / C;
+  TORCH_CHECK(K <= 1024, "head: K <= 1024");
+  TORCH_CHECK(labels.is_cuda() && labels.is_contiguous() && labels.scalar_type() == torch::kInt32 &&
+                  labels.numel() >= B, "labels");
+  mfl::HeadBn hb;
+  hb.z = fp(z);
+  hb.res = fp(res);
+  if (train) {
+    TORCH_CHECK(acc.has_value() && acc->defined(), "train-mode BN needs its statistics accumulator");
+    hb.acc = acc_ptr(*acc, C);
+    hb.reps = reps_of(*acc, C);
+    TORCH_CHECK(hb.reps <= 8, "at most 8 BN accumulator replicas");
+  }
+  hb.gamma = fp(gamma);
+  hb.beta = fp(beta);
+  hb.mean = fp(mean);
+  hb.invstd = fp(invstd);
+  hb.run_mean = fp(run_mean);
+  hb.run_var = fp(run_var);
+  hb.momentum = (float)momentum;
+  hb.eps = (float)eps;
+  hb.train = train ? 1 : 0;
+  hb.y = fp(y);
+  if (backward && acc_b.has_value() && acc_b->defined()) {
+    hb.acc_b = const_cast<double*>(acc_ptr(*acc_b, C));
+    hb.reps_b = reps_of(*acc_b, C);
+  }
+  const bool fuse = dW.has_value() && dW->defined();
+  if (fuse) {
+    check_f32(*dW, K * C, "head dW");
+    if (db.has_value() && db->defined()) check_f32(*db, K, "head db");
+  }
+  if (backward) {
+    TORCH_CHECK(feat.has_value() && dlogits.has_value() && dx.has_value(), "bwd buffers");
+    TORCH_CHECK(feat->numel() >= B * C && dlogits->numel() >= B * K, "bwd buffer sizes");
+    check_f32(*dx, n, "head dx");
+  }
+  mfl::launch_head32_fwd_bwd(fp(y), (int)B, (int)HW, (int)C, fp(W), opt_ptr<float>(bias), (int)K,
+                             labels.data_ptr<int>(), opt_ptr<float>(feat), opt_ptr<float>(dlogits),
+                             opt_ptr<float>(dx), opt_ptr<float>(stats), backward, cur_stream(z),
+                             fuse ? fp(*dW) : nullptr, fuse ? opt_ptr<float>(db) : nullptr, &hb);
+}
+
 // fp32 rows are gathered as 16-B units, like the bf16 ones
 void gather_batch32(torch::Tensor shard, torch::Tensor labels, torch::Tensor perm, torch::Tensor step,
                     int64_t steps_per_epoch, int64_t B, torch::Tensor xb, torch::Tensor yb,
@@ -532,5 +595,6 @@ void register_fp32(pybind11::module& m) {
   m.def("bn32_backward", &bn32_backward);
   m.def("bn32_backward_side", &bn32_backward_side);
   m.def("head32_forward_backward", &head32_forward_backward);
+  m.def("head32_forward_backward_bn", &head32_forward_backward_bn);
   m.def("gather_batch32", &gather_batch32);
 }

@@ -6,6 +6,7 @@
 // none, when the dgrad epilogue already summed) plus one apply).
 // Each lane moves 4 channels (one 16-B float4).  C % 4 == 0.
 #include "kernels/common.h"
+#include "kernels/bn_coef.h"
 #include "kernels/launchers.h"
 
 namespace mfl {
@@ -71,7 +72,6 @@ void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_
   bn32_stats_kernel<<<dim3(blocks_for(M, C), gy), 256, 0, s>>>(x, M, C, acc, reps > 0 ? reps : 1);
 }
 
-constexpr int kMaxReps = 8;  // replicas summed per channel (layers.py uses 8 on the fp32 GPU path)
 
 // Grid of the apply kernels.  Every block's prologue re-derives all C
 // channels' coefficients from the 8 fp64 replica pairs (16 loads per
@@ -82,24 +82,6 @@ constexpr int kMaxReps = 8;  // replicas summed per channel (layers.py uses 8 on
 #define MFL_BN32_GRID 512
 #endif
 inline unsigned apply_grid(int64_t nvec) { return stream_grid(nvec, 256, MFL_BN32_GRID); }
-
-// Sum of a channel's replicas: every load issued before the first add (a
-// runtime-bound loop serialised one memory round trip per replica).
-__device__ __forceinline__ void rep_sums(const double* acc, int reps, int C, int c, double& s0, double& s1) {
-  double a[kMaxReps], b[kMaxReps];
-#pragma unroll
-  for (int r = 0; r < kMaxReps; ++r) {
-    a[r] = r < reps ? acc[(int64_t)r * 2 * C + c] : 0.0;
-    b[r] = r < reps ? acc[(int64_t)r * 2 * C + C + c] : 0.0;
-  }
-  s0 = 0.0;
-  s1 = 0.0;
-#pragma unroll
-  for (int r = 0; r < kMaxReps; ++r) {
-    s0 += a[r];
-    s1 += b[r];
-  }
-}
 
 // Main loops: when C / 4 divides 256 the grid stride is a multiple of C / 4,
 // so a lane's channels never change -- its coefficients live in registers
@@ -119,33 +101,12 @@ __device__ __forceinline__ void bn32_apply_body(const BnFwdArgs32& a, int64_t nv
     xv = X[i];
     if (RES) rv = R[i];
   }
-  const double inv_m = 1.0 / (double)a.M;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    double mu, var;
-    if (a.train) {
-      double s0, s1;
-      rep_sums(a.acc, a.reps, C, c, s0, s1);
-      mu = s0 * inv_m;
-      var = s1 * inv_m - mu * mu;
-      if (var < 0.0) var = 0.0;
-    } else {
-      mu = a.run_mean[c];
-      var = a.run_var[c];
-    }
-    const double isd = 1.0 / sqrt(var + (double)a.eps);
-    const float sc = (float)((double)a.gamma[c] * isd);
+    float sc, sh;
+    bn_fwd_coef(a.acc, a.reps, C, c, a.M, a.train, bid == 0, a.gamma, a.beta, a.mean, a.invstd, a.run_mean,
+                a.run_var, a.momentum, a.eps, sc, sh);
     coef[c] = sc;
-    coef[C + c] = (float)((double)a.beta[c] - mu * (double)a.gamma[c] * isd);
-    if (a.train && bid == 0) {
-      a.mean[c] = (float)mu;
-      a.invstd[c] = (float)isd;
-      if (a.run_mean) {
-        const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
-        // explicit fma: the halo conv's fill publishes the same bits (hconv.hip)
-        a.run_mean[c] = fmaf(1.f - a.momentum, a.run_mean[c], a.momentum * (float)mu);
-        a.run_var[c] = fmaf(1.f - a.momentum, a.run_var[c], a.momentum * (float)unb);
-      }
-    }
+    coef[C + c] = sh;
   }
   __syncthreads();
   const int tpr = C / 4;

@@ -698,19 +698,35 @@ __device__ __forceinline__ void conv32_gemm_body(const Conv32Args& a, const Blk&
     float4 sum[F];
 #pragma unroll
     for (int u = 0; u < F; ++u) sum[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int z = 0; z < splits; ++z) {
+    // slabs requested 4 at a time (one memory latency per 4 slices instead
+    // of per slice), summed in slice order (deterministic, serial-sum bits)
+    constexpr int ZB = 4;
+    for (int z0 = 0; z0 < splits; z0 += ZB) {
+      u32x4 sl[ZB][F];
 #pragma unroll
-      for (int u = 0; u < F; ++u) {
-        const int f = t + 256 * u;
-        float4 r;
-        if (z == blk.z) {
-          r = *reinterpret_cast<const float4*>(tile + (f / C4) * TST + (f % C4) * 4);
-        } else {
-          const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rsS, (int)(z * zstride + f * 16), 0, 16);
-          r = make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]),
-                          __uint_as_float(b[3]));
+      for (int zz = 0; zz < ZB; ++zz) {
+        const int z = z0 + zz;
+        if (z >= splits) break;  // uniform: only the real slices' loads issue
+#pragma unroll
+        for (int u = 0; u < F; ++u) {
+          const int f = t + 256 * u;
+          sl[zz][u] = __builtin_amdgcn_raw_buffer_load_b128(
+              rsS, (int)(z != blk.z ? (uint32_t)(z * zstride + f * 16) : kOOB), 0, 16);  // own slice: LDS
         }
-        sum[u] = f4add(sum[u], r);
+      }
+#pragma unroll
+      for (int zz = 0; zz < ZB; ++zz) {
+        const int z = z0 + zz;
+        if (z >= splits) break;
+#pragma unroll
+        for (int u = 0; u < F; ++u) {
+          const int f = t + 256 * u;
+          const u32x4 b = sl[zz][u];
+          const float4 r = z == blk.z ? *reinterpret_cast<const float4*>(tile + (f / C4) * TST + (f % C4) * 4)
+                                      : make_float4(__uint_as_float(b[0]), __uint_as_float(b[1]),
+                                                    __uint_as_float(b[2]), __uint_as_float(b[3]));
+          sum[u] = f4add(sum[u], r);
+        }
       }
     }
     __syncthreads();

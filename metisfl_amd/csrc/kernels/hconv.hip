@@ -638,16 +638,29 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
     float4 sum[F];
 #pragma unroll
     for (int u = 0; u < F; ++u) sum[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int z = 0; z < splits; ++z) {
+    // every other slice's slab is requested at once (one memory latency,
+    // not splits - 1 in series: 2-4 us of the 8-slice 4x4x512 stage), then
+    // summed in slice order (deterministic, the same bits as a serial sum)
+    constexpr int MAXS = 8;  // plan_fwd: at most 8 slices
+    u32x4 sl[MAXS][F];
+#pragma unroll
+    for (int z = 0; z < MAXS; ++z) {
+      if (z >= splits) break;  // uniform: only the real slices' loads issue
 #pragma unroll
       for (int u = 0; u < F; ++u) {
         const int f = t + K::NTHR * u;
-        float4 r;
-        if (z == bz) {
-          r = *reinterpret_cast<const float4*>(tile + (f / C4) * K::TST + (f % C4) * 4);
-        } else {
-          r = as_f4(__builtin_amdgcn_raw_buffer_load_b128(rsS, (int)(z * zstride + f * 16), 0, 16));
-        }
+        sl[z][u] = __builtin_amdgcn_raw_buffer_load_b128(
+            rsS, (int)(z != bz ? (uint32_t)(z * zstride + f * 16) : kOOB), 0, 16);  // own slice: LDS below
+      }
+    }
+#pragma unroll
+    for (int z = 0; z < MAXS; ++z) {
+      if (z >= splits) break;
+#pragma unroll
+      for (int u = 0; u < F; ++u) {
+        const int f = t + K::NTHR * u;
+        const float4 r = z == bz ? *reinterpret_cast<const float4*>(tile + (f / C4) * K::TST + (f % C4) * 4)
+                                 : as_f4(sl[z][u]);
         sum[u] = make_float4(sum[u].x + r.x, sum[u].y + r.y, sum[u].z + r.z, sum[u].w + r.w);
       }
     }

@@ -8,6 +8,7 @@
 // count and sample count are accumulated on device (stats[0..2]) so the
 // training loop never synchronises with the host per step.
 #include "kernels/common.h"
+#include "kernels/bn_coef.h"
 #include "kernels/launchers.h"
 
 namespace mfl {
@@ -48,7 +49,10 @@ __device__ __forceinline__ float hexp(float x) { return sizeof(T) == 4 ? expf(x)
 template <typename T>
 __device__ __forceinline__ float hlog(float x) { return sizeof(T) == 4 ? logf(x) : __logf(x); }
 
-template <typename T>
+// FUSE (fp32 only): the input is relu(BN(z) + res) (HeadBn), applied as the
+// pooling loop reads it; the coefficients are derived per workgroup with
+// bn32_apply's math (bn_coef.h), workgroup 0 publishes them.
+template <typename T, bool FUSE = false>
 __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int HW, int C,
                                                    const float* __restrict__ W,
                                                    const float* __restrict__ bias, int K,
@@ -56,8 +60,8 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
                                                    float* __restrict__ feat, float* __restrict__ dlog,
                                                    T* __restrict__ dx,
                                                    float* __restrict__ stats, int B, int backward,
-                                                   float* __restrict__ dW, float* __restrict__ db) {
-  // feat[C] | logits[K] | partials[R][C] | W[K][C]
+                                                   float* __restrict__ dW, float* __restrict__ db, HeadBn hb) {
+  // feat[C] | logits[K] | partials[R][C] | W[K][C] | FUSE: sc, sh, mean, invstd [4][C]
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* f = sm;
   float* lg = sm + C;
@@ -65,6 +69,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
   const int R = max(1, 256 / G);
   float* part = sm + C + ((K + 3) & ~3);
   float* Ws = part + R * C;
+  float* bc = Ws + K * C;
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
@@ -81,11 +86,35 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
 #pragma unroll 4
     for (int i = t; i < n4; i += 256) Ws4[i] = W4[i];
   }
+  if constexpr (FUSE) {
+    for (int c = t; c < C; c += 256) {
+      float sc, sh, mu, isd;
+      bn_fwd_coef(hb.acc, hb.reps, C, c, (int64_t)B * HW, hb.train != 0, b == 0, hb.gamma, hb.beta, hb.mean,
+                  hb.invstd, hb.run_mean, hb.run_var, hb.momentum, hb.eps, sc, sh, &mu, &isd);
+      bc[c] = sc;
+      bc[C + c] = sh;
+      bc[2 * C + c] = mu;
+      bc[3 * C + c] = isd;
+    }
+    __syncthreads();
+  }
   if (rg < R) {
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int h = rg; h < HW; h += R) {
       float v[8];
-      load8(xb + (int64_t)h * C + 8 * cg, v);
+      if constexpr (FUSE) {
+        // bn32_apply's element math: fmaf(z, sc, sh) + res, then ReLU
+        const int64_t o = ((int64_t)b * HW + h) * C + 8 * cg;
+        float zz[8], rr[8];
+        load8(hb.z + o, zz);
+        load8(hb.res + o, rr);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = fmaxf(fmaf(zz[k], bc[8 * cg + k], bc[C + 8 * cg + k]) + rr[k], 0.f);
+        reinterpret_cast<float4*>(hb.y + o)[0] = make_float4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<float4*>(hb.y + o)[1] = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        load8(xb + (int64_t)h * C + 8 * cg, v);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) s[k] += v[k];
     }
@@ -155,6 +184,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
       atomicAdd(&dW[i], lg[k] * f[c]);
     }
   }
+  float gs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, gq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (rg < R) {
     float v[8];
 #pragma unroll
@@ -167,23 +197,67 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
     T* dxb = dx + (int64_t)b * HW * C + 8 * cg;
     pack_out(v, dxb, pk);
     for (int h = rg; h < HW; h += R) store8(dxb + (int64_t)h * C, pk);
+    if constexpr (FUSE) {
+      if (hb.acc_b) {
+        // the last block's BN-backward sums of dx (bn32_bwd_reduce's math):
+        // g = dx * [y > 0], sum g and sum g * (z - mean) * invstd per channel
+        for (int h = rg; h < HW; h += R) {
+          const int64_t o = ((int64_t)b * HW + h) * C + 8 * cg;
+          float yy[8], zz[8];
+          load8(hb.y + o, yy);
+          load8(hb.z + o, zz);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int c = 8 * cg + k;
+            const float g = yy[k] > 0.f ? v[k] : 0.f;
+            gs[k] += g;
+            gq[k] += g * ((zz[k] - bc[2 * C + c]) * bc[3 * C + c]);
+          }
+        }
+      }
+    }
   }
+  if constexpr (FUSE) {
+    if (hb.acc_b) {  // block-uniform: partials meet in LDS, one fp64 atomic per channel
+      for (int pass = 0; pass < 2; ++pass) {
+        if (rg < R) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) part[rg * C + 8 * cg + k] = pass ? gq[k] : gs[k];
+        }
+        __syncthreads();
+        for (int c = t; c < C; c += 256) {
+          double a = 0.0;
+          for (int r = 0; r < R; ++r) a += part[r * C + c];
+          atomicAdd(&hb.acc_b[(int64_t)(b % hb.reps_b) * 2 * C + pass * C + c], a);
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
+template <typename T, bool FUSE>
+static void head_launch_t(const T* x, int B, int HW, int C, const float* W, const float* bias, int K,
+                          const int* labels, float* feat, float* dlogits, T* dx, float* stats, bool backward,
+                          hipStream_t s, float* dW, float* db, const HeadBn& hb) {
+  const int G = C / 8, R = G >= 256 ? 1 : 256 / G;
+  const size_t sm = (size_t)(C + ((K + 3) & ~3) + (size_t)R * C + (size_t)K * C + (FUSE ? 4 * (size_t)C : 0)) *
+                    sizeof(float);
+  static bool attr = false;
+  if (!attr && sm > 65536) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_kernel<T, FUSE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    attr = true;
+  }
+  head_kernel<T, FUSE><<<B, 256, sm, s>>>(x, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, B,
+                                          backward ? 1 : 0, backward ? dW : nullptr, backward ? db : nullptr, hb);
 }
 
 template <typename T>
 static void head_launch(const T* x, int B, int HW, int C, const float* W, const float* bias, int K,
                         const int* labels, float* feat, float* dlogits, T* dx, float* stats, bool backward,
                         hipStream_t s, float* dW, float* db) {
-  const int G = C / 8, R = G >= 256 ? 1 : 256 / G;
-  const size_t sm = (size_t)(C + ((K + 3) & ~3) + (size_t)R * C + (size_t)K * C) * sizeof(float);
-  static bool attr = false;
-  if (!attr && sm > 65536) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&head_kernel<T>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    attr = true;
-  }
-  head_kernel<T><<<B, 256, sm, s>>>(x, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, B, backward ? 1 : 0,
-                                    backward ? dW : nullptr, backward ? db : nullptr);
+  head_launch_t<T, false>(x, B, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, backward, s, dW, db, HeadBn{});
 }
 
 void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,
@@ -193,7 +267,13 @@ void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W
 }
 void launch_head32_fwd_bwd(const float* x, int B, int HW, int C, const float* W, const float* bias, int K,
                            const int* labels, float* feat, float* dlogits, float* dx, float* stats, bool backward,
-                           hipStream_t s, float* dW, float* db) {
+                           hipStream_t s, float* dW, float* db, const HeadBn* bn) {
+  if (bn) {
+    HeadBn hb = *bn;
+    if (!backward) hb.acc_b = nullptr;
+    head_launch_t<float, true>(x, B, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, backward, s, dW, db, hb);
+    return;
+  }
   head_launch(x, B, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, backward, s, dW, db);
 }
 

@@ -152,9 +152,31 @@ void launch_bn32_bwd_reduce(const float* dy, const float* x, const float* y, con
 void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s);
 
 // ---- head.hip ------------------------------------------------------------
+// fp32 head whose input is relu(BN(z) + res), applied in its pooling loop
+// (the last block's BatchNorm apply folded into the head): writes the
+// activation y (the backward's ReLU mask) and, in train mode, publishes the
+// BN statistics and adds the BN-backward sums of dx (g = dx * [y > 0]: sum g,
+// sum g * xhat) into acc_b.
+struct HeadBn {
+  const float* z = nullptr;
+  const float* res = nullptr;
+  const double* acc = nullptr;
+  int reps = 1;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  float* mean = nullptr;
+  float* invstd = nullptr;
+  float* run_mean = nullptr;
+  float* run_var = nullptr;
+  float momentum = 0.1f, eps = 1e-5f;
+  int train = 1;
+  float* y = nullptr;
+  double* acc_b = nullptr;
+  int reps_b = 1;
+};
 void launch_head32_fwd_bwd(const float* x, int B, int HW, int C, const float* W, const float* bias, int K,
                            const int* labels, float* feat, float* dlogits, float* dx, float* stats, bool backward,
-                           hipStream_t s, float* dW = nullptr, float* db = nullptr);
+                           hipStream_t s, float* dW = nullptr, float* db = nullptr, const HeadBn* bn = nullptr);
 void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,
                          int K, const int* labels, float* feat, float* dlogits, uint16_t* dx,
                          float* stats, bool backward, hipStream_t s, float* dW = nullptr,

@@ -462,7 +462,28 @@ class ClassifierHead(Layer):
         self.dlogits = torch.zeros(self.N * self.K, **f32)
         self.dx = torch.zeros((self.N, self.HW, self.C), dtype=ws.dtype, device=device)
 
+    # set by forward_backward: the head added the BN-backward sums of its dx
+    # into the last block's conv2 accumulator (its backward runs presummed)
+    summed_input_bn = False
+
     def forward_backward(self, x, labels, stats, train=True):
+        """``x``: the pooled activation, or the last block's Pending output
+        (fp32 path): its BatchNorm + residual + ReLU are applied in the head's
+        pooling loop (no BatchNorm apply launch) and the head adds that BN's
+        backward sums (no reduce launch)."""
+        self.summed_input_bn = False
+        if isinstance(x, Pending):
+            p = x
+            if (p.res is not None and p.zr is None and p.relu and p.z.dtype == torch.float32
+                    and (p.z.is_cuda or FUSED_FILL_CPU)):
+                lay = p.layer
+                acc_b = lay.ws.acc(lay.acc_b) if train else None
+                K.head_forward_backward_bn(self.N, self.HW, self.C, self.W, self.b, labels, self.feat, self.dlogits,
+                                           self.dx, stats, train, self.dW if train else None,
+                                           self.db if train else None, p.z, p.res, p.bn, train, p.y, acc_b)
+                self.summed_input_bn = train
+                return self.dx
+            x = p.materialize(train)
         # the weight gradient rides in the same launch (atomics into the
         # step's zeroed gradient buffer): one kernel for the whole head
         K.head_forward_backward(x, self.N, self.HW, self.C, self.W, self.b, labels, self.feat,

@@ -132,6 +132,11 @@ class StaticNet:
     def backward(self, dlast) -> None:
         raise NotImplementedError
 
+    def forward_to_head(self, x, train: bool):
+        """The head's input (models whose last BatchNorm the head applies
+        return a layers.Pending instead of a tensor)."""
+        return self.forward(x, train)
+
     # -- step bodies ---------------------------------------------------------
     # When False (tests that inspect gradients after a step) the gradient
     # buffer is zeroed at the start of the step instead of by the optimizer.
@@ -143,7 +148,7 @@ class StaticNet:
             st.grad32.zero_()
         K.gather_batch(ds.x, ds.y, ds.perm, st.step, ds.steps_per_epoch, self.B, self.xb, self.yb,
                        xp=self.packed_input())
-        out = self.forward(self.xb, train=True)
+        out = self.forward_to_head(self.xb, train=True)
         dlast = self.head.forward_backward(out, self.yb, self.stats, train=True)
         for l in self.all_layers():
             l.prepare_backward()
@@ -157,7 +162,7 @@ class StaticNet:
     def _eval_body(self, ds: DeviceDataset) -> None:
         K.gather_batch(ds.x, ds.y, ds.perm, self.eval_step_ctr, ds.steps_per_epoch, self.B,
                        self.xb, self.yb, xp=self.packed_input())
-        out = self.forward(self.xb, train=False)
+        out = self.forward_to_head(self.xb, train=False)
         self.head.forward_backward(out, self.yb, self.stats, train=False)
         opt_ops.tick(self.eval_step_ctr, 1)
 

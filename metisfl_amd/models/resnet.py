@@ -95,7 +95,11 @@ class ResNet18(StaticNet):
         consumer is a halo conv (models/layers.py forward_fused)."""
         return any(c.hconv_ok() for b in self.blocks for c in b.sublayers())
 
-    def forward(self, x, train):
+    def forward_to_head(self, x, train):
+        # fused-fill path: the last block's BatchNorm is applied by the head
+        return self.forward(x, train, to_head=True)
+
+    def forward(self, x, train, to_head: bool = False):
         xp = None
         if self.stem.out_p() is not None:
             # bf16x3 fp32 path: every conv operand arrives packed (hi << 16 |
@@ -112,7 +116,7 @@ class ResNet18(StaticNet):
             p = Pending.of(self.stem)
             for b in self.blocks:
                 p = b.forward_fused(p, train)
-            return p.materialize(train)
+            return p if to_head else p.materialize(train)
         h = self.stem.forward(x, train=train, xp=xp)
         hp = self.stem.out_p()
         for b in self.blocks:
@@ -124,11 +128,13 @@ class ResNet18(StaticNet):
         # BN-backward reductions ride in the dgrad epilogues: every block's
         # conv1 dgrad (the last writer of the block's input gradient) sums for
         # the BN that consumes it -- the previous block's conv2, or the stem.
-        # Only the last block's conv2 (fed by the head) reduces on its own.
+        # The last block's conv2 (fed by the head) reduces on its own unless
+        # the head applied its BatchNorm and added the sums (fused fill).
         d = dlast.view(self.blocks[-1].out_shape)
         for i in range(len(self.blocks) - 1, -1, -1):
             prev = self.blocks[i - 1].c2 if i > 0 else self.stem
-            self.blocks[i].backward(d, self.dacts[i], presummed=i < len(self.blocks) - 1,
+            last = i == len(self.blocks) - 1
+            self.blocks[i].backward(d, self.dacts[i], presummed=(not last) or self.head.summed_input_bn,
                                     prev=prev.bn_target())
             d = self.dacts[i]
         self.stem.backward(d, None, presummed=True)

@@ -503,6 +503,26 @@ def head_forward_backward(x, B: int, HW: int, C: int, W, bias, labels, feat, dlo
             db.add_(d.sum(0))
 
 
+def head_forward_backward_bn(B: int, HW: int, C: int, W, bias, labels, feat, dlogits, dx, stats,
+                             backward: bool, dW, db, z, res, bn: BnParams, train: bool, y, acc_b=None) -> None:
+    """head_forward_backward of y = relu(BN(z) + res) with the BatchNorm apply
+    folded into the head's pooling loop (y is written: the backward's ReLU
+    mask) and, when ``acc_b`` is given (train, backward), the BN-backward sums
+    of dx (sum g, sum g * xhat; g = dx * [y > 0]) added into it -- that BN's
+    backward then runs presummed (no reduce launch)."""
+    if z.is_cuda:
+        ops().head32_forward_backward_bn(B, HW, C, W, bias, labels, feat, dlogits, dx, stats, backward, dW, db,
+                                         z, res, bn.acc if train else None, bn.gamma, bn.beta, bn.mean, bn.invstd,
+                                         bn.run_mean, bn.run_var, bn.momentum, bn.eps, train, y, acc_b)
+        return
+    # reference: the BatchNorm apply, the head, the BN-backward reduction
+    bn_apply(z, C, bn.acc, bn.gamma, bn.beta, bn.mean, bn.invstd, bn.run_mean, bn.run_var, y, residual=res,
+             relu=True, train=train, momentum=bn.momentum, eps=bn.eps)
+    head_forward_backward(y, B, HW, C, W, bias, labels, feat, dlogits, dx, stats, backward, dW, db)
+    if backward and acc_b is not None:
+        _bnb_sums_cpu(dx, BnBwdTarget(z, y, bn.mean, bn.invstd, acc_b[:2 * C]))
+
+
 def head_wgrad(feat, dlogits, B: int, C: int, K: int, dW, db) -> None:
     if feat.is_cuda:
         ops().head_wgrad(feat, dlogits, B, C, K, dW, db)
