@@ -55,7 +55,8 @@ struct FwdArgs {
   float* slab;         // split-K slabs
   int* counters;       // split-K arrival tickets (zero between launches)
   long long* stamps = nullptr;  // profiling: per-workgroup phase timestamps [grid][16] (core clock)
-  int dbg = 0;                  // ablation (timing only): 1 skip MFMAs, 2 skip fragment reads, 4 skip fills
+  int dbg = 0;                  // ablation (timing only): 1 skip MFMAs, 2 skip fragment reads, 4 skip fills,
+                                // 8 the first (bank-conflicting) weight-fill item order
   int xcd = 1;                  // XCD-grouped tile order (MFL_HC_XCD=0: hardware order)
 };
 

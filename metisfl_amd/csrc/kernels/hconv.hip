@@ -214,7 +214,15 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
 #pragma unroll
   for (int u = 0; u < K::NA; ++u) {
     const int i = t + K::NTHR * u;
-    const int p = i >> 2;
+    int p = i >> 2;
+    // 80-B pixel pitch: the 4 pixels of a 16-lane ds_write_b64 group are
+    // taken 2 apart (order 0 2 4 6 1 3 5 7 within each 8) so their 32-B hi /
+    // lo spans cover 4 disjoint 8-bank sets (scripts/hconv_banks.py: 90 -> 28
+    // extra cycles per chunk); full blocks of 8 only, so the map stays a
+    // bijection on the patch
+    if constexpr (K::PS == 80) {
+      if (p < (K::PIX / 8) * 8) p = (p & ~7) | ((p & 3) << 1) | ((p >> 2) & 1);
+    }
     const int img = p / (K::PH * K::PW);
     const int r2 = p - img * (K::PH * K::PW);
     const int py = r2 / K::PW, px = r2 - py * (K::PW);
@@ -243,8 +251,25 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
       b_lds[u] = item ? K::A_BYTES + (8 - tap) * (K::NT * K::BPS) + ci * K::BPS + 8 * kq
                       : K::A_BYTES + K::B_BYTES + 8 * kq;
     } else {
-      const int co = i / 36, r = i - co * 36;
-      const int tap = r >> 2, bq = r & 3;
+      // item -> (tap, co, channel quad) with co next-fastest: the 4 x 8-B LDS
+      // writes of a 16-lane group land on 4 different rows; with tap
+      // next-fastest (dbg & 8, the first layout) they were 5,120 B apart --
+      // one bank group, a 4-way conflict on every weight write
+      // (scripts/hconv_banks.py: 736 -> 0 extra cycles per chunk)
+      int co, tap, bq;
+      if (a.dbg & 8) {
+        co = i / 36;
+        const int r = i - co * 36;
+        tap = r >> 2;
+        bq = r & 3;
+      } else {
+        // rows taken 2 apart within each 8 (0 2 4 6 1 3 5 7): the 80-B row
+        // pitch then puts a group's 4 rows on disjoint banks (0 extra cycles)
+        bq = i & 3;
+        const int k = (i >> 2) % K::NT;
+        co = (k & ~7) | ((k & 3) << 1) | ((k >> 2) & 1);
+        tap = (i >> 2) / K::NT;
+      }
       b_off[u] = item ? (uint32_t)((((n0 + co) * 9 + tap) * C + 4 * bq) * 4) : kOOB;
       b_lds[u] = item ? K::A_BYTES + tap * (K::NT * K::BPS) + co * K::BPS + 8 * bq
                       : K::A_BYTES + K::B_BYTES + 8 * bq;
