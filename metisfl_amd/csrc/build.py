@@ -146,7 +146,7 @@ def write_ninja() -> str:
     for s in hip_srcs:
         # conv32.hip is built once per product variant (exact fp32 / bf16x3;
         # namespaces mfl::c32x / mfl::c32s, kernels/conv32.h)
-        variants = [("", "-DMFL_C32_BF16X3=0"), (".bf16x3", "-DMFL_C32_BF16X3=1")] \
+        variants = [("", "-DMFL_C32_BF16X3=0"), (".bf16x3", "-DMFL_C32_BF16X3=1" + os.environ.get("MFL_C32_EXTRA", ""))] \
             if os.path.basename(s) == "conv32.hip" else [("", None)]
         for tag, flag in variants:
             o = os.path.join(BUILD_DIR, "hip", os.path.basename(s) + tag + ".o")

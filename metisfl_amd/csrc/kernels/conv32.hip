@@ -119,6 +119,13 @@ __device__ __forceinline__ void split_hl(const f32x4& p, const f32x4& q, bf16x8&
 // dword = hi << 16 | lo, the same hi / lo split_hl computes): 8 v_perm per 8
 // values instead of 20 VALU
 __device__ __forceinline__ void unpack_hl(const f32x4& p, const f32x4& q, bf16x8& hi, bf16x8& lo) {
+#ifdef MFL_C32_NODECODE  // timing experiment only (MFL_C32_EXTRA=-DMFL_C32_NODECODE=1 at build time):
+                         // operands reinterpreted, no decode VALU, wrong products -- bounds what a
+                         // decode-free operand layout would return (profiles/ANALYSIS.md, round 3)
+  hi = __builtin_bit_cast(bf16x8, p);
+  lo = __builtin_bit_cast(bf16x8, q);
+  return;
+#endif
   const uint32_t d[8] = {__float_as_uint(p[0]), __float_as_uint(p[1]), __float_as_uint(p[2]), __float_as_uint(p[3]),
                          __float_as_uint(q[0]), __float_as_uint(q[1]), __float_as_uint(q[2]), __float_as_uint(q[3])};
   u32x4 h, l;

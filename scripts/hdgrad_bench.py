@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--eager", type=int, default=0, help="profiling: N eager calls of the paired backward per stage")
     args = ap.parse_args()
     K.set_conv_products("bf16x3")
     dev = torch.device("cuda")
@@ -70,6 +71,11 @@ def main():
         def hdgrad():
             K.hconv_dgrad(dy, ym, z, wp, w, dx, shp, bn, dgamma=dg, dbeta=db, ws=ws, dres=dres, dzp=dzp, bnb=bnb)
 
+        if args.eager:
+            for _ in range(args.eager):
+                pair()
+            torch.cuda.synchronize()
+            continue
         side = torch.cuda.Stream()
 
         def hdgrad_par_wgrad():  # the wgrad on a second stream, concurrent with the halo dgrad
