@@ -7,6 +7,7 @@
 // Each lane moves 4 channels (one 16-B float4).  C % 4 == 0.
 #include "kernels/common.h"
 #include "kernels/bn_coef.h"
+#include "kernels/bn32_bwd_body.h"
 #include "kernels/launchers.h"
 
 namespace mfl {
@@ -220,96 +221,165 @@ void launch_bn32_bwd_reduce(const float* dy, const float* x, const float* y, con
 }
 
 // Backward apply: dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat))
+// (bn32_bwd_body.h; the paired conv backward carries the same body)
 template <bool MASK, bool WRITE_DYM>
 __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int64_t nvec) {
-  extern __shared__ __attribute__((aligned(16))) float sc[];  // [5][C]: k1, mean g, mean g*xh, mean, invstd
-  const int C = a.C;
-  const float4* DY = reinterpret_cast<const float4*>(a.dy);
-  const float4* X = reinterpret_cast<const float4*>(a.x);
-  const float4* Y = reinterpret_cast<const float4*>(a.y);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), xv = gv, yv = gv;
-  if (i < nvec) {
-    gv = DY[i];
-    xv = X[i];
-    if (MASK) yv = Y[i];
+  extern __shared__ __attribute__((aligned(16))) float sc[];  // [5][C]
+  __shared__ float4 sh[512];                                  // side reduction
+  bn32_bwd_apply_body<MASK, WRITE_DYM, false>(a, nvec, blockIdx.x, gridDim.x, sc, sh);
+}
+
+// ---------------------------------------------------------------------------
+// The stem's backward in ONE launch.  The CIFAR stem (3x3 / stride 1 over the
+// 8-channel zero-padded 32x32 input, 64 output channels) has no dgrad, so its
+// backward was a BatchNorm backward apply writing dz (5 x 8.4 MB moved at
+// batch 32) plus an im2col wgrad over K = 72 that re-reads dz and x per
+// split-K slice (~21 us together per step, profiles/r3).  Here workgroup
+// (image n, channel group cg) loads dy, z and the ReLU output y of its 8
+// output channels over the whole image once, forms dz with bn32_bwd_apply's
+// arithmetic (the same fmaf sequence: bit-identical dz) straight into LDS
+// next to the image's input (+1-pixel halo), and wave `tap` (9 waves) sums
+// dz[p][co] * x[p + tap][0..7] over the image with exact fp32 FMAs: lane =
+// (co of the group, pixel phase), a butterfly over the 8 pixel phases, then
+// one fp32 atomic per (co, tap, ci) and image into dw (zero on entry).
+// Work split by (image, 8 output channels): every dw address takes one atomic
+// per image (N-way), 576 per workgroup.  (A first version split by 4-row
+// pixel strips with all 64 channels per workgroup: 256-way contention on
+// every dw address, 1.2M atomics -- slower than the two launches it replaced.)
+// Blocks are numbered image-fastest, so with N % 8 == 0 the 8 channel groups
+// of an image run on one XCD (round-robin placement) and share its 256-B
+// activation rows in that XCD's L2.
+constexpr int kStemCG = 8;  // output channels per workgroup
+
+__global__ __launch_bounds__(576) void stem_bwd32_kernel(BnBwdArgs32 a, const float* __restrict__ x, int N,
+                                                         float* __restrict__ dw) {
+  constexpr int H = 32, W = 32, CI = 8, CO = 64, PX = H * W, XW = W + 2, G = kStemCG;
+  constexpr int NV = PX * G / 4;            // float4 of dy / z / y per workgroup (2 per pixel)
+  constexpr int NU = (NV + 575) / 576;
+  constexpr int NX = (H + 2) * XW * CI / 4;  // float4 of the padded input image
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* dzs = sm;                 // [PX][G]
+  float* xs = dzs + PX * G;        // [H + 2][XW][CI]
+  float* cf = xs + (H + 2) * XW * CI;  // [5][G]: k1, mean g, mean g*xhat, mean, invstd
+  const int t = threadIdx.x;
+  const int img = blockIdx.x % N, cg = blockIdx.x / N;
+  const int co0 = cg * G;
+  // operand loads first: float4 i = (pixel i / 2, channels co0 + 4 (i & 1) ..)
+  const int64_t pix0 = (int64_t)img * PX;
+  float4 g[NU], z[NU], m[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int i = t + 576 * u;
+    if (NV % 576 == 0 || i < NV) {
+      const int64_t o = (pix0 + (i >> 1)) * CO + co0 + 4 * (i & 1);
+      g[u] = *reinterpret_cast<const float4*>(a.dy + o);
+      z[u] = *reinterpret_cast<const float4*>(a.x + o);
+      m[u] = *reinterpret_cast<const float4*>(a.y + o);
+    }
   }
-  const double inv_m = 1.0 / (double)a.M;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+  for (int i = t; i < NX; i += 576) {
+    const int pix = i >> 1, xr = pix / XW, xc = pix - xr * XW;
+    const int iy = xr - 1, ix = xc - 1;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+      v = reinterpret_cast<const float4*>(x)[((pix0 + iy * W + ix) * CI >> 2) + (i & 1)];
+    reinterpret_cast<float4*>(xs)[i] = v;
+  }
+  if (t < G) {
+    const int c = co0 + t;
     double s, q;
-    rep_sums(a.acc, a.reps, C, c, s, q);
-    sc[c] = a.gamma[c] * a.invstd[c];
-    sc[C + c] = (float)(s * inv_m);
-    sc[2 * C + c] = (float)(q * inv_m);
-    sc[3 * C + c] = a.mean[c];
-    sc[4 * C + c] = a.invstd[c];
-    if (blockIdx.x == 0) {
+    rep_sums(a.acc, a.reps, CO, c, s, q);
+    const double inv_m = 1.0 / (double)a.M;
+    cf[t] = a.gamma[c] * a.invstd[c];
+    cf[G + t] = (float)(s * inv_m);
+    cf[2 * G + t] = (float)(q * inv_m);
+    cf[3 * G + t] = a.mean[c];
+    cf[4 * G + t] = a.invstd[c];
+    if (img == 0) {
       if (a.dgamma) a.dgamma[c] = (float)q;
       if (a.dbeta) a.dbeta[c] = (float)s;
     }
   }
   __syncthreads();
-  const int tpr = C / 4;
-  const bool fixed = (256 % tpr) == 0;
-  int cb = fixed ? (int)(threadIdx.x % (unsigned)tpr) * 4 : 0;
-  float4 k1, mg, mx, mu, is;
-  auto load_coef = [&]() {
-    k1 = *reinterpret_cast<const float4*>(sc + cb);
-    mg = *reinterpret_cast<const float4*>(sc + C + cb);
-    mx = *reinterpret_cast<const float4*>(sc + 2 * C + cb);
-    mu = *reinterpret_cast<const float4*>(sc + 3 * C + cb);
-    is = *reinterpret_cast<const float4*>(sc + 4 * C + cb);
-  };
-  load_coef();
-  // side reduction (fixed channels only: the binding checks)
-  const bool side = WRITE_DYM && a.acc2 != nullptr;
-  float4 s2 = make_float4(0.f, 0.f, 0.f, 0.f), q2 = s2, mu2 = s2, is2 = s2;
-  if (side) {
-    mu2 = *reinterpret_cast<const float4*>(a.mean2 + cb);
-    is2 = *reinterpret_cast<const float4*>(a.invstd2 + cb);
-  }
-  for (; i < nvec; i += stride) {
-    float4 g = gv;
-    const float4 xc = xv, yc = yv;
-    if (i + stride < nvec) {
-      gv = DY[i + stride];
-      xv = X[i + stride];
-      if (MASK) yv = Y[i + stride];
+  // dz = k1 (g - mean g - xhat mean(g xhat)), g = dy [y > 0] (bn32_bwd_apply);
+  // 576 is even, so a thread's channel quad (i & 1) is fixed
+  const int cb = 4 * (t & 1);
+  const float4 k1 = *reinterpret_cast<const float4*>(cf + cb);
+  const float4 mg = *reinterpret_cast<const float4*>(cf + G + cb);
+  const float4 mx = *reinterpret_cast<const float4*>(cf + 2 * G + cb);
+  const float4 mu = *reinterpret_cast<const float4*>(cf + 3 * G + cb);
+  const float4 is = *reinterpret_cast<const float4*>(cf + 4 * G + cb);
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int i = t + 576 * u;
+    if (NV % 576 == 0 || i < NV) {
+      float4 gg = g[u];
+      gg.x = m[u].x > 0.f ? gg.x : 0.f;
+      gg.y = m[u].y > 0.f ? gg.y : 0.f;
+      gg.z = m[u].z > 0.f ? gg.z : 0.f;
+      gg.w = m[u].w > 0.f ? gg.w : 0.f;
+      float4 o;
+      o.x = k1.x * fmaf(-((z[u].x - mu.x) * is.x), mx.x, gg.x - mg.x);
+      o.y = k1.y * fmaf(-((z[u].y - mu.y) * is.y), mx.y, gg.y - mg.y);
+      o.z = k1.z * fmaf(-((z[u].z - mu.z) * is.z), mx.z, gg.z - mg.z);
+      o.w = k1.w * fmaf(-((z[u].w - mu.w) * is.w), mx.w, gg.w - mg.w);
+      reinterpret_cast<float4*>(dzs)[i] = o;
     }
-    if (!fixed) {
-      cb = (int)(i % tpr) * 4;
-      load_coef();
-    }
-    if (MASK) {
-      g.x = yc.x > 0.f ? g.x : 0.f;
-      g.y = yc.y > 0.f ? g.y : 0.f;
-      g.z = yc.z > 0.f ? g.z : 0.f;
-      g.w = yc.w > 0.f ? g.w : 0.f;
-      if (WRITE_DYM) reinterpret_cast<float4*>(a.dy_masked)[i] = g;
-      if (WRITE_DYM && side) {
-        const float4 z2 = reinterpret_cast<const float4*>(a.z2)[i];
-        s2.x += g.x; s2.y += g.y; s2.z += g.z; s2.w += g.w;
-        q2.x += g.x * ((z2.x - mu2.x) * is2.x);
-        q2.y += g.y * ((z2.y - mu2.y) * is2.y);
-        q2.z += g.z * ((z2.z - mu2.z) * is2.z);
-        q2.w += g.w * ((z2.w - mu2.w) * is2.w);
-      }
-    }
-    float4 o;
-    o.x = k1.x * fmaf(-((xc.x - mu.x) * is.x), mx.x, g.x - mg.x);
-    o.y = k1.y * fmaf(-((xc.y - mu.y) * is.y), mx.y, g.y - mg.y);
-    o.z = k1.z * fmaf(-((xc.z - mu.z) * is.z), mx.z, g.z - mg.z);
-    o.w = k1.w * fmaf(-((xc.w - mu.w) * is.w), mx.w, g.w - mg.w);
-    if (a.pack_dx)  // uniform: the bf16x3 convolutions' dY encoding
-      reinterpret_cast<uint4*>(a.dx)[i] = make_uint4(split_pack(o.x), split_pack(o.y), split_pack(o.z), split_pack(o.w));
-    else
-      reinterpret_cast<float4*>(a.dx)[i] = o;
   }
-  if (side) {
-    __syncthreads();  // sc[] reads done before channel_atomic4's LDS staging
-    channel_atomic4(s2, q2, C, tpr, 256 / tpr, a.acc2 + (int64_t)(blockIdx.x % a.reps2) * 2 * C);
+  __syncthreads();
+  // wave = filter tap (r, s); lane = (output channel cl, pixel phase ph):
+  // the lane sums pixels p = ph, ph + 8, ...  (8 lanes of a channel read 8
+  // consecutive pixels' dz and input rows per step: conflict-free)
+  const int tap = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lane = t & 63, cl = lane & 7, ph = lane >> 3;
+  const int r = tap / 3, sx = tap - 3 * r;
+  float acc[CI] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int p = ph; p < PX; p += 8) {
+    const int py = p >> 5, px = p & 31;
+    const float d = dzs[p * G + cl];
+    const float* xr = xs + ((py + r) * XW + px + sx) * CI;
+    const float4 x0 = *reinterpret_cast<const float4*>(xr);
+    const float4 x1 = *reinterpret_cast<const float4*>(xr + 4);
+    acc[0] = fmaf(d, x0.x, acc[0]);
+    acc[1] = fmaf(d, x0.y, acc[1]);
+    acc[2] = fmaf(d, x0.z, acc[2]);
+    acc[3] = fmaf(d, x0.w, acc[3]);
+    acc[4] = fmaf(d, x1.x, acc[4]);
+    acc[5] = fmaf(d, x1.y, acc[5]);
+    acc[6] = fmaf(d, x1.z, acc[6]);
+    acc[7] = fmaf(d, x1.w, acc[7]);
   }
+  // sum the 8 pixel phases (lane bits 3..5); every lane then holds its
+  // channel's 8 sums and stores the one of input channel ci = ph
+  float v = 0.f;
+#pragma unroll
+  for (int c = 0; c < CI; ++c) {
+    float w = acc[c];
+    w += __shfl_xor(w, 8, 64);
+    w += __shfl_xor(w, 16, 64);
+    w += __shfl_xor(w, 32, 64);
+    v = ph == c ? w : v;
+  }
+  atomicAdd(dw + ((int64_t)(co0 + cl) * 9 + tap) * CI + ph, v);  // KRSC [Co][3][3][Cin]
+}
+
+bool stem_bwd32_ok(int N, int H, int W, int Cin, int Co) {
+  return N > 0 && N < (1 << 24) && H == 32 && W == 32 && Cin == 8 && Co == 64;
+}
+
+void launch_stem_bwd32(const BnBwdArgs32& a, const float* x, int N, int H, int W, int Cin, float* dw, hipStream_t s) {
+  const size_t lds = ((size_t)32 * 32 * kStemCG + (size_t)34 * 34 * 8 + 5 * kStemCG) * sizeof(float);
+  static bool init = false;
+  if (!init) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_bwd32_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    init = true;
+  }
+  (void)H;
+  (void)W;
+  (void)Cin;
+  stem_bwd32_kernel<<<(unsigned)(N * (64 / kStemCG)), 576, lds, s>>>(a, x, N, dw);
 }
 
 void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s) {

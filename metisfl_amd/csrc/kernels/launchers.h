@@ -150,6 +150,12 @@ void launch_bn32_apply_pair(const BnFwdArgs32& a1, const BnFwdArgs32& a2, hipStr
 void launch_bn32_bwd_reduce(const float* dy, const float* x, const float* y, const float* mean,
                             const float* invstd, int64_t M, int C, double* acc, hipStream_t s, int reps = 1);
 void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s);
+// The stem's backward in one launch: its BatchNorm(+ReLU) backward (dz, as
+// bn32_bwd_apply, never written out) and the 3x3 / stride-1 weight gradient
+// dw[Co][3][3][Cin] += sum_p dz[p] x[p + tap] (exact fp32 FMAs).  a.dx: unused;
+// x: the stem input [N][H][W][Cin] fp32.  Shapes: stem_bwd32_ok.
+bool stem_bwd32_ok(int N, int H, int W, int Cin, int Co);
+void launch_stem_bwd32(const BnBwdArgs32& a, const float* x, int N, int H, int W, int Cin, float* dw, hipStream_t s);
 
 // ---- head.hip ------------------------------------------------------------
 // fp32 head whose input is relu(BN(z) + res), applied in its pooling loop

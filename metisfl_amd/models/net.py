@@ -84,15 +84,21 @@ class StaticNet:
     compute_dtype: torch.dtype = torch.bfloat16
 
     def __init__(self, batch_size: int, device="cpu", optimizer: OptimizerSpec | None = None,
-                 seed: int = 0):
+                 seed: int = 0, shared_state: FlatState | None = None):
         self.B = batch_size
         self.device = torch.device(device)
         self.build()
         specs: list[VarSpec] = []
         for l in self.all_layers():
             specs.extend(l.specs())
-        self.state = FlatState(specs, self.device, optimizer or OptimizerSpec(), seed=seed,
-                               compute_dtype=self.compute_dtype)
+        if shared_state is not None:
+            # a twin of an existing model (same architecture, another batch
+            # size): its layers bind to the SAME parameters / statistics
+            assert sorted(v.name for v in shared_state.specs) == sorted(v.name for v in specs), "twin of another model"
+            self.state = shared_state
+        else:
+            self.state = FlatState(specs, self.device, optimizer or OptimizerSpec(), seed=seed,
+                                   compute_dtype=self.compute_dtype)
         self.ws = Workspace(self.compute_dtype)
         for l in self.all_layers():
             l.bind(self.state, self.ws, self.device)
@@ -108,6 +114,8 @@ class StaticNet:
         self._train_graph_ds = None
         self._eval_graph = None
         self._eval_graph_ds = None
+        self._eval_twin = None     # None: not built yet, False: not available
+        self._eval_twin_ds = None  # (source dataset, the twin's view of it)
 
     # -- to override ----------------------------------------------------------
     input_shape: tuple = (32, 32, 8)
@@ -225,8 +233,39 @@ class StaticNet:
                 self._train_body(ds)
             i += 1
 
+    # Evaluation micro-batch.  BatchNorm runs on its running statistics in
+    # inference mode, so a sample's loss / prediction does not depend on the
+    # batch it is evaluated in: a full test-set pass (the reference's Keras
+    # ``evaluate`` at the training batch size, controller.cc:611) runs through
+    # a twin of the model bound to the same parameters at this wider batch --
+    # the same samples, each exactly once (padded tail skipped), at ~1.35x the
+    # throughput of batch-32 passes on MI355X (scripts/eval_probe.py: 10,000
+    # CIFAR samples 108 -> 80 ms).  MFL_EVAL_BATCH=0 disables it.
+    eval_batch: int = int(os.environ.get("MFL_EVAL_BATCH", "128"))
+
+    def _make_eval_twin(self, batch: int) -> "StaticNet | None":
+        """A model of the same architecture at ``batch`` sharing ``self.state``
+        (models opt in; None: evaluate at the training batch)."""
+        return None
+
+    def _eval_view(self, ds: DeviceDataset):
+        """(twin, the twin's dataset over ds's samples), or None."""
+        EB = self.eval_batch
+        if not (self.use_graphs() and ds.pad_tail and not ds.shuffle and EB > self.B and ds.n > self.B):
+            return None
+        if self._eval_twin is None:
+            self._eval_twin = self._make_eval_twin(EB) or False
+        if self._eval_twin is False:
+            return None
+        if self._eval_twin_ds is None or self._eval_twin_ds[0] is not ds:
+            self._eval_twin_ds = (ds, DeviceDataset(ds.x[:ds.n], ds.y[:ds.n], EB, shuffle=False, pad_tail=True))
+        return self._eval_twin, self._eval_twin_ds[1]
+
     def evaluate(self, ds: DeviceDataset, max_steps: int | None = None) -> dict:
         """Loss / accuracy of the current model on ``ds`` (BN in inference mode)."""
+        view = self._eval_view(ds) if max_steps is None else None
+        if view is not None:
+            return view[0].evaluate(view[1])
         nsteps = ds.steps_per_epoch if max_steps is None else min(max_steps, ds.steps_per_epoch)
         self.stats.zero_()
         self.eval_step_ctr.zero_()

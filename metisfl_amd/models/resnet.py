@@ -48,7 +48,7 @@ class ResNet18(StaticNet):
 
     def __init__(self, batch_size: int = 32, device="cpu", optimizer=None, seed: int = 0,
                  width_mult: float = 1.0, num_classes: int = 10, dtype: str = "fp32",
-                 conv_products: str | None = None):
+                 conv_products: str | None = None, shared_state=None):
         self.compute_dtype = DTYPES[dtype]
         self.conv_products = conv_products or default_conv_products()
         if dtype == "fp32" and torch.device(device).type == "cuda":
@@ -57,7 +57,12 @@ class ResNet18(StaticNet):
             set_conv_products(self.conv_products)
         self.width_mult = width_mult
         self.num_classes = num_classes
-        super().__init__(batch_size, device, optimizer, seed)
+        super().__init__(batch_size, device, optimizer, seed, shared_state=shared_state)
+
+    def _make_eval_twin(self, batch: int):
+        dtype = next(k for k, v in DTYPES.items() if v == self.compute_dtype)
+        return ResNet18(batch_size=batch, device=self.device, dtype=dtype, conv_products=self.conv_products,
+                        width_mult=self.width_mult, num_classes=self.num_classes, shared_state=self.state)
 
     def build(self):
         N = self.B
@@ -130,11 +135,14 @@ class ResNet18(StaticNet):
         # the BN that consumes it -- the previous block's conv2, or the stem.
         # The last block's conv2 (fed by the head) reduces on its own unless
         # the head applied its BatchNorm and added the sums (fused fill).
+        # The previous block's conv2 BN backward rides in this block's conv1
+        # pair (the last writer of its upstream gradient): layers.py FoldSpec.
         d = dlast.view(self.blocks[-1].out_shape)
         for i in range(len(self.blocks) - 1, -1, -1):
             prev = self.blocks[i - 1].c2 if i > 0 else self.stem
             last = i == len(self.blocks) - 1
+            fold = self.blocks[i - 1].c2_fold(self.dacts[i], self.dacts[i - 1]) if i > 0 else None
             self.blocks[i].backward(d, self.dacts[i], presummed=(not last) or self.head.summed_input_bn,
-                                    prev=prev.bn_target())
+                                    prev=prev.bn_target(), bn_done=not last, prev_fold=fold)
             d = self.dacts[i]
         self.stem.backward(d, None, presummed=True)

@@ -233,14 +233,51 @@ def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShap
     conv_forward(x, w2, y2, ConvShape(shp.N, shp.H, shp.W, shp.C, shp.Co, 1, 1, 2, 0), ws2, stats2)
 
 
+@dataclass
+class BnFold:
+    """A BatchNorm backward apply (bn_backward's operands, presummed) carried
+    by a paired conv backward launch as a third workgroup role (conv32.hip
+    folded_bn_bwd) instead of its own launch.  ``wait``: its upstream gradient
+    ``dy`` is that launch's dx (the apply waits for the dgrad tiles);
+    otherwise ``dy`` came from an earlier launch.  ``sync``: int32[2] device
+    scratch, zero between launches (the launch re-arms it)."""
+    dy: torch.Tensor
+    z: torch.Tensor
+    y: torch.Tensor | None
+    C: int
+    gamma: torch.Tensor
+    mean: torch.Tensor
+    invstd: torch.Tensor
+    acc: torch.Tensor
+    dgamma: torch.Tensor | None
+    dbeta: torch.Tensor | None
+    dz: torch.Tensor          # int32 view: packed bf16x3 output
+    dres: torch.Tensor | None
+    side: "BnSide | None"
+    wait: bool
+    sync: torch.Tensor
+
+
 def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
-                       bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False, xp=None) -> None:
+                       bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False, xp=None,
+                       fold: BnFold | None = None) -> bool:
     """A layer's weight gradient (dw += ..., dw zero on entry) and input
     gradient (as conv_dgrad) -- on the GPU in ONE paired launch, so the two
     independent, latency-bound GEMMs share the CUs (conv.hip
     conv_bwd_pair_kernel; MFL_CONV_PAIR=0 for two launches).  fp32: one
     launch too (conv32.hip conv32_bwd_pair_kernel, when both plans run 64x64
-    tiles on the fast address paths; MFL_C32_PAIR=0 for two launches)."""
+    tiles on the fast address paths; MFL_C32_PAIR=0 for two launches).
+    ``fold`` (fp32 GPU path): another BatchNorm's backward apply rides in the
+    same launch; returns whether it ran (False: the caller must run it)."""
+    if dy.is_cuda and dy.dtype == torch.float32 and fold is not None:
+        f, sd = fold, fold.side
+        return bool(ops().conv32_backward_pair_fold(
+            x if xp is None else xp, _dy_arg(dy, dy_packed), dw, w, dx, ws, *shp.args(), accumulate,
+            bnb.z if bnb else None, bnb.y if bnb else None, bnb.mean if bnb else None,
+            bnb.invstd if bnb else None, bnb.acc if bnb else None, wp,
+            f.dy, f.z, f.y, f.C, f.gamma, f.mean, f.invstd, f.acc, f.dgamma, f.dbeta, f.dz, f.dres,
+            sd.z if sd else None, sd.mean if sd else None, sd.invstd if sd else None, sd.acc if sd else None,
+            f.wait, f.sync))
     if dy.is_cuda and dy.dtype == torch.float32:
         dy = _dy_arg(dy, dy_packed)
         xa = x if xp is None else xp
@@ -250,7 +287,7 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
         else:
             ops().conv32_backward_pair(xa, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
                                        bnb.invstd, bnb.acc, wp)
-        return
+        return False
     if dy.is_cuda:
         if bnb is None:
             ops().conv_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None,
@@ -258,9 +295,10 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
         else:
             ops().conv_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
                                      bnb.invstd, bnb.acc)
-        return
+        return False
     conv_wgrad(x, dy, dw, shp, accumulate=True)
     conv_dgrad(dy, w, dx, shp, ws, accumulate, bnb=bnb, wp=wp)
+    return False
 
 
 def transpose_krsc(w, wt, Co: int, RS: int, Ci: int) -> None:
@@ -462,6 +500,32 @@ def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
     k1 = gamma * invstd
     out = k1 * (g - (tot[:C] / M).float() - xh * (tot[C:2 * C] / M).float())
     dx.copy_(out.to(dx.dtype))
+
+
+def stem_backward_ok(shp: ConvShape, device: torch.device) -> bool:
+    """Whether the fused stem backward (:func:`stem_backward`) covers ``shp``
+    (the CIFAR stem: 3x3 / stride 1 / pad 1, 8 padded input channels, 64
+    outputs, 32x32 images)."""
+    geo = shp.R == 3 and shp.S == 3 and shp.stride == 1 and shp.pad == 1
+    if device.type == "cuda":
+        return geo and bool(ops().stem_backward32_ok(shp.N, shp.H, shp.W, shp.C, shp.Co))
+    return geo and shp.H == 32 and shp.W == 32 and shp.C == 8 and shp.Co == 64
+
+
+def stem_backward(dy, z, y, x, shp: ConvShape, gamma, mean, invstd, acc, dgamma, dbeta, dw) -> None:
+    """A conv without dgrad (the stem): its BN(+ReLU) backward and its weight
+    gradient in ONE launch on the GPU (bn32.hip stem_bwd32_kernel; dz never
+    reaches memory, products are exact fp32).  ``acc`` holds the complete
+    backward sums (presummed); ``dw`` (zero on entry) accumulates."""
+    if dy.is_cuda:
+        ops().stem_backward32(dy, z, y, gamma, mean, invstd, acc, dgamma, dbeta, x, dw)
+        return
+    # reference: the BatchNorm backward apply, then the weight gradient
+    dz = torch.empty_like(z)
+    bn_backward(dy, z, y, shp.Co, gamma, mean, invstd, acc, dgamma, dbeta, dz, presummed=True)
+    g = torch.empty_like(dw)
+    conv_wgrad(x, dz, g, shp)
+    dw.add_(g)
 
 
 # ---------------------------------------------------------------------------
