@@ -239,8 +239,8 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
 // output channels over the whole image once, forms dz with bn32_bwd_apply's
 // arithmetic (the same fmaf sequence: bit-identical dz) straight into LDS
 // next to the image's input (+1-pixel halo), and wave `tap` (9 waves) sums
-// dz[p][co] * x[p + tap][0..7] over the image with exact fp32 FMAs: lane =
-// (co of the group, pixel phase), a butterfly over the 8 pixel phases, then
+// dz[p][co] * x[p + tap][ci] over the image with exact fp32 FMAs (lane = pixel
+// phase, all 8 x 8 products per lane, a recursive-halving butterfly), then
 // one fp32 atomic per (co, tap, ci) and image into dw (zero on entry).
 // Work split by (image, 8 output channels): every dw address takes one atomic
 // per image (N-way), 576 per workgroup.  (A first version split by 4-row
@@ -327,41 +327,47 @@ __global__ __launch_bounds__(576) void stem_bwd32_kernel(BnBwdArgs32 a, const fl
     }
   }
   __syncthreads();
-  // wave = filter tap (r, s); lane = (output channel cl, pixel phase ph):
-  // the lane sums pixels p = ph, ph + 8, ...  (8 lanes of a channel read 8
-  // consecutive pixels' dz and input rows per step: conflict-free)
+  // wave = filter tap (r, s); lane = pixel phase: a lane sums pixels p = lane,
+  // lane + 64, ... into all 8 x 8 (co, ci) products of the tap -- dz[p][0..7]
+  // and x[p + tap][0..7] are two lane-distinct b128 reads each, 64 FMAs per
+  // pixel (a lane-per-output-channel mapping re-read each input row 8 times:
+  // LDS-bound) -- then a recursive-halving butterfly leaves output o = lane
+  // on each lane (63 shuffles)
   const int tap = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int lane = t & 63, cl = lane & 7, ph = lane >> 3;
+  const int lane = t & 63;
   const int r = tap / 3, sx = tap - 3 * r;
-  float acc[CI] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int p = ph; p < PX; p += 8) {
+  float acc[G * CI];
+#pragma unroll
+  for (int o = 0; o < G * CI; ++o) acc[o] = 0.f;
+#pragma unroll 2
+  for (int p = lane; p < PX; p += 64) {
     const int py = p >> 5, px = p & 31;
-    const float d = dzs[p * G + cl];
+    const float4 d0 = *reinterpret_cast<const float4*>(dzs + p * G);
+    const float4 d1 = *reinterpret_cast<const float4*>(dzs + p * G + 4);
     const float* xr = xs + ((py + r) * XW + px + sx) * CI;
     const float4 x0 = *reinterpret_cast<const float4*>(xr);
     const float4 x1 = *reinterpret_cast<const float4*>(xr + 4);
-    acc[0] = fmaf(d, x0.x, acc[0]);
-    acc[1] = fmaf(d, x0.y, acc[1]);
-    acc[2] = fmaf(d, x0.z, acc[2]);
-    acc[3] = fmaf(d, x0.w, acc[3]);
-    acc[4] = fmaf(d, x1.x, acc[4]);
-    acc[5] = fmaf(d, x1.y, acc[5]);
-    acc[6] = fmaf(d, x1.z, acc[6]);
-    acc[7] = fmaf(d, x1.w, acc[7]);
-  }
-  // sum the 8 pixel phases (lane bits 3..5); every lane then holds its
-  // channel's 8 sums and stores the one of input channel ci = ph
-  float v = 0.f;
+    const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+    const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-  for (int c = 0; c < CI; ++c) {
-    float w = acc[c];
-    w += __shfl_xor(w, 8, 64);
-    w += __shfl_xor(w, 16, 64);
-    w += __shfl_xor(w, 32, 64);
-    v = ph == c ? w : v;
+    for (int c = 0; c < G; ++c)
+#pragma unroll
+      for (int k = 0; k < CI; ++k) acc[c * CI + k] = fmaf(dv[c], xv[k], acc[c * CI + k]);
   }
-  atomicAdd(dw + ((int64_t)(co0 + cl) * 9 + tap) * CI + ph, v);  // KRSC [Co][3][3][Cin]
+  // recursive halving over the 64 lanes: at offset d a lane keeps the half of
+  // its n values selected by its lane bit d and adds the partner's copy
+#pragma unroll
+  for (int d = 32, n = 64; d >= 1; d >>= 1, n >>= 1) {
+    const bool up = (lane & d) != 0;
+#pragma unroll
+    for (int j = 0; j < n / 2; ++j) {
+      const float send = up ? acc[j] : acc[j + n / 2];
+      const float keep = up ? acc[j + n / 2] : acc[j];
+      acc[j] = keep + __shfl_xor(send, d, 64);
+    }
+  }
+  // lane = co_local * 8 + ci
+  atomicAdd(dw + ((int64_t)(co0 + (lane >> 3)) * 9 + tap) * CI + (lane & 7), acc[0]);  // KRSC [Co][3][3][Cin]
 }
 
 bool stem_bwd32_ok(int N, int H, int W, int Cin, int Co) {
