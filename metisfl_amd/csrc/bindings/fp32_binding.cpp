@@ -202,15 +202,12 @@ void conv32_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, c10::opti
 
 // A layer's dgrad (+ fused consumer-BN reductions) and wgrad (dw zero on
 // entry or a running sum) -- one paired launch when both plans allow it.
-// Returns false when the fold was requested but the layer's plans do not pair
-// (then the fold did not run: the caller launches the BN backward itself).
-bool conv32_backward_pair_impl(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, torch::Tensor w, torch::Tensor dx,
-                               c10::optional<torch::Tensor> ws, int64_t N, int64_t H, int64_t W, int64_t C,
-                               int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate,
-                               c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
-                               c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
-                               c10::optional<torch::Tensor> bn_acc, c10::optional<torch::Tensor> wp,
-                               const mfl::BnBwdArgs32* fold, bool fold_wait, int* sync) {
+void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, torch::Tensor w, torch::Tensor dx,
+                          c10::optional<torch::Tensor> ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co,
+                          int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate,
+                          c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
+                          c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
+                          c10::optional<torch::Tensor> bn_acc, c10::optional<torch::Tensor> wp) {
   const auto gf = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
   const auto gd = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
   torch::Tensor xtmp, dtmp;
@@ -247,22 +244,11 @@ bool conv32_backward_pair_impl(torch::Tensor x, torch::Tensor dy, torch::Tensor 
   torch::Tensor tmp;
   const float* wb = wsrc(w, wp, tmp);
   if (C32_CALL(launch_conv32_bwd_pair, gd, pd, gf, pw, dyp, wb, fp(dx), slab, counters, accumulate,
-                                  fuse ? &f : nullptr, xs, fp(dw), cur_stream(dx), fold, fold_wait, sync))
-    return true;
+                                  fuse ? &f : nullptr, xs, fp(dw), cur_stream(dx)))
+    return;
   C32_CALL(launch_conv32_wgrad, gf, pw, xs, dyp, fp(dw), true, cur_stream(dw));
   C32_CALL(launch_conv32_gemm, gd, true, pd, dyp, wb, fp(dx), slab, counters, nullptr, accumulate,
                           fuse ? &f : nullptr, cur_stream(dx));
-  return fold == nullptr;
-}
-
-void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, torch::Tensor w, torch::Tensor dx,
-                          c10::optional<torch::Tensor> ws, int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co,
-                          int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate,
-                          c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
-                          c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
-                          c10::optional<torch::Tensor> bn_acc, c10::optional<torch::Tensor> wp) {
-  conv32_backward_pair_impl(x, dy, dw, w, dx, ws, N, H, W, C, Co, R, S, stride, pad, accumulate, bn_z, bn_y, bn_mean,
-                            bn_invstd, bn_acc, wp, nullptr, false, nullptr);
 }
 
 void conv32_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t N, int64_t H, int64_t W, int64_t C,
@@ -409,7 +395,7 @@ void conv32_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c1
   run(g2, false, xs, wb2, y2, ws2, st2, false, nullptr, r2);
 }
 
-mfl::BnBwdArgs32 bnbwd_args(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,
+void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,
                         torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd, torch::Tensor acc,
                         c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor dx,
                         c10::optional<torch::Tensor> dy_masked, bool presummed, c10::optional<torch::Tensor> z2,
@@ -466,17 +452,6 @@ mfl::BnBwdArgs32 bnbwd_args(torch::Tensor dy, torch::Tensor x, c10::optional<tor
     a.acc2 = const_cast<double*>(acc_ptr(*acc2, C));
     a.reps2 = reps_of(*acc2, C);
   }
-  return a;
-}
-
-void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,
-                        torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd, torch::Tensor acc,
-                        c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor dx,
-                        c10::optional<torch::Tensor> dy_masked, bool presummed, c10::optional<torch::Tensor> z2,
-                        c10::optional<torch::Tensor> mean2, c10::optional<torch::Tensor> invstd2,
-                        c10::optional<torch::Tensor> acc2) {
-  const mfl::BnBwdArgs32 a = bnbwd_args(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked, presummed,
-                                        z2, mean2, invstd2, acc2);
   auto s = cur_stream(x);
   if (!presummed)
     mfl::launch_bn32_bwd_reduce(a.dy, a.x, a.y, a.mean, a.invstd, a.M, a.C, acc.data_ptr<double>(), s, a.reps);
@@ -489,36 +464,6 @@ void bn32_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tenso
                    bool presummed) {
   bn32_backward_side(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked, presummed, c10::nullopt,
                      c10::nullopt, c10::nullopt, c10::nullopt);
-}
-
-// A layer's paired backward carrying another BatchNorm's backward apply as a
-// third workgroup role (conv32.hip folded_bn_bwd).  f_*: bn32_backward_side's
-// operands of that BN (always presummed: its sums are complete when it runs);
-// fold_wait: f_dy is THIS launch's dx (the apply waits for the dgrad tiles
-// through sync, an int32[2] zero on entry, re-armed by the launch); else f_dy
-// was produced by an earlier launch.  Returns false when the plans do not
-// pair: nothing of the fold ran (the caller runs the BN backward itself).
-bool conv32_backward_pair_fold(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, torch::Tensor w, torch::Tensor dx,
-                               c10::optional<torch::Tensor> ws, int64_t N, int64_t H, int64_t W, int64_t C,
-                               int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate,
-                               c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
-                               c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
-                               c10::optional<torch::Tensor> bn_acc, c10::optional<torch::Tensor> wp,
-                               torch::Tensor f_dy, torch::Tensor f_z, c10::optional<torch::Tensor> f_y, int64_t f_C,
-                               torch::Tensor f_gamma, torch::Tensor f_mean, torch::Tensor f_invstd, torch::Tensor f_acc,
-                               c10::optional<torch::Tensor> f_dgamma, c10::optional<torch::Tensor> f_dbeta,
-                               torch::Tensor f_dz, c10::optional<torch::Tensor> f_dres,
-                               c10::optional<torch::Tensor> f_z2, c10::optional<torch::Tensor> f_mean2,
-                               c10::optional<torch::Tensor> f_invstd2, c10::optional<torch::Tensor> f_acc2,
-                               bool fold_wait, torch::Tensor sync) {
-  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == torch::kInt32 && sync.numel() >= 2 && sync.is_contiguous(),
-              "fold sync: int32[2] device tensor");
-  if (fold_wait) TORCH_CHECK(f_dy.data_ptr() == dx.data_ptr(), "a waiting fold's upstream gradient is this dx");
-  const mfl::BnBwdArgs32 fa = bnbwd_args(f_dy, f_z, f_y, f_C, f_gamma, f_mean, f_invstd, f_acc, f_dgamma, f_dbeta,
-                                         f_dz, f_dres, true, f_z2, f_mean2, f_invstd2, f_acc2);
-  TORCH_CHECK(fa.C % 4 == 0 && 5 * fa.C * 4 + 64 + 16 + 512 * 16 <= 48 * 1024, "fold: channels");
-  return conv32_backward_pair_impl(x, dy, dw, w, dx, ws, N, H, W, C, Co, R, S, stride, pad, accumulate, bn_z, bn_y,
-                                   bn_mean, bn_invstd, bn_acc, wp, &fa, fold_wait, sync.data_ptr<int>());
 }
 
 // The stem's BatchNorm(+ReLU) backward and its 3x3 weight gradient in one
@@ -682,7 +627,6 @@ void register_fp32(pybind11::module& m) {
   m.def("conv32_dgrad", &conv32_dgrad);
   m.def("conv32_wgrad", &conv32_wgrad);
   m.def("conv32_backward_pair", &conv32_backward_pair);
-  m.def("conv32_backward_pair_fold", &conv32_backward_pair_fold);
   m.def("bn32_stats", &bn32_stats);
   m.def("bn32_apply", &bn32_apply);
   m.def("bn32_apply_pair", &bn32_apply_pair);

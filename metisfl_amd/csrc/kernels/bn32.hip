@@ -7,7 +7,6 @@
 // Each lane moves 4 channels (one 16-B float4).  C % 4 == 0.
 #include "kernels/common.h"
 #include "kernels/bn_coef.h"
-#include "kernels/bn32_bwd_body.h"
 #include "kernels/launchers.h"
 
 namespace mfl {
@@ -221,12 +220,96 @@ void launch_bn32_bwd_reduce(const float* dy, const float* x, const float* y, con
 }
 
 // Backward apply: dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat))
-// (bn32_bwd_body.h; the paired conv backward carries the same body)
 template <bool MASK, bool WRITE_DYM>
 __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int64_t nvec) {
-  extern __shared__ __attribute__((aligned(16))) float sc[];  // [5][C]
-  __shared__ float4 sh[512];                                  // side reduction
-  bn32_bwd_apply_body<MASK, WRITE_DYM, false>(a, nvec, blockIdx.x, gridDim.x, sc, sh);
+  extern __shared__ __attribute__((aligned(16))) float sc[];  // [5][C]: k1, mean g, mean g*xh, mean, invstd
+  const int C = a.C;
+  const float4* DY = reinterpret_cast<const float4*>(a.dy);
+  const float4* X = reinterpret_cast<const float4*>(a.x);
+  const float4* Y = reinterpret_cast<const float4*>(a.y);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), xv = gv, yv = gv;
+  if (i < nvec) {
+    gv = DY[i];
+    xv = X[i];
+    if (MASK) yv = Y[i];
+  }
+  const double inv_m = 1.0 / (double)a.M;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double s, q;
+    rep_sums(a.acc, a.reps, C, c, s, q);
+    sc[c] = a.gamma[c] * a.invstd[c];
+    sc[C + c] = (float)(s * inv_m);
+    sc[2 * C + c] = (float)(q * inv_m);
+    sc[3 * C + c] = a.mean[c];
+    sc[4 * C + c] = a.invstd[c];
+    if (blockIdx.x == 0) {
+      if (a.dgamma) a.dgamma[c] = (float)q;
+      if (a.dbeta) a.dbeta[c] = (float)s;
+    }
+  }
+  __syncthreads();
+  const int tpr = C / 4;
+  const bool fixed = (256 % tpr) == 0;
+  int cb = fixed ? (int)(threadIdx.x % (unsigned)tpr) * 4 : 0;
+  float4 k1, mg, mx, mu, is;
+  auto load_coef = [&]() {
+    k1 = *reinterpret_cast<const float4*>(sc + cb);
+    mg = *reinterpret_cast<const float4*>(sc + C + cb);
+    mx = *reinterpret_cast<const float4*>(sc + 2 * C + cb);
+    mu = *reinterpret_cast<const float4*>(sc + 3 * C + cb);
+    is = *reinterpret_cast<const float4*>(sc + 4 * C + cb);
+  };
+  load_coef();
+  // side reduction (fixed channels only: the binding checks)
+  const bool side = WRITE_DYM && a.acc2 != nullptr;
+  float4 s2 = make_float4(0.f, 0.f, 0.f, 0.f), q2 = s2, mu2 = s2, is2 = s2;
+  if (side) {
+    mu2 = *reinterpret_cast<const float4*>(a.mean2 + cb);
+    is2 = *reinterpret_cast<const float4*>(a.invstd2 + cb);
+  }
+  for (; i < nvec; i += stride) {
+    float4 g = gv;
+    const float4 xc = xv, yc = yv;
+    if (i + stride < nvec) {
+      gv = DY[i + stride];
+      xv = X[i + stride];
+      if (MASK) yv = Y[i + stride];
+    }
+    if (!fixed) {
+      cb = (int)(i % tpr) * 4;
+      load_coef();
+    }
+    if (MASK) {
+      g.x = yc.x > 0.f ? g.x : 0.f;
+      g.y = yc.y > 0.f ? g.y : 0.f;
+      g.z = yc.z > 0.f ? g.z : 0.f;
+      g.w = yc.w > 0.f ? g.w : 0.f;
+      if (WRITE_DYM) reinterpret_cast<float4*>(a.dy_masked)[i] = g;
+      if (WRITE_DYM && side) {
+        const float4 z2 = reinterpret_cast<const float4*>(a.z2)[i];
+        s2.x += g.x; s2.y += g.y; s2.z += g.z; s2.w += g.w;
+        q2.x += g.x * ((z2.x - mu2.x) * is2.x);
+        q2.y += g.y * ((z2.y - mu2.y) * is2.y);
+        q2.z += g.z * ((z2.z - mu2.z) * is2.z);
+        q2.w += g.w * ((z2.w - mu2.w) * is2.w);
+      }
+    }
+    float4 o;
+    o.x = k1.x * fmaf(-((xc.x - mu.x) * is.x), mx.x, g.x - mg.x);
+    o.y = k1.y * fmaf(-((xc.y - mu.y) * is.y), mx.y, g.y - mg.y);
+    o.z = k1.z * fmaf(-((xc.z - mu.z) * is.z), mx.z, g.z - mg.z);
+    o.w = k1.w * fmaf(-((xc.w - mu.w) * is.w), mx.w, g.w - mg.w);
+    if (a.pack_dx)  // uniform: the bf16x3 convolutions' dY encoding
+      reinterpret_cast<uint4*>(a.dx)[i] = make_uint4(split_pack(o.x), split_pack(o.y), split_pack(o.z), split_pack(o.w));
+    else
+      reinterpret_cast<float4*>(a.dx)[i] = o;
+  }
+  if (side) {
+    __syncthreads();  // sc[] reads done before channel_atomic4's LDS staging
+    channel_atomic4(s2, q2, C, tpr, 256 / tpr, a.acc2 + (int64_t)(blockIdx.x % a.reps2) * 2 * C);
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -2,7 +2,6 @@
 // operand pointers.  Shared by conv32.hip and its torch binding.
 #pragma once
 #include "kernels/conv.h"
-#include "kernels/launchers.h"
 
 namespace mfl {
 
@@ -37,10 +36,6 @@ struct Conv32Args {
   int par_mc;
   FastDiv dc, dq, dpq;  // / C, / Q, / (P*Q)
   int reps;             // BN accumulator replicas ([reps][2][Ng]; workgroup b adds into replica b % reps)
-  // dgrad of a paired backward that carries a folded BatchNorm-backward apply
-  // (conv32_bwd_pair_kernel): output tiles are stored device-scope and each
-  // completed tile (stores and BN-sum atomics done) increments *done
-  int* done;
 };
 
 struct BnBwdFusion32 {

@@ -55,7 +55,6 @@
 #include "kernels/common.h"
 #include "kernels/conv32.h"
 #include "kernels/lds_tiles.h"
-#include "kernels/bn32_bwd_body.h"
 
 // Built twice (csrc/build.py): MFL_C32_BF16X3=0 -> namespace mfl::c32x (exact
 // fp32 MFMA), =1 -> mfl::c32s (3-product bf16 split, see mma_tile).
@@ -343,12 +342,7 @@ __device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, const Blk& 
     const int64_t off = (int64_t)out_pixel32(a, row) * g.Ng + col;
     float4* dst = reinterpret_cast<float4*>(a.y + off);
     if (a.accum) v = f4add(v, *dst);
-    if (a.done)  // uniform: a folded apply on another XCD reads this tile in the same launch
-      __builtin_amdgcn_raw_buffer_store_b128(
-          u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)},
-          make_rsrc(a.y, 0x7FFFFFF0u), (int)(off * 4), 0, 16);  // sc1: device scope
-    else
-      *dst = v;
+    *dst = v;
     if (stats) {
       if (a.bn_acc) {
         const float4 z = *reinterpret_cast<const float4*>(a.bn_z + off);
@@ -374,34 +368,25 @@ __device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, const Blk& 
       }
     }
   }
-  if (stats) {
-    // replica of this workgroup (b % 8 = the XCD under round-robin placement)
-    stats += (int64_t)((b.x + b.y * b.gx + b.z * b.gx * b.gy) % a.reps) * 2 * g.Ng;
-    reinterpret_cast<float4*>(red)[2 * t] = s;
-    reinterpret_cast<float4*>(red)[2 * t + 1] = q;
-    __syncthreads();
-    if (t < BN) {
-      const int cgi = t >> 2, k = t & 3;
-      double sa = 0.0, sb = 0.0;
+  if (!stats) return;
+  // replica of this workgroup (b % 8 = the XCD under round-robin placement)
+  stats += (int64_t)((b.x + b.y * b.gx + b.z * b.gx * b.gy) % a.reps) * 2 * g.Ng;
+  reinterpret_cast<float4*>(red)[2 * t] = s;
+  reinterpret_cast<float4*>(red)[2 * t + 1] = q;
+  __syncthreads();
+  if (t < BN) {
+    const int cgi = t >> 2, k = t & 3;
+    double sa = 0.0, sb = 0.0;
 #pragma unroll 4
-      for (int r = 0; r < RPP; ++r) {
-        sa += red[(r * CPR + cgi) * 8 + k];
-        sb += red[(r * CPR + cgi) * 8 + 4 + k];
-      }
-      const int c = n0 + t;
-      if (c < g.Ng) {
-        atomicAdd(&stats[c], sa);
-        atomicAdd(&stats[g.Ng + c], sb);
-      }
+    for (int r = 0; r < RPP; ++r) {
+      sa += red[(r * CPR + cgi) * 8 + k];
+      sb += red[(r * CPR + cgi) * 8 + 4 + k];
     }
-  }
-  if (a.done) {
-    // tile complete: every wave's device-scope stores and memory-side BN-sum
-    // atomics acknowledged, then one relaxed agent-scope increment (no L2
-    // write-back needed: nothing this tile produced sits in the L2)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) __hip_atomic_fetch_add(a.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int c = n0 + t;
+    if (c < g.Ng) {
+      atomicAdd(&stats[c], sa);
+      atomicAdd(&stats[g.Ng + c], sb);
+    }
   }
 }
 
@@ -962,56 +947,12 @@ __global__ __launch_bounds__(256, 2) void conv32_fwd_pair_kernel(Conv32Args a1, 
   }
 }
 
-// Folded BatchNorm-backward apply (AP != 0: 1 ReLU mask + masked-gradient
-// output, 2 ReLU mask, 3 no mask): workgroups [nd + nw, nd + nw + na) of the
-// HARDWARE order run bn32_bwd_apply_body over `ab` -- the BN backward whose
-// dz the NEXT launch needs -- so it costs no launch of its own and its
-// HBM-bound work runs beside the pair's wgrad tail.  wait_tiles > 0: its
-// upstream gradient is this launch's dgrad output (the dgrad epilogue stores
-// device-scope and counts finished tiles in sync[0]); the apply workgroups
-// come after every dgrad workgroup in each XCD's in-order dispatch, so the
-// spin cannot starve a dgrad tile.  The last apply workgroup re-arms sync.
-template <int AP>
-__device__ __forceinline__ void folded_bn_bwd(const BnBwdArgs32& ab, int64_t nvec, int bid, int na, int wait_tiles,
-                                              int* sync, uint8_t* smem) {
-  if (wait_tiles > 0) {
-    if (threadIdx.x == 0) {
-      int it = 0;  // bounded: a lost signal ends in wrong values, never a hung GPU
-      while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wait_tiles &&
-             ++it < (1 << 22))
-        __builtin_amdgcn_s_sleep(2);
-    }
-    __syncthreads();
-  }
-  float* sc = reinterpret_cast<float*>(smem);
-  float4* sh = reinterpret_cast<float4*>(smem + 5 * ab.C * sizeof(float) + 64);
-  sh = reinterpret_cast<float4*>((reinterpret_cast<uintptr_t>(sh) + 15) & ~uintptr_t(15));
-  bn32_bwd_apply_body<AP != 3, AP == 1, true>(ab, nvec, bid, na, sc, sh);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int prev = __hip_atomic_fetch_add(&sync[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == na - 1) {
-      __hip_atomic_store(&sync[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sync[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-template <int KS, int ST, bool PAR, int NS, int AP = 0>
+template <int KS, int ST, bool PAR, int NS>
 __global__ __launch_bounds__(256, 2) void conv32_bwd_pair_kernel(Conv32Args ad, Conv32Args aw, float* __restrict__ dw,
                                                                  int atomic, int nd, int gdx, int gdy, int gwx,
-                                                                 int gwy, int gwz, BnBwdArgs32 ab, int na,
-                                                                 int wait_tiles, int* sync) {
+                                                                 int gwy, int gwz) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int nw = gwx * gwy * gwz;
-  if constexpr (AP != 0) {
-    if ((int)blockIdx.x >= nd + nw) {
-      folded_bn_bwd<AP>(ab, ab.M * ab.C / 4, (int)blockIdx.x - (nd + nw), na, wait_tiles, sync, smem);
-      return;
-    }
-  }
-  const int b = xcd_group(blockIdx.x, nd + nw);
+  const int b = xcd_group(blockIdx.x, gridDim.x);
   if (b < nd) {
     const Blk k{b % gdx, (b / gdx) % gdy, b / (gdx * gdy), gdx, gdy, nd / (gdx * gdy)};
     conv32_gemm_body<64, 64, true, KS, ST, PAR, NS, false>(ad, k, smem);
@@ -1352,56 +1293,32 @@ void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, c
 
 bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGeom& gf, const ConvPlan& pw,
                             const float* dy, const float* w, float* dx, float* ysplit, int* counters, bool accum,
-                            const BnBwdFusion32* bnb, const float* x, float* dw, hipStream_t s,
-                            const BnBwdArgs32* fold, bool fold_wait, int* sync) {
+                            const BnBwdFusion32* bnb, const float* x, float* dw, hipStream_t s) {
   if (env_int("MFL_C32_PAIR", 1) == 0) return false;
   const bool par = pd.par_mc != 0;
   if (pd.bm != 64 || pd.bn != 64 || pw.bm != 64 || pw.bn != 64) return false;
   if (gd.C % kBK != 0 || pd.kchunk % kBK != 0 || (MFL_C32_GENERIC)) return false;  // dgrad fast path
   if (gd.stride > 1 && !par) return false;
   if (!wgrad_fast(gf, pw.kchunk)) return false;
-  Conv32Args ad = gemm_args(gd, true, pd, dy, w, dx, ysplit, counters, nullptr, accum, bnb, 1);
+  const Conv32Args ad = gemm_args(gd, true, pd, dy, w, dx, ysplit, counters, nullptr, accum, bnb, 1);
   const Conv32Args aw = wgrad_args(gf, pw, x, dy);
   const int gdx = cdiv(gd.M, 64), gdy = cdiv(gd.Ng, 64), nd = gdx * gdy * pd.splits;
   const int gwx = cdiv(gf.Ng, 64), gwy = cdiv(gf.K, 64), gwz = pw.splits;
-  int nblk = nd + gwx * gwy * gwz;
-  size_t lds = std::max(gemm_lds(64, 64), (size_t)stages_for(64, 64) * kBK * (64 + 64) * 4);
+  const int nblk = nd + gwx * gwy * gwz;
+  const size_t lds = std::max(gemm_lds(64, 64), (size_t)stages_for(64, 64) * kBK * (64 + 64) * 4);
   constexpr int NS = stages_for(64, 64);
-  BnBwdArgs32 ab{};
-  int na = 0, wait_tiles = 0, ap = 0;
-  if (fold) {
-    ab = *fold;
-    const int64_t nvec = ab.M * ab.C / 4;
-    na = (int)std::min<int64_t>(256, std::max<int64_t>(1, (nvec + 2047) / 2048));  // ~8 float4 per thread
-    nblk += na;
-    if (fold_wait) {
-      ad.done = sync;
-      wait_tiles = gdx * gdy;  // one epilogue per output tile (split-K: the last arriver)
-    }
-    ap = ab.y ? (ab.dy_masked ? 1 : 2) : 3;
-    lds = std::max(lds, (size_t)5 * ab.C * sizeof(float) + 64 + 16 + 512 * sizeof(float4));
-  }
   auto go = [&](auto kern) {
     static_assert(NS >= 2, "ring");
     if (lds > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    kern<<<nblk, 256, lds, s>>>(ad, aw, dw, 1, nd, gdx, gdy, gwx, gwy, gwz, ab, na, wait_tiles, sync);
+    kern<<<nblk, 256, lds, s>>>(ad, aw, dw, 1, nd, gdx, gdy, gwx, gwy, gwz);
   };
-  auto geo = [&](auto apc) {
-    constexpr int AP = decltype(apc)::value;
-    if (gd.R == 3 && gd.stride == 1) go(conv32_bwd_pair_kernel<3, 1, false, NS, AP>);
-    else if (gd.R == 1 && gd.stride == 1) go(conv32_bwd_pair_kernel<1, 1, false, NS, AP>);
-    else if (gd.R == 3 && gd.stride == 2) go(conv32_bwd_pair_kernel<3, 2, true, NS, AP>);
-    else if (gd.R == 1 && gd.stride == 2) go(conv32_bwd_pair_kernel<1, 2, true, NS, AP>);
-    else return false;
-    return true;
-  };
-  switch (ap) {
-    case 1: return geo(IC<1>{});
-    case 2: return geo(IC<2>{});
-    case 3: return geo(IC<3>{});
-    default: return geo(IC<0>{});
-  }
+  if (gd.R == 3 && gd.stride == 1) go(conv32_bwd_pair_kernel<3, 1, false, NS>);
+  else if (gd.R == 1 && gd.stride == 1) go(conv32_bwd_pair_kernel<1, 1, false, NS>);
+  else if (gd.R == 3 && gd.stride == 2) go(conv32_bwd_pair_kernel<3, 2, true, NS>);
+  else if (gd.R == 1 && gd.stride == 2) go(conv32_bwd_pair_kernel<1, 2, true, NS>);
+  else return false;
+  return true;
 }
 
 bool launch_conv32_fwd_pair(const ConvGeom& g1, const ConvPlan& p1, const float* w1, float* y1, float* ys1,

@@ -86,10 +86,6 @@ HALO_DGRAD = os.environ.get("MFL_HALO_DGRAD", "0") == "1"
 # the stem's BN backward + weight gradient in one launch (MFL_STEM_FUSED=0:
 # BN backward apply + im2col wgrad, for A/B runs)
 STEM_FUSED = os.environ.get("MFL_STEM_FUSED", "1") == "1"
-# BatchNorm backward applies carried by the preceding paired conv backward
-# launch (conv32.hip folded_bn_bwd) instead of launching on their own
-# (MFL_BN_FOLD=0: every BN backward apply is its own launch, for A/B runs)
-BN_FOLD = os.environ.get("MFL_BN_FOLD", "0") == "1"
 
 
 class Pending:
@@ -122,17 +118,6 @@ class Pending:
             res = self.res_layer.bn_forward(train=train)
         self.layer.bn_forward(res, train)
         return self.y
-
-
-class FoldSpec:
-    """The BatchNorm backward of ``layer`` (upstream gradient ``dy``, masked
-    gradient out ``dres``, projection-shortcut side sums ``side``) to run
-    inside another layer's paired backward launch; ``wait``: ``dy`` is that
-    launch's own dx."""
-
-    def __init__(self, layer: "ConvBN", dy: torch.Tensor, dres: torch.Tensor | None = None,
-                 side: "K.BnSide | None" = None, wait: bool = False):
-        self.layer, self.dy, self.dres, self.side, self.wait = layer, dy, dres, side, wait
 
 
 class Layer:
@@ -210,9 +195,6 @@ class ConvBN(Layer):
         self.xp = None
         self.mean = torch.zeros(s.Co, **f32)
         self.invstd = torch.zeros(s.Co, **f32)
-        # arrival counters of a launch that carries this layer's BN backward
-        # (conv32.hip folded_bn_bwd; zero between launches)
-        self.fold_sync = torch.zeros(2, dtype=torch.int32, device=device)
         # fp64 [2C] statistics accumulators (forward sums, backward sums),
         # carved from the model-wide buffer the optimizer launch re-zeroes
         # fp32 kernels spread their fp64 atomics over 8 replicas (one per
@@ -297,45 +279,15 @@ class ConvBN(Layer):
             return K.BnSide(self.z, self.mean, self.invstd, self.ws.acc(self.acc_b))
         return None
 
-    def _packed_dz(self) -> bool:
-        # bf16x3 conv products: dz is only ever read by this layer's dgrad and
-        # wgrad, so the BN backward writes it as their packed operand encoding
-        return self.dz.is_cuda and self.dz.dtype == torch.float32 and K.conv_products() == "bf16x3"
-
-    def bn_backward(self, dy: torch.Tensor, dres: torch.Tensor | None = None, presummed: bool = False,
-                    side: K.BnSide | None = None) -> None:
-        """This layer's BN(+ReLU) backward alone: dz (packed on the bf16x3
-        path), dgamma / dbeta, the masked gradient into ``dres``."""
-        K.bn_backward(dy, self.z, self.y if self.relu else None, self.shp.Co, self.gamma, self.mean,
-                      self.invstd, self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz, dres,
-                      presummed=presummed, side=side, dx_packed=self._packed_dz())
-
-    def fold_of(self, f: FoldSpec) -> K.BnFold:
-        lay = f.layer
-        dz = lay.dz.view(torch.int32) if lay._packed_dz() else lay.dz
-        return K.BnFold(f.dy, lay.z, lay.y if lay.relu else None, lay.shp.Co, lay.gamma, lay.mean, lay.invstd,
-                        lay.ws.acc(lay.acc_b), lay.dgamma, lay.dbeta, dz, f.dres, f.side, f.wait, lay.fold_sync)
-
     def backward(self, dy: torch.Tensor, dx: torch.Tensor | None, accumulate: bool = False,
                  dres: torch.Tensor | None = None, presummed: bool = False,
-                 bnb: K.BnBwdTarget | None = None, side: K.BnSide | None = None,
-                 bn_done: bool = False, fold: FoldSpec | None = None) -> None:
+                 bnb: K.BnBwdTarget | None = None, side: K.BnSide | None = None) -> None:
         """dy: gradient w.r.t. this layer's output.  Writes dgamma/dbeta/dW into
         the flat gradient buffer and (if dx is given) d input into dx; ``dres``
         receives the ReLU-masked dy that the residual branch needs.
         ``presummed``: dy's producer already accumulated this BN's backward
         reductions; ``bnb``: the BN whose upstream gradient ``dx`` is (its
-        reductions are fused into this layer's dgrad epilogue).
-        ``bn_done``: this layer's BN backward already ran (folded into an
-        earlier launch: dz, dgamma / dbeta and dres are written).  ``fold``:
-        another layer's BN backward to carry in this layer's paired launch;
-        it has run (here or as a separate launch) when this returns."""
-        ran = self._backward(dy, dx, accumulate, dres, presummed, bnb, side, bn_done,
-                             fold if BN_FOLD else None)
-        if fold is not None and not ran:
-            fold.layer.bn_backward(fold.dy, fold.dres, presummed=True, side=fold.side)
-
-    def _backward(self, dy, dx, accumulate, dres, presummed, bnb, side, bn_done, fold) -> bool:
+        reductions are fused into this layer's dgrad epilogue)."""
         s = self.shp
         if (STEM_FUSED and dx is None and dres is None and presummed and side is None and self.relu
                 and self.z.dtype == torch.float32 and (self.z.is_cuda or FUSED_FILL_CPU)
@@ -343,8 +295,8 @@ class ConvBN(Layer):
             # no dgrad (the stem): BN backward + weight gradient in one launch
             K.stem_backward(dy, self.z, self.y, self.x, s, self.gamma, self.mean, self.invstd,
                             self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dw)
-            return False
-        if HALO_DGRAD and not bn_done and dx is not None and presummed and side is None and self.hconv_ok():
+            return
+        if HALO_DGRAD and dx is not None and presummed and side is None and self.hconv_ok():
             # halo dgrad: the BN backward runs in its operand fill and its
             # owner tiles write dz packed for the wgrad.  Opt-in: measured on
             # MI355X (scripts/hdgrad_bench.py) the halo dgrad beats BN apply +
@@ -357,24 +309,25 @@ class ConvBN(Layer):
                           dgamma=self.dgamma, dbeta=self.dbeta, ws=self._split(), dres=dres, dzp=dzp,
                           accumulate=accumulate, bnb=bnb)
             K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True, dy_packed=self.dz.is_cuda, xp=self.xp)
-            return False
-        pk = self._packed_dz()
-        if not bn_done:
-            self.bn_backward(dy, dres, presummed=presummed, side=side)
+            return
+        # bf16x3 conv products: dz is only ever read by this layer's dgrad and
+        # wgrad, so the BN backward writes it as their packed operand encoding
+        pk = self.dz.is_cuda and self.dz.dtype == torch.float32 and K.conv_products() == "bf16x3"
+        K.bn_backward(dy, self.z, self.y if self.relu else None, s.Co, self.gamma, self.mean,
+                      self.invstd, self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz, dres,
+                      presummed=presummed, side=side, dx_packed=pk)
         # weight gradient: off the critical path -> side stream (joined before
         # the optimizer); the gradient buffer is zero on entry (re-zeroed by
         # the optimizer launch), so split-K slices accumulate atomically
         if dx is not None and not self.ws.overlap:
-            # both GEMMs in one launch (their workgroups share the CUs), plus
-            # the folded BN backward when given
-            return K.conv_backward_pair(self.x, self.dz, self.dw, self.w16, dx, s, self._split(), accumulate,
-                                        bnb=bnb, wp=self.wp, dy_packed=pk, xp=self.xp,
-                                        fold=self.fold_of(fold) if fold is not None and self.dz.is_cuda else None)
+            # both GEMMs in one launch (their workgroups share the CUs)
+            K.conv_backward_pair(self.x, self.dz, self.dw, self.w16, dx, s, self._split(), accumulate,
+                                 bnb=bnb, wp=self.wp, dy_packed=pk, xp=self.xp)
+            return
         with self.ws.fork():
             K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True, dy_packed=pk, xp=self.xp)
         if dx is not None:
             K.conv_dgrad(self.dz, self.w16, dx, s, self._split(), accumulate, bnb=bnb, wp=self.wp, dy_packed=pk)
-        return False
 
 
 class BasicBlock(Layer):
@@ -479,46 +432,23 @@ class BasicBlock(Layer):
         layer.forward(x, train=train, xp=src.yp, bn=False)
         return Pending.of(layer)
 
-    def c2_fold(self, dout: torch.Tensor, dx: torch.Tensor) -> FoldSpec:
-        """conv2's BatchNorm backward as a fold into the launch that writes its
-        upstream gradient ``dout`` last (the next block's conv1 pair)."""
-        if self.sc is None:
-            return FoldSpec(self.c2, dout, dres=dx, wait=True)
-        return FoldSpec(self.c2, dout, dres=self.dres, side=self.sc.bn_side(), wait=True)
-
-    def backward(self, dout, dx, presummed: bool = False, prev: K.BnBwdTarget | None = None,
-                 bn_done: bool = False, prev_fold: FoldSpec | None = None):
+    def backward(self, dout, dx, presummed: bool = False, prev: K.BnBwdTarget | None = None):
         """``presummed``: conv2's BN reductions were fused into dout's producer;
         ``prev``: the BN consuming dx (the previous block's conv2 or the stem),
-        whose reductions are fused into the LAST dgrad writing dx (conv1's).
-        ``bn_done``: conv2's BN backward already ran (folded into the launch
-        that wrote dout); ``prev_fold``: the previous block's conv2 BN
-        backward, carried by conv1's paired launch (which writes dx last).
-        Every BN backward apply after the first rides in the paired launch
-        before it (conv32.hip folded_bn_bwd): conv1's in conv2's pair, the
-        projection shortcut's in conv2's pair and conv1's in the shortcut's."""
+        whose reductions are fused into the LAST dgrad writing dx (conv1's)."""
         if self.sc is None:
             # identity shortcut: masked dout goes straight into dx, conv1's
             # dgrad then accumulates onto it (no add kernel)
-            self.c2.backward(dout, self.da, dres=dx, presummed=presummed, bnb=self.c1.bn_target(), bn_done=bn_done,
-                             fold=FoldSpec(self.c1, self.da, wait=True))
-            self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev, bn_done=True, fold=prev_fold)
+            self.c2.backward(dout, self.da, dres=dx, presummed=presummed, bnb=self.c1.bn_target())
+            self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev)
         else:
             # the shortcut BN's backward sums ride in conv2's BN-backward launch
             # (it writes dres, the shortcut's upstream gradient)
             side = self.sc.bn_side()
-            if side is not None:
-                # sc's BN backward (dres and its sums come from conv2's BN
-                # backward, an earlier launch) rides in conv2's pair; conv1's
-                # (da and its sums: conv2's pair) in the shortcut's pair
-                self.c2.backward(dout, self.da, dres=self.dres, presummed=presummed, bnb=self.c1.bn_target(),
-                                 side=side, bn_done=bn_done, fold=FoldSpec(self.sc, self.dres))
-                self.sc.backward(self.dres, dx, presummed=True, bn_done=True, fold=FoldSpec(self.c1, self.da))
-            else:
-                self.c2.backward(dout, self.da, dres=self.dres, presummed=presummed, bnb=self.c1.bn_target(),
-                                 side=side, bn_done=bn_done, fold=FoldSpec(self.c1, self.da, wait=True))
-                self.sc.backward(self.dres, dx, presummed=False)
-            self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev, bn_done=True, fold=prev_fold)
+            self.c2.backward(dout, self.da, dres=self.dres, presummed=presummed, bnb=self.c1.bn_target(),
+                             side=side)
+            self.sc.backward(self.dres, dx, presummed=side is not None)
+            self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev)
 
 
 class ClassifierHead(Layer):

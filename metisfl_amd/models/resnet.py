@@ -135,14 +135,11 @@ class ResNet18(StaticNet):
         # the BN that consumes it -- the previous block's conv2, or the stem.
         # The last block's conv2 (fed by the head) reduces on its own unless
         # the head applied its BatchNorm and added the sums (fused fill).
-        # The previous block's conv2 BN backward rides in this block's conv1
-        # pair (the last writer of its upstream gradient): layers.py FoldSpec.
         d = dlast.view(self.blocks[-1].out_shape)
         for i in range(len(self.blocks) - 1, -1, -1):
             prev = self.blocks[i - 1].c2 if i > 0 else self.stem
             last = i == len(self.blocks) - 1
-            fold = self.blocks[i - 1].c2_fold(self.dacts[i], self.dacts[i - 1]) if i > 0 else None
             self.blocks[i].backward(d, self.dacts[i], presummed=(not last) or self.head.summed_input_bn,
-                                    prev=prev.bn_target(), bn_done=not last, prev_fold=fold)
+                                    prev=prev.bn_target())
             d = self.dacts[i]
         self.stem.backward(d, None, presummed=True)

@@ -233,51 +233,14 @@ def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShap
     conv_forward(x, w2, y2, ConvShape(shp.N, shp.H, shp.W, shp.C, shp.Co, 1, 1, 2, 0), ws2, stats2)
 
 
-@dataclass
-class BnFold:
-    """A BatchNorm backward apply (bn_backward's operands, presummed) carried
-    by a paired conv backward launch as a third workgroup role (conv32.hip
-    folded_bn_bwd) instead of its own launch.  ``wait``: its upstream gradient
-    ``dy`` is that launch's dx (the apply waits for the dgrad tiles);
-    otherwise ``dy`` came from an earlier launch.  ``sync``: int32[2] device
-    scratch, zero between launches (the launch re-arms it)."""
-    dy: torch.Tensor
-    z: torch.Tensor
-    y: torch.Tensor | None
-    C: int
-    gamma: torch.Tensor
-    mean: torch.Tensor
-    invstd: torch.Tensor
-    acc: torch.Tensor
-    dgamma: torch.Tensor | None
-    dbeta: torch.Tensor | None
-    dz: torch.Tensor          # int32 view: packed bf16x3 output
-    dres: torch.Tensor | None
-    side: "BnSide | None"
-    wait: bool
-    sync: torch.Tensor
-
-
 def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
-                       bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False, xp=None,
-                       fold: BnFold | None = None) -> bool:
+                       bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False, xp=None) -> None:
     """A layer's weight gradient (dw += ..., dw zero on entry) and input
     gradient (as conv_dgrad) -- on the GPU in ONE paired launch, so the two
     independent, latency-bound GEMMs share the CUs (conv.hip
     conv_bwd_pair_kernel; MFL_CONV_PAIR=0 for two launches).  fp32: one
     launch too (conv32.hip conv32_bwd_pair_kernel, when both plans run 64x64
-    tiles on the fast address paths; MFL_C32_PAIR=0 for two launches).
-    ``fold`` (fp32 GPU path): another BatchNorm's backward apply rides in the
-    same launch; returns whether it ran (False: the caller must run it)."""
-    if dy.is_cuda and dy.dtype == torch.float32 and fold is not None:
-        f, sd = fold, fold.side
-        return bool(ops().conv32_backward_pair_fold(
-            x if xp is None else xp, _dy_arg(dy, dy_packed), dw, w, dx, ws, *shp.args(), accumulate,
-            bnb.z if bnb else None, bnb.y if bnb else None, bnb.mean if bnb else None,
-            bnb.invstd if bnb else None, bnb.acc if bnb else None, wp,
-            f.dy, f.z, f.y, f.C, f.gamma, f.mean, f.invstd, f.acc, f.dgamma, f.dbeta, f.dz, f.dres,
-            sd.z if sd else None, sd.mean if sd else None, sd.invstd if sd else None, sd.acc if sd else None,
-            f.wait, f.sync))
+    tiles on the fast address paths; MFL_C32_PAIR=0 for two launches)."""
     if dy.is_cuda and dy.dtype == torch.float32:
         dy = _dy_arg(dy, dy_packed)
         xa = x if xp is None else xp
@@ -287,7 +250,7 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
         else:
             ops().conv32_backward_pair(xa, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
                                        bnb.invstd, bnb.acc, wp)
-        return False
+        return
     if dy.is_cuda:
         if bnb is None:
             ops().conv_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None,
@@ -295,10 +258,9 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
         else:
             ops().conv_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
                                      bnb.invstd, bnb.acc)
-        return False
+        return
     conv_wgrad(x, dy, dw, shp, accumulate=True)
     conv_dgrad(dy, w, dx, shp, ws, accumulate, bnb=bnb, wp=wp)
-    return False
 
 
 def transpose_krsc(w, wt, Co: int, RS: int, Ci: int) -> None:
