@@ -105,3 +105,4 @@ def test_stem_backward_accumulates_and_rejects_other_shapes():
     assert not K.stem_backward_ok(K.ConvShape(4, 32, 32, 16, 64, 3, 3, 1, 1), dev)  # Cin
     assert not K.stem_backward_ok(K.ConvShape(4, 16, 16, 8, 64, 3, 3, 1, 1), dev)   # 16-pixel rows
     assert not K.stem_backward_ok(K.ConvShape(4, 32, 32, 8, 64, 3, 3, 2, 1), dev)   # stride 2
+
