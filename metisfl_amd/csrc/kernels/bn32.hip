@@ -360,13 +360,18 @@ __global__ __launch_bounds__(576) void stem_bwd32_kernel(BnBwdArgs32 a, const fl
       m[u] = *reinterpret_cast<const float4*>(a.y + o);
     }
   }
-  for (int i = t; i < NX; i += 576) {
+  // the input patch: every load issued before the first LDS store (a
+  // load-store loop paid one memory latency per trip)
+  constexpr int NXU = (NX + 575) / 576;
+  float4 xv[NXU];
+#pragma unroll
+  for (int u = 0; u < NXU; ++u) {
+    const int i = t + 576 * u;
     const int pix = i >> 1, xr = pix / XW, xc = pix - xr * XW;
     const int iy = xr - 1, ix = xc - 1;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
-      v = reinterpret_cast<const float4*>(x)[((pix0 + iy * W + ix) * CI >> 2) + (i & 1)];
-    reinterpret_cast<float4*>(xs)[i] = v;
+    xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < NX && iy >= 0 && iy < H && ix >= 0 && ix < W)
+      xv[u] = reinterpret_cast<const float4*>(x)[((pix0 + iy * W + ix) * CI >> 2) + (i & 1)];
   }
   if (t < G) {
     const int c = co0 + t;
@@ -383,6 +388,9 @@ __global__ __launch_bounds__(576) void stem_bwd32_kernel(BnBwdArgs32 a, const fl
       if (a.dbeta) a.dbeta[c] = (float)s;
     }
   }
+#pragma unroll
+  for (int u = 0; u < NXU; ++u)
+    if (t + 576 * u < NX) reinterpret_cast<float4*>(xs)[t + 576 * u] = xv[u];
   __syncthreads();
   // dz = k1 (g - mean g - xhat mean(g xhat)), g = dy [y > 0] (bn32_bwd_apply);
   // 576 is even, so a thread's channel quad (i & 1) is fixed
