@@ -820,7 +820,7 @@ Plan plan_fwd(int N, int H, int W, int C, int Co) {
   else if (H == 16 && C == 128) fill(2, 8, 16, 1, 64, 2);
   else if (H == 8 && C == 256) fill(3, 8, 8, 2, 64, 4);
   else if (H == 4 && C == 512) fill(4, 4, 4, 8, 64, 8);
-  if (p.stage && p.grid.x * p.grid.y > 1024) p.stage = 0;  // counter block
+  if (p.stage && p.splits > 1 && p.grid.x * p.grid.y > 1024) p.stage = 0;  // split-K arrival counter block
   if (p.stage && p.kchunk != 64) p.stage = 0;               // Cfg::KCH
   return p;
 }

@@ -240,8 +240,17 @@ class StaticNet:
     # a twin of the model bound to the same parameters at this wider batch --
     # the same samples, each exactly once (padded tail skipped), at ~1.35x the
     # throughput of batch-32 passes on MI355X (scripts/eval_probe.py: 10,000
-    # CIFAR samples 108 -> 80 ms).  MFL_EVAL_BATCH=0 disables it.
-    eval_batch: int = int(os.environ.get("MFL_EVAL_BATCH", "128"))
+    # CIFAR samples 108 -> 80 ms at 128, 68 ms at 512).  ``eval_batch`` is the
+    # widest twin; a smaller one is used when the widest would pad the
+    # dataset's last batch by more than 1/16 of the samples (a 1,250-sample
+    # shard at 8 learners: 256).  MFL_EVAL_BATCH=0 disables it.
+    eval_batch: int = int(os.environ.get("MFL_EVAL_BATCH", "512"))
+
+    def _pick_eval_batch(self, n: int) -> int:
+        eb = self.eval_batch
+        while eb > 128 and (-(-n // eb) * eb - n) * 16 > n:
+            eb //= 2
+        return eb
 
     def _make_eval_twin(self, batch: int) -> "StaticNet | None":
         """A model of the same architecture at ``batch`` sharing ``self.state``
@@ -250,9 +259,12 @@ class StaticNet:
 
     def _eval_view(self, ds: DeviceDataset):
         """(twin, the twin's dataset over ds's samples), or None."""
-        EB = self.eval_batch
+        EB = self._pick_eval_batch(ds.n)
         if not (self.use_graphs() and ds.pad_tail and not ds.shuffle and EB > self.B and ds.n > self.B):
             return None
+        if self._eval_twin is not None and self._eval_twin is not False and self._eval_twin.B != EB:
+            self._eval_twin = None  # another dataset size: a twin of its batch
+            self._eval_twin_ds = None
         if self._eval_twin is None:
             self._eval_twin = self._make_eval_twin(EB) or False
         if self._eval_twin is False:
