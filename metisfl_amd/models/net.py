@@ -114,8 +114,8 @@ class StaticNet:
         self._train_graph_ds = None
         self._eval_graph = None
         self._eval_graph_ds = None
-        self._eval_twin = None     # None: not built yet, False: not available
-        self._eval_twin_ds = None  # (source dataset, the twin's view of it)
+        self._eval_twins = {}      # evaluation batch -> twin model (False: the model has none)
+        self._eval_views = {}      # id(source dataset) -> (source dataset, the twin's view of it)
 
     # -- to override ----------------------------------------------------------
     input_shape: tuple = (32, 32, 8)
@@ -238,12 +238,14 @@ class StaticNet:
     # batch it is evaluated in: a full test-set pass (the reference's Keras
     # ``evaluate`` at the training batch size, controller.cc:611) runs through
     # a twin of the model bound to the same parameters at this wider batch --
-    # the same samples, each exactly once (padded tail skipped), at ~1.35x the
-    # throughput of batch-32 passes on MI355X (scripts/eval_probe.py: 10,000
-    # CIFAR samples 108 -> 80 ms at 128, 68 ms at 512).  ``eval_batch`` is the
-    # widest twin; a smaller one is used when the widest would pad the
+    # the same samples, each exactly once (padded tail skipped), at 1.35-1.6x
+    # the throughput of batch-32 passes on MI355X (scripts/eval_probe.py:
+    # 10,000 CIFAR samples 108 -> 80 ms at 128, 68 ms at 512).  ``eval_batch``
+    # is the widest twin; a smaller one is used when the widest would pad the
     # dataset's last batch by more than 1/16 of the samples (a 1,250-sample
-    # shard at 8 learners: 256).  MFL_EVAL_BATCH=0 disables it.
+    # shard at 8 learners: 256).  Twins are kept per batch size (an evaluation
+    # task may cover train / validation / test sets of different sizes).
+    # MFL_EVAL_BATCH=0 disables it.
     eval_batch: int = int(os.environ.get("MFL_EVAL_BATCH", "512"))
 
     def _pick_eval_batch(self, n: int) -> int:
@@ -262,16 +264,16 @@ class StaticNet:
         EB = self._pick_eval_batch(ds.n)
         if not (self.use_graphs() and ds.pad_tail and not ds.shuffle and EB > self.B and ds.n > self.B):
             return None
-        if self._eval_twin is not None and self._eval_twin is not False and self._eval_twin.B != EB:
-            self._eval_twin = None  # another dataset size: a twin of its batch
-            self._eval_twin_ds = None
-        if self._eval_twin is None:
-            self._eval_twin = self._make_eval_twin(EB) or False
-        if self._eval_twin is False:
+        if EB not in self._eval_twins:
+            self._eval_twins[EB] = self._make_eval_twin(EB) or False
+        twin = self._eval_twins[EB]
+        if twin is False:
             return None
-        if self._eval_twin_ds is None or self._eval_twin_ds[0] is not ds:
-            self._eval_twin_ds = (ds, DeviceDataset(ds.x[:ds.n], ds.y[:ds.n], EB, shuffle=False, pad_tail=True))
-        return self._eval_twin, self._eval_twin_ds[1]
+        hit = self._eval_views.get(id(ds))
+        if hit is None or hit[0] is not ds or hit[1].batch_size != EB:
+            hit = (ds, DeviceDataset(ds.x[:ds.n], ds.y[:ds.n], EB, shuffle=False, pad_tail=True))
+            self._eval_views[id(ds)] = hit
+        return twin, hit[1]
 
     def evaluate(self, ds: DeviceDataset, max_steps: int | None = None) -> dict:
         """Loss / accuracy of the current model on ``ds`` (BN in inference mode)."""

@@ -27,8 +27,9 @@ def test_eval_twin_matches_training_batch_pass(n):
     net.eval_batch = 512
     got = net.evaluate(test_ds)
     # 1000 samples: two batches of 512 (2.4 % padding); 256: one of 256
-    assert net._eval_twin not in (None, False) and net._eval_twin.B == {1000: 512, 256: 256}[n]
-    assert net._eval_twin.state is net.state
+    twin = net._eval_twins[{1000: 512, 256: 256}[n]]
+    assert twin is not False and twin.B == {1000: 512, 256: 256}[n]
+    assert twin.state is net.state
     # the wider batch may pick other split-K plans (fp32 summation order):
     # a near-tie argmax may flip, the loss agrees to fp32 rounding
     assert abs(got["accuracy"] - ref["accuracy"]) <= 2.0 / n
