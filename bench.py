@@ -4,7 +4,7 @@
 Metric (BASELINE.json): "federation-round time (ms) + rounds/sec, 8-learner
 FedAvg CIFAR-10 ResNet-18".  One benchmark "step" is ONE federation round:
 
-  every learner (one per GPU, one process per GPU) trains its IID shard of
+  every one of the ``--learners`` (default 8) learners trains its IID shard of
   the 50,000-image CIFAR-10 training set for ``--local-epochs`` epochs
   (batch 32, MomentumSGD lr 0.005 / momentum 0.75: the reference's CIFAR-10
   experiment config, examples/config/cifar10/
@@ -14,9 +14,17 @@ FedAvg CIFAR-10 ResNet-18".  One benchmark "step" is ONE federation round:
   kernel + one RCCL all-reduce) leaving the community model resident on every
   GPU.
 
-The dataset is fixed (50k train / 10k test images) and split across the N
-learners, so total work per round is constant: scaling is "strong" and
-``value`` (rounds/s of the whole federation) is the whole-job aggregate.
+The federation is the same 8 learners at every GPU count: one process per
+GPU hosts learners/N of them (models/colocated.py: each with its own model,
+optimizer state, shard and step graphs, replayed on its own HIP stream, so
+co-located learners share the GPU concurrently -- the reference likewise
+runs several learners per GPU, e.g. 10 learners on 5 GPUs in
+examples/config/cifar10/test_localhost_synchronous_momentumsgd.yaml).  At
+N=8 that is one learner per MI355X (BASELINE config 2).  The dataset is
+fixed (50k train / 10k test images) and split across the learners, so the
+federation -- shards, step budgets, FedAvg weights -- and the total work per
+round do not depend on N: scaling is "strong" and ``value`` (rounds/s of the
+whole federation) is the whole-job aggregate.
 Data are synthetic tensors of CIFAR-10's shape, weights random-init of the
 ResNet-18 architecture (no network for datasets/checkpoints).
 
@@ -51,6 +59,8 @@ BASELINE_VALUE = None  # BASELINE.json "published": {} -- no reference number ex
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--learners", type=int, default=8,
+                    help="federation learners (BASELINE: 8), learners/N co-located on each GPU")
     ap.add_argument("--steps", type=int, default=3, help="timed federation rounds")
     ap.add_argument("--warmup", type=int, default=1, help="untimed federation rounds")
     ap.add_argument("--local-epochs", type=int, default=4)
@@ -91,23 +101,33 @@ def main() -> int:
     n = comm.world
     dev = comm.device
     torch.manual_seed(1234 + comm.rank)
+    nl = max(args.learners, n)
+    if nl % n:
+        print(f"[bench] error: {nl} learners do not split evenly over {n} GPUs", file=sys.stderr)
+        return 2
+    L = nl // n  # learners co-located on this GPU
 
-    # IID shard of the fixed-size dataset (strong scaling).
-    n_train = args.train_size // n + (1 if comm.rank < args.train_size % n else 0)
-    n_test = args.test_size // n + (1 if comm.rank < args.test_size % n else 0)
-    g = torch.Generator(device=dev)
-    g.manual_seed(1000 + comm.rank)
-    xtr = torch.randn((n_train, 32, 32, 3), generator=g, device=dev)
-    ytr = torch.randint(0, 10, (n_train,), generator=g, device=dev)
-    xte = torch.randn((n_test, 32, 32, 3), generator=g, device=dev)
-    yte = torch.randint(0, 10, (n_test,), generator=g, device=dev)
+    def share(total: int, i: int) -> int:
+        return total // nl + (1 if i < total % nl else 0)
 
     opt = OptimizerSpec("momentum_sgd", args.lr, momentum=args.momentum)
-    net = ResNet18(batch_size=args.batch, device=dev, optimizer=opt, seed=7, dtype=args.dtype,
-                   width_mult=args.width_mult, conv_products=args.conv_products)
-    train_ds = net.make_dataset(xtr, ytr, seed=comm.rank)
-    test_ds = net.make_dataset(xte, yte, seed=comm.rank, shuffle=False)
-    del xtr, xte
+    nets, train_dss, test_dss = [], [], []
+    for j in range(L):
+        gi = comm.rank * L + j  # global learner index
+        # IID shard of the fixed-size dataset (strong scaling)
+        g = torch.Generator(device=dev)
+        g.manual_seed(1000 + gi)
+        xtr = torch.randn((share(args.train_size, gi), 32, 32, 3), generator=g, device=dev)
+        ytr = torch.randint(0, 10, (xtr.shape[0],), generator=g, device=dev)
+        xte = torch.randn((share(args.test_size, gi), 32, 32, 3), generator=g, device=dev)
+        yte = torch.randint(0, 10, (xte.shape[0],), generator=g, device=dev)
+        net = ResNet18(batch_size=args.batch, device=dev, optimizer=opt, seed=7, dtype=args.dtype,
+                       width_mult=args.width_mult, conv_products=args.conv_products)
+        nets.append(net)
+        train_dss.append(net.make_dataset(xtr, ytr, seed=gi))
+        test_dss.append(net.make_dataset(xte, yte, seed=gi, shuffle=False))
+        del xtr, xte
+    net, train_ds = nets[0], train_dss[0]
     cfg = FederationConfig(protocol="synchronous", batch_size=args.batch,
                            local_epochs=args.local_epochs, evaluate_test=not args.no_eval,
                            evaluate_community=not args.no_eval,
@@ -115,9 +135,8 @@ def main() -> int:
     engine = None
     if comm.rank == 0:  # the native controller keeps the round bookkeeping
         from metisfl_amd.parallel.engine_bridge import CollectiveController
-        sizes = [args.train_size // n + (1 if r < args.train_size % n else 0) for r in range(n)]
-        engine = CollectiveController(cfg, sizes)
-    fed = CollectiveFederation(comm, net, train_ds, cfg, test_ds=test_ds, engine=engine)
+        engine = CollectiveController(cfg, [share(args.train_size, i) for i in range(nl)])
+    fed = CollectiveFederation(comm, nets, train_dss, cfg, test_ds=test_dss, engine=engine)
 
     def sync():
         if dev.type == "cuda":
@@ -149,11 +168,16 @@ def main() -> int:
     updates = fed.num_local_updates[0]
     agg_ms = sum(r.aggregation_ms for r in timed) / max(1, len(timed))
     model_bytes = net.state.model32.numel() * 4
-    if n == 1:
+    if nl == 1:
         aggregation = "none (single learner: the round ends with the local model)"
     elif args.secure_aggregation:
         aggregation = ("PWA(NUM_TRAINING_EXAMPLES) over RNS-CKKS (N=8192, 52-bit scale): "
                        "device encrypt, int64 RCCL all-reduce of ciphertexts, device decrypt")
+    elif n == 1:
+        aggregation = f"FedAvg(NUM_TRAINING_EXAMPLES) of {nl} co-located learners: one weighted-sum kernel"
+    elif L > 1:
+        aggregation = (f"FedAvg(NUM_TRAINING_EXAMPLES): weighted-sum kernel over the {L} learners of each GPU "
+                       "+ one RCCL all-reduce")
     else:
         aggregation = "FedAvg(NUM_TRAINING_EXAMPLES): scale kernel + one RCCL all-reduce"
     out = {
@@ -172,8 +196,9 @@ def main() -> int:
         "config": {
             "model": "resnet18-cifar",
             "dataset": "cifar10 (50k train / 10k test, synthetic)",
-            "learners": n,
-            "global_batch": args.batch * n,
+            "learners": nl,
+            "learners_per_gpu": L,
+            "global_batch": args.batch * nl,
             "per_learner_batch": args.batch,
             "seq_len": None,
             "local_epochs": args.local_epochs,
@@ -201,7 +226,7 @@ def main() -> int:
     out["aggregation_weights"] = [float(w) for w in timed[-1].weights] if timed and timed[-1].weights is not None else None
     out["community_model"] = _community_digests(comm, net)
     if args.dtype == "fp32" and net.conv_products == "bf16x3" and args.exact_updates > 0:
-        out["conv_products_exact"] = _exact_pass(args, comm, train_ds, opt, sync, out, updates)
+        out["conv_products_exact"] = _exact_pass(args, comm, train_dss, opt, sync, out, updates)
     if comm.rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
@@ -225,36 +250,41 @@ def _community_digests(comm, net) -> dict:
     return {"sha256_128": digests, "identical": len(set(digests)) == 1}
 
 
-def _exact_pass(args, comm, train_ds, opt, sync, out, updates) -> dict:
-    """The strict-IEEE alternative, timed after the headline rounds: a fresh
-    ResNet-18 whose convolutions multiply on the exact fp32 MFMA
-    (v_mfma_f32_32x32x2_f32) runs ``--exact-updates`` local updates (after
-    20 untimed ones that capture its step graph); the round-time estimate
-    swaps the measured bf16x3 training time for the exact one and keeps the
-    round's measured evaluation / aggregation time."""
+def _exact_pass(args, comm, train_dss, opt, sync, out, updates) -> dict:
+    """The strict-IEEE alternative, timed after the headline rounds: fresh
+    ResNet-18 learners (as many as this GPU hosts, co-located the same way)
+    whose convolutions multiply on the exact fp32 MFMA
+    (v_mfma_f32_32x32x2_f32) run ``--exact-updates`` local updates each
+    (after 16 untimed ones that capture their step graphs); the round-time
+    estimate swaps the measured bf16x3 training time for the exact one and
+    keeps the round's measured evaluation / aggregation time."""
     import torch
+    from metisfl_amd.models.colocated import CoLocatedLearners
     from metisfl_amd.models.resnet import ResNet18
-    net = ResNet18(batch_size=args.batch, device=comm.device, optimizer=opt, seed=7, dtype="fp32",
-                   width_mult=args.width_mult, conv_products="exact")
+    nets = [ResNet18(batch_size=args.batch, device=comm.device, optimizer=opt, seed=7, dtype="fp32",
+                     width_mult=args.width_mult, conv_products="exact") for _ in train_dss]
+    group = CoLocatedLearners(nets, train_dss)
     k = args.exact_updates
-    net.train_steps(train_ds, 20, step_offset=0)
+    warm = 16
+    group.train([warm] * len(nets), [0] * len(nets))
     comm.barrier()
     sync()
     t0 = time.perf_counter()
-    net.train_steps(train_ds, k, step_offset=20)
+    group.train([k] * len(nets), [warm] * len(nets))
     sync()
     el = comm.all_max(time.perf_counter() - t0)
-    exact_upd = el * 1e3 / k
+    exact_upd = el * 1e3 / k  # per local update of every co-located learner
     fast_upd = out["train_ms_mean"] / max(1, updates)
     from metisfl_amd.ops.nn import set_conv_products
     set_conv_products("bf16x3")
-    del net
+    del nets, group
     if comm.device.type == "cuda":
         torch.cuda.empty_cache()
-    return {"updates_timed": k, "ms_per_update": exact_upd, "bf16x3_ms_per_update": fast_upd,
+    return {"updates_timed": k, "learners": len(train_dss), "ms_per_update": exact_upd,
+            "bf16x3_ms_per_update": fast_upd,
             "round_ms_est": out["round_ms"] + (exact_upd - fast_upd) * updates,
-            "method": "measured per-update time x local updates per round + the measured "
-                      "non-training part of the bf16x3 round"}
+            "method": "measured time per local update of the co-located learners x local updates per "
+                      "round + the measured non-training part of the bf16x3 round"}
 
 
 if __name__ == "__main__":

@@ -169,6 +169,9 @@ void Controller::restore(const std::string& blob) {
       dq.push_back(t);
     }
   }
+  completed_iter_.clear();
+  for (const auto& [id, dq] : local_meta_)
+    if (learners_.count(id) && !dq.empty()) completed_iter_[id] = dq.front().global_iteration;
   community_set_ = in.u32() != 0;
   const std::string cm = in.str();
   if (community_set_) community_ = parse_federated_model(cm);

@@ -223,6 +223,7 @@ Dispatch Controller::remove_learner(const std::string& id, const std::string& to
   if (auto* d = DeviceAggregator::peek()) d->drop(id);
   learners_.erase(id);
   templates_.erase(id);
+  completed_iter_.erase(id);
   const auto active = active_ids_locked();
   auto ready = scheduler_->poll(active);
   if (ready.empty()) return Dispatch{};
@@ -316,10 +317,10 @@ Dispatch Controller::learner_completed_task(const std::string& id, const std::st
   const int64_t t0 = now_ns();
   // A duplicate completion (a client retry whose first reply was lost) of a
   // task already recorded is acknowledged and ignored: (learner, global
-  // iteration) identifies a task under every protocol.
-  auto lm = local_meta_.find(id);
-  if (lm != local_meta_.end() && !lm->second.empty() && tm.global_iteration != 0 &&
-      lm->second.front().global_iteration == tm.global_iteration)
+  // iteration) identifies a task under every protocol -- within one
+  // membership of the learner (completed_iter_ is cleared when it leaves).
+  auto lc = completed_iter_.find(id);
+  if (lc != completed_iter_.end() && tm.global_iteration != 0 && lc->second == tm.global_iteration)
     return Dispatch{};
   if (!metadata_.empty() && idx < metadata_.size()) {
     metadata_[idx].completed_by.push_back(id);
@@ -336,6 +337,7 @@ Dispatch Controller::learner_completed_task(const std::string& id, const std::st
   if (!metadata_.empty() && idx < metadata_.size())
     metadata_[idx].insertion_ms[id] = (double)(now_ns() - t0) / 1e6;
   local_meta_[id].push_front(tm);
+  completed_iter_[id] = tm.global_iteration;
   return schedule_tasks_locked(id, tm.global_iteration);
 }
 
@@ -357,6 +359,7 @@ Dispatch Controller::evict_learner(const std::string& id) {
   if (auto* d = DeviceAggregator::peek()) d->drop(id);
   learners_.erase(id);
   templates_.erase(id);
+  completed_iter_.erase(id);
   ++evicted_;
   const auto active = active_ids_locked();
   auto ready = scheduler_->poll(active);

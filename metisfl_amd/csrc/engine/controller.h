@@ -192,6 +192,12 @@ class Controller {
   std::map<std::string, LearnerRec> learners_;
   std::map<std::string, uint32_t> templates_;
   std::map<std::string, std::deque<TaskMeta>> local_meta_;  // newest first
+  // global iteration of each CURRENT member's last recorded completion: the
+  // duplicate-completion check.  Cleared when a learner leaves or is evicted
+  // (its local_meta_ lineage is kept, as the reference keeps
+  // local_tasks_metadata_), so a learner that rejoins under the same
+  // host:port in the same round is not mistaken for a retry.
+  std::map<std::string, uint32_t> completed_iter_;
   std::unique_ptr<Scheduler> scheduler_;
   std::unique_ptr<AggregationFunction> aggregator_;
   std::unique_ptr<ModelStore> store_;

@@ -1,0 +1,134 @@
+"""Co-located learners: several federation learners resident on ONE GPU.
+
+The reference places learners on GPUs round-robin and lets several share a
+device (its CIFAR-10 experiment runs 10 learners on 5 GPUs,
+examples/config/cifar10/test_localhost_synchronous_momentumsgd.yaml:4-27;
+driver_session.py:558-562 pins each learner process with
+CUDA_VISIBLE_DEVICES).  There every learner is its own process with its own
+framework runtime, and learners on one GPU time-share it.
+
+Here the learners of one GPU live in ONE process, each with its own model,
+optimizer state, workspace, data shard and captured step graphs, and each
+replays its graphs on its own HIP stream.  A ResNet-18 update at batch 32 is
+latency-bound on MI355X (~64 launches of 256-576 workgroups on 256 CUs, one
+workgroup per CU for the halo convs: profiles/ANALYSIS.md), so one learner
+leaves most of the chip idle between and inside launches; streams let the
+hardware queues run up to four learners' kernels side by side
+(GPU_MAX_HW_QUEUES=4, the HIP default: measured 0.70 ms per update with 4-8
+learners against 1.04 ms for one, profiles/r4/colocated/).
+
+The round's FedAvg over co-located learners is a local weighted sum (K1,
+one launch over all of them) followed by the cross-GPU all-reduce
+(parallel/federation.py), i.e. a hierarchical reduce: xGMI only ever carries
+one model per GPU.
+"""
+from __future__ import annotations
+
+import torch
+
+
+class CoLocatedLearners:
+    """L learners on one device; ``nets[j]`` trains ``train_dss[j]``."""
+
+    def __init__(self, nets: list, train_dss: list, test_dss: list | None = None):
+        assert len(nets) == len(train_dss) and nets
+        self.nets = list(nets)
+        self.train_dss = list(train_dss)
+        self.test_dss = list(test_dss) if test_dss is not None else [None] * len(nets)
+        dev = self.nets[0].device
+        self.device = dev
+        self.cuda = dev.type == "cuda"
+        self.streams = [torch.cuda.Stream(device=dev) for _ in self.nets] if self.cuda else [None] * len(nets)
+        self._ev = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                     for _ in self.nets] if self.cuda else None)
+
+    def __len__(self) -> int:
+        return len(self.nets)
+
+    def _ctx(self, j: int):
+        import contextlib
+        return torch.cuda.stream(self.streams[j]) if self.cuda else contextlib.nullcontext()
+
+    def _fork(self) -> None:
+        """Every learner stream waits for the work already issued on the
+        current stream (e.g. the aggregation that wrote the models)."""
+        if self.cuda:
+            cur = torch.cuda.current_stream(self.device)
+            for s in self.streams:
+                s.wait_stream(cur)
+
+    def _join(self) -> None:
+        if self.cuda:
+            cur = torch.cuda.current_stream(self.device)
+            for s in self.streams:
+                cur.wait_stream(s)
+
+    def train(self, nsteps: list[int], step_offsets: list[int]) -> list[float]:
+        """Run ``nsteps[j]`` local updates of every learner concurrently ->
+        per-learner milliseconds from the common start to that learner's last
+        update (its wall-clock share of the co-located run)."""
+        import time
+        # capture before the streams run concurrently (a capture synchronises
+        # the device)
+        for net, ds, n in zip(self.nets, self.train_dss, nsteps):
+            net.prepare_graphs(ds, n)
+        self._fork()
+        t0 = time.perf_counter()
+        if self.cuda:
+            for j in range(len(self)):
+                with self._ctx(j):
+                    self._ev[j][0].record()
+        gens = [net.train_steps_iter(ds, n, off)
+                for net, ds, n, off in zip(self.nets, self.train_dss, nsteps, step_offsets)]
+        live = list(range(len(gens)))
+        host_ms = [0.0] * len(gens)
+        while live:
+            nxt = []
+            for j in live:
+                with self._ctx(j):
+                    try:
+                        next(gens[j])
+                        nxt.append(j)
+                    except StopIteration:
+                        if self.cuda:
+                            self._ev[j][1].record()
+                        host_ms[j] = (time.perf_counter() - t0) * 1e3
+            live = nxt
+        self._join()
+        if not self.cuda:
+            return host_ms
+        for _, e1 in self._ev:
+            e1.synchronize()
+        return [e0.elapsed_time(e1) for e0, e1 in self._ev]
+
+    def evaluate(self, dss: list | None = None, max_steps: int | None = None) -> list[dict | None]:
+        """Every learner evaluates its current model on its dataset (default:
+        its test shard), concurrently; None where a learner has no dataset."""
+        dss = self.test_dss if dss is None else dss
+        self._fork()
+        owners = []
+        for j, (net, ds) in enumerate(zip(self.nets, dss)):
+            if ds is None:
+                owners.append(None)
+                continue
+            with self._ctx(j):
+                owners.append(net.begin_evaluate(ds, max_steps))
+        self._join()
+        return [net.finish_evaluate(o) if o is not None else None for net, o in zip(self.nets, owners)]
+
+    def weighted_sum_into(self, out: torch.Tensor, weights: list[float]) -> None:
+        """out = sum_j (fp32)(w_j * model_j) in learner order (the reference's
+        FedAvg term rounding, federated_average.cc:14-37; K1, one launch).
+        ``out`` may alias learner 0's model buffer."""
+        from metisfl_amd.ops.aggregate import weighted_sum
+        weighted_sum(out, [n.state.model32 for n in self.nets], [float(w) for w in weights])
+
+    def install(self, src: torch.Tensor) -> None:
+        """Every learner's model <- ``src`` (the community model); mirrors and
+        FedProx anchors follow."""
+        for net in self.nets:
+            st = net.state
+            if st.model32.data_ptr() != src.data_ptr():
+                st.model32.copy_(src)
+            st.refresh_bf16()
+            st.set_anchor()

@@ -182,6 +182,11 @@ class StaticNet:
         snap = self.state.model32.clone()
         step0 = self.state.step.clone()
         slots = [t.clone() if t is not None else None for t in (self.state.m, self.state.v)]
+        # the warm-up and captured bodies also accumulate loss / accuracy and
+        # tick the evaluation counter: restored too, so a task's statistics
+        # cover its own updates only
+        stats0 = self.stats.clone()
+        ectr0 = self.eval_step_ctr.clone()
         with torch.cuda.stream(s):
             body(ds)
         torch.cuda.current_stream(self.device).wait_stream(s)
@@ -194,6 +199,8 @@ class StaticNet:
         for t, c in zip((self.state.m, self.state.v), slots):
             if t is not None:
                 t.copy_(c)
+        self.stats.copy_(stats0)
+        self.eval_step_ctr.copy_(ectr0)
         self.state.refresh_bf16()
         return g
 
@@ -206,8 +213,26 @@ class StaticNet:
     # where the host reshuffles.  MFL_GRAPH_STEPS=1: one graph per update.
     graph_steps: int = int(os.environ.get("MFL_GRAPH_STEPS", "8"))
 
-    def train_steps(self, ds: DeviceDataset, nsteps: int, step_offset: int = 0) -> None:
-        """Run ``nsteps`` local updates; reshuffles at epoch boundaries."""
+    def prepare_graphs(self, ds: DeviceDataset, nsteps: int | None = None) -> None:
+        """Capture the step graphs for ``ds`` now (1-update and, when a task of
+        ``nsteps`` can use it, K-update), instead of lazily at the first
+        replay: co-located learners capture before their streams run
+        concurrently (models/colocated.py)."""
+        if not self.use_graphs():
+            return
+        if self._train_graph is None or self._train_graph_ds is not ds:
+            self._train_graph = self._capture(self._train_body, ds)
+            self._train_graph_k = None
+            self._train_graph_ds = ds
+        K = max(1, self.graph_steps)
+        if K > 1 and self._train_graph_k is None and (nsteps is None or nsteps >= K) and ds.steps_per_epoch >= K:
+            body = self._train_body
+            self._train_graph_k = self._capture(lambda d: [body(d) for _ in range(K)], ds)
+
+    def train_steps_iter(self, ds: DeviceDataset, nsteps: int, step_offset: int = 0):
+        """``train_steps`` as a generator that yields after every host launch
+        (one graph replay, or one eager step): the co-located learner runner
+        interleaves several learners' launches on their own streams."""
         graphs = self.use_graphs()
         if graphs and (self._train_graph is None or self._train_graph_ds is not ds):
             self._train_graph = self._capture(self._train_body, ds)
@@ -226,12 +251,19 @@ class StaticNet:
                     self._train_graph_k = self._capture(lambda d: [body(d) for _ in range(K)], ds)
                 self._train_graph_k.replay()
                 i += K
+                yield K
                 continue
             if graphs:
                 self._train_graph.replay()
             else:
                 self._train_body(ds)
             i += 1
+            yield 1
+
+    def train_steps(self, ds: DeviceDataset, nsteps: int, step_offset: int = 0) -> None:
+        """Run ``nsteps`` local updates; reshuffles at epoch boundaries."""
+        for _ in self.train_steps_iter(ds, nsteps, step_offset):
+            pass
 
     # Evaluation micro-batch.  BatchNorm runs on its running statistics in
     # inference mode, so a sample's loss / prediction does not depend on the
@@ -275,11 +307,14 @@ class StaticNet:
             self._eval_views[id(ds)] = hit
         return twin, hit[1]
 
-    def evaluate(self, ds: DeviceDataset, max_steps: int | None = None) -> dict:
-        """Loss / accuracy of the current model on ``ds`` (BN in inference mode)."""
+    def begin_evaluate(self, ds: DeviceDataset, max_steps: int | None = None):
+        """Issue a loss / accuracy pass over ``ds`` (BN in inference mode) on
+        the current stream without waiting for it; ``finish_evaluate`` reads
+        the result.  -> the model whose statistics hold it (self or the
+        evaluation twin)."""
         view = self._eval_view(ds) if max_steps is None else None
         if view is not None:
-            return view[0].evaluate(view[1])
+            return view[0].begin_evaluate(view[1])
         nsteps = ds.steps_per_epoch if max_steps is None else min(max_steps, ds.steps_per_epoch)
         self.stats.zero_()
         self.eval_step_ctr.zero_()
@@ -293,9 +328,17 @@ class StaticNet:
                 self._eval_graph.replay()
             else:
                 self._eval_body(ds)
-        s = self.stats.cpu().numpy()
+        return self
+
+    @staticmethod
+    def finish_evaluate(owner: "StaticNet") -> dict:
+        s = owner.stats.cpu().numpy()
         n = max(1.0, float(s[2]))
         return {"loss": float(s[0] / n), "accuracy": float(s[1] / n)}
+
+    def evaluate(self, ds: DeviceDataset, max_steps: int | None = None) -> dict:
+        """Loss / accuracy of the current model on ``ds`` (BN in inference mode)."""
+        return self.finish_evaluate(self.begin_evaluate(ds, max_steps))
 
     def reset_train_stats(self) -> None:
         self.stats.zero_()

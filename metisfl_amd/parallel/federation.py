@@ -1,7 +1,8 @@
-"""Collective (single-node, one learner per GPU) federation engine.
+"""Collective (single-node, one process per GPU) federation engine.
 
-Each process hosts ONE persistent learner whose model, optimizer state and
-data shard stay resident in HBM across rounds.  A synchronous FedAvg round is
+Each process hosts L >= 1 persistent learners (co-located on its GPU,
+models/colocated.py) whose models, optimizer states and data shards stay
+resident in HBM across rounds.  A synchronous FedAvg round is
 
   1. local training: ``num_local_updates`` graph-replayed steps,
   2. all-gather of a few scalars per learner (dataset size, completed
@@ -12,7 +13,9 @@ data shard stay resident in HBM across rounds.  A synchronous FedAvg round is
   4. in-place pre-scale ``theta_i *= w_i`` (K1) and ONE RCCL all-reduce of the
      flat model buffer: every learner now holds the community model, which is
      the reference's gather -> FedAvg -> RunTask broadcast
-     (controller.cc:428-518, 795-950) collapsed into one collective.
+     (controller.cc:428-518, 795-950) collapsed into one collective.  With L
+     co-located learners the rank first sums its own learners' scaled models
+     (one K1 launch), so xGMI carries one model per GPU whatever L is.
 
 Semi-synchronous rounds use the same barrier with per-learner step budgets
 recomputed from the measured per-batch times (controller.cc:520-569).
@@ -147,32 +150,54 @@ def install_community_model(net, fm) -> None:
 
 
 class CollectiveFederation:
-    """Drives rounds for the learner hosted by this rank."""
+    """Drives rounds for the learner(s) hosted by this rank.
+
+    ``net`` / ``train_ds`` / ``test_ds``: one learner, or lists of the L
+    learners co-located on this rank's GPU (the same L on every rank).
+    Learner ``j`` of rank ``r`` is global learner ``r * L + j``: metadata
+    rows, aggregation weights, step budgets and learner ids are per global
+    learner, in that order."""
 
     def __init__(self, comm: Comm, net, train_ds, cfg: FederationConfig, test_ds=None,
                  learner_ids: list[str] | None = None, engine=None, broadcast_initial: bool = True):
         self.comm = comm
-        self.net = net
-        self.train_ds = train_ds
-        self.test_ds = test_ds
+        nets = list(net) if isinstance(net, (list, tuple)) else [net]
+        tds = list(train_ds) if isinstance(train_ds, (list, tuple)) else [train_ds]
+        vds = list(test_ds) if isinstance(test_ds, (list, tuple)) else [test_ds] * len(nets)
+        if not (len(nets) == len(tds) == len(vds)):
+            raise ValueError(f"{len(nets)} learners, {len(tds)} train / {len(vds)} test datasets")
+        self.L = len(nets)
+        self.nets, self.train_dss, self.test_dss = nets, tds, vds
+        self.net, self.train_ds, self.test_ds = nets[0], tds[0], vds[0]
+        self.group = None
+        if self.L > 1:
+            from metisfl_amd.models.colocated import CoLocatedLearners
+            self.group = CoLocatedLearners(nets, tds, vds)
         self.cfg = cfg
         self.engine = engine if comm.rank == 0 else None
         self.world = comm.world
         self.rank = comm.rank
-        self.learner_ids = learner_ids or [f"learner_{r}" for r in range(self.world)]
-        spe = train_ds.steps_per_epoch
+        Ls = comm.all_gather_rows(torch.tensor([float(self.L)], dtype=torch.float64, device=comm.device))
+        if any(int(x) != self.L for x in Ls.cpu().numpy()[:, 0]):
+            raise ValueError(f"co-located learners per rank differ: {Ls.cpu().numpy()[:, 0].tolist()}")
+        self.n_learners = self.world * self.L
+        if self.L > 1 and self.elastic:
+            raise NotImplementedError("straggler drop (participation_ratio / round_deadline_s) runs one "
+                                      "learner per rank")
+        self.learner_ids = learner_ids or [f"learner_{r}" for r in range(self.n_learners)]
         # reference: num_local_updates = epochs * ceil(N_train / batch) per
         # learner (controller.cc:148-153); the join-time dataset sizes are
         # exchanged once
-        sizes = comm.all_gather_rows(torch.tensor([float(train_ds.n)], dtype=torch.float64,
-                                                  device=comm.device)).cpu().numpy()[:, 0]
+        sizes = comm.all_gather_rows(torch.tensor([float(d.n) for d in tds], dtype=torch.float64,
+                                                  device=comm.device)).cpu().numpy().reshape(-1)
         self.dataset_sizes = [int(x) for x in sizes]
         self.num_local_updates = [cfg.local_epochs * max(1, math.ceil(n / cfg.batch_size))
                                   for n in self.dataset_sizes]
-        self.steps_done = 0
+        self.steps_done_l = [0] * self.L
         self.global_iteration = 0
         self.history: list[RoundRecord] = []
-        self._spe = spe
+        self._spes = [d.steps_per_epoch for d in tds]
+        self._spe = self._spes[0]
         dev = comm.device
         self._ev0 = torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else None
         self._ev1 = torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else None
@@ -185,13 +210,32 @@ class CollectiveFederation:
         if broadcast_initial:
             self.broadcast_initial_model()
 
+    @property
+    def steps_done(self) -> int:
+        """Local updates run so far by this rank's first learner."""
+        return self.steps_done_l[0]
+
+    @steps_done.setter
+    def steps_done(self, v: int) -> None:
+        self.steps_done_l[0] = int(v)
+
+    def local_learners(self) -> list[int]:
+        """Global indices of this rank's learners."""
+        return [self.rank * self.L + j for j in range(self.L)]
+
     # ------------------------------------------------------------------------
     def broadcast_initial_model(self) -> None:
         """ReplaceCommunityModel equivalent: rank 0's model becomes everyone's."""
         st = self.net.state
         self.comm.broadcast_(st.model32, src=0)
-        st.refresh_bf16()
-        st.set_anchor()
+        self._install_local(st.model32)
+
+    def _install_local(self, src: torch.Tensor) -> None:
+        if self.group is not None:
+            self.group.install(src)
+        else:
+            self.net.state.refresh_bf16()
+            self.net.state.set_anchor()
 
     def _sync(self):
         if self.comm.device.type == "cuda":
@@ -230,6 +274,31 @@ class CollectiveFederation:
                 return done, False  # dropped from this round
         store.add(key, 1)
         return done, True
+
+    def local_train_all(self, nsteps: list[int]) -> list[dict]:
+        """Local training of every learner of this rank (concurrently on
+        their own streams when co-located) -> one result dict per learner."""
+        if self.L == 1:
+            return [self.local_train(nsteps[0])]
+        for net in self.nets:
+            net.reset_train_stats()
+        with tracing.range("metisfl.local_train"):
+            ms = self.group.train(list(nsteps), list(self.steps_done_l))
+        out = []
+        for j, (net, ran) in enumerate(zip(self.nets, nsteps)):
+            self.steps_done_l[j] += ran
+            tr = net.train_stats()
+            spe = self._spes[j]
+            out.append({"ms": ms[j], "ms_per_batch": ms[j] / max(1, ran), "ms_per_epoch": ms[j] / max(1, ran) * spe,
+                        "completed_batches": ran, "completed_epochs": ran / spe,
+                        "train_loss": tr["loss"], "train_accuracy": tr["accuracy"], "participated": True})
+        if self.cfg.evaluate_test:
+            with tracing.range("metisfl.evaluate"):
+                tests = self.group.evaluate(max_steps=self.cfg.eval_max_steps)
+            for o, t in zip(out, tests):
+                if t is not None:
+                    o["test"] = t
+        return out
 
     def local_train(self, nsteps: int) -> dict:
         net = self.net
@@ -272,11 +341,11 @@ class CollectiveFederation:
         if not part.all():  # stragglers dropped: scale over the participants only
             idx = np.flatnonzero(part)
             ws = scaling.compute(self.cfg.scaling_factor, meta[idx, 0], meta[idx, 1], len(idx))
-            w = [0.0] * self.world
+            w = [0.0] * self.n_learners
             for i, x in zip(idx, ws):
                 w[int(i)] = float(x)
             return w
-        w = scaling.compute(self.cfg.scaling_factor, meta[:, 0], meta[:, 1], self.world)
+        w = scaling.compute(self.cfg.scaling_factor, meta[:, 0], meta[:, 1], self.n_learners)
         if self.engine is not None:
             we = self.engine.weights(meta[:, 0], meta[:, 1])
             if not np.allclose(we, w, rtol=1e-12, atol=0):
@@ -314,7 +383,9 @@ class CollectiveFederation:
 
     def _secure_aggregate(self, weights: list[float]) -> None:
         """model32 <- Dec(PWA(Enc(model32_r), w_r)): ciphertexts are what
-        crosses the process boundary; plaintext weights stay on their GPU."""
+        crosses the process boundary; plaintext weights stay on their GPU.
+        ``weights``: one per rank (co-located learners were pre-summed in
+        plaintext inside their own process: weight 1)."""
         st = self.net.state
         if self.he_dev is not None:
             with tracing.range("metisfl.secure_allreduce"):
@@ -347,6 +418,23 @@ class CollectiveFederation:
         weights = self.aggregation_weights(meta)
         st = self.net.state
         self.last_allreduce_ms = 0.0
+        if self.L > 1:
+            # hierarchical: this GPU's learners summed locally (K1), then the
+            # cross-GPU reduction carries one model per GPU
+            with tracing.range("metisfl.local_reduce"):
+                self.group.weighted_sum_into(st.model32, [weights[i] for i in self.local_learners()])
+            if self.cfg.secure_aggregation:
+                self._secure_aggregate([1.0] * self.world)
+            elif self.world > 1:
+                self._sync()
+                t1 = time.perf_counter()
+                with tracing.range("metisfl.all_reduce"):
+                    self.comm.all_reduce_(st.model32)
+                    self._sync()
+                self.last_allreduce_ms = (time.perf_counter() - t1) * 1e3
+            self._install_local(st.model32)
+            self._sync()
+            return weights, (time.perf_counter() - t0) * 1e3
         if self.cfg.secure_aggregation:
             self._secure_aggregate(weights)
         elif self.world > 1:
@@ -393,14 +481,21 @@ class CollectiveFederation:
         if not self.cfg.evaluate_community:
             return None, 0.0
         t0 = time.perf_counter()
-        ev = {"loss": float("nan"), "accuracy": float("nan")}
-        n = 0
-        if self.test_ds is not None:
+        nan = {"loss": float("nan"), "accuracy": float("nan")}
+        if self.group is not None:
             with tracing.range("metisfl.community_eval"):
-                ev = self.net.evaluate(self.test_ds, self.cfg.eval_max_steps)
-            n = self.test_ds.n
-        row = torch.tensor([ev["loss"], ev["accuracy"], float(n)], dtype=torch.float64, device=self.comm.device)
-        rows = self.comm.all_gather_rows(row).cpu().numpy()
+                evs = self.group.evaluate(max_steps=self.cfg.eval_max_steps)
+        else:
+            evs = [None]
+            if self.test_ds is not None:
+                with tracing.range("metisfl.community_eval"):
+                    evs = [self.net.evaluate(self.test_ds, self.cfg.eval_max_steps)]
+        vals = []
+        for ev, ds in zip(evs, self.test_dss):
+            ev = ev or nan
+            vals += [ev["loss"], ev["accuracy"], float(ds.n) if ds is not None and ev is not nan else 0.0]
+        row = torch.tensor(vals, dtype=torch.float64, device=self.comm.device)
+        rows = self.comm.all_gather_rows(row).cpu().numpy().reshape(-1, 3)
         out = [{"loss": float(r[0]), "accuracy": float(r[1]), "num_examples": int(r[2])} for r in rows]
         if all(o["num_examples"] == 0 for o in out):
             return None, (time.perf_counter() - t0) * 1e3
@@ -409,16 +504,19 @@ class CollectiveFederation:
     def run_round(self) -> RoundRecord:
         self.global_iteration += 1
         started = time.time()
-        n = self.num_local_updates[self.rank]
-        res = self.local_train(n)
-        test = res.get("test") or {}
-        row = torch.tensor([self.train_ds.n, res["completed_batches"], res["ms_per_batch"],
-                            res["ms_per_epoch"], res["train_loss"], res["train_accuracy"],
-                            res["completed_epochs"], self.global_iteration,
-                            test.get("loss", float("nan")), test.get("accuracy", float("nan")),
-                            1.0 if res["participated"] else 0.0],
-                           dtype=torch.float64, device=self.comm.device)
-        meta = self.comm.all_gather_rows(row).cpu().numpy()
+        results = self.local_train_all([self.num_local_updates[i] for i in self.local_learners()])
+        vals = []
+        for ds, res in zip(self.train_dss, results):
+            test = res.get("test") or {}
+            vals += [ds.n, res["completed_batches"], res["ms_per_batch"],
+                     res["ms_per_epoch"], res["train_loss"], res["train_accuracy"],
+                     res["completed_epochs"], self.global_iteration,
+                     test.get("loss", float("nan")), test.get("accuracy", float("nan")),
+                     1.0 if res["participated"] else 0.0]
+        row = torch.tensor(vals, dtype=torch.float64, device=self.comm.device)
+        meta = self.comm.all_gather_rows(row).cpu().numpy().reshape(self.n_learners, len(META_FIELDS))
+        res = dict(results[0])
+        res["ms"] = max(r["ms"] for r in results)
         completed = time.time()
         weights, agg_ms = self.aggregate(meta)
         agg_done = time.time()
@@ -466,7 +564,7 @@ class CollectiveFederation:
         vals = st.to_numpy()
         names = [s.name for s in st.specs]
         fm = model_pb2.FederatedModel()
-        fm.num_contributors = self.world
+        fm.num_contributors = self.n_learners
         fm.global_iteration = self.global_iteration
         fm.model.CopyFrom(model_from_arrays(names, [vals[n] for n in names], [s.trainable for s in st.specs]))
         return fm
@@ -481,12 +579,19 @@ class CollectiveFederation:
         os.makedirs(path, exist_ok=True)
         st = self.net.state
         self._sync()
-        per_rank = {"step": st.step.cpu(), "steps_done": torch.tensor(self.steps_done),
-                    "perm": self.train_ds.perm.cpu()}
-        for k in ("m", "v", "anchor"):
-            t = getattr(st, k)
-            if t is not None:
-                per_rank[k] = t.cpu()
+        # learner 0's entries unprefixed (the one-learner layout); co-located
+        # learner j >= 1 under "l<j>/"
+        per_rank = {"learners": torch.tensor(self.L)}
+        for j, (net, ds) in enumerate(zip(self.nets, self.train_dss)):
+            pre = "" if j == 0 else f"l{j}/"
+            lst = net.state
+            per_rank[pre + "step"] = lst.step.cpu()
+            per_rank[pre + "steps_done"] = torch.tensor(self.steps_done_l[j])
+            per_rank[pre + "perm"] = ds.perm.cpu()
+            for k in ("m", "v", "anchor"):
+                t = getattr(lst, k)
+                if t is not None:
+                    per_rank[pre + k] = t.cpu()
         torch.save(per_rank, os.path.join(path, f"rank{self.rank}.pt"))
         if self.rank == 0:
             with open(os.path.join(path, self.COMMUNITY_FILE), "wb") as f:
@@ -494,7 +599,7 @@ class CollectiveFederation:
             with open(os.path.join(path, "federation.json"), "w") as f:
                 json.dump({"global_iteration": self.global_iteration,
                            "num_local_updates": self.num_local_updates,
-                           "world": self.world, "learner_ids": self.learner_ids,
+                           "world": self.world, "learners_per_rank": self.L, "learner_ids": self.learner_ids,
                            "dataset_sizes": self.dataset_sizes,
                            "config": {k: v for k, v in asdict(self.cfg).items() if k != "extra"},
                            "variables": [[s.name, list(s.shape), s.trainable] for s in st.specs],
@@ -505,6 +610,8 @@ class CollectiveFederation:
         """Install a ``FederatedModel`` (proto or serialized bytes) as the
         community model, matching variables by name."""
         install_community_model(self.net, fm)
+        if self.group is not None:
+            self._install_local(self.net.state.model32)
 
     def resume(self, path: str, prev_rank: int | None = None) -> None:
         """Reload a checkpoint written by ``save_checkpoint``.  The world size
@@ -532,25 +639,30 @@ class CollectiveFederation:
                 raise RuntimeError(f"old-format checkpoint {legacy}: {flat.numel()} values, model has "
                                    f"{st.model32.numel()}")
             st.model32.copy_(flat.to(st.model32.device, st.model32.dtype).view_as(st.model32))
-            st.refresh_bf16()
-            st.set_anchor()
+            self._install_local(st.model32)
         else:
             raise FileNotFoundError(f"no community model in checkpoint {path} ({self.COMMUNITY_FILE})")
-        st = self.net.state
-        dev = st.model32.device
-        same_world = meta["world"] == self.world
+        same_world = meta["world"] == self.world and int(meta.get("learners_per_rank", 1)) == self.L
         old_rank = self.rank if prev_rank is None else int(prev_rank)
         rank_file = os.path.join(path, f"rank{old_rank}.pt")
         if os.path.exists(rank_file) and 0 <= old_rank < meta["world"]:
             per_rank = torch.load(rank_file, weights_only=True)
-            st.step.copy_(per_rank["step"].to(dev))
-            for k in ("m", "v"):
-                if k in per_rank and getattr(st, k) is not None and per_rank[k].numel() == getattr(st, k).numel():
-                    getattr(st, k).copy_(per_rank[k].to(dev))
-            if same_world and old_rank == self.rank and per_rank["perm"].numel() == self.train_ds.perm.numel():
-                self.train_ds.perm.copy_(per_rank["perm"].to(self.train_ds.perm.device))
-                self.steps_done = int(per_rank["steps_done"])
-        st.set_anchor()  # FedProx anchors at the restored community model
+            for j, (net, ds) in enumerate(zip(self.nets, self.train_dss)):
+                pre = "" if j == 0 else f"l{j}/"
+                if pre + "step" not in per_rank:
+                    continue  # more co-located learners now than in the checkpoint
+                st = net.state
+                dev = st.model32.device
+                st.step.copy_(per_rank[pre + "step"].to(dev))
+                for k in ("m", "v"):
+                    t = per_rank.get(pre + k)
+                    if t is not None and getattr(st, k) is not None and t.numel() == getattr(st, k).numel():
+                        getattr(st, k).copy_(t.to(dev))
+                if same_world and old_rank == self.rank and per_rank[pre + "perm"].numel() == ds.perm.numel():
+                    ds.perm.copy_(per_rank[pre + "perm"].to(ds.perm.device))
+                    self.steps_done_l[j] = int(per_rank[pre + "steps_done"])
+        for net in self.nets:
+            net.state.set_anchor()  # FedProx anchors at the restored community model
         self.global_iteration = int(meta["global_iteration"])
         if same_world:
             self.num_local_updates = list(meta["num_local_updates"])

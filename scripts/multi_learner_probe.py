@@ -1,0 +1,66 @@
+"""Throughput of G co-resident ResNet-18 learners on one GPU: each learner
+keeps its own model, workspace and captured K-update graph; the graphs are
+replayed on G streams (concurrent HIP queues) instead of back to back.
+
+python scripts/multi_learner_probe.py --groups 1 2 4 8 --updates 256
+"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+for _i, _a in enumerate(sys.argv):  # before HIP initialises
+    if _a == "--hw-queues":
+        os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[_i + 1]
+
+import torch  # noqa: E402
+
+from metisfl_amd.models.resnet import ResNet18  # noqa: E402
+from metisfl_amd.ops.optim import OptimizerSpec  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--groups", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--updates", type=int, default=256, help="per learner")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--serial", action="store_true", help="one stream (baseline)")
+    ap.add_argument("--hw-queues", type=int, default=0)
+    a = ap.parse_args()
+    gmax = max(a.groups)
+    nets, dss = [], []
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    for i in range(gmax):
+        net = ResNet18(batch_size=a.batch, device="cuda", seed=7 + i,
+                       optimizer=OptimizerSpec("momentum_sgd", 0.005, momentum=0.75))
+        x = torch.randn((1024, 32, 32, 3), generator=gen, device="cuda")
+        y = torch.randint(0, 10, (1024,), generator=gen, device="cuda")
+        nets.append(net)
+        dss.append(net.make_dataset(x, y, seed=i))
+    for net, ds in zip(nets, dss):  # capture (1-step and K-step graphs)
+        net.train_steps(ds, 16)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(gmax)]
+    K = nets[0].graph_steps
+    for G in a.groups:
+        for mode in (["serial"] if a.serial else []) + ["streams"]:
+            reps = a.updates // K
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for r in range(reps):
+                for g in range(G):
+                    if mode == "streams":
+                        with torch.cuda.stream(streams[g]):
+                            nets[g]._train_graph_k.replay()
+                    else:
+                        nets[g]._train_graph_k.replay()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            upd = reps * K * G
+            print(f"G={G} {mode}: {dt * 1e3 / (reps * K):.3f} ms per {G}-learner step, "
+                  f"{dt * 1e3 / upd:.4f} ms per update, {upd * a.batch / dt:.0f} samples/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

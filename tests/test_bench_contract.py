@@ -48,6 +48,7 @@ def test_bench_single_process_json_contract():
     assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
     assert d["n_gpus"] == 1 and d["steps"] == 1 and d["value"] > 0 and d["higher_is_better"] is True
     assert d["config"]["model"] == "resnet18-cifar"
+    assert d["config"]["learners"] == 8 and d["config"]["learners_per_gpu"] == 8
     assert d["community_eval_ms_mean"] > 0
     ex = d["conv_products_exact"]  # the strict-IEEE alternative is timed in the same run
     assert ex["updates_timed"] == 2 and ex["ms_per_update"] > 0 and ex["round_ms_est"] > 0
@@ -60,8 +61,12 @@ def test_bench_two_ranks_one_json_line():
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)  # rank 0 only
-    assert d["n_gpus"] == 2 and d["config"]["learners"] == 2
+    # the federation is always the BASELINE's 8 learners: 4 co-located per GPU here
+    assert d["n_gpus"] == 2 and d["config"]["learners"] == 8 and d["config"]["learners_per_gpu"] == 4
     assert d["config"]["parallelism"] == "fedavg-dp2"
+    w = d["aggregation_weights"]
+    assert len(w) == 8 and abs(sum(w) - 1.0) < 1e-9
+    assert d["community_model"]["identical"]
 
 
 def test_async_bench_json_contract():
@@ -103,7 +108,7 @@ def test_bench_spawns_its_own_ranks():
                         "--width-mult", "0.125"], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
-    assert d["n_gpus"] == 2 and d["config"]["learners"] == 2
+    assert d["n_gpus"] == 2 and d["config"]["learners"] == 8
     assert d["collective"]["world_size"] == 2 and d["collective"]["backend"] == "gloo"
     assert d["dtype"] == "fp32"
 

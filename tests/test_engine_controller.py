@@ -330,6 +330,27 @@ def test_duplicate_completion_is_ignored():
     assert sorted(resp.metadata[0].completed_by_learner_id) == sorted(l for l, _ in ls)
 
 
+def test_rejoin_in_the_same_round_is_not_a_duplicate():
+    """a learner completes round 1, leaves, rejoins under the same
+    host:port before round 1 closes and is handed round 1 again; its real
+    completion must count at the barrier, not be dropped as a retry."""
+    c = E.Controller(params())
+    ls = _three_learners(c)
+    (a, ta), (b, tb), (z, tz) = ls
+    assert c.learner_completed_task(a, ta, completed([1, 1, 1], 1))["run_tasks"] == []
+    c.remove_learner(a, ta)
+    a2, ta2, d = join(c, 1, 100)  # same host:port -> same id, new token
+    assert a2 == a and [w for w, _ in d["run_tasks"]] == [a]
+    assert run_req(d["run_tasks"][0][1]).task.global_iteration == 1
+    assert c.learner_completed_task(a2, ta2, completed([1, 1, 1], 1))["run_tasks"] == []
+    assert c.learner_completed_task(b, tb, completed([2, 2, 2], 1))["run_tasks"] == []
+    d = c.learner_completed_task(z, tz, completed([4, 4, 4], 1))
+    assert sorted(w for w, _ in d["run_tasks"]) == sorted([a, b, z])  # the barrier closed with the rejoiner
+    # and a retry of the rejoined learner's completion is still a duplicate
+    assert c.learner_completed_task(a2, ta2, completed([1, 1, 1], 1))["run_tasks"] == []
+    assert c.global_iteration() == 2
+
+
 def test_completion_retries_only_on_transient_codes():
     import grpc
 

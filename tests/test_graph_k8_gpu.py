@@ -1,0 +1,100 @@
+"""The bench's hot path pinned against eager execution: the full-width fp32
+ResNet-18 at batch 32 (the BASELINE config) with its 8-update captured
+hipGraph (models/net.py ``graph_steps``, MFL_GRAPH_STEPS) against 8 eager
+``_train_body`` calls, and co-located learners (one HIP stream each,
+models/colocated.py) against the same learners run one after another.
+
+lr = 0 keeps the weights fixed, so nothing is amplified chaotically: every
+update sees the same model, and the comparisons are per-update loss /
+accuracy sums, the last update's gradient buffer and the BatchNorm running
+statistics (which integrate all 8 updates).  A second replay of the same
+graph must agree again: the halo convs' split-K arrival tickets and the BN
+accumulators must re-arm across replays."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B = 32
+
+
+def _net(seed=7, lr=0.0, conv_products=None):
+    from metisfl_amd.models.resnet import ResNet18
+    from metisfl_amd.ops.optim import OptimizerSpec
+    return ResNet18(batch_size=B, device="cuda", optimizer=OptimizerSpec("momentum_sgd", lr, momentum=0.75),
+                    seed=seed, conv_products=conv_products)
+
+
+def _data(n=512, seed=0):
+    rng = np.random.default_rng(seed)
+    return rng.standard_normal((n, 32, 32, 3)).astype(np.float32), rng.integers(0, 10, n)
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / max(1e-30, float(b.abs().max())))
+
+
+def _frozen(net):
+    st = net.state
+    return torch.cat([st.view(s.name).reshape(-1) for s in st.specs if not s.trainable])
+
+
+def test_k8_graph_replay_matches_eager_full_width():
+    x, y = _data()
+    g = _net()
+    e = _net()
+    assert g.graph_steps == 8, "the bench's graph length"
+    g.zero_grad_in_optimizer = e.zero_grad_in_optimizer = False  # the last update's gradient stays readable
+    dg = g.make_dataset(x, y, seed=1)
+    de = e.make_dataset(x, y, seed=1)
+    assert torch.equal(dg.perm, de.perm)
+    g.prepare_graphs(dg, 16)
+    assert g._train_graph_k is not None
+    for rep in range(2):
+        g.reset_train_stats()
+        e.reset_train_stats()
+        g._train_graph_k.replay()
+        for _ in range(8):
+            e._train_body(de)
+        torch.cuda.synchronize()
+        assert int(g.state.step.cpu()) == int(e.state.step.cpu()) == 8 * (rep + 1)
+        sg, se = g.stats.cpu(), e.stats.cpu()
+        assert float(sg[2]) == float(se[2]) == 8 * B
+        assert abs(float(sg[0]) - float(se[0])) <= 1e-5 * abs(float(se[0])), (rep, sg, se)  # loss sum
+        assert abs(float(sg[1]) - float(se[1])) <= 1.0  # correct predictions (a near-tie may flip)
+        rg = _rel(g.state.grad32, e.state.grad32)
+        rb = _rel(_frozen(g), _frozen(e))
+        print(f"replay {rep}: loss {float(sg[0]) / (8 * B):.5f}, grad rel {rg:.2e}, BN running stats rel {rb:.2e}")
+        assert rg <= 1e-5, rg
+        assert rb <= 1e-5, rb
+        assert torch.equal(g.state.model32[: g.state.n_params], e.state.model32[: e.state.n_params])  # lr 0
+
+
+def test_colocated_streams_match_sequential_learners():
+    """4 learners replaying their graphs concurrently on 4 streams compute
+    what the same 4 learners compute one after another (no shared scratch,
+    no cross-stream race): lr 0 (BN running statistics, loss sums) and 16
+    updates at the bench's learning rate (weights)."""
+    from metisfl_amd.models.colocated import CoLocatedLearners
+    for lr, tol in ((0.0, 1e-5), (0.005, 1e-3)):
+        seq, co = [], []
+        for grp in (seq, co):
+            for j in range(4):
+                net = _net(seed=11 + j, lr=lr)
+                x, y = _data(256, 20 + j)
+                grp.append((net, net.make_dataset(x, y, seed=j)))
+        for net, ds in seq:
+            net.train_steps(ds, 16)
+        group = CoLocatedLearners([n for n, _ in co], [d for _, d in co])
+        ms = group.train([16] * 4, [0] * 4)
+        torch.cuda.synchronize()
+        assert len(ms) == 4 and all(m > 0 for m in ms)
+        for (a, _), (b, _) in zip(seq, co):
+            assert int(a.state.step.cpu()) == int(b.state.step.cpu()) == 16
+            r = _rel(b.state.model32, a.state.model32)
+            ls = abs(b.train_stats()["loss"] - a.train_stats()["loss"])
+            print(f"lr {lr}: model rel {r:.2e}, loss diff {ls:.2e}")
+            assert r <= tol, (lr, r)
+            assert ls <= 1e-3 * (1 + lr * 1000), ls
