@@ -82,6 +82,10 @@ def main() -> int:
                     help="fp32 bf16x3 runs: also time this many local updates with exact fp32 products "
                          "(0: skip); reported as conv_products_exact")
     ap.add_argument("--width-mult", type=float, default=1.0, help=argparse.SUPPRESS)  # CPU plumbing tests only
+    ap.add_argument("--checkpoint-every", type=int, default=0,
+                    help="also checkpoint the federation every K rounds inside the timed rounds (device-staged, "
+                         "written in the background: parallel/checkpoint.py); reports checkpoint_ms")
+    ap.add_argument("--checkpoint-dir", type=str, default="")
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
 
@@ -142,8 +146,19 @@ def main() -> int:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    ckpt_dir = None
+    if args.checkpoint_every > 0:
+        import tempfile
+        ckpt_dir = args.checkpoint_dir or tempfile.mkdtemp(prefix="metisfl_bench_ckpt_")
+
+    def maybe_checkpoint():
+        r = fed.history[-1]
+        if ckpt_dir and r.global_iteration % args.checkpoint_every == 0:
+            r.checkpoint_ms = fed.save_checkpoint(ckpt_dir, block=False)
+
     for _ in range(args.warmup):
         fed.run_round()
+        maybe_checkpoint()
         if comm.rank == 0:
             r = fed.history[-1]
             print(f"[bench] warmup round {r.global_iteration}: {r.round_ms:.1f} ms "
@@ -153,6 +168,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         fed.run_round()
+        maybe_checkpoint()
         if comm.rank == 0:
             r = fed.history[-1]
             print(f"[bench] round {r.global_iteration}: {r.round_ms:.1f} ms "
@@ -161,6 +177,7 @@ def main() -> int:
     comm.barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    fed.flush_checkpoints()  # background writes finish outside the timed region
     elapsed = comm.all_max(elapsed)
     timed = fed.history[-args.steps:] if args.steps else []
     round_ms = elapsed * 1e3 / max(1, args.steps)
@@ -223,6 +240,13 @@ def main() -> int:
         "samples_per_s": (args.train_size * args.local_epochs) / (round_ms / 1e3) if round_ms else 0.0,
     }
     out["community_eval_ms_mean"] = sum(r.community_eval_ms for r in timed) / max(1, len(timed))
+    out["lineage_snapshot_ms_mean"] = sum(r.snapshot_ms for r in timed) / max(1, len(timed))
+    if ckpt_dir:
+        ck = [r.checkpoint_ms for r in timed if r.global_iteration % args.checkpoint_every == 0]
+        out["checkpoint"] = {"every": args.checkpoint_every, "count": len(ck),
+                             "critical_path_ms_mean": sum(ck) / max(1, len(ck)),
+                             "background_write_ms_last": fed._ckpt.last_write_ms if fed._ckpt else None,
+                             "dir": ckpt_dir}
     out["aggregation_weights"] = [float(w) for w in timed[-1].weights] if timed and timed[-1].weights is not None else None
     out["community_model"] = _community_digests(comm, net)
     if args.dtype == "fp32" and net.conv_products == "bf16x3" and args.exact_updates > 0:

@@ -28,29 +28,37 @@ from metisfl_amd.utils.proto_messages_factory import MetisProtoMessages as M
 
 SERVICE = "metisfl_amd.CollectiveService"
 METHODS = ("RegisterLearners", "ScalingFactors", "RecordRound", "RecordAsyncUpdate", "RecordEvaluation",
-           "RequestStop", "ShouldStop")
+           "RequestStop", "ShouldStop", "RequestRegroup")
 
 
 def add_collective_service(servicer, server: grpc.Server) -> None:
     eng = servicer.engine
-
-    registered: list[str] = []  # the current collective membership
+    # stop: leave after the current round; regroup: checkpoint after the
+    # current round and exit for a relaunch on a new membership (learners
+    # joining a running collective federation, driver_session.py)
+    state = {"stop": False, "regroup": False}
 
     def register(req: bytes, ctx) -> bytes:
-        """(Re-)register the collective ranks.  A relaunch after a lost rank
-        (driver_session.py) registers the surviving membership: learners of
-        the previous membership that are not in it leave the federation (the
-        reference's LeaveFederation, controller.cc:171-199), the survivors
-        re-join with fresh tokens."""
+        """(Re-)register the collective ranks.  A relaunch (after a lost rank,
+        or to admit joining learners: driver_session.py) registers the new
+        membership: the collective learners of the previous one that are not
+        in it leave the federation (the reference's LeaveFederation,
+        controller.cc:171-199), the others re-join with fresh specs and
+        tokens.  The previous membership is the engine's own (collective
+        learners have no gRPC server, port < 1024 or the "collective-rank"
+        host), so it survives a controller restart from its checkpoint; the
+        removals are membership changes, not failure-detector evictions."""
         d = json.loads(req)
         want = {f"{l.get('hostname', 'localhost')}:{int(l.get('port', 0))}" for l in d["learners"]}
-        current = set(eng.learner_ids())
-        for lid in list(registered):
-            if lid in current:  # leaving, or re-joining with fresh specs / token
-                eng.evict_learner(lid)
+        prev = set(servicer.collective_members) | want
+        for lid in eng.learner_ids():
+            if lid in prev:  # leaving, or re-joining with fresh specs / token
+                eng.evict_learner(lid, False)
                 if lid not in want:
                     MetisLogger.info("Collective learner %s left the federation.", lid)
+        registered = servicer.collective_members
         registered.clear()
+        state["regroup"] = False  # a requested membership change is now in effect
         ids, toks = [], []
         for l in d["learners"]:
             se = M.construct_server_entity_pb(l.get("hostname", "localhost"), int(l.get("port", 0)))
@@ -68,7 +76,6 @@ def add_collective_service(servicer, server: grpc.Server) -> None:
         f = eng.scaling_factors(d["ids"], [float(x) for x in d["num_train"]], [float(x) for x in d["batches"]])
         return json.dumps({"factors": [float(f[i]) for i in d["ids"]]}).encode()
 
-    state = {"stop": False}
 
     def record(req: bytes, ctx) -> bytes:
         d = json.loads(req)
@@ -80,7 +87,7 @@ def add_collective_service(servicer, server: grpc.Server) -> None:
             eng.record_community_evaluation(int(d["global_iteration"]), d["eval_ids"],
                                             [base64.b64decode(e) for e in d["evaluations"]])
         servicer.checkpoint()
-        return json.dumps({"stop": state["stop"]}).encode()
+        return json.dumps({"stop": state["stop"], "regroup": state["regroup"]}).encode()
 
     def record_async(req: bytes, ctx) -> bytes:
         """One FedRec update of an asynchronous collective federation: the
@@ -107,9 +114,14 @@ def add_collective_service(servicer, server: grpc.Server) -> None:
     def should_stop(req: bytes, ctx) -> bytes:
         return json.dumps({"stop": state["stop"]}).encode()
 
+    def request_regroup(req: bytes, ctx) -> bytes:
+        state["regroup"] = True
+        MetisLogger.info("Collective federation: membership change requested (regroup after this round).")
+        return b"{}"
+
     fns = {"RegisterLearners": register, "ScalingFactors": scaling, "RecordRound": record,
            "RecordAsyncUpdate": record_async, "RecordEvaluation": record_eval, "RequestStop": request_stop,
-           "ShouldStop": should_stop}
+           "ShouldStop": should_stop, "RequestRegroup": request_regroup}
     handlers = {name: grpc.unary_unary_rpc_method_handler(fn) for name, fn in fns.items()}
     server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(SERVICE, handlers),))
 

@@ -183,6 +183,9 @@ class ControllerServicer(controller_pb2_grpc.ControllerServiceServicer):
         # change and every completed round; a controller started on an
         # existing checkpoint restores it and re-dispatches the round
         self.checkpoint_dir = checkpoint_dir
+        # the learner ids of the on-node collective federation currently
+        # registered through the collective service (collective_service.py)
+        self.collective_members: list[str] = []
         self._ckpt_lock = threading.Lock()
         self._ckpt_gi = -1
         self.resumed = False

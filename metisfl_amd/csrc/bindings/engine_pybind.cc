@@ -158,15 +158,17 @@ PYBIND11_MODULE(_engine, m) {
              }
              return dispatch_to_py(d);
            })
-      .def("evict_learner",
-           [](Controller& c, const std::string& id) {
-             Dispatch d;
-             {
-               py::gil_scoped_release nogil;
-               d = c.evict_learner(id);
-             }
-             return dispatch_to_py(d);
-           })
+      .def(
+          "evict_learner",
+          [](Controller& c, const std::string& id, bool count) {
+            Dispatch d;
+            {
+              py::gil_scoped_release nogil;
+              d = c.evict_learner(id, count);
+            }
+            return dispatch_to_py(d);
+          },
+          py::arg("id"), py::arg("count") = true)
       .def("checkpoint",
            [](const Controller& c) {
              std::string s;

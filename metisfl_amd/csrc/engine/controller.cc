@@ -352,7 +352,7 @@ Dispatch Controller::schedule_tasks_locked(const std::string& id, uint32_t task_
 // Removing a learner that a synchronous barrier was waiting for may complete
 // the barrier with the remaining learners -- the reference stalls forever in
 // that case; here the round is aggregated right away.
-Dispatch Controller::evict_learner(const std::string& id) {
+Dispatch Controller::evict_learner(const std::string& id, bool count) {
   std::lock_guard<std::mutex> g(mu_);
   if (!learners_.count(id)) throw StatusError(NOT_FOUND, "learner " + id + " not found");
   store_->erase({id});
@@ -360,7 +360,7 @@ Dispatch Controller::evict_learner(const std::string& id) {
   learners_.erase(id);
   templates_.erase(id);
   completed_iter_.erase(id);
-  ++evicted_;
+  if (count) ++evicted_;
   const auto active = active_ids_locked();
   auto ready = scheduler_->poll(active);
   if (ready.empty()) return Dispatch{};

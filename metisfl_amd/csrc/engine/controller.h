@@ -125,7 +125,10 @@ class Controller {
   Dispatch remove_learner(const std::string& id, const std::string& token);
   // failure detector: drop an unresponsive learner; may complete a pending
   // synchronous barrier (returns that round's dispatch)
-  Dispatch evict_learner(const std::string& id);
+  // count = false: a membership change the controller itself makes (a
+  // collective relaunch re-registering its ranks), not a failure-detector
+  // eviction, so evicted() does not move
+  Dispatch evict_learner(const std::string& id, bool count = true);
   uint32_t evicted() const { return evicted_; }
   std::vector<std::string> learner_ids() const;
 

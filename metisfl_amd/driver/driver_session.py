@@ -75,12 +75,15 @@ class DriverSessionBase:
         os.makedirs(working_dir)
         self.device = device
         self.seed = seed
-        # collective data plane knobs: checkpoint_every (rounds, default 1),
-        # max_recoveries (lost-rank relaunches, default 2), heartbeat_timeout_s,
-        # fault ({"rank", "round"}: fault injection for tests), extra
+        # collective data plane knobs: checkpoint_every (rounds, default 5;
+        # written in the background), max_recoveries (lost-rank relaunches,
+        # default 2), heartbeat_timeout_s, fault ({"rank", "round"[, "signal":
+        # "KILL"]}: fault injection for tests), extra
         # (FederationConfig.extra: test hooks such as uneven learner delays)
         self.collective_options = dict(collective_options or {})
         self.recoveries: list[dict] = []
+        self.regroups: list[dict] = []      # learners admitted into a running collective federation
+        self._pending_joins: list = []
         self.fake_train_delay = fake_train_delay  # echo learners only
         self._model_dir = os.path.join(working_dir, "model_definition")
         self.neural_engine = self._save_model(model)
@@ -304,7 +307,9 @@ class DriverSessionBase:
                "termination": {"cutoff_mins": ts.execution_time_cutoff_mins, "metric": env.evaluation_metric,
                                "metric_cutoff": ts.metric_cutoff_score},
                "checkpoint_dir": os.path.join(self.working_dir, "collective_checkpoint"),
-               "checkpoint_every": int(o.get("checkpoint_every", 1)),
+               # staged on the device and written in the background (parallel/
+               # checkpoint.py); every 5 rounds by default, plus the last one
+               "checkpoint_every": int(o.get("checkpoint_every", 5)),
                "heartbeat_timeout_s": float(o.get("heartbeat_timeout_s", 20.0)),
                "resume_dir": resume_dir, "fault": fault,
                "backend": "gloo" if self.device == "cpu" else None,
@@ -338,26 +343,48 @@ class DriverSessionBase:
             extra = {"RANK": str(rank), "WORLD_SIZE": str(len(learners)), "MASTER_ADDR": "127.0.0.1",
                      "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0",
                      "LOCAL_RANK": str(l.devices[0] if l.devices else rank)}
+            extra["METISFL_WATCHDOG_REPORT_DIR"] = self._watchdog_dir(tag)
             if self.device == "cpu":
                 extra.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
             self._spawn(f"learner_{l.learner_id}", [sys.executable, "-m", "metisfl_amd.learner.collective", job],
                         extra)
+        self._collective_tag = tag
 
-    # a rank that lost a peer exits with this code (parallel/watchdog.py); the
-    # driver's own terminate gives -15 / -9
-    _PEER_EXIT = (75, -15, -9)
+    def _watchdog_dir(self, tag: str) -> str:
+        return os.path.join(self.working_dir, f"watchdog{tag}")
+
+    # a rank that lost a peer exits with this code (parallel/watchdog.py)
+    _PEER_EXIT = 75
 
     def _recover_collective(self, failed_name: str, code: int) -> None:
         """A collective rank died: stop the survivors (blocked in a collective,
         or already out on their watchdog), and relaunch them as fresh
         processes on the smaller world from the last FederatedModel checkpoint
         (the reference's learners may leave at any time,
-        controller.cc:171-199)."""
+        controller.cc:171-199).
+
+        Which ranks failed is decided from the exit codes seen BEFORE the
+        driver signals anyone: a rank that had already exited with anything
+        but 0 or the watchdog's peer-loss code (including -9 / -15 from a
+        signal the driver did not send, e.g. the OOM killer) is a failure;
+        ranks the driver terminates here are survivors."""
         members = list(self._collective_members)
         names = {f"learner_{l.learner_id}": l for l in members}
+        before = {n: self._procs[n].poll() for n in names if n in self._procs}
+        before[failed_name] = code
+        # give ranks that are on their way out (watchdog exit) a moment, so a
+        # peer-loss exit is not mistaken for a rank the driver had to stop
+        end = time.time() + float(self.collective_options.get("recovery_grace_s", 3.0))
+        while time.time() < end and any(self._procs[n].poll() is None for n in before if before[n] is None):
+            time.sleep(0.05)
+        for n in before:
+            if before[n] is None:
+                before[n] = self._procs[n].poll()
+        signalled = set()
         for name, p in self._procs.items():
             if name in names and p.poll() is None:
                 p.terminate()
+                signalled.add(name)
         for name, p in self._procs.items():
             if name in names:
                 try:
@@ -365,21 +392,33 @@ class DriverSessionBase:
                 except subprocess.TimeoutExpired:
                     p.kill()
                     p.wait(10)
-        failed = {n for n in names if self._procs[n].returncode not in (0,) + self._PEER_EXIT}
-        if not failed and code not in self._PEER_EXIT:
-            failed.add(failed_name)
+        failed = {n for n, rc in before.items() if n not in signalled and rc not in (None, 0, self._PEER_EXIT)}
+        # a hung rank does not exit: the survivors' watchdogs name it
+        order = [f"learner_{l.learner_id}" for l in members]
+        wdir = self._watchdog_dir(getattr(self, "_collective_tag", ""))
+        if os.path.isdir(wdir):
+            for fn in os.listdir(wdir):
+                try:
+                    with open(os.path.join(wdir, fn)) as f:
+                        peer = int(json.load(f)["peer"])
+                except (OSError, ValueError, KeyError):
+                    continue
+                if 0 <= peer < len(order) and order[peer] in signalled:
+                    failed.add(order[peer])
         if not failed:
             raise RuntimeError(f"collective learners left on a lost peer, but the failed rank is unknown "
                                f"({failed_name} exited with {code})")
         survivors = [l for l in members if f"learner_{l.learner_id}" not in failed]
         if not survivors:
             raise RuntimeError(f"every collective learner failed ({failed_name} exited with {code})")
+        from metisfl_amd.parallel import checkpoint as ck
         ckpt = os.path.join(self.working_dir, "collective_checkpoint")
-        resume = ckpt if os.path.exists(os.path.join(ckpt, "federation.json")) else None
+        found = ck.resolve(ckpt)
+        resume = ckpt if found else None
         prev = [members.index(l) for l in survivors]
         gi = None
-        if resume:
-            with open(os.path.join(ckpt, "federation.json")) as f:
+        if found:
+            with open(os.path.join(found, "federation.json")) as f:
                 gi = json.load(f)["global_iteration"]
         self.recoveries.append({"failed": sorted(failed), "exit_code": code, "survivors": len(survivors),
                                 "resumed_from_round": gi, "at": time.time()})
@@ -392,6 +431,73 @@ class DriverSessionBase:
             self._procs.pop(n, None)
         self._init_collective_learners(self.federation_environment.termination_signals.federation_rounds,
                                        survivors, resume, prev, None, tag=f"_r{len(self.recoveries)}")
+
+    # -- learners joining a running collective federation ---------------------------------------------
+    EXIT_REGROUP = 76  # learner/collective.py: checkpointed for a relaunch on a new membership
+
+    def join_collective_learner(self, learner) -> None:
+        """Admit a learner into a RUNNING collective (DataPlane: rccl)
+        federation -- the reference's JoinFederation / AddLearner, which
+        registers the joiner and schedules it right away
+        (controller.cc:98-168).  The collective ranks finish their current
+        round, write a complete checkpoint and exit (EXIT_REGROUP);
+        ``monitor_federation`` relaunches the larger membership from it as
+        fresh processes: the newcomer starts from the community model with a
+        fresh optimizer state, the step budgets and FedAvg weights are
+        recomputed over the new shards, and the round count continues.
+        ``learner``: a ``fedenv_parser.Learner`` or its YAML mapping."""
+        from metisfl_amd.controller import collective_service as cs
+        from metisfl_amd.utils.fedenv_parser import Learner
+        from metisfl_amd.utils.grpc_services import make_channel
+        if not self.collective:
+            raise RuntimeError("join_collective_learner needs DataPlane: rccl (gRPC learners join by themselves)")
+        if isinstance(learner, dict):
+            learner = Learner(learner)
+        self.federation_environment.learners.learners.append(learner)
+        self._pending_joins.append(learner)
+        ch = make_channel(self._controller_entity)
+        try:
+            cs.call(ch, "RequestRegroup", {}, timeout=30)
+        finally:
+            ch.close()
+        MetisLogger.info("learner %s joins the collective federation at the next round boundary",
+                         learner.learner_id)
+
+    def _regroup_ready(self, timeout_s: float = 120.0) -> bool:
+        """True when every collective rank left with EXIT_REGROUP (waits for
+        the stragglers of a regroup that has started); False otherwise."""
+        procs = {n: p for n, p in self._procs.items() if n.startswith("learner_")}
+        if not any(p.poll() == self.EXIT_REGROUP for p in procs.values()):
+            return False
+        end = time.time() + timeout_s
+        while time.time() < end and any(p.poll() is None for p in procs.values()):
+            time.sleep(0.05)
+        return all(p.poll() == self.EXIT_REGROUP for p in procs.values())
+
+    def _regroup_collective(self) -> None:
+        from metisfl_amd.parallel import checkpoint as ck
+        old = list(self._collective_members)
+        joins, self._pending_joins = list(self._pending_joins), []
+        members = old + joins
+        ckpt = os.path.join(self.working_dir, "collective_checkpoint")
+        found = ck.resolve(ckpt)
+        if found is None:
+            raise RuntimeError("collective regroup: the ranks left no checkpoint")
+        with open(os.path.join(found, "federation.json")) as f:
+            gi = json.load(f)["global_iteration"]
+        self.regroups.append({"joined": [l.learner_id for l in joins], "world": len(members),
+                              "at_round": gi, "at": time.time()})
+        MetisLogger.info("collective federation regroups at round %d: %d -> %d learners", gi, len(old), len(members))
+        for l in old:
+            n = f"learner_{l.learner_id}"
+            log = os.path.join(self.working_dir, f"{n}.log")
+            if os.path.exists(log):
+                os.replace(log, log + f".group{len(self.regroups)}")
+            self._procs.pop(n, None)
+        # old members keep their learner-local state (old rank = index); joiners start fresh (-1)
+        self._init_collective_learners(self.federation_environment.termination_signals.federation_rounds,
+                                       members, ckpt, list(range(len(old))) + [-1] * len(joins), None,
+                                       tag=f"_g{len(self.regroups)}")
 
     # -- public API -----------------------------------------------------------------------------------
     def initialize_federation(self):
@@ -432,6 +538,9 @@ class DriverSessionBase:
         st = time.time()
         while True:
             time.sleep(request_every_secs)
+            if self.collective and self._regroup_ready():
+                self._regroup_collective()
+                continue
             for name, p in list(self._procs.items()):
                 if p.poll() is not None and p.returncode != 0:
                     if (self.collective and name.startswith("learner_")

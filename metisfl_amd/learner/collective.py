@@ -23,7 +23,8 @@ rank 0 decides and the decision is broadcast, so every rank leaves after the
 same round.
 
 Failure handling: a ``FederatedModel`` checkpoint is written
-every ``checkpoint_every`` rounds, a RankWatchdog exits the survivors of a
+every ``checkpoint_every`` rounds (staged on the device, written by a
+background thread: parallel/checkpoint.py), a RankWatchdog exits the survivors of a
 lost rank (exit code 75), and the driver relaunches them as FRESH processes
 with ``resume_dir`` and the new world size.  ``fault`` ({"rank", "round"})
 kills a rank at the start of a round (fault injection for tests).
@@ -38,6 +39,9 @@ import sys
 import time
 
 EXIT_INJECTED_FAULT = 17
+# every rank exits with this after a blocking checkpoint when the driver asked
+# for a new membership (a learner joins the running federation)
+EXIT_REGROUP = 76
 
 
 def _load_recipe(path):
@@ -48,12 +52,28 @@ def _load_recipe(path):
         return cloudpickle.load(f)
 
 
-def _stop_decision(comm, rank0_stop: bool) -> bool:
-    """Rank 0's stop decision, identical on every rank."""
+def _inject_fault(rank: int, at: int, fault: dict) -> None:
+    """Fault injection (tests): leave now, with exit code EXIT_INJECTED_FAULT
+    or -- ``"signal": "KILL"`` -- by SIGKILL, as the kernel's OOM killer
+    would (exit -9)."""
+    import signal
+    how = str(fault.get("signal", "")).upper()
+    print(f"[collective] fault injection: rank {rank} {'is SIGKILLed' if how == 'KILL' else 'exits'} at "
+          f"{at}", flush=True)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    if how == "KILL":
+        os.kill(os.getpid(), signal.SIGKILL)
+    os._exit(EXIT_INJECTED_FAULT)
+
+
+def _decision(comm, rank0_action: int) -> int:
+    """Rank 0's decision after a round (0 continue, 1 stop, 2 regroup),
+    identical on every rank."""
     import torch
-    t = torch.tensor([1.0 if rank0_stop else 0.0], dtype=torch.float64, device=comm.device)
+    t = torch.tensor([float(rank0_action)], dtype=torch.float64, device=comm.device)
     comm.broadcast_(t, src=0)
-    return bool(t.item() > 0.5)
+    return int(round(t.item()))
 
 
 def main(argv=None) -> int:
@@ -125,9 +145,17 @@ def main(argv=None) -> int:
             comm.all_gather_rows(torch.tensor([float(train_ds.n)], dtype=torch.float64, device=comm.device))
         fed = AsyncCollectiveFederation(comm, net, train_ds, fcfg, test_ds=test_ds, engine=engine,
                                         broadcast_initial=True)
+        if job.get("resume_dir"):
+            fed.resume(job["resume_dir"], prev_rank=lcfg.get("prev_rank"))
+            if rank == 0:
+                print(f"[collective-async] resumed at version {fed.version} on {comm.world} learners "
+                      f"(dropped old ranks {getattr(fed, 'resumed', {}).get('dropped')})", flush=True)
         delay = float((fcfg.extra or {}).get("debug_delay_s", {}).get(str(rank), 0.0))
+        my_fault = fault if fault and int(fault.get("rank", -1)) == rank else None
         ups = fed.run_until(max_updates=rounds, cutoff_s=cutoff_s, metric=metric, metric_cutoff=metric_cutoff,
-                            debug_delay_s=delay)
+                            debug_delay_s=delay, checkpoint_dir=ckpt_dir, checkpoint_every=every,
+                            fault_task=int(my_fault["round"]) if my_fault else None,
+                            on_fault=lambda t: _inject_fault(rank, t, my_fault))
         if rank == 0:
             print(f"[collective-async] {len(ups)} FedRec updates, stop: {fed.stop_reason}, staleness "
                   f"{[u.staleness for u in ups]}", flush=True)
@@ -149,25 +177,44 @@ def main(argv=None) -> int:
                   f"(checkpoint of {fed.resumed_from_world})", flush=True)
     while fed.global_iteration < rounds:
         if fault and int(fault.get("rank", -1)) == rank and fed.global_iteration + 1 == int(fault.get("round", 0)):
-            print(f"[collective] fault injection: rank {rank} exits at round {fed.global_iteration + 1}", flush=True)
-            sys.stdout.flush()
-            os._exit(EXIT_INJECTED_FAULT)
+            fed.flush_checkpoints()
+            _inject_fault(rank, fed.global_iteration + 1, fault)
         rec = fed.run_round()
         if rank == 0:
             print(f"[collective] round {rec.global_iteration}: {rec.round_ms:.1f} ms "
                   f"(train {rec.train_ms:.1f}, aggregate {rec.aggregation_ms:.2f}, community eval "
                   f"{rec.community_eval_ms:.1f}) weights {rec.weights}", flush=True)
-        if ckpt_dir and every and (fed.global_iteration % every == 0 or fed.global_iteration >= rounds):
-            fed.save_checkpoint(ckpt_dir)
-        stop = False
+        if ckpt_dir and every and fed.global_iteration % every == 0 and fed.global_iteration < rounds:
+            # staged device-to-device now, written while the next round trains
+            rec.checkpoint_ms = fed.save_checkpoint(ckpt_dir, block=False)
+            if rank == 0:
+                print(f"[collective] checkpoint of round {rec.global_iteration} staged in "
+                      f"{rec.checkpoint_ms:.1f} ms", flush=True)
+        action = 0
         if rank == 0:
             m = fed.community_metric(rec, metric) if metric else None
             stop = (fed.stop_requested or (metric_cutoff is not None and m is not None and m >= float(metric_cutoff))
                     or (cutoff_s is not None and time.time() - t_start > cutoff_s))
-        if _stop_decision(comm, stop):
+            action = 1 if stop else (2 if fed.regroup_requested and fed.global_iteration < rounds else 0)
+        action = _decision(comm, action)
+        if action == 2:
+            # a learner joins: a complete checkpoint of this round, then every
+            # rank leaves; the driver relaunches the larger membership from it
+            fed.save_checkpoint(ckpt_dir)
+            fed.flush_checkpoints()
+            if rank == 0:
+                print(f"[collective] regroup after round {fed.global_iteration}: checkpointed, exiting for the "
+                      f"relaunch", flush=True)
+                fed.engine.close()
+            if wd is not None:
+                wd.stop()
+            comm.close()
+            return EXIT_REGROUP
+        if action == 1:
             break
-    if ckpt_dir and not (every and fed.global_iteration % every == 0):
-        fed.save_checkpoint(ckpt_dir)
+    if ckpt_dir:
+        fed.save_checkpoint(ckpt_dir)  # the final one, complete before the ranks leave
+    fed.flush_checkpoints()
     if rank == 0:
         st = net.state
         vals = st.to_numpy()

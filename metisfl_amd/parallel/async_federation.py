@@ -37,10 +37,28 @@ chunked).  ``serve_in_thread=False`` keeps the single-threaded variant: rank
 so a finisher waits up to one chunk.  The weights are the
 NUM_TRAINING_EXAMPLES (or batch / participant) scaling inputs,
 un-normalised, as FedRec consumes them.
+
+Failure handling (in the reference one lost learner never ends
+an asynchronous federation: controller.cc:171-199 removes it and the
+asynchronous scheduler keeps serving the others).  ``run_until`` with a
+checkpoint directory writes, every ``checkpoint_every`` community versions,
+the aggregator's FedRec state (S, Z, every learner's last contribution and
+weight, the version) plus the community model as a ``FederatedModel``
+(``<dir>/round_<version>/``, LATEST), and every learner's local state after
+its tasks (``<dir>/async_learner_rank<r>.pt``) -- staged on the device and
+written by background threads (parallel/checkpoint.py).  After a lost rank
+the driver relaunches the survivors; ``resume`` restores the FedRec state,
+drops the lost learners' contributions from S and Z, restarts every survivor
+from the restored community model and continues the version count.
+The controller bookkeeping (runtime metadata per version, the driver's stop
+request) goes through a queue served by its own thread, never under the
+aggregator lock.
 """
 from __future__ import annotations
 
 import json
+import os
+import queue
 import threading
 import time
 from dataclasses import dataclass
@@ -118,6 +136,14 @@ class AsyncCollectiveFederation:
         self.updates: list[AsyncUpdate] = []   # rank 0: every FedRec update applied
         self.version = 0                       # rank 0: community model version
         self.base_version = 0                  # version this learner's current task started from
+        self.task_index = 0                    # tasks this learner completed (kept across a resume)
+        self.ckpt_dir: str | None = None
+        self.ckpt_every = 0
+        self.snapshot_every = int(getattr(cfg, "snapshot_every", 0) or 0)
+        self._ckpt = self._lckpt = self._lineage = None
+        self._bk_q: queue.Queue | None = None
+        self._bk_thread = None
+        self._driver_stop = False
         st = net.state
         if broadcast_initial and comm.distributed:
             comm.broadcast_(st.model32, src=0)
@@ -215,6 +241,7 @@ class AsyncCollectiveFederation:
                 while self._pending():
                     if not self.serve(block=False):
                         time.sleep(0.001)
+        self._close_bookkeeping()
         return self.updates
 
     def _sync_stream(self) -> None:
@@ -282,8 +309,10 @@ class AsyncCollectiveFederation:
         if self.engine is not None:
             # one FederatedTaskRuntimeMetadata per community version + the
             # finisher's local task lineage (the reference's async controller
-            # records both per completion, controller.cc:201-259, 428-518)
-            self.engine.record_async_update(self.version, r, meta, up)
+            # records both per completion, controller.cc:201-259, 428-518);
+            # sent by the bookkeeping thread, not under the aggregator lock
+            self._bookkeep("update", self.version, r, meta, up)
+        self._after_fedrec()
 
     def _community(self) -> torch.Tensor:
         c = self.S.clone()
@@ -308,7 +337,206 @@ class AsyncCollectiveFederation:
                "accuracy": float(ev["accuracy"]), "num_examples": int(ev.get("n", 0))}
         self.evaluations.append(rec)
         if self.engine is not None:
-            self.engine.record_async_evaluation(rec)
+            self._bookkeep("eval", rec)
+
+    # ---- controller bookkeeping off the aggregator's path -----------------
+    STOP_POLL_S = 0.5
+
+    def _bookkeep(self, kind: str, *args) -> None:
+        if self._bk_q is None:
+            self._bk_q = queue.Queue()
+            self._bk_thread = threading.Thread(target=self._bookkeeping_loop, name="metisfl-async-bookkeeping",
+                                               daemon=True)
+            self._bk_thread.start()
+        self._bk_q.put((kind, args))
+
+    def _bookkeeping_loop(self) -> None:
+        last_poll = 0.0
+        while True:
+            try:
+                item = self._bk_q.get(timeout=self.STOP_POLL_S)
+            except queue.Empty:
+                item = None
+            if item is not None:
+                kind, args = item
+                if kind == "close":
+                    return
+                try:
+                    if kind == "update":
+                        self.engine.record_async_update(*args)
+                    elif kind == "eval":
+                        self.engine.record_async_evaluation(*args)
+                except Exception as e:  # noqa: BLE001 - bookkeeping must not kill the aggregator
+                    print(f"[async] controller bookkeeping failed: {e!r}", flush=True)
+            if self._until and time.time() - last_poll >= self.STOP_POLL_S:
+                last_poll = time.time()
+                try:
+                    if self.engine.should_stop():
+                        self._driver_stop = True
+                except Exception:  # noqa: BLE001
+                    pass
+
+    def _close_bookkeeping(self) -> None:
+        if self._bk_thread is not None:
+            self._bk_q.put(("close", ()))
+            self._bk_thread.join(timeout=30)
+            self._bk_thread = None
+            self._bk_q = None
+
+    # ---- checkpoints / lineage snapshots / resume ------------------------------------
+    def _after_fedrec(self) -> None:
+        """Rank 0, under the lock, after a FedRec update: the periodic
+        aggregator checkpoint and the controller's community-model lineage
+        (both staged device-to-device and written in the background; skipped
+        while the previous one is still being written)."""
+        v = self.version
+        if self.ckpt_dir and self.ckpt_every and v % self.ckpt_every == 0:
+            self._checkpoint_aggregator(block=False)
+        if self.engine is not None and self.snapshot_every and v % self.snapshot_every == 0 \
+                and hasattr(self.engine, "snapshot_community"):
+            from metisfl_amd.parallel import checkpoint as ck
+            if self._lineage is None:
+                self._lineage = ck.AsyncSnapshot(self.S.device, "metisfl-async-lineage")
+            st, engine, z = self.net.state, self.engine, float(self.Z)
+
+            def write(h):
+                flat = (h["S"].double() / z).float().numpy()
+                engine.snapshot_community([sp.name for sp in st.specs],
+                                          [flat[sp.offset: sp.offset + sp.numel].reshape(sp.shape) for sp in st.specs],
+                                          [sp.trainable for sp in st.specs], v)
+            self._lineage.try_submit({"S": self.S}, write)
+
+    def _checkpoint_aggregator(self, block: bool = False) -> None:
+        from metisfl_amd.parallel import checkpoint as ck
+        if self._ckpt is None:
+            self._ckpt = ck.AsyncSnapshot(self.S.device, "metisfl-async-checkpoint")
+        if self._ckpt.busy() and not block:
+            return
+        v, root = self.version, self.ckpt_dir
+        tensors = {"S": self.S}
+        for r, x in enumerate(self.last):
+            if x is not None:
+                tensors[f"last{r}"] = x
+        meta = {"Z": float(self.Z), "last_w": list(self.last_w), "version": v, "world": self.world,
+                "learner_ids": list(getattr(self, "learner_ids", [f"learner_{r}" for r in range(self.world)])),
+                "protocol": "asynchronous", "global_iteration": v,
+                "updates": [{"learner": u.learner, "task": u.task, "weight": u.weight, "staleness": u.staleness}
+                            for u in self.updates[-1000:]]}
+        st = self.net.state
+        n_contrib = sum(1 for x in self.last if x is not None)
+
+        def write(h):
+            d = os.path.join(root, f"round_{v}")
+            os.makedirs(d, exist_ok=True)
+            state = {k: t.clone() for k, t in h.items()}
+            ck.atomic_torch_save(state, os.path.join(d, "async_state.pt"))
+            from metisfl_amd.proto import model_pb2
+            from metisfl_amd.utils.tensor_codec import model_from_arrays
+            flat = (h["S"].double() / meta["Z"]).float().numpy() if meta["Z"] else h["S"].numpy()
+            fm = model_pb2.FederatedModel()
+            fm.num_contributors = n_contrib
+            fm.global_iteration = v
+            fm.model.CopyFrom(model_from_arrays([sp.name for sp in st.specs],
+                                                [flat[sp.offset: sp.offset + sp.numel].reshape(sp.shape)
+                                                 for sp in st.specs], [sp.trainable for sp in st.specs]))
+            ck.atomic_write(os.path.join(d, "community_model.pb"), fm.SerializeToString())
+            ck.atomic_write(os.path.join(d, "federation.json"), json.dumps(meta).encode())
+            ck.publish(root, f"round_{v}")
+
+        os.makedirs(root, exist_ok=True)
+        self._ckpt.submit(tensors, write)
+        if block:
+            self._ckpt.wait()
+
+    def _checkpoint_learner(self, block: bool = False) -> None:
+        """This learner's local state after a task (any rank)."""
+        from metisfl_amd.parallel import checkpoint as ck
+        if self._lckpt is None:
+            self._lckpt = ck.AsyncSnapshot(self.net.state.model32.device, "metisfl-async-learner")
+        st = self.net.state
+        tensors = {"step": st.step, "perm": self.train_ds.perm}
+        for k in ("m", "v", "anchor"):
+            t = getattr(st, k)
+            if t is not None:
+                tensors[k] = t
+        host = {"steps_done": self.steps_done, "base_version": self.base_version, "task": self.task_index}
+        path = os.path.join(self.ckpt_dir, f"async_learner_rank{self.rank}.pt")
+
+        def write(h):
+            d = {k: t.clone() for k, t in h.items()}
+            d.update({k: torch.tensor(v) for k, v in host.items()})
+            ck.atomic_torch_save(d, path)
+
+        os.makedirs(self.ckpt_dir, exist_ok=True)
+        if block:
+            self._lckpt.submit(tensors, write)
+            self._lckpt.wait()
+        else:
+            self._lckpt.try_submit(tensors, write)
+
+    def flush(self) -> None:
+        for w in (self._ckpt, self._lckpt, self._lineage):
+            if w is not None:
+                w.wait()
+
+    def resume(self, path: str, prev_rank: int | None = None) -> None:
+        """Collective.  Continue an asynchronous federation from its last
+        checkpoint on (possibly) fewer learners: rank 0 restores the FedRec
+        state with the contributions of the learners still present (old rank
+        ``prev_rank`` of each new rank) and without the lost ones, every
+        learner restores its local state and starts from the restored
+        community model; the version count continues."""
+        from metisfl_amd.parallel import checkpoint as ck
+        prev = self.rank if prev_rank is None else int(prev_rank)
+        dev = self.net.state.model32.device
+        prevs = self.comm.all_gather_rows(torch.tensor([float(prev)], dtype=torch.float64, device=dev))
+        prevs = [int(x) for x in prevs.cpu().numpy()[:, 0]]
+        st = self.net.state
+        lpath = os.path.join(path, f"async_learner_rank{prev}.pt")
+        if os.path.exists(lpath):
+            d = torch.load(lpath, weights_only=True)
+            st.step.copy_(d["step"].to(dev))
+            for k in ("m", "v"):
+                if k in d and getattr(st, k) is not None and d[k].numel() == getattr(st, k).numel():
+                    getattr(st, k).copy_(d[k].to(dev))
+            if d["perm"].numel() == self.train_ds.perm.numel():
+                self.train_ds.perm.copy_(d["perm"].to(dev))
+                self.steps_done = int(d["steps_done"])
+            self.task_index = int(d["task"])
+        found = ck.resolve(path)
+        ver = torch.zeros(1, dtype=torch.float64, device=dev)
+        if self.rank == 0 and found is not None:
+            with open(os.path.join(found, "federation.json")) as f:
+                meta = json.load(f)
+            state = torch.load(os.path.join(found, "async_state.pt"), weights_only=True)
+            S = state["S"].to(dev)
+            Z = float(meta["Z"])
+            old_w = list(meta["last_w"])
+            self.last = [None] * self.world
+            self.last_w = [0.0] * self.world
+            keep = set()
+            for r, p in enumerate(prevs):
+                x = state.get(f"last{p}")
+                if x is not None:
+                    self.last[r] = x.to(dev)
+                    self.last_w[r] = float(old_w[p])
+                    keep.add(p)
+            for p in range(int(meta["world"])):  # the lost learners leave the running sum
+                x = state.get(f"last{p}")
+                if p not in keep and x is not None:
+                    agg.rolling_op(S, x.to(dev), agg.MERGE_SUB, float(old_w[p]))
+                    Z -= float(old_w[p])
+            self.S.copy_(S)
+            self.Z = Z
+            self.version = int(meta["version"])
+            self.resumed = {"version": self.version, "dropped": sorted(set(range(int(meta["world"]))) - keep)}
+            st.model32.copy_(self._community())
+            ver[0] = self.version
+        self.comm.broadcast_(ver, src=0)
+        self.comm.broadcast_(st.model32, src=0)
+        self.base_version = int(ver.item())
+        st.refresh_bf16()
+        st.set_anchor()
 
     def _after_update(self) -> None:
         """Rank 0, after every FedRec update: the termination signals."""
@@ -324,7 +552,7 @@ class AsyncCollectiveFederation:
             vals = [e.get(self._metric) for e in last if e.get(self._metric) is not None]
             if vals and float(np.mean(vals)) >= self._metric_cutoff:
                 why = "metric"
-        if why is None and self.engine is not None and self.engine.should_stop():
+        if why is None and self._driver_stop:
             why = "driver"
         if why is not None:
             self._stop_flag = True
@@ -344,14 +572,20 @@ class AsyncCollectiveFederation:
 
     def run_until(self, max_updates: int | None = None, cutoff_s: float | None = None,
                   metric: str | None = None, metric_cutoff: float | None = None,
-                  debug_delay_s: float = 0.0) -> list[AsyncUpdate]:
+                  debug_delay_s: float = 0.0, checkpoint_dir: str | None = None,
+                  checkpoint_every: int = 0, fault_task: int | None = None,
+                  on_fault=None) -> list[AsyncUpdate]:
         """Asynchronous tasks until a termination signal: ``max_updates``
         community versions (FedRec updates -- the reference's global
         iterations), the wall-clock cutoff, the mean community-model test
         metric of the learners' latest evaluations, or the driver's stop
         request.  Every learner finishes the task it is running, is served,
-        and leaves; rank 0 serves until all have left."""
+        and leaves; rank 0 serves until all have left.  ``checkpoint_dir`` /
+        ``checkpoint_every``: see the module docstring; ``fault_task``: this
+        learner calls ``on_fault`` when it is about to start that task (1 =
+        its first; fault injection for tests)."""
         self._until = True
+        self.ckpt_dir, self.ckpt_every = checkpoint_dir, int(checkpoint_every or 0)
         self._max_updates = max_updates
         self._deadline = time.time() + cutoff_s if cutoff_s else None
         self._metric, self._metric_cutoff = metric, metric_cutoff
@@ -362,9 +596,12 @@ class AsyncCollectiveFederation:
                 raise RuntimeError("run_until needs the threaded aggregator (serve_in_thread=True)")
             svc = threading.Thread(target=self._serve_loop, name="metisfl-async-aggregator", daemon=True)
             svc.start()
-        task, last_eval = 0, None
+        task, last_eval = self.task_index, None
         spe = self.train_ds.steps_per_epoch
         while not self._stopped():
+            if fault_task is not None and task + 1 == int(fault_task) and on_fault is not None:
+                self.flush()
+                on_fault(task + 1)
             self.net.reset_train_stats()
             t_task = time.time()
             self._train(self.num_local_updates)
@@ -395,6 +632,9 @@ class AsyncCollectiveFederation:
                 self._install()
             last_eval = self._evaluate_received()
             task += 1
+            self.task_index = task
+            if self.ckpt_dir and self.ckpt_every and task % self.ckpt_every == 0:
+                self._checkpoint_learner()
         if self.rank == 0:
             with self._lock:
                 self._record_eval(0, last_eval)
@@ -402,7 +642,13 @@ class AsyncCollectiveFederation:
                 svc.join()
                 if self._svc_error is not None:
                     raise RuntimeError("async aggregator thread failed") from self._svc_error
+            if self.ckpt_dir:
+                self._checkpoint_aggregator(block=True)
         else:
             self.store.set(_DONE.format(self.tag, self.rank), json.dumps({"eval": last_eval}))
+        if self.ckpt_dir:
+            self._checkpoint_learner(block=True)
+        self.flush()
+        self._close_bookkeeping()
         self.tasks_run = task
         return self.updates

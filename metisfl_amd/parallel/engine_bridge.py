@@ -183,6 +183,7 @@ class RemoteCollectiveController(CollectiveController):
             "agg_completed_ns": ns(rec.aggregation_completed_at), "metas": metas,
             "zeros": [int(z) for z in zeros], "sizes": [int(z) for z in sizes], "lengths": [int(z) for z in lengths],
             "eval_ids": ids, "evaluations": [base64.b64encode(e).decode() for e in evs]})
+        self.regroup_requested = bool(r.get("regroup", False))
         return bool(r.get("stop", False))
 
     def should_stop(self) -> bool:
@@ -212,7 +213,7 @@ class RemoteCollectiveController(CollectiveController):
         c = GRPCControllerClient(self._entity, max_workers=1)
         try:
             c.replace_community_model(len(self.ids), model_from_arrays(names, arrays, trainable),
-                                      request_retries=2)
+                                      request_retries=2, global_iteration=int(global_iteration))
         finally:
             c.shutdown()
 

@@ -75,6 +75,10 @@ class FederationConfig:
     # 571-587); rank 0 records the CommunityModelEvaluation with the round
     evaluate_community: bool = True
     eval_max_steps: int | None = None
+    # rank 0 hands the community model to the controller's lineage every
+    # ``snapshot_every`` rounds (0: never; background thread, see
+    # snapshot_community)
+    snapshot_every: int = 1
     quantify: bool = True                  # per-variable zero counts of each community model
     jsonl_log: str | None = None           # rank 0: one JSON line per round (utils/tracing.py)
     # CKKS secure aggregation (reference: PWA over Palisade CKKS, HESchemeConfig
@@ -127,6 +131,8 @@ class RoundRecord:
     # started_at, as in the reference) but inside round_ms
     community_eval: list | None = None
     community_eval_ms: float = 0.0
+    snapshot_ms: float = 0.0               # rank 0: staging the community model for the controller's lineage
+    checkpoint_ms: float = 0.0             # this rank: time the round's checkpoint held it (staging)
 
     def to_json(self) -> dict:
         d = asdict(self)
@@ -194,6 +200,10 @@ class CollectiveFederation:
         self.num_local_updates = [cfg.local_epochs * max(1, math.ceil(n / cfg.batch_size))
                                   for n in self.dataset_sizes]
         self.steps_done_l = [0] * self.L
+        self._ckpt = self._lineage = None   # background writers (parallel/checkpoint.py)
+        self._ckpt_tag = f"{os.getpid()}_{id(self)}" if comm.rank == 0 else ""
+        if comm.distributed:  # every rank uses rank 0's tag for its store keys
+            self._ckpt_tag = comm.broadcast_bytes(self._ckpt_tag.encode() if comm.rank == 0 else None).decode()
         self.global_iteration = 0
         self.history: list[RoundRecord] = []
         self._spes = [d.steps_per_epoch for d in tds]
@@ -537,10 +547,15 @@ class CollectiveFederation:
             self._log.write({"kind": "round", **rec.to_json(),
                              "rounds_per_s": 1e3 / rec.round_ms if rec.round_ms > 0 else 0.0})
         self.stop_requested = False
+        self.regroup_requested = False
         if self.engine is not None:
             r = self.engine.record_round(rec, self.cfg.batch_size,
                                          self._quantifiers() if self.cfg.quantify else None)
             self.stop_requested = bool(r)  # the driver asked the federation to stop
+            # the driver asked for a relaunch on a new membership (a learner joins)
+            self.regroup_requested = bool(getattr(self.engine, "regroup_requested", False))
+            if self.cfg.snapshot_every and self.global_iteration % self.cfg.snapshot_every == 0:
+                rec.snapshot_ms = self.snapshot_community()
         self.update_templates(meta)
         self.history.append(rec)
         return rec
@@ -569,42 +584,114 @@ class CollectiveFederation:
         fm.model.CopyFrom(model_from_arrays(names, [vals[n] for n in names], [s.trainable for s in st.specs]))
         return fm
 
-    def save_checkpoint(self, path: str) -> None:
-        """Collective.  Rank 0 writes the community model as a serialized
-        ``FederatedModel`` proto (the layout the gRPC controller exchanges:
-        ``ReplaceCommunityModel`` / ``GetCommunityModelLineage`` carry the
-        same message) plus federation.json; every rank writes its learner-
-        local optimizer state (torch.save of plain tensors, loadable with
-        weights_only=True)."""
-        os.makedirs(path, exist_ok=True)
+    def _community_proto_from(self, flat: np.ndarray, gi: int):
+        """``FederatedModel`` of a host copy of the flat community model of
+        round ``gi``."""
+        from metisfl_amd.proto import model_pb2
+        from metisfl_amd.utils.tensor_codec import model_from_arrays
         st = self.net.state
-        self._sync()
+        fm = model_pb2.FederatedModel()
+        fm.num_contributors = self.n_learners
+        fm.global_iteration = gi
+        fm.model.CopyFrom(model_from_arrays([s.name for s in st.specs],
+                                            [flat[s.offset: s.offset + s.numel].reshape(s.shape) for s in st.specs],
+                                            [s.trainable for s in st.specs]))
+        return fm
+
+    def _federation_json(self) -> dict:
+        st = self.net.state
+        return {"global_iteration": self.global_iteration, "protocol": self.cfg.protocol,
+                "num_local_updates": list(self.num_local_updates),
+                "world": self.world, "learners_per_rank": self.L, "learner_ids": self.learner_ids,
+                "dataset_sizes": self.dataset_sizes,
+                "config": {k: v for k, v in asdict(self.cfg).items() if k != "extra"},
+                "variables": [[s.name, list(s.shape), s.trainable] for s in st.specs],
+                "history": [r.to_json() for r in self.history]}
+
+    def save_checkpoint(self, path: str, block: bool = True, keep: int = 2) -> float:
+        """Collective.  Checkpoint ``path/round_<gi>/``: rank 0 writes the
+        community model as a serialized ``FederatedModel`` proto (the layout
+        the gRPC controller exchanges: ``ReplaceCommunityModel`` /
+        ``GetCommunityModelLineage`` carry the same message) plus
+        federation.json; every rank writes its learners' local optimizer
+        state (torch.save of plain tensors, loadable with weights_only=True);
+        ``path/LATEST`` moves to it once every rank's files are written
+        (parallel/checkpoint.py).  ``block=False``: the tensors are snapshot
+        device-to-device now and written by a background thread while the
+        next round runs.  -> milliseconds the call held this rank."""
+        from metisfl_amd.parallel import checkpoint as ck
+        if self._ckpt is None:
+            self._ckpt = ck.AsyncSnapshot(self.comm.device, "metisfl-checkpoint")
+        gi = self.global_iteration
+        name = f"round_{gi}"
+        d = os.path.join(path, name)
+        tensors, host = {}, {"learners": torch.tensor(self.L)}
         # learner 0's entries unprefixed (the one-learner layout); co-located
         # learner j >= 1 under "l<j>/"
-        per_rank = {"learners": torch.tensor(self.L)}
         for j, (net, ds) in enumerate(zip(self.nets, self.train_dss)):
             pre = "" if j == 0 else f"l{j}/"
             lst = net.state
-            per_rank[pre + "step"] = lst.step.cpu()
-            per_rank[pre + "steps_done"] = torch.tensor(self.steps_done_l[j])
-            per_rank[pre + "perm"] = ds.perm.cpu()
+            tensors[pre + "step"] = lst.step
+            tensors[pre + "perm"] = ds.perm
+            host[pre + "steps_done"] = torch.tensor(self.steps_done_l[j])
             for k in ("m", "v", "anchor"):
                 t = getattr(lst, k)
                 if t is not None:
-                    per_rank[pre + k] = t.cpu()
-        torch.save(per_rank, os.path.join(path, f"rank{self.rank}.pt"))
+                    tensors[pre + k] = t
         if self.rank == 0:
-            with open(os.path.join(path, self.COMMUNITY_FILE), "wb") as f:
-                f.write(self.community_model_proto().SerializeToString())
-            with open(os.path.join(path, "federation.json"), "w") as f:
-                json.dump({"global_iteration": self.global_iteration,
-                           "num_local_updates": self.num_local_updates,
-                           "world": self.world, "learners_per_rank": self.L, "learner_ids": self.learner_ids,
-                           "dataset_sizes": self.dataset_sizes,
-                           "config": {k: v for k, v in asdict(self.cfg).items() if k != "extra"},
-                           "variables": [[s.name, list(s.shape), s.trainable] for s in st.specs],
-                           "history": [r.to_json() for r in self.history]}, f)
-        self.comm.barrier()
+            tensors["@community"] = self.net.state.model32
+            fed_json = self._federation_json()
+        store = self._store() if self.comm.distributed else None
+        key = f"metisfl_ckpt/{self._ckpt_tag}/{gi}"
+        rank, world = self.rank, self.world
+
+        def write(h):
+            os.makedirs(d, exist_ok=True)
+            per_rank = dict(host)
+            per_rank.update({k: v.clone() for k, v in h.items() if not k.startswith("@")})
+            ck.atomic_torch_save(per_rank, os.path.join(d, f"rank{rank}.pt"))
+            if store is not None:
+                store.set(f"{key}/{rank}", "1")
+            if rank == 0:
+                fm = self._community_proto_from(h["@community"].numpy(), gi)
+                ck.atomic_write(os.path.join(d, self.COMMUNITY_FILE), fm.SerializeToString())
+                ck.atomic_write(os.path.join(d, "federation.json"), json.dumps(fed_json).encode())
+                ck.publish(path, name, store, world, key, keep)
+
+        os.makedirs(path, exist_ok=True)
+        ms = self._ckpt.submit(tensors, write)
+        if block:
+            self._ckpt.wait()
+            self.comm.barrier()
+        return ms
+
+    def flush_checkpoints(self) -> None:
+        """Wait for background checkpoint / lineage writes of this rank."""
+        for w in (self._ckpt, self._lineage):
+            if w is not None:
+                w.wait()
+
+    def snapshot_community(self) -> float:
+        """Rank 0 with a controller bridge: hand the community model to the
+        controller's lineage (``ReplaceCommunityModel``; the reference
+        replaces its community model every global iteration,
+        controller.cc:466), staged now and sent from a background thread.
+        -> milliseconds on the caller's path."""
+        if self.engine is None or not hasattr(self.engine, "snapshot_community"):
+            return 0.0
+        from metisfl_amd.parallel import checkpoint as ck
+        if self._lineage is None:
+            self._lineage = ck.AsyncSnapshot(self.comm.device, "metisfl-lineage")
+        st = self.net.state
+        gi, engine = self.global_iteration, self.engine
+
+        def write(h):
+            flat = h["model"].numpy()
+            engine.snapshot_community([s.name for s in st.specs],
+                                      [flat[s.offset: s.offset + s.numel].reshape(s.shape) for s in st.specs],
+                                      [s.trainable for s in st.specs], gi)
+
+        return self._lineage.submit({"model": st.model32}, write)
 
     def load_community_model(self, fm) -> None:
         """Install a ``FederatedModel`` (proto or serialized bytes) as the
@@ -623,6 +710,11 @@ class CollectiveFederation:
         (computed at construction from the new dataset sizes).  ``prev_rank``:
         this learner's rank in the checkpointed federation (a relaunch after a
         lost rank renumbers the survivors); default: the same rank."""
+        from metisfl_amd.parallel import checkpoint as ck
+        found = ck.resolve(path)
+        if found is None:
+            raise FileNotFoundError(f"no complete checkpoint under {path}")
+        path = found
         with open(os.path.join(path, "federation.json")) as f:
             meta = json.load(f)
         pb = os.path.join(path, self.COMMUNITY_FILE)

@@ -24,7 +24,20 @@ EXIT_PEER_LOST = 75
 
 
 def _default_failure(rank: int, peer: int) -> None:
+    """Exit with EXIT_PEER_LOST.  With METISFL_WATCHDOG_REPORT_DIR set (the
+    driver sets it), first record which peer went silent: a HUNG rank never
+    exits by itself, so the driver learns from these reports which of the
+    ranks it has to stop is the failed one (driver_session._recover_collective)."""
     MetisLogger.error("rank %d: peer rank %d lost its heartbeat; exiting for an elastic restart", rank, peer)
+    d = os.environ.get("METISFL_WATCHDOG_REPORT_DIR")
+    if d:
+        try:
+            import json
+            os.makedirs(d, exist_ok=True)
+            with open(os.path.join(d, f"lost_by_rank{rank}.json"), "w") as f:
+                json.dump({"rank": rank, "peer": peer}, f)
+        except OSError:
+            pass
     os._exit(EXIT_PEER_LOST)
 
 

@@ -123,9 +123,9 @@ class GRPCControllerClient(GRPCServerClient):
         return self._call(_req, request_retries, request_timeout, block)
 
     def replace_community_model(self, num_contributors, model_pb, request_retries=1, request_timeout=None,
-                                block=True):
+                                block=True, global_iteration: int = 0):
         def _req(t=None):
-            fm = pf.ModelProtoMessages.construct_federated_model_pb(num_contributors, model_pb)
+            fm = pf.ModelProtoMessages.construct_federated_model_pb(num_contributors, model_pb, global_iteration)
             resp = self._stub.ReplaceCommunityModel(C.construct_replace_community_model_request_pb(fm),
                                                     timeout=t)
             return resp.ack.status

@@ -71,7 +71,8 @@ def test_collective_asynchronous_protocol_through_the_driver(tmp_path):
 
 
 def test_collective_recovers_from_a_lost_rank(tmp_path):
-    sess = _session(tmp_path, 3, rounds=3, fault={"rank": 2, "round": 2}, heartbeat_timeout_s=10)
+    sess = _session(tmp_path, 3, rounds=3, fault={"rank": 2, "round": 2}, heartbeat_timeout_s=10,
+                    checkpoint_every=1)
     stats = sess.run_collective(request_every_secs=0.3)
     assert len(sess.recoveries) == 1
     rc = sess.recoveries[0]
@@ -89,3 +90,127 @@ def test_collective_recovers_from_a_lost_rank(tmp_path):
     assert "resumed at round 1 on 2 learners (checkpoint of 3)" in log
     w = [json.loads(l.split("weights ")[1]) for l in log.splitlines() if l.startswith("[collective] round 3")]
     assert w and np.isclose(sum(w[-1]), 1.0) and len(w[-1]) == 2
+
+
+def _recovered(sess, tmp_path, failed, resumed_round, world_after):
+    assert len(sess.recoveries) == 1, sess.recoveries
+    rc = sess.recoveries[0]
+    assert rc["failed"] == [failed] and rc["survivors"] == world_after and rc["resumed_from_round"] == resumed_round
+    return rc
+
+
+def test_collective_recovers_from_a_sigkilled_rank(tmp_path):
+    """A rank killed by SIGKILL (exit -9, as the OOM killer does) is the failed
+    rank, not a peer the driver stopped."""
+    sess = _session(tmp_path, 3, rounds=3, fault={"rank": 1, "round": 2, "signal": "KILL"}, heartbeat_timeout_s=10,
+                    checkpoint_every=1)
+    stats = sess.run_collective(request_every_secs=0.3)
+    rc = _recovered(sess, tmp_path, "learner_localhost-1", 1, 2)
+    assert rc["exit_code"] == -9
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert sorted({int(m["global_iteration"]) for m in md}) == [1, 2, 3]
+
+
+def test_collective_recovers_when_rank0_dies(tmp_path):
+    """Rank 0 hosts the rendezvous store and the controller bridge: when it
+    dies the survivors' watchdogs lose the store, exit as peers, and are
+    relaunched with the old rank 1 as the new rank 0."""
+    sess = _session(tmp_path, 3, rounds=3, fault={"rank": 0, "round": 2}, heartbeat_timeout_s=8,
+                    checkpoint_every=1)
+    stats = sess.run_collective(request_every_secs=0.3)
+    _recovered(sess, tmp_path, "learner_localhost-0", 1, 2)
+    md = stats["federation_runtime_metadata"]["metadata"]
+    by_gi = {}
+    for m in md:
+        by_gi.setdefault(int(m["global_iteration"]), m)
+    assert sorted(by_gi) == [1, 2, 3] and len(by_gi[3]["completed_by_learner_id"]) == 2
+    log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-1.log")).read()
+    assert "resumed at round 1 on 2 learners (checkpoint of 3)" in log
+
+
+def test_async_collective_recovers_from_a_lost_rank(tmp_path):
+    """Asynchronous protocol: rank 2 of 3 dies at its second task; the
+    survivors continue from the last checkpointed community version (FedRec
+    state restored, the lost learner's contribution dropped), not from the
+    initial model, and the federation reaches its version budget."""
+    sess = _session(tmp_path, 3, rounds=10, protocol="Asynchronous", fault={"rank": 2, "round": 2},
+                    heartbeat_timeout_s=8, checkpoint_every=1, extra={"debug_delay_s": {"0": 0.3, "1": 0.3}})
+    stats = sess.run_collective(request_every_secs=0.3)
+    rc = _recovered(sess, tmp_path, "learner_localhost-2", sess.recoveries[0]["resumed_from_round"], 2)
+    assert rc["resumed_from_round"] is not None and rc["resumed_from_round"] >= 1
+    log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
+    line = [l for l in log.splitlines() if l.startswith("[collective-async] resumed at version")]
+    assert line and int(line[-1].split("version ")[1].split()[0]) == rc["resumed_from_round"]
+    assert "dropped old ranks [2]" in line[-1]
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert max(int(m["global_iteration"]) for m in md) >= 10
+
+
+def test_community_model_lineage_is_current_mid_run(tmp_path):
+    """Rank 0 hands every round's community model to the controller (in the
+    background): GetCommunityModelLineage serves the latest round while the
+    federation is still running (the reference replaces its community model
+    every global iteration, controller.cc:466)."""
+    import time
+    sess = _session(tmp_path, 2, rounds=4, extra={"debug_slow_s": {"0": 0.0}})
+    seen = set()
+    try:
+        sess.initialize_federation()
+        c = sess._driver_controller_grpc_client
+        end = time.time() + 300
+        while time.time() < end:
+            running = any(p.poll() is None for n, p in sess._procs.items() if n.startswith("learner_"))
+            lin = c.get_community_model_lineage(1)
+            if running and len(lin.federated_models):
+                fm = lin.federated_models[-1]
+                if fm.global_iteration >= 1:
+                    seen.add(int(fm.global_iteration))
+                    assert len(fm.model.variables) > 10
+            if not running:
+                break
+            time.sleep(0.1)
+        sess.monitor_federation(request_every_secs=0.3)
+    finally:
+        sess.shutdown_federation(timeout=60)
+    assert any(1 <= g < 4 for g in seen), seen  # an intermediate round's model, while the ranks ran
+
+
+def test_learner_joins_a_running_collective_federation(tmp_path):
+    """The reference's AddLearner admits a learner at any time
+    (controller.cc:98-168).  2 learners run; a third joins during round 1;
+    the ranks checkpoint at the round boundary, the driver relaunches 3 ranks
+    from it, and the following rounds have 3 contributors with weights over
+    the 3 shards."""
+    import time
+    from metisfl_amd.driver.driver_session import free_port
+    sess = _session(tmp_path, 2, rounds=4, extra={"debug_slow_s": {"0": 0.0}})
+    try:
+        sess.initialize_federation()
+        c = sess._driver_controller_grpc_client
+        end = time.time() + 120
+        while time.time() < end:  # wait until round 1 is under way
+            if c.get_runtime_metadata(num_backtracks=0).metadata:
+                break
+            time.sleep(0.2)
+        sess.join_collective_learner({"LearnerID": "localhost-2", "ProjectHome": ".",
+                                      "GRPCServicer": {"Hostname": "127.0.0.1", "Port": free_port()}})
+        reason = sess.monitor_federation(request_every_secs=0.3)
+    finally:
+        sess.shutdown_federation(timeout=60)
+    assert reason == "rounds"
+    assert len(sess.regroups) == 1 and sess.regroups[0]["joined"] == ["localhost-2"]
+    at = sess.regroups[0]["at_round"]
+    assert 1 <= at < 4
+    stats = sess.get_federation_statistics()
+    md = stats["federation_runtime_metadata"]["metadata"]
+    by_gi = {}
+    for m in md:
+        by_gi[int(m["global_iteration"])] = m  # the last record of each round
+    assert sorted(by_gi) == [1, 2, 3, 4]
+    assert len(by_gi[at]["completed_by_learner_id"]) == 2
+    assert len(by_gi[4]["completed_by_learner_id"]) == 3
+    assert len(stats["learners_descriptor"]["learner"]) == 3
+    log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
+    assert f"resumed at round {at} on 3 learners (checkpoint of 2)" in log
+    w = [json.loads(l.split("weights ")[1]) for l in log.splitlines() if l.startswith("[collective] round 4")]
+    assert w and len(w[-1]) == 3 and np.isclose(sum(w[-1]), 1.0)

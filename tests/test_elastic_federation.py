@@ -96,7 +96,10 @@ def test_checkpoint_is_federated_model_proto_and_resumes_on_fewer_learners(tmp_p
     from metisfl_amd.proto import model_pb2
     from metisfl_amd.utils.tensor_codec import model_to_arrays
     fm = model_pb2.FederatedModel()
-    fm.ParseFromString(open(tmp_path / "ckpt" / "community_model.pb", "rb").read())
+    from metisfl_amd.parallel.checkpoint import resolve
+    d = resolve(str(tmp_path / "ckpt"))  # versioned: ckpt/LATEST -> ckpt/round_1
+    assert d is not None and d.endswith("round_1")
+    fm.ParseFromString(open(os.path.join(d, "community_model.pb"), "rb").read())
     assert fm.global_iteration == 1 and fm.num_contributors == 3
     names, arrays, trainable = model_to_arrays(fm.model)
     assert "stem.conv.weight" in names and "fc.kernel" in names and not all(trainable)
