@@ -173,6 +173,40 @@ class DeviceCKKS:
         return {"encrypt_ms": ev[0].elapsed_time(ev[1]), "allreduce_ms": ev[1].elapsed_time(ev[2]),
                 "decrypt_ms": ev[2].elapsed_time(ev[3]), "ciphertext_bytes": ct.numel() * 8}
 
+    def secure_weighted_allreduce_many(self, comm, flats: list, weights: list, out: torch.Tensor,
+                                       ct: torch.Tensor | None = None, tmp: torch.Tensor | None = None) -> dict:
+        """out <- Dec(sum over every learner of every rank of Enc(flat) * w):
+        the co-located learners of a GPU each encrypt their own model (the
+        reference's learner-side encryption), their weighted ciphertexts are
+        summed on the device (int64 limbs, reduced mod q before the
+        cross-rank all-reduce), then one all-reduce of ciphertexts and one
+        decryption.  Returns timings (ms)."""
+        if comm.world > MAX_ALLREDUCE_RANKS:
+            raise ValueError(f"the int64 ciphertext all-reduce is exact for <= {MAX_ALLREDUCE_RANKS} ranks")
+        n = flats[0].numel()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record()
+        ct = self.encrypt(flats[0], out=ct)
+        self.scale_(ct, weights[0])
+        for k, (x, w) in enumerate(zip(flats[1:], weights[1:]), start=1):
+            tmp = self.encrypt(x, out=tmp)
+            self.scale_(tmp, w)
+            ct.add_(tmp)
+            if k % (MAX_ALLREDUCE_RANKS - 1) == 0:
+                self.reduce_(ct)  # keep the int64 sums from wrapping
+        self.reduce_(ct)
+        ev[1].record()
+        if comm.world > 1:
+            comm.all_reduce_(ct)
+            self.reduce_(ct)
+        ev[2].record()
+        self.decrypt(ct, n, self.bits + WEIGHT_BITS, out=out.view(-1))
+        ev[3].record()
+        ev[3].synchronize()
+        return {"encrypt_ms": ev[0].elapsed_time(ev[1]), "allreduce_ms": ev[1].elapsed_time(ev[2]),
+                "decrypt_ms": ev[2].elapsed_time(ev[3]), "ciphertext_bytes": ct.numel() * 8,
+                "ciphertexts_encrypted": len(flats) * self.num_ciphertexts(n)}
+
     # ------------------------------------------------------------------
     # host byte format (he/ckks.h): "MCK1" | u32 N | u32 L | u32 nct | f64 log2 scale | u64 q[L] | body
     def to_bytes(self, ct: torch.Tensor, log2_scale: float | None = None) -> bytes:

@@ -81,6 +81,9 @@ class Workspace:
 
 # Host-side tests run the fused-fill orchestration on the CPU references.
 FUSED_FILL_CPU = os.environ.get("METISFL_AMD_FUSED_FILL_CPU", "0") == "1"
+# halo-tiled forward convs with the producer's BatchNorm in the operand fill
+# (MFL_HCONV=0: BN apply + im2col conv, for A/B runs)
+HCONV = os.environ.get("MFL_HCONV", "1") == "1"
 # halo dgrad with the BatchNorm backward in its fill (see ConvBN.backward)
 HALO_DGRAD = os.environ.get("MFL_HALO_DGRAD", "0") == "1"
 # the stem's BN backward + weight gradient in one launch (MFL_STEM_FUSED=0:
@@ -212,7 +215,7 @@ class ConvBN(Layer):
         # halo conv with the fused BN fill: fp32 activations with bf16x3
         # products on the GPU (or FUSED_FILL_CPU for the host-side tests)
         self._hconv_ws = -1
-        if ws.dtype == torch.float32 and (
+        if HCONV and ws.dtype == torch.float32 and (
                 (dev.type == "cuda" and K.conv_products() == "bf16x3") or (dev.type == "cpu" and FUSED_FILL_CPU)):
             self._hconv_ws = K.hconv_workspace(s, dev)
             if self._hconv_ws > 0:

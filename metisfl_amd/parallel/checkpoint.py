@@ -79,6 +79,7 @@ class AsyncSnapshot:
         self._error: BaseException | None = None
         self.name = name
         self.last_stage_ms = 0.0
+        self.last_wait_ms = 0.0    # of last_stage_ms: waiting for the previous snapshot's writer
         self.last_write_ms = 0.0
 
     def _buf(self, pool: dict, key: str, t: torch.Tensor, pinned: bool, device=None) -> torch.Tensor:
@@ -120,6 +121,7 @@ class AsyncSnapshot:
         (the critical-path cost)."""
         t0 = time.perf_counter()
         self.wait()  # the staging buffers are about to be reused
+        self.last_wait_ms = (time.perf_counter() - t0) * 1e3
         host = {}
         ev = None
         if self.cuda:

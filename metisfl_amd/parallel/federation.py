@@ -429,12 +429,28 @@ class CollectiveFederation:
         st = self.net.state
         self.last_allreduce_ms = 0.0
         if self.L > 1:
+            wl = [weights[i] for i in self.local_learners()]
+            if self.cfg.secure_aggregation and self.he_dev is not None:
+                # every co-located learner encrypts its own model; the weighted
+                # ciphertexts are summed on the device, then all-reduced
+                with tracing.range("metisfl.secure_allreduce"):
+                    if self._he_ct is None:
+                        self._he_ct = torch.empty(self.he_dev.ct_numel(st.model32.numel()),
+                                                  dtype=torch.int64, device=self.comm.device)
+                        self._he_tmp = torch.empty_like(self._he_ct)
+                    self.last_he_stats = self.he_dev.secure_weighted_allreduce_many(
+                        self.comm, [n.state.model32 for n in self.nets], wl, st.model32, ct=self._he_ct,
+                        tmp=self._he_tmp)
+                self.last_allreduce_ms = self.last_he_stats["allreduce_ms"]
+                self._install_local(st.model32)
+                self._sync()
+                return weights, (time.perf_counter() - t0) * 1e3
             # hierarchical: this GPU's learners summed locally (K1), then the
             # cross-GPU reduction carries one model per GPU
             with tracing.range("metisfl.local_reduce"):
-                self.group.weighted_sum_into(st.model32, [weights[i] for i in self.local_learners()])
+                self.group.weighted_sum_into(st.model32, wl)
             if self.cfg.secure_aggregation:
-                self._secure_aggregate([1.0] * self.world)
+                self._secure_aggregate([1.0] * self.world)  # host CKKS path (CPU runs)
             elif self.world > 1:
                 self._sync()
                 t1 = time.perf_counter()

@@ -12,7 +12,7 @@ while IFS='|' read -r name tmo cmd; do
   [ -z "$name" ] && continue
   case "$name" in \#*) continue;; esac
   echo "[gpu_steps] $name (limit ${tmo}s): $cmd"
-  ( cd "$ROOTD" && eval "timeout -k 10 $tmo $cmd" ) > "gpurun_out/$name.log" 2>&1
+  ( cd "$ROOTD" && eval "timeout -k 10 $tmo env $cmd" ) > "gpurun_out/$name.log" 2>&1
   rc=$?
   echo "[gpu_steps] $name rc=$rc"; tail -4 "gpurun_out/$name.log"
   case $rc in 124|134|137|139) echo "[gpu_steps] crash-class exit; stopping"; exit $rc;; esac

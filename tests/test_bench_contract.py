@@ -71,11 +71,25 @@ def test_bench_two_ranks_one_json_line():
 
 def test_async_bench_json_contract():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "async_bench.py"), "--train-size", "32",
-                        "--batch", "8", "--tasks", "1", "--warmup", "0", "--poll-every", "2"], cwd=ROOT,
-                       env=_env(), capture_output=True, text=True, timeout=600)
+                        "--batch", "8", "--tasks", "1", "--warmup", "0", "--poll-every", "2", "--learners", "1"],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
     assert REQUIRED <= set(d) and d["updates"] == 1
+
+
+def test_async_bench_colocated_learners():
+    """BASELINE config 3 on one GPU: 4 co-located asynchronous learners, FedRec
+    on the device after every task; later finishers see staleness > 0 and the
+    community model equals the host recomputation."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "async_bench.py"), "--train-size", "64",
+                        "--batch", "4", "--tasks", "2", "--warmup", "1", "--learners", "4", "--width-mult", "0.125"],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert REQUIRED <= set(d) and d["updates"] == 8 and d["updates_per_learner"] == [2, 2, 2, 2]
+    assert d["config"]["learners_per_gpu"] == 4 and d["staleness_max"] > 0
+    assert d["community_model_matches_host"] is True
 
 
 def test_async_bench_eight_ranks_uneven_delays():

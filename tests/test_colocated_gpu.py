@@ -1,0 +1,78 @@
+"""Co-located learners on the GPU beyond synchronous FedAvg: the
+asynchronous protocol (FedRec on the device after each finished task,
+parallel/async_colocated.py) and CKKS secure aggregation with one
+encryption per co-located learner (encryption/device.py
+secure_weighted_allreduce_many)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _learners(n, batch=32, shard=128, lr=0.005):
+    from metisfl_amd.models.resnet import ResNet18
+    from metisfl_amd.ops.optim import OptimizerSpec
+    nets, dss = [], []
+    for j in range(n):
+        net = ResNet18(batch_size=batch, device="cuda", seed=7,
+                       optimizer=OptimizerSpec("momentum_sgd", lr, momentum=0.75))
+        rng = np.random.default_rng(30 + j)
+        m = shard + 32 * j  # unequal shards: unequal FedRec weights and task lengths
+        nets.append(net)
+        dss.append(net.make_dataset(rng.standard_normal((m, 32, 32, 3)).astype(np.float32), rng.integers(0, 10, m),
+                                    seed=j))
+    return nets, dss
+
+
+def test_colocated_async_fedrec_on_device():
+    from metisfl_amd.models.colocated import CoLocatedLearners
+    from metisfl_amd.parallel.async_colocated import CoLocatedAsyncFederation
+    from metisfl_amd.parallel.federation import FederationConfig
+    nets, dss = _learners(3)
+    cfg = FederationConfig(protocol="asynchronous", batch_size=32, local_epochs=1, staleness="polynomial")
+    fed = CoLocatedAsyncFederation(CoLocatedLearners(nets, dss), cfg)
+    ups = fed.run(3)
+    torch.cuda.synchronize()
+    assert len(ups) == 9 and sorted(u.learner for u in ups) == [0, 0, 0, 1, 1, 1, 2, 2, 2]
+    assert fed.version == 9 and max(u.staleness for u in ups) > 0
+    assert all(np.isfinite(u.train_loss) for u in ups)
+    ref = fed.community_reference()
+    got = fed.community().double().cpu().numpy()
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-6), np.abs(got - ref).max()
+    # every learner left its last task holding the community version it received
+    last = {}
+    for k, u in enumerate(ups):
+        last[u.learner] = k
+    assert max(last.values()) == len(ups) - 1
+    fin = ups[-1].learner
+    assert torch.allclose(nets[fin].state.model32, fed.community(), rtol=1e-6, atol=1e-7)
+
+
+def test_colocated_secure_aggregation_matches_plaintext_fedavg():
+    from metisfl_amd.parallel.comm import Comm
+    from metisfl_amd.parallel.federation import CollectiveFederation, FederationConfig
+    comm = Comm()
+    nets, dss = _learners(3, shard=64)
+    cfg = FederationConfig(batch_size=32, local_epochs=1, evaluate_test=False, evaluate_community=False,
+                           secure_aggregation=True)
+    fed = CollectiveFederation(comm, nets, dss, cfg)
+    locals_ = []
+    orig = fed.aggregate
+
+    def spy(meta):
+        locals_.append([n.state.model32.double().clone() for n in nets])
+        return orig(meta)
+    fed.aggregate = spy
+    rec = fed.run_round()
+    w = rec.weights
+    sizes = np.array([d.n for d in dss], dtype=np.float64)
+    assert np.allclose(w, sizes / sizes.sum())
+    ref = sum(wi * x for wi, x in zip(w, locals_[0]))
+    got = nets[0].state.model32.double()
+    err = float((got - ref).abs().max())
+    assert err < 1e-5, err
+    assert rec.he_stats["ciphertexts_encrypted"] == 3 * fed.he_dev.num_ciphertexts(got.numel())
+    for n in nets[1:]:
+        assert torch.equal(n.state.model32, nets[0].state.model32)
+    comm.close()
