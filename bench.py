@@ -247,6 +247,8 @@ def main() -> int:
                              "critical_path_ms_mean": sum(ck) / max(1, len(ck)),
                              "background_write_ms_last": fed._ckpt.last_write_ms if fed._ckpt else None,
                              "wait_for_previous_ms_last": fed._ckpt.last_wait_ms if fed._ckpt else None,
+                             "d2d_issue_ms_last": fed._ckpt.last_d2d_issue_ms if fed._ckpt else None,
+                             "prep_ms_last": getattr(fed, "last_checkpoint_prep_ms", None),
                              "dir": ckpt_dir}
     out["aggregation_weights"] = [float(w) for w in timed[-1].weights] if timed and timed[-1].weights is not None else None
     out["community_model"] = _community_digests(comm, net)

@@ -80,6 +80,7 @@ class AsyncSnapshot:
         self.name = name
         self.last_stage_ms = 0.0
         self.last_wait_ms = 0.0    # of last_stage_ms: waiting for the previous snapshot's writer
+        self.last_d2d_issue_ms = 0.0
         self.last_write_ms = 0.0
 
     def _buf(self, pool: dict, key: str, t: torch.Tensor, pinned: bool, device=None) -> torch.Tensor:
@@ -132,6 +133,8 @@ class AsyncSnapshot:
                     d = self._buf(self._dev, k, t, False, device=t.device)
                     d.copy_(t)
                     staged[k] = d
+            t1 = time.perf_counter()
+            self.last_d2d_issue_ms = (t1 - t0) * 1e3 - self.last_wait_ms
             self.stream.wait_stream(cur)
             with torch.cuda.stream(self.stream):
                 for k, t in tensors.items():

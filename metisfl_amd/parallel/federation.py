@@ -636,6 +636,7 @@ class CollectiveFederation:
         device-to-device now and written by a background thread while the
         next round runs.  -> milliseconds the call held this rank."""
         from metisfl_amd.parallel import checkpoint as ck
+        t_prep = time.perf_counter()
         if self._ckpt is None:
             self._ckpt = ck.AsyncSnapshot(self.comm.device, "metisfl-checkpoint")
         gi = self.global_iteration
@@ -675,7 +676,8 @@ class CollectiveFederation:
                 ck.publish(path, name, store, world, key, keep)
 
         os.makedirs(path, exist_ok=True)
-        ms = self._ckpt.submit(tensors, write)
+        self.last_checkpoint_prep_ms = (time.perf_counter() - t_prep) * 1e3
+        ms = self._ckpt.submit(tensors, write) + self.last_checkpoint_prep_ms
         if block:
             self._ckpt.wait()
             self.comm.barrier()
