@@ -34,6 +34,8 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--local-steps", type=int, default=20)
     ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--learners-per-gpu", type=int, default=1,
+                    help="co-located learners per GPU (models/colocated.py), each on its own HIP stream")
     ap.add_argument("--json-out", type=str, default="")
     args = ap.parse_args()
     from metisfl_amd.utils.launch import ensure_world
@@ -53,13 +55,19 @@ def main() -> int:
     n = comm.world
     dev = comm.device
     opt = OptimizerSpec("adam_weight_decay", args.lr, weight_decay=0.01, epsilon=1e-6)
-    net = BertMLM(batch_size=args.batch, device=dev, optimizer=opt, seed=7)
-    c = net.cfg
-    rec = synthetic_mlm(args.batch * args.local_steps, c.seq, c.max_pred, c.vocab, seed=100 + comm.rank,
-                        rec_stride=c.rec_stride)
-    ds = net.make_dataset(rec, seed=comm.rank)
+    L = max(1, args.learners_per_gpu)
+    nets, dss = [], []
+    for j in range(L):
+        gi = comm.rank * L + j
+        net = BertMLM(batch_size=args.batch, device=dev, optimizer=opt, seed=7)
+        c = net.cfg
+        rec = synthetic_mlm(args.batch * args.local_steps, c.seq, c.max_pred, c.vocab, seed=100 + gi,
+                            rec_stride=c.rec_stride)
+        nets.append(net)
+        dss.append(net.make_dataset(rec, seed=gi))
+    net = nets[0]
     cfg = FederationConfig(protocol="synchronous", batch_size=args.batch, local_epochs=1, evaluate_test=False)
-    fed = CollectiveFederation(comm, net, ds, cfg)
+    fed = CollectiveFederation(comm, nets, dss, cfg)
 
     def sync():
         if dev.type == "cuda":
@@ -84,7 +92,7 @@ def main() -> int:
     timed = fed.history[-args.steps:]
     train_ms = sum(r.train_ms for r in timed) / max(1, len(timed))
     step_ms = train_ms / args.local_steps
-    tokens = n * args.local_steps * net.tokens_per_step()
+    tokens = n * L * args.local_steps * net.tokens_per_step()
     out = {
         "metric": "BERT-base MLM federation throughput (tokens/s, whole job)",
         "value": tokens / (round_ms / 1e3),
@@ -98,12 +106,13 @@ def main() -> int:
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic MLM records (bigram token chains, 20 masks/seq), random-init BERT-base",
-        "config": {"model": "bert-base-mlm (110M, post-LN, tied decoder)", "global_batch": args.batch * n,
+        "config": {"model": "bert-base-mlm (110M, post-LN, tied decoder)", "global_batch": args.batch * n * L,
+                   "learners": n * L, "learners_per_gpu": L,
                    "seq_len": c.seq, "local_steps": args.local_steps, "optimizer": "adamw",
                    "aggregation": "FedAvg(NUM_TRAINING_EXAMPLES), RCCL all-reduce",
                    "parallelism": f"fedavg-dp{n}"},
-        "local_step_ms": step_ms,
-        "model_tflops_per_gpu": net.flops_per_step() / (step_ms / 1e3) / 1e12,
+        "local_step_ms": step_ms,  # per update of each learner (co-located: the GPU runs L meanwhile)
+        "model_tflops_per_gpu": L * net.flops_per_step() / (step_ms / 1e3) / 1e12,
         "aggregation_ms_mean": sum(r.aggregation_ms for r in timed) / max(1, len(timed)),
     }
     if comm.rank == 0:

@@ -1118,7 +1118,11 @@ static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
     kred = ((g.R + 1) / 2) * ((g.S + 1) / 2) * g.C;  // the largest parity class
   }
   int fb = env_int("MFL_C32_BM", 0), fn = env_int("MFL_C32_BN", 0), fs = env_int("MFL_C32_SPLIT", 0);
-  if (!fb && !fn && !fs) tuned_plan(g, mode, fb, fn, fs);
+  // CU slots one launch can count on: 256 (the whole chip) for one learner;
+  // fewer when co-located learners' launches share the CUs (MFL_C32_SLOTS,
+  // A/B runs).  The measured plan table assumes the whole chip.
+  const int slots_env = env_int("MFL_C32_SLOTS", 256);
+  if (!fb && !fn && !fs && slots_env == 256) tuned_plan(g, mode, fb, fn, fs);
   const double clk = 2.4e3;  // cycles per us
   ConvPlan best;
   double best_t = 1e30;
@@ -1129,7 +1133,7 @@ static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
     if (par && ((g.N * (g.P / 2) * (g.Q / 2)) % c.bm)) continue;
     const int tiles = cdiv(rows, c.bm) * cdiv(cols, c.bn);
     const int occ = 1;  // a 64-deep ring of >= 3 stages fills most of a CU's LDS
-    const int slots = 256 * occ;
+    const int slots = slots_env * occ;
     for (int sp = 1; sp <= 64 && sp <= nkt_all; ++sp) {
       if (fs && sp != fs) continue;
       const int kt = cdiv(nkt_all, sp);
@@ -1142,7 +1146,7 @@ static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
       const double pace = MFL_C32_BF16X3 ? (c.bm == 64 && c.bn == 64 ? 0.6 : 0.47) : 1.0;
       const double t_alone = pace * c.bm * c.bn * kt * kBK * 2 / 256.0 / clk + 1.2;
       const int full = nwg / slots, rem = nwg % slots;
-      double tt = full * occ * t_alone + (rem ? (rem > 256 ? occ : 1) * t_alone : 0.0);
+      double tt = full * occ * t_alone + (rem ? (rem > slots_env ? occ : 1) * t_alone : 0.0);
       if (s_eff > 1) {
         if (mode == 2) tt += (double)tiles * s_eff * c.bm * c.bn * 4 / 1.3e6;  // atomic bytes at 1.3 TB/s
         else tt += (double)s_eff * c.bm * c.bn * 4 / 1.0e5 + 1.0;              // serial slab reduce
