@@ -289,8 +289,10 @@ class DriverSessionBase:
                 "extra": dict(self.collective_options.get("extra", {}))}
 
     def _collective_job(self, rounds: int, learners=None, resume_dir: str | None = None,
-                        prev_ranks: list[int] | None = None, fault: dict | None = None, tag: str = "") -> str:
-        """The JSON job description every collective rank reads."""
+                        prev_ranks: list[int] | None = None, fault: dict | None = None, tag: str = "",
+                        ranks: list[list[int]] | None = None) -> str:
+        """The JSON job description every collective rank reads (``learners``
+        in rank order, ``ranks``: the learner indices each process hosts)."""
         env = self.federation_environment
         lm = env.local_model_config
         if self.neural_engine != "static":
@@ -319,7 +321,8 @@ class DriverSessionBase:
                              "test_path": l.dataset_configs.test_dataset_path, "devices": l.devices,
                              "seed": self._learner_index(l),
                              "prev_rank": prev_ranks[i] if prev_ranks is not None else None}
-                            for i, l in enumerate(learners)]}
+                            for i, l in enumerate(learners)],
+               "ranks": ranks or [[i] for i in range(len(learners))]}
         p = os.path.join(self.working_dir, f"collective_job{tag}.json")
         with open(p, "w") as f:
             json.dump(job, f)
@@ -328,27 +331,56 @@ class DriverSessionBase:
     def _learner_index(self, learner) -> int:
         return [l.learner_id for l in self.federation_environment.learners].index(learner.learner_id)
 
+    @staticmethod
+    def _device_groups(learners) -> list[list]:
+        """Learners that name the same device(s) share one process: RCCL runs
+        one rank per GPU, and co-located learners train concurrently on their
+        own HIP streams (models/colocated.py) -- the reference's 10 learners
+        on 5 GPUs (examples/config/cifar10/...momentumsgd.yaml) become 5 ranks
+        of 2.  Learners without devices get a process each."""
+        groups: dict = {}
+        for i, l in enumerate(learners):
+            key = tuple(l.devices) if l.devices else ("solo", i)
+            groups.setdefault(key, []).append(l)
+        return list(groups.values())
+
     def _init_collective_learners(self, rounds: int, learners=None, resume_dir=None, prev_ranks=None,
                                   fault=None, tag: str = ""):
-        """One process per learner (= per GPU) under one process group; the
-        torch.distributed env is set here, before any of them touches a GPU
-        (reference counterpart: driver_session.py:529-582).  Each launch is a
-        set of FRESH processes (never a re-exec of one that touched the GPU)."""
+        """One process per device (hosting that device's learners) under one
+        process group; the torch.distributed env is set here, before any of
+        them touches a GPU (reference counterpart: driver_session.py:529-582).
+        Each launch is a set of FRESH processes (never a re-exec of one that
+        touched the GPU)."""
         import sys
         learners = list(self.federation_environment.learners) if learners is None else learners
-        job = self._collective_job(rounds, learners, resume_dir, prev_ranks, fault, tag)
+        groups = self._device_groups(learners)
+        flat = [l for g in groups for l in g]  # rank order
+        if prev_ranks is not None:  # legacy per-rank checkpoints: follow the learners into rank order
+            by_id = {l.learner_id: pr for l, pr in zip(learners, prev_ranks)}
+            prev_ranks = [by_id[l.learner_id] for l in flat]
+        ranks, k = [], 0
+        for g in groups:
+            ranks.append(list(range(k, k + len(g))))
+            k += len(g)
+        job = self._collective_job(rounds, flat, resume_dir, prev_ranks, fault, tag, ranks)
         port = free_port()
-        self._collective_members = learners
-        for rank, l in enumerate(learners):
-            extra = {"RANK": str(rank), "WORLD_SIZE": str(len(learners)), "MASTER_ADDR": "127.0.0.1",
+        self._collective_members = flat
+        self._collective_groups = groups
+        for rank, g in enumerate(groups):
+            l = g[0]
+            extra = {"RANK": str(rank), "WORLD_SIZE": str(len(groups)), "MASTER_ADDR": "127.0.0.1",
                      "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0",
                      "LOCAL_RANK": str(l.devices[0] if l.devices else rank)}
             extra["METISFL_WATCHDOG_REPORT_DIR"] = self._watchdog_dir(tag)
             if self.device == "cpu":
                 extra.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-            self._spawn(f"learner_{l.learner_id}", [sys.executable, "-m", "metisfl_amd.learner.collective", job],
-                        extra)
+            self._spawn(self._proc_name(g), [sys.executable, "-m", "metisfl_amd.learner.collective", job], extra)
         self._collective_tag = tag
+
+    @staticmethod
+    def _proc_name(group) -> str:
+        """A collective process is named (and logs) after the first learner it hosts."""
+        return f"learner_{group[0].learner_id}"
 
     def _watchdog_dir(self, tag: str) -> str:
         return os.path.join(self.working_dir, f"watchdog{tag}")
@@ -369,7 +401,8 @@ class DriverSessionBase:
         signal the driver did not send, e.g. the OOM killer) is a failure;
         ranks the driver terminates here are survivors."""
         members = list(self._collective_members)
-        names = {f"learner_{l.learner_id}": l for l in members}
+        groups = list(getattr(self, "_collective_groups", [[l] for l in members]))
+        names = {self._proc_name(g): g for g in groups}
         before = {n: self._procs[n].poll() for n in names if n in self._procs}
         before[failed_name] = code
         # give ranks that are on their way out (watchdog exit) a moment, so a
@@ -394,7 +427,7 @@ class DriverSessionBase:
                     p.wait(10)
         failed = {n for n, rc in before.items() if n not in signalled and rc not in (None, 0, self._PEER_EXIT)}
         # a hung rank does not exit: the survivors' watchdogs name it
-        order = [f"learner_{l.learner_id}" for l in members]
+        order = [self._proc_name(g) for g in groups]
         wdir = self._watchdog_dir(getattr(self, "_collective_tag", ""))
         if os.path.isdir(wdir):
             for fn in os.listdir(wdir):
@@ -408,19 +441,21 @@ class DriverSessionBase:
         if not failed:
             raise RuntimeError(f"collective learners left on a lost peer, but the failed rank is unknown "
                                f"({failed_name} exited with {code})")
-        survivors = [l for l in members if f"learner_{l.learner_id}" not in failed]
+        survivors = [l for n, g in names.items() if n not in failed for l in g]
         if not survivors:
             raise RuntimeError(f"every collective learner failed ({failed_name} exited with {code})")
         from metisfl_amd.parallel import checkpoint as ck
         ckpt = os.path.join(self.working_dir, "collective_checkpoint")
         found = ck.resolve(ckpt)
         resume = ckpt if found else None
-        prev = [members.index(l) for l in survivors]
+        rank_of = {l.learner_id: r for r, g in enumerate(groups) for l in g}
+        prev = [rank_of[l.learner_id] for l in survivors]
         gi = None
         if found:
             with open(os.path.join(found, "federation.json")) as f:
                 gi = json.load(f)["global_iteration"]
         self.recoveries.append({"failed": sorted(failed), "exit_code": code, "survivors": len(survivors),
+                                "lost_learners": sorted(l.learner_id for n in failed for l in names[n]),
                                 "resumed_from_round": gi, "at": time.time()})
         MetisLogger.warning("collective learner(s) %s lost (exit %d): relaunching %d survivors from round %s",
                             sorted(failed), code, len(survivors), gi)
@@ -488,15 +523,17 @@ class DriverSessionBase:
         self.regroups.append({"joined": [l.learner_id for l in joins], "world": len(members),
                               "at_round": gi, "at": time.time()})
         MetisLogger.info("collective federation regroups at round %d: %d -> %d learners", gi, len(old), len(members))
-        for l in old:
-            n = f"learner_{l.learner_id}"
+        for g in getattr(self, "_collective_groups", [[l] for l in old]):
+            n = self._proc_name(g)
             log = os.path.join(self.working_dir, f"{n}.log")
             if os.path.exists(log):
                 os.replace(log, log + f".group{len(self.regroups)}")
             self._procs.pop(n, None)
-        # old members keep their learner-local state (old rank = index); joiners start fresh (-1)
+        # old members keep their learner-local state (checkpoint files by learner id); joiners start fresh
+        rank_of = {l.learner_id: r for r, g in enumerate(getattr(self, "_collective_groups", [[l] for l in old]))
+                   for l in g}
         self._init_collective_learners(self.federation_environment.termination_signals.federation_rounds,
-                                       members, ckpt, list(range(len(old))) + [-1] * len(joins), None,
+                                       members, ckpt, [rank_of.get(l.learner_id, -1) for l in members], None,
                                        tag=f"_g{len(self.regroups)}")
 
     # -- public API -----------------------------------------------------------------------------------

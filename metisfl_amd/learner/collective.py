@@ -94,18 +94,29 @@ def main(argv=None) -> int:
 
     comm = Comm(backend=job.get("backend"))
     rank = comm.rank
-    if comm.world != len(job["learners"]):
-        raise RuntimeError(f"WORLD_SIZE {comm.world} != {len(job['learners'])} learners in the job")
-    lcfg = job["learners"][rank]
+    # "ranks": the learners each process hosts (learners sharing a device are
+    # co-located in one process: RCCL runs one rank per GPU); default one each
+    ranks = job.get("ranks") or [[i] for i in range(len(job["learners"]))]
+    if comm.world != len(ranks):
+        raise RuntimeError(f"WORLD_SIZE {comm.world} != {len(ranks)} ranks in the job")
+    mine = [job["learners"][i] for i in ranks[rank]]
+    lcfg = mine[0]
     torch.manual_seed(job.get("seed", 0) + rank)
     opt = OptimizerSpec.from_proto(model_pb2.OptimizerConfig.FromString(bytes.fromhex(job["optimizer_hex"])))
     model_def = StaticModelDef.load(job["model_dir"])
-    net = model_def.get_model(batch_size=job["batch_size"], device=comm.device, optimizer=opt,
-                              seed=job.get("seed", 0))
-    train = resolve_dataset(_load_recipe(job.get("train_recipe")), lcfg.get("train_path"))
-    test = resolve_dataset(_load_recipe(job.get("test_recipe")), lcfg.get("test_path"))
-    train_ds = net.make_dataset(train.get_x(), train.get_y(), seed=lcfg.get("seed", rank))
-    test_ds = net.make_dataset(test.get_x(), test.get_y(), seed=rank, shuffle=False) if test is not None else None
+    train_recipe, test_recipe = _load_recipe(job.get("train_recipe")), _load_recipe(job.get("test_recipe"))
+    nets, train_dss, test_dss = [], [], []
+    for lc in mine:
+        n_ = model_def.get_model(batch_size=job["batch_size"], device=comm.device, optimizer=opt,
+                                 seed=job.get("seed", 0))
+        train = resolve_dataset(train_recipe, lc.get("train_path"))
+        test = resolve_dataset(test_recipe, lc.get("test_path"))
+        nets.append(n_)
+        train_dss.append(n_.make_dataset(train.get_x(), train.get_y(), seed=lc.get("seed", rank)))
+        test_dss.append(n_.make_dataset(test.get_x(), test.get_y(), seed=lc.get("seed", rank), shuffle=False)
+                        if test is not None else None)
+    net, train_ds, test_ds = nets[0], train_dss[0], test_dss[0]
+    learner_ids = [l.get("id", f"learner_{i}") for i, l in enumerate(job["learners"])]
     fcfg = FederationConfig(**job["federation"])
     term = job.get("termination") or {}
     rounds = int(job["rounds"])
@@ -133,6 +144,9 @@ def main(argv=None) -> int:
 
     endpoints = [(l["hostname"], l["port"]) for l in job["learners"]]
     if fcfg.protocol == "asynchronous":
+        if len(mine) > 1:
+            raise RuntimeError("DataPlane: rccl runs the asynchronous protocol with one learner per device "
+                               f"(rank {rank} hosts {len(mine)})")
         from metisfl_amd.parallel.async_federation import AsyncCollectiveFederation
         from metisfl_amd.parallel.federation import install_community_model
         initial_model(lambda fm: install_community_model(net, fm))
@@ -165,7 +179,8 @@ def main(argv=None) -> int:
         comm.close()
         return 0
 
-    fed = CollectiveFederation(comm, net, train_ds, fcfg, test_ds=test_ds, broadcast_initial=False)
+    fed = CollectiveFederation(comm, nets, train_dss, fcfg, test_ds=test_dss, learner_ids=learner_ids,
+                               broadcast_initial=False)
     initial_model(fed.load_community_model)
     if rank == 0:
         fed.engine = RemoteCollectiveController(entity, fed.dataset_sizes, endpoints)
@@ -173,8 +188,8 @@ def main(argv=None) -> int:
     if job.get("resume_dir"):
         fed.resume(job["resume_dir"], prev_rank=lcfg.get("prev_rank"))
         if rank == 0:
-            print(f"[collective] resumed at round {fed.global_iteration} on {comm.world} learners "
-                  f"(checkpoint of {fed.resumed_from_world})", flush=True)
+            print(f"[collective] resumed at round {fed.global_iteration} on {fed.n_learners} learners "
+                  f"(checkpoint of {fed.resumed_from_learners})", flush=True)
     while fed.global_iteration < rounds:
         if fault and int(fault.get("rank", -1)) == rank and fed.global_iteration + 1 == int(fault.get("round", 0)):
             fed.flush_checkpoints()

@@ -155,6 +155,13 @@ def install_community_model(net, fm) -> None:
     st.set_anchor()
 
 
+def learner_file(learner_id: str) -> str:
+    """Checkpoint file of one learner's local state (optimizer slots, step
+    counter, epoch permutation)."""
+    safe = "".join(c if c.isalnum() or c in "-_." else "_" for c in str(learner_id))
+    return f"learner_{safe}.pt"
+
+
 class CollectiveFederation:
     """Drives rounds for the learner(s) hosted by this rank.
 
@@ -183,10 +190,12 @@ class CollectiveFederation:
         self.engine = engine if comm.rank == 0 else None
         self.world = comm.world
         self.rank = comm.rank
+        # co-located learners per rank (may differ: learners grouped by device)
         Ls = comm.all_gather_rows(torch.tensor([float(self.L)], dtype=torch.float64, device=comm.device))
-        if any(int(x) != self.L for x in Ls.cpu().numpy()[:, 0]):
-            raise ValueError(f"co-located learners per rank differ: {Ls.cpu().numpy()[:, 0].tolist()}")
-        self.n_learners = self.world * self.L
+        self.Ls = [int(x) for x in Ls.cpu().numpy()[:, 0]]
+        self.Lmax = max(self.Ls)
+        self.offsets = [sum(self.Ls[:r]) for r in range(self.world)]
+        self.n_learners = sum(self.Ls)
         if self.L > 1 and self.elastic:
             raise NotImplementedError("straggler drop (participation_ratio / round_deadline_s) runs one "
                                       "learner per rank")
@@ -194,8 +203,7 @@ class CollectiveFederation:
         # reference: num_local_updates = epochs * ceil(N_train / batch) per
         # learner (controller.cc:148-153); the join-time dataset sizes are
         # exchanged once
-        sizes = comm.all_gather_rows(torch.tensor([float(d.n) for d in tds], dtype=torch.float64,
-                                                  device=comm.device)).cpu().numpy().reshape(-1)
+        sizes = self._gather_learner_rows([[float(d.n)] for d in tds])[:, 0]
         self.dataset_sizes = [int(x) for x in sizes]
         self.num_local_updates = [cfg.local_epochs * max(1, math.ceil(n / cfg.batch_size))
                                   for n in self.dataset_sizes]
@@ -231,7 +239,19 @@ class CollectiveFederation:
 
     def local_learners(self) -> list[int]:
         """Global indices of this rank's learners."""
-        return [self.rank * self.L + j for j in range(self.L)]
+        return [self.offsets[self.rank] + j for j in range(self.L)]
+
+    def _gather_learner_rows(self, rows: list[list[float]]) -> np.ndarray:
+        """Every rank's per-learner rows (equal width), in global learner
+        order -> [n_learners, width] (host).  Ranks may host different
+        numbers of learners: rows are padded to the largest count for the
+        all-gather."""
+        width = len(rows[0])
+        buf = torch.full((self.Lmax, width), float("nan"), dtype=torch.float64)
+        buf[: len(rows)] = torch.tensor(rows, dtype=torch.float64)
+        got = self.comm.all_gather_rows(buf.reshape(-1).to(self.comm.device)).cpu().numpy()
+        got = got.reshape(self.world, self.Lmax, width)
+        return np.concatenate([got[r, : self.Ls[r]] for r in range(self.world)], axis=0)
 
     # ------------------------------------------------------------------------
     def broadcast_initial_model(self) -> None:
@@ -362,6 +382,11 @@ class CollectiveFederation:
                 raise RuntimeError(f"scaler mismatch: engine {we} vs collective {w}")
         return w
 
+    def _rank_weights(self, weights: list[float]) -> list[float]:
+        """Per-rank PWA weights: a one-learner rank's learner weight; ranks
+        hosting several learners sum them (scaled) before encrypting: 1."""
+        return [float(weights[self.offsets[r]]) if self.Ls[r] == 1 else 1.0 for r in range(self.world)]
+
     def _setup_he(self) -> None:
         """One CKKS key pair shared by all learners (the reference's driver
         generates it once, driver_session.py:122-135): rank 0 generates,
@@ -403,7 +428,7 @@ class CollectiveFederation:
                     self._he_ct = torch.empty(self.he_dev.ct_numel(st.model32.numel()),
                                               dtype=torch.int64, device=self.comm.device)
                 self.last_he_stats = self.he_dev.secure_weighted_allreduce(
-                    self.comm, st.model32, weights[self.rank], ct=self._he_ct)
+                    self.comm, st.model32, weights[self.rank], ct=self._he_ct)  # per-rank weights
             self.last_allreduce_ms = self.last_he_stats["allreduce_ms"]
             return
         # host path (CPU / gloo): host encrypt, all-gather ciphertexts, host PWA
@@ -450,7 +475,7 @@ class CollectiveFederation:
             with tracing.range("metisfl.local_reduce"):
                 self.group.weighted_sum_into(st.model32, wl)
             if self.cfg.secure_aggregation:
-                self._secure_aggregate([1.0] * self.world)  # host CKKS path (CPU runs)
+                self._secure_aggregate(self._rank_weights(weights))  # host CKKS path (CPU runs)
             elif self.world > 1:
                 self._sync()
                 t1 = time.perf_counter()
@@ -462,10 +487,10 @@ class CollectiveFederation:
             self._sync()
             return weights, (time.perf_counter() - t0) * 1e3
         if self.cfg.secure_aggregation:
-            self._secure_aggregate(weights)
+            self._secure_aggregate(self._rank_weights(weights))
         elif self.world > 1:
             with tracing.range("metisfl.scale"):
-                opt_ops.scale_(st.model32, weights[self.rank])
+                opt_ops.scale_(st.model32, weights[self.local_learners()[0]])
             self._sync()
             t1 = time.perf_counter()
             with tracing.range("metisfl.all_reduce"):
@@ -519,9 +544,8 @@ class CollectiveFederation:
         vals = []
         for ev, ds in zip(evs, self.test_dss):
             ev = ev or nan
-            vals += [ev["loss"], ev["accuracy"], float(ds.n) if ds is not None and ev is not nan else 0.0]
-        row = torch.tensor(vals, dtype=torch.float64, device=self.comm.device)
-        rows = self.comm.all_gather_rows(row).cpu().numpy().reshape(-1, 3)
+            vals.append([ev["loss"], ev["accuracy"], float(ds.n) if ds is not None and ev is not nan else 0.0])
+        rows = self._gather_learner_rows(vals)
         out = [{"loss": float(r[0]), "accuracy": float(r[1]), "num_examples": int(r[2])} for r in rows]
         if all(o["num_examples"] == 0 for o in out):
             return None, (time.perf_counter() - t0) * 1e3
@@ -531,16 +555,15 @@ class CollectiveFederation:
         self.global_iteration += 1
         started = time.time()
         results = self.local_train_all([self.num_local_updates[i] for i in self.local_learners()])
-        vals = []
+        rows = []
         for ds, res in zip(self.train_dss, results):
             test = res.get("test") or {}
-            vals += [ds.n, res["completed_batches"], res["ms_per_batch"],
-                     res["ms_per_epoch"], res["train_loss"], res["train_accuracy"],
-                     res["completed_epochs"], self.global_iteration,
-                     test.get("loss", float("nan")), test.get("accuracy", float("nan")),
-                     1.0 if res["participated"] else 0.0]
-        row = torch.tensor(vals, dtype=torch.float64, device=self.comm.device)
-        meta = self.comm.all_gather_rows(row).cpu().numpy().reshape(self.n_learners, len(META_FIELDS))
+            rows.append([ds.n, res["completed_batches"], res["ms_per_batch"],
+                         res["ms_per_epoch"], res["train_loss"], res["train_accuracy"],
+                         res["completed_epochs"], self.global_iteration,
+                         test.get("loss", float("nan")), test.get("accuracy", float("nan")),
+                         1.0 if res["participated"] else 0.0])
+        meta = self._gather_learner_rows(rows)
         res = dict(results[0])
         res["ms"] = max(r["ms"] for r in results)
         completed = time.time()
@@ -642,11 +665,12 @@ class CollectiveFederation:
         gi = self.global_iteration
         name = f"round_{gi}"
         d = os.path.join(path, name)
-        tensors, host = {}, {"learners": torch.tensor(self.L)}
-        # learner 0's entries unprefixed (the one-learner layout); co-located
-        # learner j >= 1 under "l<j>/"
+        # one file per learner, keyed by its (stable) learner id, so a relaunch
+        # may pack the learners onto processes differently (a lost GPU, a
+        # joining learner, learners sharing a device)
+        tensors, host = {}, {}
         for j, (net, ds) in enumerate(zip(self.nets, self.train_dss)):
-            pre = "" if j == 0 else f"l{j}/"
+            pre = f"{j}/"
             lst = net.state
             tensors[pre + "step"] = lst.step
             tensors[pre + "perm"] = ds.perm
@@ -655,6 +679,7 @@ class CollectiveFederation:
                 t = getattr(lst, k)
                 if t is not None:
                     tensors[pre + k] = t
+        my_ids = [self.learner_ids[i] for i in self.local_learners()]
         if self.rank == 0:
             tensors["@community"] = self.net.state.model32
             fed_json = self._federation_json()
@@ -664,9 +689,11 @@ class CollectiveFederation:
 
         def write(h):
             os.makedirs(d, exist_ok=True)
-            per_rank = dict(host)
-            per_rank.update({k: v.clone() for k, v in h.items() if not k.startswith("@")})
-            ck.atomic_torch_save(per_rank, os.path.join(d, f"rank{rank}.pt"))
+            for j, lid in enumerate(my_ids):
+                pre = f"{j}/"
+                per = {k[len(pre):]: v for k, v in host.items() if k.startswith(pre)}
+                per.update({k[len(pre):]: v.clone() for k, v in h.items() if k.startswith(pre)})
+                ck.atomic_torch_save(per, os.path.join(d, learner_file(lid)))
             if store is not None:
                 store.set(f"{key}/{rank}", "1")
             if rank == 0:
@@ -723,11 +750,13 @@ class CollectiveFederation:
         may differ (learners joined or left, SURVEY §5.3 / the reference's
         join-leave semantics, controller.cc:99-199): the community model is
         restored on every rank, learner-local state (optimizer slots, step
-        counter, epoch permutation) only on ranks that existed before, and
-        the step budgets / aggregation weights follow the CURRENT shards
-        (computed at construction from the new dataset sizes).  ``prev_rank``:
-        this learner's rank in the checkpointed federation (a relaunch after a
-        lost rank renumbers the survivors); default: the same rank."""
+        counter, epoch permutation) for every learner the checkpoint has a
+        file for (by learner id, whatever rank or co-located slot it has
+        now; learners that joined since start fresh), and the step budgets /
+        aggregation weights follow the CURRENT shards (computed at
+        construction from the new dataset sizes).  ``prev_rank``: for
+        checkpoints of the rounds-1..3 layout (one file per rank), this
+        learner's rank in the checkpointed federation."""
         from metisfl_amd.parallel import checkpoint as ck
         found = ck.resolve(path)
         if found is None:
@@ -753,8 +782,27 @@ class CollectiveFederation:
         else:
             raise FileNotFoundError(f"no community model in checkpoint {path} ({self.COMMUNITY_FILE})")
         same_world = meta["world"] == self.world and int(meta.get("learners_per_rank", 1)) == self.L
+        old_ids = list(meta.get("learner_ids", []))
+        for j, (net, ds) in enumerate(zip(self.nets, self.train_dss)):
+            lid = self.learner_ids[self.local_learners()[j]]
+            f = os.path.join(path, learner_file(lid))
+            if not os.path.exists(f):
+                continue  # a learner that joined after the checkpoint: fresh optimizer state
+            per = torch.load(f, weights_only=True)
+            st = net.state
+            dev = st.model32.device
+            st.step.copy_(per["step"].to(dev))
+            for k in ("m", "v"):
+                t = per.get(k)
+                if t is not None and getattr(st, k) is not None and t.numel() == getattr(st, k).numel():
+                    getattr(st, k).copy_(t.to(dev))
+            # the epoch order continues only on an unchanged shard (same
+            # learner, same dataset size -> same steps per epoch)
+            if lid in old_ids and per["perm"].numel() == ds.perm.numel():
+                ds.perm.copy_(per["perm"].to(ds.perm.device))
+                self.steps_done_l[j] = int(per["steps_done"])
         old_rank = self.rank if prev_rank is None else int(prev_rank)
-        rank_file = os.path.join(path, f"rank{old_rank}.pt")
+        rank_file = os.path.join(path, f"rank{old_rank}.pt")  # round-1..3 layout: one file per rank
         if os.path.exists(rank_file) and 0 <= old_rank < meta["world"]:
             per_rank = torch.load(rank_file, weights_only=True)
             for j, (net, ds) in enumerate(zip(self.nets, self.train_dss)):
@@ -777,3 +825,4 @@ class CollectiveFederation:
         if same_world:
             self.num_local_updates = list(meta["num_local_updates"])
         self.resumed_from_world = int(meta["world"])
+        self.resumed_from_learners = len(meta.get("learner_ids") or []) or self.resumed_from_world

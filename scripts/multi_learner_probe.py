@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--serial", action="store_true", help="one stream (baseline)")
     ap.add_argument("--hw-queues", type=int, default=0)
+    ap.add_argument("--cu-mask", choices=("none", "contig", "interleave"), default="none",
+                    help="confine learner g's stream to 256/G CUs (hipExtStreamCreateWithCUMask): a contiguous "
+                         "CU-id range, or CU ids with id %% G == g")
     a = ap.parse_args()
     gmax = max(a.groups)
     nets, dss = [], []
@@ -42,6 +45,27 @@ def main():
         net.train_steps(ds, 16)
     torch.cuda.synchronize()
     streams = [torch.cuda.Stream() for _ in range(gmax)]
+    masked = {}
+    if a.cu_mask != "none":
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        ncu = torch.cuda.get_device_properties(0).multi_processor_count
+        for G in a.groups:
+            per = ncu // G
+            lst = []
+            for g in range(G):
+                bits = [0] * ((ncu + 31) // 32)
+                for cu in range(ncu):
+                    mine = (cu // per == g) if a.cu_mask == "contig" else (cu % G == g)
+                    if mine:
+                        bits[cu // 32] |= 1 << (cu % 32)
+                arr = (ctypes.c_uint32 * len(bits))(*bits)
+                h = ctypes.c_void_p()
+                err = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(bits)), arr)
+                assert err == 0, f"hipExtStreamCreateWithCUMask: {err}"
+                lst.append(torch.cuda.ExternalStream(h.value))
+            masked[G] = lst
+        print(f"CU-masked streams ({a.cu_mask}), {ncu} CUs", flush=True)
     K = nets[0].graph_steps
     for G in a.groups:
         for mode in (["serial"] if a.serial else []) + ["streams"]:
@@ -51,7 +75,7 @@ def main():
             for r in range(reps):
                 for g in range(G):
                     if mode == "streams":
-                        with torch.cuda.stream(streams[g]):
+                        with torch.cuda.stream(masked[G][g] if masked else streams[g]):
                             nets[g]._train_graph_k.replay()
                     else:
                         nets[g]._train_graph_k.replay()

@@ -214,3 +214,36 @@ def test_learner_joins_a_running_collective_federation(tmp_path):
     assert f"resumed at round {at} on 3 learners (checkpoint of 2)" in log
     w = [json.loads(l.split("weights ")[1]) for l in log.splitlines() if l.startswith("[collective] round 4")]
     assert w and len(w[-1]) == 3 and np.isclose(sum(w[-1]), 1.0)
+
+
+def test_learners_sharing_a_device_are_colocated_in_one_rank(tmp_path):
+    """The reference runs several learners per GPU (10 learners on 5 GPUs in
+    examples/config/cifar10/...momentumsgd.yaml).  RCCL runs one rank per
+    GPU, so learners naming the same device are hosted by ONE process
+    (models/colocated.py): 3 learners on 2 "devices" -> 2 ranks, 3
+    contributors per round, weights over 3 shards."""
+    from metisfl_amd.driver.driver_session import DriverSession, free_port
+    from metisfl_amd.models.model_def import StaticModelDef
+    from metisfl_amd.utils.fedenv_parser import FederationEnvironment
+    d = env_dict([free_port() for _ in range(3)], rounds=2)
+    d["FederationEnvironment"]["DataPlane"] = "rccl"
+    for l, dev in zip(d["FederationEnvironment"]["Learners"], ([0], [0], [1])):
+        l["Devices"] = dev
+    sess = DriverSession(FederationEnvironment(config=d), StaticModelDef("resnet18", width_mult=0.125), train_recipe,
+                         None, eval_recipe, working_dir=str(tmp_path / "w"), device="cpu",
+                         collective_options={"checkpoint_every": 1})
+    stats = sess.run_collective(request_every_secs=0.3)
+    assert [len(g) for g in sess._collective_groups] == [2, 1]
+    job = json.load(open(os.path.join(str(tmp_path / "w"), "collective_job.json")))
+    assert job["ranks"] == [[0, 1], [2]]
+    md = stats["federation_runtime_metadata"]["metadata"]
+    by_gi = {int(m["global_iteration"]): m for m in md}
+    assert sorted(by_gi) == [1, 2] and len(by_gi[2]["completed_by_learner_id"]) == 3
+    log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
+    w = [json.loads(l.split("weights ")[1]) for l in log.splitlines() if l.startswith("[collective] round 2")]
+    assert w and len(w[-1]) == 3 and np.isclose(sum(w[-1]), 1.0)
+    assert not os.path.exists(os.path.join(str(tmp_path / "w"), "learner_localhost-1.log"))  # hosted by rank 0
+    from metisfl_amd.parallel.checkpoint import resolve
+    ck = resolve(os.path.join(str(tmp_path / "w"), "collective_checkpoint"))
+    assert sorted(f for f in os.listdir(ck) if f.startswith("learner_")) == [
+        "learner_localhost-0.pt", "learner_localhost-1.pt", "learner_localhost-2.pt"]
