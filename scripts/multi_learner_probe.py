@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--serial", action="store_true", help="one stream (baseline)")
     ap.add_argument("--hw-queues", type=int, default=0)
+    ap.add_argument("--stagger-us", type=float, default=0.0,
+                    help="delay stream g's first launch by (g %% 4) x this many microseconds (phase offset)")
     ap.add_argument("--cu-mask", choices=("none", "contig", "interleave"), default="none",
                     help="confine learner g's stream to 256/G CUs (hipExtStreamCreateWithCUMask): a contiguous "
                          "CU-id range, or CU ids with id %% G == g")
@@ -72,6 +74,12 @@ def main():
             reps = a.updates // K
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            if mode == "streams" and a.stagger_us > 0:
+                cyc = int(a.stagger_us * 2100)  # ~2.1 GHz shader clock
+                for g in range(G):
+                    if g % 4:
+                        with torch.cuda.stream(masked[G][g] if masked else streams[g]):
+                            torch.cuda._sleep(cyc * (g % 4))
             for r in range(reps):
                 for g in range(G):
                     if mode == "streams":
