@@ -60,7 +60,9 @@ def main():
             print(f"round {rec.global_iteration}: {rec.round_ms:.0f} ms, mean test accuracy {test_acc:.3f}",
                   flush=True)
         if a.checkpoint_every and fed.global_iteration % a.checkpoint_every == 0:
-            fed.save_checkpoint(os.path.join(a.checkpoint_dir, f"round_{fed.global_iteration}"))
+            # versioned: <dir>/round_<gi>/ + <dir>/LATEST (parallel/checkpoint.py); --resume <dir>
+            fed.save_checkpoint(a.checkpoint_dir, block=False)
+    fed.flush_checkpoints()
     if comm.rank == 0:
         from google.protobuf.json_format import MessageToDict
         with open(a.out, "w") as f:
