@@ -24,6 +24,8 @@ one model per GPU.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 
@@ -38,9 +40,36 @@ class CoLocatedLearners:
         dev = self.nets[0].device
         self.device = dev
         self.cuda = dev.type == "cuda"
-        self.streams = [torch.cuda.Stream(device=dev) for _ in self.nets] if self.cuda else [None] * len(nets)
+        self.streams = (self._make_streams(dev, len(self.nets)) if self.cuda else [None] * len(nets))
         self._ev = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                      for _ in self.nets] if self.cuda else None)
+
+    # MFL_COLOC_CUMASK=contig|interleave: confine learner j's stream to its
+    # share of the CUs (hipExtStreamCreateWithCUMask) instead of letting every
+    # learner's kernels spread over the whole chip (A/B knob, off by default)
+    cu_mask = os.environ.get("MFL_COLOC_CUMASK", "")
+
+    @classmethod
+    def _make_streams(cls, dev, n: int) -> list:
+        if not cls.cu_mask or n < 2:
+            return [torch.cuda.Stream(device=dev) for _ in range(n)]
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        per = max(1, ncu // n)
+        out = []
+        with torch.cuda.device(dev):
+            for g in range(n):
+                bits = [0] * ((ncu + 31) // 32)
+                for cu in range(ncu):
+                    if (cu // per == g) if cls.cu_mask == "contig" else (cu % n == g):
+                        bits[cu // 32] |= 1 << (cu % 32)
+                arr = (ctypes.c_uint32 * len(bits))(*bits)
+                h = ctypes.c_void_p()
+                if hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(bits)), arr) != 0:
+                    raise RuntimeError("hipExtStreamCreateWithCUMask failed")
+                out.append(torch.cuda.ExternalStream(h.value, device=dev))
+        return out
 
     def __len__(self) -> int:
         return len(self.nets)
