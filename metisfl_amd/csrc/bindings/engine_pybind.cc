@@ -15,6 +15,7 @@
 #include "he/ckks.h"
 #include "common/chacha20.h"
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 
 namespace py = pybind11;
@@ -344,6 +345,78 @@ PYBIND11_MODULE(_engine, m) {
       out.append(py::make_tuple(q.non_zeros, q.zeros, q.size_bytes));
     }
     return out;
+  });
+  // Checkpoint writers that run with the GIL released (parallel/checkpoint.py:
+  // a background writer thread must not starve the training thread's launch
+  // loop): the community model as a serialized FederatedModel, and tensors
+  // in the safetensors layout (8-byte little-endian header length, JSON
+  // header, raw little-endian data), read back with safetensors' own loader.
+  m.def("write_federated_model", [](const std::string& path, py::buffer flat, const std::vector<std::string>& names,
+                                    const std::vector<std::vector<int64_t>>& shapes,
+                                    const std::vector<int64_t>& offsets, const std::vector<bool>& trainable,
+                                    uint32_t num_contributors, uint32_t global_iteration) {
+    py::buffer_info bi = flat.request();
+    if (bi.itemsize != 4 || bi.format != py::format_descriptor<float>::format())
+      throw std::invalid_argument("write_federated_model: float32 buffer expected");
+    const float* base = static_cast<const float*>(bi.ptr);
+    const int64_t n = bi.size;
+    if (names.size() != shapes.size() || names.size() != offsets.size() || names.size() != trainable.size())
+      throw std::invalid_argument("write_federated_model: ragged variable lists");
+    py::gil_scoped_release nogil;
+    FederatedModelT fm;
+    fm.num_contributors = num_contributors;
+    fm.global_iteration = global_iteration;
+    fm.model.vars.resize(names.size());
+    for (size_t i = 0; i < names.size(); ++i) {
+      VariableT& v = fm.model.vars[i];
+      v.name = names[i];
+      v.trainable = trainable[i];
+      int64_t numel = 1;
+      for (int64_t d : shapes[i]) numel *= d;
+      if (offsets[i] < 0 || offsets[i] + numel > n) throw std::out_of_range("variable outside the flat buffer");
+      v.t.length = (uint32_t)numel;
+      v.t.dims = shapes[i];
+      v.t.dtype = DT_FLOAT32;
+      v.t.byte_order = BO_LITTLE;
+      v.t.value.assign(reinterpret_cast<const char*>(base + offsets[i]), (size_t)numel * 4);
+    }
+    const std::string bytes = serialize_federated_model(fm);
+    const std::string tmp = path + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot open " + tmp);
+    const size_t w = std::fwrite(bytes.data(), 1, bytes.size(), f);
+    if (std::fclose(f) != 0 || w != bytes.size()) throw std::runtime_error("short write " + tmp);
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("rename " + tmp);
+  });
+  m.def("write_safetensors", [](const std::string& path, const std::vector<std::string>& names,
+                                const std::vector<py::buffer>& bufs, const std::vector<std::string>& dtypes,
+                                const std::vector<std::vector<int64_t>>& shapes) {
+    if (names.size() != bufs.size() || names.size() != dtypes.size() || names.size() != shapes.size())
+      throw std::invalid_argument("write_safetensors: ragged lists");
+    std::vector<std::pair<const char*, size_t>> data;
+    std::string header = "{";
+    size_t off = 0;
+    for (size_t i = 0; i < names.size(); ++i) {
+      py::buffer_info bi = bufs[i].request();
+      const size_t nb = (size_t)bi.size * (size_t)bi.itemsize;
+      data.emplace_back(static_cast<const char*>(bi.ptr), nb);
+      if (i) header += ",";
+      header += "\"" + names[i] + "\":{\"dtype\":\"" + dtypes[i] + "\",\"shape\":[";
+      for (size_t k = 0; k < shapes[i].size(); ++k) header += (k ? "," : "") + std::to_string(shapes[i][k]);
+      header += "],\"data_offsets\":[" + std::to_string(off) + "," + std::to_string(off + nb) + "]}";
+      off += nb;
+    }
+    header += "}";
+    while (header.size() % 8) header += " ";  // 8-byte aligned data section
+    py::gil_scoped_release nogil;
+    const std::string tmp = path + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot open " + tmp);
+    const uint64_t hl = header.size();
+    bool ok = std::fwrite(&hl, 8, 1, f) == 1 && std::fwrite(header.data(), 1, header.size(), f) == header.size();
+    for (auto& [p, nb] : data) ok = ok && (nb == 0 || std::fwrite(p, 1, nb, f) == nb);
+    if (std::fclose(f) != 0 || !ok) throw std::runtime_error("short write " + tmp);
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("rename " + tmp);
   });
   m.def("roundtrip_model", [](py::bytes model) {
     return B(serialize_model(parse_model(std::string(model))));

@@ -66,6 +66,43 @@ def atomic_torch_save(obj, path: str) -> None:
     os.replace(tmp, path)
 
 
+_ST_DTYPES = {torch.float32: "F32", torch.float64: "F64", torch.float16: "F16", torch.bfloat16: "BF16",
+              torch.int64: "I64", torch.int32: "I32", torch.int16: "I16", torch.int8: "I8", torch.uint8: "U8",
+              torch.bool: "BOOL"}
+
+
+def save_tensors(tensors: dict, path: str) -> None:
+    """Write host tensors in the safetensors layout, atomically.  The native
+    writer (_engine.write_safetensors) holds no GIL while it writes, so a
+    background checkpoint never competes with the training thread's launch
+    loop for the interpreter; ``load_tensors`` (safetensors' own reader)
+    reads it back without executing anything from the file."""
+    from metisfl_amd import _engine as E
+    names, bufs, dts, shapes = [], [], [], []
+    for k in sorted(tensors):
+        t = tensors[k].detach().cpu().contiguous()
+        names.append(k)
+        # bf16 has no buffer protocol: ship its bits as int16
+        bufs.append((t.view(torch.int16) if t.dtype == torch.bfloat16 else t).reshape(-1).numpy())
+        dts.append(_ST_DTYPES[t.dtype])
+        shapes.append(list(t.shape))
+    E.write_safetensors(path, names, bufs, dts, shapes)
+
+
+def load_tensors(path: str) -> dict:
+    from safetensors.torch import load_file
+    return load_file(path)
+
+
+def write_federated_model(path: str, flat, specs, num_contributors: int, global_iteration: int) -> None:
+    """Serialize the flat fp32 community model as the reference's
+    ``FederatedModel`` message (model.proto:48-52) natively, GIL released."""
+    from metisfl_amd import _engine as E
+    E.write_federated_model(path, flat, [s.name for s in specs], [list(s.shape) for s in specs],
+                            [int(s.offset) for s in specs], [bool(s.trainable) for s in specs],
+                            int(num_contributors), int(global_iteration))
+
+
 class AsyncSnapshot:
     """One background writer with reusable pinned staging buffers."""
 

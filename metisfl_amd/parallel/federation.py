@@ -159,7 +159,7 @@ def learner_file(learner_id: str) -> str:
     """Checkpoint file of one learner's local state (optimizer slots, step
     counter, epoch permutation)."""
     safe = "".join(c if c.isalnum() or c in "-_." else "_" for c in str(learner_id))
-    return f"learner_{safe}.pt"
+    return f"learner_{safe}.safetensors"
 
 
 class CollectiveFederation:
@@ -653,7 +653,8 @@ class CollectiveFederation:
         the gRPC controller exchanges: ``ReplaceCommunityModel`` /
         ``GetCommunityModelLineage`` carry the same message) plus
         federation.json; every rank writes its learners' local optimizer
-        state (torch.save of plain tensors, loadable with weights_only=True);
+        state (safetensors layout).  Both writers are native and run with
+        the GIL released (checkpoint.save_tensors / write_federated_model);
         ``path/LATEST`` moves to it once every rank's files are written
         (parallel/checkpoint.py).  ``block=False``: the tensors are snapshot
         device-to-device now and written by a background thread while the
@@ -686,19 +687,20 @@ class CollectiveFederation:
         store = self._store() if self.comm.distributed else None
         key = f"metisfl_ckpt/{self._ckpt_tag}/{gi}"
         rank, world = self.rank, self.world
+        specs, n_learners = self.net.state.specs, self.n_learners
 
         def write(h):
             os.makedirs(d, exist_ok=True)
             for j, lid in enumerate(my_ids):
                 pre = f"{j}/"
                 per = {k[len(pre):]: v for k, v in host.items() if k.startswith(pre)}
-                per.update({k[len(pre):]: v.clone() for k, v in h.items() if k.startswith(pre)})
-                ck.atomic_torch_save(per, os.path.join(d, learner_file(lid)))
+                per.update({k[len(pre):]: v for k, v in h.items() if k.startswith(pre)})
+                ck.save_tensors(per, os.path.join(d, learner_file(lid)))
             if store is not None:
                 store.set(f"{key}/{rank}", "1")
             if rank == 0:
-                fm = self._community_proto_from(h["@community"].numpy(), gi)
-                ck.atomic_write(os.path.join(d, self.COMMUNITY_FILE), fm.SerializeToString())
+                ck.write_federated_model(os.path.join(d, self.COMMUNITY_FILE), h["@community"].numpy(), specs,
+                                         n_learners, gi)
                 ck.atomic_write(os.path.join(d, "federation.json"), json.dumps(fed_json).encode())
                 ck.publish(path, name, store, world, key, keep)
 
@@ -786,9 +788,13 @@ class CollectiveFederation:
         for j, (net, ds) in enumerate(zip(self.nets, self.train_dss)):
             lid = self.learner_ids[self.local_learners()[j]]
             f = os.path.join(path, learner_file(lid))
-            if not os.path.exists(f):
+            f_pt = f[: -len(".safetensors")] + ".pt"  # round-4 interim layout (torch.save)
+            if os.path.exists(f):
+                per = ck.load_tensors(f)
+            elif os.path.exists(f_pt):
+                per = torch.load(f_pt, weights_only=True)
+            else:
                 continue  # a learner that joined after the checkpoint: fresh optimizer state
-            per = torch.load(f, weights_only=True)
             st = net.state
             dev = st.model32.device
             st.step.copy_(per["step"].to(dev))

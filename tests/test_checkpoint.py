@@ -68,3 +68,45 @@ def test_latest_points_at_complete_checkpoints_and_prunes(tmp_path):
 def test_legacy_flat_checkpoint_resolves(tmp_path):
     (tmp_path / "federation.json").write_text("{}")
     assert ck.resolve(str(tmp_path)) == str(tmp_path)
+
+
+def test_native_tensor_writer_roundtrips(tmp_path):
+    ts = {"step": torch.tensor(7, dtype=torch.int64), "perm": torch.randperm(33, dtype=torch.int32),
+          "m": torch.randn(5, 3), "h": torch.randn(4).to(torch.bfloat16), "flag": torch.tensor([True, False]),
+          "empty": torch.zeros(0)}
+    p = str(tmp_path / "x.safetensors")
+    ck.save_tensors(ts, p)
+    got = ck.load_tensors(p)
+    assert sorted(got) == sorted(ts)
+    for k, v in ts.items():
+        assert got[k].dtype == v.dtype and got[k].shape == v.shape and torch.equal(got[k], v), k
+    assert not os.path.exists(p + ".tmp")
+
+
+def test_native_federated_model_writer_matches_python_proto(tmp_path):
+    from types import SimpleNamespace
+    import numpy as np
+    from metisfl_amd.proto import model_pb2
+    from metisfl_amd.utils.tensor_codec import model_from_arrays, model_to_arrays
+    shapes = [(3, 4), (4,), (2, 2, 2)]
+    specs, off = [], 0
+    for i, sh in enumerate(shapes):
+        n = int(np.prod(sh))
+        specs.append(SimpleNamespace(name=f"v{i}", shape=sh, offset=off, numel=n, trainable=i != 1))
+        off += n
+    flat = np.random.default_rng(0).standard_normal(off).astype(np.float32)
+    p = str(tmp_path / "community_model.pb")
+    ck.write_federated_model(p, flat, specs, 3, 11)
+    fm = model_pb2.FederatedModel()
+    fm.ParseFromString(open(p, "rb").read())
+    assert fm.num_contributors == 3 and fm.global_iteration == 11
+    names, arrays, trainable = model_to_arrays(fm.model)
+    assert names == ["v0", "v1", "v2"] and list(trainable) == [True, False, True]
+    for s, a in zip(specs, arrays):
+        assert a.shape == s.shape and np.array_equal(a, flat[s.offset: s.offset + s.numel].reshape(s.shape))
+    ref = model_pb2.FederatedModel(num_contributors=3, global_iteration=11)
+    ref.model.CopyFrom(model_from_arrays(names, [flat[s.offset: s.offset + s.numel].reshape(s.shape) for s in specs],
+                                         [s.trainable for s in specs]))
+    got = model_pb2.FederatedModel()
+    got.ParseFromString(open(p, "rb").read())
+    assert got == ref

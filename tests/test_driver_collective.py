@@ -246,4 +246,5 @@ def test_learners_sharing_a_device_are_colocated_in_one_rank(tmp_path):
     from metisfl_amd.parallel.checkpoint import resolve
     ck = resolve(os.path.join(str(tmp_path / "w"), "collective_checkpoint"))
     assert sorted(f for f in os.listdir(ck) if f.startswith("learner_")) == [
-        "learner_localhost-0.pt", "learner_localhost-1.pt", "learner_localhost-2.pt"]
+        "learner_localhost-0.safetensors", "learner_localhost-1.safetensors",
+        "learner_localhost-2.safetensors"]
