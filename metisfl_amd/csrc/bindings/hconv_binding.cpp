@@ -63,40 +63,46 @@ void hconv_forward(torch::Tensor z, torch::Tensor wp, torch::Tensor out, OptT ws
   TORCH_CHECK(ws_need >= 0, "halo conv: unsupported geometry N=", N, " H=", H, " W=", W, " C=", C, " Co=", Co);
   const int64_t nin = N * H * W * C, nout = N * H * W * Co;
   TORCH_CHECK(nin * 4 < (1LL << 31) && nout * 4 < (1LL << 31), "activation too large for 32-bit byte offsets");
-  check(z, torch::kFloat32, nin, "z");
-  check(wp, torch::kInt32, Co * 9 * C, "packed weights");
-  check(out, torch::kFloat32, nout, "out");
+  // fp32 activations with the packed bf16x3 weight mirror, or the bf16
+  // option: bf16 activations, residual, output and weights
+  const bool bf = z.scalar_type() == torch::kBFloat16;
+  const auto act = bf ? torch::kBFloat16 : torch::kFloat32;
+  check(z, act, nin, "z");
+  check(wp, bf ? torch::kBFloat16 : torch::kInt32, Co * 9 * C, "weights");
+  check(out, act, nout, "out");
   mfl::hc::FwdArgs a{};
+  a.bf16 = bf ? 1 : 0;
   a.N = (int)N; a.H = (int)H; a.W = (int)W; a.C = (int)C; a.Co = (int)Co;
-  a.x.z = z.data_ptr<float>();
+  a.x.z = reinterpret_cast<const float*>(z.data_ptr());
   a.x.has_bn = 1;
   a.x.bn = bn_src(acc, gamma, beta, mean, invstd, run_mean, run_var, C, train, momentum, eps);
   if (has(res)) {
-    check(*res, torch::kFloat32, nin, "res");
-    a.x.res = res->data_ptr<float>();
+    check(*res, act, nin, "res");
+    a.x.res = reinterpret_cast<const float*>(res->data_ptr());
   }
   if (has(zr)) {
     TORCH_CHECK(!has(res), "one residual: res or zr");
-    check(*zr, torch::kFloat32, nin, "zr");
+    check(*zr, act, nin, "zr");
     TORCH_CHECK(has(gamma2) && has(beta2) && has(mean2) && has(invstd2) && has(run_mean2) && has(run_var2),
                 "zr needs its BN parameters");
-    a.x.zr = zr->data_ptr<float>();
+    a.x.zr = reinterpret_cast<const float*>(zr->data_ptr());
     a.x.bnr = bn_src(acc2, *gamma2, *beta2, *mean2, *invstd2, *run_mean2, *run_var2, C, train, momentum, eps);
   }
   a.x.relu = relu ? 1 : 0;
   a.x.train = train ? 1 : 0;
   a.x.M = (int)(N * H * W);
   if (has(y)) {
-    check(*y, torch::kFloat32, nin, "y");
-    a.x.y = y->data_ptr<float>();
+    check(*y, act, nin, "y");
+    a.x.y = reinterpret_cast<float*>(y->data_ptr());
   }
   if (has(yp)) {
+    TORCH_CHECK(!bf, "the bf16 option has no packed mirror");
     TORCH_CHECK(has(y), "yp is written with y");
     check(*yp, torch::kInt32, nin, "yp");
     a.x.yp = reinterpret_cast<uint32_t*>(yp->data_ptr());
   }
   a.wp = reinterpret_cast<const uint32_t*>(wp.data_ptr());
-  a.out = out.data_ptr<float>();
+  a.out = reinterpret_cast<float*>(out.data_ptr());
   a.reps = 1;
   if (has(stats)) {
     TORCH_CHECK(train, "output statistics are a train-mode product");

@@ -58,6 +58,7 @@ struct FwdArgs {
   int dbg = 0;                  // ablation (timing only): 1 skip MFMAs, 2 skip fragment reads, 4 skip fills,
                                 // 8 the first (bank-conflicting) weight-fill item order
   int xcd = 1;                  // XCD-grouped tile order (MFL_HC_XCD=0: hardware order)
+  int bf16 = 0;                 // the bf16 option: z / res / zr / y / out bf16, wp = the bf16 weights
 };
 
 // ---- backward data (dgrad) -------------------------------------------------

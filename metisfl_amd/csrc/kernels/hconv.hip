@@ -48,6 +48,7 @@ namespace hc {
 namespace {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16v2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t cvt_pk_bf16(f32x2 v) {  // one v_cvt_pk_bf16_f32 (RNE)
@@ -104,6 +105,10 @@ __device__ __forceinline__ f32x16 mfma_bf16x16(const bf16x8& a, const bf16x8& b,
 __device__ __forceinline__ float4 as_f4(const u32x4& v) {
   return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
+__device__ __forceinline__ float4 as_f4(const u32x2& v) {  // 4 bf16 -> fp32 (exact)
+  return make_float4(__uint_as_float(v[0] << 16), __uint_as_float(v[0] & 0xffff0000u), __uint_as_float(v[1] << 16),
+                     __uint_as_float(v[1] & 0xffff0000u));
+}
 
 // In-kernel phase stamps (profiling only, a.stamps != nullptr): lane 0 of
 // wave 0 records the core clock at phase boundaries with a vector store.
@@ -143,9 +148,16 @@ __device__ __forceinline__ void rep_load(const double* acc, int reps, int C, int
 // the transposed weights are the forward's flipped (B slot 8 - tap).
 // Grid: x = spatial tiles, y = output channel tiles, z = input-channel
 // slices (split-K; kchunk channels each).
-template <class K, int MODE, int RK, class A>
+// BF (forward only): the bf16 option's tensors -- bf16 activations, residual,
+// weights and output; the fill rounds the transformed value to bf16 once
+// (the hi half only: one MFMA per product, the lo slots stay unused), the
+// owner tiles write it as y, the output is rounded to bf16 and its BN sums
+// are taken of the rounded values (as conv.hip's tile_epilogue).
+template <class K, int MODE, int RK, bool BF, class A>
 __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem) {
   constexpr bool DG = MODE == 1;
+  static_assert(!(DG && BF), "the bf16 halo conv is forward-only");
+  constexpr int EB = BF ? 2 : 4;  // activation / weight element bytes
   static_assert(K::NTHR == 512 && K::KCH == 64, "the coefficient prologue maps 8 waves onto 8 replicas x 64 channels");
   // input chunks whose loads are in flight ahead of their fill: every chunk
   // (forward, 1-2 inputs per element), or a ring of 2 (dgrad: 3 inputs)
@@ -229,7 +241,7 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
     const int iy = y0 + py - 1, ix = x0 + px - 1;
     const bool item = i < K::PIX * 4;
     const bool in = item && (img0 + img < a.N) && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-    a_off[u] = in ? (uint32_t)(((((img0 + img) * a.H + iy) * a.W + ix) * C + 4 * q) * 4) : kOOB;
+    a_off[u] = in ? (uint32_t)(((((img0 + img) * a.H + iy) * a.W + ix) * C + 4 * q) * EB) : kOOB;
     a_lds[u] = item ? img * K::IMGB + py * K::ROWB + px * K::PS + 8 * q : K::A_BYTES + K::B_BYTES + 8 * q;
     a_own[u] = own_tile && in && py >= 1 && py <= K::TH && px >= 1 && px <= K::TW;
   }
@@ -270,12 +282,12 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
         co = (k & ~7) | ((k & 3) << 1) | ((k >> 2) & 1);
         tap = (i >> 2) / K::NT;
       }
-      b_off[u] = item ? (uint32_t)((((n0 + co) * 9 + tap) * C + 4 * bq) * 4) : kOOB;
+      b_off[u] = item ? (uint32_t)((((n0 + co) * 9 + tap) * C + 4 * bq) * EB) : kOOB;
       b_lds[u] = item ? K::A_BYTES + tap * (K::NT * K::BPS) + co * K::BPS + 8 * bq
                       : K::A_BYTES + K::B_BYTES + 8 * bq;
     }
   }
-  const uint32_t in_bytes = (uint32_t)((int64_t)a.N * a.H * a.W * C * 4);
+  const uint32_t in_bytes = (uint32_t)((int64_t)a.N * a.H * a.W * C * EB);
   const float* src0;
   const float* src1;
   const float* src2 = nullptr;
@@ -290,7 +302,7 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
   const auto rs0 = make_rsrc(src0, in_bytes);
   const auto rs1 = make_rsrc(src1, in_bytes);
   const auto rs2 = make_rsrc(src2, in_bytes);
-  const auto rsW = make_rsrc(a.wp, (uint32_t)((int64_t)a.Co * 9 * C * 4));
+  const auto rsW = make_rsrc(a.wp, (uint32_t)((int64_t)a.Co * 9 * C * EB));
   constexpr bool IN1 = DG || RK != 0;  // second input per element
   constexpr bool IN2 = DG && RK == 1;  // third (dgrad ReLU mask)
 
@@ -298,16 +310,23 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
   // producer's output comes from the Infinity Cache / HBM, ~2 us: its latency
   // is paid once, under the coefficient prologue); the weights (L2-resident)
   // stream one chunk ahead through a single register set.
-  u32x4 az[PF][K::NA], ar[PF][K::NA], am[PF][K::NA], bw[K::NB];
+  using AV = std::conditional_t<BF, u32x2, u32x4>;  // 4 channels of one pixel
+  AV az[PF][K::NA], ar[PF][K::NA];
+  u32x4 am[PF][K::NA];
+  AV bw[K::NB];
+  auto ld4 = [&](__amdgpu_buffer_rsrc_t r, uint32_t off) -> AV {
+    if constexpr (BF) return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+    else return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  };
   auto load_a = [&](auto kc) {
     constexpr int k = decltype(kc)::value, S = k % PF;
     if (a.dbg & 4) return;
-    const uint32_t cb = (uint32_t)((kbeg + k * K::CC) * 4);
+    const uint32_t cb = (uint32_t)((kbeg + k * K::CC) * EB);
 #pragma unroll
     for (int u = 0; u < K::NA; ++u) {
       const uint32_t off = a_off[u] == kOOB ? kOOB : a_off[u] + cb;
-      az[S][u] = __builtin_amdgcn_raw_buffer_load_b128(rs0, (int)off, 0, 0);
-      if constexpr (IN1) ar[S][u] = __builtin_amdgcn_raw_buffer_load_b128(rs1, (int)off, 0, 0);
+      az[S][u] = ld4(rs0, off);
+      if constexpr (IN1) ar[S][u] = ld4(rs1, off);
       if constexpr (IN2) am[S][u] = __builtin_amdgcn_raw_buffer_load_b128(rs2, (int)off, 0, 0);
     }
   };
@@ -324,11 +343,11 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
           bw[u][e] = __builtin_amdgcn_raw_buffer_load_b32(rsW, (int)(off == kOOB ? kOOB : off + e * kst), 0, 0);
       }
     } else {
-      const uint32_t cb = (uint32_t)((kbeg + k * K::CC) * 4);
+      const uint32_t cb = (uint32_t)((kbeg + k * K::CC) * EB);
 #pragma unroll
       for (int u = 0; u < K::NB; ++u) {
         const uint32_t off = b_off[u] == kOOB ? kOOB : b_off[u] + cb;
-        bw[u] = __builtin_amdgcn_raw_buffer_load_b128(rsW, (int)off, 0, 0);
+        bw[u] = ld4(rsW, off);
       }
     }
   };
@@ -397,10 +416,19 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
         v.x = fmaxf(v.x, lo); v.y = fmaxf(v.y, lo); v.z = fmaxf(v.z, lo); v.w = fmaxf(v.w, lo);
       }
       v.x = oob ? 0.f : v.x; v.y = oob ? 0.f : v.y; v.z = oob ? 0.f : v.z; v.w = oob ? 0.f : v.w;
+      uint8_t* d = stage + a_lds[u];
+      if constexpr (BF) {
+        const uint32_t h01 = cvt_pk_bf16(f32x2{v.x, v.y}), h23 = cvt_pk_bf16(f32x2{v.z, v.w});
+        *reinterpret_cast<uint2*>(d) = make_uint2(h01, h23);
+        if (a_own[u]) {
+          const uint32_t go = a_off[u] + (uint32_t)((kbeg + k * K::CC) * EB);
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(X.y) + go) = make_uint2(h01, h23);
+        }
+        return;
+      }
       uint32_t h01, l01, h23, l23;
       split2(v.x, v.y, h01, l01);
       split2(v.z, v.w, h23, l23);
-      uint8_t* d = stage + a_lds[u];
       *reinterpret_cast<uint2*>(d) = make_uint2(h01, h23);
       *reinterpret_cast<uint2*>(d + 32) = make_uint2(l01, l23);
       if (a_own[u]) {
@@ -415,6 +443,9 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
           if (X.yp) *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(X.yp) + go) = pk;
         }
       }
+    } else if constexpr (BF) {
+      constexpr int u = U - K::NA;
+      *reinterpret_cast<uint2*>(stage + b_lds[u]) = make_uint2(bw[u][0], bw[u][1]);
     } else {
       constexpr int u = U - K::NA;
       const u32x4 d = bw[u];
@@ -550,12 +581,12 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
 #pragma unroll
       for (int i = 0; i < K::TM; ++i) {
         ah[S][i] = *reinterpret_cast<const bf16x8*>(st + fa_off[i] + AO);
-        al[S][i] = *reinterpret_cast<const bf16x8*>(st + fa_off[i] + AO + 32);
+        if constexpr (!BF) al[S][i] = *reinterpret_cast<const bf16x8*>(st + fa_off[i] + AO + 32);
       }
 #pragma unroll
       for (int j = 0; j < K::TN; ++j) {
         bh[S][j] = *reinterpret_cast<const bf16x8*>(st + fb_off[j] + BO);
-        bl[S][j] = *reinterpret_cast<const bf16x8*>(st + fb_off[j] + BO + 32);
+        if constexpr (!BF) bl[S][j] = *reinterpret_cast<const bf16x8*>(st + fb_off[j] + BO + 32);
       }
     };
     rd(IC<0>{});
@@ -571,8 +602,10 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
         for (int i = 0; i < K::TM; ++i)
 #pragma unroll
           for (int j = 0; j < K::TN; ++j) {
-            acc[i][j] = mfma_bf16x16(al[S][i], bh[S][j], acc[i][j]);
-            acc[i][j] = mfma_bf16x16(ah[S][i], bl[S][j], acc[i][j]);
+            if constexpr (!BF) {
+              acc[i][j] = mfma_bf16x16(al[S][i], bh[S][j], acc[i][j]);
+              acc[i][j] = mfma_bf16x16(ah[S][i], bl[S][j], acc[i][j]);
+            }
             acc[i][j] = mfma_bf16x16(ah[S][i], bh[S][j], acc[i][j]);
           }
       }
@@ -721,6 +754,14 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
     if (img0 + img >= a.N) continue;
     float4 v = *reinterpret_cast<const float4*>(tile + rl * K::TST + cg * 4);
     const int64_t off = (((int64_t)(img0 + img) * a.H + y0 + y) * a.W + x0 + x) * a.Co + col;
+    if constexpr (BF) {
+      const uint32_t p01 = cvt_pk_bf16(f32x2{v.x, v.y}), p23 = cvt_pk_bf16(f32x2{v.z, v.w});
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.out) + off) = make_uint2(p01, p23);
+      v = as_f4(u32x2{p01, p23});  // the statistics of the stored (rounded) output
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      sq.x += v.x * v.x; sq.y += v.y * v.y; sq.z += v.z * v.z; sq.w += v.w * v.w;
+      continue;
+    }
     float4* dst = reinterpret_cast<float4*>(a.out + off);
     if constexpr (DG) {
       if (a.accumulate) {
@@ -772,16 +813,16 @@ __device__ __forceinline__ void hconv_body(const A& a, int kchunk, uint8_t* smem
   stamp(a, 8);
 }
 
-template <class K, int RK>
+template <class K, int RK, bool BF>
 __global__ __launch_bounds__(K::NTHR, 1) void hconv_fwd_kernel(FwdArgs a, int kchunk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  hconv_body<K, 0, RK>(a, kchunk, smem);
+  hconv_body<K, 0, RK, BF>(a, kchunk, smem);
 }
 
 template <class K, int MASK>
 __global__ __launch_bounds__(K::NTHR, 1) void hconv_dgrad_kernel(DgArgs a, int kchunk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  hconv_body<K, 1, MASK>(a, kchunk, smem);
+  hconv_body<K, 1, MASK, false>(a, kchunk, smem);
 }
 
 // Stage configurations for the CIFAR ResNet-18 shapes at any batch (3x3, s1):
@@ -841,12 +882,18 @@ size_t lds_of(const Plan& p) {
   return (size_t)K::LDS_MAIN + 5 * (size_t)p.kchunk * sizeof(float);  // + coef [5][kchunk]
 }
 
-template <class K>
+template <class K, bool BF>
 void go_rk(const FwdArgs& a, const Plan& p, hipStream_t s) {
   const size_t lds = lds_of<K>(p);
-  if (a.x.zr) launch(&hconv_fwd_kernel<K, 2>, a, p, lds, K::NTHR, s);
-  else if (a.x.res) launch(&hconv_fwd_kernel<K, 1>, a, p, lds, K::NTHR, s);
-  else launch(&hconv_fwd_kernel<K, 0>, a, p, lds, K::NTHR, s);
+  if (a.x.zr) launch(&hconv_fwd_kernel<K, 2, BF>, a, p, lds, K::NTHR, s);
+  else if (a.x.res) launch(&hconv_fwd_kernel<K, 1, BF>, a, p, lds, K::NTHR, s);
+  else launch(&hconv_fwd_kernel<K, 0, BF>, a, p, lds, K::NTHR, s);
+}
+
+template <class K>
+void go_rk(const FwdArgs& a, const Plan& p, hipStream_t s) {
+  if (a.bf16) go_rk<K, true>(a, p, s);
+  else go_rk<K, false>(a, p, s);
 }
 
 template <class K>

@@ -84,6 +84,8 @@ FUSED_FILL_CPU = os.environ.get("METISFL_AMD_FUSED_FILL_CPU", "0") == "1"
 # halo-tiled forward convs with the producer's BatchNorm in the operand fill
 # (MFL_HCONV=0: BN apply + im2col conv, for A/B runs)
 HCONV = os.environ.get("MFL_HCONV", "1") == "1"
+# ... for the bf16 option too (MFL_HCONV_BF16=0: BN apply + im2col conv)
+HCONV_BF16 = os.environ.get("MFL_HCONV_BF16", "1") == "1"
 # halo dgrad with the BatchNorm backward in its fill (see ConvBN.backward)
 HALO_DGRAD = os.environ.get("MFL_HALO_DGRAD", "0") == "1"
 # the stem's BN backward + weight gradient in one launch (MFL_STEM_FUSED=0:
@@ -213,10 +215,12 @@ class ConvBN(Layer):
         ws.need_split(self.pf.workspace)
         ws.need_split(self.pd.workspace)
         # halo conv with the fused BN fill: fp32 activations with bf16x3
-        # products on the GPU (or FUSED_FILL_CPU for the host-side tests)
+        # products on the GPU (or FUSED_FILL_CPU for the host-side tests), or
+        # the bf16 option's activations with plain bf16 products
         self._hconv_ws = -1
-        if HCONV and ws.dtype == torch.float32 and (
-                (dev.type == "cuda" and K.conv_products() == "bf16x3") or (dev.type == "cpu" and FUSED_FILL_CPU)):
+        if HCONV and ((ws.dtype == torch.float32 and (
+                (dev.type == "cuda" and K.conv_products() == "bf16x3") or (dev.type == "cpu" and FUSED_FILL_CPU)))
+                or (ws.dtype == torch.bfloat16 and dev.type == "cuda" and HCONV_BF16)):
             self._hconv_ws = K.hconv_workspace(s, dev)
             if self._hconv_ws > 0:
                 ws.need_split(self._hconv_ws)
@@ -299,7 +303,8 @@ class ConvBN(Layer):
             K.stem_backward(dy, self.z, self.y, self.x, s, self.gamma, self.mean, self.invstd,
                             self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dw)
             return
-        if HALO_DGRAD and dx is not None and presummed and side is None and self.hconv_ok():
+        if (HALO_DGRAD and dx is not None and presummed and side is None and self.hconv_ok()
+                and self.z.dtype == torch.float32):
             # halo dgrad: the BN backward runs in its operand fill and its
             # owner tiles write dz packed for the wgrad.  Opt-in: measured on
             # MI355X (scripts/hdgrad_bench.py) the halo dgrad beats BN apply +

@@ -312,7 +312,8 @@ def hconv_forward(z, wp, w, out, shp: ConvShape, bn: BnParams, train: bool, relu
     C = shp.C
     if z.is_cuda:
         b2 = bnr if bnr is not None else None
-        ops().hconv_forward(z, wp, out, ws, stats, shp.N, shp.H, shp.W, C, shp.Co, train, relu,
+        # bf16 option: the bf16 weights themselves (no packed mirror)
+        ops().hconv_forward(z, wp if wp is not None else w, out, ws, stats, shp.N, shp.H, shp.W, C, shp.Co, train, relu,
                             bn.acc if train else None, bn.gamma, bn.beta, bn.mean, bn.invstd, bn.run_mean,
                             bn.run_var, bn.momentum, bn.eps, res, zr,
                             (b2.acc if train else None) if b2 else None, b2.gamma if b2 else None,

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--groups", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--updates", type=int, default=256, help="per learner")
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--dtype", default="fp32", choices=("fp32", "bf16"))
     ap.add_argument("--serial", action="store_true", help="one stream (baseline)")
     ap.add_argument("--hw-queues", type=int, default=0)
     ap.add_argument("--stagger-us", type=float, default=0.0,
@@ -37,7 +38,7 @@ def main():
     nets, dss = [], []
     gen = torch.Generator(device="cuda").manual_seed(0)
     for i in range(gmax):
-        net = ResNet18(batch_size=a.batch, device="cuda", seed=7 + i,
+        net = ResNet18(batch_size=a.batch, device="cuda", seed=7 + i, dtype=a.dtype,
                        optimizer=OptimizerSpec("momentum_sgd", 0.005, momentum=0.75))
         x = torch.randn((1024, 32, 32, 3), generator=gen, device="cuda")
         y = torch.randint(0, 10, (1024,), generator=gen, device="cuda")

@@ -185,3 +185,66 @@ def test_hconv_dgrad_fused_bn_backward(st, mode):
     K.hconv_dgrad(dy, ym, z, wp, w, out2, shp, bn, ws=ws, accumulate=accum)
     torch.cuda.synchronize()
     assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("rk", [0, 1, 2], ids=["nores", "res", "bnres"])
+@pytest.mark.parametrize("st", STAGES, ids=lambda s: f"{s[0]}x{s[1]}x{s[2]}")
+def test_hconv_forward_bf16_option(st, rk):
+    """The bf16 option's halo conv (bf16 activations / weights / output, one
+    bf16 product): against a plain PyTorch reference of the same op -- the
+    BatchNorm (+ residual) + ReLU in fp32 from the fp64 sums, rounded to bf16,
+    then the convolution in fp64 of the bf16 operands."""
+    from metisfl_amd.ops import nn as K
+    H, W, C = st
+    N = 32
+    shp = K.ConvShape(N, H, W, C, C, 3, 3, 1, 1)
+    ws_n = K.hconv_workspace(shp, torch.device(DEV))
+    assert ws_n >= 0
+    g = torch.Generator().manual_seed(7000 + 1000 * H + rk)
+    z = (torch.randn(N, H, W, C, generator=g) * 1.5 + 0.3).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(C, 3, 3, C, generator=g) / (9 * C) ** 0.5).to(torch.bfloat16).to(DEV)
+    bn = _bn(C, g, z.float().cpu())
+    res = zr = bnr = None
+    if rk == 1:
+        res = torch.randn(N, H, W, C, generator=g).to(torch.bfloat16).to(DEV)
+    elif rk == 2:
+        zr = (torch.randn(N, H, W, C, generator=g) - 0.2).to(torch.bfloat16).to(DEV)
+        bnr = _bn(C, g, zr.float().cpu())
+    M = N * H * W
+
+    def coef(b, x):
+        acc = b.acc.cpu().reshape(-1, 2, C).sum(0)
+        mu = acc[0] / M
+        var = (acc[1] / M - mu * mu).clamp_min(0)
+        isd = 1.0 / torch.sqrt(var + b.eps)
+        gm, bt = b.gamma.cpu().double(), b.beta.cpu().double()
+        sc, sh = (gm * isd).float(), (bt - mu * gm * isd).float()
+        return x.float().cpu() * sc + sh, mu, isd
+
+    v, mu, isd = coef(bn, z)
+    if rk == 1:
+        v = v + res.float().cpu()
+    elif rk == 2:
+        v = v + coef(bnr, zr)[0]
+    y_ref = v.clamp_min(0).to(torch.bfloat16)
+    out_ref = F.conv2d(y_ref.double().permute(0, 3, 1, 2), w.double().cpu().permute(0, 3, 1, 2),
+                       padding=1).permute(0, 2, 3, 1)
+    out = torch.zeros(N, H, W, C, dtype=torch.bfloat16, device=DEV)
+    y = torch.zeros_like(z)
+    stats = torch.zeros(2 * C, dtype=torch.float64, device=DEV)
+    ws = torch.zeros(max(4, ws_n), device=DEV)
+    K.hconv_forward(z, None, w, out, shp, bn, True, True, ws=ws, stats=stats, res=res, zr=zr, bnr=bnr, y=y)
+    torch.cuda.synchronize()
+    # bf16 output rounding: ~2^-9 per element
+    assert _rel(out, out_ref) <= 3e-3, _rel(out, out_ref)
+    assert _rel(y, y_ref) <= 2e-3
+    assert _rel(bn.mean, mu) <= 1e-6 and _rel(bn.invstd, isd) <= 1e-6
+    o2 = out.double().cpu().reshape(-1, C)  # the sums are of the stored (rounded) output
+    s = stats.reshape(2, C).cpu()
+    assert (s[0] - o2.sum(0)).norm() / o2.abs().sum(0).norm() <= 1e-5
+    assert _rel(s[1], (o2 * o2).sum(0)) <= 1e-5
+    out2 = torch.zeros_like(out)
+    K.hconv_forward(z, None, w, out2, shp, _clone(bn), True, True, ws=ws, res=res, zr=zr,
+                    bnr=_clone(bnr) if bnr is not None else None)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
