@@ -480,18 +480,24 @@ void stem_backward32(torch::Tensor dy, torch::Tensor z, torch::Tensor y, torch::
   const int64_t N = z.size(0), H = z.size(1), W = z.size(2), Co = z.size(3), Cin = x.size(3);
   TORCH_CHECK(x.size(0) == N && x.size(1) == H && x.size(2) == W, "stem backward: x / z shapes");
   TORCH_CHECK(stem_backward32_ok(N, H, W, Cin, Co), "stem backward: unsupported shape");
-  check_nhwc32(dy, Co);
-  check_nhwc32(z, Co);
-  check_nhwc32(y, Co);
-  check_nhwc32(x, Cin);
+  // fp32 activations, or the bf16 option's (dy, z, y, x all bf16)
+  const bool bf = z.scalar_type() == torch::kBFloat16;
+  for (auto* t : {&dy, &z, &y, &x}) {
+    if (bf) {
+      TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == torch::kBFloat16,
+                  "stem backward: contiguous bf16 device tensors expected");
+    } else {
+      check_nhwc32(*t, t == &x ? Cin : Co);
+    }
+  }
   TORCH_CHECK(dy.numel() == z.numel() && y.numel() == z.numel(), "stem backward sizes");
   TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == torch::kFloat32 && dw.is_contiguous() && dw.numel() == Co * 9 * Cin,
               "stem backward: dw [Co][3][3][Cin] fp32");
   for (auto* t : {&gamma, &mean, &invstd}) check_pc(*t, Co, "bn param");
   mfl::BnBwdArgs32 a{};
-  a.dy = fp(dy);
-  a.x = fp(z);
-  a.y = fp(y);
+  a.dy = reinterpret_cast<const float*>(dy.data_ptr());
+  a.x = reinterpret_cast<const float*>(z.data_ptr());
+  a.y = reinterpret_cast<const float*>(y.data_ptr());
   a.acc = acc_ptr(acc, Co);
   a.reps = reps_of(acc, Co);
   TORCH_CHECK(a.reps <= 8, "at most 8 BN accumulator replicas");
@@ -502,7 +508,8 @@ void stem_backward32(torch::Tensor dy, torch::Tensor z, torch::Tensor y, torch::
   if (dbeta.has_value() && dbeta->defined()) { check_pc(*dbeta, Co, "dbeta"); a.dbeta = fp(*dbeta); }
   a.M = z.numel() / Co;
   a.C = (int)Co;
-  mfl::launch_stem_bwd32(a, fp(x), (int)N, (int)H, (int)W, (int)Cin, fp(dw), cur_stream(z));
+  if (bf) mfl::launch_stem_bwd_bf16(a, reinterpret_cast<const uint16_t*>(x.data_ptr()), (int)N, fp(dw), cur_stream(z));
+  else mfl::launch_stem_bwd32(a, fp(x), (int)N, (int)H, (int)W, (int)Cin, fp(dw), cur_stream(z));
 }
 
 // ---- head / data ---------------------------------------------------------
@@ -547,9 +554,16 @@ void head32_forward_backward_bn(int64_t B, int64_t HW, int64_t C, torch::Tensor 
                                 torch::Tensor run_var, double momentum, double eps, bool train, torch::Tensor y,
                                 c10::optional<torch::Tensor> acc_b) {
   const int64_t n = B * HW * C;
-  check_f32(z, n, "head z");
-  check_f32(res, n, "head res");
-  check_f32(y, n, "head y");
+  // fp32 activations, or the bf16 option's (z / res / y / dx bf16)
+  const bool bf = z.scalar_type() == torch::kBFloat16;
+  auto check_act = [&](const torch::Tensor& t, const char* nm) {
+    if (!bf) return check_f32(t, n, nm);
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kBFloat16 && t.numel() == n, nm,
+                ": contiguous bf16 device tensor of ", n, " elements expected");
+  };
+  check_act(z, "head z");
+  check_act(res, "head res");
+  check_act(y, "head y");
   for (auto* t : {&gamma, &beta, &mean, &invstd, &run_mean, &run_var}) check_pc(*t, C, "head bn param");
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "head: C must be a multiple of 8 (<= 2048)");
   check_f32(W, 0, "head W", false);
@@ -559,8 +573,8 @@ void head32_forward_backward_bn(int64_t B, int64_t HW, int64_t C, torch::Tensor 
   TORCH_CHECK(labels.is_cuda() && labels.is_contiguous() && labels.scalar_type() == torch::kInt32 &&
                   labels.numel() >= B, "labels");
   mfl::HeadBn hb;
-  hb.z = fp(z);
-  hb.res = fp(res);
+  hb.z = reinterpret_cast<const float*>(z.data_ptr());
+  hb.res = reinterpret_cast<const float*>(res.data_ptr());
   if (train) {
     TORCH_CHECK(acc.has_value() && acc->defined(), "train-mode BN needs its statistics accumulator");
     hb.acc = acc_ptr(*acc, C);
@@ -576,7 +590,7 @@ void head32_forward_backward_bn(int64_t B, int64_t HW, int64_t C, torch::Tensor 
   hb.momentum = (float)momentum;
   hb.eps = (float)eps;
   hb.train = train ? 1 : 0;
-  hb.y = fp(y);
+  hb.y = reinterpret_cast<float*>(y.data_ptr());
   if (backward && acc_b.has_value() && acc_b->defined()) {
     hb.acc_b = const_cast<double*>(acc_ptr(*acc_b, C));
     hb.reps_b = reps_of(*acc_b, C);
@@ -589,7 +603,16 @@ void head32_forward_backward_bn(int64_t B, int64_t HW, int64_t C, torch::Tensor 
   if (backward) {
     TORCH_CHECK(feat.has_value() && dlogits.has_value() && dx.has_value(), "bwd buffers");
     TORCH_CHECK(feat->numel() >= B * C && dlogits->numel() >= B * K, "bwd buffer sizes");
-    check_f32(*dx, n, "head dx");
+    check_act(*dx, "head dx");
+  }
+  if (bf) {
+    mfl::launch_head_fwd_bwd(reinterpret_cast<const uint16_t*>(y.data_ptr()), (int)B, (int)HW, (int)C, fp(W),
+                             opt_ptr<float>(bias), (int)K, labels.data_ptr<int>(), opt_ptr<float>(feat),
+                             opt_ptr<float>(dlogits),
+                             backward ? reinterpret_cast<uint16_t*>(dx->data_ptr()) : nullptr,
+                             opt_ptr<float>(stats), backward, cur_stream(z), fuse ? fp(*dW) : nullptr,
+                             fuse ? opt_ptr<float>(db) : nullptr, &hb);
+    return;
   }
   mfl::launch_head32_fwd_bwd(fp(y), (int)B, (int)HW, (int)C, fp(W), opt_ptr<float>(bias), (int)K,
                              labels.data_ptr<int>(), opt_ptr<float>(feat), opt_ptr<float>(dlogits),

@@ -332,9 +332,19 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
 // Blocks are numbered image-fastest, so with N % 8 == 0 the 8 channel groups
 // of an image run on one XCD (round-robin placement) and share its 256-B
 // activation rows in that XCD's L2.
+// T = uint16_t: the bf16 option's tensors (dy, z, y, x bf16; dz and the
+// products stay fp32).
 constexpr int kStemCG = 8;  // output channels per workgroup
 
-__global__ __launch_bounds__(576) void stem_bwd32_kernel(BnBwdArgs32 a, const float* __restrict__ x, int N,
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 ld4(const uint16_t* p) {
+  const uint2 v = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u), __uint_as_float(v.y << 16),
+                     __uint_as_float(v.y & 0xffff0000u));
+}
+
+template <typename T>
+__global__ __launch_bounds__(576) void stem_bwd32_kernel(BnBwdArgs32 a, const T* __restrict__ x, int N,
                                                          float* __restrict__ dw) {
   constexpr int H = 32, W = 32, CI = 8, CO = 64, PX = H * W, XW = W + 2, G = kStemCG;
   constexpr int NV = PX * G / 4;            // float4 of dy / z / y per workgroup (2 per pixel)
@@ -355,9 +365,9 @@ __global__ __launch_bounds__(576) void stem_bwd32_kernel(BnBwdArgs32 a, const fl
     const int i = t + 576 * u;
     if (NV % 576 == 0 || i < NV) {
       const int64_t o = (pix0 + (i >> 1)) * CO + co0 + 4 * (i & 1);
-      g[u] = *reinterpret_cast<const float4*>(a.dy + o);
-      z[u] = *reinterpret_cast<const float4*>(a.x + o);
-      m[u] = *reinterpret_cast<const float4*>(a.y + o);
+      g[u] = ld4(reinterpret_cast<const T*>(a.dy) + o);
+      z[u] = ld4(reinterpret_cast<const T*>(a.x) + o);
+      m[u] = ld4(reinterpret_cast<const T*>(a.y) + o);
     }
   }
   // the input patch: every load issued before the first LDS store (a
@@ -371,7 +381,7 @@ __global__ __launch_bounds__(576) void stem_bwd32_kernel(BnBwdArgs32 a, const fl
     const int iy = xr - 1, ix = xc - 1;
     xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (i < NX && iy >= 0 && iy < H && ix >= 0 && ix < W)
-      xv[u] = reinterpret_cast<const float4*>(x)[((pix0 + iy * W + ix) * CI >> 2) + (i & 1)];
+      xv[u] = ld4(x + (pix0 + iy * W + ix) * CI + 4 * (i & 1));
   }
   if (t < G) {
     const int c = co0 + t;
@@ -465,18 +475,27 @@ bool stem_bwd32_ok(int N, int H, int W, int Cin, int Co) {
   return N > 0 && N < (1 << 24) && H == 32 && W == 32 && Cin == 8 && Co == 64;
 }
 
-void launch_stem_bwd32(const BnBwdArgs32& a, const float* x, int N, int H, int W, int Cin, float* dw, hipStream_t s) {
+template <typename T>
+static void stem_bwd_launch(const BnBwdArgs32& a, const T* x, int N, float* dw, hipStream_t s) {
   const size_t lds = ((size_t)32 * 32 * kStemCG + (size_t)34 * 34 * 8 + 5 * kStemCG) * sizeof(float);
   static bool init = false;
   if (!init) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_bwd32_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_bwd32_kernel<T>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     init = true;
   }
+  stem_bwd32_kernel<T><<<(unsigned)(N * (64 / kStemCG)), 576, lds, s>>>(a, x, N, dw);
+}
+
+void launch_stem_bwd32(const BnBwdArgs32& a, const float* x, int N, int H, int W, int Cin, float* dw, hipStream_t s) {
   (void)H;
   (void)W;
   (void)Cin;
-  stem_bwd32_kernel<<<(unsigned)(N * (64 / kStemCG)), 576, lds, s>>>(a, x, N, dw);
+  stem_bwd_launch(a, x, N, dw, s);
+}
+
+void launch_stem_bwd_bf16(const BnBwdArgs32& a, const uint16_t* x, int N, float* dw, hipStream_t s) {
+  stem_bwd_launch(a, x, N, dw, s);
 }
 
 void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s) {

@@ -49,9 +49,10 @@ __device__ __forceinline__ float hexp(float x) { return sizeof(T) == 4 ? expf(x)
 template <typename T>
 __device__ __forceinline__ float hlog(float x) { return sizeof(T) == 4 ? logf(x) : __logf(x); }
 
-// FUSE (fp32 only): the input is relu(BN(z) + res) (HeadBn), applied as the
-// pooling loop reads it; the coefficients are derived per workgroup with
-// bn32_apply's math (bn_coef.h), workgroup 0 publishes them.
+// FUSE: the input is relu(BN(z) + res) (HeadBn; z / res / y in the model's
+// activation type T), applied as the pooling loop reads it; the coefficients
+// are derived per workgroup with bn32_apply's math (bn_coef.h), workgroup 0
+// publishes them.  bf16: the pooled value is the stored (rounded) y.
 template <typename T, bool FUSE = false>
 __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int HW, int C,
                                                    const float* __restrict__ W,
@@ -106,12 +107,15 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
         // bn32_apply's element math: fmaf(z, sc, sh) + res, then ReLU
         const int64_t o = ((int64_t)b * HW + h) * C + 8 * cg;
         float zz[8], rr[8];
-        load8(hb.z + o, zz);
-        load8(hb.res + o, rr);
+        load8(reinterpret_cast<const T*>(hb.z) + o, zz);
+        load8(reinterpret_cast<const T*>(hb.res) + o, rr);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = fmaxf(fmaf(zz[k], bc[8 * cg + k], bc[C + 8 * cg + k]) + rr[k], 0.f);
-        reinterpret_cast<float4*>(hb.y + o)[0] = make_float4(v[0], v[1], v[2], v[3]);
-        reinterpret_cast<float4*>(hb.y + o)[1] = make_float4(v[4], v[5], v[6], v[7]);
+        T* yo = reinterpret_cast<T*>(hb.y) + o;
+        Pack8 pk;
+        pack_out(v, yo, pk);
+        store8(yo, pk);
+        if constexpr (sizeof(T) == 2) unpack8(pk.h, v);
       } else {
         load8(xb + (int64_t)h * C + 8 * cg, v);
       }
@@ -204,8 +208,8 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
         for (int h = rg; h < HW; h += R) {
           const int64_t o = ((int64_t)b * HW + h) * C + 8 * cg;
           float yy[8], zz[8];
-          load8(hb.y + o, yy);
-          load8(hb.z + o, zz);
+          load8(reinterpret_cast<const T*>(hb.y) + o, yy);
+          load8(reinterpret_cast<const T*>(hb.z) + o, zz);
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             const int c = 8 * cg + k;
@@ -262,7 +266,14 @@ static void head_launch(const T* x, int B, int HW, int C, const float* W, const 
 
 void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,
                          int K, const int* labels, float* feat, float* dlogits, uint16_t* dx,
-                         float* stats, bool backward, hipStream_t s, float* dW, float* db) {
+                         float* stats, bool backward, hipStream_t s, float* dW, float* db, const HeadBn* bn) {
+  if (bn) {
+    HeadBn hb = *bn;
+    if (!backward) hb.acc_b = nullptr;
+    head_launch_t<uint16_t, true>(x, B, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, backward, s, dW, db,
+                                  hb);
+    return;
+  }
   head_launch(x, B, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, backward, s, dW, db);
 }
 void launch_head32_fwd_bwd(const float* x, int B, int HW, int C, const float* W, const float* bias, int K,

@@ -156,6 +156,8 @@ void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s);
 // x: the stem input [N][H][W][Cin] fp32.  Shapes: stem_bwd32_ok.
 bool stem_bwd32_ok(int N, int H, int W, int Cin, int Co);
 void launch_stem_bwd32(const BnBwdArgs32& a, const float* x, int N, int H, int W, int Cin, float* dw, hipStream_t s);
+// the same with the bf16 option's dy / z / y / x (a.dy, a.x, a.y point at bf16)
+void launch_stem_bwd_bf16(const BnBwdArgs32& a, const uint16_t* x, int N, float* dw, hipStream_t s);
 
 // ---- head.hip ------------------------------------------------------------
 // fp32 head whose input is relu(BN(z) + res), applied in its pooling loop
@@ -186,7 +188,7 @@ void launch_head32_fwd_bwd(const float* x, int B, int HW, int C, const float* W,
 void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,
                          int K, const int* labels, float* feat, float* dlogits, uint16_t* dx,
                          float* stats, bool backward, hipStream_t s, float* dW = nullptr,
-                         float* db = nullptr);
+                         float* db = nullptr, const HeadBn* bn = nullptr);
 void launch_head_wgrad(const float* feat, const float* dlogits, int B, int C, int K, float* dW,
                        float* db, hipStream_t s);
 

@@ -297,7 +297,8 @@ class ConvBN(Layer):
         reductions are fused into this layer's dgrad epilogue)."""
         s = self.shp
         if (STEM_FUSED and dx is None and dres is None and presummed and side is None and self.relu
-                and self.z.dtype == torch.float32 and (self.z.is_cuda or FUSED_FILL_CPU)
+                and ((self.z.dtype == torch.float32 and (self.z.is_cuda or FUSED_FILL_CPU))
+                     or (self.z.dtype == torch.bfloat16 and self.z.is_cuda))
                 and K.stem_backward_ok(s, self.z.device)):
             # no dgrad (the stem): BN backward + weight gradient in one launch
             K.stem_backward(dy, self.z, self.y, self.x, s, self.gamma, self.mean, self.invstd,
@@ -492,8 +493,9 @@ class ClassifierHead(Layer):
         self.summed_input_bn = False
         if isinstance(x, Pending):
             p = x
-            if (p.res is not None and p.zr is None and p.relu and p.z.dtype == torch.float32
-                    and (p.z.is_cuda or FUSED_FILL_CPU)):
+            if (p.res is not None and p.zr is None and p.relu
+                    and ((p.z.dtype == torch.float32 and (p.z.is_cuda or FUSED_FILL_CPU))
+                         or (p.z.dtype == torch.bfloat16 and p.z.is_cuda))):
                 lay = p.layer
                 acc_b = lay.ws.acc(lay.acc_b) if train else None
                 K.head_forward_backward_bn(self.N, self.HW, self.C, self.W, self.b, labels, self.feat, self.dlogits,
