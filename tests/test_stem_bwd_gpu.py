@@ -106,3 +106,25 @@ def test_stem_backward_accumulates_and_rejects_other_shapes():
     assert not K.stem_backward_ok(K.ConvShape(4, 16, 16, 8, 64, 3, 3, 1, 1), dev)   # 16-pixel rows
     assert not K.stem_backward_ok(K.ConvShape(4, 32, 32, 8, 64, 3, 3, 2, 1), dev)   # stride 2
 
+
+
+def test_stem_backward_fused_bf16_option():
+    """The bf16 option's tensors (dy, z, y, x bf16) through the same launch:
+    against the fp64 reference of the bf16-rounded inputs (dz and the products
+    stay fp32 inside the kernel)."""
+    from metisfl_amd.ops import nn as K
+    N = 32
+    c = _case(N, seed=77)
+    for k in ("x", "z", "y", "dy"):
+        c[k] = c[k].to(torch.bfloat16).float()  # what the kernel sees
+    shp = K.ConvShape(N, 32, 32, 8, 64, 3, 3, 1, 1)
+    d = {k: (v.to(torch.bfloat16) if k in ("x", "z", "y", "dy") else v).to(DEV) for k, v in c.items()}
+    dw = torch.zeros(64, 3, 3, 8, device=DEV)
+    dgamma = torch.zeros(64, device=DEV)
+    dbeta = torch.zeros(64, device=DEV)
+    K.stem_backward(d["dy"], d["z"], d["y"], d["x"], shp, d["gamma"], d["mean"], d["invstd"], d["acc"], dgamma,
+                    dbeta, dw)
+    torch.cuda.synchronize()
+    ref = _ref_dw(c)
+    assert _rel(dw, ref) <= 1e-5, _rel(dw, ref)
+    assert _rel(dbeta, c["tot"][0]) <= 1e-6 and _rel(dgamma, c["tot"][1]) <= 1e-6
