@@ -91,6 +91,33 @@ void gemm_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t M, 
                          stream_of(x), ws_n > 0 ? ws.data_ptr<float>() : nullptr);
 }
 
+// dw0 = dy0^T x0 and dw1 = dy1^T x1 over the same M rows, both zeroed on
+// entry, in one grouped launch (gemm_big.hip gemm_pp_group_kernel); two
+// ordinary launches where the pair does not fit it.  -> whether grouped.
+bool gemm_wgrad2(torch::Tensor x0, torch::Tensor dy0, torch::Tensor dw0, int64_t N0, int64_t K0, torch::Tensor x1,
+                 torch::Tensor dy1, torch::Tensor dw1, int64_t N1, int64_t K1, int64_t M) {
+  dense_dims(M, N0, K0);
+  dense_dims(M, N1, K1);
+  need(x0, torch::kBFloat16, M * K0, "x0");
+  need(dy0, torch::kBFloat16, M * N0, "dy0");
+  need(dw0, torch::kFloat32, N0 * K0, "dw0");
+  need(x1, torch::kBFloat16, M * K1, "x1");
+  need(dy1, torch::kBFloat16, M * N1, "dy1");
+  need(dw1, torch::kFloat32, N1 * K1, "dw1");
+  if (!mfl::gemm_big_enabled() || !mfl::gemm_big_wgrad2_ok((int)M, (int)N0, (int)K0, (int)N1, (int)K1)) {
+    gemm_wgrad(x0, dy0, dw0, M, N0, K0, false, true);
+    gemm_wgrad(x1, dy1, dw1, M, N1, K1, false, true);
+    return false;
+  }
+  const int64_t ws_n = mfl::gemm_big_wgrad2_workspace((int)M, (int)N0, (int)K0, (int)N1, (int)K1);
+  torch::Tensor ws;
+  if (ws_n > 0) ws = torch::empty({ws_n}, dw0.options());
+  mfl::launch_gemm_big_wgrad2(bfp(x0), bfp(dy0), dw0.data_ptr<float>(), (int)N0, (int)K0, bfp(x1), bfp(dy1),
+                              dw1.data_ptr<float>(), (int)N1, (int)K1, (int)M, stream_of(x0),
+                              ws_n > 0 ? ws.data_ptr<float>() : nullptr);
+  return true;
+}
+
 void ln_dims(int64_t H) {
   TORCH_CHECK(H % 256 == 0 && H <= 1024, "LayerNorm width must be 256, 512, 768 or 1024");
 }
@@ -350,6 +377,7 @@ void register_bert(pybind11::module& m) {
   m.def("gemm_dgrad", &gemm_dgrad);
   m.def("gemm_dgrad_gelu", &gemm_dgrad_gelu);
   m.def("gemm_wgrad", &gemm_wgrad);
+  m.def("gemm_wgrad2", &gemm_wgrad2);
   m.def("ln_fwd", &ln_fwd);
   m.def("emb_ln_fwd", &emb_ln_fwd);
   m.def("ln_bwd", &ln_bwd);

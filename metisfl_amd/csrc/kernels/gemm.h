@@ -43,6 +43,11 @@ void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int
                            bool accumulate, hipStream_t s, float* ws = nullptr);
 int gemm_big_wgrad_splits(int M, int N, int K);
 int64_t gemm_big_wgrad_workspace(int M, int N, int K);
+// two weight gradients over the same M in one launch (zeroed dW0 / dW1)
+bool gemm_big_wgrad2_ok(int M, int N0, int K0, int N1, int K1);
+int64_t gemm_big_wgrad2_workspace(int M, int N0, int K0, int N1, int K1);
+void launch_gemm_big_wgrad2(const uint16_t* x0, const uint16_t* dy0, float* dw0, int N0, int K0, const uint16_t* x1,
+                            const uint16_t* dy1, float* dw1, int N1, int K1, int M, hipStream_t s, float* ws);
 void launch_gemm_big_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t* dz, const uint16_t* z,
                                 float* dbias, int M, int N, int K, hipStream_t s);
 // dz[M][K] = (dy W) * gelu'(z) (exact erf), dbias[K] += column sums of dz:

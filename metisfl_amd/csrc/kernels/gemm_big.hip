@@ -557,26 +557,32 @@ __device__ __forceinline__ bf16x8 pp_frag(const uint8_t* half, int kk, int r0, i
   else return b128_frag<128>(half, kk, r0, lane);
 }
 
+// XCD-aware bijective workgroup -> tile index (tiles sharing an A row panel
+// run on one XCD's L2)
+__device__ __forceinline__ int pp_wgid() {
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// One 256 x BN output tile (wgid: its index in p's row-major tile grid) of
+// split-K slice `split`.
 template <bool AT, bool BT, bool OUT32, int BN>
-__global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
+__device__ __forceinline__ void gemm_pp_body(const BigGemmArgs& p, int wgid, int split, uint8_t* smem) {
   constexpr int BW = BN / 4;            // columns per wave
   constexpr int NJ1 = (BW - 32) / 16;   // 16-column tiles of a wave in the B1 half
   constexpr int NR1 = 4 * (BW - 32);    // B1 half-tile rows
   constexpr int VM = 6 + NR1 / 64;      // DMA instructions per wave per k-tile
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
   const int tiles_n = (p.N + BN - 1) / BN;
   const int m0 = (wgid / tiles_n) * GB_BM;
   const int n0 = (wgid - (wgid / tiles_n) * tiles_n) * BN;
   const auto rsA = make_rsrc(p.a, p.a_bytes);
   const auto rsB = make_rsrc(p.b, p.b_bytes);
-  const int kt0 = blockIdx.y * p.kt_per_split;
+  const int kt0 = split * p.kt_per_split;
   const int nk = min(p.K / 64 - kt0, p.kt_per_split);
   if (nk <= 0) return;  // block-uniform
 
@@ -710,13 +716,33 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
     // splitk_reduce_kernel): memory-side float atomics run at ~1.3 TB/s of
     // added bytes, streaming stores at ~6 (MI355X_MICROARCH 'Global float atomics')
     BigGemmArgs q = p;
-    q.c32 = p.ws + (int64_t)blockIdx.y * p.M * p.ldc;
+    q.c32 = p.ws + (int64_t)split * p.M * p.ldc;
     q.accum = 0;
     q.splits = 1;
     big_epilogue<OUT32, BW>(q, acc, smem, m0, n0, wm, wn, wave, lane);
     return;
   }
   big_epilogue<OUT32, BW>(p, acc, smem, m0, n0, wm, wn, wave, lane);
+}
+
+template <bool AT, bool BT, bool OUT32, int BN>
+__global__ __launch_bounds__(512) void gemm_pp_kernel(BigGemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  gemm_pp_body<AT, BT, OUT32, BN>(p, pp_wgid(), blockIdx.y, smem);
+}
+
+// Two independent problems of the same layout in ONE launch: workgroups
+// [0, tiles0) take p0's tiles, the rest p1's; both split their reduction into
+// gridDim.y slices.  For weight gradients with few output tiles (BERT's
+// attention-output 768 x 768 next to its QKV 2304 x 768): alone, the small one
+// needs ~28 short slices to fill the chip; together both run a handful of
+// long ones, and the split-K slabs shrink with the slice count.
+template <bool AT, bool BT, bool OUT32, int BN>
+__global__ __launch_bounds__(512) void gemm_pp_group_kernel(BigGemmArgs p0, BigGemmArgs p1, int tiles0) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int w = pp_wgid();
+  if (w < tiles0) gemm_pp_body<AT, BT, OUT32, BN>(p0, w, blockIdx.y, smem);
+  else gemm_pp_body<AT, BT, OUT32, BN>(p1, w - tiles0, blockIdx.y, smem);
 }
 
 // out (+)= sum over the split-K slabs, 16 B per lane
@@ -744,6 +770,21 @@ void launch_pp_t(const BigGemmArgs& p, hipStream_t s) {
   }
   const dim3 grid((unsigned)(((p.M + GB_BM - 1) / GB_BM) * ((p.N + BN - 1) / BN)), (unsigned)p.splits);
   gemm_pp_kernel<AT, BT, OUT32, BN><<<grid, 512, kLds, s>>>(p);
+}
+
+template <bool AT, bool BT, bool OUT32, int BN>
+void launch_pp_group_t(const BigGemmArgs& p0, const BigGemmArgs& p1, hipStream_t s) {
+  constexpr size_t kLds = 8 * (size_t)PP_HALF;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_group_kernel<AT, BT, OUT32, BN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds);
+    attr = true;
+  }
+  const int t0 = ((p0.M + GB_BM - 1) / GB_BM) * ((p0.N + BN - 1) / BN);
+  const int t1 = ((p1.M + GB_BM - 1) / GB_BM) * ((p1.N + BN - 1) / BN);
+  const dim3 grid((unsigned)(t0 + t1), (unsigned)p0.splits);
+  gemm_pp_group_kernel<AT, BT, OUT32, BN><<<grid, 512, kLds, s>>>(p0, p1, t0);
 }
 
 // Tile width for the ping-pong kernel: 192 when it needs fewer workgroup
@@ -891,6 +932,54 @@ void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int
     return;
   }
   launch_big<true, true, true>(p, M, s);
+}
+
+// Two weight gradients with the same reduction length M in one launch
+// (gemm_pp_group_kernel): dW0[N0][K0] = dY0^T X0, dW1[N1][K1] = dY1^T X1, both
+// dW zero on entry.  ws: split-K slabs of splits * (N0 K0 + N1 K1) floats
+// (gemm_big_wgrad2_workspace).  Falls back to two launches when the pair does
+// not fit the grouped kernel (shapes off the 256 grid, other pipelines).
+int gemm_big_wgrad2_splits(int M, int N0, int K0, int N1, int K1) {
+  const int tiles = (N0 / GB_BM) * (K0 / GB_BN) + (N1 / GB_BM) * (K1 / GB_BN);
+  return std::max(1, std::min(256 / std::max(1, tiles), (M / GB_KQ) / 16));
+}
+
+bool gemm_big_wgrad2_ok(int M, int N0, int K0, int N1, int K1) {
+  return (gb_pipe() == 2 || gb_pipe() == 3) && M % GB_KQ == 0 && N0 % GB_BM == 0 && K0 % GB_BN == 0 &&
+         N1 % GB_BM == 0 && K1 % GB_BN == 0 && gemm_big_ok(N0, K0, M) && gemm_big_ok(N1, K1, M);
+}
+
+int64_t gemm_big_wgrad2_workspace(int M, int N0, int K0, int N1, int K1) {
+  if (!gemm_big_wgrad2_ok(M, N0, K0, N1, K1)) return 0;
+  const int sp = gemm_big_wgrad2_splits(M, N0, K0, N1, K1);
+  return sp > 1 ? (int64_t)sp * ((int64_t)N0 * K0 + (int64_t)N1 * K1) : 0;
+}
+
+void launch_gemm_big_wgrad2(const uint16_t* x0, const uint16_t* dy0, float* dw0, int N0, int K0, const uint16_t* x1,
+                            const uint16_t* dy1, float* dw1, int N1, int K1, int M, hipStream_t s, float* ws) {
+  auto args = [&](const uint16_t* x, const uint16_t* dy, float* dw, int N, int K, int sp) {
+    BigGemmArgs p{};
+    p.a = dy; p.b = x; p.M = N; p.N = K; p.K = M; p.lda = N; p.ldb = K;
+    p.a_bytes = (uint32_t)((int64_t)M * N * 2); p.b_bytes = (uint32_t)((int64_t)M * K * 2);
+    p.c32 = dw; p.ldc = K; p.accum = 0;
+    p.splits = sp;
+    p.kt_per_split = (M / GB_KQ + sp - 1) / sp;
+    return p;
+  };
+  const int sp = gemm_big_wgrad2_splits(M, N0, K0, N1, K1);
+  BigGemmArgs p0 = args(x0, dy0, dw0, N0, K0, sp), p1 = args(x1, dy1, dw1, N1, K1, sp);
+  if (sp > 1) {
+    p0.ws = ws;
+    p1.ws = ws + (int64_t)sp * N0 * K0;
+  }
+  launch_pp_group_t<true, true, true, 256>(p0, p1, s);
+  if (sp > 1) {
+    const int64_t n0 = (int64_t)N0 * K0 / 4, n1 = (int64_t)N1 * K1 / 4;
+    splitk_reduce_kernel<<<stream_grid(n0, 256, 2048), 256, 0, s>>>(reinterpret_cast<const float4*>(p0.ws), sp, n0,
+                                                                     reinterpret_cast<float4*>(dw0), 0);
+    splitk_reduce_kernel<<<stream_grid(n1, 256, 2048), 256, 0, s>>>(reinterpret_cast<const float4*>(p1.ws), sp, n1,
+                                                                     reinterpret_cast<float4*>(dw1), 0);
+  }
 }
 
 // Few output tiles, long reduction: split M so that tiles * slices fills ONE

@@ -21,6 +21,8 @@ and 12 backward launches.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import numpy as np
@@ -32,6 +34,11 @@ from metisfl_amd.ops import bert as BO
 from metisfl_amd.ops import nn as K
 from metisfl_amd.ops import optim as opt_ops
 from metisfl_amd.ops.optim import OptimizerSpec
+
+
+# attention-output + QKV weight gradients grouped in one launch (MFL_BERT_WGRAD2=0:
+# two launches, for A/B runs)
+WGRAD2 = os.environ.get("MFL_BERT_WGRAD2", "1") == "1"
 
 
 @dataclass
@@ -233,11 +240,19 @@ class BertMLM(StaticNet):
             BO.gemm_dgrad(self.g_z, self._w(p + "ffn1.w"), self.g_a, M, F, H, accumulate=True)
             BO.ln_bwd(self.g_a, A["ao"], A["m1"], A["r1"], self._p(p + "ln1.gamma"), self.g_ao, g(p + "ln1.gamma"),
                       g(p + "ln1.beta"), M, H, dx2=dx, dbias_prev=g(p + "out.b"))
-            BO.gemm_wgrad(A["ctx"], self.g_ao, g(p + "out.w"), M, H, H, zeroed=True)
+            if not WGRAD2:
+                BO.gemm_wgrad(A["ctx"], self.g_ao, g(p + "out.w"), M, H, H, zeroed=True)
             BO.gemm_dgrad(self.g_ao, self._w(p + "out.w"), self.g_ctx, M, H, H)
             BO.attn_bwd(A["qkv"], A["ctx"], A["lse"], self.g_ctx, self.g_qkv, B, c.heads, scale,
                         dbias=g(p + "qkv.b"))
-            BO.gemm_wgrad(A["x"], self.g_qkv, g(p + "qkv.w"), M, 3 * H, H, zeroed=True)
+            if WGRAD2:
+                # the attention-output and QKV weight gradients in one grouped
+                # launch: alone the 768 x 768 one needs ~28 short split-K
+                # slices to fill the chip (gemm_big.hip gemm_pp_group_kernel)
+                BO.gemm_wgrad2(A["ctx"], self.g_ao, g(p + "out.w"), H, H, A["x"], self.g_qkv, g(p + "qkv.w"),
+                               3 * H, H, M)
+            else:
+                BO.gemm_wgrad(A["x"], self.g_qkv, g(p + "qkv.w"), M, 3 * H, H, zeroed=True)
             BO.gemm_dgrad(self.g_qkv, self._w(p + "qkv.w"), dx, M, 3 * H, H, accumulate=True)
             dout = dx
         BO.emb_ln_bwd(dout, self.emb_x, self.emb_mean, self.emb_rstd, self._p("emb.ln.gamma"), self.rec,

@@ -83,6 +83,17 @@ def gemm_wgrad(x, dy, dw, M, N, K, accumulate=False, zeroed=False) -> None:
         dw.copy_(v.reshape(dw.shape))
 
 
+def gemm_wgrad2(x0, dy0, dw0, N0, K0, x1, dy1, dw1, N1, K1, M) -> bool:
+    """dw0 = dy0^T x0 and dw1 = dy1^T x1 (fp32, both zero on entry) over the
+    same M rows in ONE grouped launch on the GPU (gemm_big.hip
+    gemm_pp_group_kernel) -> whether it was grouped."""
+    if x0.is_cuda:
+        return bool(ops().gemm_wgrad2(x0, dy0, dw0, N0, K0, x1, dy1, dw1, N1, K1, M))
+    gemm_wgrad(x0, dy0, dw0, M, N0, K0)
+    gemm_wgrad(x1, dy1, dw1, M, N1, K1)
+    return False
+
+
 # ---- LayerNorm ----------------------------------------------------------------
 def _ln_ref(x, gamma, beta, eps):
     mean = x.mean(-1)
