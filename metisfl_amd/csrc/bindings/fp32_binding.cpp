@@ -207,9 +207,52 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
                           int64_t R, int64_t S, int64_t stride, int64_t pad, bool accumulate,
                           c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
                           c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
-                          c10::optional<torch::Tensor> bn_acc, c10::optional<torch::Tensor> wp) {
+                          c10::optional<torch::Tensor> bn_acc, c10::optional<torch::Tensor> wp,
+                          c10::optional<torch::Tensor> opt_p, c10::optional<torch::Tensor> opt_g,
+                          c10::optional<torch::Tensor> opt_m, c10::optional<torch::Tensor> opt_v,
+                          c10::optional<torch::Tensor> opt_anchor, c10::optional<torch::Tensor> opt_mirror,
+                          c10::optional<torch::Tensor> opt_lr_scale, c10::optional<torch::Tensor> opt_step,
+                          int64_t opt_mode, std::vector<double> opt_hyper, bool opt_zero_grad) {
   const auto gf = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
   const auto gd = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
+  // optimizer tail (conv32.h OptTail): a flat-model range whose gradients are
+  // final, updated by extra workgroups of this launch
+  mfl::OptTail ot;
+  const bool tail = opt_p.has_value() && opt_p->defined();
+  if (tail) {
+    const int64_t n = opt_p->numel();
+    check_f32(*opt_p, n, "opt p");
+    TORCH_CHECK(n % 4 == 0 && (reinterpret_cast<uintptr_t>(opt_p->data_ptr()) & 15) == 0, "opt range: 16-B float4s");
+    TORCH_CHECK(opt_hyper.size() == 9, "opt hyper: lr l1 l2 momentum mu beta1 beta2 eps wd");
+    auto same = [&](const c10::optional<torch::Tensor>& t, const char* nm) -> float* {
+      if (!(t.has_value() && t->defined())) return nullptr;
+      TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->numel() == n, "opt ", nm, " range");
+      return reinterpret_cast<float*>(t->data_ptr());
+    };
+    ot.p = fp(*opt_p);
+    ot.g = same(opt_g, "g");
+    TORCH_CHECK(ot.g != nullptr, "opt tail needs the gradient range");
+    ot.m = same(opt_m, "m");
+    ot.v = same(opt_v, "v");
+    ot.anchor = same(opt_anchor, "anchor");
+    ot.mirror = same(opt_mirror, "mirror");
+    TORCH_CHECK(!ot.mirror || opt_mirror->scalar_type() == torch::kInt32, "opt tail mirror: the packed split");
+    ot.mirror_kind = ot.mirror ? 2 : 0;
+    ot.mode = (int)opt_mode;
+    TORCH_CHECK(ot.mode != mfl::OPT_MOMENTUM || ot.m, "momentum buffer");
+    TORCH_CHECK(ot.mode != mfl::OPT_FEDPROX || ot.anchor, "proximal anchor");
+    TORCH_CHECK((ot.mode != mfl::OPT_ADAM && ot.mode != mfl::OPT_ADAMW) || (ot.m && ot.v), "adam slots");
+    ot.h.lr = (float)opt_hyper[0]; ot.h.l1 = (float)opt_hyper[1]; ot.h.l2 = (float)opt_hyper[2];
+    ot.h.momentum = (float)opt_hyper[3]; ot.h.mu = (float)opt_hyper[4]; ot.h.beta1 = (float)opt_hyper[5];
+    ot.h.beta2 = (float)opt_hyper[6]; ot.h.eps = (float)opt_hyper[7]; ot.h.wd = (float)opt_hyper[8];
+    ot.lr_ptr = opt_lr_scale.has_value() && opt_lr_scale->defined() ? fp(*opt_lr_scale) : nullptr;
+    ot.step_ptr = opt_step.has_value() && opt_step->defined() ? opt_step->data_ptr<int>() : nullptr;
+    ot.zero_grad = opt_zero_grad ? 1 : 0;
+    ot.n4 = n / 4;
+    // ~4 float4 per thread: enough workgroups to stream at full rate, few
+    // enough to land in the GEMMs' tail
+    ot.nblk = (int)std::max<int64_t>(16, std::min<int64_t>(256, ot.n4 / (256 * 4)));
+  }
   torch::Tensor xtmp, dtmp;
   const float* xs = dysrc(x, (int64_t)N * H * W * C, xtmp, "x");
   const float* dyp = dysrc(dy, (int64_t)gf.M * Co, dtmp);
@@ -244,11 +287,15 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
   torch::Tensor tmp;
   const float* wb = wsrc(w, wp, tmp);
   if (C32_CALL(launch_conv32_bwd_pair, gd, pd, gf, pw, dyp, wb, fp(dx), slab, counters, accumulate,
-                                  fuse ? &f : nullptr, xs, fp(dw), cur_stream(dx)))
+                                  fuse ? &f : nullptr, xs, fp(dw), cur_stream(dx), tail ? &ot : nullptr))
     return;
   C32_CALL(launch_conv32_wgrad, gf, pw, xs, dyp, fp(dw), true, cur_stream(dw));
   C32_CALL(launch_conv32_gemm, gd, true, pd, dyp, wb, fp(dx), slab, counters, nullptr, accumulate,
                           fuse ? &f : nullptr, cur_stream(dx));
+  if (tail)  // the pair did not launch: the range's optimizer as its own launch
+    mfl::launch_fused_optimizer(ot.mode, ot.p, ot.g, ot.m, ot.v, ot.anchor, ot.mirror, ot.n4 * 4, ot.h, ot.lr_ptr,
+                                ot.step_ptr, ot.zero_grad != 0, nullptr, 0, cur_stream(dx), nullptr,
+                                ot.mirror_kind);
 }
 
 void conv32_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t N, int64_t H, int64_t W, int64_t C,
@@ -395,12 +442,14 @@ void conv32_forward_pair(torch::Tensor x, torch::Tensor w1, torch::Tensor y1, c1
   run(g2, false, xs, wb2, y2, ws2, st2, false, nullptr, r2);
 }
 
-void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,
-                        torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd, torch::Tensor acc,
-                        c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor dx,
-                        c10::optional<torch::Tensor> dy_masked, bool presummed, c10::optional<torch::Tensor> z2,
-                        c10::optional<torch::Tensor> mean2, c10::optional<torch::Tensor> invstd2,
-                        c10::optional<torch::Tensor> acc2) {
+// Validated BN-backward apply arguments (and, unless presummed, the reduce
+// launch that completes `acc` first).
+static mfl::BnBwdArgs32 bn32_bwd_args(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,
+                                      torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd, torch::Tensor acc,
+                                      c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta,
+                                      torch::Tensor dx, c10::optional<torch::Tensor> dy_masked, bool presummed,
+                                      c10::optional<torch::Tensor> z2, c10::optional<torch::Tensor> mean2,
+                                      c10::optional<torch::Tensor> invstd2, c10::optional<torch::Tensor> acc2) {
   check_nhwc32(dy, C);
   check_nhwc32(x, C);
   // an int32 dx receives the packed bf16x3 split of the gradient: the dY
@@ -452,10 +501,37 @@ void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::
     a.acc2 = const_cast<double*>(acc_ptr(*acc2, C));
     a.reps2 = reps_of(*acc2, C);
   }
-  auto s = cur_stream(x);
   if (!presummed)
-    mfl::launch_bn32_bwd_reduce(a.dy, a.x, a.y, a.mean, a.invstd, a.M, a.C, acc.data_ptr<double>(), s, a.reps);
-  mfl::launch_bn32_bwd_apply(a, s);
+    mfl::launch_bn32_bwd_reduce(a.dy, a.x, a.y, a.mean, a.invstd, a.M, a.C, acc.data_ptr<double>(), cur_stream(x),
+                                a.reps);
+  return a;
+}
+
+void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C,
+                        torch::Tensor gamma, torch::Tensor mean, torch::Tensor invstd, torch::Tensor acc,
+                        c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor dx,
+                        c10::optional<torch::Tensor> dy_masked, bool presummed, c10::optional<torch::Tensor> z2,
+                        c10::optional<torch::Tensor> mean2, c10::optional<torch::Tensor> invstd2,
+                        c10::optional<torch::Tensor> acc2) {
+  const auto a = bn32_bwd_args(dy, x, y, C, gamma, mean, invstd, acc, dgamma, dbeta, dx, dy_masked, presummed, z2,
+                               mean2, invstd2, acc2);
+  mfl::launch_bn32_bwd_apply(a, cur_stream(x));
+}
+
+// Two presummed BN-backward applies in one launch (bn32.hip
+// bn32_bwd_apply_pair_kernel): role 1 with its ReLU mask y1 (a downsampling
+// block's conv1), role 2 without (its projection shortcut).
+void bn32_backward_pair(torch::Tensor dy1, torch::Tensor x1, torch::Tensor y1, int64_t C1, torch::Tensor gamma1,
+                        torch::Tensor mean1, torch::Tensor invstd1, torch::Tensor acc1, torch::Tensor dgamma1,
+                        torch::Tensor dbeta1, torch::Tensor dx1, torch::Tensor dy2, torch::Tensor x2, int64_t C2,
+                        torch::Tensor gamma2, torch::Tensor mean2, torch::Tensor invstd2, torch::Tensor acc2,
+                        torch::Tensor dgamma2, torch::Tensor dbeta2, torch::Tensor dx2) {
+  const auto a1 = bn32_bwd_args(dy1, x1, y1, C1, gamma1, mean1, invstd1, acc1, dgamma1, dbeta1, dx1, c10::nullopt,
+                                true, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt);
+  const auto a2 = bn32_bwd_args(dy2, x2, c10::nullopt, C2, gamma2, mean2, invstd2, acc2, dgamma2, dbeta2, dx2,
+                                c10::nullopt, true, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt);
+  TORCH_CHECK(a1.pack_dx == a2.pack_dx, "bn backward pair: both dx packed or both fp32");
+  mfl::launch_bn32_bwd_apply_pair(a1, a2, cur_stream(x1));
 }
 
 void bn32_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> y, int64_t C, torch::Tensor gamma,
@@ -656,6 +732,7 @@ void register_fp32(pybind11::module& m) {
   m.def("conv32_forward_pair", &conv32_forward_pair);
   m.def("bn32_backward", &bn32_backward);
   m.def("bn32_backward_side", &bn32_backward_side);
+  m.def("bn32_backward_pair", &bn32_backward_pair);
   m.def("stem_backward32", &stem_backward32);
   m.def("stem_backward32_ok", &stem_backward32_ok);
   m.def("head32_forward_backward", &head32_forward_backward);

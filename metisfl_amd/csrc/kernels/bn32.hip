@@ -219,16 +219,18 @@ void launch_bn32_bwd_reduce(const float* dy, const float* x, const float* y, con
                                                                       reps > 0 ? reps : 1);
 }
 
-// Backward apply: dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat))
+// Backward apply: dx = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)).
+// Workgroup `bid` of `nblk` (a stand-alone launch, or one role of a paired
+// launch); sc: [5][C] floats of LDS (k1, mean g, mean g*xh, mean, invstd).
 template <bool MASK, bool WRITE_DYM>
-__global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int64_t nvec) {
-  extern __shared__ __attribute__((aligned(16))) float sc[];  // [5][C]: k1, mean g, mean g*xh, mean, invstd
+__device__ __forceinline__ void bn32_bwd_apply_body(const BnBwdArgs32& a, int64_t nvec, int bid, int nblk,
+                                                    float* sc) {
   const int C = a.C;
   const float4* DY = reinterpret_cast<const float4*>(a.dy);
   const float4* X = reinterpret_cast<const float4*>(a.x);
   const float4* Y = reinterpret_cast<const float4*>(a.y);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)nblk * blockDim.x;
+  int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
   float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), xv = gv, yv = gv;
   if (i < nvec) {
     gv = DY[i];
@@ -244,7 +246,7 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
     sc[2 * C + c] = (float)(q * inv_m);
     sc[3 * C + c] = a.mean[c];
     sc[4 * C + c] = a.invstd[c];
-    if (blockIdx.x == 0) {
+    if (bid == 0) {
       if (a.dgamma) a.dgamma[c] = (float)q;
       if (a.dbeta) a.dbeta[c] = (float)s;
     }
@@ -308,8 +310,26 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
   }
   if (side) {
     __syncthreads();  // sc[] reads done before channel_atomic4's LDS staging
-    channel_atomic4(s2, q2, C, tpr, 256 / tpr, a.acc2 + (int64_t)(blockIdx.x % a.reps2) * 2 * C);
+    channel_atomic4(s2, q2, C, tpr, 256 / tpr, a.acc2 + (int64_t)(bid % a.reps2) * 2 * C);
   }
+}
+
+template <bool MASK, bool WRITE_DYM>
+__global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int64_t nvec) {
+  extern __shared__ __attribute__((aligned(16))) float sc[];
+  bn32_bwd_apply_body<MASK, WRITE_DYM>(a, nvec, blockIdx.x, gridDim.x, sc);
+}
+
+// A downsampling block's conv1 BatchNorm (ReLU) and projection-shortcut
+// BatchNorm (no ReLU) backward applies in one launch: both sums are complete
+// once conv2's backward has run (conv1's from conv2's dgrad epilogue, the
+// shortcut's from conv2's BN-backward side reduction), so the two
+// bandwidth-bound passes share one launch instead of two dependent ones.
+__global__ __launch_bounds__(256) void bn32_bwd_apply_pair_kernel(BnBwdArgs32 a1, int64_t n1, int g1,
+                                                                  BnBwdArgs32 a2, int64_t n2) {
+  extern __shared__ __attribute__((aligned(16))) float sc[];
+  if ((int)blockIdx.x < g1) bn32_bwd_apply_body<true, false>(a1, n1, blockIdx.x, g1, sc);
+  else bn32_bwd_apply_body<false, false>(a2, n2, blockIdx.x - g1, gridDim.x - g1, sc);
 }
 
 // ---------------------------------------------------------------------------
@@ -496,6 +516,13 @@ void launch_stem_bwd32(const BnBwdArgs32& a, const float* x, int N, int H, int W
 
 void launch_stem_bwd_bf16(const BnBwdArgs32& a, const uint16_t* x, int N, float* dw, hipStream_t s) {
   stem_bwd_launch(a, x, N, dw, s);
+}
+
+void launch_bn32_bwd_apply_pair(const BnBwdArgs32& a1, const BnBwdArgs32& a2, hipStream_t s) {
+  const int64_t n1 = a1.M * a1.C / 4, n2 = a2.M * a2.C / 4;
+  const unsigned g1 = apply_grid(n1), g2 = apply_grid(n2);
+  const size_t sm = 5 * (size_t)(a1.C > a2.C ? a1.C : a2.C) * sizeof(float);
+  bn32_bwd_apply_pair_kernel<<<g1 + g2, 256, sm, s>>>(a1, n1, (int)g1, a2, n2);
 }
 
 void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s) {

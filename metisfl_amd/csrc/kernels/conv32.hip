@@ -54,6 +54,7 @@
 
 #include "kernels/common.h"
 #include "kernels/conv32.h"
+#include "kernels/opt_body.h"
 #include "kernels/lds_tiles.h"
 
 // Built twice (csrc/build.py): MFL_C32_BF16X3=0 -> namespace mfl::c32x (exact
@@ -947,12 +948,42 @@ __global__ __launch_bounds__(256, 2) void conv32_fwd_pair_kernel(Conv32Args a1, 
   }
 }
 
+// The optimizer tail's grid-stride pass over its range (workgroup t of n).
+template <int MODE, int MIRROR>
+__device__ __forceinline__ void opt_tail_loop(const OptTail& o, int t, int n, float lr, float bc1, float bc2) {
+  const int64_t stride = (int64_t)n * 256;
+  for (int64_t i = (int64_t)t * 256 + threadIdx.x; i < o.n4; i += stride)
+    opt_update4<MODE, MIRROR>(o.p, o.g, o.m, o.v, o.anchor, o.mirror, i, o.h, lr, bc1, bc2, o.zero_grad != 0);
+}
+template <int MIRROR>
+__device__ __forceinline__ void opt_tail_mirror(const OptTail& o, int t, int n) {
+  const float lr = o.lr_ptr ? o.lr_ptr[0] * o.h.lr : o.h.lr;
+  float bc1, bc2;
+  opt_bias_corr(o.mode, o.h, o.step_ptr, bc1, bc2);
+  switch (o.mode) {
+    case OPT_SGD: opt_tail_loop<OPT_SGD, MIRROR>(o, t, n, lr, bc1, bc2); break;
+    case OPT_MOMENTUM: opt_tail_loop<OPT_MOMENTUM, MIRROR>(o, t, n, lr, bc1, bc2); break;
+    case OPT_FEDPROX: opt_tail_loop<OPT_FEDPROX, MIRROR>(o, t, n, lr, bc1, bc2); break;
+    case OPT_ADAM: opt_tail_loop<OPT_ADAM, MIRROR>(o, t, n, lr, bc1, bc2); break;
+    default: opt_tail_loop<OPT_ADAMW, MIRROR>(o, t, n, lr, bc1, bc2); break;
+  }
+}
+__device__ __forceinline__ void opt_tail_body(const OptTail& o, int t) {
+  if (o.mirror_kind == 2) opt_tail_mirror<2>(o, t, o.nblk);
+  else opt_tail_mirror<0>(o, t, o.nblk);
+}
+
 template <int KS, int ST, bool PAR, int NS>
 __global__ __launch_bounds__(256, 2) void conv32_bwd_pair_kernel(Conv32Args ad, Conv32Args aw, float* __restrict__ dw,
                                                                  int atomic, int nd, int gdx, int gdy, int gwx,
-                                                                 int gwy, int gwz) {
+                                                                 int gwy, int gwz, OptTail ot) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = xcd_group(blockIdx.x, gridDim.x);
+  const int nconv = (int)gridDim.x - ot.nblk;
+  if (b >= nconv) {  // optimizer tail (dispatched last: it fills the GEMMs' tail)
+    opt_tail_body(ot, b - nconv);
+    return;
+  }
   if (b < nd) {
     const Blk k{b % gdx, (b / gdx) % gdy, b / (gdx * gdy), gdx, gdy, nd / (gdx * gdy)};
     conv32_gemm_body<64, 64, true, KS, ST, PAR, NS, false>(ad, k, smem);
@@ -1297,7 +1328,8 @@ void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, c
 
 bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGeom& gf, const ConvPlan& pw,
                             const float* dy, const float* w, float* dx, float* ysplit, int* counters, bool accum,
-                            const BnBwdFusion32* bnb, const float* x, float* dw, hipStream_t s) {
+                            const BnBwdFusion32* bnb, const float* x, float* dw, hipStream_t s,
+                            const OptTail* ot) {
   if (env_int("MFL_C32_PAIR", 1) == 0) return false;
   const bool par = pd.par_mc != 0;
   if (pd.bm != 64 || pd.bn != 64 || pw.bm != 64 || pw.bn != 64) return false;
@@ -1308,14 +1340,19 @@ bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGe
   const Conv32Args aw = wgrad_args(gf, pw, x, dy);
   const int gdx = cdiv(gd.M, 64), gdy = cdiv(gd.Ng, 64), nd = gdx * gdy * pd.splits;
   const int gwx = cdiv(gf.Ng, 64), gwy = cdiv(gf.K, 64), gwz = pw.splits;
-  const int nblk = nd + gwx * gwy * gwz;
+  const OptTail tail = ot ? *ot : OptTail{};
+  const int nblk = nd + gwx * gwy * gwz + tail.nblk;
   const size_t lds = std::max(gemm_lds(64, 64), (size_t)stages_for(64, 64) * kBK * (64 + 64) * 4);
   constexpr int NS = stages_for(64, 64);
+  // dw is zero on entry (the step's gradient buffer): an unsplit weight
+  // gradient (ResNet-18's 512-channel stage) owns every element it writes, so
+  // it stores instead of adding atomically (MFL_C32_WSTORE=0: always atomics)
+  const int wg_atomic = (pw.splits > 1 || env_int("MFL_C32_WSTORE", 1) == 0) ? 1 : 0;
   auto go = [&](auto kern) {
     static_assert(NS >= 2, "ring");
     if (lds > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    kern<<<nblk, 256, lds, s>>>(ad, aw, dw, 1, nd, gdx, gdy, gwx, gwy, gwz);
+    kern<<<nblk, 256, lds, s>>>(ad, aw, dw, wg_atomic, nd, gdx, gdy, gwx, gwy, gwz, tail);
   };
   if (gd.R == 3 && gd.stride == 1) go(conv32_bwd_pair_kernel<3, 1, false, NS>);
   else if (gd.R == 1 && gd.stride == 1) go(conv32_bwd_pair_kernel<1, 1, false, NS>);

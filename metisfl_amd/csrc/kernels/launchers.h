@@ -150,6 +150,7 @@ void launch_bn32_apply_pair(const BnFwdArgs32& a1, const BnFwdArgs32& a2, hipStr
 void launch_bn32_bwd_reduce(const float* dy, const float* x, const float* y, const float* mean,
                             const float* invstd, int64_t M, int C, double* acc, hipStream_t s, int reps = 1);
 void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s);
+void launch_bn32_bwd_apply_pair(const BnBwdArgs32& a1, const BnBwdArgs32& a2, hipStream_t s);
 // The stem's backward in one launch: its BatchNorm(+ReLU) backward (dz, as
 // bn32_bwd_apply, never written out) and the 3x3 / stride-1 weight gradient
 // dw[Co][3][3][Cin] += sum_p dz[p] x[p + tap] (exact fp32 FMAs).  a.dx: unused;

@@ -13,6 +13,7 @@
 // the community model the learner received this round, not a zero slot.
 #include "kernels/common.h"
 #include "kernels/launchers.h"
+#include "kernels/opt_body.h"
 
 namespace mfl {
 
@@ -26,72 +27,13 @@ __global__ __launch_bounds__(256) void fused_opt_kernel(
     const float* __restrict__ lr_ptr, const int* __restrict__ step_ptr, int zero_grad,
     uint4* __restrict__ zero, int64_t zero16, int* __restrict__ tick_step) {
   const float lr = lr_ptr ? lr_ptr[0] * h.lr : h.lr;
-  float bc1 = 1.f, bc2 = 1.f;
-  if (MODE == OPT_ADAM || MODE == OPT_ADAMW) {
-    const float t = (float)(step_ptr ? step_ptr[0] + 1 : 1);
-    bc1 = 1.f - powf(h.beta1, t);
-    bc2 = 1.f - powf(h.beta2, t);
-  }
+  float bc1, bc2;
+  opt_bias_corr(MODE, h, step_ptr, bc1, bc2);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int64_t i = tid; i < zero16; i += stride) zero[i] = make_uint4(0, 0, 0, 0);
-  for (int64_t i = tid; i < n4; i += stride) {
-    float4 pv = reinterpret_cast<float4*>(p)[i];
-    const float4 gv = reinterpret_cast<const float4*>(g)[i];
-    if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    float* pp = &pv.x;
-    const float* gg = &gv.x;
-    if (MODE == OPT_SGD) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float gr = gg[k] + h.l2 * pp[k];
-        if (h.l1 != 0.f) gr += h.l1 * ((pp[k] > 0.f) - (pp[k] < 0.f));
-        pp[k] -= lr * gr;
-      }
-    } else if (MODE == OPT_MOMENTUM) {
-      // Keras SGD(momentum) form: v = mu*v - lr*g ; p += v
-      float4 mv = reinterpret_cast<float4*>(m)[i];
-      float* mm = &mv.x;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        mm[k] = h.momentum * mm[k] - lr * gg[k];
-        pp[k] += mm[k];
-      }
-      reinterpret_cast<float4*>(m)[i] = mv;
-    } else if (MODE == OPT_FEDPROX) {
-      const float4 av = reinterpret_cast<const float4*>(anchor)[i];
-      const float* aa = &av.x;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) pp[k] -= lr * (gg[k] + h.mu * (pp[k] - aa[k]));
-    } else {  // Adam / AdamW
-      float4 mv = reinterpret_cast<float4*>(m)[i];
-      float4 vv = reinterpret_cast<float4*>(v)[i];
-      float* mm = &mv.x;
-      float* vq = &vv.x;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        mm[k] = h.beta1 * mm[k] + (1.f - h.beta1) * gg[k];
-        vq[k] = h.beta2 * vq[k] + (1.f - h.beta2) * gg[k] * gg[k];
-        const float mh = mm[k] / bc1;
-        const float vh = vq[k] / bc2;
-        float upd = mh / (sqrtf(vh) + h.eps);
-        if (MODE == OPT_ADAMW) upd += h.wd * pp[k];
-        pp[k] -= lr * upd;
-      }
-      reinterpret_cast<float4*>(m)[i] = mv;
-      reinterpret_cast<float4*>(v)[i] = vv;
-    }
-    reinterpret_cast<float4*>(p)[i] = pv;
-    if (MIRROR == 1) {
-      uint2 o;
-      o.x = pack2bf(pp[0], pp[1]);
-      o.y = pack2bf(pp[2], pp[3]);
-      reinterpret_cast<uint2*>(mirror)[i] = o;
-    } else if (MIRROR == 2) {
-      reinterpret_cast<uint4*>(mirror)[i] = make_uint4(split_pack(pp[0]), split_pack(pp[1]), split_pack(pp[2]),
-                                                       split_pack(pp[3]));
-    }
-  }
+  for (int64_t i = tid; i < n4; i += stride)
+    opt_update4<MODE, MIRROR>(p, g, m, v, anchor, mirror, i, h, lr, bc1, bc2, zero_grad != 0);
   // the step-counter increment that used to be its own launch; these modes
   // never read the counter, so one lane bumps it (Adam / AdamW read it in
   // every block: their launcher ticks in a separate launch -- a last-block

@@ -172,15 +172,35 @@ class FlatState:
             self.anchor = self.params32.clone()
 
     def optimizer_step(self, zero_grad: bool = True, zero_region: torch.Tensor | None = None,
-                       tick: bool = False) -> bool:
-        """One fused optimizer launch; ``tick``: it also increments the step
-        counter (returns False when no launch happened -- the caller ticks)."""
+                       tick: bool = False, hi: int | None = None) -> bool:
+        """One fused optimizer launch over the trainables [0, hi) (default:
+        all; the rest was updated by optimizer tails); ``tick``: it also
+        increments the step counter (returns False when no launch happened --
+        the caller ticks)."""
         if self.n_params == 0 or self.optimizer is None:
             return False
-        opt_ops.fused_step(self.optimizer, self.params32, self.grad32, self.m, self.v, self.anchor,
-                           self.p16 if self.p16 is not None else self.psplit, self.lr_scale, self.step,
+        r = self.opt_range(0, self.n_params if hi is None else hi, zero_grad)
+        opt_ops.fused_step(self.optimizer, r.p, r.g, r.m, r.v, r.anchor, r.mirror, self.lr_scale, self.step,
                            zero_grad, zero_region, tick)
         return True
+
+    def opt_range(self, lo: int, hi: int, zero_grad: bool = True) -> "opt_ops.OptRange":
+        """The optimizer step over trainables [lo, hi) (multiples of ALIGN)."""
+        assert 0 <= lo <= hi <= self.n_params and lo % ALIGN == 0 and (hi % ALIGN == 0 or hi == self.n_params)
+
+        def part(t):
+            return None if t is None else t[lo:hi]
+        mirror = self.p16 if self.p16 is not None else self.psplit
+        return opt_ops.OptRange(self.optimizer, part(self.params32), part(self.grad32), part(self.m), part(self.v),
+                                part(self.anchor), part(mirror), self.lr_scale, self.step, zero_grad)
+
+    def offset_of_prefix(self, prefix: str) -> int | None:
+        """Offset of the first trainable variable whose name starts with
+        ``prefix`` (trainables are laid out in layer order), or None."""
+        for s in self.specs:
+            if s.trainable and s.name.startswith(prefix):
+                return s.offset
+        return None
 
     def set_anchor(self) -> None:
         """Snapshot the received community model as the FedProx anchor."""

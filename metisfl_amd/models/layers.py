@@ -24,6 +24,41 @@ from metisfl_amd.ops import nn as K
 from metisfl_amd.ops.nn import ConvShape
 
 
+class OptTailScheduler:
+    """Optimizer tails for one training step (see ops.optim.OptRange,
+    conv32.h OptTail).  The flat buffer holds the trainable variables in
+    layer order and the backward finishes them from the end, so the
+    gradients of [ready, n) are final once the layers from ``ready`` on have
+    run their backward.  Every fp32 paired backward launch after that takes
+    the next chunk (at most ``chunk`` parameters, from the top down) of the
+    final-but-not-updated range [ready, done) as extra workgroups of its own
+    launch; the step's last optimizer launch updates only [0, done).
+    MFL_OPT_TAIL = parameters per launch (0: off)."""
+
+    chunk = int(os.environ.get("MFL_OPT_TAIL", "0"))
+    ALIGN = 64  # flat segments start at multiples of 64 elements (models/flat.py)
+
+    def __init__(self, st: FlatState, zero_grad: bool):
+        self.st = st
+        self.zero_grad = zero_grad
+        self.ready = st.n_params
+        self.done = st.n_params
+
+    def mark_ready(self, lo: int) -> None:
+        """Gradients of every trainable variable from offset ``lo`` on are final."""
+        assert lo % self.ALIGN == 0
+        self.ready = min(self.ready, lo)
+
+    def take(self):
+        """The next tail (an OptRange) or None."""
+        if self.chunk <= 0 or self.done <= self.ready:
+            return None
+        lo = max(self.ready, (self.done - self.chunk) // self.ALIGN * self.ALIGN)
+        r = self.st.opt_range(lo, self.done, self.zero_grad)
+        self.done = lo
+        return r
+
+
 class Workspace:
     """Shared scratch: the split-K fp32 slab (kernels on one stream run in
     order, so one buffer of the maximum size serves every layer) and the
@@ -36,6 +71,10 @@ class Workspace:
         self.split: torch.Tensor | None = None
         self.acc_len = 0
         self.bn_acc: torch.Tensor | None = None
+        self.opt_tails: OptTailScheduler | None = None  # set for the duration of a training step
+
+    def take_opt_tail(self):
+        return self.opt_tails.take() if self.opt_tails is not None else None
 
     def need_split(self, n: int) -> None:
         self.split_floats = max(self.split_floats, n)
@@ -86,6 +125,9 @@ FUSED_FILL_CPU = os.environ.get("METISFL_AMD_FUSED_FILL_CPU", "0") == "1"
 HCONV = os.environ.get("MFL_HCONV", "1") == "1"
 # ... for the bf16 option too (MFL_HCONV_BF16=0: BN apply + im2col conv)
 HCONV_BF16 = os.environ.get("MFL_HCONV_BF16", "1") == "1"
+# a downsampling block's conv1 and shortcut BN-backward applies in one launch
+# (MFL_BN_BWD_PAIR=0: two launches, for A/B runs)
+BN_BWD_PAIR = os.environ.get("MFL_BN_BWD_PAIR", "1") == "1"
 # halo dgrad with the BatchNorm backward in its fill (see ConvBN.backward)
 HALO_DGRAD = os.environ.get("MFL_HALO_DGRAD", "0") == "1"
 # the stem's BN backward + weight gradient in one launch (MFL_STEM_FUSED=0:
@@ -286,16 +328,29 @@ class ConvBN(Layer):
             return K.BnSide(self.z, self.mean, self.invstd, self.ws.acc(self.acc_b))
         return None
 
+    def bn_backward_args(self, dy: torch.Tensor) -> tuple:
+        """(dy, z, relu mask, C, gamma, mean, invstd, acc, dgamma, dbeta, dz):
+        this layer's presummed BN-backward apply writing its packed dz (the
+        operands of bn_backward_pair)."""
+        return (dy, self.z, self.y if self.relu else None, self.shp.Co, self.gamma, self.mean, self.invstd,
+                self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz)
+
     def backward(self, dy: torch.Tensor, dx: torch.Tensor | None, accumulate: bool = False,
                  dres: torch.Tensor | None = None, presummed: bool = False,
-                 bnb: K.BnBwdTarget | None = None, side: K.BnSide | None = None) -> None:
+                 bnb: K.BnBwdTarget | None = None, side: K.BnSide | None = None,
+                 bn_done: bool = False) -> None:
         """dy: gradient w.r.t. this layer's output.  Writes dgamma/dbeta/dW into
         the flat gradient buffer and (if dx is given) d input into dx; ``dres``
         receives the ReLU-masked dy that the residual branch needs.
         ``presummed``: dy's producer already accumulated this BN's backward
         reductions; ``bnb``: the BN whose upstream gradient ``dx`` is (its
-        reductions are fused into this layer's dgrad epilogue)."""
+        reductions are fused into this layer's dgrad epilogue); ``bn_done``:
+        the BN backward already wrote dz (a paired apply launch)."""
         s = self.shp
+        if bn_done:
+            pk = self.dz.is_cuda and self.dz.dtype == torch.float32 and K.conv_products() == "bf16x3"
+            self._conv_backward(dx, accumulate, bnb, pk)
+            return
         if (STEM_FUSED and dx is None and dres is None and presummed and side is None and self.relu
                 and ((self.z.dtype == torch.float32 and (self.z.is_cuda or FUSED_FILL_CPU))
                      or (self.z.dtype == torch.bfloat16 and self.z.is_cuda))
@@ -325,13 +380,19 @@ class ConvBN(Layer):
         K.bn_backward(dy, self.z, self.y if self.relu else None, s.Co, self.gamma, self.mean,
                       self.invstd, self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz, dres,
                       presummed=presummed, side=side, dx_packed=pk)
+        self._conv_backward(dx, accumulate, bnb, pk)
+
+    def _conv_backward(self, dx, accumulate: bool, bnb, pk: bool) -> None:
+        s = self.shp
         # weight gradient: off the critical path -> side stream (joined before
         # the optimizer); the gradient buffer is zero on entry (re-zeroed by
         # the optimizer launch), so split-K slices accumulate atomically
         if dx is not None and not self.ws.overlap:
-            # both GEMMs in one launch (their workgroups share the CUs)
+            # both GEMMs in one launch (their workgroups share the CUs); the
+            # fp32 launch also carries the next optimizer tail, if any
+            opt = self.ws.take_opt_tail() if self.dz.dtype == torch.float32 else None
             K.conv_backward_pair(self.x, self.dz, self.dw, self.w16, dx, s, self._split(), accumulate,
-                                 bnb=bnb, wp=self.wp, dy_packed=pk, xp=self.xp)
+                                 bnb=bnb, wp=self.wp, dy_packed=pk, xp=self.xp, opt=opt)
             return
         with self.ws.fork():
             K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True, dy_packed=pk, xp=self.xp)
@@ -456,6 +517,15 @@ class BasicBlock(Layer):
             side = self.sc.bn_side()
             self.c2.backward(dout, self.da, dres=self.dres, presummed=presummed, bnb=self.c1.bn_target(),
                              side=side)
+            if side is not None and BN_BWD_PAIR and not HALO_DGRAD and self.da.dtype == torch.float32:
+                # conv1's and the shortcut's sums are both complete now (conv2's
+                # dgrad epilogue / its BN backward's side reduction): their two
+                # BN-backward applies in one launch
+                K.bn_backward_pair(self.c1.bn_backward_args(self.da), self.sc.bn_backward_args(self.dres),
+                                   dx_packed=self.da.is_cuda and K.conv_products() == "bf16x3")
+                self.sc.backward(self.dres, dx, bn_done=True)
+                self.c1.backward(self.da, dx, accumulate=True, bnb=prev, bn_done=True)
+                return
             self.sc.backward(self.dres, dx, presummed=side is not None)
             self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev)
 

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from metisfl_amd.models.flat import FlatState, VarSpec
-from metisfl_amd.models.layers import Layer, Workspace
+from metisfl_amd.models.layers import Layer, OptTailScheduler, Workspace
 from metisfl_amd.ops import nn as K
 from metisfl_amd.ops import optim as opt_ops
 from metisfl_amd.ops.optim import OptimizerSpec
@@ -150,10 +150,27 @@ class StaticNet:
     # buffer is zeroed at the start of the step instead of by the optimizer.
     zero_grad_in_optimizer: bool = True
 
+    # Models whose backward reports finished variable ranges
+    # (``grads_final_from``) let later paired fp32 backward launches carry the
+    # optimizer step of those ranges (layers.OptTailScheduler, MFL_OPT_TAIL).
+    opt_tails_supported: bool = False
+
+    def grads_final_from(self, prefix: str) -> None:
+        """The backward of every trainable variable from the one named
+        ``prefix``... on has been issued (their gradients are final)."""
+        sched = self.ws.opt_tails
+        if sched is not None:
+            lo = self.state.offset_of_prefix(prefix)
+            if lo is not None:
+                sched.mark_ready(lo)
+
     def _train_body(self, ds: DeviceDataset) -> None:
         st = self.state
         if not self.zero_grad_in_optimizer:
             st.grad32.zero_()
+        tails = (self.opt_tails_supported and OptTailScheduler.chunk > 0 and st.optimizer is not None
+                 and st.n_params > 0)
+        self.ws.opt_tails = OptTailScheduler(st, self.zero_grad_in_optimizer) if tails else None
         K.gather_batch(ds.x, ds.y, ds.perm, st.step, ds.steps_per_epoch, self.B, self.xb, self.yb,
                        xp=self.packed_input())
         out = self.forward_to_head(self.xb, train=True)
@@ -162,9 +179,12 @@ class StaticNet:
             l.prepare_backward()
         self.backward(dlast)
         self.ws.join()  # weight-gradient branch (side stream) must land first
-        # one launch: optimizer + grad re-zero + BN accumulator re-zero + step tick
+        hi = self.ws.opt_tails.done if self.ws.opt_tails is not None else None
+        self.ws.opt_tails = None
+        # one launch: optimizer (of what no tail covered) + grad re-zero + BN
+        # accumulator re-zero + step tick
         if not st.optimizer_step(zero_grad=self.zero_grad_in_optimizer, zero_region=self.ws.bn_acc,
-                                 tick=True):
+                                 tick=True, hi=hi):
             opt_ops.tick(st.step, 1)
 
     def _eval_body(self, ds: DeviceDataset) -> None:

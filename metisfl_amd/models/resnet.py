@@ -43,6 +43,7 @@ def default_conv_products() -> str:
 
 class ResNet18(StaticNet):
     input_shape = (32, 32, 8)
+    opt_tails_supported = True
     num_classes = 10
     widths = (64, 128, 256, 512)
 
@@ -135,11 +136,15 @@ class ResNet18(StaticNet):
         # the BN that consumes it -- the previous block's conv2, or the stem.
         # The last block's conv2 (fed by the head) reduces on its own unless
         # the head applied its BatchNorm and added the sums (fused fill).
+        # Optimizer tails: the head's and every finished block's variables are
+        # updated by later paired launches (StaticNet.grads_final_from).
         d = dlast.view(self.blocks[-1].out_shape)
+        self.grads_final_from(self.head.name + ".")
         for i in range(len(self.blocks) - 1, -1, -1):
             prev = self.blocks[i - 1].c2 if i > 0 else self.stem
             last = i == len(self.blocks) - 1
             self.blocks[i].backward(d, self.dacts[i], presummed=(not last) or self.head.summed_input_bn,
                                     prev=prev.bn_target())
             d = self.dacts[i]
+            self.grads_final_from(self.blocks[i].name + ".")
         self.stem.backward(d, None, presummed=True)

@@ -234,23 +234,35 @@ def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShap
 
 
 def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
-                       bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False, xp=None) -> None:
+                       bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False, xp=None,
+                       opt=None) -> None:
     """A layer's weight gradient (dw += ..., dw zero on entry) and input
     gradient (as conv_dgrad) -- on the GPU in ONE paired launch, so the two
     independent, latency-bound GEMMs share the CUs (conv.hip
     conv_bwd_pair_kernel; MFL_CONV_PAIR=0 for two launches).  fp32: one
     launch too (conv32.hip conv32_bwd_pair_kernel, when both plans run 64x64
-    tiles on the fast address paths; MFL_C32_PAIR=0 for two launches)."""
+    tiles on the fast address paths; MFL_C32_PAIR=0 for two launches).
+    ``opt`` (ops.optim.OptRange): an optimizer step over a range whose
+    gradients are final, run by extra workgroups of the fp32 paired launch
+    (elsewhere: its own launch after the pair)."""
     if dy.is_cuda and dy.dtype == torch.float32:
         dy = _dy_arg(dy, dy_packed)
         xa = x if xp is None else xp
+        from metisfl_amd.ops.optim import NO_OPT_TAIL
+        tail = opt.binding_args() if opt is not None else NO_OPT_TAIL
         if bnb is None:
             ops().conv32_backward_pair(xa, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None, None,
-                                       wp)
+                                       wp, *tail)
         else:
             ops().conv32_backward_pair(xa, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
-                                       bnb.invstd, bnb.acc, wp)
+                                       bnb.invstd, bnb.acc, wp, *tail)
         return
+    _conv_backward_pair_unfused(x, dy, dw, w, dx, shp, ws, accumulate, bnb, wp)
+    if opt is not None:
+        opt.run()
+
+
+def _conv_backward_pair_unfused(x, dy, dw, w, dx, shp, ws, accumulate, bnb, wp) -> None:
     if dy.is_cuda:
         if bnb is None:
             ops().conv_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None,
@@ -463,6 +475,24 @@ def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
     k1 = gamma * invstd
     out = k1 * (g - (tot[:C] / M).float() - xh * (tot[C:2 * C] / M).float())
     dx.copy_(out.to(dx.dtype))
+
+
+def bn_backward_pair(a1: tuple, a2: tuple, dx_packed: bool = False) -> None:
+    """Two presummed BN(+ReLU) backward applies in one launch on the GPU
+    (bn32.hip bn32_bwd_apply_pair_kernel): ``a1`` / ``a2`` are
+    (dy, z, relu mask y or None, C, gamma, mean, invstd, acc, dgamma, dbeta,
+    dz) of a downsampling block's conv1 (with its ReLU mask) and projection
+    shortcut (without); their sums must already be complete in ``acc``."""
+    (dy1, x1, y1, C1, g1, m1, i1, acc1, dg1, db1, dx1) = a1
+    (dy2, x2, y2, C2, g2, m2, i2, acc2, dg2, db2, dx2) = a2
+    if dy1.is_cuda and dy1.dtype == torch.float32 and y1 is not None and y2 is None:
+        if dx_packed:
+            dx1, dx2 = dx1.view(torch.int32), dx2.view(torch.int32)
+        ops().bn32_backward_pair(dy1, x1, y1, C1, g1, m1, i1, acc1, dg1, db1, dx1,
+                                 dy2, x2, C2, g2, m2, i2, acc2, dg2, db2, dx2)
+        return
+    bn_backward(dy1, x1, y1, C1, g1, m1, i1, acc1, dg1, db1, dx1, presummed=True, dx_packed=dx_packed)
+    bn_backward(dy2, x2, y2, C2, g2, m2, i2, acc2, dg2, db2, dx2, presummed=True, dx_packed=dx_packed)
 
 
 def stem_backward_ok(shp: ConvShape, device: torch.device) -> bool:

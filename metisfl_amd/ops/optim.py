@@ -112,6 +112,40 @@ def fused_step(spec: OptimizerSpec, p: torch.Tensor, g: torch.Tensor,
         step.add_(1)
 
 
+class OptRange:
+    """One fused optimizer step over a range of the flat model (views of the
+    master, gradient, slots, anchor and weight mirror): the unit an
+    optimizer tail carries (conv32.h OptTail -- the range's update rides in a
+    later layer's paired backward launch).  ``run()`` is the stand-alone
+    launch (fallback paths)."""
+
+    def __init__(self, spec: OptimizerSpec, p, g, m=None, v=None, anchor=None, mirror=None,
+                 lr_scale=None, step=None, zero_grad: bool = True):
+        self.spec, self.p, self.g, self.m, self.v = spec, p, g, m, v
+        self.anchor, self.mirror, self.lr_scale, self.step, self.zero_grad = anchor, mirror, lr_scale, step, zero_grad
+
+    @property
+    def numel(self) -> int:
+        return int(self.p.numel())
+
+    def hyper(self) -> list[float]:
+        s = self.spec
+        return [s.learning_rate, s.l1, s.l2, s.momentum, s.proximal_term, s.beta1, s.beta2, s.epsilon,
+                s.weight_decay]
+
+    def binding_args(self) -> tuple:
+        """The trailing optimizer-tail arguments of conv32_backward_pair."""
+        return (self.p, self.g, self.m, self.v, self.anchor, self.mirror, self.lr_scale, self.step,
+                self.spec.mode, self.hyper(), self.zero_grad)
+
+    def run(self) -> None:
+        fused_step(self.spec, self.p, self.g, self.m, self.v, self.anchor, self.mirror, self.lr_scale, self.step,
+                   zero_grad=self.zero_grad)
+
+
+NO_OPT_TAIL = (None, None, None, None, None, None, None, None, 0, [0.0] * 9, False)
+
+
 @torch.no_grad()
 def _reference_step(spec, p, g, m, v, anchor, p16, lr_scale, step):
     lr = spec.learning_rate * (float(lr_scale[0]) if lr_scale is not None else 1.0)
