@@ -472,7 +472,7 @@ static mfl::BnBwdArgs32 bn32_bwd_args(torch::Tensor dy, torch::Tensor x, c10::op
   }
   if (dy_masked.has_value() && dy_masked->defined()) {
     check_nhwc32(*dy_masked, C);
-    TORCH_CHECK(a.y != nullptr && dy_masked->numel() == x.numel(), "dy_masked requires y");
+    TORCH_CHECK(dy_masked->numel() == x.numel(), "dy_masked size");
     a.dy_masked = fp(*dy_masked);
   }
   if (dgamma.has_value() && dgamma->defined()) { check_pc(*dgamma, C, "dgamma"); a.dgamma = fp(*dgamma); }
@@ -519,9 +519,11 @@ void bn32_backward_side(torch::Tensor dy, torch::Tensor x, c10::optional<torch::
 }
 
 // Two presummed BN-backward applies in one launch (bn32.hip
-// bn32_bwd_apply_pair_kernel): role 1 with its ReLU mask y1 (a downsampling
-// block's conv1), role 2 without (its projection shortcut).
-void bn32_backward_pair(torch::Tensor dy1, torch::Tensor x1, torch::Tensor y1, int64_t C1, torch::Tensor gamma1,
+// bn32_bwd_apply_pair_kernel): role 1 a downsampling block's conv1 (with its
+// ReLU mask y1, or none when dy1 arrives masked), role 2 its projection
+// shortcut (no ReLU).
+void bn32_backward_pair(torch::Tensor dy1, torch::Tensor x1, c10::optional<torch::Tensor> y1, int64_t C1,
+                        torch::Tensor gamma1,
                         torch::Tensor mean1, torch::Tensor invstd1, torch::Tensor acc1, torch::Tensor dgamma1,
                         torch::Tensor dbeta1, torch::Tensor dx1, torch::Tensor dy2, torch::Tensor x2, int64_t C2,
                         torch::Tensor gamma2, torch::Tensor mean2, torch::Tensor invstd2, torch::Tensor acc2,

@@ -288,15 +288,16 @@ __device__ __forceinline__ void bn32_bwd_apply_body(const BnBwdArgs32& a, int64_
       g.y = yc.y > 0.f ? g.y : 0.f;
       g.z = yc.z > 0.f ? g.z : 0.f;
       g.w = yc.w > 0.f ? g.w : 0.f;
-      if (WRITE_DYM) reinterpret_cast<float4*>(a.dy_masked)[i] = g;
-      if (WRITE_DYM && side) {
-        const float4 z2 = reinterpret_cast<const float4*>(a.z2)[i];
-        s2.x += g.x; s2.y += g.y; s2.z += g.z; s2.w += g.w;
-        q2.x += g.x * ((z2.x - mu2.x) * is2.x);
-        q2.y += g.y * ((z2.y - mu2.y) * is2.y);
-        q2.z += g.z * ((z2.z - mu2.z) * is2.z);
-        q2.w += g.w * ((z2.w - mu2.w) * is2.w);
-      }
+    }
+    // !MASK: dy arrives masked (its producing dgrad applied the mask)
+    if (WRITE_DYM) reinterpret_cast<float4*>(a.dy_masked)[i] = g;
+    if (WRITE_DYM && side) {
+      const float4 z2 = reinterpret_cast<const float4*>(a.z2)[i];
+      s2.x += g.x; s2.y += g.y; s2.z += g.z; s2.w += g.w;
+      q2.x += g.x * ((z2.x - mu2.x) * is2.x);
+      q2.y += g.y * ((z2.y - mu2.y) * is2.y);
+      q2.z += g.z * ((z2.z - mu2.z) * is2.z);
+      q2.w += g.w * ((z2.w - mu2.w) * is2.w);
     }
     float4 o;
     o.x = k1.x * fmaf(-((xc.x - mu.x) * is.x), mx.x, g.x - mg.x);
@@ -328,8 +329,12 @@ __global__ __launch_bounds__(256) void bn32_bwd_apply_kernel(BnBwdArgs32 a, int6
 __global__ __launch_bounds__(256) void bn32_bwd_apply_pair_kernel(BnBwdArgs32 a1, int64_t n1, int g1,
                                                                   BnBwdArgs32 a2, int64_t n2) {
   extern __shared__ __attribute__((aligned(16))) float sc[];
-  if ((int)blockIdx.x < g1) bn32_bwd_apply_body<true, false>(a1, n1, blockIdx.x, g1, sc);
-  else bn32_bwd_apply_body<false, false>(a2, n2, blockIdx.x - g1, gridDim.x - g1, sc);
+  if ((int)blockIdx.x < g1) {
+    if (a1.y) bn32_bwd_apply_body<true, false>(a1, n1, blockIdx.x, g1, sc);
+    else bn32_bwd_apply_body<false, false>(a1, n1, blockIdx.x, g1, sc);  // dy arrives masked
+  } else {
+    bn32_bwd_apply_body<false, false>(a2, n2, blockIdx.x - g1, gridDim.x - g1, sc);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -533,7 +538,8 @@ void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s) {
     if (a.dy_masked) bn32_bwd_apply_kernel<true, true><<<g, 256, sm, s>>>(a, nvec);
     else bn32_bwd_apply_kernel<true, false><<<g, 256, sm, s>>>(a, nvec);
   } else {
-    bn32_bwd_apply_kernel<false, false><<<g, 256, sm, s>>>(a, nvec);
+    if (a.dy_masked) bn32_bwd_apply_kernel<false, true><<<g, 256, sm, s>>>(a, nvec);
+    else bn32_bwd_apply_kernel<false, false><<<g, 256, sm, s>>>(a, nvec);
   }
 }
 

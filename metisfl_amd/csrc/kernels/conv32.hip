@@ -49,6 +49,10 @@
 //    the write-through slabs in slice order: bitwise deterministic).
 //  * Stride-2 dgrad runs parity-class decomposed (PAR), as in conv.hip.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
 #include <type_traits>
 #include <utility>
 
@@ -343,18 +347,20 @@ __device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, const Blk& 
     const int64_t off = (int64_t)out_pixel32(a, row) * g.Ng + col;
     float4* dst = reinterpret_cast<float4*>(a.y + off);
     if (a.accum) v = f4add(v, *dst);
+    if (a.bn_acc && a.bn_y) {
+      // the consumer BN's ReLU mask applied on the way out: dX is stored as
+      // g = dX [y > 0], so that BN's backward apply reads no mask
+      const float4 ym = *reinterpret_cast<const float4*>(a.bn_y + off);
+      v.x = ym.x > 0.f ? v.x : 0.f;
+      v.y = ym.y > 0.f ? v.y : 0.f;
+      v.z = ym.z > 0.f ? v.z : 0.f;
+      v.w = ym.w > 0.f ? v.w : 0.f;
+    }
     *dst = v;
     if (stats) {
       if (a.bn_acc) {
         const float4 z = *reinterpret_cast<const float4*>(a.bn_z + off);
-        float4 gk = v;
-        if (a.bn_y) {
-          const float4 ym = *reinterpret_cast<const float4*>(a.bn_y + off);
-          gk.x = ym.x > 0.f ? gk.x : 0.f;
-          gk.y = ym.y > 0.f ? gk.y : 0.f;
-          gk.z = ym.z > 0.f ? gk.z : 0.f;
-          gk.w = ym.w > 0.f ? gk.w : 0.f;
-        }
+        const float4 gk = v;
         s = f4add(s, gk);
         q.x += gk.x * ((z.x - mu.x) * is.x);
         q.y += gk.y * ((z.y - mu.y) * is.y);
@@ -1110,10 +1116,13 @@ constexpr TunedPlan kTuned[] = {
     {0, 32, 16, 16, 128, 256, 3, 2, 64, 64, 4}, {0, 32, 8, 8, 256, 256, 3, 1, 64, 64, 4},
     {0, 32, 8, 8, 256, 512, 3, 2, 64, 64, 4},   {0, 32, 4, 4, 512, 512, 3, 1, 64, 64, 8},
     {1, 32, 32, 32, 64, 64, 3, 1, 64, 64, 1},   {1, 32, 32, 32, 64, 128, 3, 2, 64, 64, 1},
-    {1, 32, 32, 32, 64, 128, 1, 2, 64, 64, 1},  {1, 32, 16, 16, 128, 128, 3, 1, 64, 64, 3},
+    // 16x16x128 backward pair: dgrad 2 x wgrad 7 slices = 764 workgroups, one
+    // wave of 3 per CU, instead of 3 x 14 = 1,272 (1.66 waves) -- whole-step
+    // sweep with MFL_C32_PLANS, profiles/r4/plans/: -1.4 % per update
+    {1, 32, 32, 32, 64, 128, 1, 2, 64, 64, 1},  {1, 32, 16, 16, 128, 128, 3, 1, 64, 64, 2},
     {1, 32, 16, 16, 128, 256, 3, 2, 64, 64, 3}, {1, 32, 8, 8, 256, 256, 3, 1, 64, 64, 4},
     {1, 32, 8, 8, 256, 512, 3, 2, 64, 64, 4},   {1, 32, 4, 4, 512, 512, 3, 1, 64, 64, 8},
-    {2, 32, 16, 16, 128, 128, 3, 1, 64, 64, 14}, {2, 32, 16, 16, 128, 256, 3, 2, 64, 64, 7},
+    {2, 32, 16, 16, 128, 128, 3, 1, 64, 64, 7}, {2, 32, 16, 16, 128, 256, 3, 2, 64, 64, 7},
     {2, 32, 8, 8, 256, 256, 3, 1, 64, 64, 3},   {2, 32, 8, 8, 256, 512, 3, 2, 64, 64, 2},
     {2, 32, 4, 4, 512, 512, 3, 1, 64, 64, 1},
 };
@@ -1126,9 +1135,43 @@ constexpr TunedPlan kTuned[] = {
     {2, 32, 4, 4, 512, 512, 3, 1, 64, 64, 2},
 };
 #endif
+// MFL_C32_PLANS="mode,h,c,co,r,stride,splits;..." overrides the split-K
+// factor of matching shapes (64x64 tiles; batch-size independent) -- for
+// sweeps of whole-step plans, where a paired launch's total workgroup count
+// (waves of 3 per CU) matters more than each GEMM's stand-alone optimum.
+struct PlanOverride {
+  int mode, h, c, co, r, stride, splits;
+};
+static const std::vector<PlanOverride>& plan_overrides() {
+  static const std::vector<PlanOverride> v = [] {
+    std::vector<PlanOverride> out;
+    const char* e = std::getenv("MFL_C32_PLANS");
+    if (!e) return out;
+    std::string str(e);
+    size_t pos = 0;
+    while (pos < str.size()) {
+      size_t end = str.find(';', pos);
+      if (end == std::string::npos) end = str.size();
+      PlanOverride o{};
+      if (std::sscanf(str.substr(pos, end - pos).c_str(), "%d,%d,%d,%d,%d,%d,%d", &o.mode, &o.h, &o.c, &o.co, &o.r,
+                      &o.stride, &o.splits) == 7)
+        out.push_back(o);
+      pos = end + 1;
+    }
+    return out;
+  }();
+  return v;
+}
+
 static void tuned_plan(const ConvGeom& g, int mode, int& bm, int& bn, int& sp) {
   const bool dg = mode == 1;
   const int h = dg ? g.P : g.H, w = dg ? g.Q : g.W, c = dg ? g.Ng : g.C, co = dg ? g.C : g.Ng;
+  for (const PlanOverride& o : plan_overrides())
+    if (o.mode == mode && o.h == h && o.c == c && o.co == co && o.r == g.R && o.stride == g.stride) {
+      bm = bn = 64;
+      sp = o.splits;
+      return;
+    }
   for (const TunedPlan& t : kTuned)
     if (t.mode == mode && t.n == g.N && t.h == h && t.w == w && t.c == c && t.co == co && t.r == g.R &&
         t.stride == g.stride) {

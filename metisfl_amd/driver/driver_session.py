@@ -560,7 +560,7 @@ class DriverSessionBase:
             raise RuntimeError("run_collective needs DataPlane: rccl in the federation environment")
         self.initialize_federation()
         try:
-            self.monitor_federation(request_every_secs)
+            self.termination_reason = self.monitor_federation(request_every_secs)
         finally:
             self.shutdown_federation()
         return self.get_federation_statistics()

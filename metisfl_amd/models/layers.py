@@ -33,9 +33,11 @@ class OptTailScheduler:
     the next chunk (at most ``chunk`` parameters, from the top down) of the
     final-but-not-updated range [ready, done) as extra workgroups of its own
     launch; the step's last optimizer launch updates only [0, done).
-    MFL_OPT_TAIL = parameters per launch (0: off)."""
+    MFL_OPT_TAIL = parameters per launch (0: off; default 512K)."""
 
-    chunk = int(os.environ.get("MFL_OPT_TAIL", "0"))
+    # measured (profiles/r4/step/{c,d,e}_t*.log): 512K parameters per launch
+    # -1.0..-1.3 % per update for one learner, -2 % for two co-located
+    chunk = int(os.environ.get("MFL_OPT_TAIL", "524288"))
     ALIGN = 64  # flat segments start at multiples of 64 elements (models/flat.py)
 
     def __init__(self, st: FlatState, zero_grad: bool):
@@ -125,6 +127,18 @@ FUSED_FILL_CPU = os.environ.get("METISFL_AMD_FUSED_FILL_CPU", "0") == "1"
 HCONV = os.environ.get("MFL_HCONV", "1") == "1"
 # ... for the bf16 option too (MFL_HCONV_BF16=0: BN apply + im2col conv)
 HCONV_BF16 = os.environ.get("MFL_HCONV_BF16", "1") == "1"
+def premasked(t: torch.Tensor) -> bool:
+    """Whether a dgrad that fuses a consumer BN's backward sums (``bnb``) into
+    its epilogue stores dX already multiplied by that BN's ReLU mask (the
+    fp32 conv32 epilogue and its host mirror; not the bf16 kernels or the
+    opt-in halo dgrad), so the consumer's BN backward reads no mask."""
+    return t.dtype == torch.float32 and not HALO_DGRAD and PREMASK
+
+
+# MFL_BN_PREMASK=0: consumers re-apply the ReLU mask (A/B runs)
+PREMASK = os.environ.get("MFL_BN_PREMASK", "1") == "1"
+
+
 # a downsampling block's conv1 and shortcut BN-backward applies in one launch
 # (MFL_BN_BWD_PAIR=0: two launches, for A/B runs)
 BN_BWD_PAIR = os.environ.get("MFL_BN_BWD_PAIR", "1") == "1"
@@ -328,24 +342,26 @@ class ConvBN(Layer):
             return K.BnSide(self.z, self.mean, self.invstd, self.ws.acc(self.acc_b))
         return None
 
-    def bn_backward_args(self, dy: torch.Tensor) -> tuple:
+    def bn_backward_args(self, dy: torch.Tensor, dy_masked: bool = False) -> tuple:
         """(dy, z, relu mask, C, gamma, mean, invstd, acc, dgamma, dbeta, dz):
         this layer's presummed BN-backward apply writing its packed dz (the
-        operands of bn_backward_pair)."""
-        return (dy, self.z, self.y if self.relu else None, self.shp.Co, self.gamma, self.mean, self.invstd,
-                self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz)
+        operands of bn_backward_pair); ``dy_masked``: dy arrives masked."""
+        return (dy, self.z, self.y if self.relu and not dy_masked else None, self.shp.Co, self.gamma, self.mean,
+                self.invstd, self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz)
 
     def backward(self, dy: torch.Tensor, dx: torch.Tensor | None, accumulate: bool = False,
                  dres: torch.Tensor | None = None, presummed: bool = False,
                  bnb: K.BnBwdTarget | None = None, side: K.BnSide | None = None,
-                 bn_done: bool = False) -> None:
+                 bn_done: bool = False, dy_masked: bool = False) -> None:
         """dy: gradient w.r.t. this layer's output.  Writes dgamma/dbeta/dW into
         the flat gradient buffer and (if dx is given) d input into dx; ``dres``
         receives the ReLU-masked dy that the residual branch needs.
         ``presummed``: dy's producer already accumulated this BN's backward
         reductions; ``bnb``: the BN whose upstream gradient ``dx`` is (its
         reductions are fused into this layer's dgrad epilogue); ``bn_done``:
-        the BN backward already wrote dz (a paired apply launch)."""
+        the BN backward already wrote dz (a paired apply launch);
+        ``dy_masked``: dy arrives multiplied by this layer's ReLU mask (see
+        :func:`premasked`)."""
         s = self.shp
         if bn_done:
             pk = self.dz.is_cuda and self.dz.dtype == torch.float32 and K.conv_products() == "bf16x3"
@@ -377,7 +393,7 @@ class ConvBN(Layer):
         # bf16x3 conv products: dz is only ever read by this layer's dgrad and
         # wgrad, so the BN backward writes it as their packed operand encoding
         pk = self.dz.is_cuda and self.dz.dtype == torch.float32 and K.conv_products() == "bf16x3"
-        K.bn_backward(dy, self.z, self.y if self.relu else None, s.Co, self.gamma, self.mean,
+        K.bn_backward(dy, self.z, self.y if self.relu and not dy_masked else None, s.Co, self.gamma, self.mean,
                       self.invstd, self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dz, dres,
                       presummed=presummed, side=side, dx_packed=pk)
         self._conv_backward(dx, accumulate, bnb, pk)
@@ -502,32 +518,37 @@ class BasicBlock(Layer):
         layer.forward(x, train=train, xp=src.yp, bn=False)
         return Pending.of(layer)
 
-    def backward(self, dout, dx, presummed: bool = False, prev: K.BnBwdTarget | None = None):
+    def backward(self, dout, dx, presummed: bool = False, prev: K.BnBwdTarget | None = None,
+                 dout_masked: bool = False):
         """``presummed``: conv2's BN reductions were fused into dout's producer;
         ``prev``: the BN consuming dx (the previous block's conv2 or the stem),
-        whose reductions are fused into the LAST dgrad writing dx (conv1's)."""
+        whose reductions are fused into the LAST dgrad writing dx (conv1's);
+        ``dout_masked``: dout arrives multiplied by conv2's ReLU mask."""
+        pm = premasked(self.da)  # conv2's dgrad stores da masked for conv1's BN
         if self.sc is None:
             # identity shortcut: masked dout goes straight into dx, conv1's
             # dgrad then accumulates onto it (no add kernel)
-            self.c2.backward(dout, self.da, dres=dx, presummed=presummed, bnb=self.c1.bn_target())
-            self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev)
+            self.c2.backward(dout, self.da, dres=dx, presummed=presummed, bnb=self.c1.bn_target(),
+                             dy_masked=dout_masked)
+            self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev, dy_masked=pm)
         else:
             # the shortcut BN's backward sums ride in conv2's BN-backward launch
             # (it writes dres, the shortcut's upstream gradient)
             side = self.sc.bn_side()
             self.c2.backward(dout, self.da, dres=self.dres, presummed=presummed, bnb=self.c1.bn_target(),
-                             side=side)
+                             side=side, dy_masked=dout_masked)
             if side is not None and BN_BWD_PAIR and not HALO_DGRAD and self.da.dtype == torch.float32:
                 # conv1's and the shortcut's sums are both complete now (conv2's
                 # dgrad epilogue / its BN backward's side reduction): their two
                 # BN-backward applies in one launch
-                K.bn_backward_pair(self.c1.bn_backward_args(self.da), self.sc.bn_backward_args(self.dres),
+                K.bn_backward_pair(self.c1.bn_backward_args(self.da, dy_masked=pm),
+                                   self.sc.bn_backward_args(self.dres),
                                    dx_packed=self.da.is_cuda and K.conv_products() == "bf16x3")
                 self.sc.backward(self.dres, dx, bn_done=True)
                 self.c1.backward(self.da, dx, accumulate=True, bnb=prev, bn_done=True)
                 return
             self.sc.backward(self.dres, dx, presummed=side is not None)
-            self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev)
+            self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev, dy_masked=pm)
 
 
 class ClassifierHead(Layer):

@@ -29,7 +29,7 @@ import os
 
 import torch
 
-from metisfl_amd.models.layers import BasicBlock, ClassifierHead, ConvBN, Pending
+from metisfl_amd.models.layers import BasicBlock, ClassifierHead, ConvBN, Pending, premasked
 from metisfl_amd.models.net import StaticNet
 from metisfl_amd.ops.optim import split_pack
 
@@ -143,8 +143,11 @@ class ResNet18(StaticNet):
         for i in range(len(self.blocks) - 1, -1, -1):
             prev = self.blocks[i - 1].c2 if i > 0 else self.stem
             last = i == len(self.blocks) - 1
+            # dacts[i + 1] was written by block i + 1's conv1 dgrad, which stored
+            # it masked for this block's conv2 BN (layers.premasked); the head's
+            # dx is not
             self.blocks[i].backward(d, self.dacts[i], presummed=(not last) or self.head.summed_input_bn,
-                                    prev=prev.bn_target())
+                                    prev=prev.bn_target(), dout_masked=(not last) and premasked(d))
             d = self.dacts[i]
             self.grads_final_from(self.blocks[i].name + ".")
         self.stem.backward(d, None, presummed=True)

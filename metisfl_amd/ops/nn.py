@@ -157,6 +157,8 @@ def _bnb_sums_cpu(dx: torch.Tensor, t: BnBwdTarget) -> None:
     g = dx.float().reshape(-1, C)
     if t.y is not None:
         g = torch.where(t.y.float().reshape(-1, C) > 0, g, torch.zeros_like(g))
+        if dx.dtype == torch.float32:  # as the fp32 GPU epilogue: dX is stored masked
+            dx.copy_(g.view(dx.shape))
     xh = (t.z.float().reshape(-1, C) - t.mean) * t.invstd
     t.acc[:C] += g.double().sum(0)
     t.acc[C:2 * C] += (g.double() * xh.double()).sum(0)
@@ -453,8 +455,8 @@ def bn_backward(dy, x, y, C: int, gamma, mean, invstd, acc, dgamma, dbeta, dx,
     g = dy.float()
     if y is not None:
         g = torch.where(y.float() > 0, g, torch.zeros_like(g))
-        if dy_masked is not None:
-            dy_masked.copy_(g.to(dy_masked.dtype))
+    if dy_masked is not None:  # (y None: dy arrives masked)
+        dy_masked.copy_(g.to(dy_masked.dtype))
     if side is not None:
         gs = g.reshape(-1, C).double()
         xs = ((side.z.float() - side.mean) * side.invstd).reshape(-1, C).double()
@@ -485,7 +487,7 @@ def bn_backward_pair(a1: tuple, a2: tuple, dx_packed: bool = False) -> None:
     shortcut (without); their sums must already be complete in ``acc``."""
     (dy1, x1, y1, C1, g1, m1, i1, acc1, dg1, db1, dx1) = a1
     (dy2, x2, y2, C2, g2, m2, i2, acc2, dg2, db2, dx2) = a2
-    if dy1.is_cuda and dy1.dtype == torch.float32 and y1 is not None and y2 is None:
+    if dy1.is_cuda and dy1.dtype == torch.float32 and y2 is None:
         if dx_packed:
             dx1, dx2 = dx1.view(torch.int32), dx2.view(torch.int32)
         ops().bn32_backward_pair(dy1, x1, y1, C1, g1, m1, i1, acc1, dg1, db1, dx1,

@@ -597,6 +597,9 @@ class AsyncCollectiveFederation:
             svc = threading.Thread(target=self._serve_loop, name="metisfl-async-aggregator", daemon=True)
             svc.start()
         task, last_eval = self.task_index, None
+        # submission keys count this run's tasks from 0 (rank 0's next_task
+        # does): a resumed learner's task_index continues its lifetime count
+        sub = 0
         spe = self.train_ds.steps_per_epoch
         while not self._stopped():
             if fault_task is not None and task + 1 == int(fault_task) and on_fault is not None:
@@ -625,12 +628,13 @@ class AsyncCollectiveFederation:
                     self._after_update()
                 self._install()
             else:
-                self.store.set(_KEY.format(self.tag, self.rank, task), json.dumps(meta))
+                self.store.set(_KEY.format(self.tag, self.rank, sub), json.dumps(meta))
                 dist.send(self.net.state.model32, dst=0, group=self.p2p)
                 dist.recv(self.net.state.model32, src=0, group=self.p2p)
-                self.base_version = int(self.store.get(_VER.format(self.tag, self.rank, task)))
+                self.base_version = int(self.store.get(_VER.format(self.tag, self.rank, sub)))
                 self._install()
             last_eval = self._evaluate_received()
+            sub += 1
             task += 1
             self.task_index = task
             if self.ckpt_dir and self.ckpt_every and task % self.ckpt_every == 0:

@@ -144,6 +144,12 @@ def test_async_collective_recovers_from_a_lost_rank(tmp_path):
     assert "dropped old ranks [2]" in line[-1]
     md = stats["federation_runtime_metadata"]["metadata"]
     assert max(int(m["global_iteration"]) for m in md) >= 10
+    # the federation ends on its version budget with BOTH survivors served
+    # after the resume (not on the time cutoff with rank 1 never served)
+    assert sess.termination_reason == "rounds", sess.termination_reason
+    after = {lid for m in md if int(m["global_iteration"]) > rc["resumed_from_round"]
+             for lid in m.get("completed_by_learner_id", [])}
+    assert len(after) == 2, after
 
 
 def test_community_model_lineage_is_current_mid_run(tmp_path):
