@@ -4,6 +4,7 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
+#include "bindings/opt_tail_args.h"
 #include "kernels/conv.h"
 #include "kernels/gemm.h"
 
@@ -261,9 +262,17 @@ void conv_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, tor
                         int64_t C, int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad,
                         bool accumulate, c10::optional<torch::Tensor> bn_z, c10::optional<torch::Tensor> bn_y,
                         c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_invstd,
-                        c10::optional<torch::Tensor> bn_acc) {
+                        c10::optional<torch::Tensor> bn_acc, c10::optional<torch::Tensor> opt_p,
+                        c10::optional<torch::Tensor> opt_g, c10::optional<torch::Tensor> opt_m,
+                        c10::optional<torch::Tensor> opt_v, c10::optional<torch::Tensor> opt_anchor,
+                        c10::optional<torch::Tensor> opt_mirror, c10::optional<torch::Tensor> opt_lr_scale,
+                        c10::optional<torch::Tensor> opt_step, int64_t opt_mode, std::vector<double> opt_hyper,
+                        bool opt_zero_grad) {
   auto gw = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
   auto gd = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
+  mfl::OptTail ot;  // optimizer tail (opt_tail.h), bf16 compute-copy mirror
+  const bool tail = opt_tail_args(ot, opt_p, opt_g, opt_m, opt_v, opt_anchor, opt_mirror, opt_lr_scale, opt_step,
+                                  opt_mode, opt_hyper, opt_zero_grad);
   check_bf16(x, N * H * W * C, "x");
   check_bf16(dy, (int64_t)gw.M * Co, "dy");
   check_f32(dw, Co * R * S * C, "dw");
@@ -282,11 +291,12 @@ void conv_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, tor
     wsp = ws->data_ptr<float>() + counter_words(gd, pd);
   }
   if (mfl::launch_conv_bwd_pair(gd, pd, bf(dy), bf(wt), bf(dx), wsp, counters, accumulate, fused ? &f : nullptr,
-                                gw, bf(x), dw.data_ptr<float>(), cur_stream(dx)))
+                                gw, bf(x), dw.data_ptr<float>(), cur_stream(dx), tail ? &ot : nullptr))
     return;
   mfl::launch_conv_wgrad(gw, mfl::plan_conv_wgrad(gw), bf(x), bf(dy), dw.data_ptr<float>(), cur_stream(x));
   if (fused) run_gemm(gd, true, dy, wt, dx, ws, c10::nullopt, accumulate, &f);
   else run_gemm(gd, true, dy, wt, dx, ws, c10::nullopt, accumulate);
+  if (tail) opt_tail_fallback(ot, cur_stream(dx));
 }
 
 void transpose_krsc(torch::Tensor w, torch::Tensor wt, int64_t Co, int64_t RS, int64_t Ci) {

@@ -8,6 +8,7 @@
 
 #include "kernels/conv32.h"
 #include "kernels/launchers.h"
+#include "bindings/opt_tail_args.h"
 
 namespace {
 
@@ -215,44 +216,11 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
                           int64_t opt_mode, std::vector<double> opt_hyper, bool opt_zero_grad) {
   const auto gf = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
   const auto gd = dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
-  // optimizer tail (conv32.h OptTail): a flat-model range whose gradients are
+  // optimizer tail (opt_tail.h): a flat-model range whose gradients are
   // final, updated by extra workgroups of this launch
   mfl::OptTail ot;
-  const bool tail = opt_p.has_value() && opt_p->defined();
-  if (tail) {
-    const int64_t n = opt_p->numel();
-    check_f32(*opt_p, n, "opt p");
-    TORCH_CHECK(n % 4 == 0 && (reinterpret_cast<uintptr_t>(opt_p->data_ptr()) & 15) == 0, "opt range: 16-B float4s");
-    TORCH_CHECK(opt_hyper.size() == 9, "opt hyper: lr l1 l2 momentum mu beta1 beta2 eps wd");
-    auto same = [&](const c10::optional<torch::Tensor>& t, const char* nm) -> float* {
-      if (!(t.has_value() && t->defined())) return nullptr;
-      TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->numel() == n, "opt ", nm, " range");
-      return reinterpret_cast<float*>(t->data_ptr());
-    };
-    ot.p = fp(*opt_p);
-    ot.g = same(opt_g, "g");
-    TORCH_CHECK(ot.g != nullptr, "opt tail needs the gradient range");
-    ot.m = same(opt_m, "m");
-    ot.v = same(opt_v, "v");
-    ot.anchor = same(opt_anchor, "anchor");
-    ot.mirror = same(opt_mirror, "mirror");
-    TORCH_CHECK(!ot.mirror || opt_mirror->scalar_type() == torch::kInt32, "opt tail mirror: the packed split");
-    ot.mirror_kind = ot.mirror ? 2 : 0;
-    ot.mode = (int)opt_mode;
-    TORCH_CHECK(ot.mode != mfl::OPT_MOMENTUM || ot.m, "momentum buffer");
-    TORCH_CHECK(ot.mode != mfl::OPT_FEDPROX || ot.anchor, "proximal anchor");
-    TORCH_CHECK((ot.mode != mfl::OPT_ADAM && ot.mode != mfl::OPT_ADAMW) || (ot.m && ot.v), "adam slots");
-    ot.h.lr = (float)opt_hyper[0]; ot.h.l1 = (float)opt_hyper[1]; ot.h.l2 = (float)opt_hyper[2];
-    ot.h.momentum = (float)opt_hyper[3]; ot.h.mu = (float)opt_hyper[4]; ot.h.beta1 = (float)opt_hyper[5];
-    ot.h.beta2 = (float)opt_hyper[6]; ot.h.eps = (float)opt_hyper[7]; ot.h.wd = (float)opt_hyper[8];
-    ot.lr_ptr = opt_lr_scale.has_value() && opt_lr_scale->defined() ? fp(*opt_lr_scale) : nullptr;
-    ot.step_ptr = opt_step.has_value() && opt_step->defined() ? opt_step->data_ptr<int>() : nullptr;
-    ot.zero_grad = opt_zero_grad ? 1 : 0;
-    ot.n4 = n / 4;
-    // ~4 float4 per thread: enough workgroups to stream at full rate, few
-    // enough to land in the GEMMs' tail
-    ot.nblk = (int)std::max<int64_t>(16, std::min<int64_t>(256, ot.n4 / (256 * 4)));
-  }
+  const bool tail = opt_tail_args(ot, opt_p, opt_g, opt_m, opt_v, opt_anchor, opt_mirror, opt_lr_scale, opt_step,
+                                  opt_mode, opt_hyper, opt_zero_grad);
   torch::Tensor xtmp, dtmp;
   const float* xs = dysrc(x, (int64_t)N * H * W * C, xtmp, "x");
   const float* dyp = dysrc(dy, (int64_t)gf.M * Co, dtmp);
@@ -292,10 +260,7 @@ void conv32_backward_pair(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, t
   C32_CALL(launch_conv32_wgrad, gf, pw, xs, dyp, fp(dw), true, cur_stream(dw));
   C32_CALL(launch_conv32_gemm, gd, true, pd, dyp, wb, fp(dx), slab, counters, nullptr, accumulate,
                           fuse ? &f : nullptr, cur_stream(dx));
-  if (tail)  // the pair did not launch: the range's optimizer as its own launch
-    mfl::launch_fused_optimizer(ot.mode, ot.p, ot.g, ot.m, ot.v, ot.anchor, ot.mirror, ot.n4 * 4, ot.h, ot.lr_ptr,
-                                ot.step_ptr, ot.zero_grad != 0, nullptr, 0, cur_stream(dx), nullptr,
-                                ot.mirror_kind);
+  if (tail) opt_tail_fallback(ot, cur_stream(dx));
 }
 
 void conv32_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int64_t N, int64_t H, int64_t W, int64_t C,
@@ -683,19 +648,24 @@ void head32_forward_backward_bn(int64_t B, int64_t HW, int64_t C, torch::Tensor 
     TORCH_CHECK(feat->numel() >= B * C && dlogits->numel() >= B * K, "bwd buffer sizes");
     check_act(*dx, "head dx");
   }
+  // split head scratch: [B][C / 128][K] partial logits (stream-ordered lifetime)
+  torch::Tensor lpart;
+  if (C % 128 == 0 && feat.has_value() && feat->defined() && feat->numel() >= B * C)
+    lpart = torch::empty({B * (C / 128) * K}, z.options().dtype(torch::kFloat32));
+  float* lp = lpart.defined() ? lpart.data_ptr<float>() : nullptr;
   if (bf) {
     mfl::launch_head_fwd_bwd(reinterpret_cast<const uint16_t*>(y.data_ptr()), (int)B, (int)HW, (int)C, fp(W),
                              opt_ptr<float>(bias), (int)K, labels.data_ptr<int>(), opt_ptr<float>(feat),
                              opt_ptr<float>(dlogits),
                              backward ? reinterpret_cast<uint16_t*>(dx->data_ptr()) : nullptr,
                              opt_ptr<float>(stats), backward, cur_stream(z), fuse ? fp(*dW) : nullptr,
-                             fuse ? opt_ptr<float>(db) : nullptr, &hb);
+                             fuse ? opt_ptr<float>(db) : nullptr, &hb, lp);
     return;
   }
   mfl::launch_head32_fwd_bwd(fp(y), (int)B, (int)HW, (int)C, fp(W), opt_ptr<float>(bias), (int)K,
                              labels.data_ptr<int>(), opt_ptr<float>(feat), opt_ptr<float>(dlogits),
                              opt_ptr<float>(dx), opt_ptr<float>(stats), backward, cur_stream(z),
-                             fuse ? fp(*dW) : nullptr, fuse ? opt_ptr<float>(db) : nullptr, &hb);
+                             fuse ? fp(*dW) : nullptr, fuse ? opt_ptr<float>(db) : nullptr, &hb, lp);
 }
 
 // fp32 rows are gathered as 16-B units, like the bf16 ones

@@ -86,9 +86,13 @@ struct BnBwdFusion {
 // optional fused BN-backward reductions f) and wgrad (forward geometry gw,
 // dw += ..., zero on entry) in one launch.  false: not supported for this
 // shape (or MFL_CONV_PAIR=0) -- nothing was launched.
+// ot (optional): an optimizer tail run by extra workgroups of the same launch
+// (opt_tail.h; mirror_kind 1 = the bf16 compute copy)
+struct OptTail;
 bool launch_conv_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const uint16_t* dy, const uint16_t* wt,
                           uint16_t* dx, float* ysplit, int* counters, bool accum, const BnBwdFusion* f,
-                          const ConvGeom& gw, const uint16_t* x, float* dw, hipStream_t s);
+                          const ConvGeom& gw, const uint16_t* x, float* dw, hipStream_t s,
+                          const OptTail* ot = nullptr);
 // A downsampling block's 3x3/s2 conv1 (g1) and 1x1/s2 shortcut (g2) forward
 // convolutions of the same input x in one launch (plans / workspaces / stats
 // as for launch_conv_gemm); false: not supported -- nothing was launched.

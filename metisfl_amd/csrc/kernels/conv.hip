@@ -48,6 +48,7 @@
 #include "kernels/common.h"
 #include "kernels/conv.h"
 #include "kernels/lds_tiles.h"
+#include "kernels/opt_tail_dev.h"
 
 #ifndef MFL_CONV_DBG
 #define MFL_CONV_DBG 0  // timing experiments only: bit0 skip MFMAs, bit1 skip operand DMA (compile-time: a runtime test split the k-loop into basic blocks)
@@ -641,10 +642,14 @@ struct PairGrid {
 };
 template <int BM, int BN, int KS, int ST, bool PAR>
 __global__ __launch_bounds__(256) void conv_bwd_pair_kernel(ConvArgs da, ConvArgs wa, float* __restrict__ dw,
-                                                            PairGrid pg) {
+                                                            PairGrid pg, OptTail ot) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int id = blockIdx.x;
   const int nd = pg.dgx * pg.dgy * pg.dgz, nw = pg.wgx * pg.wgy * pg.wgz;
+  if (id >= nd + nw) {  // optimizer tail (opt_tail.h), dispatched after both GEMMs
+    opt_tail_body(ot, id - nd - nw);
+    return;
+  }
   bool isd;
   int lid;
   if (pg.order == 0) {
@@ -966,24 +971,26 @@ void launch_conv_wgrad(const ConvGeom& g, const ConvPlan& p, const uint16_t* x, 
 // ---- paired dgrad + wgrad ----------------------------------------------------
 namespace {
 template <int BM, int BN, int KS, int ST, bool PAR>
-void launch_pair_t(const ConvArgs& da, const ConvArgs& wa, float* dw, const PairGrid& pg, hipStream_t s) {
+void launch_pair_t(const ConvArgs& da, const ConvArgs& wa, float* dw, const PairGrid& pg, hipStream_t s,
+                   const OptTail& ot) {
   size_t lds = (size_t)kStages * (BM + BN) * 64 * 2;
   const size_t epi = ((size_t)BM * (BN + 4) + 256 * 16 + 8) * sizeof(float);
   const size_t wl = (size_t)kStages * 2 * 64 * 128;
   lds = std::max(lds, std::max(epi, wl));
   static bool attr = false;
   set_lds_limit(&conv_bwd_pair_kernel<BM, BN, KS, ST, PAR>, lds, attr);
-  const unsigned n = (unsigned)(pg.dgx * pg.dgy * pg.dgz + pg.wgx * pg.wgy * pg.wgz);
-  conv_bwd_pair_kernel<BM, BN, KS, ST, PAR><<<n, 256, lds, s>>>(da, wa, dw, pg);
+  const unsigned n = (unsigned)(pg.dgx * pg.dgy * pg.dgz + pg.wgx * pg.wgy * pg.wgz + ot.nblk);
+  conv_bwd_pair_kernel<BM, BN, KS, ST, PAR><<<n, 256, lds, s>>>(da, wa, dw, pg, ot);
 }
 
 template <int BM, int BN>
-bool launch_pair_bm(const ConvArgs& da, const ConvArgs& wa, float* dw, const PairGrid& pg, hipStream_t s) {
+bool launch_pair_bm(const ConvArgs& da, const ConvArgs& wa, float* dw, const PairGrid& pg, hipStream_t s,
+                    const OptTail& ot) {
   const int ks = da.g.R, st = da.g.stride;
-  if (ks == 3 && st == 1) launch_pair_t<BM, BN, 3, 1, false>(da, wa, dw, pg, s);
-  else if (ks == 3 && st == 2 && da.par_mc) launch_pair_t<BM, BN, 3, 2, true>(da, wa, dw, pg, s);
-  else if (ks == 3 && st == 2) launch_pair_t<BM, BN, 3, 2, false>(da, wa, dw, pg, s);
-  else if (ks == 1 && st == 2) launch_pair_t<BM, BN, 1, 2, false>(da, wa, dw, pg, s);
+  if (ks == 3 && st == 1) launch_pair_t<BM, BN, 3, 1, false>(da, wa, dw, pg, s, ot);
+  else if (ks == 3 && st == 2 && da.par_mc) launch_pair_t<BM, BN, 3, 2, true>(da, wa, dw, pg, s, ot);
+  else if (ks == 3 && st == 2) launch_pair_t<BM, BN, 3, 2, false>(da, wa, dw, pg, s, ot);
+  else if (ks == 1 && st == 2) launch_pair_t<BM, BN, 1, 2, false>(da, wa, dw, pg, s, ot);
   else return false;
   return true;
 }
@@ -996,7 +1003,7 @@ bool conv_pair_enabled() {
 
 bool launch_conv_bwd_pair(const ConvGeom& gd, const ConvPlan& pd_in, const uint16_t* dy, const uint16_t* wt,
                           uint16_t* dx, float* ysplit, int* counters, bool accum, const BnBwdFusion* f,
-                          const ConvGeom& gw, const uint16_t* x, float* dw, hipStream_t s) {
+                          const ConvGeom& gw, const uint16_t* x, float* dw, hipStream_t s, const OptTail* ot) {
   if (!conv_pair_enabled()) return false;
   if (!((pd_in.bm == 128 && pd_in.bn == 64) || (pd_in.bm == 64 && pd_in.bn == 64))) return false;
   static const int wg_target = env_int("MFL_PAIR_WGRAD_TARGET", 0);
@@ -1049,8 +1056,9 @@ bool launch_conv_bwd_pair(const ConvGeom& gd, const ConvPlan& pd_in, const uint1
   pg.wgz = pw.splits;
   static const int order = env_int("MFL_CONV_PAIR_ORDER", 0);
   pg.order = order;
-  if (pd.bm == 128) return launch_pair_bm<128, 64>(da, wa, dw, pg, s);
-  return launch_pair_bm<64, 64>(da, wa, dw, pg, s);
+  const OptTail tail = ot ? *ot : OptTail{};
+  if (pd.bm == 128) return launch_pair_bm<128, 64>(da, wa, dw, pg, s, tail);
+  return launch_pair_bm<64, 64>(da, wa, dw, pg, s, tail);
 }
 
 namespace {

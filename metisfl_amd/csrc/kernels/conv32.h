@@ -3,6 +3,7 @@
 #pragma once
 #include "kernels/conv.h"
 #include "kernels/launchers.h"
+#include "kernels/opt_tail.h"
 
 namespace mfl {
 
@@ -46,28 +47,6 @@ struct BnBwdFusion32 {
   const float* invstd = nullptr;
   double* acc = nullptr;
   int reps = 1;
-};
-
-// Optimizer tail of a paired backward launch: workgroups appended after the
-// dgrad / wgrad ones apply the fused optimizer (opt_body.h) to a range of the
-// flat model whose gradients are already final (a later layer's), so its
-// HBM-bound pass fills the CUs the latency-bound GEMMs leave idle instead of
-// running as the step's last launch.  nblk == 0: no tail.
-struct OptTail {
-  float* p = nullptr;
-  float* g = nullptr;
-  float* m = nullptr;
-  float* v = nullptr;
-  const float* anchor = nullptr;
-  void* mirror = nullptr;
-  int64_t n4 = 0;        // float4 elements
-  OptHyper h{};
-  const float* lr_ptr = nullptr;
-  const int* step_ptr = nullptr;
-  int mode = 0;          // OptMode
-  int mirror_kind = 0;   // 0 none, 2 packed bf16x3 split
-  int zero_grad = 1;
-  int nblk = 0;
 };
 
 // The API exists twice: mfl::c32x (exact fp32 MFMA) and mfl::c32s (fp32

@@ -58,7 +58,7 @@
 
 #include "kernels/common.h"
 #include "kernels/conv32.h"
-#include "kernels/opt_body.h"
+#include "kernels/opt_tail_dev.h"
 #include "kernels/lds_tiles.h"
 
 // Built twice (csrc/build.py): MFL_C32_BF16X3=0 -> namespace mfl::c32x (exact
@@ -952,31 +952,6 @@ __global__ __launch_bounds__(256, 2) void conv32_fwd_pair_kernel(Conv32Args a1, 
     const Blk k{w % g2x, (w / g2x) % g2y, w / (g2x * g2y), g2x, g2y, g2z};
     conv32_gemm_body<64, 64, false, 1, 2, false, NS, false>(a2, k, smem);
   }
-}
-
-// The optimizer tail's grid-stride pass over its range (workgroup t of n).
-template <int MODE, int MIRROR>
-__device__ __forceinline__ void opt_tail_loop(const OptTail& o, int t, int n, float lr, float bc1, float bc2) {
-  const int64_t stride = (int64_t)n * 256;
-  for (int64_t i = (int64_t)t * 256 + threadIdx.x; i < o.n4; i += stride)
-    opt_update4<MODE, MIRROR>(o.p, o.g, o.m, o.v, o.anchor, o.mirror, i, o.h, lr, bc1, bc2, o.zero_grad != 0);
-}
-template <int MIRROR>
-__device__ __forceinline__ void opt_tail_mirror(const OptTail& o, int t, int n) {
-  const float lr = o.lr_ptr ? o.lr_ptr[0] * o.h.lr : o.h.lr;
-  float bc1, bc2;
-  opt_bias_corr(o.mode, o.h, o.step_ptr, bc1, bc2);
-  switch (o.mode) {
-    case OPT_SGD: opt_tail_loop<OPT_SGD, MIRROR>(o, t, n, lr, bc1, bc2); break;
-    case OPT_MOMENTUM: opt_tail_loop<OPT_MOMENTUM, MIRROR>(o, t, n, lr, bc1, bc2); break;
-    case OPT_FEDPROX: opt_tail_loop<OPT_FEDPROX, MIRROR>(o, t, n, lr, bc1, bc2); break;
-    case OPT_ADAM: opt_tail_loop<OPT_ADAM, MIRROR>(o, t, n, lr, bc1, bc2); break;
-    default: opt_tail_loop<OPT_ADAMW, MIRROR>(o, t, n, lr, bc1, bc2); break;
-  }
-}
-__device__ __forceinline__ void opt_tail_body(const OptTail& o, int t) {
-  if (o.mirror_kind == 2) opt_tail_mirror<2>(o, t, o.nblk);
-  else opt_tail_mirror<0>(o, t, o.nblk);
 }
 
 template <int KS, int ST, bool PAR, int NS>

@@ -240,6 +240,242 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ x, int 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split head (the fused-BN path, C % 128 == 0): the one-sample-per-workgroup
+// kernel above is a serial chain of ~8 dependent phases on 32 of the 256 CUs
+// (24.7 us at batch 32, ~2.4 % of the fp32 step).  Here a workgroup owns one
+// sample's 128-channel group (B x C/128 workgroups) and the chain is cut in
+// two launches: (A) BN coefficients, relu(BN(z) + res) -> y, pooling, and
+// the group's partial logits; (B) logits (partials summed in a fixed order,
+// so every group of a sample computes identical values), softmax / loss,
+// dlogits, dW / db, dx and the BN-backward sums of dx -- each group for its
+// own channels.
+constexpr int kHeadCW = 128;  // channels per workgroup (16 lane groups x 8)
+constexpr int kHeadMaxPix = 4;  // pixel rows per thread kept in registers (HW <= 64)
+
+template <typename T>
+__global__ __launch_bounds__(256) void head_split_fwd_kernel(int HW, int C, const float* __restrict__ W, int K,
+                                                             float* __restrict__ feat, float* __restrict__ lpart,
+                                                             int B, HeadBn hb) {
+  __shared__ float sc[kHeadCW], sh[kHeadCW], f[kHeadCW];
+  __shared__ float part[16 * kHeadCW];
+  const int CG = C / kHeadCW;
+  const int b = blockIdx.x / CG, cg = blockIdx.x - b * CG, c0 = cg * kHeadCW;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int lgp = t & 15, rg = t >> 4;  // 8-channel lane group, pixel row group
+  // the activation loads go out before the coefficients' fp64 sums
+  float zz[kHeadMaxPix][8], rr[kHeadMaxPix][8];
+#pragma unroll
+  for (int j = 0; j < kHeadMaxPix; ++j) {
+    const int h = rg + 16 * j;
+    if (h < HW) {
+      const int64_t o = ((int64_t)b * HW + h) * C + c0 + 8 * lgp;
+      load8(reinterpret_cast<const T*>(hb.z) + o, zz[j]);
+      load8(reinterpret_cast<const T*>(hb.res) + o, rr[j]);
+    }
+  }
+  if (t < kHeadCW) {
+    float a, bb;
+    bn_fwd_coef(hb.acc, hb.reps, C, c0 + t, (int64_t)B * HW, hb.train != 0, b == 0, hb.gamma, hb.beta, hb.mean,
+                hb.invstd, hb.run_mean, hb.run_var, hb.momentum, hb.eps, a, bb);
+    sc[t] = a;
+    sh[t] = bb;
+  }
+  __syncthreads();
+  float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < kHeadMaxPix; ++j) {
+    const int h = rg + 16 * j;
+    if (h >= HW) break;
+    const int64_t o = ((int64_t)b * HW + h) * C + c0 + 8 * lgp;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fmaxf(fmaf(zz[j][k], sc[8 * lgp + k], sh[8 * lgp + k]) + rr[j][k], 0.f);
+    T* yo = reinterpret_cast<T*>(hb.y) + o;
+    Pack8 pk;
+    pack_out(v, yo, pk);
+    store8(yo, pk);
+    if constexpr (sizeof(T) == 2) unpack8(pk.h, v);  // bf16: the pooled value is the stored y
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s8[k] += v[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) part[rg * kHeadCW + 8 * lgp + k] = s8[k];
+  __syncthreads();
+  if (t < kHeadCW) {
+    float a = 0.f;
+    for (int r = 0; r < 16; ++r) a += part[r * kHeadCW + t];
+    a *= 1.f / (float)HW;
+    f[t] = a;
+    feat[(int64_t)b * C + c0 + t] = a;
+  }
+  __syncthreads();
+  for (int k = wv; k < K; k += 4) {
+    const float* wr = W + (int64_t)k * C + c0;
+    float a = f[lane] * wr[lane] + f[lane + 64] * wr[lane + 64];
+    a = wave_sum(a);
+    if (lane == 0) lpart[((int64_t)b * CG + cg) * K + k] = a;
+  }
+}
+
+// Every load that does not depend on the logits (the group's W slice into
+// LDS, feat, this thread's y / z pixels, mean / invstd) is issued before the
+// partial logits are summed, so their latency overlaps the softmax instead
+// of following it (the first version, loading them after, ran 16 us).
+template <typename T>
+__global__ __launch_bounds__(256) void head_split_bwd_kernel(int HW, int C, const float* __restrict__ W,
+                                                             const float* __restrict__ bias, int K,
+                                                             const int* __restrict__ labels,
+                                                             const float* __restrict__ feat,
+                                                             const float* __restrict__ lpart,
+                                                             float* __restrict__ dlog, T* __restrict__ dx,
+                                                             float* __restrict__ stats, int B, int backward,
+                                                             float* __restrict__ dW, float* __restrict__ db,
+                                                             HeadBn hb) {
+  extern __shared__ __attribute__((aligned(16))) float dyn[];  // lg[K] | Ws[K][128]
+  float* lg = dyn;
+  float* Ws = dyn + ((K + 3) & ~3);
+  __shared__ float part[2][16 * kHeadCW];
+  const int CG = C / kHeadCW;
+  const int b = blockIdx.x / CG, cg = blockIdx.x - b * CG, c0 = cg * kHeadCW;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int lgp = t & 15, rg = t >> 4;
+  const bool sums = backward && hb.acc_b;
+  // independent loads first
+  float yy[kHeadMaxPix][8], zz[kHeadMaxPix][8], mu[8], isd[8];
+  float fc = 0.f;
+  if (backward) {
+    for (int i = t; i < K * kHeadCW; i += 256) {
+      const int k = i / kHeadCW, c = i - k * kHeadCW;
+      Ws[i] = W[(int64_t)k * C + c0 + c];
+    }
+    if (t < kHeadCW) fc = feat[(int64_t)b * C + c0 + t];
+    if (sums) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        mu[k] = hb.mean[c0 + 8 * lgp + k];
+        isd[k] = hb.invstd[c0 + 8 * lgp + k];
+      }
+#pragma unroll
+      for (int j = 0; j < kHeadMaxPix; ++j) {
+        const int h = rg + 16 * j;
+        if (h < HW) {
+          const int64_t o = ((int64_t)b * HW + h) * C + c0 + 8 * lgp;
+          load8(reinterpret_cast<const T*>(hb.y) + o, yy[j]);
+          load8(reinterpret_cast<const T*>(hb.z) + o, zz[j]);
+        }
+      }
+    }
+  }
+  for (int k = t; k < K; k += 256) {
+    float a = bias ? bias[k] : 0.f;
+    for (int g = 0; g < CG; ++g) a += lpart[((int64_t)b * CG + g) * K + k];
+    lg[k] = a;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    float mx = -INFINITY;
+    for (int k = lane; k < K; k += 64) mx = fmaxf(mx, lg[k]);
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int k = lane; k < K; k += 64) se += hexp<T>(lg[k] - mx);
+    se = wave_sum(se);
+    const int y = labels[b];
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int k = lane; k < K; k += 64) {
+      if (lg[k] > best) { best = lg[k]; bi = k; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    const float lse = mx + hlog<T>(se);
+    if (lane == 0 && cg == 0 && stats && y >= 0) {
+      atomicAdd(&stats[0], lse - lg[y]);
+      atomicAdd(&stats[1], bi == y ? 1.f : 0.f);
+      atomicAdd(&stats[2], 1.f);
+    }
+    if (backward) {
+      const float invB = 1.f / (float)B;
+      for (int k = lane; k < K; k += 64) {  // each lane reads and writes only its own k
+        const float d = (hexp<T>(lg[k] - lse) - (k == y ? 1.f : 0.f)) * invB;
+        lg[k] = d;
+        if (cg == 0) {
+          dlog[(int64_t)b * K + k] = d;
+          if (db) atomicAdd(&db[k], d);
+        }
+      }
+    }
+  }
+  if (!backward) return;
+  __syncthreads();
+  if (dW && t < kHeadCW) {
+    for (int k = 0; k < K; ++k) atomicAdd(&dW[(int64_t)k * C + c0 + t], lg[k] * fc);
+  }
+  const float inv_hw = 1.f / (float)HW;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float a = 0.f;
+    for (int k = 0; k < K; ++k) a += lg[k] * Ws[k * kHeadCW + 8 * lgp + e];
+    v[e] = a * inv_hw;
+  }
+  Pack8 pk;
+  T* dxb = dx + (int64_t)b * HW * C + c0 + 8 * lgp;
+  pack_out(v, dxb, pk);
+  float gs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, gq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < kHeadMaxPix; ++j) {
+    const int h = rg + 16 * j;
+    if (h >= HW) break;
+    store8(dxb + (int64_t)h * C, pk);
+    if (sums) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float g = yy[j][k] > 0.f ? v[k] : 0.f;
+        gs[k] += g;
+        gq[k] += g * ((zz[j][k] - mu[k]) * isd[k]);
+      }
+    }
+  }
+  if (!sums) return;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    part[0][rg * kHeadCW + 8 * lgp + k] = gs[k];
+    part[1][rg * kHeadCW + 8 * lgp + k] = gq[k];
+  }
+  __syncthreads();
+  if (t < 2 * kHeadCW) {
+    const int pass = t / kHeadCW, c = t - pass * kHeadCW;
+    double a = 0.0;
+    for (int r = 0; r < 16; ++r) a += part[pass][r * kHeadCW + c];
+    atomicAdd(&hb.acc_b[(int64_t)(b % hb.reps_b) * 2 * C + pass * C + c0 + c], a);
+  }
+}
+
+// MFL_HEAD_SPLIT=0: the one-launch head for A/B runs
+static bool head_split_ok(int C, int HW, int K) {
+  const char* e = getenv("MFL_HEAD_SPLIT");
+  const int on = e && *e ? atoi(e) : 1;
+  return on && C % kHeadCW == 0 && HW >= 1 && HW <= 16 * kHeadMaxPix && K <= 64;
+}
+
+template <typename T>
+static void head_split_launch(int B, int HW, int C, const float* W, const float* bias, int K, const int* labels,
+                              float* feat, float* dlogits, T* dx, float* stats, bool backward, hipStream_t s,
+                              float* dW, float* db, const HeadBn& hb, float* lpart) {
+  const int n = B * (C / kHeadCW);
+  head_split_fwd_kernel<T><<<n, 256, 0, s>>>(HW, C, W, K, feat, lpart, B, hb);
+  const size_t dyn = ((size_t)((K + 3) & ~3) + (size_t)K * kHeadCW) * sizeof(float);
+  head_split_bwd_kernel<T><<<n, 256, dyn, s>>>(HW, C, W, bias, K, labels, feat, lpart,
+                                                                    dlogits, dx, stats, B, backward ? 1 : 0,
+                                                                    backward ? dW : nullptr,
+                                                                    backward ? db : nullptr, hb);
+}
+
 template <typename T, bool FUSE>
 static void head_launch_t(const T* x, int B, int HW, int C, const float* W, const float* bias, int K,
                           const int* labels, float* feat, float* dlogits, T* dx, float* stats, bool backward,
@@ -266,10 +502,16 @@ static void head_launch(const T* x, int B, int HW, int C, const float* W, const 
 
 void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,
                          int K, const int* labels, float* feat, float* dlogits, uint16_t* dx,
-                         float* stats, bool backward, hipStream_t s, float* dW, float* db, const HeadBn* bn) {
+                         float* stats, bool backward, hipStream_t s, float* dW, float* db, const HeadBn* bn,
+                         float* lpart) {
   if (bn) {
     HeadBn hb = *bn;
     if (!backward) hb.acc_b = nullptr;
+    if (lpart && feat && head_split_ok(C, HW, K)) {
+      head_split_launch<uint16_t>(B, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, backward, s, dW, db, hb,
+                                  lpart);
+      return;
+    }
     head_launch_t<uint16_t, true>(x, B, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, backward, s, dW, db,
                                   hb);
     return;
@@ -278,10 +520,15 @@ void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W
 }
 void launch_head32_fwd_bwd(const float* x, int B, int HW, int C, const float* W, const float* bias, int K,
                            const int* labels, float* feat, float* dlogits, float* dx, float* stats, bool backward,
-                           hipStream_t s, float* dW, float* db, const HeadBn* bn) {
+                           hipStream_t s, float* dW, float* db, const HeadBn* bn, float* lpart) {
   if (bn) {
     HeadBn hb = *bn;
     if (!backward) hb.acc_b = nullptr;
+    if (lpart && feat && head_split_ok(C, HW, K)) {
+      head_split_launch<float>(B, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, backward, s, dW, db, hb,
+                               lpart);
+      return;
+    }
     head_launch_t<float, true>(x, B, HW, C, W, bias, K, labels, feat, dlogits, dx, stats, backward, s, dW, db, hb);
     return;
   }

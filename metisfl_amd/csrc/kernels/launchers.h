@@ -183,13 +183,16 @@ struct HeadBn {
   double* acc_b = nullptr;
   int reps_b = 1;
 };
+// lpart (fused-BN path): [B][C / 128][K] fp32 scratch of the split head
+// (head.hip head_split_*); nullptr: the one-launch head
 void launch_head32_fwd_bwd(const float* x, int B, int HW, int C, const float* W, const float* bias, int K,
                            const int* labels, float* feat, float* dlogits, float* dx, float* stats, bool backward,
-                           hipStream_t s, float* dW = nullptr, float* db = nullptr, const HeadBn* bn = nullptr);
+                           hipStream_t s, float* dW = nullptr, float* db = nullptr, const HeadBn* bn = nullptr,
+                           float* lpart = nullptr);
 void launch_head_fwd_bwd(const uint16_t* x, int B, int HW, int C, const float* W, const float* bias,
                          int K, const int* labels, float* feat, float* dlogits, uint16_t* dx,
                          float* stats, bool backward, hipStream_t s, float* dW = nullptr,
-                         float* db = nullptr, const HeadBn* bn = nullptr);
+                         float* db = nullptr, const HeadBn* bn = nullptr, float* lpart = nullptr);
 void launch_head_wgrad(const float* feat, const float* dlogits, int B, int C, int K, float* dW,
                        float* db, hipStream_t s);
 

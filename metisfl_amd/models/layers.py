@@ -406,7 +406,7 @@ class ConvBN(Layer):
         if dx is not None and not self.ws.overlap:
             # both GEMMs in one launch (their workgroups share the CUs); the
             # fp32 launch also carries the next optimizer tail, if any
-            opt = self.ws.take_opt_tail() if self.dz.dtype == torch.float32 else None
+            opt = self.ws.take_opt_tail()
             K.conv_backward_pair(self.x, self.dz, self.dw, self.w16, dx, s, self._split(), accumulate,
                                  bnb=bnb, wp=self.wp, dy_packed=pk, xp=self.xp, opt=opt)
             return

@@ -152,12 +152,12 @@ class BnBwdTarget:
     acc: torch.Tensor
 
 
-def _bnb_sums_cpu(dx: torch.Tensor, t: BnBwdTarget) -> None:
+def _bnb_sums_cpu(dx: torch.Tensor, t: BnBwdTarget, store_masked: bool = True) -> None:
     C = dx.shape[-1]
     g = dx.float().reshape(-1, C)
     if t.y is not None:
         g = torch.where(t.y.float().reshape(-1, C) > 0, g, torch.zeros_like(g))
-        if dx.dtype == torch.float32:  # as the fp32 GPU epilogue: dX is stored masked
+        if store_masked and dx.dtype == torch.float32:  # as the fp32 GPU dgrad epilogue: dX is stored masked
             dx.copy_(g.view(dx.shape))
     xh = (t.z.float().reshape(-1, C) - t.mean) * t.invstd
     t.acc[:C] += g.double().sum(0)
@@ -259,22 +259,25 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
             ops().conv32_backward_pair(xa, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
                                        bnb.invstd, bnb.acc, wp, *tail)
         return
-    _conv_backward_pair_unfused(x, dy, dw, w, dx, shp, ws, accumulate, bnb, wp)
-    if opt is not None:
+    if not _conv_backward_pair_unfused(x, dy, dw, w, dx, shp, ws, accumulate, bnb, wp, opt) and opt is not None:
         opt.run()
 
 
-def _conv_backward_pair_unfused(x, dy, dw, w, dx, shp, ws, accumulate, bnb, wp) -> None:
+def _conv_backward_pair_unfused(x, dy, dw, w, dx, shp, ws, accumulate, bnb, wp, opt=None) -> bool:
+    """-> whether ``opt`` (an optimizer tail) was taken by the launch."""
     if dy.is_cuda:
+        from metisfl_amd.ops.optim import NO_OPT_TAIL
+        tail = opt.binding_args() if opt is not None else NO_OPT_TAIL
         if bnb is None:
             ops().conv_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, None, None, None, None,
-                                     None)
+                                     None, *tail)
         else:
             ops().conv_backward_pair(x, dy, dw, w, dx, ws, *shp.args(), accumulate, bnb.z, bnb.y, bnb.mean,
-                                     bnb.invstd, bnb.acc)
-        return
+                                     bnb.invstd, bnb.acc, *tail)
+        return True
     conv_wgrad(x, dy, dw, shp, accumulate=True)
     conv_dgrad(dy, w, dx, shp, ws, accumulate, bnb=bnb, wp=wp)
+    return False
 
 
 def transpose_krsc(w, wt, Co: int, RS: int, Ci: int) -> None:
@@ -579,7 +582,7 @@ def head_forward_backward_bn(B: int, HW: int, C: int, W, bias, labels, feat, dlo
              relu=True, train=train, momentum=bn.momentum, eps=bn.eps)
     head_forward_backward(y, B, HW, C, W, bias, labels, feat, dlogits, dx, stats, backward, dW, db)
     if backward and acc_b is not None:
-        _bnb_sums_cpu(dx, BnBwdTarget(z, y, bn.mean, bn.invstd, acc_b[:2 * C]))
+        _bnb_sums_cpu(dx, BnBwdTarget(z, y, bn.mean, bn.invstd, acc_b[:2 * C]), store_masked=False)
 
 
 def head_wgrad(feat, dlogits, B: int, C: int, K: int, dW, db) -> None:

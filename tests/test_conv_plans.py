@@ -1,0 +1,44 @@
+"""The fp32 convolution plan table (conv32.hip kTuned, queried through the
+host-side planner -- no GPU needed) and the MFL_C32_PLANS override used by
+whole-step plan sweeps (scripts/gpu_plans/r4_plans*.txt)."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CODE = """
+from metisfl_amd.ops._native import ops
+o = ops(); o.set_conv32_mode(1)
+for s in [(32,16,16,128,128,3,3,1,1), (32,32,32,64,64,3,3,1,1), (32,4,4,512,512,3,3,1,1)]:
+    d, w = o.conv32_plan(1, *s), o.conv32_plan(2, *s)
+    print(d[0], d[1], d[2], w[0], w[1], w[2])
+"""
+
+
+def _plans(env_extra=None):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("MFL_C32_PLANS", None)
+    env.update(env_extra or {})
+    out = subprocess.run([sys.executable, "-c", CODE], env=env, capture_output=True, text=True, cwd=ROOT,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    return [tuple(int(v) for v in line.split()) for line in out.stdout.strip().splitlines()]
+
+
+def test_paired_backward_plans_fill_one_wave():
+    """Every stride-1 3x3 backward pair of ResNet-18 at batch 32 runs 64x64
+    tiles (the pairing condition); the 16x16x128 pair is dgrad 2 x wgrad 7
+    slices = 764 workgroups, one wave of 3 per CU (profiles/r4/plans/)."""
+    l2, l1, l4 = _plans()
+    assert l2 == (64, 64, 2, 64, 64, 7)
+    assert l1[:2] == (64, 64) and l1[3:5] == (64, 64)
+    assert l4[:2] == (64, 64) and l4[3:5] == (64, 64)
+    tiles_d = (32 * 16 * 16 // 64) * (128 // 64)
+    tiles_w = (128 // 64) * (128 * 9 // 64)
+    assert tiles_d * l2[2] + tiles_w * l2[5] <= 3 * 256
+
+
+def test_plan_override_env():
+    l2, l1, _ = _plans({"MFL_C32_PLANS": "1,16,128,128,3,1,4;2,16,128,128,3,1,3"})
+    assert l2[2] == 4 and l2[5] == 3
+    assert l1 == _plans()[1]  # other shapes untouched

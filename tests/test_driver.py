@@ -110,6 +110,7 @@ def test_driver_runs_rccl_data_plane_collective(tmp_path):
     sess = DriverSession(fe, StaticModelDef("resnet18", width_mult=0.125), train_recipe, None, eval_recipe,
                          working_dir=str(tmp_path / "w"), device="cpu")
     stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason  # not the time cutoff
     assert set(stats) == {"learners_descriptor", "learners_models_results", "federation_runtime_metadata",
                           "community_model_results"}
     md = stats["federation_runtime_metadata"]["metadata"]

@@ -58,6 +58,7 @@ def test_collective_asynchronous_protocol_through_the_driver(tmp_path):
     sess = _session(tmp_path, 3, rounds=8, protocol="Asynchronous",
                     extra={"debug_delay_s": {"2": 0.6, "1": 0.1}})
     stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason  # not the time cutoff
     md = stats["federation_runtime_metadata"]["metadata"]
     gis = sorted(int(m["global_iteration"]) for m in md)
     assert gis[:8] == list(range(1, 9))  # one record per community version (FedRec update)
@@ -74,6 +75,7 @@ def test_collective_recovers_from_a_lost_rank(tmp_path):
     sess = _session(tmp_path, 3, rounds=3, fault={"rank": 2, "round": 2}, heartbeat_timeout_s=10,
                     checkpoint_every=1)
     stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason  # not the time cutoff
     assert len(sess.recoveries) == 1
     rc = sess.recoveries[0]
     assert rc["failed"] == ["learner_localhost-2"] and rc["survivors"] == 2 and rc["resumed_from_round"] == 1
@@ -105,6 +107,7 @@ def test_collective_recovers_from_a_sigkilled_rank(tmp_path):
     sess = _session(tmp_path, 3, rounds=3, fault={"rank": 1, "round": 2, "signal": "KILL"}, heartbeat_timeout_s=10,
                     checkpoint_every=1)
     stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason  # not the time cutoff
     rc = _recovered(sess, tmp_path, "learner_localhost-1", 1, 2)
     assert rc["exit_code"] == -9
     md = stats["federation_runtime_metadata"]["metadata"]
@@ -118,6 +121,7 @@ def test_collective_recovers_when_rank0_dies(tmp_path):
     sess = _session(tmp_path, 3, rounds=3, fault={"rank": 0, "round": 2}, heartbeat_timeout_s=8,
                     checkpoint_every=1)
     stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason  # not the time cutoff
     _recovered(sess, tmp_path, "learner_localhost-0", 1, 2)
     md = stats["federation_runtime_metadata"]["metadata"]
     by_gi = {}
@@ -136,6 +140,7 @@ def test_async_collective_recovers_from_a_lost_rank(tmp_path):
     sess = _session(tmp_path, 3, rounds=10, protocol="Asynchronous", fault={"rank": 2, "round": 2},
                     heartbeat_timeout_s=8, checkpoint_every=1, extra={"debug_delay_s": {"0": 0.3, "1": 0.3}})
     stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason  # not the time cutoff
     rc = _recovered(sess, tmp_path, "learner_localhost-2", sess.recoveries[0]["resumed_from_round"], 2)
     assert rc["resumed_from_round"] is not None and rc["resumed_from_round"] >= 1
     log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
@@ -144,9 +149,8 @@ def test_async_collective_recovers_from_a_lost_rank(tmp_path):
     assert "dropped old ranks [2]" in line[-1]
     md = stats["federation_runtime_metadata"]["metadata"]
     assert max(int(m["global_iteration"]) for m in md) >= 10
-    # the federation ends on its version budget with BOTH survivors served
-    # after the resume (not on the time cutoff with rank 1 never served)
-    assert sess.termination_reason == "rounds", sess.termination_reason
+    # BOTH survivors were served after the resume (before the fix rank 1
+    # never was, and the run ended on the time cutoff)
     after = {lid for m in md if int(m["global_iteration"]) > rc["resumed_from_round"]
              for lid in m.get("completed_by_learner_id", [])}
     assert len(after) == 2, after
@@ -239,6 +243,7 @@ def test_learners_sharing_a_device_are_colocated_in_one_rank(tmp_path):
                          None, eval_recipe, working_dir=str(tmp_path / "w"), device="cpu",
                          collective_options={"checkpoint_every": 1})
     stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason  # not the time cutoff
     assert [len(g) for g in sess._collective_groups] == [2, 1]
     job = json.load(open(os.path.join(str(tmp_path / "w"), "collective_job.json")))
     assert job["ranks"] == [[0, 1], [2]]

@@ -495,3 +495,51 @@ def test_bf16x3_weight_mirror_tracks_master():
     net.state.refresh_bf16()
     torch.cuda.synchronize()
     assert torch.equal(net.state.psplit.cpu(), ref())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,HW,C", [(32, 16, 512), (8, 16, 256), (512, 16, 512)])
+def test_split_head_matches_one_launch_head(dtype, B, HW, C, monkeypatch):
+    """The split head (head.hip head_split_*: B x C/128 workgroups, two
+    launches) against the one-launch head on the same inputs: the BN apply
+    (y, published mean / invstd / running statistics) bit-identical, pooled
+    features / logits-derived outputs to fp32 summation order."""
+    from metisfl_amd.ops import nn as K
+    K_ = 10
+    g = torch.Generator(device="cpu").manual_seed(5)
+
+    def mk(*shape, scale=1.0):
+        return (torch.randn(*shape, generator=g) * scale).to(DEV)
+    z, res = mk(B, HW, C).to(dtype), mk(B, HW, C).to(dtype)
+    W, bias = mk(K_, C, scale=0.05), mk(K_, scale=0.1)
+    labels = torch.randint(0, K_, (B,), generator=g).to(torch.int32).to(DEV)
+    acc = torch.zeros(8 * 2 * C, dtype=torch.float64, device=DEV)
+    acc[: 2 * C] = torch.cat([z.double().reshape(-1, C).sum(0), (z.double().reshape(-1, C) ** 2).sum(0)]).to(DEV)
+    outs = {}
+    for split in ("0", "1"):
+        monkeypatch.setenv("MFL_HEAD_SPLIT", split)
+        bn = K.BnParams(acc.clone(), torch.ones(C, device=DEV) * 1.1, torch.full((C,), 0.05, device=DEV),
+                        torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), torch.zeros(C, device=DEV),
+                        torch.ones(C, device=DEV), 0.1, 1e-5)
+        y = torch.empty_like(z)
+        feat = torch.zeros(B * C, device=DEV)
+        dlog = torch.zeros(B * K_, device=DEV)
+        dx = torch.empty_like(z)
+        stats = torch.zeros(4, device=DEV)
+        dW, db = torch.zeros(K_, C, device=DEV), torch.zeros(K_, device=DEV)
+        acc_b = torch.zeros(8 * 2 * C, dtype=torch.float64, device=DEV)
+        K.head_forward_backward_bn(B, HW, C, W, bias, labels, feat, dlog, dx, stats, True, dW, db, z, res, bn,
+                                   True, y, acc_b)
+        torch.cuda.synchronize()
+        outs[split] = dict(y=y, feat=feat, dlog=dlog, dx=dx, stats=stats, dW=dW, db=db, acc_b=acc_b,
+                           mean=bn.mean, invstd=bn.invstd, rm=bn.run_mean, rv=bn.run_var)
+    a, b = outs["0"], outs["1"]
+    for k in ("y", "mean", "invstd", "rm", "rv"):
+        assert torch.equal(a[k], b[k]), k
+    for k in ("feat", "dlog", "dx", "dW", "db", "acc_b"):
+        ref = a[k].double()
+        rel = float((b[k].double() - ref).abs().max() / max(1e-30, float(ref.abs().max())))
+        # bf16 dx: a summation-order difference can flip one bf16 rounding (2^-8)
+        tol = 2e-5 if (dtype == torch.float32 or k != "dx") else 8e-3
+        assert rel <= tol, (k, rel)
+    assert torch.allclose(a["stats"], b["stats"], rtol=1e-5, atol=1e-3)

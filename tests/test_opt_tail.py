@@ -10,12 +10,13 @@ import pytest
 import torch
 
 
-def _pair(device, chunk, monkeypatch, B=4, width=0.25, lr=0.05, kind="momentum_sgd"):
+def _pair(device, chunk, monkeypatch, B=4, width=0.25, lr=0.05, kind="momentum_sgd", dtype="fp32"):
     from metisfl_amd.models.layers import OptTailScheduler
     from metisfl_amd.models.resnet import ResNet18
     from metisfl_amd.ops.optim import OptimizerSpec
     spec = OptimizerSpec(kind, lr, momentum=0.75) if kind == "momentum_sgd" else OptimizerSpec(kind, lr)
-    nets = [ResNet18(batch_size=B, device=device, seed=3, width_mult=width, optimizer=spec) for _ in range(2)]
+    nets = [ResNet18(batch_size=B, device=device, seed=3, width_mult=width, optimizer=spec, dtype=dtype)
+            for _ in range(2)]
     return nets, OptTailScheduler
 
 
@@ -77,9 +78,10 @@ def test_opt_tails_are_bitwise_on_host(kind, chunk, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_opt_tails_graph_full_width(monkeypatch):
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_opt_tails_graph_full_width(monkeypatch, dtype):
     B = 32
-    (base, tail), S = _pair("cuda", 0, monkeypatch, B=B, width=1.0, lr=0.0)
+    (base, tail), S = _pair("cuda", 0, monkeypatch, B=B, width=1.0, lr=0.0, dtype=dtype)
     x, y = _data(512)
     dsb = base.make_dataset(x, y, seed=1)
     dst = tail.make_dataset(x, y, seed=1)
@@ -94,7 +96,8 @@ def test_opt_tails_graph_full_width(monkeypatch):
     # lr 0: nothing moves, the mirror stays the split of the master, every
     # gradient range was consumed and re-zeroed
     assert torch.equal(base.state.model32, tail.state.model32)
-    assert torch.equal(base.state.psplit, tail.state.psplit)
+    mirror = "psplit" if dtype == "fp32" else "p16"
+    assert torch.equal(getattr(base.state, mirror), getattr(tail.state, mirror))
     assert float(tail.state.grad32.abs().max()) == 0.0
     assert int(tail.state.step) == 16
 
