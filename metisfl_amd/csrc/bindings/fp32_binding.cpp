@@ -518,7 +518,12 @@ bool stem_backward32_ok(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Co
 
 void stem_backward32(torch::Tensor dy, torch::Tensor z, torch::Tensor y, torch::Tensor gamma, torch::Tensor mean,
                      torch::Tensor invstd, torch::Tensor acc, c10::optional<torch::Tensor> dgamma,
-                     c10::optional<torch::Tensor> dbeta, torch::Tensor x, torch::Tensor dw) {
+                     c10::optional<torch::Tensor> dbeta, torch::Tensor x, torch::Tensor dw,
+                     c10::optional<torch::Tensor> opt_p, c10::optional<torch::Tensor> opt_g,
+                     c10::optional<torch::Tensor> opt_m, c10::optional<torch::Tensor> opt_v,
+                     c10::optional<torch::Tensor> opt_anchor, c10::optional<torch::Tensor> opt_mirror,
+                     c10::optional<torch::Tensor> opt_lr_scale, c10::optional<torch::Tensor> opt_step,
+                     int64_t opt_mode, std::vector<double> opt_hyper, bool opt_zero_grad) {
   TORCH_CHECK(z.dim() == 4 && x.dim() == 4, "stem backward: NHWC tensors");
   const int64_t N = z.size(0), H = z.size(1), W = z.size(2), Co = z.size(3), Cin = x.size(3);
   TORCH_CHECK(x.size(0) == N && x.size(1) == H && x.size(2) == W, "stem backward: x / z shapes");
@@ -551,8 +556,16 @@ void stem_backward32(torch::Tensor dy, torch::Tensor z, torch::Tensor y, torch::
   if (dbeta.has_value() && dbeta->defined()) { check_pc(*dbeta, Co, "dbeta"); a.dbeta = fp(*dbeta); }
   a.M = z.numel() / Co;
   a.C = (int)Co;
-  if (bf) mfl::launch_stem_bwd_bf16(a, reinterpret_cast<const uint16_t*>(x.data_ptr()), (int)N, fp(dw), cur_stream(z));
-  else mfl::launch_stem_bwd32(a, fp(x), (int)N, (int)H, (int)W, (int)Cin, fp(dw), cur_stream(z));
+  // optimizer tail: the rest of the model (every variable but the stem's),
+  // final by now, rides in this launch (opt_tail.h)
+  mfl::OptTail ot;
+  const bool tail = opt_tail_args(ot, opt_p, opt_g, opt_m, opt_v, opt_anchor, opt_mirror, opt_lr_scale, opt_step,
+                                  opt_mode, opt_hyper, opt_zero_grad);
+  if (bf)
+    mfl::launch_stem_bwd_bf16(a, reinterpret_cast<const uint16_t*>(x.data_ptr()), (int)N, fp(dw), cur_stream(z),
+                              tail ? &ot : nullptr);
+  else
+    mfl::launch_stem_bwd32(a, fp(x), (int)N, (int)H, (int)W, (int)Cin, fp(dw), cur_stream(z), tail ? &ot : nullptr);
 }
 
 // ---- head / data ---------------------------------------------------------

@@ -8,6 +8,7 @@
 #include "kernels/common.h"
 #include "kernels/bn_coef.h"
 #include "kernels/launchers.h"
+#include "kernels/opt_tail_dev.h"
 
 namespace mfl {
 
@@ -370,7 +371,11 @@ __device__ __forceinline__ float4 ld4(const uint16_t* p) {
 
 template <typename T>
 __global__ __launch_bounds__(576) void stem_bwd32_kernel(BnBwdArgs32 a, const T* __restrict__ x, int N,
-                                                         float* __restrict__ dw) {
+                                                         float* __restrict__ dw, OptTail ot) {
+  if ((int)blockIdx.x >= (int)gridDim.x - ot.nblk) {  // optimizer tail (opt_tail.h), dispatched last
+    opt_tail_body(ot, blockIdx.x - (gridDim.x - ot.nblk));
+    return;
+  }
   constexpr int H = 32, W = 32, CI = 8, CO = 64, PX = H * W, XW = W + 2, G = kStemCG;
   constexpr int NV = PX * G / 4;            // float4 of dy / z / y per workgroup (2 per pixel)
   constexpr int NU = (NV + 575) / 576;
@@ -501,7 +506,8 @@ bool stem_bwd32_ok(int N, int H, int W, int Cin, int Co) {
 }
 
 template <typename T>
-static void stem_bwd_launch(const BnBwdArgs32& a, const T* x, int N, float* dw, hipStream_t s) {
+static void stem_bwd_launch(const BnBwdArgs32& a, const T* x, int N, float* dw, hipStream_t s, const OptTail* ot) {
+  const OptTail tail = ot ? *ot : OptTail{};
   const size_t lds = ((size_t)32 * 32 * kStemCG + (size_t)34 * 34 * 8 + 5 * kStemCG) * sizeof(float);
   static bool init = false;
   if (!init) {
@@ -509,18 +515,20 @@ static void stem_bwd_launch(const BnBwdArgs32& a, const T* x, int N, float* dw, 
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     init = true;
   }
-  stem_bwd32_kernel<T><<<(unsigned)(N * (64 / kStemCG)), 576, lds, s>>>(a, x, N, dw);
+  stem_bwd32_kernel<T><<<(unsigned)(N * (64 / kStemCG) + tail.nblk), 576, lds, s>>>(a, x, N, dw, tail);
 }
 
-void launch_stem_bwd32(const BnBwdArgs32& a, const float* x, int N, int H, int W, int Cin, float* dw, hipStream_t s) {
+void launch_stem_bwd32(const BnBwdArgs32& a, const float* x, int N, int H, int W, int Cin, float* dw, hipStream_t s,
+                       const OptTail* ot) {
   (void)H;
   (void)W;
   (void)Cin;
-  stem_bwd_launch(a, x, N, dw, s);
+  stem_bwd_launch(a, x, N, dw, s, ot);
 }
 
-void launch_stem_bwd_bf16(const BnBwdArgs32& a, const uint16_t* x, int N, float* dw, hipStream_t s) {
-  stem_bwd_launch(a, x, N, dw, s);
+void launch_stem_bwd_bf16(const BnBwdArgs32& a, const uint16_t* x, int N, float* dw, hipStream_t s,
+                          const OptTail* ot) {
+  stem_bwd_launch(a, x, N, dw, s, ot);
 }
 
 void launch_bn32_bwd_apply_pair(const BnBwdArgs32& a1, const BnBwdArgs32& a2, hipStream_t s) {

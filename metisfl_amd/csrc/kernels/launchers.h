@@ -156,9 +156,12 @@ void launch_bn32_bwd_apply_pair(const BnBwdArgs32& a1, const BnBwdArgs32& a2, hi
 // dw[Co][3][3][Cin] += sum_p dz[p] x[p + tap] (exact fp32 FMAs).  a.dx: unused;
 // x: the stem input [N][H][W][Cin] fp32.  Shapes: stem_bwd32_ok.
 bool stem_bwd32_ok(int N, int H, int W, int Cin, int Co);
-void launch_stem_bwd32(const BnBwdArgs32& a, const float* x, int N, int H, int W, int Cin, float* dw, hipStream_t s);
+struct OptTail;  // opt_tail.h: an optimizer tail riding in the stem backward launch (optional)
+void launch_stem_bwd32(const BnBwdArgs32& a, const float* x, int N, int H, int W, int Cin, float* dw, hipStream_t s,
+                       const OptTail* ot = nullptr);
 // the same with the bf16 option's dy / z / y / x (a.dy, a.x, a.y point at bf16)
-void launch_stem_bwd_bf16(const BnBwdArgs32& a, const uint16_t* x, int N, float* dw, hipStream_t s);
+void launch_stem_bwd_bf16(const BnBwdArgs32& a, const uint16_t* x, int N, float* dw, hipStream_t s,
+                          const OptTail* ot = nullptr);
 
 // ---- head.hip ------------------------------------------------------------
 // fp32 head whose input is relu(BN(z) + res), applied in its pooling loop

@@ -9,8 +9,8 @@ namespace opt_tail_detail {
 // The optimizer tail's grid-stride pass over its range (workgroup t of n).
 template <int MODE, int MIRROR>
 static __device__ __forceinline__ void opt_tail_loop(const OptTail& o, int t, int n, float lr, float bc1, float bc2) {
-  const int64_t stride = (int64_t)n * 256;
-  for (int64_t i = (int64_t)t * 256 + threadIdx.x; i < o.n4; i += stride)
+  const int64_t stride = (int64_t)n * blockDim.x;
+  for (int64_t i = (int64_t)t * blockDim.x + threadIdx.x; i < o.n4; i += stride)
     opt_update4<MODE, MIRROR>(o.p, o.g, o.m, o.v, o.anchor, o.mirror, i, o.h, lr, bc1, bc2, o.zero_grad != 0);
 }
 template <int MIRROR>

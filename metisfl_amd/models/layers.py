@@ -51,11 +51,12 @@ class OptTailScheduler:
         assert lo % self.ALIGN == 0
         self.ready = min(self.ready, lo)
 
-    def take(self):
-        """The next tail (an OptRange) or None."""
+    def take(self, everything: bool = False):
+        """The next tail (an OptRange) or None; ``everything``: all of the
+        final-but-not-updated range at once (the step's last backward launch)."""
         if self.chunk <= 0 or self.done <= self.ready:
             return None
-        lo = max(self.ready, (self.done - self.chunk) // self.ALIGN * self.ALIGN)
+        lo = self.ready if everything else max(self.ready, (self.done - self.chunk) // self.ALIGN * self.ALIGN)
         r = self.st.opt_range(lo, self.done, self.zero_grad)
         self.done = lo
         return r
@@ -75,8 +76,8 @@ class Workspace:
         self.bn_acc: torch.Tensor | None = None
         self.opt_tails: OptTailScheduler | None = None  # set for the duration of a training step
 
-    def take_opt_tail(self):
-        return self.opt_tails.take() if self.opt_tails is not None else None
+    def take_opt_tail(self, everything: bool = False):
+        return self.opt_tails.take(everything) if self.opt_tails is not None else None
 
     def need_split(self, n: int) -> None:
         self.split_floats = max(self.split_floats, n)
@@ -147,6 +148,11 @@ HALO_DGRAD = os.environ.get("MFL_HALO_DGRAD", "0") == "1"
 # the stem's BN backward + weight gradient in one launch (MFL_STEM_FUSED=0:
 # BN backward apply + im2col wgrad, for A/B runs)
 STEM_FUSED = os.environ.get("MFL_STEM_FUSED", "1") == "1"
+# MFL_STEM_TAIL=1: the rest of the pending optimizer rides in the fused stem
+# backward launch instead of the step's last optimizer launch -- measured
+# neutral (1.0224 / 1.0225 vs 1.0162 / 1.0270 ms per update,
+# profiles/r4/step/tail3/), so off
+STEM_TAIL = os.environ.get("MFL_STEM_TAIL", "0") == "1"
 
 
 class Pending:
@@ -371,9 +377,12 @@ class ConvBN(Layer):
                 and ((self.z.dtype == torch.float32 and (self.z.is_cuda or FUSED_FILL_CPU))
                      or (self.z.dtype == torch.bfloat16 and self.z.is_cuda))
                 and K.stem_backward_ok(s, self.z.device)):
-            # no dgrad (the stem): BN backward + weight gradient in one launch
+            # no dgrad (the stem): BN backward + weight gradient in one launch,
+            # which also carries the optimizer of everything still pending
+            # but the stem's own variables
             K.stem_backward(dy, self.z, self.y, self.x, s, self.gamma, self.mean, self.invstd,
-                            self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dw)
+                            self.ws.acc(self.acc_b), self.dgamma, self.dbeta, self.dw,
+                            opt=self.ws.take_opt_tail(everything=True) if STEM_TAIL else None)
             return
         if (HALO_DGRAD and dx is not None and presummed and side is None and self.hconv_ok()
                 and self.z.dtype == torch.float32):

@@ -510,13 +510,16 @@ def stem_backward_ok(shp: ConvShape, device: torch.device) -> bool:
     return geo and shp.H == 32 and shp.W == 32 and shp.C == 8 and shp.Co == 64
 
 
-def stem_backward(dy, z, y, x, shp: ConvShape, gamma, mean, invstd, acc, dgamma, dbeta, dw) -> None:
+def stem_backward(dy, z, y, x, shp: ConvShape, gamma, mean, invstd, acc, dgamma, dbeta, dw, opt=None) -> None:
     """A conv without dgrad (the stem): its BN(+ReLU) backward and its weight
     gradient in ONE launch on the GPU (bn32.hip stem_bwd32_kernel; dz never
     reaches memory, products are exact fp32).  ``acc`` holds the complete
-    backward sums (presummed); ``dw`` (zero on entry) accumulates."""
+    backward sums (presummed); ``dw`` (zero on entry) accumulates.  ``opt``
+    (ops.optim.OptRange): an optimizer step riding in the same launch."""
     if dy.is_cuda:
-        ops().stem_backward32(dy, z, y, gamma, mean, invstd, acc, dgamma, dbeta, x, dw)
+        from metisfl_amd.ops.optim import NO_OPT_TAIL
+        tail = opt.binding_args() if opt is not None else NO_OPT_TAIL
+        ops().stem_backward32(dy, z, y, gamma, mean, invstd, acc, dgamma, dbeta, x, dw, *tail)
         return
     # reference: the BatchNorm backward apply, then the weight gradient
     dz = torch.empty_like(z)
@@ -524,6 +527,8 @@ def stem_backward(dy, z, y, x, shp: ConvShape, gamma, mean, invstd, acc, dgamma,
     g = torch.empty_like(dw)
     conv_wgrad(x, dz, g, shp)
     dw.add_(g)
+    if opt is not None:
+        opt.run()
 
 
 # ---------------------------------------------------------------------------
