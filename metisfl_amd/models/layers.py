@@ -536,9 +536,12 @@ class BasicBlock(Layer):
         pm = premasked(self.da)  # conv2's dgrad stores da masked for conv1's BN
         if self.sc is None:
             # identity shortcut: masked dout goes straight into dx, conv1's
-            # dgrad then accumulates onto it (no add kernel)
-            self.c2.backward(dout, self.da, dres=dx, presummed=presummed, bnb=self.c1.bn_target(),
-                             dy_masked=dout_masked)
+            # dgrad then accumulates onto it (no add kernel).  A model may give
+            # dx the SAME buffer as a masked dout (in-place residual gradient):
+            # then there is nothing to copy at all
+            inplace = dout_masked and dx.data_ptr() == dout.data_ptr()
+            self.c2.backward(dout, self.da, dres=None if inplace else dx, presummed=presummed,
+                             bnb=self.c1.bn_target(), dy_masked=dout_masked)
             self.c1.backward(self.da, dx, accumulate=True, presummed=True, bnb=prev, dy_masked=pm)
         else:
             # the shortcut BN's backward sums ride in conv2's BN-backward launch

@@ -35,6 +35,9 @@ from metisfl_amd.ops.optim import split_pack
 
 DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16}
 DEFAULT_CONV_PRODUCTS = "bf16x3"
+# MFL_INPLACE_RESGRAD=1: identity blocks accumulate the residual gradient in
+# place in dout's buffer instead of copying it (opt-in until measured)
+INPLACE_RESIDUAL_GRAD = os.environ.get("MFL_INPLACE_RESGRAD", "0") == "1"
 
 
 def default_conv_products() -> str:
@@ -87,8 +90,15 @@ class ResNet18(StaticNet):
 
     def post_bind(self):
         dev = self.device
-        # gradient buffers at block boundaries: dx of block i is dout of block i-1
+        # gradient buffers at block boundaries: dx of block i is dout of block i-1.
+        # An identity block (not the last: the head's dx arrives unmasked)
+        # whose dout arrives pre-masked accumulates its input gradient in place
+        # in dout's buffer (layers.BasicBlock.backward): the two share it.
         self.dacts = [torch.zeros(b.in_shape, dtype=self.compute_dtype, device=dev) for b in self.blocks]
+        if premasked(self.dacts[0]) and INPLACE_RESIDUAL_GRAD:
+            for i in range(len(self.blocks) - 2, -1, -1):
+                if self.blocks[i].sc is None:
+                    self.dacts[i] = self.dacts[i + 1]
         self._xbp = None  # packed input batch (bf16x3 fp32 path), sized on first use
         if self.stem.yp is not None:
             self._xbp = torch.zeros((self.B,) + self.input_shape, dtype=torch.int32, device=dev)
