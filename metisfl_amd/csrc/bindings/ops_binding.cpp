@@ -315,7 +315,7 @@ void bn_backward(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor>
   }
   if (dy_masked.has_value() && dy_masked->defined()) {
     check_nhwc(*dy_masked, C);
-    TORCH_CHECK(a.y != nullptr, "dy_masked requires y");
+    // (without y: dy arrives masked and is copied as is)
     a.dy_masked = bf(*dy_masked);
   }
   if (dgamma.has_value() && dgamma->defined()) { check_pc(*dgamma, C, "dgamma"); a.dgamma = dgamma->data_ptr<float>(); }

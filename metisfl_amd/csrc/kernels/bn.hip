@@ -287,8 +287,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a, int64_t 
       unpack8(yc, yf);
 #pragma unroll
       for (int k = 0; k < 8; ++k) g[k] = yf[k] > 0.f ? g[k] : 0.f;
-      if (WRITE_DYM) reinterpret_cast<uint4*>(a.dy_masked)[i] = pack8(g);
     }
+    // !MASK: dy arrives masked (its producing dgrad applied the mask)
+    if (WRITE_DYM) reinterpret_cast<uint4*>(a.dy_masked)[i] = pack8(g);
     float o[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -308,7 +309,8 @@ void launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t s) {
     if (a.dy_masked) bn_bwd_apply_kernel<true, true><<<g, 256, sm, s>>>(a, nvec);
     else bn_bwd_apply_kernel<true, false><<<g, 256, sm, s>>>(a, nvec);
   } else {
-    bn_bwd_apply_kernel<false, false><<<g, 256, sm, s>>>(a, nvec);
+    if (a.dy_masked) bn_bwd_apply_kernel<false, true><<<g, 256, sm, s>>>(a, nvec);
+    else bn_bwd_apply_kernel<false, false><<<g, 256, sm, s>>>(a, nvec);
   }
 }
 

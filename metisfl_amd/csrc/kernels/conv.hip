@@ -132,6 +132,14 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int n0,
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += o[k];
     }
+    if (a.bn_acc && a.bn_y) {
+      // the consumer BN's ReLU mask applied on the way out (as conv32.hip):
+      // dX is stored as g = dX [y > 0], its BN backward reads no mask
+      float ym[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.bn_y + off), ym);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = ym[k] > 0.f ? v[k] : 0.f;
+    }
     const uint4 packed = pack8(v);
     *reinterpret_cast<uint4*>(dst) = packed;
     if (a.act_out) {  // exact (erf) GELU of the stored pre-activation

@@ -131,9 +131,9 @@ HCONV_BF16 = os.environ.get("MFL_HCONV_BF16", "1") == "1"
 def premasked(t: torch.Tensor) -> bool:
     """Whether a dgrad that fuses a consumer BN's backward sums (``bnb``) into
     its epilogue stores dX already multiplied by that BN's ReLU mask (the
-    fp32 conv32 epilogue and its host mirror; not the bf16 kernels or the
-    opt-in halo dgrad), so the consumer's BN backward reads no mask."""
-    return t.dtype == torch.float32 and not HALO_DGRAD and PREMASK
+    conv32 / conv epilogues and their host mirror; not the opt-in halo
+    dgrad), so the consumer's BN backward reads no mask."""
+    return t.dtype in (torch.float32, torch.bfloat16) and not HALO_DGRAD and PREMASK
 
 
 # MFL_BN_PREMASK=0: consumers re-apply the ReLU mask (A/B runs)

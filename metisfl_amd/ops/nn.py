@@ -157,8 +157,8 @@ def _bnb_sums_cpu(dx: torch.Tensor, t: BnBwdTarget, store_masked: bool = True) -
     g = dx.float().reshape(-1, C)
     if t.y is not None:
         g = torch.where(t.y.float().reshape(-1, C) > 0, g, torch.zeros_like(g))
-        if store_masked and dx.dtype == torch.float32:  # as the fp32 GPU dgrad epilogue: dX is stored masked
-            dx.copy_(g.view(dx.shape))
+        if store_masked:  # as the GPU dgrad epilogues: dX is stored masked
+            dx.copy_(g.view(dx.shape).to(dx.dtype))
     xh = (t.z.float().reshape(-1, C) - t.mean) * t.invstd
     t.acc[:C] += g.double().sum(0)
     t.acc[C:2 * C] += (g.double() * xh.double()).sum(0)
