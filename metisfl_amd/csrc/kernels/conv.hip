@@ -1047,7 +1047,10 @@ bool launch_conv_bwd_pair(const ConvGeom& gd, const ConvPlan& pd_in, const uint1
   da.par_mc = pd.par_mc;
   fill_shifts(da);
   ConvArgs wa{};
-  wa.accum = 1;  // the training step's gradient buffer is zero on entry
+  // the training step's gradient buffer is zero on entry: split-K slices
+  // add atomically (grid z > 1), an unsplit plan stores (as conv32.hip;
+  // MFL_C32_WSTORE=0: always atomics)
+  wa.accum = env_int("MFL_C32_WSTORE", 1) == 0 ? 1 : 0;
   wa.g = gw;
   wa.src = dy;
   wa.wgt = x;

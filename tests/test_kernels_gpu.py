@@ -195,12 +195,13 @@ def test_conv_backward_pair_matches_separate(case, with_bnb):
                                       dy.float().permute(0, 3, 1, 2), stride=s,
                                       padding=k // 2).permute(0, 2, 3, 1)
     assert rel_err(dw, wref) < 5e-3
+    xref_out = xref
     if with_bnb:
         # the fused consumer BN's ReLU mask is applied on the way out (dX is
         # stored as g = dX [y > 0], layers.premasked), by both launches alike
-        xref = torch.where(t_pair.y.float() > 0, xref, torch.zeros_like(xref))
-        assert torch.equal(dx == 0, dx_sep == 0) or rel_err(dx, dx_sep) < 1e-2
-    assert rel_err(dx, xref) < 1e-2
+        xref_out = torch.where(t_pair.y.float() > 0, xref, torch.zeros_like(xref))
+        assert rel_err(dx, dx_sep) < 1e-2
+    assert rel_err(dx, xref_out) < 1e-2
     if with_bnb:
         assert rel_err(t_pair.acc, t_sep.acc) < 1e-2
     # accumulate epilogue into an existing dx
