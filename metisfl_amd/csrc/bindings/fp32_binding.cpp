@@ -18,6 +18,12 @@ namespace {
 int g_c32_mode = 0;
 #define C32_CALL(fn, ...) (g_c32_mode ? mfl::c32s::fn(__VA_ARGS__) : mfl::c32x::fn(__VA_ARGS__))
 
+void set_conv32_pair_ring(int64_t ns) {
+  TORCH_CHECK(ns == 0 || ns == 2 || ns == 3, "pair ring depth is 0 (build default), 2 or 3");
+  mfl::c32x::set_conv32_pair_ring((int)ns);
+  mfl::c32s::set_conv32_pair_ring((int)ns);
+}
+
 void set_conv32_mode(int64_t m) {
   TORCH_CHECK(m == 0 || m == 1, "conv32 mode is 0 (exact fp32) or 1 (bf16x3)");
   g_c32_mode = (int)m;
@@ -705,6 +711,7 @@ void gather_batch32(torch::Tensor shard, torch::Tensor labels, torch::Tensor per
 
 void register_fp32(pybind11::module& m) {
   m.def("set_conv32_mode", &set_conv32_mode);
+  m.def("set_conv32_pair_ring", &set_conv32_pair_ring);
   m.def("conv32_mode", &conv32_mode);
   m.def("conv32_plan", &conv32_plan);
   m.def("conv32_forward", &conv32_forward);

@@ -1344,6 +1344,21 @@ void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, c
   }
 }
 
+// Pair ring depth (set_conv32_pair_ring): the throughput regime (4-8
+// co-located learners, models/colocated.py) trades the third ring stage for
+// a fourth resident workgroup per CU -- 0.693 / 0.696 -> 0.689 / 0.690 ms per
+// update with 8 learners when every conv32 kernel ran 2 stages, while one
+// learner (latency-bound) went 1.027 -> 1.071 (profiles/r4/ns/).  Only the
+// bf16x3 build carries the 2-stage pair instantiations.
+int g_pair_ns = 0;
+void set_conv32_pair_ring(int ns) { g_pair_ns = ns; }
+size_t pair_lds(int ns) {  // ring of ns 64x64 stages or the gemm epilogue, whichever is larger
+  return std::max((size_t)ns * (64 + 64) * kRowB, (size_t)64 * (64 + 4) * 4 + 256 * 8 * 4 + 16);
+}
+bool pair_ring2() {
+  return MFL_C32_BF16X3 && stages_for(64, 64) > 2 && (g_pair_ns ? g_pair_ns : env_int("MFL_C32_PAIR_NS", 0)) == 2;
+}
+
 bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGeom& gf, const ConvPlan& pw,
                             const float* dy, const float* w, float* dx, float* ysplit, int* counters, bool accum,
                             const BnBwdFusion32* bnb, const float* x, float* dw, hipStream_t s,
@@ -1360,8 +1375,10 @@ bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGe
   const int gwx = cdiv(gf.Ng, 64), gwy = cdiv(gf.K, 64), gwz = pw.splits;
   const OptTail tail = ot ? *ot : OptTail{};
   const int nblk = nd + gwx * gwy * gwz + tail.nblk;
-  const size_t lds = std::max(gemm_lds(64, 64), (size_t)stages_for(64, 64) * kBK * (64 + 64) * 4);
   constexpr int NS = stages_for(64, 64);
+  constexpr int NS2 = MFL_C32_BF16X3 && NS > 2 ? 2 : NS;
+  const bool r2 = pair_ring2();
+  const size_t lds = pair_lds(r2 ? NS2 : NS);
   // dw is zero on entry (the step's gradient buffer): an unsplit weight
   // gradient (ResNet-18's 512-channel stage) owns every element it writes, so
   // it stores instead of adding atomically (MFL_C32_WSTORE=0: always atomics)
@@ -1372,10 +1389,10 @@ bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGe
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     kern<<<nblk, 256, lds, s>>>(ad, aw, dw, wg_atomic, nd, gdx, gdy, gwx, gwy, gwz, tail);
   };
-  if (gd.R == 3 && gd.stride == 1) go(conv32_bwd_pair_kernel<3, 1, false, NS>);
-  else if (gd.R == 1 && gd.stride == 1) go(conv32_bwd_pair_kernel<1, 1, false, NS>);
-  else if (gd.R == 3 && gd.stride == 2) go(conv32_bwd_pair_kernel<3, 2, true, NS>);
-  else if (gd.R == 1 && gd.stride == 2) go(conv32_bwd_pair_kernel<1, 2, true, NS>);
+  if (gd.R == 3 && gd.stride == 1) r2 ? go(conv32_bwd_pair_kernel<3, 1, false, NS2>) : go(conv32_bwd_pair_kernel<3, 1, false, NS>);
+  else if (gd.R == 1 && gd.stride == 1) r2 ? go(conv32_bwd_pair_kernel<1, 1, false, NS2>) : go(conv32_bwd_pair_kernel<1, 1, false, NS>);
+  else if (gd.R == 3 && gd.stride == 2) r2 ? go(conv32_bwd_pair_kernel<3, 2, true, NS2>) : go(conv32_bwd_pair_kernel<3, 2, true, NS>);
+  else if (gd.R == 1 && gd.stride == 2) r2 ? go(conv32_bwd_pair_kernel<1, 2, true, NS2>) : go(conv32_bwd_pair_kernel<1, 2, true, NS>);
   else return false;
   return true;
 }
@@ -1393,11 +1410,12 @@ bool launch_conv32_fwd_pair(const ConvGeom& g1, const ConvPlan& p1, const float*
   const int g1x = cdiv(g1.M, 64), g1y = cdiv(g1.Ng, 64), n1 = g1x * g1y * p1.splits;
   const int g2x = cdiv(g2.M, 64), g2y = cdiv(g2.Ng, 64), g2z = p2.splits;
   constexpr int NS = stages_for(64, 64);
-  const size_t lds = gemm_lds(64, 64);
-  if (lds > 65536)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv32_fwd_pair_kernel<NS>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  conv32_fwd_pair_kernel<NS><<<n1 + g2x * g2y * g2z, 256, lds, s>>>(a1, a2, n1, g1x, g1y, g2x, g2y, g2z);
+  constexpr int NS2 = MFL_C32_BF16X3 && NS > 2 ? 2 : NS;
+  const bool r2 = pair_ring2();
+  const size_t lds = pair_lds(r2 ? NS2 : NS);
+  const int nblk = n1 + g2x * g2y * g2z;
+  if (r2) conv32_fwd_pair_kernel<NS2><<<nblk, 256, lds, s>>>(a1, a2, n1, g1x, g1y, g2x, g2y, g2z);
+  else conv32_fwd_pair_kernel<NS><<<nblk, 256, lds, s>>>(a1, a2, n1, g1x, g1y, g2x, g2y, g2z);
   return true;
 }
 

@@ -41,6 +41,8 @@ class CoLocatedLearners:
         self.device = dev
         self.cuda = dev.type == "cuda"
         self.streams = (self._make_streams(dev, len(self.nets)) if self.cuda else [None] * len(nets))
+        if self.cuda and len(self.nets) >= self.pair_ring_min_learners and self.pair_ring:
+            self._set_pair_ring(int(self.pair_ring))
         self._ev = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                      for _ in self.nets] if self.cuda else None)
 
@@ -48,6 +50,18 @@ class CoLocatedLearners:
     # share of the CUs (hipExtStreamCreateWithCUMask) instead of letting every
     # learner's kernels spread over the whole chip (A/B knob, off by default)
     cu_mask = os.environ.get("MFL_COLOC_CUMASK", "")
+
+    # In the throughput regime the fp32 paired conv launches run a 2-stage LDS
+    # ring (32 KiB: 4 workgroups per CU instead of 3; conv32.hip
+    # set_conv32_pair_ring).  Process-wide, set before the learners capture
+    # their graphs.  MFL_COLOC_PAIR_RING=0 keeps the build default.
+    pair_ring = os.environ.get("MFL_COLOC_PAIR_RING", "2")
+    pair_ring_min_learners = int(os.environ.get("MFL_COLOC_PAIR_RING_MIN", "4"))
+
+    @staticmethod
+    def _set_pair_ring(ns: int) -> None:
+        from metisfl_amd.ops._native import ops
+        ops().set_conv32_pair_ring(ns)
 
     @classmethod
     def _make_streams(cls, dev, n: int) -> list:

@@ -130,6 +130,45 @@ def test_conv32_backward_pair_matches_fp64(t, products):
     assert _rel(dw, ref_dw) <= 1e-5
 
 
+@pytest.mark.parametrize("t", [s for s in RESNET_SHAPES if s[3] != 8], ids=lambda t: "x".join(map(str, t)))
+def test_conv32_pair_ring2_matches_ring3(t):
+    """The 2-stage LDS ring of the paired launches (set_conv32_pair_ring,
+    the co-located throughput setting) changes the pipelining only: dX and
+    the forward outputs bitwise, dW to the order of its split-K atomics."""
+    from metisfl_amd.ops import nn as K
+    from metisfl_amd.ops._native import ops
+    K.set_conv_products("bf16x3")
+    shp = _shape(t)
+    g = torch.Generator().manual_seed(5 + (hash(t) & 0xFFFF))
+    x = torch.randn(shp.N, shp.H, shp.W, shp.C, generator=g).to(DEV)
+    dy = torch.randn(shp.N, shp.P, shp.Q, shp.Co, generator=g).to(DEV)
+    w = (torch.randn(shp.Co, shp.R, shp.S, shp.C, generator=g) / (shp.R * shp.S * shp.C) ** 0.5).to(DEV)
+    out = []
+    try:
+        for ns in (3, 2):
+            ops().set_conv32_pair_ring(ns)
+            dx = torch.zeros(shp.N, shp.H, shp.W, shp.C, device=DEV)
+            dw = torch.zeros_like(w)
+            K.conv_backward_pair(x, dy, dw, w, dx, shp, _ws(shp), accumulate=False)
+            fw = None
+            if shp.R == 3 and shp.stride == 2:
+                s2 = _shape((shp.N, shp.H, shp.W, shp.C, shp.Co, 1, 2))
+                w2 = w[:, 1:2, 1:2, :].contiguous()
+                y1 = torch.zeros_like(dy)
+                y2 = torch.zeros_like(dy)
+                K.conv_forward_pair(x, w, y1, _ws(shp), None, w2, y2, _ws(s2), None, shp)
+                fw = (y1, y2)
+            torch.cuda.synchronize()
+            out.append((dx, dw, fw))
+    finally:
+        ops().set_conv32_pair_ring(0)
+    (dx3, dw3, f3), (dx2, dw2, f2) = out
+    assert torch.equal(dx3, dx2)
+    assert _rel(dw2, dw3) <= 1e-6
+    if f3 is not None:
+        assert torch.equal(f3[0], f2[0]) and torch.equal(f3[1], f2[1])
+
+
 @pytest.mark.parametrize("t", RESNET_SHAPES + ODD_SHAPES, ids=lambda t: "x".join(map(str, t)))
 def test_conv32_dgrad_matches_fp64(t, products):
     from metisfl_amd.ops import nn as K
