@@ -1094,11 +1094,16 @@ constexpr TunedPlan kTuned[] = {
     // 16x16x128 backward pair: dgrad 2 x wgrad 7 slices = 764 workgroups, one
     // wave of 3 per CU, instead of 3 x 14 = 1,272 (1.66 waves) -- whole-step
     // sweep with MFL_C32_PLANS, profiles/r4/plans/: -1.4 % per update
+    // 4x4x512 dgrad 4 slices (832 workgroups with its wgrad) and 8x8x256
+    // wgrad 2 (800 with its dgrad), instead of 8 / 3: neutral for one learner
+    // (1.048 / 1.049 vs 1.045 / 1.050 ms), -0.7 % per update with 8 co-located
+    // learners on the 2-stage pair ring (0.690 / 0.689 -> 0.685 / 0.685 ms,
+    // profiles/r4/ns/tq_*.log)
     {1, 32, 32, 32, 64, 128, 1, 2, 64, 64, 1},  {1, 32, 16, 16, 128, 128, 3, 1, 64, 64, 2},
     {1, 32, 16, 16, 128, 256, 3, 2, 64, 64, 3}, {1, 32, 8, 8, 256, 256, 3, 1, 64, 64, 4},
-    {1, 32, 8, 8, 256, 512, 3, 2, 64, 64, 4},   {1, 32, 4, 4, 512, 512, 3, 1, 64, 64, 8},
+    {1, 32, 8, 8, 256, 512, 3, 2, 64, 64, 4},   {1, 32, 4, 4, 512, 512, 3, 1, 64, 64, 4},
     {2, 32, 16, 16, 128, 128, 3, 1, 64, 64, 7}, {2, 32, 16, 16, 128, 256, 3, 2, 64, 64, 7},
-    {2, 32, 8, 8, 256, 256, 3, 1, 64, 64, 3},   {2, 32, 8, 8, 256, 512, 3, 2, 64, 64, 2},
+    {2, 32, 8, 8, 256, 256, 3, 1, 64, 64, 2},   {2, 32, 8, 8, 256, 512, 3, 2, 64, 64, 2},
     {2, 32, 4, 4, 512, 512, 3, 1, 64, 64, 1},
 };
 #else

@@ -36,6 +36,10 @@ def test_paired_backward_plans_fill_one_wave():
     tiles_d = (32 * 16 * 16 // 64) * (128 // 64)
     tiles_w = (128 // 64) * (128 * 9 // 64)
     assert tiles_d * l2[2] + tiles_w * l2[5] <= 3 * 256
+    # 4x4x512: dgrad 4 x wgrad 1 = 832 workgroups, one wave of 4 per CU on the
+    # co-located learners' 2-stage pair ring (profiles/r4/ns/tq_*.log)
+    assert l4[2] == 4 and l4[5] == 1
+    assert (32 * 4 * 4 // 64) * (512 // 64) * l4[2] + (512 // 64) * (512 * 9 // 64) * l4[5] <= 4 * 256
 
 
 def test_plan_override_env():
