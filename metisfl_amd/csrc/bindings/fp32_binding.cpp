@@ -94,10 +94,12 @@ std::vector<int64_t> conv32_plan(int64_t mode, int64_t N, int64_t H, int64_t W, 
   if (mode == 2) {
     const auto g = fwd_geom(N, H, W, C, Co, R, S, stride, pad);
     const auto p = C32_CALL(plan_conv32, g, 2);
+    TORCH_CHECK(p.kchunk > 0, "no feasible conv32 plan for this shape");
     return {p.bm, p.bn, p.splits, p.kchunk, 0, 0};
   }
   const auto g = mode == 0 ? fwd_geom(N, H, W, C, Co, R, S, stride, pad) : dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
   const auto p = C32_CALL(plan_conv32, g, (int)mode);
+  TORCH_CHECK(p.kchunk > 0, "no feasible conv32 plan for this shape");
   return {p.bm, p.bn, p.splits, p.kchunk, mode == 0 ? 1 : 0, ws_floats(g, p)};
 }
 

@@ -1181,6 +1181,10 @@ static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
   ConvPlan best;
   double best_t = 1e30;
   const int nkt_all = cdiv(kred, kBK);
+  // a forced slice count (table, MFL_C32_PLANS, MFL_C32_SPLIT) snaps to the
+  // feasible count it implies: equal k-tile shares, no empty slice (an
+  // infeasible request used to leave the plan without a tile)
+  if (fs > 0) fs = cdiv(nkt_all, cdiv(nkt_all, std::min(fs, nkt_all)));
   for (const Cand& c : kCands) {
     if (fb && c.bm != fb) continue;
     if (fn && c.bn != fn) continue;

@@ -46,3 +46,11 @@ def test_plan_override_env():
     l2, l1, _ = _plans({"MFL_C32_PLANS": "1,16,128,128,3,1,4;2,16,128,128,3,1,3"})
     assert l2[2] == 4 and l2[5] == 3
     assert l1 == _plans()[1]  # other shapes untouched
+
+
+def test_infeasible_split_override_snaps_to_a_feasible_count():
+    """1,024 k-tiles cannot split into 56 equal shares: the request runs 54
+    slices of 19 tiles (it used to leave the plan without a tile, and the
+    weight gradient unwritten)."""
+    _, l1, _ = _plans({"MFL_C32_PLANS": "2,32,64,64,3,1,56"})
+    assert l1[5] == 54
