@@ -14,7 +14,8 @@ plane: its learners always ship models through the controller
 
 Protocols: synchronous / semi-synchronous rounds (CollectiveFederation), or
 the asynchronous protocol (AsyncCollectiveFederation.run_until: FedRec over
-point-to-point transfers, one community version per completed task).
+point-to-point transfers, one community version per completed task of any
+learner; a rank's co-located learners are FedRec participants of their own).
 
 Termination (the driver's TerminationSignals, driver_session.py:423-467):
 FederationRounds (sync: rounds; async: community versions), the wall-clock
@@ -144,26 +145,30 @@ def main(argv=None) -> int:
 
     endpoints = [(l["hostname"], l["port"]) for l in job["learners"]]
     if fcfg.protocol == "asynchronous":
-        if len(mine) > 1:
-            raise RuntimeError("DataPlane: rccl runs the asynchronous protocol with one learner per device "
-                               f"(rank {rank} hosts {len(mine)})")
+        # every learner is its own FedRec participant, whatever its placement:
+        # the ones this rank hosts run concurrently on their own streams
         from metisfl_amd.parallel.async_federation import AsyncCollectiveFederation
         from metisfl_amd.parallel.federation import install_community_model
         initial_model(lambda fm: install_community_model(net, fm))
-        engine = None
-        if rank == 0:
-            sizes = comm.all_gather_rows(torch.tensor([float(train_ds.n)], dtype=torch.float64,
-                                                      device=comm.device)).cpu().numpy()[:, 0]
-            engine = RemoteCollectiveController(entity, [int(x) for x in sizes], endpoints)
-        else:
-            comm.all_gather_rows(torch.tensor([float(train_ds.n)], dtype=torch.float64, device=comm.device))
-        fed = AsyncCollectiveFederation(comm, net, train_ds, fcfg, test_ds=test_ds, engine=engine,
-                                        broadcast_initial=True)
+        owners = [0] * len(job["learners"])
+        for r, idx in enumerate(ranks):
+            for i in idx:
+                owners[i] = r
+        gids = list(ranks[rank])
+        # per-learner dataset sizes, in the job's learner order (the
+        # controller's scaling inputs): every rank fills its learners' slots
+        sz = torch.zeros(len(owners), dtype=torch.float64, device=comm.device)
+        for g, d in zip(gids, train_dss):
+            sz[g] = float(d.n)
+        sizes = comm.all_gather_rows(sz).sum(0).cpu().numpy()
+        engine = RemoteCollectiveController(entity, [int(x) for x in sizes], endpoints) if rank == 0 else None
+        fed = AsyncCollectiveFederation(comm, nets, train_dss, fcfg, test_ds=test_dss, engine=engine,
+                                        broadcast_initial=True, gids=gids, owners=owners, learner_ids=learner_ids)
         if job.get("resume_dir"):
-            fed.resume(job["resume_dir"], prev_rank=lcfg.get("prev_rank"))
+            fed.resume(job["resume_dir"])
             if rank == 0:
-                print(f"[collective-async] resumed at version {fed.version} on {comm.world} learners "
-                      f"(dropped old ranks {getattr(fed, 'resumed', {}).get('dropped')})", flush=True)
+                print(f"[collective-async] resumed at version {fed.version} on {len(owners)} learners "
+                      f"(dropped learners {getattr(fed, 'resumed', {}).get('dropped')})", flush=True)
         delay = float((fcfg.extra or {}).get("debug_delay_s", {}).get(str(rank), 0.0))
         my_fault = fault if fault and int(fault.get("rank", -1)) == rank else None
         ups = fed.run_until(max_updates=rounds, cutoff_s=cutoff_s, metric=metric, metric_cutoff=metric_cutoff,
@@ -171,8 +176,8 @@ def main(argv=None) -> int:
                             fault_task=int(my_fault["round"]) if my_fault else None,
                             on_fault=lambda t: _inject_fault(rank, t, my_fault))
         if rank == 0:
-            print(f"[collective-async] {len(ups)} FedRec updates, stop: {fed.stop_reason}, staleness "
-                  f"{[u.staleness for u in ups]}", flush=True)
+            print(f"[collective-async] {len(ups)} FedRec updates over {len(owners)} learners on {comm.world} "
+                  f"ranks, stop: {fed.stop_reason}, staleness {[u.staleness for u in ups]}", flush=True)
             engine.close()
         if wd is not None:
             wd.stop()

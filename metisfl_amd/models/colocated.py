@@ -43,6 +43,10 @@ class CoLocatedLearners:
         self.streams = (self._make_streams(dev, len(self.nets)) if self.cuda else [None] * len(nets))
         if self.cuda and len(self.nets) >= self.pair_ring_min_learners and self.pair_ring:
             self._set_pair_ring(int(self.pair_ring))
+        if self.cuda and len(self.nets) >= self.tconv_min_learners and self.tconv:
+            for net in self.nets:
+                if hasattr(net, "set_throughput_conv"):
+                    net.set_throughput_conv(True)
         self._ev = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                      for _ in self.nets] if self.cuda else None)
 
@@ -57,6 +61,14 @@ class CoLocatedLearners:
     # their graphs.  MFL_COLOC_PAIR_RING=0 keeps the build default.
     pair_ring = os.environ.get("MFL_COLOC_PAIR_RING", "2")
     pair_ring_min_learners = int(os.environ.get("MFL_COLOC_PAIR_RING_MIN", "4"))
+    # MFL_COLOC_TCONV=1: the 3x3 / stride-1 backward GEMMs run as the
+    # throughput kernels (tconv.hip, StaticNet.set_throughput_conv) instead of
+    # the paired latency-regime launches.  Off by default: faster per call in
+    # isolation (8 learners' launches over 4 streams: ~10 us per wgrad or
+    # dgrad vs ~23 us per pair) but slower in the co-located step (0.690 ->
+    # 0.747 ms per update of the GPU, profiles/r5/tconv/)
+    tconv = os.environ.get("MFL_COLOC_TCONV", "0") == "1"
+    tconv_min_learners = int(os.environ.get("MFL_COLOC_TCONV_MIN", "4"))
 
     @staticmethod
     def _set_pair_ring(ns: int) -> None:

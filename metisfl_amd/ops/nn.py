@@ -52,6 +52,31 @@ def conv_products() -> str:
     return CONV_PRODUCTS[ops().conv32_mode()]
 
 
+# Co-located regime (models/colocated.py): the 3x3 / stride-1 backward GEMMs
+# of the fp32 / bf16x3 path can run as the throughput kernels (tconv.hip:
+# 4-wave 128 x 128 tiles on the pair-expanded packed operands, separate wgrad
+# and dgrad launches) instead of the latency-regime paired launch
+# (conv32.hip).  Measured with 8 learners' launches over 4 streams
+# (profiles/r5/tconv/): ~10 us per wgrad or dgrad call against ~23 us per
+# paired call.  Chosen per model (layers.Workspace.throughput, set by
+# StaticNet.set_throughput_conv).
+_TCONV_OK: dict = {}
+
+
+def tconv_shape_ok(shp: ConvShape) -> bool:
+    """Whether the throughput kernels take this layer shape."""
+    key = shp.args()
+    if key not in _TCONV_OK:
+        _TCONV_OK[key] = bool(ops().tconv_backward_ok(*key))
+    return _TCONV_OK[key]
+
+
+def tconv_workspace(shp: ConvShape) -> tuple[int, int]:
+    """(split-K slab floats, arrival-counter ints) of the throughput dgrad."""
+    f, c = ops().tconv_workspace(*shp.args())
+    return int(f), int(c)
+
+
 def out_dim(n: int, k: int, stride: int, pad: int) -> int:
     return (n + 2 * pad - k) // stride + 1
 
@@ -237,7 +262,7 @@ def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShap
 
 def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
                        bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False, xp=None,
-                       opt=None) -> None:
+                       opt=None, counters=None, throughput: bool = False) -> None:
     """A layer's weight gradient (dw += ..., dw zero on entry) and input
     gradient (as conv_dgrad) -- on the GPU in ONE paired launch, so the two
     independent, latency-bound GEMMs share the CUs (conv.hip
@@ -246,7 +271,17 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
     tiles on the fast address paths; MFL_C32_PAIR=0 for two launches).
     ``opt`` (ops.optim.OptRange): an optimizer step over a range whose
     gradients are final, run by extra workgroups of the fp32 paired launch
-    (elsewhere: its own launch after the pair)."""
+    (elsewhere: its own launch after the pair).  ``throughput`` (co-located
+    regime): 3x3 / stride-1 layers with packed operands run the throughput
+    kernels instead (``counters``: their split-K arrival tickets, int32, zero
+    between launches)."""
+    if (throughput and dy.is_cuda and dy.dtype == torch.float32 and dy_packed and xp is not None
+            and wp is not None and conv_products() == "bf16x3" and tconv_shape_ok(shp)):
+        f = (bnb.z, bnb.y, bnb.mean, bnb.invstd, bnb.acc) if bnb is not None else (None,) * 5
+        ops().tconv_backward(xp, dy, dw, wp, dx, ws, counters, *shp.args(), accumulate, *f)
+        if opt is not None:
+            opt.run()
+        return
     if dy.is_cuda and dy.dtype == torch.float32:
         dy = _dy_arg(dy, dy_packed)
         xa = x if xp is None else xp

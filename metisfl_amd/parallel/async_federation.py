@@ -1,4 +1,4 @@
-"""Asynchronous collective federation: FedRec over point-to-point RCCL.
+"""Asynchronous collective federation: ONE FedRec core for every placement.
 
 The reference's asynchronous protocol re-dispatches every learner the moment
 its task completes (AsynchronousScheduler, scheduling/asynchronous_scheduler.h:
@@ -6,62 +6,65 @@ its task completes (AsynchronousScheduler, scheduling/asynchronous_scheduler.h:
 (ScheduledCardinality selector, selection/scheduled_cardinality.h:21-29) with
 the recency rule FedRec (aggregation/federated_recency.cc:8-100: replace the
 finisher's previous contribution in a running weighted sum) and sends the new
-community model to the finisher only.  All models cross the controller as
-serialized gRPC messages.
+community model to the finisher only.  Scheduling is per learner, whatever
+the placement -- its own asynchronous configs put all 10 learners on GPU 0
+(examples/config/fashionmnist/test_localhost_asynchronous_vanillasgd.yaml).
+All models cross the controller as serialized gRPC messages.
 
-Here one process per GPU hosts a learner; rank 0
-is also the aggregator.  A finished learner posts its task metadata to the
-process group's key-value store (the control channel), then ``send``s its
-flat fp32 model to rank 0 and ``recv``s the community model back -- one
-point-to-point RCCL transfer each way over xGMI, nothing through the host.
-Rank 0 keeps, in HBM, the running sum S = sum_i w_i theta_i, Z = sum_i w_i
-and every learner's last contribution, and applies the FedRec update with
-the K2 rolling kernels:
+Here one process per GPU hosts that GPU's learners (``nets``: one or several,
+co-located on their own HIP streams as in models/colocated.py); rank 0 is
+also the aggregator.  Every learner -- global id ``g`` in the job's learner
+order -- is its own FedRec participant:
+
+* a learner hosted by rank 0 folds its model into the running sum on the
+  device, under the aggregator lock, the moment its task's last launch has
+  completed (a HIP event polled without blocking the other learners);
+* a learner hosted by another rank posts its task metadata to the process
+  group's key-value store (the control channel), ``send``s its flat fp32
+  model to rank 0 and ``recv``s the community model back -- one point-to-point
+  RCCL transfer each way over xGMI, nothing through the host.  Rank 0's
+  service thread (own process group, own HIP stream) serves those.
+
+Rank 0 keeps, in HBM, S = sum_g w_g theta_g, Z = sum_g w_g and every
+learner's last contribution, and applies the FedRec update with the K2
+rolling kernels:
 
     S -= w_old * theta_old ; Z -= w_old        (learner seen before)
     S += w_new * theta_new ; Z += w_new
     community = S / Z
 
 Staleness-aware weighting (the reference's FedRec has
-none): rank 0 versions the community model (+1 per applied update) and
-answers every submission with the new version through the store; a
+none): rank 0 versions the community model (+1 per applied update); a
 learner's next submission carries the version it trained from, and its
 FedRec weight is multiplied by cfg.staleness's discount of
 t = version_now - version_base (``staleness_discount``).
-
-Rank 0's aggregator runs in a service thread with its own process group
-(point-to-point transfers) and its own HIP stream, so a finisher is served
-the moment it posts -- rank 0's own training never blocks it (and is not
-chunked).  ``serve_in_thread=False`` keeps the single-threaded variant: rank
-0 trains in chunks of ``poll_every`` local steps and serves between chunks,
-so a finisher waits up to one chunk.  The weights are the
-NUM_TRAINING_EXAMPLES (or batch / participant) scaling inputs,
-un-normalised, as FedRec consumes them.
 
 Failure handling (in the reference one lost learner never ends
 an asynchronous federation: controller.cc:171-199 removes it and the
 asynchronous scheduler keeps serving the others).  ``run_until`` with a
 checkpoint directory writes, every ``checkpoint_every`` community versions,
 the aggregator's FedRec state (S, Z, every learner's last contribution and
-weight, the version) plus the community model as a ``FederatedModel``
-(``<dir>/round_<version>/``, LATEST), and every learner's local state after
-its tasks (``<dir>/async_learner_rank<r>.pt``) -- staged on the device and
-written by background threads (parallel/checkpoint.py).  After a lost rank
-the driver relaunches the survivors; ``resume`` restores the FedRec state,
-drops the lost learners' contributions from S and Z, restarts every survivor
-from the restored community model and continues the version count.
-The controller bookkeeping (runtime metadata per version, the driver's stop
-request) goes through a queue served by its own thread, never under the
-aggregator lock.
+weight -- keyed by STABLE learner id, ``last:<id>`` -- and the version) plus
+the community model as a ``FederatedModel`` (``<dir>/round_<version>/``,
+LATEST), and every learner's local state after its tasks
+(``<dir>/async_learner_<id>.pt``) -- staged on the device and written by
+background threads (parallel/checkpoint.py).  After a lost rank the driver
+relaunches the survivors (possibly regrouped onto fewer ranks); ``resume``
+restores the FedRec state of the learner ids still present, drops the lost
+ones' contributions from S and Z, restarts every survivor from the restored
+community model and continues the version count.  The controller
+bookkeeping (runtime metadata per version, the driver's stop request) goes
+through a queue served by its own thread, never under the aggregator lock.
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 import queue
 import threading
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -103,20 +106,58 @@ class AsyncUpdate:
     base_weight: float = 0.0
 
 
+@dataclass
+class _Local:
+    """One learner hosted by this rank."""
+    j: int                      # index among this rank's learners
+    gid: int                    # global learner index (the job's learner order)
+    lid: str                    # stable learner id (checkpoint keys)
+    net: object
+    train_ds: object
+    test_ds: object
+    num_local_updates: int
+    steps_done: int = 0
+    base_version: int = 0       # community version its current task started from
+    task_index: int = 0         # tasks completed (kept across a resume)
+    sub: int = 0                # this run's submissions (store keys)
+    last_eval: dict | None = None
+    gen: object = None          # the running task's launch generator
+    done_ev: object = None
+    started: float = 0.0
+    finished: bool = False
+    lckpt: object = None
+    tasks_run: int = 0
+    extra: dict = field(default_factory=dict)
+
+
 class AsyncCollectiveFederation:
-    def __init__(self, comm: Comm, net, train_ds, cfg: FederationConfig, tasks_per_learner: int = 2,
+    """``nets`` / ``train_dss`` / ``test_ds``: this rank's learner(s) (a model or
+    a list).  ``gids``: their global learner indices and ``owners[g]``: the
+    rank hosting learner g (default: one learner per rank, learner g on rank
+    g).  ``learner_ids``: stable ids of all learners, by global index."""
+
+    def __init__(self, comm: Comm, nets, train_dss, cfg: FederationConfig, tasks_per_learner: int = 2,
                  poll_every: int = 16, store=None, broadcast_initial: bool = True,
-                 serve_in_thread: bool = True, test_ds=None, engine=None):
-        self.comm, self.net, self.train_ds, self.cfg = comm, net, train_ds, cfg
-        self.test_ds = test_ds
-        # rank 0: the controller bridge (engine_bridge.py) every FedRec update
-        # and community evaluation is recorded with (runtime metadata, local
-        # task lineage, community-model evaluations)
+                 serve_in_thread: bool = True, test_ds=None, engine=None, gids=None, owners=None,
+                 learner_ids=None, streams=None):
+        single = not isinstance(nets, (list, tuple))
+        nets = [nets] if single else list(nets)
+        train_dss = [train_dss] if single else list(train_dss)
+        test_dss = ([test_ds] if single else list(test_ds)) if test_ds is not None else [None] * len(nets)
+        self.comm, self.cfg = comm, cfg
+        self.rank, self.world = comm.rank, comm.world
+        if owners is None:
+            owners = list(range(self.world)) if len(nets) == 1 else [0] * len(nets)
+        self.owners = [int(o) for o in owners]
+        self.G = len(self.owners)
+        if gids is None:
+            gids = [g for g, o in enumerate(self.owners) if o == self.rank]
+        assert len(gids) == len(nets), (gids, len(nets))
+        self.learner_ids = list(learner_ids) if learner_ids else [f"learner_{g}" for g in range(self.G)]
         self.engine = engine if comm.rank == 0 else None
         self.evaluations: list[dict] = []  # rank 0: {"version", "learner", "loss", "accuracy"}
         self._stop_flag = False            # termination mode (run_until)
-        self._done: set[int] = set()
-        self.rank, self.world = comm.rank, comm.world
+        self._done: set[int] = set()       # rank 0: remote learners that left (global ids)
         _INSTANCES[0] += 1
         self.tag = _INSTANCES[0]  # store-key namespace: repeated federations never see old keys
         self.tasks = tasks_per_learner
@@ -130,56 +171,240 @@ class AsyncCollectiveFederation:
         self._svc_error: BaseException | None = None
         self.store = store if store is not None else (
             dist.distributed_c10d._get_default_store() if comm.distributed else None)
-        n = int(train_ds.n)
-        self.num_local_updates = cfg.local_epochs * max(1, -(-n // cfg.batch_size))
-        self.steps_done = 0
+        self.learners = [
+            _Local(j, int(g), self.learner_ids[int(g)], n, d, t,
+                   cfg.local_epochs * max(1, -(-int(d.n) // cfg.batch_size)))
+            for j, (g, n, d, t) in enumerate(zip(gids, nets, train_dss, test_dss))]
         self.updates: list[AsyncUpdate] = []   # rank 0: every FedRec update applied
         self.version = 0                       # rank 0: community model version
-        self.base_version = 0                  # version this learner's current task started from
-        self.task_index = 0                    # tasks this learner completed (kept across a resume)
         self.ckpt_dir: str | None = None
         self.ckpt_every = 0
         self.snapshot_every = int(getattr(cfg, "snapshot_every", 0) or 0)
-        self._ckpt = self._lckpt = self._lineage = None
+        self._ckpt = self._lineage = None
         self._bk_q: queue.Queue | None = None
         self._bk_thread = None
         self._driver_stop = False
-        st = net.state
+        st = self.net.state
+        self.cuda = st.model32.is_cuda
+        # co-located learners replay their step graphs on their own streams
+        if streams is not None:
+            self.streams = list(streams)
+        elif self.cuda and len(nets) > 1:
+            self.streams = [torch.cuda.Stream(device=st.model32.device) for _ in nets]
+        else:
+            self.streams = [None] * len(nets)
         if broadcast_initial and comm.distributed:
             comm.broadcast_(st.model32, src=0)
-            st.refresh_bf16()
-            st.set_anchor()
+        for L in self.learners[1:]:  # every learner starts from the community model
+            L.net.state.model32.copy_(st.model32)
+        for L in self.learners:
+            self._install(L)
         if self.rank == 0:
-            dev = st.model32.device
             self.S = torch.zeros_like(st.model32)
             self.Z = 0.0
-            self.last = [None] * self.world        # each learner's last contribution (HBM)
-            self.last_w = [0.0] * self.world
-            self.next_task = [0] * self.world       # next expected task per learner
-            self.rbuf = torch.empty_like(st.model32, device=dev)
+            self.last = [None] * self.G        # each learner's last contribution (HBM)
+            self.last_w = [0.0] * self.G
+            self.next_task = [0] * self.G       # next expected submission per remote learner
+            self.rbuf = torch.empty_like(st.model32)
+        self.remote = [g for g, o in enumerate(self.owners) if o != 0]
+
+    # ---- compatibility: the first hosted learner ----------------------------------
+    @property
+    def net(self):
+        return self.learners[0].net
+
+    @property
+    def train_ds(self):
+        return self.learners[0].train_ds
+
+    @property
+    def num_local_updates(self) -> int:
+        return self.learners[0].num_local_updates
+
+    @property
+    def steps_done(self) -> int:
+        return self.learners[0].steps_done
+
+    @property
+    def base_version(self) -> int:
+        return self.learners[0].base_version
+
+    @property
+    def task_index(self) -> int:
+        return self.learners[0].task_index
 
     # ---- learner side ------------------------------------------------------------
-    def _weight(self, completed_batches: int) -> float:
+    def _weight(self, L: _Local, completed_batches: int) -> float:
         sf = self.cfg.scaling_factor
         if sf == "NUM_TRAINING_EXAMPLES":
-            return float(self.train_ds.n)
+            return float(L.train_ds.n)
         if sf == "NUM_COMPLETED_BATCHES":
             return float(completed_batches)
         return 1.0  # NUM_PARTICIPANTS
 
-    def _train(self, nsteps: int) -> None:
-        self.net.train_steps(self.train_ds, nsteps, step_offset=self.steps_done)
-        self.steps_done += nsteps
+    def _ctx(self, L: _Local):
+        s = self.streams[L.j]
+        return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
+
+    def _sync_stream(self) -> None:
+        if self.cuda:
+            torch.cuda.current_stream(self.net.state.model32.device).synchronize()
+
+    def _install(self, L: _Local) -> None:
+        st = L.net.state
+        st.refresh_bf16()
+        st.set_anchor()
+
+    def _start_task(self, L: _Local) -> None:
+        with self._ctx(L):
+            L.net.reset_train_stats()
+            L.gen = L.net.train_steps_iter(L.train_ds, L.num_local_updates, step_offset=L.steps_done)
+        L.started = time.time()
+        L.done_ev = None
+
+    def _step(self, L: _Local) -> bool:
+        """Issue the running task's next launch (one graph replay / eager
+        step).  False once the task has issued everything."""
+        with self._ctx(L):
+            try:
+                next(L.gen)
+                return True
+            except StopIteration:
+                pass
+            if self.cuda:
+                L.done_ev = torch.cuda.Event()
+                L.done_ev.record()
+        L.gen = None
+        return False
+
+    def _task_meta(self, L: _Local, debug_delay_s: float) -> dict:
+        """The finished task's metadata (host-side once its launches completed)."""
+        if debug_delay_s:
+            time.sleep(debug_delay_s)  # test hook: uneven learner speeds
+        ms_b = (time.time() - L.started) * 1e3 / max(1, L.num_local_updates)
+        L.steps_done += L.num_local_updates
+        spe = L.train_ds.steps_per_epoch
+        tr = L.net.train_stats()
+        return {"task": L.task_index, "weight": self._weight(L, L.num_local_updates),
+                "loss": tr["loss"], "accuracy": tr["accuracy"], "batches": L.num_local_updates,
+                "base_version": L.base_version, "eval": L.last_eval, "started_at": L.started,
+                "n_train": int(L.train_ds.n), "ms_per_batch": ms_b, "ms_per_epoch": ms_b * spe,
+                "epochs": L.num_local_updates / spe}
+
+    def _submit(self, L: _Local, meta: dict) -> None:
+        """FedRec of the finished task; the learner leaves holding the new
+        community model."""
+        model = L.net.state.model32
+        if self.rank == 0:
+            with self._lock:
+                self._record_eval(L.gid, meta.get("eval"))
+                self._fedrec(L.gid, model, meta)
+                model.copy_(self._community())
+                self._sync_stream()
+                L.base_version = self.version
+                self._after_update()
+        else:
+            self.store.set(_KEY.format(self.tag, L.gid, L.sub), json.dumps(meta))
+            dist.send(model, dst=0, group=self.p2p)
+            dist.recv(model, src=0, group=self.p2p)
+            self._sync_stream()  # the learner's stream reads it next
+            L.base_version = int(self.store.get(_VER.format(self.tag, L.gid, L.sub)))
+        self._install(L)
+        L.sub += 1
+        L.task_index += 1
+        L.tasks_run += 1
+
+    def _evaluate_received(self, L: _Local) -> dict | None:
+        if L.test_ds is None or not self.cfg.evaluate_community:
+            return None
+        with self._ctx(L):
+            ev = L.net.evaluate(L.test_ds, self.cfg.eval_max_steps)
+        return {"version": L.base_version, "loss": ev["loss"], "accuracy": ev["accuracy"], "n": L.test_ds.n}
+
+    # ---- the event loop over this rank's learners ---------------------------------
+    def _drive(self, more_tasks, debug_delay_s: float = 0.0, fault_task: int | None = None, on_fault=None,
+               after_task=None) -> None:
+        """Run this rank's learners concurrently (co-located: one stream each)
+        until each has finished its last task.  ``more_tasks(L)``: whether
+        learner L starts another task; ``after_task(L)``: called after each
+        completed submission."""
+        for L in self.learners:  # capture before the streams run concurrently
+            L.net.prepare_graphs(L.train_ds, L.num_local_updates)
+        if self.cuda:
+            cur = torch.cuda.current_stream(self.net.state.model32.device)
+            for s in self.streams:
+                if s is not None:
+                    s.wait_stream(cur)
+
+        def start_or_finish(L: _Local) -> None:
+            if more_tasks(L):
+                if fault_task is not None and L.task_index + 1 == int(fault_task) and on_fault is not None:
+                    self.flush()
+                    on_fault(L.task_index + 1)
+                self._start_task(L)
+            else:
+                L.finished = True
+                self._leave(L)
+
+        for L in self.learners:
+            L.finished = False
+            start_or_finish(L)
+        chunked_server = self.rank == 0 and self.world > 1 and not self.threaded
+        while not all(L.finished for L in self.learners):
+            progressed = False
+            for L in self.learners:
+                if L.finished or L.gen is None:
+                    continue
+                if self._step(L):
+                    progressed = True
+                    if chunked_server:
+                        self.serve(block=False)
+            for L in self.learners:
+                if L.finished or L.gen is not None:
+                    continue
+                if L.done_ev is not None and not L.done_ev.query():
+                    continue
+                progressed = True
+                meta = self._task_meta(L, debug_delay_s)
+                self._submit(L, meta)
+                L.last_eval = self._evaluate_received(L)
+                if after_task is not None:
+                    after_task(L)
+                start_or_finish(L)
+            if chunked_server:
+                progressed = bool(self.serve(block=False)) or progressed
+            if not progressed:
+                time.sleep(0.0002)
+        if self.cuda:
+            cur = torch.cuda.current_stream(self.net.state.model32.device)
+            for s in self.streams:
+                if s is not None:
+                    cur.wait_stream(s)
+
+    def _leave(self, L: _Local) -> None:
+        """A learner that starts no more tasks: its last evaluation reaches rank
+        0 (remote learners: through their done message)."""
+        if not self._until:
+            return
+        if self.rank == 0:
+            with self._lock:
+                self._record_eval(L.gid, L.last_eval)
+        else:
+            self.store.set(_DONE.format(self.tag, L.gid), json.dumps({"eval": L.last_eval}))
+
+    # ---- the two entry points -----------------------------------------------------
+    _until = False
 
     def _pending(self) -> bool:
         if self._until:
-            return len(self._done) < self.world - 1
-        return any(self.next_task[r] < self.tasks for r in range(1, self.world))
+            return len(self._done) < len(self.remote)
+        return any(self.next_task[g] < self._goal[g] for g in self.remote)
 
-    _until = False
+    _goal: dict = {}  # rank 0, run(): the submission count each remote learner reaches
 
     def _serve_loop(self) -> None:
-        """Rank 0 service thread: serve submissions as they arrive."""
+        """Rank 0 service thread: serve the remote learners' submissions as
+        they arrive."""
         try:
             st = self.net.state
             if st.model32.is_cuda:
@@ -187,7 +412,6 @@ class AsyncCollectiveFederation:
                 stream = torch.cuda.Stream(device=st.model32.device)
                 ctx = torch.cuda.stream(stream)
             else:
-                import contextlib
                 ctx = contextlib.nullcontext()
             with ctx:
                 while self._pending():
@@ -196,114 +420,129 @@ class AsyncCollectiveFederation:
         except BaseException as e:  # noqa: BLE001 - re-raised on the main thread
             self._svc_error = e
 
-    def run(self, debug_delay_s: float = 0.0) -> list[AsyncUpdate]:
-        """Run ``tasks_per_learner`` asynchronous tasks on this learner; rank 0
-        also serves every other learner's submissions until all are done.
-        ``debug_delay_s``: sleep after each task (uneven learner speeds)."""
-        svc = None
-        if self.rank == 0 and self.threaded:
+    def _start_service(self):
+        if self.rank == 0 and self.world > 1 and self.remote and self.threaded:
             svc = threading.Thread(target=self._serve_loop, name="metisfl-async-aggregator", daemon=True)
             svc.start()
-        for task in range(self.tasks):
-            self.net.reset_train_stats()
-            left = self.num_local_updates
-            while left > 0:
-                k = min(left, self.poll_every) if (self.rank == 0 and not self.threaded) else left
-                self._train(k)
-                left -= k
-                if self.rank == 0 and not self.threaded:
-                    self.serve(block=False)
-            if debug_delay_s:
-                self._sync_stream()
-                time.sleep(debug_delay_s)
-            meta = {"task": task, "weight": self._weight(self.num_local_updates),
-                    "loss": self.net.train_stats()["loss"], "batches": self.num_local_updates,
-                    "base_version": self.base_version}
-            if self.rank == 0:
-                with self._lock:
-                    self._fedrec(0, self.net.state.model32, meta)
-                    self.net.state.model32.copy_(self._community())
-                    self._sync_stream()
-                    self.base_version = self.version
-                self._install()
-            else:
-                self.store.set(_KEY.format(self.tag, self.rank, task), json.dumps(meta))
-                dist.send(self.net.state.model32, dst=0, group=self.p2p)
-                dist.recv(self.net.state.model32, src=0, group=self.p2p)
-                self.base_version = int(self.store.get(_VER.format(self.tag, self.rank, task)))
-                self._install()
+            return svc
+        return None
+
+    def _end_service(self, svc) -> None:
+        if self.rank != 0:
+            return
+        if svc is not None:
+            svc.join()
+            if self._svc_error is not None:
+                raise RuntimeError("async aggregator thread failed") from self._svc_error
+        else:
+            while self._pending():
+                if not self.serve(block=False):
+                    time.sleep(0.001)
+
+    def run(self, debug_delay_s: float = 0.0) -> list[AsyncUpdate]:
+        """Run ``tasks_per_learner`` asynchronous tasks on every hosted learner;
+        rank 0 also serves every remote learner's submissions until all are
+        done.  ``debug_delay_s``: sleep after each task (uneven speeds)."""
+        self._until = False
         if self.rank == 0:
-            if svc is not None:
-                svc.join()
-                if self._svc_error is not None:
-                    raise RuntimeError("async aggregator thread failed") from self._svc_error
-            else:
-                while self._pending():
-                    if not self.serve(block=False):
-                        time.sleep(0.001)
+            self._goal = {g: self.next_task[g] + self.tasks for g in self.remote}
+        svc = self._start_service()
+        start = {L.j: L.tasks_run for L in self.learners}
+        self._drive(lambda L: L.tasks_run - start[L.j] < self.tasks, debug_delay_s)
+        self._end_service(svc)
         self._close_bookkeeping()
         return self.updates
 
-    def _sync_stream(self) -> None:
-        t = self.net.state.model32
-        if t.is_cuda:
-            torch.cuda.current_stream(t.device).synchronize()
+    def run_until(self, max_updates: int | None = None, cutoff_s: float | None = None,
+                  metric: str | None = None, metric_cutoff: float | None = None,
+                  debug_delay_s: float = 0.0, checkpoint_dir: str | None = None,
+                  checkpoint_every: int = 0, fault_task: int | None = None,
+                  on_fault=None) -> list[AsyncUpdate]:
+        """Asynchronous tasks until a termination signal: ``max_updates``
+        community versions (FedRec updates -- the reference's global
+        iterations), the wall-clock cutoff, the mean community-model test
+        metric of the learners' latest evaluations, or the driver's stop
+        request.  Every learner finishes the task it is running, is served,
+        and leaves; rank 0 serves until all remote learners have left.
+        ``checkpoint_dir`` / ``checkpoint_every``: see the module docstring;
+        ``fault_task``: the rank calls ``on_fault`` when one of its learners
+        is about to start that task (1 = its first; fault injection)."""
+        self._until = True
+        self.ckpt_dir, self.ckpt_every = checkpoint_dir, int(checkpoint_every or 0)
+        self._max_updates = max_updates
+        self._deadline = time.time() + cutoff_s if cutoff_s else None
+        self._metric, self._metric_cutoff = metric, metric_cutoff
+        self.stop_reason = None
+        svc = self._start_service()
 
-    def _install(self) -> None:
-        st = self.net.state
-        st.refresh_bf16()
-        st.set_anchor()
+        def after(L: _Local) -> None:
+            if self.ckpt_dir and self.ckpt_every and L.task_index % self.ckpt_every == 0:
+                self._checkpoint_learner(L)
+
+        self._drive(lambda L: not self._stopped(), debug_delay_s, fault_task, on_fault, after)
+        self._end_service(svc)
+        if self.rank == 0 and self.ckpt_dir:
+            self._checkpoint_aggregator(block=True)
+        if self.ckpt_dir:
+            for L in self.learners:
+                self._checkpoint_learner(L, block=True)
+        self.flush()
+        self._close_bookkeeping()
+        self.tasks_run = sum(L.tasks_run for L in self.learners)
+        return self.updates
 
     # ---- aggregator side (rank 0) ---------------------------------------------------
     def serve(self, block: bool = False) -> int:
-        """Apply every pending submission (FedRec) and answer it with the
-        community model.  Returns the number served."""
+        """Apply every pending remote submission (FedRec) and answer it with
+        the community model.  Returns the number served."""
         served = 0
-        for r in range(1, self.world):
-            t = self.next_task[r]
-            if (not self._until and t >= self.tasks) or r in self._done:
+        for g in self.remote:
+            t = self.next_task[g]
+            if (not self._until and t >= self._goal[g]) or g in self._done:
                 continue
-            key = _KEY.format(self.tag, r, t)
+            key = _KEY.format(self.tag, g, t)
             if not block and not self.store.check([key]):
                 if self._until:
-                    dkey = _DONE.format(self.tag, r)
+                    dkey = _DONE.format(self.tag, g)
                     if self.store.check([dkey]):  # its last submission was served
-                        self._record_eval(r, json.loads(self.store.get(dkey)).get("eval"))
-                        self._done.add(r)
+                        with self._lock:
+                            self._record_eval(g, json.loads(self.store.get(dkey)).get("eval"))
+                        self._done.add(g)
                 continue
             meta = json.loads(self.store.get(key))
-            self._record_eval(r, meta.get("eval"))
-            dist.recv(self.rbuf, src=r, group=self.p2p)
+            src = self.owners[g]
+            dist.recv(self.rbuf, src=src, group=self.p2p)
             with self._lock:
-                self._fedrec(r, self.rbuf, meta)
+                self._record_eval(g, meta.get("eval"))
+                self._fedrec(g, self.rbuf, meta)
                 comm_model = self._community()
                 ver = self.version
                 self._sync_stream()
-            self.store.set(_VER.format(self.tag, r, t), str(ver))
-            dist.send(comm_model, dst=r, group=self.p2p)
-            self.next_task[r] = t + 1
+                self._after_update()
+            self.store.set(_VER.format(self.tag, g, t), str(ver))
+            dist.send(comm_model, dst=src, group=self.p2p)
+            self.next_task[g] = t + 1
             served += 1
-            self._after_update()
         return served
 
-    def _fedrec(self, r: int, theta: torch.Tensor, meta: dict) -> None:
+    def _fedrec(self, g: int, theta: torch.Tensor, meta: dict) -> None:
         t0 = time.perf_counter()
         stale = self.version - int(meta.get("base_version", self.version))
         w0 = float(meta["weight"])
         w = w0 * staleness_discount(self.cfg.staleness, stale, self.cfg.staleness_a, self.cfg.staleness_b)
-        if self.last[r] is not None:
-            agg.rolling_op(self.S, self.last[r], agg.MERGE_SUB, self.last_w[r])
-            self.Z -= self.last_w[r]
+        if self.last[g] is not None:
+            agg.rolling_op(self.S, self.last[g], agg.MERGE_SUB, self.last_w[g])
+            self.Z -= self.last_w[g]
         else:
-            self.last[r] = torch.empty_like(theta)
+            self.last[g] = torch.empty_like(theta)
         agg.rolling_op(self.S, theta, agg.MERGE_ADD, w)
         self.Z += w
-        self.last[r].copy_(theta)
-        self.last_w[r] = w
+        self.last[g].copy_(theta)
+        self.last_w[g] = w
         self.version += 1
-        if theta.is_cuda:  # this stream only: rank 0's training keeps running on its own
+        if theta.is_cuda:  # this thread's stream only: the learners keep running on theirs
             torch.cuda.current_stream(theta.device).synchronize()
-        up = AsyncUpdate(r, int(meta["task"]), w, time.time(), (time.perf_counter() - t0) * 1e3,
+        up = AsyncUpdate(g, int(meta["task"]), w, time.time(), (time.perf_counter() - t0) * 1e3,
                          float(meta["loss"]), int(meta["batches"]), stale, w0)
         self.updates.append(up)
         if self.engine is not None:
@@ -311,7 +550,7 @@ class AsyncCollectiveFederation:
             # finisher's local task lineage (the reference's async controller
             # records both per completion, controller.cc:201-259, 428-518);
             # sent by the bookkeeping thread, not under the aggregator lock
-            self._bookkeep("update", self.version, r, meta, up)
+            self._bookkeep("update", self.version, g, meta, up)
         self._after_fedrec()
 
     def _community(self) -> torch.Tensor:
@@ -319,21 +558,51 @@ class AsyncCollectiveFederation:
         agg.rolling_op(c, None, agg.SCALE_DIV, self.Z)
         return c
 
+    def community(self) -> torch.Tensor:
+        return self._community()
+
     def community_reference(self) -> np.ndarray:
-        """Host recomputation of sum_i w_i theta_i / sum_i w_i over the latest
+        """Host recomputation of sum_g w_g theta_g / sum_g w_g over the latest
         contributions (tests)."""
         xs = [x.double().cpu().numpy() for x in self.last if x is not None]
         ws = [w for x, w in zip(self.last, self.last_w) if x is not None]
         return sum(w * x for w, x in zip(ws, xs)) / sum(ws)
 
+    def _after_update(self) -> None:
+        """Rank 0, under the lock, after every FedRec update: the termination
+        signals."""
+        if not self._until or self._stop_flag:
+            return
+        why = None
+        if self._max_updates and self.version >= self._max_updates:
+            why = "rounds"
+        elif self._deadline is not None and time.time() > self._deadline:
+            why = "time"
+        elif self._metric_cutoff is not None and self.evaluations:
+            last = [e for e in self.evaluations if e["num_examples"]][-self.G:]
+            vals = [e.get(self._metric) for e in last if e.get(self._metric) is not None]
+            if vals and float(np.mean(vals)) >= self._metric_cutoff:
+                why = "metric"
+        if why is None and self._driver_stop:
+            why = "driver"
+        if why is not None:
+            self._stop_flag = True
+            self.stop_reason = why
+            if self.store is not None:
+                self.store.set(_STOP.format(self.tag), why)
 
-    # ---- termination-driven mode (the driver-launched asynchronous protocol) ------------
-    def _record_eval(self, r: int, ev) -> None:
+    def _stopped(self) -> bool:
+        if self.rank == 0:
+            return self._stop_flag
+        return bool(self.store.check([_STOP.format(self.tag)]))
+
+    # ---- termination-driven mode: evaluations ---------------------------------------
+    def _record_eval(self, g: int, ev) -> None:
         """A learner's evaluation of the community model version it received
         (it rides in its next submission / its done message)."""
         if not ev:
             return
-        rec = {"version": int(ev["version"]), "learner": r, "loss": float(ev["loss"]),
+        rec = {"version": int(ev["version"]), "learner": g, "loss": float(ev["loss"]),
                "accuracy": float(ev["accuracy"]), "num_examples": int(ev.get("n", 0))}
         self.evaluations.append(rec)
         if self.engine is not None:
@@ -414,14 +683,15 @@ class AsyncCollectiveFederation:
             return
         v, root = self.version, self.ckpt_dir
         tensors = {"S": self.S}
-        for r, x in enumerate(self.last):
+        for g, x in enumerate(self.last):
             if x is not None:
-                tensors[f"last{r}"] = x
-        meta = {"Z": float(self.Z), "last_w": list(self.last_w), "version": v, "world": self.world,
-                "learner_ids": list(getattr(self, "learner_ids", [f"learner_{r}" for r in range(self.world)])),
+                tensors[f"last:{self.learner_ids[g]}"] = x
+        meta = {"Z": float(self.Z), "version": v, "world": self.world, "learners": self.G,
+                "learner_ids": list(self.learner_ids),
+                "last_w": {self.learner_ids[g]: w for g, w in enumerate(self.last_w) if self.last[g] is not None},
                 "protocol": "asynchronous", "global_iteration": v,
-                "updates": [{"learner": u.learner, "task": u.task, "weight": u.weight, "staleness": u.staleness}
-                            for u in self.updates[-1000:]]}
+                "updates": [{"learner": self.learner_ids[u.learner], "task": u.task, "weight": u.weight,
+                             "staleness": u.staleness} for u in self.updates[-1000:]]}
         st = self.net.state
         n_contrib = sum(1 for x in self.last if x is not None)
 
@@ -448,19 +718,23 @@ class AsyncCollectiveFederation:
         if block:
             self._ckpt.wait()
 
-    def _checkpoint_learner(self, block: bool = False) -> None:
-        """This learner's local state after a task (any rank)."""
+    @staticmethod
+    def learner_file(root: str, lid: str) -> str:
+        return os.path.join(root, f"async_learner_{lid}.pt")
+
+    def _checkpoint_learner(self, L: _Local, block: bool = False) -> None:
+        """Learner L's local state after a task, keyed by its stable id."""
         from metisfl_amd.parallel import checkpoint as ck
-        if self._lckpt is None:
-            self._lckpt = ck.AsyncSnapshot(self.net.state.model32.device, "metisfl-async-learner")
-        st = self.net.state
-        tensors = {"step": st.step, "perm": self.train_ds.perm}
+        if L.lckpt is None:
+            L.lckpt = ck.AsyncSnapshot(L.net.state.model32.device, f"metisfl-async-learner-{L.lid}")
+        st = L.net.state
+        tensors = {"step": st.step, "perm": L.train_ds.perm}
         for k in ("m", "v", "anchor"):
             t = getattr(st, k)
             if t is not None:
                 tensors[k] = t
-        host = {"steps_done": self.steps_done, "base_version": self.base_version, "task": self.task_index}
-        path = os.path.join(self.ckpt_dir, f"async_learner_rank{self.rank}.pt")
+        host = {"steps_done": L.steps_done, "base_version": L.base_version, "task": L.task_index}
+        path = self.learner_file(self.ckpt_dir, L.lid)
 
         def write(h):
             d = {k: t.clone() for k, t in h.items()}
@@ -469,190 +743,77 @@ class AsyncCollectiveFederation:
 
         os.makedirs(self.ckpt_dir, exist_ok=True)
         if block:
-            self._lckpt.submit(tensors, write)
-            self._lckpt.wait()
+            L.lckpt.submit(tensors, write)
+            L.lckpt.wait()
         else:
-            self._lckpt.try_submit(tensors, write)
+            L.lckpt.try_submit(tensors, write)
 
     def flush(self) -> None:
-        for w in (self._ckpt, self._lckpt, self._lineage):
+        for w in [self._ckpt, self._lineage] + [L.lckpt for L in self.learners]:
             if w is not None:
                 w.wait()
 
     def resume(self, path: str, prev_rank: int | None = None) -> None:
         """Collective.  Continue an asynchronous federation from its last
-        checkpoint on (possibly) fewer learners: rank 0 restores the FedRec
-        state with the contributions of the learners still present (old rank
-        ``prev_rank`` of each new rank) and without the lost ones, every
-        learner restores its local state and starts from the restored
-        community model; the version count continues."""
+        checkpoint on (possibly) fewer learners, on any placement: every
+        learner restores its local state from its own file (stable learner
+        id), rank 0 restores the FedRec state of the learner ids present now
+        and drops the contributions of the ones that are gone; everyone starts
+        from the restored community model and the version count continues.
+        (``prev_rank``: accepted for the driver's legacy relaunch arguments;
+        state is matched by learner id.)"""
         from metisfl_amd.parallel import checkpoint as ck
-        prev = self.rank if prev_rank is None else int(prev_rank)
         dev = self.net.state.model32.device
-        prevs = self.comm.all_gather_rows(torch.tensor([float(prev)], dtype=torch.float64, device=dev))
-        prevs = [int(x) for x in prevs.cpu().numpy()[:, 0]]
-        st = self.net.state
-        lpath = os.path.join(path, f"async_learner_rank{prev}.pt")
-        if os.path.exists(lpath):
+        for L in self.learners:
+            st = L.net.state
+            lpath = self.learner_file(path, L.lid)
+            if not os.path.exists(lpath):
+                continue
             d = torch.load(lpath, weights_only=True)
             st.step.copy_(d["step"].to(dev))
             for k in ("m", "v"):
                 if k in d and getattr(st, k) is not None and d[k].numel() == getattr(st, k).numel():
                     getattr(st, k).copy_(d[k].to(dev))
-            if d["perm"].numel() == self.train_ds.perm.numel():
-                self.train_ds.perm.copy_(d["perm"].to(dev))
-                self.steps_done = int(d["steps_done"])
-            self.task_index = int(d["task"])
+            if d["perm"].numel() == L.train_ds.perm.numel():
+                L.train_ds.perm.copy_(d["perm"].to(dev))
+                L.steps_done = int(d["steps_done"])
+            L.task_index = int(d["task"])
         found = ck.resolve(path)
         ver = torch.zeros(1, dtype=torch.float64, device=dev)
+        st = self.net.state
         if self.rank == 0 and found is not None:
             with open(os.path.join(found, "federation.json")) as f:
                 meta = json.load(f)
             state = torch.load(os.path.join(found, "async_state.pt"), weights_only=True)
             S = state["S"].to(dev)
             Z = float(meta["Z"])
-            old_w = list(meta["last_w"])
-            self.last = [None] * self.world
-            self.last_w = [0.0] * self.world
-            keep = set()
-            for r, p in enumerate(prevs):
-                x = state.get(f"last{p}")
-                if x is not None:
-                    self.last[r] = x.to(dev)
-                    self.last_w[r] = float(old_w[p])
-                    keep.add(p)
-            for p in range(int(meta["world"])):  # the lost learners leave the running sum
-                x = state.get(f"last{p}")
-                if p not in keep and x is not None:
-                    agg.rolling_op(S, x.to(dev), agg.MERGE_SUB, float(old_w[p]))
-                    Z -= float(old_w[p])
+            old_w = dict(meta["last_w"])
+            present = {lid: g for g, lid in enumerate(self.learner_ids)}
+            self.last = [None] * self.G
+            self.last_w = [0.0] * self.G
+            dropped = []
+            for lid, w in old_w.items():
+                x = state.get(f"last:{lid}")
+                if x is None:
+                    continue
+                if lid in present:
+                    g = present[lid]
+                    self.last[g] = x.to(dev)
+                    self.last_w[g] = float(w)
+                else:  # the lost learners leave the running sum
+                    agg.rolling_op(S, x.to(dev), agg.MERGE_SUB, float(w))
+                    Z -= float(w)
+                    dropped.append(lid)
             self.S.copy_(S)
             self.Z = Z
             self.version = int(meta["version"])
-            self.resumed = {"version": self.version, "dropped": sorted(set(range(int(meta["world"]))) - keep)}
+            self.resumed = {"version": self.version, "dropped": sorted(dropped)}
             st.model32.copy_(self._community())
             ver[0] = self.version
         self.comm.broadcast_(ver, src=0)
         self.comm.broadcast_(st.model32, src=0)
-        self.base_version = int(ver.item())
-        st.refresh_bf16()
-        st.set_anchor()
-
-    def _after_update(self) -> None:
-        """Rank 0, after every FedRec update: the termination signals."""
-        if not self._until or self._stop_flag:
-            return
-        why = None
-        if self._max_updates and self.version >= self._max_updates:
-            why = "rounds"
-        elif self._deadline is not None and time.time() > self._deadline:
-            why = "time"
-        elif self._metric_cutoff is not None and self.evaluations:
-            last = [e for e in self.evaluations if e["num_examples"]][-self.world:]
-            vals = [e.get(self._metric) for e in last if e.get(self._metric) is not None]
-            if vals and float(np.mean(vals)) >= self._metric_cutoff:
-                why = "metric"
-        if why is None and self._driver_stop:
-            why = "driver"
-        if why is not None:
-            self._stop_flag = True
-            self.stop_reason = why
-            self.store.set(_STOP.format(self.tag), why)
-
-    def _stopped(self) -> bool:
-        if self.rank == 0:
-            return self._stop_flag
-        return bool(self.store.check([_STOP.format(self.tag)]))
-
-    def _evaluate_received(self) -> dict | None:
-        if self.test_ds is None or not self.cfg.evaluate_community:
-            return None
-        ev = self.net.evaluate(self.test_ds, self.cfg.eval_max_steps)
-        return {"version": self.base_version, "loss": ev["loss"], "accuracy": ev["accuracy"], "n": self.test_ds.n}
-
-    def run_until(self, max_updates: int | None = None, cutoff_s: float | None = None,
-                  metric: str | None = None, metric_cutoff: float | None = None,
-                  debug_delay_s: float = 0.0, checkpoint_dir: str | None = None,
-                  checkpoint_every: int = 0, fault_task: int | None = None,
-                  on_fault=None) -> list[AsyncUpdate]:
-        """Asynchronous tasks until a termination signal: ``max_updates``
-        community versions (FedRec updates -- the reference's global
-        iterations), the wall-clock cutoff, the mean community-model test
-        metric of the learners' latest evaluations, or the driver's stop
-        request.  Every learner finishes the task it is running, is served,
-        and leaves; rank 0 serves until all have left.  ``checkpoint_dir`` /
-        ``checkpoint_every``: see the module docstring; ``fault_task``: this
-        learner calls ``on_fault`` when it is about to start that task (1 =
-        its first; fault injection for tests)."""
-        self._until = True
-        self.ckpt_dir, self.ckpt_every = checkpoint_dir, int(checkpoint_every or 0)
-        self._max_updates = max_updates
-        self._deadline = time.time() + cutoff_s if cutoff_s else None
-        self._metric, self._metric_cutoff = metric, metric_cutoff
-        self.stop_reason = None
-        svc = None
-        if self.rank == 0 and self.world > 1:
-            if not self.threaded:
-                raise RuntimeError("run_until needs the threaded aggregator (serve_in_thread=True)")
-            svc = threading.Thread(target=self._serve_loop, name="metisfl-async-aggregator", daemon=True)
-            svc.start()
-        task, last_eval = self.task_index, None
-        # submission keys count this run's tasks from 0 (rank 0's next_task
-        # does): a resumed learner's task_index continues its lifetime count
-        sub = 0
-        spe = self.train_ds.steps_per_epoch
-        while not self._stopped():
-            if fault_task is not None and task + 1 == int(fault_task) and on_fault is not None:
-                self.flush()
-                on_fault(task + 1)
-            self.net.reset_train_stats()
-            t_task = time.time()
-            self._train(self.num_local_updates)
-            self._sync_stream()
-            if debug_delay_s:
-                time.sleep(debug_delay_s)  # test hook: uneven learner speeds
-            ms_b = (time.time() - t_task) * 1e3 / max(1, self.num_local_updates)
-            tr = self.net.train_stats()
-            meta = {"task": task, "weight": self._weight(self.num_local_updates),
-                    "loss": tr["loss"], "accuracy": tr["accuracy"], "batches": self.num_local_updates,
-                    "base_version": self.base_version, "eval": last_eval, "started_at": t_task,
-                    "n_train": int(self.train_ds.n), "ms_per_batch": ms_b, "ms_per_epoch": ms_b * spe,
-                    "epochs": self.num_local_updates / spe}
-            if self.rank == 0:
-                with self._lock:
-                    self._record_eval(0, last_eval)
-                    self._fedrec(0, self.net.state.model32, meta)
-                    self.net.state.model32.copy_(self._community())
-                    self._sync_stream()
-                    self.base_version = self.version
-                    self._after_update()
-                self._install()
-            else:
-                self.store.set(_KEY.format(self.tag, self.rank, sub), json.dumps(meta))
-                dist.send(self.net.state.model32, dst=0, group=self.p2p)
-                dist.recv(self.net.state.model32, src=0, group=self.p2p)
-                self.base_version = int(self.store.get(_VER.format(self.tag, self.rank, sub)))
-                self._install()
-            last_eval = self._evaluate_received()
-            sub += 1
-            task += 1
-            self.task_index = task
-            if self.ckpt_dir and self.ckpt_every and task % self.ckpt_every == 0:
-                self._checkpoint_learner()
-        if self.rank == 0:
-            with self._lock:
-                self._record_eval(0, last_eval)
-            if svc is not None:
-                svc.join()
-                if self._svc_error is not None:
-                    raise RuntimeError("async aggregator thread failed") from self._svc_error
-            if self.ckpt_dir:
-                self._checkpoint_aggregator(block=True)
-        else:
-            self.store.set(_DONE.format(self.tag, self.rank), json.dumps({"eval": last_eval}))
-        if self.ckpt_dir:
-            self._checkpoint_learner(block=True)
-        self.flush()
-        self._close_bookkeeping()
-        self.tasks_run = task
-        return self.updates
+        for L in self.learners:
+            if L.net is not self.net:
+                L.net.state.model32.copy_(st.model32)
+            L.base_version = int(ver.item())
+            self._install(L)

@@ -33,6 +33,7 @@ import time
 import torch
 
 LATEST = "LATEST"
+PUBLISH_POLL_S = 0.05  # rank 0's poll interval for the other ranks' checkpoint keys
 
 
 def resolve(path: str | None) -> str | None:
@@ -210,7 +211,15 @@ def publish(root: str, name: str, store=None, world: int = 1, key: str = "", kee
     stay)."""
     if store is not None and world > 1:
         keys = [f"{key}/{r}" for r in range(world)]
-        store.wait(keys, _td(timeout_s))
+        # short polls, not one long store.wait: the c10d store client
+        # serialises its operations, and the rank watchdog's heartbeats go
+        # through the same client (ADVICE r4) -- a blocking wait for a slow or
+        # dead peer's key would silence this rank's heartbeat as well
+        end = time.time() + timeout_s
+        while not store.check(keys):
+            if time.time() > end:
+                raise TimeoutError(f"checkpoint {name}: not every rank reported its files in {timeout_s:.0f} s")
+            time.sleep(PUBLISH_POLL_S)
     atomic_write(os.path.join(root, LATEST), name.encode())
     rounds = sorted((d for d in os.listdir(root) if d.startswith("round_") and d != name),
                     key=lambda d: int(d.split("_")[1]) if d.split("_")[1].isdigit() else -1)
@@ -218,6 +227,3 @@ def publish(root: str, name: str, store=None, world: int = 1, key: str = "", kee
         shutil.rmtree(os.path.join(root, d), ignore_errors=True)
 
 
-def _td(s: float):
-    import datetime
-    return datetime.timedelta(seconds=s)

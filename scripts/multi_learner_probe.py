@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--dtype", default="fp32", choices=("fp32", "bf16"))
     ap.add_argument("--serial", action="store_true", help="one stream (baseline)")
     ap.add_argument("--hw-queues", type=int, default=0)
+    ap.add_argument("--tconv", type=int, default=0,
+                    help="1: the throughput backward kernels (tconv.hip), as CoLocatedLearners sets from 4 learners")
     ap.add_argument("--stagger-us", type=float, default=0.0,
                     help="delay stream g's first launch by (g %% 4) x this many microseconds (phase offset)")
     ap.add_argument("--cu-mask", choices=("none", "contig", "interleave"), default="none",
@@ -42,6 +44,8 @@ def main():
                        optimizer=OptimizerSpec("momentum_sgd", 0.005, momentum=0.75))
         x = torch.randn((1024, 32, 32, 3), generator=gen, device="cuda")
         y = torch.randint(0, 10, (1024,), generator=gen, device="cuda")
+        if a.tconv:
+            net.set_throughput_conv(True)
         nets.append(net)
         dss.append(net.make_dataset(x, y, seed=i))
     for net, ds in zip(nets, dss):  # capture (1-step and K-step graphs)

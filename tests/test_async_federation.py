@@ -93,3 +93,89 @@ def test_async_staleness_aware_weights(tmp_path):
     assert r0["stale"][0][0] == 0          # the very first update is fresh
     assert any(st > 0 for st, _, _ in r0["stale"])
     assert r0["max_err"] < 1e-5
+
+
+def _coloc_worker(rank, world, port, out_dir, per_rank, tasks):
+    """Rank r hosts ``per_rank`` co-located learners (global ids r*per_rank + j)."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from metisfl_amd.models.sequential import HousingMLP
+    from metisfl_amd.ops.optim import OptimizerSpec
+    from metisfl_amd.parallel.async_federation import AsyncCollectiveFederation
+    from metisfl_amd.parallel.comm import Comm
+    from metisfl_amd.parallel.federation import FederationConfig
+    comm = Comm(backend="gloo")
+    nets, dss = [], []
+    gids = [rank * per_rank + j for j in range(per_rank)]
+    for g in gids:
+        net = HousingMLP(batch_size=4, device="cpu", seed=g + 1, optimizer=OptimizerSpec("vanilla_sgd", 0.01))
+        rng = np.random.default_rng(g)
+        n = 8 + 4 * g
+        nets.append(net)
+        dss.append(net.make_dataset(rng.standard_normal((n, 13)).astype(np.float32),
+                                    rng.standard_normal(n).astype(np.float32), seed=g))
+    owners = [g // per_rank for g in range(world * per_rank)]
+    cfg = FederationConfig(batch_size=4, local_epochs=1, evaluate_test=False, staleness="polynomial")
+    fed = AsyncCollectiveFederation(comm, nets, dss, cfg, tasks_per_learner=tasks, gids=gids, owners=owners,
+                                    learner_ids=[f"L{g}" for g in range(len(owners))])
+    ups = fed.run()
+    res = {"rank": rank, "finals": [n.state.model32.numpy().tolist() for n in nets]}
+    if rank == 0:
+        res["updates"] = [(u.learner, u.task, u.base_weight, u.staleness) for u in ups]
+        ref = fed.community_reference()
+        got = fed._community().double().numpy()
+        res["max_err"] = float(np.abs(got - ref).max() / (np.abs(ref).max() + 1e-12))
+        res["community"] = got.tolist()
+    with open(os.path.join(out_dir, f"coloc_{rank}.json"), "w") as f:
+        json.dump(res, f)
+    comm.barrier()
+    comm.close()
+
+
+def test_async_fedrec_colocated_learners_on_two_ranks(tmp_path):
+    """The reference schedules asynchronously per LEARNER whatever the
+    placement (asynchronous_scheduler.h:12-18): 2 ranks x 2 co-located
+    learners = 4 FedRec participants; every task of every learner is applied
+    in order with its own NUM_TRAINING_EXAMPLES weight, and the incremental
+    community equals the host recomputation over each learner's latest model."""
+    world, per, tasks = 2, 2, 3
+    mp.start_processes(_coloc_worker, args=(world, _free_port(), str(tmp_path), per, tasks), nprocs=world,
+                       join=True, start_method="spawn")
+    r0 = json.load(open(tmp_path / "coloc_0.json"))
+    ups = r0["updates"]
+    assert len(ups) == world * per * tasks
+    for g in range(world * per):
+        assert [t for (l, t, _, _) in ups if l == g] == list(range(tasks))
+        assert all(w == 8 + 4 * g for (l, _, w, _) in ups if l == g)
+    assert any(st > 0 for (_, _, _, st) in ups)  # interleaved finishers: staleness
+    assert r0["max_err"] < 1e-5
+    for r in range(world):
+        res = json.load(open(tmp_path / f"coloc_{r}.json"))
+        assert all(np.all(np.isfinite(f)) for f in res["finals"])
+
+
+def test_async_colocated_single_process():
+    """World 1 (no process group): several co-located learners, all FedRec on
+    rank 0's device path -- the on-one-GPU asynchronous configuration."""
+    from metisfl_amd.models.sequential import HousingMLP
+    from metisfl_amd.ops.optim import OptimizerSpec
+    from metisfl_amd.parallel.async_federation import AsyncCollectiveFederation
+    from metisfl_amd.parallel.comm import Comm
+    from metisfl_amd.parallel.federation import FederationConfig
+    comm = Comm(backend="gloo")  # no RANK / WORLD_SIZE here: world 1, no process group
+    assert not comm.distributed
+    nets, dss = [], []
+    for g in range(3):
+        net = HousingMLP(batch_size=4, device="cpu", seed=g + 1, optimizer=OptimizerSpec("vanilla_sgd", 0.01))
+        rng = np.random.default_rng(g)
+        nets.append(net)
+        dss.append(net.make_dataset(rng.standard_normal((8 + 4 * g, 13)).astype(np.float32),
+                                    rng.standard_normal(8 + 4 * g).astype(np.float32), seed=g))
+    cfg = FederationConfig(batch_size=4, local_epochs=1, evaluate_test=False)
+    fed = AsyncCollectiveFederation(comm, nets, dss, cfg, tasks_per_learner=2)
+    ups = fed.run()
+    assert len(ups) == 6 and fed.version == 6
+    assert sorted(u.learner for u in ups) == [0, 0, 1, 1, 2, 2]
+    ref = fed.community_reference()
+    assert np.abs(fed.community().double().numpy() - ref).max() <= 1e-5 * (np.abs(ref).max() + 1e-12)

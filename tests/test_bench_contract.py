@@ -92,6 +92,22 @@ def test_async_bench_colocated_learners():
     assert d["community_model_matches_host"] is True
 
 
+def test_async_bench_colocated_learners_on_two_ranks():
+    """BASELINE config 3 at N = 2: 8 asynchronous learners, 4 co-located per
+    rank -- every learner a FedRec participant (rank 0's on the device, rank
+    1's over point-to-point transfers)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "async_bench.py"), "--gpus", "2",
+                        "--learners", "8", "--train-size", "128", "--batch", "4", "--tasks", "2", "--warmup", "0",
+                        "--width-mult", "0.125", "--delays-ms", "0,30"], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["learners"] == 8 and d["config"]["learners_per_gpu"] == 4
+    assert d["updates"] == 16 and d["updates_per_learner"] == [2] * 8
+    assert d["staleness_max"] > 0
+    assert d["community_model_matches_host"] is True
+
+
 def test_async_bench_eight_ranks_uneven_delays():
     """8 asynchronous learners (gloo) with uneven per-task delays: the
     threaded aggregator serves every submission under contention, staleness

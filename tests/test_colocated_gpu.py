@@ -1,6 +1,6 @@
 """Co-located learners on the GPU beyond synchronous FedAvg: the
-asynchronous protocol (FedRec on the device after each finished task,
-parallel/async_colocated.py) and CKKS secure aggregation with one
+asynchronous protocol (FedRec on the device after each finished task, the
+one FedRec core of parallel/async_federation.py) and CKKS secure aggregation with one
 encryption per co-located learner (encryption/device.py
 secure_weighted_allreduce_many)."""
 import numpy as np
@@ -27,16 +27,20 @@ def _learners(n, batch=32, shard=128, lr=0.005):
 
 def test_colocated_async_fedrec_on_device():
     from metisfl_amd.models.colocated import CoLocatedLearners
-    from metisfl_amd.parallel.async_colocated import CoLocatedAsyncFederation
+    from metisfl_amd.parallel.async_federation import AsyncCollectiveFederation
+    from metisfl_amd.parallel.comm import Comm
     from metisfl_amd.parallel.federation import FederationConfig
     nets, dss = _learners(3)
-    cfg = FederationConfig(protocol="asynchronous", batch_size=32, local_epochs=1, staleness="polynomial")
-    fed = CoLocatedAsyncFederation(CoLocatedLearners(nets, dss), cfg)
-    ups = fed.run(3)
+    cfg = FederationConfig(protocol="asynchronous", batch_size=32, local_epochs=1, staleness="polynomial",
+                           evaluate_test=False)
+    group = CoLocatedLearners(nets, dss)
+    fed = AsyncCollectiveFederation(Comm(), nets, dss, cfg, tasks_per_learner=3, streams=group.streams)
+    ups = fed.run()
     torch.cuda.synchronize()
     assert len(ups) == 9 and sorted(u.learner for u in ups) == [0, 0, 0, 1, 1, 1, 2, 2, 2]
     assert fed.version == 9 and max(u.staleness for u in ups) > 0
     assert all(np.isfinite(u.train_loss) for u in ups)
+    assert len({id(s) for s in fed.streams}) == 3  # one stream per co-located learner
     ref = fed.community_reference()
     got = fed.community().double().cpu().numpy()
     assert np.allclose(got, ref, rtol=1e-5, atol=1e-6), np.abs(got - ref).max()

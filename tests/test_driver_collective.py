@@ -146,7 +146,7 @@ def test_async_collective_recovers_from_a_lost_rank(tmp_path):
     log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
     line = [l for l in log.splitlines() if l.startswith("[collective-async] resumed at version")]
     assert line and int(line[-1].split("version ")[1].split()[0]) == rc["resumed_from_round"]
-    assert "dropped old ranks [2]" in line[-1]
+    assert "dropped learners ['localhost-2']" in line[-1]
     md = stats["federation_runtime_metadata"]["metadata"]
     assert max(int(m["global_iteration"]) for m in md) >= 10
     # BOTH survivors were served after the resume (before the fix rank 1
@@ -259,3 +259,72 @@ def test_learners_sharing_a_device_are_colocated_in_one_rank(tmp_path):
     assert sorted(f for f in os.listdir(ck) if f.startswith("learner_")) == [
         "learner_localhost-0.safetensors", "learner_localhost-1.safetensors",
         "learner_localhost-2.safetensors"]
+
+
+def _session_devices(tmp_path, devices, rounds, protocol="Asynchronous", **opts):
+    """Learners placed on devices (learners naming the same device share one
+    rank: co-located)."""
+    from metisfl_amd.driver.driver_session import DriverSession, free_port
+    from metisfl_amd.models.model_def import StaticModelDef
+    from metisfl_amd.utils.fedenv_parser import FederationEnvironment
+    d = env_dict([free_port() for _ in range(len(devices))], rounds=rounds, protocol=protocol)
+    d["FederationEnvironment"]["DataPlane"] = "rccl"
+    for l, dev in zip(d["FederationEnvironment"]["Learners"], devices):
+        l["Devices"] = dev
+    return DriverSession(FederationEnvironment(config=d), StaticModelDef("resnet18", width_mult=0.125), train_recipe,
+                         None, eval_recipe, working_dir=str(tmp_path / "w"), device="cpu", collective_options=opts)
+
+
+def test_async_colocated_learners_through_the_driver(tmp_path):
+    """The reference's asynchronous configs place several learners on one GPU
+    (examples/config/fashionmnist/test_localhost_asynchronous_vanillasgd.yaml:
+    all 10 on GPU 0) and schedule each learner on its own
+    (asynchronous_scheduler.h:12-18).  4 learners on 2 devices -> 2 ranks of 2
+    co-located learners, each learner a FedRec participant: one
+    runtime-metadata record per community version up to the budget, every
+    learner contributing, stale updates from the slower rank."""
+    sess = _session_devices(tmp_path, [[0], [0], [1], [1]], rounds=12, checkpoint_every=2,
+                            extra={"debug_delay_s": {"1": 0.3}})
+    stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason
+    job = json.load(open(os.path.join(str(tmp_path / "w"), "collective_job.json")))
+    assert job["ranks"] == [[0, 1], [2, 3]]
+    md = stats["federation_runtime_metadata"]["metadata"]
+    gis = sorted(int(m["global_iteration"]) for m in md)
+    assert gis[:12] == list(range(1, 13))
+    who = {lid for m in md for lid in m.get("completed_by_learner_id", [])}
+    assert len(who) == 4, who
+    log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
+    line = [l for l in log.splitlines() if l.startswith("[collective-async]")][-1]
+    assert "over 4 learners on 2 ranks" in line
+    stal = json.loads(line.split("staleness ")[1])
+    assert max(stal) > 0
+    assert stats["community_model_results"]["community_evaluation"]
+
+
+def test_async_colocated_rank_lost_resumes_from_checkpoint(tmp_path):
+    """Rank 1 (hosting learners 2 and 3) dies at its learners' second task;
+    the driver relaunches the survivors (learners 0 and 1, now one rank) from
+    the last checkpointed community version, their FedRec contributions kept
+    by learner id and the lost learners' dropped, and the federation reaches
+    its version budget."""
+    sess = _session_devices(tmp_path, [[0], [0], [1], [1]], rounds=14, fault={"rank": 1, "round": 2},
+                            heartbeat_timeout_s=8, checkpoint_every=1, extra={"debug_delay_s": {"0": 0.2}})
+    stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason
+    rc = sess.recoveries[0]
+    assert len(sess.recoveries) == 1 and rc["failed"] == ["learner_localhost-2"]
+    assert sorted(rc["lost_learners"]) == ["localhost-2", "localhost-3"] and rc["survivors"] == 2
+    assert rc["resumed_from_round"] is not None and rc["resumed_from_round"] >= 1
+    log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
+    line = [l for l in log.splitlines() if l.startswith("[collective-async] resumed at version")]
+    assert line and int(line[-1].split("version ")[1].split()[0]) == rc["resumed_from_round"]
+    # the lost learners' contributions leave the running sum (a learner whose
+    # first task had not finished contributed nothing yet)
+    dropped = json.loads(line[-1].split("dropped learners ")[1].rstrip(")").replace("'", '"'))
+    assert dropped and set(dropped) <= {"localhost-2", "localhost-3"}, dropped
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert max(int(m["global_iteration"]) for m in md) >= 14
+    after = {lid for m in md if int(m["global_iteration"]) > rc["resumed_from_round"]
+             for lid in m.get("completed_by_learner_id", [])}
+    assert len(after) == 2, after  # both survivors served after the resume

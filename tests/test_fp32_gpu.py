@@ -392,16 +392,18 @@ def _x8(x):
     return F.pad(torch.as_tensor(x), (0, 5))
 
 
-@pytest.mark.parametrize("conv_products", ["exact", "bf16x3", "bf16x3_halo_dgrad"])
+@pytest.mark.parametrize("conv_products", ["exact", "bf16x3", "bf16x3_halo_dgrad", "bf16x3_throughput"])
 def test_fp32_resnet18_step_matches_torch_nn(conv_products, monkeypatch):
     """The whole fp32 training step (gather -> 20 conv/BN layers -> head ->
     backward) vs an independent torch.nn ResNet-18 in fp64, for both fp32
-    convolution product modes (and the opt-in halo dgrad backward)."""
+    convolution product modes (and the opt-in halo dgrad backward, and the
+    co-located regime's throughput backward kernels, tconv.hip)."""
     from metisfl_amd.models import layers as L
     from metisfl_amd.models.resnet import ResNet18
+    throughput = conv_products.endswith("_throughput")
     if conv_products.endswith("_halo_dgrad"):
         monkeypatch.setattr(L, "HALO_DGRAD", True)
-        conv_products = "bf16x3"
+    conv_products = conv_products.split("_")[0]
     from metisfl_amd.ops.optim import OptimizerSpec
     from tests.torch_resnet_ref import reference_step
     rng = np.random.default_rng(0)
@@ -411,6 +413,8 @@ def test_fp32_resnet18_step_matches_torch_nn(conv_products, monkeypatch):
     net = ResNet18(batch_size=B, device=DEV, optimizer=OptimizerSpec("vanilla_sgd", 0.0), seed=4,
                    conv_products=conv_products)
     assert net.compute_dtype == torch.float32
+    if throughput:
+        net.set_throughput_conv(True)
     values = net.state.to_numpy()
     ds = net.make_dataset(x, y, shuffle=False)
     net.zero_grad_in_optimizer = False

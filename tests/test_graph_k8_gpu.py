@@ -86,6 +86,9 @@ def test_colocated_streams_match_sequential_learners():
         out = []
         for j in range(4):
             net = _net(seed=11 + j, lr=lr)
+            # the kernels a 4-learner group runs (CoLocatedLearners turns the
+            # throughput backward on from 4 learners per GPU)
+            net.set_throughput_conv(True)
             x, y = _data(256, 20 + j)
             out.append((net, net.make_dataset(x, y, seed=j)))
         return out
