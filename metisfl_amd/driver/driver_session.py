@@ -265,10 +265,7 @@ class DriverSessionBase:
         if rname not in self._RULES:
             raise RuntimeError(f"aggregation rule {rule.aggregation_rule_name!r} is not supported on DataPlane: rccl")
         if cp.is_asynchronous:
-            protocol = "asynchronous"
-            if self._he_scheme is not None:
-                raise RuntimeError("DataPlane: rccl runs CKKS secure aggregation (PWA) on synchronous / "
-                                   "semi-synchronous rounds only; use DataPlane: grpc for asynchronous PWA")
+            protocol = "asynchronous"  # with CKKS: PWA over the learners' latest ciphertexts (AsyncPWA)
         elif cp.is_semi_synchronous:
             protocol = "semi_synchronous"
         elif cp.is_synchronous:
@@ -286,7 +283,19 @@ class DriverSessionBase:
                 "semi_sync_recompute": bool(cp.semi_sync_recompute_num_updates),
                 "participation_ratio": float(env.global_model_config.participation_ratio or 1.0),
                 "secure_aggregation": self._he_scheme is not None,
+                **self._collective_he(),
                 "extra": dict(self.collective_options.get("extra", {}))}
+
+    def _collective_he(self) -> dict:
+        """The driver's CKKS parameters and key files for the collective ranks
+        (the reference's learners load the driver's key pair,
+        driver_session.py:122-135)."""
+        if self._he_scheme is None:
+            return {}
+        he = self.federation_environment.homomorphic_encryption
+        files = self._he_scheme.get_crypto_params_files()
+        return {"he_batch_size": int(he.batch_size), "he_scaling_bits": int(he.scaling_factor_bits),
+                "he_key_dir": os.path.dirname(files["crypto_context_file"])}
 
     def _collective_job(self, rounds: int, learners=None, resume_dir: str | None = None,
                         prev_ranks: list[int] | None = None, fault: dict | None = None, tag: str = "",

@@ -77,6 +77,19 @@ def _decision(comm, rank0_action: int) -> int:
     return int(round(t.item()))
 
 
+def _he_decoder(fcfg, device):
+    """The driver's CKKS key pair (rank 0 decrypts an encrypted initial
+    model; on a GPU through the device kernels)."""
+    if not (fcfg.secure_aggregation and fcfg.he_key_dir):
+        return None
+    from metisfl_amd.parallel.federation import setup_ckks
+    scheme, _ = setup_ckks(None, fcfg)
+    if device.type == "cuda":
+        from metisfl_amd.encryption.device import AcceleratedCKKS
+        return AcceleratedCKKS(scheme, device)
+    return scheme
+
+
 def main(argv=None) -> int:
     argv = argv if argv is not None else sys.argv[1:]
     with open(argv[0]) as f:
@@ -149,7 +162,7 @@ def main(argv=None) -> int:
         # the ones this rank hosts run concurrently on their own streams
         from metisfl_amd.parallel.async_federation import AsyncCollectiveFederation
         from metisfl_amd.parallel.federation import install_community_model
-        initial_model(lambda fm: install_community_model(net, fm))
+        initial_model(lambda fm: install_community_model(net, fm, _he_decoder(fcfg, comm.device)))
         owners = [0] * len(job["learners"])
         for r, idx in enumerate(ranks):
             for i in idx:
@@ -176,8 +189,9 @@ def main(argv=None) -> int:
                             fault_task=int(my_fault["round"]) if my_fault else None,
                             on_fault=lambda t: _inject_fault(rank, t, my_fault))
         if rank == 0:
+            how = "secure PWA over ciphertexts" if fed.secure else "FedRec"
             print(f"[collective-async] {len(ups)} FedRec updates over {len(owners)} learners on {comm.world} "
-                  f"ranks, stop: {fed.stop_reason}, staleness {[u.staleness for u in ups]}", flush=True)
+                  f"ranks ({how}), stop: {fed.stop_reason}, staleness {[u.staleness for u in ups]}", flush=True)
             engine.close()
         if wd is not None:
             wd.stop()

@@ -156,6 +156,98 @@ class CoLocatedLearners:
             e1.synchronize()
         return [e0.elapsed_time(e1) for e0, e1 in self._ev]
 
+    def train_elastic(self, nsteps: list[int], step_offsets: list[int], stop, on_finish, poll_steps: int = 64,
+                      slow_s: list[float] | None = None, poll_s: float = 0.005):
+        """``train`` with straggler drop: every learner runs its budget in
+        chunks of ``poll_steps`` updates, at most two chunks in flight on its
+        stream.  A learner whose last chunk has completed on the device calls
+        ``on_finish(j)`` (the round's quorum counter).  Once ``stop()`` is
+        true (quorum reached / deadline passed; polled at most every
+        ``poll_s`` seconds) no further chunk is issued: learners with updates
+        still unissued are dropped from the round, those whose whole budget
+        is already on the device complete and participate.  ``slow_s[j]``:
+        test hook, learner j waits that long after each of its chunks
+        completes (a deliberately slow learner, without stalling the others).
+        -> (ms per learner, updates run per learner, participated per learner)."""
+        import time
+        n = len(self)
+        for net, ds, k in zip(self.nets, self.train_dss, nsteps):
+            net.prepare_graphs(ds, k)
+        self._fork()
+        t0 = time.perf_counter()
+        if self.cuda:
+            for j in range(n):
+                with self._ctx(j):
+                    self._ev[j][0].record()
+        gens = [net.train_steps_iter(ds, k, off)
+                for net, ds, k, off in zip(self.nets, self.train_dss, nsteps, step_offsets)]
+        slow = list(slow_s) if slow_s is not None else [0.0] * n
+        issued = [0] * n
+        inflight = [[] for _ in range(n)]      # (event or None, updates issued through it)
+        ready_at = [0.0] * n                   # slow hook: no chunk before this host time
+        finished = [False] * n
+        ms = [0.0] * n
+        stopped = False
+        last_poll = 0.0
+
+        def issue(j: int) -> None:
+            got = 0
+            with self._ctx(j):
+                while got < poll_steps and issued[j] + got < nsteps[j]:
+                    got += next(gens[j])  # one replay: K updates (may overshoot the chunk)
+                issued[j] += got
+                ev = None
+                if self.cuda:
+                    ev = torch.cuda.Event()
+                    ev.record()
+                inflight[j].append((ev, issued[j]))
+
+        def finish(j: int) -> None:
+            finished[j] = True
+            if self.cuda:
+                with self._ctx(j):
+                    self._ev[j][1].record()
+            ms[j] = (time.perf_counter() - t0) * 1e3
+            on_finish(j)
+
+        while True:
+            now = time.perf_counter()
+            busy = progressed = False
+            for j in range(n):
+                if finished[j]:
+                    continue
+                # retire completed chunks
+                while inflight[j] and (inflight[j][0][0] is None or inflight[j][0][0].query()):
+                    inflight[j].pop(0)
+                    progressed = True
+                    if slow[j]:
+                        ready_at[j] = time.perf_counter() + slow[j]
+                if issued[j] >= nsteps[j] and not inflight[j]:
+                    finish(j)
+                    continue
+                busy = True
+                if not stopped and issued[j] < nsteps[j] and len(inflight[j]) < 2 and now >= ready_at[j]:
+                    issue(j)
+                    progressed = True
+            if not busy:
+                break
+            if not stopped and now - last_poll >= poll_s:
+                last_poll = now
+                stopped = bool(stop())
+            if stopped and all(finished[j] or issued[j] < nsteps[j] for j in range(n)):
+                break  # only dropped learners left (their issued chunks drain in _join)
+            if not progressed:
+                time.sleep(2e-4)
+        self._join()
+        ran = list(issued)
+        if not self.cuda:
+            return ms, ran, finished
+        torch.cuda.synchronize(self.device)
+        out = []
+        for j, (e0, e1) in enumerate(self._ev):
+            out.append(e0.elapsed_time(e1) if finished[j] else (time.perf_counter() - t0) * 1e3)
+        return out, ran, finished
+
     def evaluate(self, dss: list | None = None, max_steps: int | None = None) -> list[dict | None]:
         """Every learner evaluates its current model on its dataset (default:
         its test shard), concurrently; None where a learner has no dataset."""

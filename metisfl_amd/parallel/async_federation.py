@@ -93,6 +93,86 @@ def staleness_discount(kind: str, t: int, a: float = 0.5, b: int = 4) -> float:
     raise ValueError(f"unknown staleness function {kind!r}")
 
 
+class AsyncPWA:
+    """The encrypted side of the asynchronous protocol (secure aggregation).
+
+    The reference's controller keeps every learner's latest encrypted model
+    and computes the private weighted average over them when a learner
+    completes (aggregation/private_weighted_average.cc:24-82 over the
+    ScheduledCardinality selection); only learners hold the private key.
+    Here a finishing learner encrypts its flat model where it lives (device
+    RNS-CKKS, kernels/ckks.hip), the ciphertext crosses to rank 0 over the
+    process group (point-to-point), rank 0 keeps the latest ciphertext of
+    every learner in HBM and runs the PWA over them (K9, one launch over all
+    learners, weights normalised to sum 1), and the finisher decrypts the
+    community ciphertext it gets back.  The aggregator never decrypts.  On a
+    CPU process group the host scheme (csrc/he/ckks.cc) does the same on
+    MCK1 byte blobs carried as uint8 tensors."""
+
+    def __init__(self, scheme, device: torch.device, n: int):
+        from metisfl_amd.encryption.fhe import WEIGHT_BITS
+        self.scheme, self.n, self.device = scheme, int(n), torch.device(device)
+        self.wbits = WEIGHT_BITS
+        self.dev = None
+        if self.device.type == "cuda":
+            from metisfl_amd.encryption.device import DeviceCKKS
+            self.dev = DeviceCKKS(scheme, self.device)
+            self.numel, self.dtype = self.dev.ct_numel(self.n), torch.int64
+            self.nct = self.dev.num_ciphertexts(self.n)
+        else:
+            self.numel, self.dtype = len(scheme.encrypt(np.zeros(self.n))), torch.uint8
+
+    def buffer(self) -> torch.Tensor:
+        return torch.empty(self.numel, dtype=self.dtype, device=self.device)
+
+    def encrypt(self, flat: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        if self.dev is not None:
+            return self.dev.encrypt(flat, out=out)
+        b = self.scheme.encrypt(flat.detach().double().reshape(-1).numpy())
+        t = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        if out is None:
+            return t
+        out.copy_(t)
+        return out
+
+    def pwa(self, cts: list, weights: list[float], out: torch.Tensor | None = None) -> torch.Tensor:
+        """Enc(sum_i w_i theta_i / sum_i w_i) from the learners' ciphertexts."""
+        z = float(sum(weights))
+        ws = [float(w) / z for w in weights]
+        if self.dev is None:
+            b = self.scheme.compute_weighted_average([bytes(c.numpy().tobytes()) for c in cts], ws)
+            t = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+            return t if out is None else out.copy_(t)
+        from metisfl_amd.ops._native import ops
+        d = self.dev
+        if out is None:
+            out = self.buffer()
+        wq = np.zeros((len(ws), d.L, 2), dtype=np.uint64)
+        for i, w in enumerate(ws):
+            wi = int(round(w * (1 << self.wbits)))
+            for j, qj in enumerate(d.q):
+                r = wi % qj
+                wq[i, j] = (r, (r << 64) // qj)  # Shoup precomputation
+        ptrs = torch.tensor([c.data_ptr() for c in cts], dtype=torch.int64).to(self.device)
+        wqt = torch.from_numpy(wq.view(np.int64).reshape(-1)).to(self.device)
+        ops().ckks_pwa(ptrs, wqt, out, d.tables[0], d.L, d.N, self.nct)
+        return out
+
+    def decrypt_into(self, ct: torch.Tensor, flat: torch.Tensor) -> None:
+        """flat <- Dec(community ciphertext) (the PWA's scale: 2^(bits + 30))."""
+        if self.dev is not None:
+            self.dev.decrypt(ct, self.n, self.dev.bits + self.wbits, out=flat.view(-1))
+            return
+        v = self.scheme.decrypt(bytes(ct.numpy().tobytes()), self.n)
+        flat.view(-1).copy_(torch.from_numpy(np.asarray(v)).to(flat.dtype))
+
+    def decrypt_fresh(self, ct: torch.Tensor) -> np.ndarray:
+        """A learner's own (unweighted) ciphertext -> host fp64 (tests)."""
+        if self.dev is not None:
+            return self.dev.decrypt(ct, self.n, dtype=torch.float64).cpu().numpy()
+        return np.asarray(self.scheme.decrypt(bytes(ct.numpy().tobytes()), self.n), dtype=np.float64)
+
+
 @dataclass
 class AsyncUpdate:
     learner: int
@@ -199,13 +279,23 @@ class AsyncCollectiveFederation:
             L.net.state.model32.copy_(st.model32)
         for L in self.learners:
             self._install(L)
+        # secure aggregation: learners submit CKKS ciphertexts, rank 0 runs the
+        # private weighted average over the latest ones (AsyncPWA)
+        self.secure = bool(getattr(cfg, "secure_aggregation", False))
+        self.he = None
+        if self.secure:
+            from metisfl_amd.parallel.federation import setup_ckks
+            scheme, self._he_dir = setup_ckks(comm, cfg)
+            self.he = AsyncPWA(scheme, st.model32.device, st.model32.numel())
         if self.rank == 0:
             self.S = torch.zeros_like(st.model32)
             self.Z = 0.0
-            self.last = [None] * self.G        # each learner's last contribution (HBM)
+            # each learner's last contribution (HBM): its flat model, or its
+            # ciphertext under secure aggregation
+            self.last = [None] * self.G
             self.last_w = [0.0] * self.G
             self.next_task = [0] * self.G       # next expected submission per remote learner
-            self.rbuf = torch.empty_like(st.model32)
+            self.rbuf = self.he.buffer() if self.secure else torch.empty_like(st.model32)
         self.remote = [g for g, o in enumerate(self.owners) if o != 0]
 
     # ---- compatibility: the first hosted learner ----------------------------------
@@ -295,20 +385,30 @@ class AsyncCollectiveFederation:
         """FedRec of the finished task; the learner leaves holding the new
         community model."""
         model = L.net.state.model32
+        # secure aggregation: the learner encrypts its model where it lives and
+        # decrypts the community ciphertext it gets back
+        sub = self.he.encrypt(model, out=L.extra.get("ct")) if self.secure else model
+        if self.secure:
+            L.extra["ct"] = sub
         if self.rank == 0:
             with self._lock:
                 self._record_eval(L.gid, meta.get("eval"))
-                self._fedrec(L.gid, model, meta)
-                model.copy_(self._community())
+                self._fedrec(L.gid, sub, meta)
+                back = self._community()
+                if not self.secure:
+                    model.copy_(back)
                 self._sync_stream()
                 L.base_version = self.version
                 self._after_update()
         else:
             self.store.set(_KEY.format(self.tag, L.gid, L.sub), json.dumps(meta))
-            dist.send(model, dst=0, group=self.p2p)
-            dist.recv(model, src=0, group=self.p2p)
-            self._sync_stream()  # the learner's stream reads it next
+            dist.send(sub, dst=0, group=self.p2p)
+            back = sub if self.secure else model
+            dist.recv(back, src=0, group=self.p2p)
             L.base_version = int(self.store.get(_VER.format(self.tag, L.gid, L.sub)))
+        if self.secure:
+            self.he.decrypt_into(back, model)
+        self._sync_stream()  # the learner's stream reads the model next
         self._install(L)
         L.sub += 1
         L.task_index += 1
@@ -530,12 +630,16 @@ class AsyncCollectiveFederation:
         stale = self.version - int(meta.get("base_version", self.version))
         w0 = float(meta["weight"])
         w = w0 * staleness_discount(self.cfg.staleness, stale, self.cfg.staleness_a, self.cfg.staleness_b)
+        # plaintext: the FedRec running sum; secure: only the latest ciphertext
+        # and weight are kept, the PWA runs over all of them (_community)
         if self.last[g] is not None:
-            agg.rolling_op(self.S, self.last[g], agg.MERGE_SUB, self.last_w[g])
+            if not self.secure:
+                agg.rolling_op(self.S, self.last[g], agg.MERGE_SUB, self.last_w[g])
             self.Z -= self.last_w[g]
         else:
             self.last[g] = torch.empty_like(theta)
-        agg.rolling_op(self.S, theta, agg.MERGE_ADD, w)
+        if not self.secure:
+            agg.rolling_op(self.S, theta, agg.MERGE_ADD, w)
         self.Z += w
         self.last[g].copy_(theta)
         self.last_w[g] = w
@@ -554,17 +658,34 @@ class AsyncCollectiveFederation:
         self._after_fedrec()
 
     def _community(self) -> torch.Tensor:
+        """The community model as rank 0 hands it out: S / Z, or (secure
+        aggregation) the PWA ciphertext over every learner's latest one."""
+        if self.secure:
+            idx = [g for g in range(self.G) if self.last[g] is not None]
+            return self.he.pwa([self.last[g] for g in idx], [self.last_w[g] for g in idx])
         c = self.S.clone()
         agg.rolling_op(c, None, agg.SCALE_DIV, self.Z)
         return c
 
     def community(self) -> torch.Tensor:
-        return self._community()
+        """Rank 0: the plaintext community model (secure aggregation: rank 0
+        decrypts it as the host of its own learners -- the key pair is shared
+        by all learners, as in the reference)."""
+        c = self._community()
+        if not self.secure:
+            return c
+        out = torch.empty_like(self.net.state.model32)
+        self.he.decrypt_into(c, out)
+        return out
 
     def community_reference(self) -> np.ndarray:
         """Host recomputation of sum_g w_g theta_g / sum_g w_g over the latest
-        contributions (tests)."""
-        xs = [x.double().cpu().numpy() for x in self.last if x is not None]
+        contributions (tests; secure aggregation: each learner's latest
+        ciphertext decrypted on its own)."""
+        if self.secure:
+            xs = [self.he.decrypt_fresh(x) for x in self.last if x is not None]
+        else:
+            xs = [x.double().cpu().numpy() for x in self.last if x is not None]
         ws = [w for x, w in zip(self.last, self.last_w) if x is not None]
         return sum(w * x for w, x in zip(ws, xs)) / sum(ws)
 
@@ -661,8 +782,10 @@ class AsyncCollectiveFederation:
         v = self.version
         if self.ckpt_dir and self.ckpt_every and v % self.ckpt_every == 0:
             self._checkpoint_aggregator(block=False)
+        # (secure aggregation: the aggregator holds no plaintext model to hand
+        # to the controller's lineage)
         if self.engine is not None and self.snapshot_every and v % self.snapshot_every == 0 \
-                and hasattr(self.engine, "snapshot_community"):
+                and not self.secure and hasattr(self.engine, "snapshot_community"):
             from metisfl_amd.parallel import checkpoint as ck
             if self._lineage is None:
                 self._lineage = ck.AsyncSnapshot(self.S.device, "metisfl-async-lineage")
@@ -681,13 +804,15 @@ class AsyncCollectiveFederation:
             self._ckpt = ck.AsyncSnapshot(self.S.device, "metisfl-async-checkpoint")
         if self._ckpt.busy() and not block:
             return
-        v, root = self.version, self.ckpt_dir
-        tensors = {"S": self.S}
+        v, root, secure = self.version, self.ckpt_dir, self.secure
+        # secure aggregation: the latest ciphertext of every learner (the
+        # aggregator's whole state; no plaintext community model is written)
+        tensors = {} if secure else {"S": self.S}
         for g, x in enumerate(self.last):
             if x is not None:
                 tensors[f"last:{self.learner_ids[g]}"] = x
         meta = {"Z": float(self.Z), "version": v, "world": self.world, "learners": self.G,
-                "learner_ids": list(self.learner_ids),
+                "learner_ids": list(self.learner_ids), "secure_aggregation": secure,
                 "last_w": {self.learner_ids[g]: w for g, w in enumerate(self.last_w) if self.last[g] is not None},
                 "protocol": "asynchronous", "global_iteration": v,
                 "updates": [{"learner": self.learner_ids[u.learner], "task": u.task, "weight": u.weight,
@@ -700,16 +825,17 @@ class AsyncCollectiveFederation:
             os.makedirs(d, exist_ok=True)
             state = {k: t.clone() for k, t in h.items()}
             ck.atomic_torch_save(state, os.path.join(d, "async_state.pt"))
-            from metisfl_amd.proto import model_pb2
-            from metisfl_amd.utils.tensor_codec import model_from_arrays
-            flat = (h["S"].double() / meta["Z"]).float().numpy() if meta["Z"] else h["S"].numpy()
-            fm = model_pb2.FederatedModel()
-            fm.num_contributors = n_contrib
-            fm.global_iteration = v
-            fm.model.CopyFrom(model_from_arrays([sp.name for sp in st.specs],
-                                                [flat[sp.offset: sp.offset + sp.numel].reshape(sp.shape)
-                                                 for sp in st.specs], [sp.trainable for sp in st.specs]))
-            ck.atomic_write(os.path.join(d, "community_model.pb"), fm.SerializeToString())
+            if not secure:
+                from metisfl_amd.proto import model_pb2
+                from metisfl_amd.utils.tensor_codec import model_from_arrays
+                flat = (h["S"].double() / meta["Z"]).float().numpy() if meta["Z"] else h["S"].numpy()
+                fm = model_pb2.FederatedModel()
+                fm.num_contributors = n_contrib
+                fm.global_iteration = v
+                fm.model.CopyFrom(model_from_arrays([sp.name for sp in st.specs],
+                                                    [flat[sp.offset: sp.offset + sp.numel].reshape(sp.shape)
+                                                     for sp in st.specs], [sp.trainable for sp in st.specs]))
+                ck.atomic_write(os.path.join(d, "community_model.pb"), fm.SerializeToString())
             ck.atomic_write(os.path.join(d, "federation.json"), json.dumps(meta).encode())
             ck.publish(root, f"round_{v}")
 
@@ -785,7 +911,10 @@ class AsyncCollectiveFederation:
             with open(os.path.join(found, "federation.json")) as f:
                 meta = json.load(f)
             state = torch.load(os.path.join(found, "async_state.pt"), weights_only=True)
-            S = state["S"].to(dev)
+            if bool(meta.get("secure_aggregation", False)) != self.secure:
+                raise RuntimeError(f"checkpoint {found}: secure aggregation "
+                                   f"{meta.get('secure_aggregation', False)}, this federation {self.secure}")
+            S = self.S.clone() if self.secure else state["S"].to(dev)
             Z = float(meta["Z"])
             old_w = dict(meta["last_w"])
             present = {lid: g for g, lid in enumerate(self.learner_ids)}
@@ -800,15 +929,18 @@ class AsyncCollectiveFederation:
                     g = present[lid]
                     self.last[g] = x.to(dev)
                     self.last_w[g] = float(w)
-                else:  # the lost learners leave the running sum
-                    agg.rolling_op(S, x.to(dev), agg.MERGE_SUB, float(w))
+                else:  # the lost learners leave the running sum (secure: the PWA set)
+                    if not self.secure:
+                        agg.rolling_op(S, x.to(dev), agg.MERGE_SUB, float(w))
                     Z -= float(w)
                     dropped.append(lid)
             self.S.copy_(S)
             self.Z = Z
             self.version = int(meta["version"])
             self.resumed = {"version": self.version, "dropped": sorted(dropped)}
-            st.model32.copy_(self._community())
+            # secure: rank 0 decrypts as the host of its own learners
+            if any(x is not None for x in self.last):
+                st.model32.copy_(self.community())
             ver[0] = self.version
         self.comm.broadcast_(ver, src=0)
         self.comm.broadcast_(st.model32, src=0)

@@ -208,14 +208,17 @@ class RemoteCollectiveController(CollectiveController):
             "evaluations": [base64.b64encode(self._model_evaluations(ev)).decode()]})
 
     def snapshot_community(self, names, arrays, trainable, global_iteration: int) -> None:
-        from metisfl_amd.utils.grpc_controller_client import GRPCControllerClient
+        """Called from the lineage writer thread (one at a time): one client,
+        and its channel, reused for every round's ReplaceCommunityModel."""
         from metisfl_amd.utils.tensor_codec import model_from_arrays
-        c = GRPCControllerClient(self._entity, max_workers=1)
-        try:
-            c.replace_community_model(len(self.ids), model_from_arrays(names, arrays, trainable),
-                                      request_retries=2, global_iteration=int(global_iteration))
-        finally:
-            c.shutdown()
+        if getattr(self, "_lineage_client", None) is None:
+            from metisfl_amd.utils.grpc_controller_client import GRPCControllerClient
+            self._lineage_client = GRPCControllerClient(self._entity, max_workers=1)
+        self._lineage_client.replace_community_model(len(self.ids), model_from_arrays(names, arrays, trainable),
+                                                     request_retries=2, global_iteration=int(global_iteration))
 
     def close(self) -> None:
+        c, self._lineage_client = getattr(self, "_lineage_client", None), None
+        if c is not None:
+            c.shutdown()
         self._ch.close()

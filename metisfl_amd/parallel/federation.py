@@ -93,6 +93,10 @@ class FederationConfig:
     secure_aggregation: bool = False
     he_batch_size: int = 4096
     he_scaling_bits: int = 52
+    # directory of the driver's CKKS key files (cryptocontext / public /
+    # private key, driver_session.py): every rank loads them; None: rank 0
+    # generates a key pair and broadcasts it
+    he_key_dir: str | None = None
     # Straggler handling (the reference carries
     # GlobalModelSpecs.learners_participation_ratio, metis.proto:307, but
     # never acts on it).  A synchronous round closes once
@@ -140,16 +144,18 @@ class RoundRecord:
         return d
 
 
-def install_community_model(net, fm) -> None:
+def install_community_model(net, fm, he_scheme=None) -> None:
     """Install a ``FederatedModel`` (proto or serialized bytes) into ``net``
-    as the community model, matching variables by name."""
+    as the community model, matching variables by name (``he_scheme``:
+    decrypts ciphertext variables, e.g. the driver's initial model under
+    CKKS)."""
     from metisfl_amd.proto import model_pb2
     from metisfl_amd.utils.tensor_codec import model_to_arrays
     if isinstance(fm, (bytes, bytearray)):
         m = model_pb2.FederatedModel()
         m.ParseFromString(bytes(fm))
         fm = m
-    names, arrays, _ = model_to_arrays(fm.model)
+    names, arrays, _ = model_to_arrays(fm.model, he_scheme)
     st = net.state
     st.load_numpy(dict(zip(names, arrays)))
     st.set_anchor()
@@ -160,6 +166,36 @@ def learner_file(learner_id: str) -> str:
     counter, epoch permutation)."""
     safe = "".join(c if c.isalnum() or c in "-_." else "_" for c in str(learner_id))
     return f"learner_{safe}.safetensors"
+
+
+def setup_ckks(comm: Comm, cfg: FederationConfig):
+    """Collective.  One CKKS key pair shared by all learners (the reference's
+    driver generates it once, driver_session.py:122-135): rank 0 generates,
+    the key files travel as bytes over the process group -> (scheme, key
+    directory of this rank)."""
+    import tempfile
+
+    from metisfl_amd.encryption import CKKS
+    names = ("cryptocontext.txt", "key-public.txt", "key-private.txt")
+    scheme = CKKS(cfg.he_batch_size, cfg.he_scaling_bits)
+    if cfg.he_key_dir:
+        scheme.load_context_and_keys_from_files(*(os.path.join(cfg.he_key_dir, nm) for nm in names))
+        return scheme, cfg.he_key_dir
+    d = tempfile.mkdtemp(prefix=f"metisfl_amd_ckks_r{comm.rank}_")
+    blobs = []
+    if comm.rank == 0:
+        scheme.gen_crypto_context_and_keys(d)
+        for nm in names:
+            with open(os.path.join(d, nm), "rb") as f:
+                blobs.append(f.read())
+    for i, nm in enumerate(names):
+        b = comm.broadcast_bytes(blobs[i] if comm.rank == 0 else None)
+        if comm.rank != 0:
+            with open(os.path.join(d, nm), "wb") as f:
+                f.write(b)
+    if comm.rank != 0:
+        scheme.load_context_and_keys_from_files(*(os.path.join(d, nm) for nm in names))
+    return scheme, d
 
 
 class CollectiveFederation:
@@ -196,9 +232,7 @@ class CollectiveFederation:
         self.Lmax = max(self.Ls)
         self.offsets = [sum(self.Ls[:r]) for r in range(self.world)]
         self.n_learners = sum(self.Ls)
-        if self.L > 1 and self.elastic:
-            raise NotImplementedError("straggler drop (participation_ratio / round_deadline_s) runs one "
-                                      "learner per rank")
+        self._local_done = 0  # quorum counter of a one-process federation (no store)
         self.learner_ids = learner_ids or [f"learner_{r}" for r in range(self.n_learners)]
         # reference: num_local_updates = epochs * ceil(N_train / batch) per
         # learner (controller.cc:148-153); the join-time dataset sizes are
@@ -273,15 +307,56 @@ class CollectiveFederation:
 
     @property
     def elastic(self) -> bool:
-        """Straggler drop active (participation ratio < 1 or a round deadline)."""
-        return self.world > 1 and (self.cfg.participation_ratio < 1.0 or self.cfg.round_deadline_s is not None)
+        """Straggler drop active (participation ratio < 1 or a round deadline)
+        in a federation of more than one learner (co-located or not)."""
+        return self.n_learners > 1 and (self.cfg.participation_ratio < 1.0 or self.cfg.round_deadline_s is not None)
 
     def quorum(self) -> int:
-        return max(1, min(self.world, math.ceil(self.cfg.participation_ratio * self.world - 1e-9)))
+        """Learners (global, co-located ones counted one by one) whose
+        completion ends the round."""
+        n = self.n_learners
+        return max(1, min(n, math.ceil(self.cfg.participation_ratio * n - 1e-9)))
 
     def _store(self):
         import torch.distributed as dist
         return dist.distributed_c10d._get_default_store()
+
+    def _slow_s(self, g: int) -> float:
+        """Test hook ``extra.debug_slow_s``: {global learner index: seconds of
+        host delay after each chunk} (with one learner per rank: the rank)."""
+        return float(self.cfg.extra.get("debug_slow_s", {}).get(str(g), 0.0))
+
+    def _train_elastic_group(self, nsteps: list[int], t0: float) -> tuple[list, list, list]:
+        """Straggler drop for this rank's co-located learners: each learner's
+        completion counts toward the round's quorum (the process group's
+        store key, shared with one-learner ranks; a local counter in a
+        one-process federation); once the quorum has finished or the deadline
+        passed, learners still training stop issuing updates and sit the
+        round out -> (ms, updates run, participated) per local learner."""
+        q, deadline = self.quorum(), self.cfg.round_deadline_s
+        if self.comm.distributed:
+            store, key = self._store(), f"metisfl/round{self.global_iteration}/done"
+
+            def on_finish(j):
+                store.add(key, 1)
+
+            def count():
+                return int(store.add(key, 0))
+        else:
+            self._local_done = 0
+
+            def on_finish(j):
+                self._local_done += 1
+
+            def count():
+                return self._local_done
+
+        def stop():
+            return count() >= q or (deadline is not None and time.perf_counter() - t0 > deadline)
+
+        slow = [self._slow_s(g) for g in self.local_learners()]
+        return self.group.train_elastic(list(nsteps), list(self.steps_done_l), stop, on_finish,
+                                        poll_steps=max(1, self.cfg.poll_steps), slow_s=slow)
 
     def _train_elastic(self, nsteps: int, t0: float) -> tuple[int, bool]:
         """Chunked local training that stops early once the round's quorum
@@ -289,7 +364,7 @@ class CollectiveFederation:
         store, key = self._store(), f"metisfl/round{self.global_iteration}/done"
         q = self.quorum()
         deadline = self.cfg.round_deadline_s
-        slow = float(self.cfg.extra.get("debug_slow_s", {}).get(str(self.rank), 0.0))
+        slow = self._slow_s(self.offsets[self.rank])
         done = 0
         while done < nsteps:
             k = min(self.cfg.poll_steps, nsteps - done)
@@ -312,8 +387,12 @@ class CollectiveFederation:
             return [self.local_train(nsteps[0])]
         for net in self.nets:
             net.reset_train_stats()
+        part = [True] * self.L
         with tracing.range("metisfl.local_train"):
-            ms = self.group.train(list(nsteps), list(self.steps_done_l))
+            if self.elastic:
+                ms, nsteps, part = self._train_elastic_group(nsteps, time.perf_counter())
+            else:
+                ms = self.group.train(list(nsteps), list(self.steps_done_l))
         out = []
         for j, (net, ran) in enumerate(zip(self.nets, nsteps)):
             self.steps_done_l[j] += ran
@@ -321,7 +400,7 @@ class CollectiveFederation:
             spe = self._spes[j]
             out.append({"ms": ms[j], "ms_per_batch": ms[j] / max(1, ran), "ms_per_epoch": ms[j] / max(1, ran) * spe,
                         "completed_batches": ran, "completed_epochs": ran / spe,
-                        "train_loss": tr["loss"], "train_accuracy": tr["accuracy"], "participated": True})
+                        "train_loss": tr["loss"], "train_accuracy": tr["accuracy"], "participated": bool(part[j])})
         if self.cfg.evaluate_test:
             with tracing.range("metisfl.evaluate"):
                 tests = self.group.evaluate(max_steps=self.cfg.eval_max_steps)
@@ -388,30 +467,7 @@ class CollectiveFederation:
         return [float(weights[self.offsets[r]]) if self.Ls[r] == 1 else 1.0 for r in range(self.world)]
 
     def _setup_he(self) -> None:
-        """One CKKS key pair shared by all learners (the reference's driver
-        generates it once, driver_session.py:122-135): rank 0 generates,
-        the key files travel as bytes over the process group."""
-        import tempfile
-
-        from metisfl_amd.encryption import CKKS
-        cfg = self.cfg
-        names = ("cryptocontext.txt", "key-public.txt", "key-private.txt")
-        self._he_dir = tempfile.mkdtemp(prefix=f"metisfl_amd_ckks_r{self.rank}_")
-        scheme = CKKS(cfg.he_batch_size, cfg.he_scaling_bits)
-        blobs = []
-        if self.rank == 0:
-            scheme.gen_crypto_context_and_keys(self._he_dir)
-            for nm in names:
-                with open(os.path.join(self._he_dir, nm), "rb") as f:
-                    blobs.append(f.read())
-        for i, nm in enumerate(names):
-            b = self.comm.broadcast_bytes(blobs[i] if self.rank == 0 else None)
-            if self.rank != 0:
-                with open(os.path.join(self._he_dir, nm), "wb") as f:
-                    f.write(b)
-        if self.rank != 0:
-            scheme.load_context_and_keys_from_files(*(os.path.join(self._he_dir, nm) for nm in names))
-        self.he = scheme
+        self.he, self._he_dir = setup_ckks(self.comm, self.cfg)
         if self.comm.device.type == "cuda":
             from metisfl_amd.encryption.device import DeviceCKKS
             self.he_dev = DeviceCKKS(scheme, self.comm.device)
@@ -641,7 +697,7 @@ class CollectiveFederation:
         st = self.net.state
         return {"global_iteration": self.global_iteration, "protocol": self.cfg.protocol,
                 "num_local_updates": list(self.num_local_updates),
-                "world": self.world, "learners_per_rank": self.L, "learner_ids": self.learner_ids,
+                "world": self.world, "learners_per_rank": list(self.Ls), "learner_ids": self.learner_ids,
                 "dataset_sizes": self.dataset_sizes,
                 "config": {k: v for k, v in asdict(self.cfg).items() if k != "extra"},
                 "variables": [[s.name, list(s.shape), s.trainable] for s in st.specs],
@@ -713,7 +769,11 @@ class CollectiveFederation:
         return ms
 
     def flush_checkpoints(self) -> None:
-        """Wait for background checkpoint / lineage writes of this rank."""
+        """Wait for background checkpoint / lineage writes of this rank (and
+        send the last community model if the lineage skipped its round)."""
+        if self._lineage is not None and getattr(self, "_lineage_skipped", False):
+            self._lineage.wait()
+            self.snapshot_community()
         for w in (self._ckpt, self._lineage):
             if w is not None:
                 w.wait()
@@ -723,7 +783,10 @@ class CollectiveFederation:
         controller's lineage (``ReplaceCommunityModel``; the reference
         replaces its community model every global iteration,
         controller.cc:466), staged now and sent from a background thread.
-        -> milliseconds on the caller's path."""
+        Latest wins: while the controller is still receiving an earlier
+        round's model the round is not staged (the caller never waits on the
+        controller); ``flush_checkpoints`` sends the final model if its round
+        was skipped.  -> milliseconds on the caller's path."""
         if self.engine is None or not hasattr(self.engine, "snapshot_community"):
             return 0.0
         from metisfl_amd.parallel import checkpoint as ck
@@ -738,12 +801,17 @@ class CollectiveFederation:
                                       [flat[s.offset: s.offset + s.numel].reshape(s.shape) for s in st.specs],
                                       [s.trainable for s in st.specs], gi)
 
-        return self._lineage.submit({"model": st.model32}, write)
+        ms = self._lineage.try_submit({"model": st.model32}, write)
+        self._lineage_skipped = ms is None
+        if ms is None:
+            self.lineage_skipped_rounds = getattr(self, "lineage_skipped_rounds", 0) + 1
+            return 0.0
+        return ms
 
     def load_community_model(self, fm) -> None:
         """Install a ``FederatedModel`` (proto or serialized bytes) as the
         community model, matching variables by name."""
-        install_community_model(self.net, fm)
+        install_community_model(self.net, fm, self.he)
         if self.group is not None:
             self._install_local(self.net.state.model32)
 
@@ -783,7 +851,9 @@ class CollectiveFederation:
             self._install_local(st.model32)
         else:
             raise FileNotFoundError(f"no community model in checkpoint {path} ({self.COMMUNITY_FILE})")
-        same_world = meta["world"] == self.world and int(meta.get("learners_per_rank", 1)) == self.L
+        lpr = meta.get("learners_per_rank", 1)  # a list per rank; one int in round-4 checkpoints
+        old_ls = [int(x) for x in lpr] if isinstance(lpr, list) else [int(lpr)] * int(meta["world"])
+        same_world = meta["world"] == self.world and old_ls == list(self.Ls)
         old_ids = list(meta.get("learner_ids", []))
         for j, (net, ds) in enumerate(zip(self.nets, self.train_dss)):
             lid = self.learner_ids[self.local_learners()[j]]

@@ -35,12 +35,22 @@ def main():
     ap.add_argument("--cu-mask", choices=("none", "contig", "interleave"), default="none",
                     help="confine learner g's stream to 256/G CUs (hipExtStreamCreateWithCUMask): a contiguous "
                          "CU-id range, or CU ids with id %% G == g")
+    ap.add_argument("--pair-ring", type=int, default=-1,
+                    help="conv32 paired-launch LDS ring stages (-1: what CoLocatedLearners selects for the group)")
+    ap.add_argument("--conv-products", default=None, choices=("bf16x3", "exact"))
     a = ap.parse_args()
     gmax = max(a.groups)
+    from metisfl_amd.models.colocated import CoLocatedLearners
+    ring = a.pair_ring if a.pair_ring >= 0 else (int(CoLocatedLearners.pair_ring or 0)
+                                                 if gmax >= CoLocatedLearners.pair_ring_min_learners else 0)
+    if ring:
+        CoLocatedLearners._set_pair_ring(ring)
+    print(f"pair ring {ring or 'build default'}, conv products {a.conv_products or 'default'}", flush=True)
     nets, dss = [], []
     gen = torch.Generator(device="cuda").manual_seed(0)
     for i in range(gmax):
         net = ResNet18(batch_size=a.batch, device="cuda", seed=7 + i, dtype=a.dtype,
+                       conv_products=a.conv_products,
                        optimizer=OptimizerSpec("momentum_sgd", 0.005, momentum=0.75))
         x = torch.randn((1024, 32, 32, 3), generator=gen, device="cuda")
         y = torch.randint(0, 10, (1024,), generator=gen, device="cuda")

@@ -155,6 +155,84 @@ def test_async_fedrec_colocated_learners_on_two_ranks(tmp_path):
         assert all(np.all(np.isfinite(f)) for f in res["finals"])
 
 
+def _secure_worker(rank, world, port, out_dir, per_rank, tasks):
+    """Secure aggregation (CKKS PWA) with the asynchronous protocol: every
+    learner records the plaintext model it submitted (test hook) so the test
+    can recompute the PWA on the host."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from metisfl_amd.models.sequential import HousingMLP
+    from metisfl_amd.ops.optim import OptimizerSpec
+    from metisfl_amd.parallel.async_federation import AsyncCollectiveFederation
+    from metisfl_amd.parallel.comm import Comm
+    from metisfl_amd.parallel.federation import FederationConfig
+    comm = Comm(backend="gloo")
+    gids = [rank * per_rank + j for j in range(per_rank)]
+    nets, dss = [], []
+    for g in gids:
+        net = HousingMLP(batch_size=4, device="cpu", seed=g + 1, optimizer=OptimizerSpec("vanilla_sgd", 0.01))
+        rng = np.random.default_rng(g)
+        n = 8 + 4 * g
+        nets.append(net)
+        dss.append(net.make_dataset(rng.standard_normal((n, 13)).astype(np.float32),
+                                    rng.standard_normal(n).astype(np.float32), seed=g))
+    owners = [g // per_rank for g in range(world * per_rank)]
+    cfg = FederationConfig(batch_size=4, local_epochs=1, evaluate_test=False, staleness="polynomial",
+                           secure_aggregation=True)
+    fed = AsyncCollectiveFederation(comm, nets, dss, cfg, tasks_per_learner=tasks, gids=gids, owners=owners)
+    submitted = {g: [] for g in gids}
+    orig = fed._submit
+
+    def spy(L, meta, _orig=orig):
+        submitted[L.gid].append(L.net.state.model32.numpy().astype(np.float64).tolist())
+        _orig(L, meta)
+        # the learner now holds the decrypted community model
+        submitted[L.gid].append(L.net.state.model32.numpy().astype(np.float64).tolist())
+    fed._submit = spy
+    ups = fed.run()
+    res = {"rank": rank, "submitted": {str(g): v for g, v in submitted.items()}}
+    if rank == 0:
+        res["updates"] = [(u.learner, u.task, u.weight, u.staleness) for u in ups]
+        res["community"] = fed.community().double().numpy().tolist()
+        res["ref"] = fed.community_reference().tolist()
+        res["ct_is_bytes"] = bool(fed.last[0].dtype == torch.uint8)
+    with open(os.path.join(out_dir, f"secure_{rank}.json"), "w") as f:
+        json.dump(res, f)
+    comm.barrier()
+    comm.close()
+
+
+def test_async_secure_pwa_over_latest_ciphertexts(tmp_path):
+    """asynchronous PWA on the collective plane.  2 ranks x 2
+    learners submit CKKS ciphertexts; rank 0 keeps the latest one per learner
+    and answers each finisher with the PWA ciphertext, which the finisher
+    decrypts.  Replaying the updates on the host (each learner's latest
+    submitted plaintext, its staleness-discounted weight) reproduces every
+    community model a learner received, to CKKS precision."""
+    world, per, tasks = 2, 2, 2
+    mp.start_processes(_secure_worker, args=(world, _free_port(), str(tmp_path), per, tasks), nprocs=world,
+                       join=True, start_method="spawn")
+    res = [json.load(open(tmp_path / f"secure_{r}.json")) for r in range(world)]
+    r0 = res[0]
+    assert r0["ct_is_bytes"]  # the aggregator holds ciphertexts, not models
+    sub = {}
+    for r in res:
+        sub.update({int(g): v for g, v in r["submitted"].items()})
+    ups = r0["updates"]
+    assert len(ups) == world * per * tasks
+    latest, weights = {}, {}
+    for (g, t, w, _) in ups:  # replay in aggregation order
+        latest[g] = np.array(sub[g][2 * t])
+        weights[g] = w
+        ref = sum(weights[k] * latest[k] for k in latest) / sum(weights.values())
+        got = np.array(sub[g][2 * t + 1])  # what the finisher decrypted
+        assert np.abs(got - ref).max() <= 1e-5 * (np.abs(ref).max() + 1e-9), (g, t)
+    final = np.array(r0["community"])
+    assert np.abs(final - ref).max() <= 1e-5 * (np.abs(ref).max() + 1e-9)
+    assert np.abs(np.array(r0["ref"]) - ref).max() <= 1e-5 * (np.abs(ref).max() + 1e-9)
+
+
 def test_async_colocated_single_process():
     """World 1 (no process group): several co-located learners, all FedRec on
     rank 0's device path -- the on-one-GPU asynchronous configuration."""

@@ -80,3 +80,42 @@ def test_colocated_secure_aggregation_matches_plaintext_fedavg():
     for n in nets[1:]:
         assert torch.equal(n.state.model32, nets[0].state.model32)
     comm.close()
+
+
+def test_colocated_async_secure_pwa_on_device():
+    """Asynchronous protocol + CKKS (the reference's
+    test_localhost_asynchronous_vanillasgd_with_fhe.yaml) on the device path:
+    each finisher encrypts its model with the device RNS-CKKS kernels, the
+    aggregator keeps the latest ciphertext per learner and runs the K9 PWA
+    over them, and the finisher decrypts.  Every community model a learner
+    received equals the host PWA of the latest submitted plaintexts."""
+    from metisfl_amd.models.colocated import CoLocatedLearners
+    from metisfl_amd.parallel.async_federation import AsyncCollectiveFederation
+    from metisfl_amd.parallel.comm import Comm
+    from metisfl_amd.parallel.federation import FederationConfig
+    nets, dss = _learners(3, shard=64)
+    cfg = FederationConfig(protocol="asynchronous", batch_size=32, local_epochs=1, staleness="polynomial",
+                           evaluate_test=False, secure_aggregation=True)
+    group = CoLocatedLearners(nets, dss)
+    fed = AsyncCollectiveFederation(Comm(), nets, dss, cfg, tasks_per_learner=2, streams=group.streams)
+    assert fed.he.dev is not None  # device CKKS
+    subs, got = {}, []
+    orig = fed._submit
+
+    def spy(L, meta, _orig=orig):
+        subs.setdefault(L.gid, []).append(L.net.state.model32.double().cpu().clone())
+        _orig(L, meta)
+        got.append((L.gid, len(subs[L.gid]) - 1, L.net.state.model32.double().cpu().clone()))
+    fed._submit = spy
+    ups = fed.run()
+    torch.cuda.synchronize()
+    assert len(ups) == 6 and all(x.dtype == torch.int64 and x.is_cuda for x in fed.last if x is not None)
+    latest, ws = {}, {}
+    for (g, t, back), u in zip(got, ups):
+        assert u.learner == g and u.task == t
+        latest[g], ws[g] = subs[g][t], u.weight
+        ref = sum(ws[k] * latest[k] for k in latest) / sum(ws.values())
+        err = float((back - ref).abs().max() / ref.abs().max())
+        assert err < 1e-5, (g, t, err)
+    c = fed.community().double().cpu()
+    assert float((c - ref).abs().max() / ref.abs().max()) < 1e-5

@@ -261,14 +261,18 @@ def test_learners_sharing_a_device_are_colocated_in_one_rank(tmp_path):
         "learner_localhost-2.safetensors"]
 
 
-def _session_devices(tmp_path, devices, rounds, protocol="Asynchronous", **opts):
+def _session_devices(tmp_path, devices, rounds, protocol="Asynchronous", he=False, **opts):
     """Learners placed on devices (learners naming the same device share one
-    rank: co-located)."""
+    rank: co-located).  ``he``: PWA under CKKS."""
     from metisfl_amd.driver.driver_session import DriverSession, free_port
     from metisfl_amd.models.model_def import StaticModelDef
     from metisfl_amd.utils.fedenv_parser import FederationEnvironment
-    d = env_dict([free_port() for _ in range(len(devices))], rounds=rounds, protocol=protocol)
+    d = env_dict([free_port() for _ in range(len(devices))], rounds=rounds, protocol=protocol,
+                 rule="PWA" if he else "FedAvg")
     d["FederationEnvironment"]["DataPlane"] = "rccl"
+    if he:
+        d["FederationEnvironment"]["HomomorphicEncryption"] = {"Scheme": "CKKS", "BatchSize": 4096,
+                                                               "ScalingFactorBits": 52}
     for l, dev in zip(d["FederationEnvironment"]["Learners"], devices):
         l["Devices"] = dev
     return DriverSession(FederationEnvironment(config=d), StaticModelDef("resnet18", width_mult=0.125), train_recipe,
@@ -300,6 +304,34 @@ def test_async_colocated_learners_through_the_driver(tmp_path):
     stal = json.loads(line.split("staleness ")[1])
     assert max(stal) > 0
     assert stats["community_model_results"]["community_evaluation"]
+
+
+def test_async_secure_pwa_through_the_driver(tmp_path):
+    """asynchronous PWA (CKKS) on the collective data plane.  3
+    learners on 2 devices (rank 0 hosts two), PWA + HomomorphicEncryption:
+    the ranks load the driver's key files, every finisher submits a
+    ciphertext, rank 0 aggregates over the latest ciphertexts (checkpointing
+    them), and the federation reaches its version budget with every learner
+    contributing."""
+    sess = _session_devices(tmp_path, [[0], [0], [1]], rounds=6, he=True, checkpoint_every=2,
+                            extra={"debug_delay_s": {"1": 0.2}})
+    stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason
+    job = json.load(open(os.path.join(str(tmp_path / "w"), "collective_job.json")))
+    fj = job["federation"]
+    assert fj["secure_aggregation"] and fj["he_key_dir"] and os.path.exists(
+        os.path.join(fj["he_key_dir"], "key-private.txt"))
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert sorted(int(m["global_iteration"]) for m in md)[:6] == list(range(1, 7))
+    who = {lid for m in md for lid in m.get("completed_by_learner_id", [])}
+    assert len(who) == 3, who
+    log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
+    line = [l for l in log.splitlines() if l.startswith("[collective-async]")][-1]
+    assert "over 3 learners on 2 ranks" in line and "secure PWA over ciphertexts" in line
+    from metisfl_amd.parallel import checkpoint as ck
+    d = ck.resolve(job["checkpoint_dir"])
+    meta = json.load(open(os.path.join(d, "federation.json")))
+    assert meta["secure_aggregation"] and not os.path.exists(os.path.join(d, "community_model.pb"))
 
 
 def test_async_colocated_rank_lost_resumes_from_checkpoint(tmp_path):

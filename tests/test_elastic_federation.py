@@ -83,6 +83,84 @@ def _worker(rank, world, port, out_dir, mode):
     comm.close()
 
 
+def _coloc_worker(rank, world, port, out_dir, L, slow, ratio):
+    """``L`` co-located learners per rank (global learner g = rank * L + j,
+    shard of 8 + 4 g examples); learner ``slow`` is deliberately slow."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    from metisfl_amd.models.resnet import ResNet18
+    from metisfl_amd.ops.optim import OptimizerSpec
+    from metisfl_amd.parallel.comm import Comm
+    from metisfl_amd.parallel.federation import CollectiveFederation, FederationConfig
+    comm = Comm(backend="gloo")
+    nets, dss = [], []
+    for j in range(L):
+        g = rank * L + j
+        net = ResNet18(batch_size=4, device="cpu", seed=g + 1, width_mult=0.125,
+                       optimizer=OptimizerSpec("momentum_sgd", learning_rate=0.01, momentum=0.9))
+        x, y = _shard(g, 8 + 4 * g)
+        nets.append(net)
+        dss.append(net.make_dataset(x, y, seed=g))
+    cfg = FederationConfig(batch_size=4, local_epochs=4, evaluate_test=False, participation_ratio=ratio,
+                           poll_steps=1, extra={"debug_slow_s": {str(slow): 0.4}})
+    fed = CollectiveFederation(comm, nets, dss, cfg)
+    orig = fed.aggregate
+    rounds = []
+
+    def spy(meta, _orig=orig):
+        np.save(os.path.join(out_dir, f"local_r{fed.global_iteration}_{rank}.npy"),
+                np.stack([n.state.model32.numpy().copy() for n in nets]))
+        return _orig(meta)
+    fed.aggregate = spy
+    for _ in range(2):
+        rec = fed.run_round()
+        np.save(os.path.join(out_dir, f"community_r{rec.global_iteration}_{rank}.npy"),
+                np.stack([n.state.model32.numpy().copy() for n in nets]))
+        rounds.append({"weights": rec.weights, "participated": rec.learner_meta[:, 10].tolist(),
+                       "batches": rec.learner_meta[:, 1].tolist(), "budgets": rec.num_local_updates})
+    with open(os.path.join(out_dir, f"res_coloc_{rank}.json"), "w") as f:
+        json.dump(rounds, f)
+    comm.close()
+
+
+def _run_coloc(tmp_path, world, L, slow, ratio):
+    mp.start_processes(_coloc_worker, args=(world, _free_port(), str(tmp_path), L, slow, ratio), nprocs=world,
+                       join=True, start_method="spawn")
+    return [json.load(open(tmp_path / f"res_coloc_{r}.json")) for r in range(world)]
+
+
+def _check_coloc(tmp_path, res, world, L, slow):
+    n = world * L
+    sizes = np.array([8 + 4 * g for g in range(n)], dtype=np.float64)
+    keep = np.arange(n) != slow
+    for gi, rnd in enumerate(res[0], start=1):
+        assert rnd["participated"] == [0.0 if g == slow else 1.0 for g in range(n)], rnd
+        assert rnd["batches"][slow] < rnd["budgets"][slow]  # cut off before its budget
+        w = np.array(rnd["weights"])
+        assert w[slow] == 0.0 and np.allclose(w[keep], sizes[keep] / sizes[keep].sum())
+        locs = np.concatenate([np.load(tmp_path / f"local_r{gi}_{r}.npy") for r in range(world)]).astype(np.float64)
+        comm = [np.load(tmp_path / f"community_r{gi}_{r}.npy") for r in range(world)]
+        # every learner (the straggler too) holds the participants' average
+        assert all(np.array_equal(comm[0][0], c[j]) for c in comm for j in range(L))
+        assert np.allclose(comm[0][0], np.tensordot(w, locs, axes=1), rtol=1e-5, atol=1e-6)
+
+
+def test_straggler_dropped_among_colocated_learners(tmp_path):
+    """straggler drop with co-located learners.  2 ranks x 2
+    learners, learner 3 deliberately slow, participation_ratio 3/4: every
+    round ends on the quorum of 3 finishers; the slow learner stops issuing
+    updates, weighs 0, and receives the community model."""
+    res = _run_coloc(tmp_path, 2, 2, slow=3, ratio=3 / 4)
+    _check_coloc(tmp_path, res, 2, 2, slow=3)
+
+
+def test_straggler_dropped_in_a_one_process_colocated_federation(tmp_path):
+    """The same on one rank hosting 3 learners (quorum counted in-process)."""
+    res = _run_coloc(tmp_path, 1, 3, slow=1, ratio=2 / 3)
+    _check_coloc(tmp_path, res, 1, 3, slow=1)
+
+
 def _run(tmp_path, mode, world):
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world,
                        join=True, start_method="spawn")

@@ -72,23 +72,32 @@ def test_k8_graph_replay_matches_eager_full_width():
         assert torch.equal(g.state.model32[: g.state.n_params], e.state.model32[: e.state.n_params])  # lr 0
 
 
-def test_colocated_streams_match_sequential_learners():
-    """4 learners replaying their graphs concurrently on 4 streams compute
-    what the same 4 learners compute one after another (no shared scratch,
-    no cross-stream race).  lr 0: bitwise (forward, BN running statistics,
-    loss sums).  16 updates at the bench's learning rate: the split-K weight
-    gradients accumulate with fp32 atomics in arrival order, so two
-    SEQUENTIAL runs already differ and the difference grows chaotically;
-    the co-located run must stay within a few times that run-to-run spread."""
+def _pair_ring():
+    """The LDS ring the co-located group selects (process-wide, before any
+    capture): the sequential references run the same kernels."""
     from metisfl_amd.models.colocated import CoLocatedLearners
+    if CoLocatedLearners.pair_ring:
+        CoLocatedLearners._set_pair_ring(int(CoLocatedLearners.pair_ring))
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_colocated_streams_match_sequential_learners(n):
+    """n learners replaying their graphs concurrently on n streams compute
+    what the same n learners compute one after another (no shared scratch,
+    no cross-stream race) -- 8 is the bench's group, more streams than the
+    4 hardware queues (GPU_MAX_HW_QUEUES), with the 2-stage pair ring.
+    lr 0: bitwise (forward, BN running statistics, loss sums).  16 updates
+    at the bench's learning rate: the split-K weight gradients accumulate
+    with fp32 atomics in arrival order, so two SEQUENTIAL runs already differ
+    and the difference grows chaotically; the co-located run must stay
+    within a few times that run-to-run spread."""
+    from metisfl_amd.models.colocated import CoLocatedLearners
+    _pair_ring()
 
     def make(lr):
         out = []
-        for j in range(4):
+        for j in range(n):
             net = _net(seed=11 + j, lr=lr)
-            # the kernels a 4-learner group runs (CoLocatedLearners turns the
-            # throughput backward on from 4 learners per GPU)
-            net.set_throughput_conv(True)
             x, y = _data(256, 20 + j)
             out.append((net, net.make_dataset(x, y, seed=j)))
         return out
@@ -98,10 +107,11 @@ def test_colocated_streams_match_sequential_learners():
         for grp in (seq, seq2):
             for net, ds in grp:
                 net.train_steps(ds, 16)
-        group = CoLocatedLearners([n for n, _ in co], [d for _, d in co])
-        ms = group.train([16] * 4, [0] * 4)
+        group = CoLocatedLearners([n_ for n_, _ in co], [d for _, d in co])
+        assert len(group.streams) == n and len({s.stream_id for s in group.streams}) == n
+        ms = group.train([16] * n, [0] * n)
         torch.cuda.synchronize()
-        assert len(ms) == 4 and all(m > 0 for m in ms)
+        assert len(ms) == n and all(m > 0 for m in ms)
         for (a, _), (a2, _), (b, _) in zip(seq, seq2, co):
             assert int(a.state.step.cpu()) == int(b.state.step.cpu()) == 16
             r = _rel(b.state.model32, a.state.model32)
@@ -113,3 +123,48 @@ def test_colocated_streams_match_sequential_learners():
                 assert r == 0.0 and ls <= 1e-6, (r, ls)
             else:
                 assert r <= max(5 * spread, 1e-5), (r, spread)
+
+
+def test_colocated_federation_round_matches_sequential_fedavg():
+    """One CollectiveFederation round of the bench's shape (8 co-located
+    learners on one GPU, hierarchical FedAvg: one weighted-sum launch) against
+    the same federation whose learners train one after another on the default
+    stream.  lr 0: the community model (weights, and the BN running
+    statistics the round averages) is bitwise equal; lr 0.005: within the
+    run-to-run spread of two sequential federations."""
+    from metisfl_amd.parallel.comm import Comm
+    from metisfl_amd.parallel.federation import CollectiveFederation, FederationConfig
+    _pair_ring()
+
+    def fed_round(lr, sequential):
+        nets, dss = [], []
+        for j in range(8):
+            net = _net(seed=31 + j, lr=lr)
+            x, y = _data(256, 40 + j)
+            nets.append(net)
+            dss.append(net.make_dataset(x, y, seed=j))
+        cfg = FederationConfig(batch_size=B, local_epochs=2, evaluate_test=False, evaluate_community=False)
+        fed = CollectiveFederation(Comm(), nets, dss, cfg)
+        assert fed.group is not None and len(fed.group.streams) == 8
+        if sequential:
+            def one_after_another(nsteps, offsets):
+                for net, ds, k, off in zip(nets, dss, nsteps, offsets):
+                    net.train_steps(ds, k, step_offset=off)
+                torch.cuda.synchronize()
+                return [1.0] * len(nets)
+            fed.group.train = one_after_another
+        rec = fed.run_round()
+        assert rec.num_local_updates == [16] * 8
+        torch.cuda.synchronize()
+        return fed.net.state.model32.clone(), [n.train_stats()["loss"] for n in nets]
+
+    for lr in (0.0, 0.005):
+        a, la = fed_round(lr, True)
+        a2, _ = fed_round(lr, True)
+        b, lb = fed_round(lr, False)
+        r, spread = _rel(b, a), _rel(a2, a)
+        print(f"lr {lr}: 8 co-located vs sequential community rel {r:.2e}, sequential run-to-run {spread:.2e}")
+        if lr == 0.0:
+            assert torch.equal(a, b) and max(abs(x - y) for x, y in zip(la, lb)) <= 1e-6
+        else:
+            assert r <= max(5 * spread, 1e-5), (r, spread)
