@@ -954,7 +954,9 @@ __global__ __launch_bounds__(256, 2) void conv32_fwd_pair_kernel(Conv32Args a1, 
   }
 }
 
-template <int KS, int ST, bool PAR, int NS>
+// DBM: the dgrad's pixel tile (64, or 128 -- half the W^T re-reads per
+// output pixel; MFL_C32_PAIR_DBM, stride-1 pairs)
+template <int KS, int ST, bool PAR, int NS, int DBM = 64>
 __global__ __launch_bounds__(256, 2) void conv32_bwd_pair_kernel(Conv32Args ad, Conv32Args aw, float* __restrict__ dw,
                                                                  int atomic, int nd, int gdx, int gdy, int gwx,
                                                                  int gwy, int gwz, OptTail ot) {
@@ -967,7 +969,7 @@ __global__ __launch_bounds__(256, 2) void conv32_bwd_pair_kernel(Conv32Args ad, 
   }
   if (b < nd) {
     const Blk k{b % gdx, (b / gdx) % gdy, b / (gdx * gdy), gdx, gdy, nd / (gdx * gdy)};
-    conv32_gemm_body<64, 64, true, KS, ST, PAR, NS, false>(ad, k, smem);
+    conv32_gemm_body<DBM, 64, true, KS, ST, PAR, NS, false>(ad, k, smem);
   } else {
     const int w = b - nd;
     const Blk k{w % gwx, (w / gwx) % gwy, w / (gwx * gwy), gwx, gwy, gwz};
@@ -1361,6 +1363,9 @@ void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, c
 // bf16x3 build carries the 2-stage pair instantiations.
 int g_pair_ns = 0;
 void set_conv32_pair_ring(int ns) { g_pair_ns = ns; }
+size_t gemm_lds_ns(int bm, int bn, int ns) {  // ring of ns stages or the gemm epilogue, whichever is larger
+  return std::max((size_t)ns * (bm + bn) * kRowB, (size_t)bm * (bn + 4) * 4 + 256 * 8 * 4 + 16);
+}
 size_t pair_lds(int ns) {  // ring of ns 64x64 stages or the gemm epilogue, whichever is larger
   return std::max((size_t)ns * (64 + 64) * kRowB, (size_t)64 * (64 + 4) * 4 + 256 * 8 * 4 + 16);
 }
@@ -1380,14 +1385,18 @@ bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGe
   if (!wgrad_fast(gf, pw.kchunk)) return false;
   const Conv32Args ad = gemm_args(gd, true, pd, dy, w, dx, ysplit, counters, nullptr, accum, bnb, 1);
   const Conv32Args aw = wgrad_args(gf, pw, x, dy);
-  const int gdx = cdiv(gd.M, 64), gdy = cdiv(gd.Ng, 64), nd = gdx * gdy * pd.splits;
+  // a 128-pixel dgrad tile (stride-1 pairs, MFL_C32_PAIR_DBM=128): half the
+  // workgroups re-read the layer's W^T tile
+  const int dbm = (gd.stride == 1 && gd.M % 128 == 0 && env_int("MFL_C32_PAIR_DBM", 64) == 128) ? 128 : 64;
+  const int gdx = cdiv(gd.M, dbm), gdy = cdiv(gd.Ng, 64), nd = gdx * gdy * pd.splits;
   const int gwx = cdiv(gf.Ng, 64), gwy = cdiv(gf.K, 64), gwz = pw.splits;
   const OptTail tail = ot ? *ot : OptTail{};
   const int nblk = nd + gwx * gwy * gwz + tail.nblk;
   constexpr int NS = stages_for(64, 64);
   constexpr int NS2 = MFL_C32_BF16X3 && NS > 2 ? 2 : NS;
   const bool r2 = pair_ring2();
-  const size_t lds = pair_lds(r2 ? NS2 : NS);
+  const size_t lds = dbm == 128 ? std::max(pair_lds(r2 ? NS2 : NS), gemm_lds_ns(128, 64, r2 ? NS2 : NS))
+                                : pair_lds(r2 ? NS2 : NS);
   // dw is zero on entry (the step's gradient buffer): an unsplit weight
   // gradient (ResNet-18's 512-channel stage) owns every element it writes, so
   // it stores instead of adding atomically (MFL_C32_WSTORE=0: always atomics)
@@ -1398,7 +1407,11 @@ bool launch_conv32_bwd_pair(const ConvGeom& gd, const ConvPlan& pd, const ConvGe
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     kern<<<nblk, 256, lds, s>>>(ad, aw, dw, wg_atomic, nd, gdx, gdy, gwx, gwy, gwz, tail);
   };
-  if (gd.R == 3 && gd.stride == 1) r2 ? go(conv32_bwd_pair_kernel<3, 1, false, NS2>) : go(conv32_bwd_pair_kernel<3, 1, false, NS>);
+  if (gd.R == 3 && gd.stride == 1 && dbm == 128)
+    r2 ? go(conv32_bwd_pair_kernel<3, 1, false, NS2, 128>) : go(conv32_bwd_pair_kernel<3, 1, false, NS, 128>);
+  else if (gd.R == 3 && gd.stride == 1) r2 ? go(conv32_bwd_pair_kernel<3, 1, false, NS2>) : go(conv32_bwd_pair_kernel<3, 1, false, NS>);
+  else if (gd.R == 1 && gd.stride == 1 && dbm == 128)
+    r2 ? go(conv32_bwd_pair_kernel<1, 1, false, NS2, 128>) : go(conv32_bwd_pair_kernel<1, 1, false, NS, 128>);
   else if (gd.R == 1 && gd.stride == 1) r2 ? go(conv32_bwd_pair_kernel<1, 1, false, NS2>) : go(conv32_bwd_pair_kernel<1, 1, false, NS>);
   else if (gd.R == 3 && gd.stride == 2) r2 ? go(conv32_bwd_pair_kernel<3, 2, true, NS2>) : go(conv32_bwd_pair_kernel<3, 2, true, NS>);
   else if (gd.R == 1 && gd.stride == 2) r2 ? go(conv32_bwd_pair_kernel<1, 2, true, NS2>) : go(conv32_bwd_pair_kernel<1, 2, true, NS>);

@@ -10,3 +10,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 
 python3 scripts/kstats.py $(find $O/prof -name "*kernel_stats.csv") 1 40 > $O/kstats8.txt && head -45 $O/kstats8.txt
 timeout -k 10 300 python -u scripts/multi_learner_probe.py --groups 8 --updates 128 --conv-products exact 2>&1 | grep "ms per" | sed "s/^/exact /" >> $O/exact.log || exit 1
 cat $O/exact.log
+for k in MFL_OPT_TAIL=0 MFL_C32_WSTORE=0 MFL_BN_PREMASK=0 MFL_BN_BWD_PAIR=0 MFL_INPLACE_RESGRAD=0 NONE=1; do env $k timeout -k 10 300 python -u scripts/multi_learner_probe.py --groups 8 --updates 128 --conv-products exact 2>&1 | grep "ms per" | sed "s/^/exact $k /" >> $O/exact.log || exit 1; done
+cat $O/exact.log

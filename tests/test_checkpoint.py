@@ -110,3 +110,54 @@ def test_native_federated_model_writer_matches_python_proto(tmp_path):
     got = model_pb2.FederatedModel()
     got.ParseFromString(open(p, "rb").read())
     assert got == ref
+
+
+def _publish_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from metisfl_amd.parallel.comm import Comm
+    from metisfl_amd.parallel.watchdog import RankWatchdog
+    comm = Comm(backend="gloo")
+    lost = []
+    wd = RankWatchdog(comm, interval_s=0.2, timeout_s=1.5, on_failure=lambda r, p: lost.append(p)).start()
+    store = dist.distributed_c10d._get_default_store()
+    res = {}
+    if rank == 0:
+        # rank 1 never reports its files: rank 0 waits (in short polls) for
+        # 4 s, well past the peers' 1.5 s heartbeat timeout
+        os.makedirs(os.path.join(out_dir, "ck", "round_1"), exist_ok=True)
+        t0 = time.time()
+        try:
+            ck.publish(os.path.join(out_dir, "ck"), "round_1", store, world, "test_publish/1", timeout_s=4.0)
+            res["published"] = True
+        except TimeoutError:
+            res["published"] = False
+        res["waited_s"] = time.time() - t0
+    else:
+        time.sleep(5.0)  # alive and beating, but never sets its key
+    res["lost"] = lost
+    comm.barrier()
+    wd.stop()
+    with open(os.path.join(out_dir, f"pub_{rank}.json"), "w") as f:
+        json.dump(res, f)
+    comm.close()
+
+
+def test_publish_wait_keeps_rank0_heartbeat(tmp_path):
+    """rank 0's publish waits for the other ranks' checkpoint keys
+    through the store client its heartbeats also use.  With one peer that
+    never reports, rank 0 gives up after its timeout and, meanwhile, keeps
+    beating: no rank reports rank 0 (or anyone) lost."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_publish_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    r0 = json.load(open(tmp_path / "pub_0.json"))
+    r1 = json.load(open(tmp_path / "pub_1.json"))
+    assert r0["published"] is False and r0["waited_s"] >= 3.9
+    assert r0["lost"] == [] and r1["lost"] == []
+    assert not (tmp_path / "ck" / "LATEST").exists()
