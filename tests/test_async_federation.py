@@ -257,3 +257,52 @@ def test_async_colocated_single_process():
     assert sorted(u.learner for u in ups) == [0, 0, 1, 1, 2, 2]
     ref = fed.community_reference()
     assert np.abs(fed.community().double().numpy() - ref).max() <= 1e-5 * (np.abs(ref).max() + 1e-12)
+
+
+def test_async_secure_checkpoint_resume_drops_lost_learner(tmp_path):
+    """Secure asynchronous checkpoints hold every learner's latest CIPHERTEXT
+    (no plaintext community model is written); a resume on fewer learners
+    drops the lost learner's ciphertext from the PWA set and restarts the
+    survivors from the PWA of the remaining ones (decrypted by the learners'
+    host, rank 0), continuing the version count."""
+    from metisfl_amd.models.sequential import HousingMLP
+    from metisfl_amd.ops.optim import OptimizerSpec
+    from metisfl_amd.parallel import checkpoint as ck
+    from metisfl_amd.parallel.async_federation import AsyncCollectiveFederation
+    from metisfl_amd.parallel.comm import Comm
+    from metisfl_amd.parallel.federation import FederationConfig
+
+    def learners(gs):
+        nets, dss = [], []
+        for g in gs:
+            net = HousingMLP(batch_size=4, device="cpu", seed=g + 1, optimizer=OptimizerSpec("vanilla_sgd", 0.01))
+            rng = np.random.default_rng(g)
+            nets.append(net)
+            dss.append(net.make_dataset(rng.standard_normal((8 + 4 * g, 13)).astype(np.float32),
+                                        rng.standard_normal(8 + 4 * g).astype(np.float32), seed=g))
+        return nets, dss
+
+    cfg = FederationConfig(batch_size=4, local_epochs=1, evaluate_test=False, secure_aggregation=True)
+    comm = Comm(backend="gloo")
+    nets, dss = learners([0, 1, 2])
+    fed = AsyncCollectiveFederation(comm, nets, dss, cfg, learner_ids=["L0", "L1", "L2"])
+    fed.run_until(max_updates=6, checkpoint_dir=str(tmp_path / "ck"), checkpoint_every=1)
+    assert fed.version >= 6
+    d = ck.resolve(str(tmp_path / "ck"))
+    meta = json.load(open(os.path.join(d, "federation.json")))
+    assert meta["secure_aggregation"] and not os.path.exists(os.path.join(d, "community_model.pb"))
+    plain = {lid: fed.he.decrypt_fresh(fed.last[g]) for g, lid in enumerate(["L0", "L1", "L2"])}
+    w = dict(zip(["L0", "L1", "L2"], fed.last_w))
+    # two learners come back (L1 is lost); they share the key pair
+    nets2, dss2 = learners([0, 2])
+    cfg2 = FederationConfig(batch_size=4, local_epochs=1, evaluate_test=False, secure_aggregation=True,
+                            he_key_dir=fed._he_dir)
+    fed2 = AsyncCollectiveFederation(comm, nets2, dss2, cfg2, learner_ids=["L0", "L2"])
+    fed2.resume(str(tmp_path / "ck"))
+    assert fed2.version == meta["version"] and fed2.resumed["dropped"] == ["L1"]
+    ref = (w["L0"] * plain["L0"] + w["L2"] * plain["L2"]) / (w["L0"] + w["L2"])
+    for n in nets2:
+        got = n.state.model32.double().numpy()
+        assert np.abs(got - ref).max() <= 1e-5 * (np.abs(ref).max() + 1e-9)
+    ups = fed2.run()
+    assert len(ups) == 2 * fed2.tasks and fed2.version == meta["version"] + 2 * fed2.tasks
