@@ -55,6 +55,12 @@ ones' contributions from S and Z, restarts every survivor from the restored
 community model and continues the version count.  The controller
 bookkeeping (runtime metadata per version, the driver's stop request) goes
 through a queue served by its own thread, never under the aggregator lock.
+
+Secure aggregation (``cfg.secure_aggregation``; the reference's
+test_localhost_asynchronous_vanillasgd_with_fhe.yaml): learners submit CKKS
+ciphertexts instead of models and rank 0 keeps each learner's latest
+ciphertext and answers with the private weighted average over them
+(``AsyncPWA``); checkpoints then hold ciphertexts only.
 """
 from __future__ import annotations
 
@@ -283,6 +289,7 @@ class AsyncCollectiveFederation:
         # private weighted average over the latest ones (AsyncPWA)
         self.secure = bool(getattr(cfg, "secure_aggregation", False))
         self.he = None
+        self._ct_buf = None
         if self.secure:
             from metisfl_amd.parallel.federation import setup_ckks
             scheme, self._he_dir = setup_ckks(comm, cfg)
@@ -387,9 +394,11 @@ class AsyncCollectiveFederation:
         model = L.net.state.model32
         # secure aggregation: the learner encrypts its model where it lives and
         # decrypts the community ciphertext it gets back
-        sub = self.he.encrypt(model, out=L.extra.get("ct")) if self.secure else model
+        # (one ciphertext buffer per rank: this rank's submissions are sequential
+        # and the aggregator copies what it keeps)
+        sub = self.he.encrypt(model, out=self._ct_buf) if self.secure else model
         if self.secure:
-            L.extra["ct"] = sub
+            self._ct_buf = sub
         if self.rank == 0:
             with self._lock:
                 self._record_eval(L.gid, meta.get("eval"))
