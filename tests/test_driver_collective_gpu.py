@@ -1,0 +1,53 @@
+"""The driver's collective data plane (``DataPlane: rccl``) on the GPU: the
+learners of a federation environment that share GPU 0 become one rank with
+co-located learners (models/colocated.py, parallel/async_federation.py), run
+to their budget under the driver and report to its controller.  The CPU
+suite covers the same paths under gloo (tests/test_driver_collective.py);
+these runs exercise the HIP streams, events and device CKKS underneath."""
+import json
+import os
+
+import pytest
+
+from tests.test_driver import env_dict, eval_recipe, train_recipe
+
+pytestmark = pytest.mark.gpu
+
+
+def _session(tmp_path, n, rounds, protocol, he=False, **opts):
+    from metisfl_amd.driver.driver_session import DriverSession, free_port
+    from metisfl_amd.models.model_def import StaticModelDef
+    from metisfl_amd.utils.fedenv_parser import FederationEnvironment
+    d = env_dict([free_port() for _ in range(n)], rounds=rounds, protocol=protocol, rule="PWA" if he else "FedAvg")
+    fe = d["FederationEnvironment"]
+    fe["DataPlane"] = "rccl"
+    if he:
+        fe["HomomorphicEncryption"] = {"Scheme": "CKKS", "BatchSize": 4096, "ScalingFactorBits": 52}
+    for l in fe["Learners"]:
+        l["Devices"] = [0]
+    return DriverSession(FederationEnvironment(config=d), StaticModelDef("resnet18", width_mult=0.125), train_recipe,
+                         None, eval_recipe, working_dir=str(tmp_path / "w"), device="cuda", collective_options=opts)
+
+
+def test_driver_synchronous_colocated_on_gpu(tmp_path):
+    sess = _session(tmp_path, 2, rounds=3, protocol="Synchronous")
+    stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason
+    job = json.load(open(os.path.join(str(tmp_path / "w"), "collective_job.json")))
+    assert job["ranks"] == [[0, 1]]  # both learners in one process on GPU 0
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert sorted({int(m["global_iteration"]) for m in md}) == [1, 2, 3]
+    assert all(len(m["completed_by_learner_id"]) == 2 for m in md)
+    assert stats["community_model_results"]["community_evaluation"]
+
+
+def test_driver_asynchronous_secure_pwa_on_gpu(tmp_path):
+    sess = _session(tmp_path, 3, rounds=6, protocol="Asynchronous", he=True, checkpoint_every=2)
+    stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert sorted(int(m["global_iteration"]) for m in md)[:6] == list(range(1, 7))
+    assert len({lid for m in md for lid in m.get("completed_by_learner_id", [])}) == 3
+    log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
+    line = [l for l in log.splitlines() if l.startswith("[collective-async]")][-1]
+    assert "over 3 learners on 1 ranks" in line and "secure PWA over ciphertexts" in line
