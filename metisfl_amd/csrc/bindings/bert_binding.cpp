@@ -48,14 +48,21 @@ void gemm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::optional<t
                        opt_ptr<uint16_t>(act_out), (int)M, (int)N, (int)K, stream_of(x));
 }
 
-// dx[M][K] (+)= dy[M][N] w[N][K]
+// dx[M][K] (+)= dy[M][N] w[N][K].  Long reductions over few output tiles
+// run split-K through an fp32 slab workspace taken from the caching
+// allocator on the current stream (stream-ordered: co-located learners on
+// their own streams, and graph capture, get their own).
 void gemm_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, int64_t M, int64_t N, int64_t K,
                 bool accumulate) {
   dense_dims(M, N, K);
   need(dy, torch::kBFloat16, M * N, "dy");
   need(w, torch::kBFloat16, N * K, "w");
   need(dx, torch::kBFloat16, M * K, "dx");
-  mfl::launch_gemm_dgrad(bfp(dy), bfp(w), bfp(dx), (int)M, (int)N, (int)K, accumulate, stream_of(dy));
+  const int64_t wsn = mfl::gemm_dgrad_workspace((int)M, (int)N, (int)K);
+  torch::Tensor ws;
+  if (wsn > 0) ws = torch::empty({wsn}, dy.options().dtype(torch::kFloat32));
+  mfl::launch_gemm_dgrad(bfp(dy), bfp(w), bfp(dx), (int)M, (int)N, (int)K, accumulate, stream_of(dy),
+                         wsn > 0 ? ws.data_ptr<float>() : nullptr);
 }
 
 // dz = (dy w) * gelu'(z); dbias += colsum(dz)  (FFN1 backward, one launch)
@@ -375,6 +382,8 @@ void register_bert(pybind11::module& m) {
   m.def("set_gemm_big", [](bool on) { mfl::set_gemm_big(on ? 1 : 0); });
   m.def("gemm_big_enabled", []() { return mfl::gemm_big_enabled() != 0; });
   m.def("gemm_dgrad", &gemm_dgrad);
+  m.def("gemm_dgrad_workspace",
+        [](int64_t M, int64_t N, int64_t K) { return mfl::gemm_dgrad_workspace((int)M, (int)N, (int)K); });
   m.def("gemm_dgrad_gelu", &gemm_dgrad_gelu);
   m.def("gemm_wgrad", &gemm_wgrad);
   m.def("gemm_wgrad2", &gemm_wgrad2);

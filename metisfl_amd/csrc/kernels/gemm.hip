@@ -73,9 +73,9 @@ void launch_gemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const fl
 }
 
 void launch_gemm_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
-                       bool accumulate, hipStream_t s) {
+                       bool accumulate, hipStream_t s, float* ws) {
   if (gemm_big_enabled() && gemm_big_ok(M, K, N)) {
-    launch_gemm_big_dgrad(dy, w, dx, M, N, K, accumulate, s);
+    launch_gemm_big_dgrad(dy, w, dx, M, N, K, accumulate, s, ws);
     return;
   }
   // dgrad geometry: "dY" has C = N channels, the output dX has Ng = K columns
@@ -102,6 +102,10 @@ void launch_gemm_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, 
   }
   const ConvGeom g = dense_geom(M, N, K);
   launch_conv_wgrad(g, plan_conv_wgrad(g), x, dy, dw, s, accumulate);
+}
+
+int64_t gemm_dgrad_workspace(int M, int N, int K) {
+  return (gemm_big_enabled() && gemm_big_ok(M, K, N)) ? gemm_big_dgrad_workspace(M, N, K) : 0;
 }
 
 int64_t gemm_wgrad_workspace(int M, int N, int K) {

@@ -153,6 +153,27 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
+    // the chunk's global reads (bf16 output: the residual, the GELU
+    // pre-activation, the accumulated output) are issued BEFORE it is staged
+    // through LDS, so their latency overlaps the staging instead of being
+    // exposed item by item after it
+    uint4 rd_res[NU], rd_z[NU], rd_acc[NU];
+    if constexpr (!OUT32) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int item = lane + 64 * u;
+        const int rl = item / CG, cg = item - rl * CG;
+        const int row = m0 + wm * 128 + 32 * c + rl;
+        const int col = n0 + wn * WN + cg * 8;
+        rd_res[u] = rd_z[u] = rd_acc[u] = uint4{0u, 0u, 0u, 0u};
+        if (row < p.M && col < p.N) {
+          const int64_t off = (int64_t)row * p.ldc + col;
+          if (p.resid) rd_res[u] = *reinterpret_cast<const uint4*>(p.resid + off);
+          if (p.gelu_z) rd_z[u] = *reinterpret_cast<const uint4*>(p.gelu_z + off);
+          if (p.accum) rd_acc[u] = *reinterpret_cast<const uint4*>(p.c16 + off);
+        }
+      }
+    }
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2)
 #pragma unroll
@@ -187,7 +208,7 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[
         uint16_t* dst = p.c16 + off;
         if (p.accum) {
           float o[8];
-          unpack8(*reinterpret_cast<const uint4*>(dst), o);
+          unpack8(rd_acc[u], o);
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] += o[k];
         }
@@ -197,13 +218,13 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[
         }
         if (p.resid) {
           float o[8];
-          unpack8(*reinterpret_cast<const uint4*>(p.resid + off), o);
+          unpack8(rd_res[u], o);
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] += o[k];
         }
         if (p.gelu_z) {  // dz = dh * gelu'(z), exact erf GELU
           float zz[8];
-          unpack8(*reinterpret_cast<const uint4*>(p.gelu_z + off), zz);
+          unpack8(rd_z[u], zz);
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             v[k] *= gelu_grad_f(zz[k]);
@@ -759,6 +780,23 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float4* __rest
   }
 }
 
+// bf16 out (+)= sum over the split-K slabs (8 outputs per lane): the output
+// stage of a split long-reduction dgrad (the MLM decoder's 30,528-deep one)
+__global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float4* __restrict__ ws, int splits,
+                                                                 int64_t n8, uint4* __restrict__ out, int accum) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (accum) unpack8(out[i], v);
+    for (int k = 0; k < splits; ++k) {
+      const float4 a = ws[(int64_t)k * 2 * n8 + 2 * i], b = ws[(int64_t)k * 2 * n8 + 2 * i + 1];
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+    out[i] = pack8(v);
+  }
+}
+
 template <bool AT, bool BT, bool OUT32, int BN>
 void launch_pp_t(const BigGemmArgs& p, hipStream_t s) {
   constexpr size_t kLds = 8 * (size_t)PP_HALF;  // 2 k-tiles x 4 half-tile slots = 128 KiB
@@ -875,13 +913,42 @@ void launch_gemm_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, cons
   launch_big<false, false, false>(p, K, s);
 }
 
+// Split-K slices for a dgrad dX[M][K] = dY[M][N] W[N][K] whose output tiles
+// cannot fill the chip while its reduction is long: the MLM decoder's
+// 2,560 x 768 output (40 tiles) over the 30,528-word vocabulary ran at one
+// workgroup per 6 CUs (289 us).  Same rule as the weight gradients:
+// floor(256 / tiles) slices, at least 16 k-tiles each; 1 = no split.
+int gemm_big_dgrad_splits(int M, int N, int K) {
+  const int tiles = ((M + GB_BM - 1) / GB_BM) * ((K + GB_BN - 1) / GB_BN);
+  if (tiles >= 128 || gb_pipe() != 2) return 1;
+  return std::max(1, std::min(256 / std::max(1, tiles), (N / GB_KQ) / 16));
+}
+
+int64_t gemm_big_dgrad_workspace(int M, int N, int K) {
+  const int sp = gemm_big_dgrad_splits(M, N, K);
+  return sp > 1 ? (int64_t)sp * M * K : 0;
+}
+
 void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
-                           bool accumulate, hipStream_t s) {
+                           bool accumulate, hipStream_t s, float* ws) {
   // dX[M][K] = dY[M][N] . W[N][K]: output columns = K, reduction = N
   BigGemmArgs p{};
   p.a = dy; p.b = w; p.M = M; p.N = K; p.K = N; p.lda = N; p.ldb = K;
   p.a_bytes = (uint32_t)((int64_t)M * N * 2); p.b_bytes = (uint32_t)((int64_t)N * K * 2);
-  p.c16 = dx; p.ldc = K; p.accum = accumulate;
+  p.ldc = K;
+  const int sp = ws ? gemm_big_dgrad_splits(M, N, K) : 1;
+  if (sp > 1 && K % 8 == 0) {
+    // fp32 partials per slice into the slab workspace, one reduce to bf16
+    p.c32 = ws; p.ws = ws; p.accum = 0;
+    p.splits = sp;
+    p.kt_per_split = (N / GB_KQ + sp - 1) / sp;
+    launch_big<false, true, true>(p, N, s);
+    const int64_t n8 = (int64_t)M * K / 8;
+    splitk_reduce_bf16_kernel<<<stream_grid(n8, 256, 2048), 256, 0, s>>>(
+        reinterpret_cast<const float4*>(ws), sp, n8, reinterpret_cast<uint4*>(dx), accumulate ? 1 : 0);
+    return;
+  }
+  p.c16 = dx; p.accum = accumulate;
   p.splits = 1; p.kt_per_split = N / GB_KQ;
   launch_big<false, true, false>(p, N, s);
 }

@@ -47,6 +47,27 @@ def test_linear_gemms(M, N, K):
         assert rel(a, c) < 1e-2
 
 
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_split_k_dgrad_long_reduction(accumulate):
+    """A dgrad whose output tiles cannot fill the chip but whose reduction is
+    long (the MLM decoder: 2,560 x 768 over the vocabulary) runs split-K
+    through fp32 slabs and one bf16 reduce."""
+    from metisfl_amd.ops import bert as BO
+    from metisfl_amd.ops._native import ops
+    _native()
+    M, N, K = 512, 8192, 768
+    assert ops().gemm_dgrad_workspace(M, N, K) > 0  # the split plan is taken
+    assert ops().gemm_dgrad_workspace(16384, 768, 768) == 0  # full-chip shapes are not split
+    g = torch.Generator().manual_seed(3)
+    dy = torch.randn(M, N, generator=g).to(BF)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(BF)
+    dx0 = torch.randn(M, K, generator=g).to(BF)
+    ref = dy.float() @ w.float() + (dx0.float() if accumulate else 0.0)
+    dx = dx0.clone().to(DEV)
+    BO.gemm_dgrad(dy.to(DEV), w.to(DEV), dx, M, N, K, accumulate=accumulate)
+    assert rel(dx.cpu(), ref) < 1e-2
+
+
 @pytest.mark.parametrize("H", [256, 768])
 def test_layernorm_fwd_bwd(H):
     from metisfl_amd.ops import bert as BO
