@@ -340,17 +340,37 @@ __device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, const Blk& 
     mu = *reinterpret_cast<const float4*>(a.bn_mean + col);
     is = *reinterpret_cast<const float4*>(a.bn_invstd + col);
   }
-  for (int rl = r0; rl < BM; rl += RPP) {
-    const int row = m0 + rl;
-    if (row >= g.M || !col_ok) continue;
+  // Every global read of the output stage (the accumulated output, the
+  // consumer BN's mask y and input z) is issued up front for all of this
+  // thread's rows: issued row by row after each row's store they could not
+  // be hoisted (the store may alias them) and each row paid a full
+  // load latency.  The buffers never alias y (dX vs the BN's saved
+  // activations).
+  constexpr int NIT = (BM + RPP - 1) / RPP;
+  float4 pre_acc[NIT], pre_y[NIT], pre_z[NIT];
+  const bool rd_y = a.bn_acc && a.bn_y, rd_z = stats && a.bn_acc;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int rl = r0 + it * RPP, row = m0 + rl;
+    pre_acc[it] = pre_y[it] = pre_z[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rl >= BM || row >= g.M || !col_ok) continue;
+    const int64_t off = (int64_t)out_pixel32(a, row) * g.Ng + col;
+    if (a.accum) pre_acc[it] = *reinterpret_cast<const float4*>(a.y + off);
+    if (rd_y) pre_y[it] = *reinterpret_cast<const float4*>(a.bn_y + off);
+    if (rd_z) pre_z[it] = *reinterpret_cast<const float4*>(a.bn_z + off);
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int rl = r0 + it * RPP, row = m0 + rl;
+    if (rl >= BM || row >= g.M || !col_ok) continue;
     float4 v = *reinterpret_cast<const float4*>(tile + rl * TST + cg * 4);
     const int64_t off = (int64_t)out_pixel32(a, row) * g.Ng + col;
     float4* dst = reinterpret_cast<float4*>(a.y + off);
-    if (a.accum) v = f4add(v, *dst);
-    if (a.bn_acc && a.bn_y) {
+    if (a.accum) v = f4add(v, pre_acc[it]);
+    if (rd_y) {
       // the consumer BN's ReLU mask applied on the way out: dX is stored as
       // g = dX [y > 0], so that BN's backward apply reads no mask
-      const float4 ym = *reinterpret_cast<const float4*>(a.bn_y + off);
+      const float4 ym = pre_y[it];
       v.x = ym.x > 0.f ? v.x : 0.f;
       v.y = ym.y > 0.f ? v.y : 0.f;
       v.z = ym.z > 0.f ? v.z : 0.f;
@@ -359,7 +379,7 @@ __device__ __forceinline__ void tile_epilogue32(const Conv32Args& a, const Blk& 
     *dst = v;
     if (stats) {
       if (a.bn_acc) {
-        const float4 z = *reinterpret_cast<const float4*>(a.bn_z + off);
+        const float4 z = pre_z[it];
         const float4 gk = v;
         s = f4add(s, gk);
         q.x += gk.x * ((z.x - mu.x) * is.x);
