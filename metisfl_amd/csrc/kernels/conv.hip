@@ -109,16 +109,35 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int n0,
 #pragma unroll
     for (int k = 0; k < 8; ++k) bv[k] = a.bias[col + k];
   }
-  for (int rl = r0; rl < BM; rl += RPP) {
-    const int row = m0 + rl;
-    if (row >= g.M || !col_ok) continue;
+  // every global read of the output stage (accumulated output, residual, the
+  // consumer BN's mask y and input z) is issued for all of this thread's rows
+  // before the first store (issued behind each row's possibly-aliasing store
+  // they paid one load latency per row; conv32.hip's tile_epilogue32)
+  constexpr int NIT = (BM + RPP - 1) / RPP;
+  uint4 p_acc[NIT], p_res[NIT], p_y[NIT], p_z[NIT];
+  const bool rd_y = a.bn_acc && a.bn_y, rd_z = stats && a.bn_acc;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int rl = r0 + it * RPP, row = m0 + rl;
+    p_acc[it] = p_res[it] = p_y[it] = p_z[it] = make_uint4(0u, 0u, 0u, 0u);
+    if (rl >= BM || row >= g.M || !col_ok) continue;
+    const int64_t off = (int64_t)out_pixel(a, row) * g.Ng + col;
+    if (accum) p_acc[it] = *reinterpret_cast<const uint4*>(y + off);
+    if (a.resid) p_res[it] = *reinterpret_cast<const uint4*>(a.resid + off);
+    if (rd_y) p_y[it] = *reinterpret_cast<const uint4*>(a.bn_y + off);
+    if (rd_z) p_z[it] = *reinterpret_cast<const uint4*>(a.bn_z + off);
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int rl = r0 + it * RPP, row = m0 + rl;
+    if (rl >= BM || row >= g.M || !col_ok) continue;
     float v[8];
     get(rl, cg * 8, v);
     const int64_t off = (int64_t)out_pixel(a, row) * g.Ng + col;
     uint16_t* dst = y + off;
     if (accum) {
       float o[8];
-      unpack8(*reinterpret_cast<const uint4*>(dst), o);
+      unpack8(p_acc[it], o);
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += o[k];
     }
@@ -128,15 +147,15 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int n0,
     }
     if (a.resid) {
       float o[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.resid + off), o);
+      unpack8(p_res[it], o);
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += o[k];
     }
-    if (a.bn_acc && a.bn_y) {
+    if (rd_y) {
       // the consumer BN's ReLU mask applied on the way out (as conv32.hip):
       // dX is stored as g = dX [y > 0], its BN backward reads no mask
       float ym[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.bn_y + off), ym);
+      unpack8(p_y[it], ym);
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = ym[k] > 0.f ? v[k] : 0.f;
     }
@@ -154,8 +173,8 @@ __device__ __forceinline__ void tile_epilogue(const ConvArgs& a, int m0, int n0,
       unpack8(packed, f);
       if (a.bn_acc) {
         float zz[8], ym[8];
-        unpack8(*reinterpret_cast<const uint4*>(a.bn_z + off), zz);
-        if (a.bn_y) unpack8(*reinterpret_cast<const uint4*>(a.bn_y + off), ym);
+        unpack8(p_z[it], zz);
+        if (a.bn_y) unpack8(p_y[it], ym);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float gk = (a.bn_y && !(ym[k] > 0.f)) ? 0.f : f[k];
