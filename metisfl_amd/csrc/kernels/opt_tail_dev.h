@@ -7,11 +7,22 @@ namespace mfl {
 
 namespace opt_tail_detail {
 // The optimizer tail's grid-stride pass over its range (workgroup t of n).
+// (software-pipelined: the next element's operands are loaded before this
+// one is updated and stored -- the stores could alias them, so otherwise
+// every element of a thread's range paid a full memory latency)
 template <int MODE, int MIRROR>
 static __device__ __forceinline__ void opt_tail_loop(const OptTail& o, int t, int n, float lr, float bc1, float bc2) {
   const int64_t stride = (int64_t)n * blockDim.x;
-  for (int64_t i = (int64_t)t * blockDim.x + threadIdx.x; i < o.n4; i += stride)
-    opt_update4<MODE, MIRROR>(o.p, o.g, o.m, o.v, o.anchor, o.mirror, i, o.h, lr, bc1, bc2, o.zero_grad != 0);
+  int64_t i = (int64_t)t * blockDim.x + threadIdx.x;
+  if (i >= o.n4) return;
+  OptIn4 cur = opt_load4<MODE>(o.p, o.g, o.m, o.v, o.anchor, i);
+  for (; i < o.n4; i += stride) {
+    const bool more = i + stride < o.n4;
+    OptIn4 nxt;
+    if (more) nxt = opt_load4<MODE>(o.p, o.g, o.m, o.v, o.anchor, i + stride);
+    opt_apply4<MODE, MIRROR>(cur, o.p, o.g, o.m, o.v, o.mirror, i, o.h, lr, bc1, bc2, o.zero_grad != 0);
+    if (more) cur = nxt;
+  }
 }
 template <int MIRROR>
 static __device__ __forceinline__ void opt_tail_mirror(const OptTail& o, int t, int n) {

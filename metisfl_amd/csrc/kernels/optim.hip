@@ -32,8 +32,18 @@ __global__ __launch_bounds__(256) void fused_opt_kernel(
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int64_t i = tid; i < zero16; i += stride) zero[i] = make_uint4(0, 0, 0, 0);
-  for (int64_t i = tid; i < n4; i += stride)
-    opt_update4<MODE, MIRROR>(p, g, m, v, anchor, mirror, i, h, lr, bc1, bc2, zero_grad != 0);
+  // software-pipelined (the next element's operands in flight while this
+  // one is updated: BERT's AdamW runs ~50 elements per thread)
+  if (tid < n4) {
+    OptIn4 cur = opt_load4<MODE>(p, g, m, v, anchor, tid);
+    for (int64_t i = tid; i < n4; i += stride) {
+      const bool more = i + stride < n4;
+      OptIn4 nxt;
+      if (more) nxt = opt_load4<MODE>(p, g, m, v, anchor, i + stride);
+      opt_apply4<MODE, MIRROR>(cur, p, g, m, v, mirror, i, h, lr, bc1, bc2, zero_grad != 0);
+      if (more) cur = nxt;
+    }
+  }
   // the step-counter increment that used to be its own launch; these modes
   // never read the counter, so one lane bumps it (Adam / AdamW read it in
   // every block: their launcher ticks in a separate launch -- a last-block

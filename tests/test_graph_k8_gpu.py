@@ -165,6 +165,7 @@ def test_colocated_federation_round_matches_sequential_fedavg():
         r, spread = _rel(b, a), _rel(a2, a)
         print(f"lr {lr}: 8 co-located vs sequential community rel {r:.2e}, sequential run-to-run {spread:.2e}")
         if lr == 0.0:
-            assert torch.equal(a, b) and max(abs(x - y) for x, y in zip(la, lb)) <= 1e-6
+            # (the per-step loss sums are fp32 atomics: ulp-level order effects)
+            assert torch.equal(a, b) and max(abs(x - y) / max(1.0, abs(y)) for x, y in zip(la, lb)) <= 2e-6
         else:
             assert r <= max(5 * spread, 1e-5), (r, spread)
