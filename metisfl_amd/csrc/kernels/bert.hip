@@ -927,21 +927,46 @@ __global__ __launch_bounds__(256) void vocab_xent_kernel(VocabXentArgs a) {
   const int r = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint16_t* z = a.logits + (int64_t)r * a.Vp;
   const int nv = a.V / 8;  // V % 8 == 0 is not required: the tail is scalar
+  // one pass: running max / rescaled sum per 8 logits (one rescale per 8,
+  // not per logit) and the first index of this thread's maximum (accuracy);
+  // two row vectors in flight per iteration
   float m = -INFINITY, s = 0.f;
-  for (int v = t; v < nv; v += 256) {
-    float f[8];
-    unpack8(reinterpret_cast<const uint4*>(z)[v], f);
+  int am = a.V;
+  auto fold8 = [&](const float (&f)[8], int base) __attribute__((always_inline)) {
+    float m8 = f[0];
+    int i8 = base;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float nm = fmaxf(m, f[k]);
-      s = s * __expf(m - nm) + __expf(f[k] - nm);
-      m = nm;
+    for (int k = 1; k < 8; ++k)
+      if (f[k] > m8) {
+        m8 = f[k];
+        i8 = base + k;
+      }
+    if (m8 > m) am = i8;  // strictly greater: indices rise within a thread
+    const float nm = fmaxf(m, m8);
+    float e = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e += __expf(f[k] - nm);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + e;
+    m = nm;
+  };
+  for (int v = t; v < nv; v += 512) {
+    const bool two = v + 256 < nv;
+    const uint4 u0 = reinterpret_cast<const uint4*>(z)[v];
+    uint4 u1 = make_uint4(0u, 0u, 0u, 0u);
+    if (two) u1 = reinterpret_cast<const uint4*>(z)[v + 256];
+    float f[8];
+    unpack8(u0, f);
+    fold8(f, v * 8);
+    if (two) {
+      unpack8(u1, f);
+      fold8(f, (v + 256) * 8);
     }
   }
   for (int k = nv * 8 + t; k < a.V; k += 256) {
     const float f = bf2f(z[k]);
+    if (f > m) am = k;
     const float nm = fmaxf(m, f);
-    s = s * __expf(m - nm) + __expf(f - nm);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + __expf(f - nm);
     m = nm;
   }
   // block max / sum
@@ -951,10 +976,9 @@ __global__ __launch_bounds__(256) void vocab_xent_kernel(VocabXentArgs a) {
   bm = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
   float bs = wave_sum(m == -INFINITY ? 0.f : s * __expf(m - bm));
   if (lane == 0) ss[w] = bs;
-  // first index of the maximum (accuracy)
-  int am = a.V;
-  for (int k = t; k < a.V; k += 256)
-    if (bf2f(z[k]) == bm) { am = k; break; }
+  // first index of the row maximum: the smallest index among the threads
+  // whose own maximum is it
+  if (m != bm) am = a.V;
   for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o));
   if (lane == 0) sa[w] = am;
   __syncthreads();
@@ -966,9 +990,16 @@ __global__ __launch_bounds__(256) void vocab_xent_kernel(VocabXentArgs a) {
   const float inv_s = 1.f / bs, inv_r = 1.f / (float)a.R;
   if (a.dlogits) {
     uint16_t* d = a.dlogits + (int64_t)r * a.Vp;
-    for (int v = t; v < a.Vp / 8; v += 256) {
+    // (software-pipelined: the next logits vector is requested before this
+    // one's gradient is stored -- the store may alias it, so otherwise each
+    // of the row's ~15 vectors per thread paid a full load latency)
+    const int nvp = a.Vp / 8;
+    uint4 nxt = t < nvp ? reinterpret_cast<const uint4*>(z)[t] : make_uint4(0u, 0u, 0u, 0u);
+    for (int v = t; v < nvp; v += 256) {
+      const uint4 cur = nxt;
+      if (v + 256 < nvp) nxt = reinterpret_cast<const uint4*>(z)[v + 256];
       float f[8];
-      unpack8(reinterpret_cast<const uint4*>(z)[v], f);
+      unpack8(cur, f);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int col = v * 8 + k;
