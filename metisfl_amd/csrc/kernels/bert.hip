@@ -446,26 +446,12 @@ __device__ __forceinline__ void load_head(uint8_t* dst, const uint16_t* src, int
 
 constexpr float kLog2e = 1.4426950408889634f;
 
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* Ks = smem;
-  uint8_t* Vs = smem + kT * kD * 2;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint8_t* Pw = smem + 2 * kT * kD * 2 + wave * (32 * kT * 2);  // this wave's [32][128]
-  const int b = blockIdx.x / a.heads, h = blockIdx.x - b * a.heads;
-  const int H = a.heads * kD, ld = 3 * H;
-  const int64_t row0 = (int64_t)b * kT;
-  load_head(Ks, a.qkv, row0, ld, H + h * kD);
-  load_head(Vs, a.qkv, row0, ld, 2 * H + h * kD);
+// One attention item (batch b, head h) once K and V sit in LDS and this
+// wave's Q fragments in registers, in two halves: S = Q K^T and the row
+// softmax into this wave's P tile (lse saved), then O = P V.
+__device__ __forceinline__ void attn_fwd_scores(const AttnArgs& a, int b, int h, const uint8_t* Ks, uint8_t* Pw,
+                                                const bf16x8 (&qf)[2][2], int lane, int wave) {
   const int t0 = wave * 32;
-  bf16x8 qf[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-      qf[i][kk] = *reinterpret_cast<const bf16x8*>(a.qkv + (row0 + t0 + 16 * i + (lane & 15)) * ld + h * kD +
-                                                   32 * kk + 8 * (lane >> 4));
-  __syncthreads();
   f32x4 s[2][8];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -506,6 +492,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       if ((lane & 15) == 0) a.lse[((int64_t)b * a.heads + h) * kT + t0 + r] = mx * a.scale + __logf(sum);
     }
   __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void attn_fwd_pv(const AttnArgs& a, int b, int h, const uint8_t* Vs, const uint8_t* Pw,
+                                            int lane, int wave) {
+  const int H = a.heads * kD;
+  const int64_t row0 = (int64_t)b * kT;
+  const int t0 = wave * 32;
   f32x4 o[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -532,6 +524,84 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
         const int t = t0 + 16 * i + 4 * (lane >> 4) + e;
         a.ctx[(row0 + t) * H + h * kD + 16 * dj + (lane & 15)] = f2bf(o[i][dj][e]);
       }
+}
+
+// this wave's Q fragments of item (b, h), straight from global memory
+__device__ __forceinline__ void attn_q_frags(const AttnArgs& a, int b, int h, int lane, int wave, bf16x8 (&qf)[2][2]) {
+  const int H = a.heads * kD, ld = 3 * H;
+  const int64_t row0 = (int64_t)b * kT;
+  const int t0 = wave * 32;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      qf[i][kk] = *reinterpret_cast<const bf16x8*>(a.qkv + (row0 + t0 + 16 * i + (lane & 15)) * ld + h * kD +
+                                                   32 * kk + 8 * (lane >> 4));
+}
+
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* Ks = smem;
+  uint8_t* Vs = smem + kT * kD * 2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* Pw = smem + 2 * kT * kD * 2 + wave * (32 * kT * 2);  // this wave's [32][128]
+  const int b = blockIdx.x / a.heads, h = blockIdx.x - b * a.heads;
+  const int H = a.heads * kD, ld = 3 * H;
+  const int64_t row0 = (int64_t)b * kT;
+  load_head(Ks, a.qkv, row0, ld, H + h * kD);
+  load_head(Vs, a.qkv, row0, ld, 2 * H + h * kD);
+  bf16x8 qf[2][2];
+  attn_q_frags(a, b, h, lane, wave, qf);
+  __syncthreads();
+  attn_fwd_scores(a, b, h, Ks, Pw, qf, lane, wave);
+  attn_fwd_pv(a, b, h, Vs, Pw, lane, wave);
+}
+
+// Persistent forward: a workgroup walks items blockIdx.x, + gridDim.x, ...
+// with the NEXT item's K / V slices (4 + 4 16-B chunks per thread) in
+// flight while it computes this one's P V and writes its context (one item per
+// workgroup paid its load latency with nothing to overlap: 2 workgroups per
+// CU by LDS).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd_persist_kernel(AttnArgs a, int nitems) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* Ks = smem;
+  uint8_t* Vs = smem + kT * kD * 2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* Pw = smem + 2 * kT * kD * 2 + wave * (32 * kT * 2);
+  const int H = a.heads * kD, ld = 3 * H;
+  const int r = threadIdx.x >> 3, cc = (threadIdx.x & 7) * 8;  // rows r + 32 u, u < 4
+  u32x4 kr[4], vr[4];  // (native vectors: HIP uint4 arrays stayed in scratch)
+  bf16x8 qf[2][2];
+  // (a macro, not a lambda: a lambda capturing the register arrays by
+  // reference put them in scratch)
+#define MFL_ATTN_FWD_FETCH(ITEM)                                                         \
+  {                                                                                      \
+    const int b_ = (ITEM) / a.heads, h_ = (ITEM) - b_ * a.heads;                         \
+    const uint16_t* base = a.qkv + ((int64_t)b_ * kT + r) * ld + h_ * kD + cc;           \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                      \
+      kr[u] = *reinterpret_cast<const u32x4*>(base + (int64_t)32 * u * ld + H);          \
+      vr[u] = *reinterpret_cast<const u32x4*>(base + (int64_t)32 * u * ld + 2 * H);      \
+    }                                                                                    \
+  }
+  int it = blockIdx.x;  // grid <= nitems
+  MFL_ATTN_FWD_FETCH(it)
+#pragma unroll 1
+  for (; it < nitems; it += gridDim.x) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      *reinterpret_cast<u32x4*>(Ks + toff<128>(r + 32 * u, cc)) = kr[u];
+      *reinterpret_cast<u32x4*>(Vs + toff<128>(r + 32 * u, cc)) = vr[u];
+    }
+    const int b = it / a.heads, h = it - b * a.heads;
+    attn_q_frags(a, b, h, lane, wave, qf);
+    __syncthreads();
+    attn_fwd_scores(a, b, h, Ks, Pw, qf, lane, wave);
+    // the scores are dead once P is in LDS: their registers hold the fetch
+    if (it + gridDim.x < nitems) MFL_ATTN_FWD_FETCH(it + gridDim.x)
+    attn_fwd_pv(a, b, h, Vs, Pw, lane, wave);
+    __syncthreads();  // every wave is done with Ks / Vs / Pw before the next staging
+  }
+#undef MFL_ATTN_FWD_FETCH
 }
 
 template <int NI>
@@ -842,7 +912,20 @@ size_t attn_fwd_lds() { return 2 * kT * kD * 2 + 4 * 32 * kT * 2; }
 size_t attn_bwd_lds() { return 4 * kT * kD * 2 + 2 * kT * kT * 2 + (2 * kT + 3 * kD) * 4; }
 
 void launch_attn_fwd(const AttnArgs& a, hipStream_t s) {
-  attn_fwd_kernel<<<a.batch * a.heads, 256, attn_fwd_lds(), s>>>(a);
+  // persistent by default (two workgroups per CU, next item prefetched);
+  // MFL_ATTN_FWD_PERSIST=0: one item per workgroup
+  const char* pv = getenv("MFL_ATTN_FWD_PERSIST");  // read per launch (tests toggle it)
+  const int nitems = a.batch * a.heads;
+  if (!(pv && *pv == '0')) {
+    static const int ncu = [] {
+      int dev = 0, n = 256;
+      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      return n > 0 ? n : 256;
+    }();
+    attn_fwd_persist_kernel<<<std::min(nitems, 2 * ncu), 256, attn_fwd_lds(), s>>>(a, nitems);
+    return;
+  }
+  attn_fwd_kernel<<<nitems, 256, attn_fwd_lds(), s>>>(a);
 }
 
 void launch_attn_bwd(const AttnArgs& a, hipStream_t s) {

@@ -310,3 +310,27 @@ def test_attention_bwd_persistent_matches_per_item_launch(monkeypatch):
     assert rel(a, b) < 1e-3
     assert (a == b).float().mean().item() > 0.99
     assert rel(out["1"][1], out["0"][1]) < 1e-4
+
+
+def test_attention_fwd_persistent_matches_per_item_launch(monkeypatch):
+    """The persistent attention forward (a workgroup walks items with the next
+    item's K / V slices in flight, 1152 items over <= 512 workgroups) runs the
+    per-item arithmetic unchanged: context and lse bitwise equal to the
+    one-item-per-workgroup launch."""
+    from metisfl_amd.ops import bert as BO
+    _native()
+    torch.manual_seed(10)
+    B, heads = 96, 12
+    T, H = 128, heads * 64
+    qkv = (torch.randn(B * T, 3 * H) * 1.5).to(BF).to(DEV)
+    scale = 1.0 / math.sqrt(64)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MFL_ATTN_FWD_PERSIST", mode)
+        ctx = torch.full((B * T, H), float("nan"), dtype=BF, device=DEV)
+        lse = torch.full((B * heads * T,), float("nan"), device=DEV)
+        BO.attn_fwd(qkv, ctx, lse, B, heads, scale)
+        torch.cuda.synchronize()
+        out[mode] = (ctx, lse)
+    assert torch.equal(out["1"][0], out["0"][0])
+    assert torch.equal(out["1"][1], out["0"][1])
