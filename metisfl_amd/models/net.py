@@ -10,6 +10,7 @@ a task.  Loss / accuracy are accumulated on device and read once per task.
 """
 from __future__ import annotations
 
+import gc
 import os
 import time
 
@@ -211,8 +212,19 @@ class StaticNet:
             body(ds)
         torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            body(ds)
+        # no garbage collection while capturing: a collected object whose
+        # destructor frees device memory or destroys an event / stream (another
+        # learner's CKKS buffers, a finished task's events) is an illegal call
+        # under global-mode capture and aborts the process
+        gc.collect()
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.graph(g, stream=s):
+                body(ds)
+        finally:
+            if was:
+                gc.enable()
         torch.cuda.synchronize(self.device)
         self.state.model32.copy_(snap)
         self.state.step.copy_(step0)
