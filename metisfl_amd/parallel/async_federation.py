@@ -411,9 +411,9 @@ class AsyncCollectiveFederation:
                 self._after_update()
         else:
             self.store.set(_KEY.format(self.tag, L.gid, L.sub), json.dumps(meta))
-            dist.send(sub, dst=0, group=self.p2p)
+            self.comm.send(sub, 0, group=self.p2p)
             back = sub if self.secure else model
-            dist.recv(back, src=0, group=self.p2p)
+            self.comm.recv(back, 0, group=self.p2p)
             L.base_version = int(self.store.get(_VER.format(self.tag, L.gid, L.sub)))
         if self.secure:
             self.he.decrypt_into(back, model)
@@ -620,7 +620,7 @@ class AsyncCollectiveFederation:
                 continue
             meta = json.loads(self.store.get(key))
             src = self.owners[g]
-            dist.recv(self.rbuf, src=src, group=self.p2p)
+            self.comm.recv(self.rbuf, src, group=self.p2p)
             with self._lock:
                 self._record_eval(g, meta.get("eval"))
                 self._fedrec(g, self.rbuf, meta)
@@ -629,7 +629,7 @@ class AsyncCollectiveFederation:
                 self._sync_stream()
                 self._after_update()
             self.store.set(_VER.format(self.tag, g, t), str(ver))
-            dist.send(comm_model, dst=src, group=self.p2p)
+            self.comm.send(comm_model, src, group=self.p2p)
             self.next_task[g] = t + 1
             served += 1
         return served

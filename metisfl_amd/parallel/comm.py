@@ -7,6 +7,15 @@ RCCL collectives between the learner processes (torch.distributed backend
 ``nccl`` IS RCCL on ROCm); the gRPC services remain the control plane for
 remote learners and API parity.  CPU-only runs (tests) use ``gloo`` with the
 identical code path.
+
+``MFL_COMM_BACKEND=gloo`` on a GPU host keeps the compute on the GPU and runs
+the collectives over gloo, staged through host memory: several ranks can then
+share ONE GPU (RCCL refuses two ranks on the same device), which is how the
+multi-rank paths -- the hierarchical co-located sum + all-reduce, rank 0's
+asynchronous service thread -- are rehearsed with real HIP graphs and streams
+on a one-GPU box (tests/test_multirank_gpu.py).  Ranks map to
+``LOCAL_RANK % device_count``.  A rehearsal mode, not a data plane: every
+collective pays a device <-> host round trip.
 """
 from __future__ import annotations
 
@@ -22,13 +31,16 @@ class Comm:
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        # host-staged gloo on GPU ranks (module docstring)
+        self.staged = backend is None and os.environ.get("MFL_COMM_BACKEND") == "gloo" and torch.cuda.is_available()
         use_cuda = torch.cuda.is_available() and backend != "gloo"
         if use_cuda:
-            torch.cuda.set_device(self.local_rank)
-            self.device = torch.device("cuda", self.local_rank)
+            idx = self.local_rank % torch.cuda.device_count() if self.staged else self.local_rank
+            torch.cuda.set_device(idx)
+            self.device = torch.device("cuda", idx)
         else:
             self.device = torch.device("cpu")
-        self.backend = backend or ("nccl" if use_cuda else "gloo")
+        self.backend = "gloo" if self.staged else (backend or ("nccl" if use_cuda else "gloo"))
         self.owned = False
         if self.world > 1 and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -51,24 +63,46 @@ class Comm:
             else:
                 dist.barrier()
 
+    # host staging of a device tensor for the gloo rehearsal mode
+    def _host(self, t: torch.Tensor) -> torch.Tensor:
+        return t.cpu() if self.staged and t.is_cuda else t
+
+    @staticmethod
+    def _back(t: torch.Tensor, h: torch.Tensor) -> None:
+        if h is not t:
+            t.copy_(h)
+
     def all_reduce_(self, t: torch.Tensor) -> None:
         if self.distributed:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            h = self._host(t)
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            self._back(t, h)
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> None:
         if self.distributed:
-            dist.broadcast(t, src=src)
+            h = self._host(t)
+            dist.broadcast(h, src=src)
+            self._back(t, h)
+
+    def send(self, t: torch.Tensor, dst: int, group=None) -> None:
+        """Point-to-point send (``group``: e.g. the asynchronous protocol's own)."""
+        dist.send(self._host(t), dst=dst, group=group)
+
+    def recv(self, t: torch.Tensor, src: int, group=None) -> None:
+        h = self._host(t)
+        dist.recv(h, src=src, group=group)
+        self._back(t, h)
 
     def broadcast_bytes(self, data: bytes | None, src: int = 0) -> bytes:
         """Small host blob (keys, configs) from ``src`` to every rank."""
         if not self.distributed:
             return data or b""
         n = torch.tensor([len(data) if self.rank == src else 0], dtype=torch.int64, device=self.device)
-        dist.broadcast(n, src=src)
+        self.broadcast_(n, src=src)
         buf = torch.empty(int(n.item()), dtype=torch.uint8, device=self.device)
         if self.rank == src:
             buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
-        dist.broadcast(buf, src=src)
+        self.broadcast_(buf, src=src)
         return bytes(buf.cpu().numpy().tobytes())
 
     def all_gather_rows(self, row: torch.Tensor) -> torch.Tensor:
@@ -76,16 +110,18 @@ class Comm:
         if not self.distributed:
             return row.reshape(1, -1).clone()
         # flat output: gloo's allgather_base wants chunks shaped like the input
-        out = torch.empty(self.world * row.numel(), dtype=row.dtype, device=row.device)
-        dist.all_gather_into_tensor(out, row.contiguous().reshape(-1))
-        return out.view(self.world, row.numel())
+        dev = torch.device("cpu") if self.staged else row.device
+        out = torch.empty(self.world * row.numel(), dtype=row.dtype, device=dev)
+        dist.all_gather_into_tensor(out, self._host(row.contiguous().reshape(-1)))
+        return out.view(self.world, row.numel()).to(row.device)
 
     def all_max(self, x: float) -> float:
         if not self.distributed:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=self.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        h = self._host(t)
+        dist.all_reduce(h, op=dist.ReduceOp.MAX)
+        return float(h.item())
 
     def close(self) -> None:
         if self.owned and dist.is_initialized():

@@ -1,0 +1,76 @@
+"""Multi-rank federation paths on ONE GPU, with real HIP graphs and streams.
+
+RCCL refuses two ranks on one device, so these runs use the host-staged gloo
+mode of ``parallel/comm.py`` (``MFL_COMM_BACKEND=gloo``): 2 / 4 / 8 ranks share
+GPU 0, each hosting 4 / 2 / 1 co-located learners on its own HIP streams, and every
+collective travels through host memory.  What they pin is the multi-rank
+logic that the CPU gloo tests can only run without graphs:
+
+* the synchronous round's hierarchical sum -- K1 over a rank's learners into
+  learner 0's buffer, then the in-place all-reduce (parallel/federation.py) --
+  leaves bitwise-identical community models on every rank (bench.py's digest);
+* the asynchronous protocol's rank-0 service thread (blocking p2p on its own
+  group while rank 0's learners replay their graphs) serves every learner of
+  both ranks, plain FedRec and CKKS PWA over ciphertexts, and the community
+  model matches the host re-computation (parallel/async_federation.py).
+
+The 8-GPU RCCL run itself is the driver's (SCALE_rNN.json); the ranks here
+use at most 8 GPU processes (the 8-rank case is bench.py's N = 8 shape: one
+learner per rank).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _torchrun(script_args, nproc=2, timeout=400):
+    env = dict(os.environ, MFL_COMM_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}"] + script_args
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert lines, p.stdout[-2000:]
+    return json.loads(lines[-1])
+
+
+@pytest.mark.parametrize("nproc", [2, 4, 8])
+def test_sync_rounds_over_ranks(nproc):
+    """bench.py's 8-learner federation over 2 / 4 / 8 ranks (4 / 2 / 1
+    learners per rank: the N = 8 shape runs the one-learner-per-rank path)."""
+    out = _torchrun(["bench.py", "--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--train-size", "8192",
+                     "--test-size", "2048", "--local-epochs", "1", "--exact-updates", "0"], nproc=nproc)
+    assert out["n_gpus"] == nproc
+    assert out["config"]["learners"] == 8 and out["config"]["learners_per_gpu"] == 8 // nproc
+    cm = out["community_model"]
+    assert len(cm["sha256_128"]) == nproc and cm["identical"], cm
+    w = out["aggregation_weights"]
+    assert len(w) == 8 and abs(sum(w) - 1.0) < 1e-6
+
+
+@pytest.mark.parametrize("secure", [False, True])
+def test_async_two_ranks_service_thread(secure):
+    args = ["benchmarks/async_bench.py", "--gpus", "2", "--learners", "4", "--tasks", "2", "--warmup", "1",
+            "--train-size", "4096"]
+    if secure:
+        args.append("--secure-aggregation")
+    out = _torchrun(args)
+    assert out["config"]["learners"] == 4 and out["config"]["learners_per_gpu"] == 2
+    assert out["updates"] == 4 * 2
+    assert all(n == 2 for n in out["updates_per_learner"]), out["updates_per_learner"]
+    assert out["community_model_matches_host"]
+    assert ("CKKS PWA" in out["config"]["aggregation"]) == secure
