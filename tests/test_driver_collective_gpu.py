@@ -14,7 +14,7 @@ from tests.test_driver import env_dict, eval_recipe, train_recipe
 pytestmark = pytest.mark.gpu
 
 
-def _session(tmp_path, n, rounds, protocol, he=False, **opts):
+def _session(tmp_path, n, rounds, protocol, he=False, devices=None, **opts):
     from metisfl_amd.driver.driver_session import DriverSession, free_port
     from metisfl_amd.models.model_def import StaticModelDef
     from metisfl_amd.utils.fedenv_parser import FederationEnvironment
@@ -23,8 +23,8 @@ def _session(tmp_path, n, rounds, protocol, he=False, **opts):
     fe["DataPlane"] = "rccl"
     if he:
         fe["HomomorphicEncryption"] = {"Scheme": "CKKS", "BatchSize": 4096, "ScalingFactorBits": 52}
-    for l in fe["Learners"]:
-        l["Devices"] = [0]
+    for i, l in enumerate(fe["Learners"]):
+        l["Devices"] = [devices[i] if devices else 0]
     return DriverSession(FederationEnvironment(config=d), StaticModelDef("resnet18", width_mult=0.125), train_recipe,
                          None, eval_recipe, working_dir=str(tmp_path / "w"), device="cuda", collective_options=opts)
 
@@ -51,3 +51,29 @@ def test_driver_asynchronous_secure_pwa_on_gpu(tmp_path):
     log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
     line = [l for l in log.splitlines() if l.startswith("[collective-async]")][-1]
     assert "over 3 learners on 1 ranks" in line and "secure PWA over ciphertexts" in line
+
+
+def test_driver_two_ranks_on_one_gpu_sync_and_async(tmp_path, monkeypatch):
+    """Learners on ``Devices`` 0 and 1 become two ranks; with the host-staged
+    gloo collectives (parallel/comm.py, MFL_COMM_BACKEND=gloo) both map to GPU
+    0 of this box, so the driver's multi-rank collective plane runs with real
+    HIP graphs: a synchronous FedAvg federation (2 ranks x 2 co-located
+    learners) and the asynchronous protocol with CKKS PWA (rank 0's service
+    thread serving rank 1's learners)."""
+    monkeypatch.setenv("MFL_COMM_BACKEND", "gloo")
+    sess = _session(tmp_path / "sync", 4, rounds=2, protocol="Synchronous", devices=[0, 0, 1, 1])
+    stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason
+    job = json.load(open(os.path.join(str(tmp_path / "sync" / "w"), "collective_job.json")))
+    assert job["ranks"] == [[0, 1], [2, 3]]
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert all(len(m["completed_by_learner_id"]) == 4 for m in md)
+
+    sess = _session(tmp_path / "async", 3, rounds=5, protocol="Asynchronous", he=True, devices=[0, 1, 1])
+    stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert len({lid for m in md for lid in m.get("completed_by_learner_id", [])}) == 3
+    log = open(os.path.join(str(tmp_path / "async" / "w"), "learner_localhost-0.log")).read()
+    line = [l for l in log.splitlines() if l.startswith("[collective-async]")][-1]
+    assert "over 3 learners on 2 ranks" in line and "secure PWA over ciphertexts" in line
