@@ -90,7 +90,31 @@ def _he_decoder(fcfg, device):
     return scheme
 
 
+def _await_peer_verdict(wd) -> None:
+    """A collective raised (gloo reports a closed peer connection at once;
+    RCCL would block instead): if a peer died, this rank's heartbeat watchdog
+    names it within its timeout and exits with EXIT_PEER_LOST -- the code the
+    driver treats as a survivor's.  Waits for that verdict; returns (and the
+    caller re-raises, a genuine failure of this rank) if no peer went silent."""
+    from metisfl_amd.utils.metis_logger import MetisLogger
+    MetisLogger.warning("collective call failed; waiting up to %.0f s for the heartbeat watchdog",
+                        wd.timeout + 3 * wd.interval)
+    end = time.time() + wd.timeout + 3 * wd.interval + 1.0
+    while time.time() < end:
+        time.sleep(0.1)  # the watchdog thread os._exit()s on a lost peer
+
+
 def main(argv=None) -> int:
+    ctx: dict = {}
+    try:
+        return _main(argv, ctx)
+    except Exception:
+        if ctx.get("wd") is not None:
+            _await_peer_verdict(ctx["wd"])
+        raise
+
+
+def _main(argv, ctx: dict) -> int:
     argv = argv if argv is not None else sys.argv[1:]
     with open(argv[0]) as f:
         job = json.load(f)
@@ -143,6 +167,7 @@ def main(argv=None) -> int:
     if comm.world > 1 and job.get("watchdog", True):
         wd = RankWatchdog(comm, interval_s=float(job.get("heartbeat_s", 1.0)),
                           timeout_s=float(job.get("heartbeat_timeout_s", 20.0))).start()
+    ctx["wd"] = wd
     t_start = time.time()
 
     def initial_model(fed_load):

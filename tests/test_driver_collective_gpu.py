@@ -77,3 +77,43 @@ def test_driver_two_ranks_on_one_gpu_sync_and_async(tmp_path, monkeypatch):
     log = open(os.path.join(str(tmp_path / "async" / "w"), "learner_localhost-0.log")).read()
     line = [l for l in log.splitlines() if l.startswith("[collective-async]")][-1]
     assert "over 3 learners on 2 ranks" in line and "secure PWA over ciphertexts" in line
+
+
+def test_driver_recovers_a_sigkilled_gpu_rank(tmp_path, monkeypatch):
+    """Two ranks of two co-located learners on GPU 0 (host-staged gloo); rank
+    1 is SIGKILLed at round 2.  The driver relaunches the survivor rank from
+    the last checkpoint (fresh processes: nothing re-execs after touching the
+    GPU) and the federation reaches its round budget on the remaining two
+    learners."""
+    monkeypatch.setenv("MFL_COMM_BACKEND", "gloo")
+    sess = _session(tmp_path, 4, rounds=4, protocol="Synchronous", devices=[0, 0, 1, 1],
+                    fault={"rank": 1, "round": 2, "signal": "KILL"}, heartbeat_timeout_s=10, checkpoint_every=1)
+    stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason
+    assert len(sess.recoveries) == 1
+    rc = sess.recoveries[0]
+    assert rc["exit_code"] == -9 and rc["survivors"] == 2, rc  # learners
+    assert sorted(rc["lost_learners"]) == ["localhost-2", "localhost-3"], rc
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert sorted({int(m["global_iteration"]) for m in md}) == [1, 2, 3, 4]
+    last = max(md, key=lambda m: int(m["global_iteration"]))
+    assert len(last["completed_by_learner_id"]) == 2
+
+
+def test_driver_async_recovers_a_lost_gpu_rank(tmp_path, monkeypatch):
+    """The asynchronous protocol over two GPU ranks (host-staged gloo): rank 1
+    (learners 2 and 3) dies at its second task; the survivors resume from the
+    last checkpointed community version with the lost learners' FedRec
+    contributions dropped, and reach the version budget."""
+    monkeypatch.setenv("MFL_COMM_BACKEND", "gloo")
+    sess = _session(tmp_path, 4, rounds=12, protocol="Asynchronous", devices=[0, 0, 1, 1],
+                    fault={"rank": 1, "round": 2}, heartbeat_timeout_s=8, checkpoint_every=1)
+    stats = sess.run_collective(request_every_secs=0.3)
+    assert sess.termination_reason == "rounds", sess.termination_reason
+    assert len(sess.recoveries) == 1
+    rc = sess.recoveries[0]
+    assert sorted(rc["lost_learners"]) == ["localhost-2", "localhost-3"] and rc["survivors"] == 2, rc
+    md = stats["federation_runtime_metadata"]["metadata"]
+    assert max(int(m["global_iteration"]) for m in md) >= 12
+    log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
+    assert "[collective-async] resumed at version" in log
