@@ -117,3 +117,36 @@ def test_driver_async_recovers_a_lost_gpu_rank(tmp_path, monkeypatch):
     assert max(int(m["global_iteration"]) for m in md) >= 12
     log = open(os.path.join(str(tmp_path / "w"), "learner_localhost-0.log")).read()
     assert "[collective-async] resumed at version" in log
+
+
+def test_driver_learner_joins_gpu_ranks(tmp_path, monkeypatch):
+    """A learner joins a running 2-rank federation on the GPU (host-staged
+    gloo): the ranks checkpoint at the round boundary and the driver relaunches
+    three ranks from it; the last round has three contributors."""
+    import time
+
+    from metisfl_amd.driver.driver_session import free_port
+    monkeypatch.setenv("MFL_COMM_BACKEND", "gloo")
+    R = 30  # GPU rounds take well under a second: the join must land mid-run
+    sess = _session(tmp_path, 2, rounds=R, protocol="Synchronous", devices=[0, 1])
+    try:
+        sess.initialize_federation()
+        c = sess._driver_controller_grpc_client
+        end = time.time() + 120
+        while time.time() < end:  # wait until round 1 is under way
+            if c.get_runtime_metadata(num_backtracks=0).metadata:
+                break
+            time.sleep(0.2)
+        sess.join_collective_learner({"LearnerID": "localhost-2", "ProjectHome": ".", "Devices": [2],
+                                      "GRPCServicer": {"Hostname": "127.0.0.1", "Port": free_port()}})
+        reason = sess.monitor_federation(request_every_secs=0.3)
+    finally:
+        sess.shutdown_federation(timeout=60)
+    assert reason == "rounds"
+    assert len(sess.regroups) == 1 and sess.regroups[0]["joined"] == ["localhost-2"]
+    md = sess.get_federation_statistics()["federation_runtime_metadata"]["metadata"]
+    last = {}
+    for m in md:
+        last[int(m["global_iteration"])] = m
+    assert sorted(last) == list(range(1, R + 1))
+    assert len(last[R]["completed_by_learner_id"]) == 3

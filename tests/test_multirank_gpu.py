@@ -62,6 +62,17 @@ def test_sync_rounds_over_ranks(nproc):
     assert len(w) == 8 and abs(sum(w) - 1.0) < 1e-6
 
 
+def test_sync_round_with_ckks_over_two_ranks():
+    """BASELINE config 4 shape over 2 ranks: every learner encrypts on the
+    device, the int64 ciphertext all-reduce crosses the ranks, the decrypted
+    community model is identical on both."""
+    out = _torchrun(["bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--train-size", "4096",
+                     "--test-size", "1024", "--local-epochs", "1", "--exact-updates", "0", "--secure-aggregation"])
+    assert out["n_gpus"] == 2 and "CKKS" in out["config"]["aggregation"]
+    cm = out["community_model"]
+    assert cm["identical"], cm
+
+
 @pytest.mark.parametrize("secure", [False, True])
 def test_async_two_ranks_service_thread(secure):
     args = ["benchmarks/async_bench.py", "--gpus", "2", "--learners", "4", "--tasks", "2", "--warmup", "1",
