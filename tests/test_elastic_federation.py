@@ -83,9 +83,11 @@ def _worker(rank, world, port, out_dir, mode):
     comm.close()
 
 
-def _coloc_worker(rank, world, port, out_dir, L, slow, ratio):
+def _coloc_worker(rank, world, port, out_dir, L, slow, ratio, device="cpu"):
     """``L`` co-located learners per rank (global learner g = rank * L + j,
-    shard of 8 + 4 g examples); learner ``slow`` is deliberately slow."""
+    shard of 8 + 4 g examples); learner ``slow`` is deliberately slow.
+    ``device="cuda"``: the ranks share the GPU over host-staged gloo
+    (parallel/comm.py; tests/test_multirank_gpu.py)."""
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
@@ -93,11 +95,16 @@ def _coloc_worker(rank, world, port, out_dir, L, slow, ratio):
     from metisfl_amd.ops.optim import OptimizerSpec
     from metisfl_amd.parallel.comm import Comm
     from metisfl_amd.parallel.federation import CollectiveFederation, FederationConfig
-    comm = Comm(backend="gloo")
+    if device == "cuda":
+        os.environ["MFL_COMM_BACKEND"] = "gloo"
+        comm = Comm()
+        device = comm.device
+    else:
+        comm = Comm(backend="gloo")
     nets, dss = [], []
     for j in range(L):
         g = rank * L + j
-        net = ResNet18(batch_size=4, device="cpu", seed=g + 1, width_mult=0.125,
+        net = ResNet18(batch_size=4, device=device, seed=g + 1, width_mult=0.125,
                        optimizer=OptimizerSpec("momentum_sgd", learning_rate=0.01, momentum=0.9))
         x, y = _shard(g, 8 + 4 * g)
         nets.append(net)
@@ -110,13 +117,13 @@ def _coloc_worker(rank, world, port, out_dir, L, slow, ratio):
 
     def spy(meta, _orig=orig):
         np.save(os.path.join(out_dir, f"local_r{fed.global_iteration}_{rank}.npy"),
-                np.stack([n.state.model32.numpy().copy() for n in nets]))
+                np.stack([n.state.model32.cpu().numpy().copy() for n in nets]))
         return _orig(meta)
     fed.aggregate = spy
     for _ in range(2):
         rec = fed.run_round()
         np.save(os.path.join(out_dir, f"community_r{rec.global_iteration}_{rank}.npy"),
-                np.stack([n.state.model32.numpy().copy() for n in nets]))
+                np.stack([n.state.model32.cpu().numpy().copy() for n in nets]))
         rounds.append({"weights": rec.weights, "participated": rec.learner_meta[:, 10].tolist(),
                        "batches": rec.learner_meta[:, 1].tolist(), "budgets": rec.num_local_updates})
     with open(os.path.join(out_dir, f"res_coloc_{rank}.json"), "w") as f:
@@ -124,9 +131,9 @@ def _coloc_worker(rank, world, port, out_dir, L, slow, ratio):
     comm.close()
 
 
-def _run_coloc(tmp_path, world, L, slow, ratio):
-    mp.start_processes(_coloc_worker, args=(world, _free_port(), str(tmp_path), L, slow, ratio), nprocs=world,
-                       join=True, start_method="spawn")
+def _run_coloc(tmp_path, world, L, slow, ratio, device="cpu"):
+    mp.start_processes(_coloc_worker, args=(world, _free_port(), str(tmp_path), L, slow, ratio, device),
+                       nprocs=world, join=True, start_method="spawn")
     return [json.load(open(tmp_path / f"res_coloc_{r}.json")) for r in range(world)]
 
 

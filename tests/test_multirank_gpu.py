@@ -85,3 +85,14 @@ def test_async_two_ranks_service_thread(secure):
     assert all(n == 2 for n in out["updates_per_learner"]), out["updates_per_learner"]
     assert out["community_model_matches_host"]
     assert ("CKKS PWA" in out["config"]["aggregation"]) == secure
+
+
+def test_straggler_dropped_over_two_gpu_ranks(tmp_path):
+    """Straggler drop with co-located learners on the GPU over 2 ranks: 2 x 2
+    learners on their HIP streams, learner 3 slowed, participation ratio 3/4;
+    every round ends on the 3-learner quorum (the rendezvous store's done key
+    crosses the ranks), the straggler weighs 0 and receives the community
+    model (tests/test_elastic_federation.py's checks)."""
+    from tests.test_elastic_federation import _check_coloc, _run_coloc
+    res = _run_coloc(tmp_path, 2, 2, slow=3, ratio=3 / 4, device="cuda")
+    _check_coloc(tmp_path, res, 2, 2, slow=3)
