@@ -42,7 +42,13 @@ def _torchrun(script_args, nproc=2, timeout=400):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}"] + script_args
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
-    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    if p.returncode != 0:  # shown in the failing test's captured output, and kept in full
+        print("---- stdout ----\n" + p.stdout[-4000:] + "\n---- stderr ----\n" + p.stderr[-12000:])
+        d = os.path.join(ROOT, "gpurun_out", "multirank_failures")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"{os.getpid()}_{_port()}.log"), "w") as f:
+            f.write(" ".join(cmd) + "\n---- stdout ----\n" + p.stdout + "\n---- stderr ----\n" + p.stderr)
+    assert p.returncode == 0, p.returncode
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert lines, p.stdout[-2000:]
     return json.loads(lines[-1])
@@ -67,7 +73,8 @@ def test_sync_round_with_ckks_over_two_ranks():
     device, the int64 ciphertext all-reduce crosses the ranks, the decrypted
     community model is identical on both."""
     out = _torchrun(["bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--train-size", "4096",
-                     "--test-size", "1024", "--local-epochs", "1", "--exact-updates", "0", "--secure-aggregation"])
+                     "--test-size", "1024", "--local-epochs", "1", "--exact-updates", "0", "--secure-aggregation",
+                     "--width-mult", "0.25"])  # (ciphertext size: see the async test)
     assert out["n_gpus"] == 2 and "CKKS" in out["config"]["aggregation"]
     cm = out["community_model"]
     assert cm["identical"], cm
@@ -75,8 +82,10 @@ def test_sync_round_with_ckks_over_two_ranks():
 
 @pytest.mark.parametrize("secure", [False, True])
 def test_async_two_ranks_service_thread(secure):
+    # a quarter-width ResNet-18: the full model's CKKS ciphertext is 1.07 GB,
+    # and every transfer of the rehearsal mode crosses host memory and TCP
     args = ["benchmarks/async_bench.py", "--gpus", "2", "--learners", "4", "--tasks", "2", "--warmup", "1",
-            "--train-size", "4096"]
+            "--train-size", "4096", "--width-mult", "0.25"]
     if secure:
         args.append("--secure-aggregation")
     out = _torchrun(args)
