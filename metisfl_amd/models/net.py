@@ -216,11 +216,20 @@ class StaticNet:
         # destructor frees device memory or destroys an event / stream (another
         # learner's CKKS buffers, a finished task's events) is an illegal call
         # under global-mode capture and aborts the process
+        # thread-local capture mode: other threads of this process keep using
+        # the GPU while a learner captures -- the asynchronous aggregator's
+        # service thread (receives, FedRec kernels, host copies), the
+        # background checkpoint writer -- and under the default global mode
+        # any "unsafe" call of theirs (a synchronous copy, a stream sync, a
+        # device allocation) invalidates this capture
+        # (hipErrorStreamCaptureInvalidated; seen on rank 0 of a 2-rank async
+        # run, tests/test_multirank_gpu.py).  Their work runs on their own
+        # streams, so none of it enters the graph.
         gc.collect()
         was = gc.isenabled()
         gc.disable()
         try:
-            with torch.cuda.graph(g, stream=s):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 body(ds)
         finally:
             if was:

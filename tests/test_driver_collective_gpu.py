@@ -69,7 +69,10 @@ def test_driver_two_ranks_on_one_gpu_sync_and_async(tmp_path, monkeypatch):
     md = stats["federation_runtime_metadata"]["metadata"]
     assert all(len(m["completed_by_learner_id"]) == 4 for m in md)
 
-    sess = _session(tmp_path / "async", 3, rounds=5, protocol="Asynchronous", he=True, devices=[0, 1, 1])
+    # rank 0's learner (no transfer, no wait) is held 0.3 s per task so the
+    # version budget is not spent before rank 1's learners have submitted
+    sess = _session(tmp_path / "async", 3, rounds=8, protocol="Asynchronous", he=True, devices=[0, 1, 1],
+                    extra={"debug_delay_s": {"0": 0.3}})
     stats = sess.run_collective(request_every_secs=0.3)
     assert sess.termination_reason == "rounds", sess.termination_reason
     md = stats["federation_runtime_metadata"]["metadata"]
