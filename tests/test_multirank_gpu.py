@@ -105,3 +105,40 @@ def test_straggler_dropped_over_two_gpu_ranks(tmp_path):
     from tests.test_elastic_federation import _check_coloc, _run_coloc
     res = _run_coloc(tmp_path, 2, 2, slow=3, ratio=3 / 4, device="cuda")
     _check_coloc(tmp_path, res, 2, 2, slow=3)
+
+
+@pytest.mark.parametrize("nproc", [4, 8])
+def test_async_over_more_ranks(nproc):
+    """The asynchronous protocol at 4 / 8 ranks (8 learners: 2 / 1 per rank):
+    rank 0's service thread serves 6 / 7 remote ranks while its own learners
+    capture and replay their graphs."""
+    out = _torchrun(["benchmarks/async_bench.py", "--gpus", str(nproc), "--learners", "8", "--tasks", "2",
+                     "--warmup", "1", "--train-size", "8192", "--width-mult", "0.25"], nproc=nproc)
+    assert out["config"]["learners"] == 8 and out["config"]["learners_per_gpu"] == 8 // nproc
+    assert out["updates"] == 8 * 2
+    assert all(n == 2 for n in out["updates_per_learner"]), out["updates_per_learner"]
+    assert out["community_model_matches_host"]
+
+
+def test_bert_federation_over_two_ranks():
+    """BASELINE config 5's path over 2 ranks (one BERT-base learner each, a
+    few AdamW steps per round): FedAvg of the bf16-trained flat fp32 models
+    through the host-staged all-reduce."""
+    out = _torchrun(["benchmarks/bert_bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--batch", "16",
+                     "--local-steps", "2"])
+    assert out["n_gpus"] == 2
+    assert out["value"] > 0
+
+
+@pytest.mark.parametrize("extra", [["--dtype", "bf16"], ["--checkpoint-every", "1"]], ids=["bf16", "checkpoints"])
+def test_sync_variants_over_two_ranks(extra, tmp_path):
+    """The bf16 option and per-round background checkpoints (device staging,
+    a writer thread per rank while the next round captures / trains) over 2
+    ranks; replicas stay identical."""
+    if extra[0] == "--checkpoint-every":
+        extra = extra + ["--checkpoint-dir", str(tmp_path / "ck")]
+    out = _torchrun(["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--train-size", "8192",
+                     "--test-size", "2048", "--local-epochs", "1", "--exact-updates", "0"] + extra)
+    assert out["community_model"]["identical"], out["community_model"]
+    if extra[0] == "--checkpoint-every":
+        assert os.path.isdir(tmp_path / "ck")
