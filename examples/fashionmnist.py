@@ -4,6 +4,11 @@ learner process per shard (GPU round-robin), FashionMNIST FC on the static
 HIP executor, statistics dumped to experiment.json.
 
     python examples/fashionmnist.py --learners 4 --rounds 5 [--device cpu]
+    python examples/fashionmnist.py --env examples/config/fashionmnist/<config>.yaml [--rounds N]
+
+``--env`` runs one of the federation environment files as written (protocol,
+aggregation rule, CKKS, data plane, device placement, learner count); only
+the ports, dataset paths and, with ``--rounds``, the round budget are set here.
 
 Data is synthetic with FashionMNIST shapes (no network access here); pass
 --npz path/with/x_train,y_train,x_test,y_test arrays to use real data.
@@ -37,18 +42,27 @@ def main():
     ap.add_argument("--gpus", type=int, default=8)
     ap.add_argument("--npz", default="")
     ap.add_argument("--workdir", default="/tmp/metis_amd_fashionmnist")
+    ap.add_argument("--env", default="", help="federation environment YAML (examples/config/fashionmnist/*)")
+    ap.add_argument("--train-size", type=int, default=6000)
     a = ap.parse_args()
     if a.npz:
         with np.load(a.npz, allow_pickle=False) as z:
             xtr, ytr, xte, yte = z["x_train"], z["y_train"], z["x_test"], z["y_test"]
     else:
-        xtr, ytr = synthetic_classification("fashionmnist", 6000, seed=0)
+        xtr, ytr = synthetic_classification("fashionmnist", a.train_size, seed=0)
         xte, yte = synthetic_classification("fashionmnist", 1000, seed=1)
-    xs, ys = DataPartitioning(xtr / max(1.0, float(np.abs(xtr).max())), ytr, a.learners).iid_partition()
+    if a.env:
+        from metisfl_amd.utils.fedenv_parser import FederationEnvironment
+        env = FederationEnvironment(a.env)
+        if "--rounds" in sys.argv:
+            env.termination_signals.federation_rounds = a.rounds
+    else:
+        env = EnvGen(os.path.join(os.path.dirname(__file__), "config", "template.yaml")).generate_localhost(
+            federation_rounds=a.rounds, learners_num=a.learners,
+            gpu_devices=list(range(a.gpus)) if a.device != "cpu" else [-1])
+    n = len(env.learners)
+    xs, ys = DataPartitioning(xtr / max(1.0, float(np.abs(xtr).max())), ytr, n).iid_partition()
     os.makedirs(a.workdir + "_data", exist_ok=True)
-    env = EnvGen(os.path.join(os.path.dirname(__file__), "config", "template.yaml")).generate_localhost(
-        federation_rounds=a.rounds, learners_num=a.learners,
-        gpu_devices=list(range(a.gpus)) if a.device != "cpu" else [-1])
     env.controller.grpc_servicer.port = free_port()
     test_p = os.path.join(a.workdir + "_data", "test.npz")
     np.savez(test_p, x=xte, y=yte)
