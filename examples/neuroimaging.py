@@ -4,6 +4,11 @@ with the 3D CNN as a user PyTorch model (TorchModelDef), trained by learner
 processes through the driver with the fused HIP optimizer.
 
     python examples/neuroimaging.py --learners 2 --rounds 3 [--device cpu] [--dims 2]
+    python examples/neuroimaging.py --env examples/config/brainage/<config>.yaml [--rounds N]
+
+``--env`` runs a federation environment file as written (protocol, rule,
+batch size, local epochs, learner count and placement); ports, dataset paths
+and, with ``--rounds``, the round budget are set here.
 
 Volumes are synthetic with MRI-like shapes (no network / UK Biobank access);
 --shape 91 109 91 gives the reference's full resolution.  As in the
@@ -62,15 +67,22 @@ def main():
     ap.add_argument("--gpus", type=int, default=8)
     ap.add_argument("--workdir", default="/tmp/metis_amd_neuroimaging")
     ap.add_argument("--npz", action="store_true", help="plain .npz shards instead of TFRecords")
+    ap.add_argument("--env", default="", help="federation environment YAML (examples/config/brainage/*, ...)")
     a = ap.parse_args()
     shape = tuple(a.shape or ((32, 32, 32) if a.dims == 3 else (96, 96)))
     model = BrainAge3DCNN() if a.dims == 3 else BrainAge2DCNN()
-    env = EnvGen(os.path.join(os.path.dirname(__file__), "config", "template.yaml")).generate_localhost(
-        federation_rounds=a.rounds, learners_num=a.learners,
-        gpu_devices=list(range(a.gpus)) if a.device != "cpu" else [-1])
+    if a.env:
+        from metisfl_amd.utils.fedenv_parser import FederationEnvironment
+        env = FederationEnvironment(a.env)
+        if "--rounds" in sys.argv:
+            env.termination_signals.federation_rounds = a.rounds
+    else:
+        env = EnvGen(os.path.join(os.path.dirname(__file__), "config", "template.yaml")).generate_localhost(
+            federation_rounds=a.rounds, learners_num=a.learners,
+            gpu_devices=list(range(a.gpus)) if a.device != "cpu" else [-1])
+        env.local_model_config.batch_size = 8
+        env.local_model_config.local_epochs = 1
     env.controller.grpc_servicer.port = free_port()
-    env.local_model_config.batch_size = 8
-    env.local_model_config.local_epochs = 1
     d = a.workdir + "_data"
     os.makedirs(d, exist_ok=True)
     xte, yte = synthetic_volumes(16, shape, seed=999)
