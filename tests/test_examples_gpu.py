@@ -36,3 +36,4 @@ def test_fashionmnist_async_ckks_config_on_gpu(tmp_path):
     log = open(os.path.join(wd, "learner_localhost-1.log")).read()
     line = [l for l in log.splitlines() if l.startswith("[collective-async]")][-1]
     assert "over 10 learners on 1 ranks" in line and "secure PWA over ciphertexts" in line, line
+
