@@ -89,7 +89,8 @@ class Comm:
         dist.send(self._host(t), dst=dst, group=group)
 
     def recv(self, t: torch.Tensor, src: int, group=None) -> None:
-        h = self._host(t)
+        # (staged: a host landing buffer, nothing to copy down first)
+        h = torch.empty(t.shape, dtype=t.dtype) if self.staged and t.is_cuda else t
         dist.recv(h, src=src, group=group)
         self._back(t, h)
 
