@@ -59,7 +59,13 @@ static void launch_mode(float* p, float* g, float* m, float* v, const float* anc
                         hipStream_t s, int* tick_step) {
   const int64_t n4 = n / 4;
   const int64_t z16 = zero ? zero_bytes / 16 : 0;
-  const unsigned grid = stream_grid(n4 > z16 ? n4 : z16, 256, 2048);
+  // MFL_OPT_GRID_CAP: workgroup cap of the grid-stride loop (A/B knob)
+  static const int cap = [] {
+    const char* e = getenv("MFL_OPT_GRID_CAP");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 2048;
+  }();
+  const unsigned grid = stream_grid(n4 > z16 ? n4 : z16, 256, cap);
   uint4* z = reinterpret_cast<uint4*>(zero);
   if (p16 && mirror == 2)
     fused_opt_kernel<MODE, 2><<<grid, 256, 0, s>>>(p, g, m, v, anchor, p16, n4, h, lr_ptr, step_ptr, zg ? 1 : 0,
