@@ -4,7 +4,7 @@ with the 3D CNN as a user PyTorch model (TorchModelDef), trained by learner
 processes through the driver with the fused HIP optimizer.
 
     python examples/neuroimaging.py --learners 2 --rounds 3 [--device cpu] [--dims 2]
-    python examples/neuroimaging.py --env examples/config/brainage/<config>.yaml [--rounds N]
+    python examples/neuroimaging.py --env examples/config/brainage/<config>.yaml [--rounds N] [--data-plane rccl]
 
 ``--env`` runs a federation environment file as written (protocol, rule,
 batch size, local epochs, learner count and placement); ports, dataset paths
@@ -68,6 +68,9 @@ def main():
     ap.add_argument("--workdir", default="/tmp/metis_amd_neuroimaging")
     ap.add_argument("--npz", action="store_true", help="plain .npz shards instead of TFRecords")
     ap.add_argument("--env", default="", help="federation environment YAML (examples/config/brainage/*, ...)")
+    ap.add_argument("--data-plane", default=None, choices=["grpc", "rccl"],
+                    help="override the file's DataPlane: rccl trains the user model on the collective ranks "
+                         "(models/torch_net.py)")
     a = ap.parse_args()
     shape = tuple(a.shape or ((32, 32, 32) if a.dims == 3 else (96, 96)))
     model = BrainAge3DCNN() if a.dims == 3 else BrainAge2DCNN()
@@ -82,6 +85,8 @@ def main():
             gpu_devices=list(range(a.gpus)) if a.device != "cpu" else [-1])
         env.local_model_config.batch_size = 8
         env.local_model_config.local_epochs = 1
+    if a.data_plane:
+        env.data_plane = a.data_plane
     env.controller.grpc_servicer.port = free_port()
     d = a.workdir + "_data"
     os.makedirs(d, exist_ok=True)

@@ -866,6 +866,12 @@ int gb_pipe() {
   return v;
 }
 
+// Slices actually holding k-tiles when ``nk`` k-tiles are dealt ``per`` to a
+// slice: ceil(nk / ceil(nk / sp)) can be < sp (e.g. 500 tiles over 31 slices of
+// 17: slice 30 would start at tile 510).  Split-K launches use this count, so
+// every launched slice writes its slab.
+static int used_splits(int nk, int per) { return per > 0 ? std::max(1, (nk + per - 1) / per) : 1; }
+
 template <bool AT, bool BT, bool OUT32>
 void launch_big(BigGemmArgs p, int kdim, hipStream_t s) {
   static const int dbg = [] {
@@ -940,12 +946,14 @@ void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, 
   if (sp > 1 && K % 8 == 0) {
     // fp32 partials per slice into the slab workspace, one reduce to bf16
     p.c32 = ws; p.ws = ws; p.accum = 0;
-    p.splits = sp;
     p.kt_per_split = (N / GB_KQ + sp - 1) / sp;
+    // slices that own no k-tile would leave their slab unwritten (and the
+    // reduce below would add stale workspace): launch only the slices used
+    p.splits = used_splits(N / GB_KQ, p.kt_per_split);
     launch_big<false, true, true>(p, N, s);
     const int64_t n8 = (int64_t)M * K / 8;
     splitk_reduce_bf16_kernel<<<stream_grid(n8, 256, 2048), 256, 0, s>>>(
-        reinterpret_cast<const float4*>(ws), sp, n8, reinterpret_cast<uint4*>(dx), accumulate ? 1 : 0);
+        reinterpret_cast<const float4*>(ws), p.splits, n8, reinterpret_cast<uint4*>(dx), accumulate ? 1 : 0);
     return;
   }
   p.c16 = dx; p.accum = accumulate;
@@ -990,6 +998,7 @@ void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int
   p.c32 = dw; p.ldc = K; p.accum = accumulate;
   p.splits = wgrad_splits_env(M, N, K);
   p.kt_per_split = (M / GB_KQ + p.splits - 1) / p.splits;
+  p.splits = used_splits(M / GB_KQ, p.kt_per_split);  // no empty slice (slab mode sums every slice)
   if (ws && p.splits > 1 && gemm_big_wgrad_workspace(M, N, K) > 0) {
     p.ws = ws;
     launch_big<true, true, true>(p, M, s);
@@ -1033,7 +1042,8 @@ void launch_gemm_big_wgrad2(const uint16_t* x0, const uint16_t* dy0, float* dw0,
     p.kt_per_split = (M / GB_KQ + sp - 1) / sp;
     return p;
   };
-  const int sp = gemm_big_wgrad2_splits(M, N0, K0, N1, K1);
+  const int sp0 = gemm_big_wgrad2_splits(M, N0, K0, N1, K1);
+  const int sp = used_splits(M / GB_KQ, (M / GB_KQ + sp0 - 1) / sp0);
   BigGemmArgs p0 = args(x0, dy0, dw0, N0, K0, sp), p1 = args(x1, dy1, dw1, N1, K1, sp);
   if (sp > 1) {
     p0.ws = ws;

@@ -304,13 +304,14 @@ class DriverSessionBase:
         in rank order, ``ranks``: the learner indices each process hosts)."""
         env = self.federation_environment
         lm = env.local_model_config
-        if self.neural_engine != "static":
-            raise RuntimeError("the collective data plane runs static-graph models (StaticModelDef)")
+        if self.neural_engine not in ("static", "torch"):
+            raise RuntimeError("the collective data plane runs StaticModelDef / TorchModelDef models")
         learners = list(env.learners) if learners is None else learners
         opt = MM.construct_optimizer_config_pb_from_kwargs(lm.optimizer_config.optimizer_pb_kwargs)
         ts = env.termination_signals
         o = self.collective_options
-        job = {"model_dir": self._model_dir, "batch_size": lm.batch_size, "seed": self.seed,
+        job = {"model_dir": self._model_dir, "model_kind": self.neural_engine,
+               "batch_size": lm.batch_size, "seed": self.seed,
                "optimizer_hex": opt.SerializeToString().hex(),
                "controller_hex": self._controller_entity.SerializeToString().hex(),
                "train_recipe": self.train_dataset_recipe_fp, "test_recipe": self.test_dataset_recipe_fp,

@@ -53,6 +53,31 @@ def _load_recipe(path):
         return cloudpickle.load(f)
 
 
+class _TorchNetDef:
+    """A user TorchModelDef as a collective-plane model factory: each learner
+    gets a TorchNet over its own module (models/torch_net.py)."""
+
+    def __init__(self, model_def):
+        self.model_def = model_def
+
+    def get_model(self, batch_size: int, device="cpu", optimizer=None, seed: int = 0):
+        from metisfl_amd.models.torch_net import TorchNet
+        return TorchNet(self.model_def, batch_size, device=device, optimizer=optimizer, seed=seed)
+
+
+def _load_model_def(job: dict):
+    """The driver's model: a static-family JSON document, or (``model_kind``
+    "torch") the user's cloudpickled TorchModelDef -- the driver's own file,
+    as the reference's learners load the driver's pickled PyTorchDef
+    (pytorch_model_ops.py:52-59)."""
+    if job.get("model_kind", "static") == "torch":
+        import cloudpickle
+        with open(os.path.join(job["model_dir"], "model_def.pkl"), "rb") as f:
+            return _TorchNetDef(cloudpickle.load(f))
+    from metisfl_amd.models.model_def import StaticModelDef
+    return StaticModelDef.load(job["model_dir"])
+
+
 def _inject_fault(rank: int, at: int, fault: dict) -> None:
     """Fault injection (tests): leave now, with exit code EXIT_INJECTED_FAULT
     or -- ``"signal": "KILL"`` -- by SIGKILL, as the kernel's OOM killer
@@ -121,7 +146,6 @@ def _main(argv, ctx: dict) -> int:
     import torch
 
     from metisfl_amd.learner.learner import resolve_dataset
-    from metisfl_amd.models.model_def import StaticModelDef
     from metisfl_amd.ops.optim import OptimizerSpec
     from metisfl_amd.parallel.comm import Comm
     from metisfl_amd.parallel.engine_bridge import RemoteCollectiveController
@@ -141,7 +165,7 @@ def _main(argv, ctx: dict) -> int:
     lcfg = mine[0]
     torch.manual_seed(job.get("seed", 0) + rank)
     opt = OptimizerSpec.from_proto(model_pb2.OptimizerConfig.FromString(bytes.fromhex(job["optimizer_hex"])))
-    model_def = StaticModelDef.load(job["model_dir"])
+    model_def = _load_model_def(job)
     train_recipe, test_recipe = _load_recipe(job.get("train_recipe")), _load_recipe(job.get("test_recipe"))
     nets, train_dss, test_dss = [], [], []
     for lc in mine:

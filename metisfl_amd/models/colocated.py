@@ -49,6 +49,11 @@ class CoLocatedLearners:
                     net.set_throughput_conv(True)
         self._ev = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                      for _ in self.nets] if self.cuda else None)
+        # learners dropped from the last elastic round whose already-issued
+        # chunks may still be running on their streams: the round closed
+        # without waiting for them, so the current stream is NOT ordered after
+        # their streams (``settle`` orders it)
+        self.pending: set[int] = set()
 
     # MFL_COLOC_CUMASK=contig|interleave: confine learner j's stream to its
     # share of the CUs (hipExtStreamCreateWithCUMask) instead of letting every
@@ -112,11 +117,26 @@ class CoLocatedLearners:
             for s in self.streams:
                 s.wait_stream(cur)
 
-    def _join(self) -> None:
+    def _join(self, only=None) -> None:
+        """The current stream waits for the learners' streams (``only``: those
+        learners)."""
         if self.cuda:
             cur = torch.cuda.current_stream(self.device)
-            for s in self.streams:
-                cur.wait_stream(s)
+            for j, s in enumerate(self.streams):
+                if only is None or j in only:
+                    cur.wait_stream(s)
+
+    def settle(self, only=None) -> None:
+        """Order the current stream after the pending (dropped) learners'
+        streams -- before anything on it reads or writes their buffers (their
+        optimizer state for a checkpoint, their models for a test)."""
+        js = set(self.pending) if only is None else set(only) & self.pending
+        if js:
+            self._join(js)
+            self.pending -= js
+
+    def active(self) -> list[int]:
+        return [j for j in range(len(self)) if j not in self.pending]
 
     def train(self, nsteps: list[int], step_offsets: list[int]) -> list[float]:
         """Run ``nsteps[j]`` local updates of every learner concurrently ->
@@ -150,6 +170,7 @@ class CoLocatedLearners:
                         host_ms[j] = (time.perf_counter() - t0) * 1e3
             live = nxt
         self._join()
+        self.pending = set()
         if not self.cuda:
             return host_ms
         for _, e1 in self._ev:
@@ -235,14 +256,25 @@ class CoLocatedLearners:
                 last_poll = now
                 stopped = bool(stop())
             if stopped and all(finished[j] or issued[j] < nsteps[j] for j in range(n)):
-                break  # only dropped learners left (their issued chunks drain in _join)
+                break  # only dropped learners left
             if not progressed:
                 time.sleep(2e-4)
-        self._join()
+        # the round closes on its participants: the current stream joins
+        # only their streams; a dropped learner's chunks already on the
+        # device keep running on its own stream (``pending``), and nothing
+        # of this round waits for them -- the aggregation reads participants
+        # only, ``install`` orders the dropped learner's copy of the
+        # community model after its own chunks, the evaluations skip it
+        # (the deadline is a deadline)
+        done = [j for j in range(n) if finished[j]]
+        self._join(set(done))
+        self.pending = set(range(n)) - set(done)
         ran = list(issued)
         if not self.cuda:
+            self.pending = set()
             return ms, ran, finished
-        torch.cuda.synchronize(self.device)
+        for j in done:
+            self._ev[j][1].synchronize()
         out = []
         for j, (e0, e1) in enumerate(self._ev):
             out.append(e0.elapsed_time(e1) if finished[j] else (time.perf_counter() - t0) * 1e3)
@@ -255,27 +287,56 @@ class CoLocatedLearners:
         self._fork()
         owners = []
         for j, (net, ds) in enumerate(zip(self.nets, dss)):
-            if ds is None:
+            if ds is None or j in self.pending:  # a dropped learner still busy: not evaluated
                 owners.append(None)
                 continue
             with self._ctx(j):
                 owners.append(net.begin_evaluate(ds, max_steps))
-        self._join()
+        self._join(set(self.active()))
         return [net.finish_evaluate(o) if o is not None else None for net, o in zip(self.nets, owners)]
 
     def weighted_sum_into(self, out: torch.Tensor, weights: list[float]) -> None:
         """out = sum_j (fp32)(w_j * model_j) in learner order (the reference's
         FedAvg term rounding, federated_average.cc:14-37; K1, one launch).
-        ``out`` may alias learner 0's model buffer."""
+        ``out`` may alias learner 0's model buffer.
+        Participants only: a learner of weight 0 (dropped from the round) is
+        not read at all -- the reference's selector never hands a
+        non-participant's model to the aggregation
+        (scheduled_cardinality.h:21-29), and 0 * NaN would poison the sum.
+        """
         from metisfl_amd.ops.aggregate import weighted_sum
-        weighted_sum(out, [n.state.model32 for n in self.nets], [float(w) for w in weights])
+        idx = [j for j, w in enumerate(weights) if float(w) != 0.0] or list(range(len(self)))
+        for j, n in enumerate(self.nets):  # ``out`` is a still-busy learner's buffer
+            if j in self.pending and n.state.model32.data_ptr() == out.data_ptr():
+                self.settle([j])
+        weighted_sum(out, [self.nets[j].state.model32 for j in idx], [float(weights[j]) for j in idx])
 
     def install(self, src: torch.Tensor) -> None:
         """Every learner's model <- ``src`` (the community model); mirrors and
-        FedProx anchors follow."""
-        for net in self.nets:
+        FedProx anchors follow.  A pending (dropped, still busy) learner's
+        copy is issued on its own stream after the current stream's work, so
+        it lands after its in-flight chunks without the caller waiting."""
+        cur = torch.cuda.current_stream(self.device) if self.cuda else None
+        for j, net in enumerate(self.nets):
             st = net.state
-            if st.model32.data_ptr() != src.data_ptr():
-                st.model32.copy_(src)
-            st.refresh_bf16()
-            st.set_anchor()
+            ctx = _null()
+            if j in self.pending and self.cuda:
+                self.streams[j].wait_stream(cur)
+                ctx = self._ctx(j)
+            with ctx:
+                if st.model32.data_ptr() != src.data_ptr():
+                    st.model32.copy_(src)
+                st.refresh_bf16()
+                st.set_anchor()
+
+    def reset_train_stats(self) -> None:
+        """Zero every learner's loss / accuracy accumulators (a pending
+        learner's on its own stream, after its in-flight chunks)."""
+        for j, net in enumerate(self.nets):
+            with self._ctx(j) if j in self.pending else _null():
+                net.reset_train_stats()
+
+
+def _null():
+    import contextlib
+    return contextlib.nullcontext()

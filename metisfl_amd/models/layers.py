@@ -435,8 +435,7 @@ class ConvBN(Layer):
             # fp32 launch also carries the next optimizer tail, if any.  The
             # throughput kernels (co-located regime) carry none: the step's
             # last optimizer launch takes the rest
-            tput = (self.ws.throughput and pk and self.xp is not None and self.wp is not None
-                    and K.tconv_shape_ok(s))
+            tput = self.ws.throughput and K.throughput_backward_ok(self.dz, pk, self.xp, self.wp, s)
             opt = None if tput else self.ws.take_opt_tail()
             K.conv_backward_pair(self.x, self.dz, self.dw, self.w16, dx, s,
                                  self.ws.tc_slab if tput else self._split(), accumulate,

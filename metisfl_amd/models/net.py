@@ -67,7 +67,14 @@ class DeviceDataset:
             p = torch.cat([p, torch.full((need - p.numel(),), self.n, dtype=p.dtype)])
         if p.numel() < need:  # last partial batch wraps around
             p = torch.cat([p, p[: need - p.numel()]])
-        self.perm.copy_(p[:need].to(torch.int32), non_blocking=True)
+        p = p[:need].to(torch.int32)
+        if self.perm.is_cuda:
+            # from pinned memory: a pageable host-to-device copy returns only
+            # once the stream has drained up to it, which stalled the host
+            # (and every co-located learner it feeds) at each epoch boundary
+            # until this learner's queued updates had run
+            p = p.pin_memory()
+        self.perm.copy_(p, non_blocking=True)
 
     @property
     def row_shape(self):

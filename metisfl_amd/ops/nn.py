@@ -260,6 +260,15 @@ def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShap
     conv_forward(x, w2, y2, ConvShape(shp.N, shp.H, shp.W, shp.C, shp.Co, 1, 1, 2, 0), ws2, stats2)
 
 
+def throughput_backward_ok(dy, dy_packed: bool, xp, wp, shp: ConvShape) -> bool:
+    """Whether a layer's backward can run the throughput kernels (tconv.hip):
+    packed bf16x3 operands of a 3x3 / stride-1 fp32 layer.  The one predicate
+    both the caller (which picks the workspace and optimizer tail) and
+    :func:`conv_backward_pair` (which picks the kernel) use."""
+    return (dy.is_cuda and dy.dtype == torch.float32 and bool(dy_packed) and xp is not None
+            and wp is not None and conv_products() == "bf16x3" and tconv_shape_ok(shp))
+
+
 def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
                        bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False, xp=None,
                        opt=None, counters=None, throughput: bool = False) -> None:
@@ -275,8 +284,7 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
     regime): 3x3 / stride-1 layers with packed operands run the throughput
     kernels instead (``counters``: their split-K arrival tickets, int32, zero
     between launches)."""
-    if (throughput and dy.is_cuda and dy.dtype == torch.float32 and dy_packed and xp is not None
-            and wp is not None and conv_products() == "bf16x3" and tconv_shape_ok(shp)):
+    if throughput and throughput_backward_ok(dy, dy_packed, xp, wp, shp):
         f = (bnb.z, bnb.y, bnb.mean, bnb.invstd, bnb.acc) if bnb is not None else (None,) * 5
         ops().tconv_backward(xp, dy, dw, wp, dx, ws, counters, *shp.args(), accumulate, *f)
         if opt is not None:

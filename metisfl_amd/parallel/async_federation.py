@@ -351,8 +351,22 @@ class AsyncCollectiveFederation:
         st = L.net.state
         st.refresh_bf16()
         st.set_anchor()
+        self._order(L)
+
+    def _order(self, L: _Local) -> None:
+        """Learner L's stream waits for the work issued so far on the current
+        stream: the community model copy, its bf16 / packed mirrors and FedProx
+        anchor (``_install``), and the device-to-device staging of a learner
+        checkpoint -- all issued outside ``_ctx(L)``.  Without it the
+        learner's next graph replay (evaluation of the received model, its
+        next task) could read a stale mirror or anchor, or overwrite m / v
+        before the checkpoint copy read them."""
+        s = self.streams[L.j]
+        if s is not None and self.cuda:
+            s.wait_stream(torch.cuda.current_stream(L.net.state.model32.device))
 
     def _start_task(self, L: _Local) -> None:
+        self._order(L)  # after a checkpoint staged on the current stream (after_task)
         with self._ctx(L):
             L.net.reset_train_stats()
             L.gen = L.net.train_steps_iter(L.train_ds, L.num_local_updates, step_offset=L.steps_done)
@@ -653,6 +667,9 @@ class AsyncCollectiveFederation:
         self.last[g].copy_(theta)
         self.last_w[g] = w
         self.version += 1
+        k = int(getattr(self.cfg, "fedrec_resum_every", 0) or 0)
+        if k and self.version % k == 0:
+            self._resum()
         if theta.is_cuda:  # this thread's stream only: the learners keep running on theirs
             torch.cuda.current_stream(theta.device).synchronize()
         up = AsyncUpdate(g, int(meta["task"]), w, time.time(), (time.perf_counter() - t0) * 1e3,
@@ -665,6 +682,21 @@ class AsyncCollectiveFederation:
             # sent by the bookkeeping thread, not under the aggregator lock
             self._bookkeep("update", self.version, g, meta, up)
         self._after_fedrec()
+
+    def _resum(self) -> None:
+        """S <- sum_g w_g theta_g and Z <- sum_g w_g, recomputed from every
+        learner's last contribution (one K1 launch over the resident models;
+        Z with exact fp64 summation): the rounding the incremental FedRec
+        updates accumulated (S -= w_old theta_old; S += w_new theta_new, in
+        fp32, every version) is dropped.  Secure aggregation keeps no running
+        sum (the PWA runs over the latest ciphertexts)."""
+        import math
+        idx = [g for g in range(self.G) if self.last[g] is not None]
+        if not idx:
+            return
+        self.Z = math.fsum(self.last_w[g] for g in idx)
+        if not self.secure:
+            agg.weighted_sum(self.S, [self.last[g] for g in idx], [self.last_w[g] for g in idx])
 
     def _community(self) -> torch.Tensor:
         """The community model as rank 0 hands it out: S / Z, or (secure
@@ -793,19 +825,37 @@ class AsyncCollectiveFederation:
             self._checkpoint_aggregator(block=False)
         # (secure aggregation: the aggregator holds no plaintext model to hand
         # to the controller's lineage)
-        if self.engine is not None and self.snapshot_every and v % self.snapshot_every == 0 \
-                and not self.secure and hasattr(self.engine, "snapshot_community"):
-            from metisfl_amd.parallel import checkpoint as ck
-            if self._lineage is None:
-                self._lineage = ck.AsyncSnapshot(self.S.device, "metisfl-async-lineage")
-            st, engine, z = self.net.state, self.engine, float(self.Z)
+        if self.snapshot_every and v % self.snapshot_every == 0:
+            self._snapshot_community(block=False)
 
-            def write(h):
-                flat = (h["S"].double() / z).float().numpy()
-                engine.snapshot_community([sp.name for sp in st.specs],
-                                          [flat[sp.offset: sp.offset + sp.numel].reshape(sp.shape) for sp in st.specs],
-                                          [sp.trainable for sp in st.specs], v)
-            self._lineage.try_submit({"S": self.S}, write)
+    _snap_sent = -1  # rank 0: last community version handed to the controller's lineage
+
+    def _snapshot_community(self, block: bool) -> None:
+        """Rank 0 (under the lock): hand community version ``self.version``
+        to the controller's lineage, staged device-to-device and sent from a
+        background thread.  Latest wins while a send is in flight
+        (``block=False`` skips the version); ``flush`` re-sends the final
+        version when it was skipped, as the synchronous path's
+        ``flush_checkpoints`` does."""
+        if self.engine is None or self.secure or not hasattr(self.engine, "snapshot_community"):
+            return
+        from metisfl_amd.parallel import checkpoint as ck
+        if self._lineage is None:
+            self._lineage = ck.AsyncSnapshot(self.S.device, "metisfl-async-lineage")
+        st, engine, z, v = self.net.state, self.engine, float(self.Z), self.version
+        if v == self._snap_sent or z == 0.0:
+            return
+
+        def write(h):
+            flat = (h["S"].double() / z).float().numpy()
+            engine.snapshot_community([sp.name for sp in st.specs],
+                                      [flat[sp.offset: sp.offset + sp.numel].reshape(sp.shape) for sp in st.specs],
+                                      [sp.trainable for sp in st.specs], v)
+        if block:
+            self._lineage.submit({"S": self.S}, write)
+        elif self._lineage.try_submit({"S": self.S}, write) is None:
+            return
+        self._snap_sent = v
 
     def _checkpoint_aggregator(self, block: bool = False) -> None:
         from metisfl_amd.parallel import checkpoint as ck
@@ -884,6 +934,9 @@ class AsyncCollectiveFederation:
             L.lckpt.try_submit(tensors, write)
 
     def flush(self) -> None:
+        if self.rank == 0 and self._lineage is not None and self.snapshot_every:
+            with self._lock:  # the final community version, if its snapshot was skipped
+                self._snapshot_community(block=True)
         for w in [self._ckpt, self._lineage] + [L.lckpt for L in self.learners]:
             if w is not None:
                 w.wait()

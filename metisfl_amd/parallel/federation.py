@@ -90,6 +90,12 @@ class FederationConfig:
     staleness: str = "none"
     staleness_a: float = 0.5
     staleness_b: int = 4
+    # asynchronous protocol: every ``fedrec_resum_every`` community versions
+    # the aggregator re-sums S = sum_g w_g theta_g from every learner's last
+    # contribution (resident in HBM; one K1 launch) instead of carrying the
+    # fp32 subtract / add running sum forever (0: never, the reference's
+    # behaviour, federated_recency.cc:8-100)
+    fedrec_resum_every: int = 32
     secure_aggregation: bool = False
     he_batch_size: int = 4096
     he_scaling_bits: int = 52
@@ -302,8 +308,11 @@ class CollectiveFederation:
             self.net.state.set_anchor()
 
     def _sync(self):
+        """Wait for the current stream (every learner stream the round joined
+        into it; not a dropped learner's chunks still in flight on its own
+        stream, models/colocated.py ``pending``)."""
         if self.comm.device.type == "cuda":
-            torch.cuda.synchronize(self.comm.device)
+            torch.cuda.current_stream(self.comm.device).synchronize()
 
     @property
     def elastic(self) -> bool:
@@ -385,8 +394,7 @@ class CollectiveFederation:
         their own streams when co-located) -> one result dict per learner."""
         if self.L == 1:
             return [self.local_train(nsteps[0])]
-        for net in self.nets:
-            net.reset_train_stats()
+        self.group.reset_train_stats()
         part = [True] * self.L
         with tracing.range("metisfl.local_train"):
             if self.elastic:
@@ -396,7 +404,10 @@ class CollectiveFederation:
         out = []
         for j, (net, ran) in enumerate(zip(self.nets, nsteps)):
             self.steps_done_l[j] += ran
-            tr = net.train_stats()
+            # a dropped learner's statistics are still being accumulated on
+            # its stream: it completed no task this round (no train metrics)
+            tr = net.train_stats() if j not in self.group.pending else {"loss": float("nan"),
+                                                                        "accuracy": float("nan")}
             spe = self._spes[j]
             out.append({"ms": ms[j], "ms_per_batch": ms[j] / max(1, ran), "ms_per_epoch": ms[j] / max(1, ran) * spe,
                         "completed_batches": ran, "completed_epochs": ran / spe,
@@ -512,6 +523,8 @@ class CollectiveFederation:
         if self.L > 1:
             wl = [weights[i] for i in self.local_learners()]
             if self.cfg.secure_aggregation and self.he_dev is not None:
+                self.group.settle([0])  # the output buffer is learner 0's model
+                parts = [j for j, w in enumerate(wl) if w != 0.0] or list(range(self.L))
                 # every co-located learner encrypts its own model; the weighted
                 # ciphertexts are summed on the device, then all-reduced
                 with tracing.range("metisfl.secure_allreduce"):
@@ -519,9 +532,10 @@ class CollectiveFederation:
                         self._he_ct = torch.empty(self.he_dev.ct_numel(st.model32.numel()),
                                                   dtype=torch.int64, device=self.comm.device)
                         self._he_tmp = torch.empty_like(self._he_ct)
+                    # participants only (a dropped learner's model is never read)
                     self.last_he_stats = self.he_dev.secure_weighted_allreduce_many(
-                        self.comm, [n.state.model32 for n in self.nets], wl, st.model32, ct=self._he_ct,
-                        tmp=self._he_tmp)
+                        self.comm, [self.nets[j].state.model32 for j in parts], [wl[j] for j in parts],
+                        st.model32, ct=self._he_ct, tmp=self._he_tmp)
                 self.last_allreduce_ms = self.last_he_stats["allreduce_ms"]
                 self._install_local(st.model32)
                 self._sync()
@@ -717,6 +731,8 @@ class CollectiveFederation:
         next round runs.  -> milliseconds the call held this rank."""
         from metisfl_amd.parallel import checkpoint as ck
         t_prep = time.perf_counter()
+        if self.group is not None:
+            self.group.settle()  # dropped learners' optimizer state is final once their chunks land
         if self._ckpt is None:
             self._ckpt = ck.AsyncSnapshot(self.comm.device, "metisfl-checkpoint")
         gi = self.global_iteration

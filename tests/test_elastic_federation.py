@@ -83,7 +83,7 @@ def _worker(rank, world, port, out_dir, mode):
     comm.close()
 
 
-def _coloc_worker(rank, world, port, out_dir, L, slow, ratio, device="cpu"):
+def _coloc_worker(rank, world, port, out_dir, L, slow, ratio, device="cpu", poison=False):
     """``L`` co-located learners per rank (global learner g = rank * L + j,
     shard of 8 + 4 g examples); learner ``slow`` is deliberately slow.
     ``device="cuda"``: the ranks share the GPU over host-staged gloo
@@ -116,6 +116,10 @@ def _coloc_worker(rank, world, port, out_dir, L, slow, ratio, device="cpu"):
     rounds = []
 
     def spy(meta, _orig=orig):
+        if poison and fed.group is not None and rank * L <= slow < (rank + 1) * L:
+            # the straggler's model went non-finite: it must not reach the sum
+            fed.group.settle([slow - rank * L])
+            nets[slow - rank * L].state.model32.fill_(float("nan"))
         np.save(os.path.join(out_dir, f"local_r{fed.global_iteration}_{rank}.npy"),
                 np.stack([n.state.model32.cpu().numpy().copy() for n in nets]))
         return _orig(meta)
@@ -131,8 +135,8 @@ def _coloc_worker(rank, world, port, out_dir, L, slow, ratio, device="cpu"):
     comm.close()
 
 
-def _run_coloc(tmp_path, world, L, slow, ratio, device="cpu"):
-    mp.start_processes(_coloc_worker, args=(world, _free_port(), str(tmp_path), L, slow, ratio, device),
+def _run_coloc(tmp_path, world, L, slow, ratio, device="cpu", poison=False):
+    mp.start_processes(_coloc_worker, args=(world, _free_port(), str(tmp_path), L, slow, ratio, device, poison),
                        nprocs=world, join=True, start_method="spawn")
     return [json.load(open(tmp_path / f"res_coloc_{r}.json")) for r in range(world)]
 
@@ -150,7 +154,8 @@ def _check_coloc(tmp_path, res, world, L, slow):
         comm = [np.load(tmp_path / f"community_r{gi}_{r}.npy") for r in range(world)]
         # every learner (the straggler too) holds the participants' average
         assert all(np.array_equal(comm[0][0], c[j]) for c in comm for j in range(L))
-        assert np.allclose(comm[0][0], np.tensordot(w, locs, axes=1), rtol=1e-5, atol=1e-6)
+        assert np.isfinite(comm[0][0]).all()
+        assert np.allclose(comm[0][0], np.tensordot(w[keep], locs[keep], axes=1), rtol=1e-5, atol=1e-6)
 
 
 def test_straggler_dropped_among_colocated_learners(tmp_path):
@@ -165,6 +170,15 @@ def test_straggler_dropped_among_colocated_learners(tmp_path):
 def test_straggler_dropped_in_a_one_process_colocated_federation(tmp_path):
     """The same on one rank hosting 3 learners (quorum counted in-process)."""
     res = _run_coloc(tmp_path, 1, 3, slow=1, ratio=2 / 3)
+    _check_coloc(tmp_path, res, 1, 3, slow=1)
+
+
+def test_dropped_nonfinite_learner_does_not_poison_the_community(tmp_path):
+    """VERDICT r5 #5a: a dropped co-located learner whose model went NaN
+    leaves a finite community model equal to the participants-only FedAvg
+    (the weighted sum reads participants only; the reference's selector never
+    hands a non-participant to the aggregation, scheduled_cardinality.h:21-29)."""
+    res = _run_coloc(tmp_path, 1, 3, slow=1, ratio=2 / 3, poison=True)
     _check_coloc(tmp_path, res, 1, 3, slow=1)
 
 

@@ -140,3 +140,22 @@ def test_grouped_wgrad_pair(M):
     dw0b, dw1b = torch.zeros_like(dw0), torch.zeros_like(dw1)
     _ops().gemm_wgrad2(x0, dy0, dw0b, H, H, x1, dy1, dw1b, 3 * H, H, M)
     assert torch.equal(dw0, dw0b) and torch.equal(dw1, dw1b)
+
+
+def test_dgrad_split_k_uneven_slices():
+    """A split-K dgrad whose slice count does not divide the k-tiles: a
+    32,000-word vocabulary at M = 512, K = 768 gives 31 slices of 17 k-tiles
+    over 500, so a 31st slice would own none.  The launch must use only the
+    slices that hold tiles; the workspace is poisoned with NaN first (the
+    caching allocator hands the freed block back), so a slab left unwritten
+    shows up in dx."""
+    M, N, K = 512, 32000, 768
+    g = torch.Generator(device="cuda").manual_seed(5)
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.05).bfloat16()
+    dx = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+    poison = torch.full((40 * M * K,), float("nan"), device="cuda")
+    del poison
+    _ops().gemm_dgrad(dy, w, dx, M, N, K, False)
+    assert torch.isfinite(dx.float()).all()
+    assert _rel(dx, dy.float() @ w.float()) < 1e-2

@@ -142,3 +142,17 @@ def test_sync_variants_over_two_ranks(extra, tmp_path):
     assert out["community_model"]["identical"], out["community_model"]
     if extra[0] == "--checkpoint-every":
         assert os.path.isdir(tmp_path / "ck")
+
+
+@pytest.mark.parametrize("model", ["brainage3d", "ionosphere"])
+def test_torch_model_federation_over_two_ranks(model):
+    """a user TorchModelDef (the BrainAge 3D CNN, the
+    Ionosphere MLP) federated over 2 host-staged ranks x 2 co-located
+    learners on the GPU (models/torch_net.py): the community replicas are
+    bitwise identical on both ranks and the round weights sum to 1."""
+    out = _torchrun(["benchmarks/torch_model_bench.py", "--gpus", "2", "--learners", "4", "--model", model,
+                     "--rounds", "2", "--samples", "16"])
+    assert out["n_gpus"] == 2 and out["learners_per_gpu"] == 2
+    cm = out["community_model"]
+    assert len(cm["sha256_128"]) == 2 and cm["identical"], cm
+    assert abs(sum(out["last_round_weights"]) - 1.0) < 1e-9
