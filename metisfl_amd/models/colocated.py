@@ -221,11 +221,18 @@ class CoLocatedLearners:
                 if self.cuda:
                     ev = torch.cuda.Event()
                     ev.record()
+                    if issued[j] >= nsteps[j]:
+                        # the end marker goes in right behind the last chunk:
+                        # recorded later (at finish), it would queue behind
+                        # whatever a co-located straggler issued meanwhile on
+                        # a shared hardware queue (4 per process), and the
+                        # round would wait for the straggler through it
+                        self._ev[j][1].record()
                 inflight[j].append((ev, issued[j]))
 
         def finish(j: int) -> None:
             finished[j] = True
-            if self.cuda:
+            if self.cuda and issued[j] == 0:  # an empty budget: no chunk carried the end marker
                 with self._ctx(j):
                     self._ev[j][1].record()
             ms[j] = (time.perf_counter() - t0) * 1e3
@@ -267,7 +274,10 @@ class CoLocatedLearners:
         # community model after its own chunks, the evaluations skip it
         # (the deadline is a deadline)
         done = [j for j in range(n) if finished[j]]
-        self._join(set(done))
+        if self.cuda:  # on the end markers (not a fresh marker behind a straggler's chunks)
+            cur = torch.cuda.current_stream(self.device)
+            for j in done:
+                cur.wait_event(self._ev[j][1])
         self.pending = set(range(n)) - set(done)
         ran = list(issued)
         if not self.cuda:
