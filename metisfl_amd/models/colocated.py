@@ -138,10 +138,17 @@ class CoLocatedLearners:
     def active(self) -> list[int]:
         return [j for j in range(len(self)) if j not in self.pending]
 
-    def train(self, nsteps: list[int], step_offsets: list[int]) -> list[float]:
+    def train(self, nsteps: list[int], step_offsets: list[int], eval_dss: list | None = None,
+              eval_max_steps: int | None = None):
         """Run ``nsteps[j]`` local updates of every learner concurrently ->
         per-learner milliseconds from the common start to that learner's last
-        update (its wall-clock share of the co-located run)."""
+        update (its wall-clock share of the co-located run).
+
+        ``eval_dss``: each learner then evaluates its model on ``eval_dss[j]``
+        (the reference learner's test evaluation at task end,
+        keras_model_ops.py:174-176), issued on its stream right behind its
+        last update -- an early finisher's evaluation overlaps the others'
+        training -> (ms, [metrics or None per learner])."""
         import time
         # capture before the streams run concurrently (a capture synchronises
         # the device)
@@ -157,6 +164,7 @@ class CoLocatedLearners:
                 for net, ds, n, off in zip(self.nets, self.train_dss, nsteps, step_offsets)]
         live = list(range(len(gens)))
         host_ms = [0.0] * len(gens)
+        owners = [None] * len(gens)
         while live:
             nxt = []
             for j in live:
@@ -168,14 +176,20 @@ class CoLocatedLearners:
                         if self.cuda:
                             self._ev[j][1].record()
                         host_ms[j] = (time.perf_counter() - t0) * 1e3
+                        if eval_dss is not None and eval_dss[j] is not None:
+                            owners[j] = self.nets[j].begin_evaluate(eval_dss[j], eval_max_steps)
             live = nxt
         self._join()
         self.pending = set()
-        if not self.cuda:
-            return host_ms
-        for _, e1 in self._ev:
-            e1.synchronize()
-        return [e0.elapsed_time(e1) for e0, e1 in self._ev]
+        if self.cuda:
+            for _, e1 in self._ev:
+                e1.synchronize()
+            ms = [e0.elapsed_time(e1) for e0, e1 in self._ev]
+        else:
+            ms = host_ms
+        if eval_dss is None:
+            return ms
+        return ms, [n.finish_evaluate(o) if o is not None else None for n, o in zip(self.nets, owners)]
 
     def train_elastic(self, nsteps: list[int], step_offsets: list[int], stop, on_finish, poll_steps: int = 64,
                       slow_s: list[float] | None = None, poll_s: float = 0.005):

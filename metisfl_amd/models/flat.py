@@ -207,6 +207,36 @@ class FlatState:
         if self.anchor is not None:
             self.anchor.copy_(self.params32)
 
+    def detached_copy(self) -> "FlatState":
+        """A state of the same layout with its OWN model buffers (fp32 master
+        and compute mirror) and no optimizer: a frozen snapshot a forward-only
+        model binds to (the deferred community evaluation evaluates the
+        round's community model on it while the learners already train the
+        next round).  The gradient buffer is shared: a forward pass never
+        writes it."""
+        import copy
+        c = copy.copy(self)
+        c.model32 = self.model32.clone()
+        c.params32 = c.model32[: self.n_params]
+        c.p16 = self.p16.clone() if self.p16 is not None else None
+        c.psplit = self.psplit.clone() if self.psplit is not None else None
+        c.anchor = c.m = c.v = None
+        c.optimizer = None
+        c.step = self.step.clone()
+        c.lr_scale = self.lr_scale.clone()
+        return c
+
+    def copy_model_from(self, src: "FlatState") -> None:
+        """model32 and its compute mirror <- ``src``'s (same layout; on the
+        current stream)."""
+        self.model32.copy_(src.model32)
+        if self.p16 is not None and src.p16 is not None:
+            self.p16.copy_(src.p16)
+        if self.psplit is not None and src.psplit is not None:
+            self.psplit.copy_(src.psplit)
+        elif self.psplit is not None or self.p16 is not None:
+            self.refresh_bf16()
+
     # ---- variable export / import (Model proto boundary) ---------------------
     def named_variables(self):
         for s in self.specs:

@@ -345,9 +345,10 @@ class StaticNet:
             eb //= 2
         return eb
 
-    def _make_eval_twin(self, batch: int) -> "StaticNet | None":
-        """A model of the same architecture at ``batch`` sharing ``self.state``
-        (models opt in; None: evaluate at the training batch)."""
+    def _make_eval_twin(self, batch: int, state: FlatState | None = None) -> "StaticNet | None":
+        """A model of the same architecture at ``batch`` bound to
+        ``self.state`` (or ``state``: a detached copy of it) -- models opt in;
+        None: evaluate at the training batch."""
         return None
 
     def _eval_view(self, ds: DeviceDataset):
@@ -365,6 +366,19 @@ class StaticNet:
             hit = (ds, DeviceDataset(ds.x[:ds.n], ds.y[:ds.n], EB, shuffle=False, pad_tail=True))
             self._eval_views[id(ds)] = hit
         return twin, hit[1]
+
+    def detached_evaluator(self, ds: DeviceDataset, state: FlatState):
+        """(model, dataset view) evaluating ``ds`` on ``state`` -- a
+        ``FlatState.detached_copy`` of this model's state -- with the
+        evaluation twin this model would use, or None when the model has no
+        twin (then evaluation stays on the live model)."""
+        if not (self.use_graphs() and ds.pad_tail and not ds.shuffle):
+            return None
+        eb = self._pick_eval_batch(ds.n) if ds.n > self.B else self.B
+        twin = self._make_eval_twin(eb, state=state)
+        if twin is None:
+            return None
+        return twin, DeviceDataset(ds.x[:ds.n], ds.y[:ds.n], eb, shuffle=False, pad_tail=True)
 
     def begin_evaluate(self, ds: DeviceDataset, max_steps: int | None = None):
         """Issue a loss / accuracy pass over ``ds`` (BN in inference mode) on

@@ -64,10 +64,11 @@ class ResNet18(StaticNet):
         self.num_classes = num_classes
         super().__init__(batch_size, device, optimizer, seed, shared_state=shared_state)
 
-    def _make_eval_twin(self, batch: int):
+    def _make_eval_twin(self, batch: int, state=None):
         dtype = next(k for k, v in DTYPES.items() if v == self.compute_dtype)
         return ResNet18(batch_size=batch, device=self.device, dtype=dtype, conv_products=self.conv_products,
-                        width_mult=self.width_mult, num_classes=self.num_classes, shared_state=self.state)
+                        width_mult=self.width_mult, num_classes=self.num_classes,
+                        shared_state=self.state if state is None else state)
 
     def build(self):
         N = self.B

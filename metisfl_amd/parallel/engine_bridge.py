@@ -95,6 +95,17 @@ class CollectiveController:
             self.engine.record_community_evaluation(rec.global_iteration, ids, evs)
         return False
 
+    def record_evaluations(self, global_iteration: int, community_eval: list) -> None:
+        """A round's community-model evaluations recorded after the round (the
+        deferred evaluation, FederationConfig.defer_community_eval)."""
+        ids = [self.ids[i] for i, e in enumerate(community_eval) if e.get("num_examples") and i < len(self.ids)]
+        evs = [self._model_evaluations(e) for e in community_eval if e.get("num_examples")]
+        if ids:
+            self._record_evaluations(int(global_iteration), ids, evs)
+
+    def _record_evaluations(self, gi: int, ids: list, evs: list) -> None:
+        self.engine.record_community_evaluation(gi, ids, evs)
+
     # -- asynchronous collective federation (async_federation.run_until) ---------------
     def _async_args(self, version: int, r: int, meta: dict, up):
         row = [meta.get("n_train", 0), meta["batches"], meta.get("ms_per_batch", 0.0), meta.get("ms_per_epoch", 0.0),
@@ -200,6 +211,11 @@ class RemoteCollectiveController(CollectiveController):
             "agg_started_ns": ag0, "agg_completed_ns": ag1,
             "meta": base64.b64encode(self._task_meta(row, batch_size)).decode()})
         self._stop_seen = getattr(self, "_stop_seen", False) or bool(resp.get("stop", False))
+
+    def _record_evaluations(self, gi: int, ids: list, evs: list) -> None:
+        import base64
+        self._cs.call(self._ch, "RecordEvaluation", {"global_iteration": gi, "ids": list(ids),
+                                                     "evaluations": [base64.b64encode(e).decode() for e in evs]})
 
     def record_async_evaluation(self, ev: dict) -> None:
         import base64

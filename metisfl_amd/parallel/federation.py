@@ -74,6 +74,13 @@ class FederationConfig:
     # the all-reduce (the reference's SendEvaluationTasks, controller.cc:469-485,
     # 571-587); rank 0 records the CommunityModelEvaluation with the round
     evaluate_community: bool = True
+    # the community evaluation runs in the background, on a frozen copy of
+    # the community model, while the learners train the next round (the
+    # reference's evaluation is asynchronous too: SendEvaluationTasks is
+    # dispatched after the round and digested by its own completion-queue
+    # thread, controller.cc:469-485, 589-694); its results are recorded with
+    # their round once complete (next round's end, or finish_evaluations)
+    defer_community_eval: bool = False
     eval_max_steps: int | None = None
     # rank 0 hands the community model to the controller's lineage every
     # ``snapshot_every`` rounds (0: never; background thread, see
@@ -204,6 +211,64 @@ def setup_ckks(comm: Comm, cfg: FederationConfig):
     return scheme, d
 
 
+class DeferredCommunityEval:
+    """The community model's evaluation on every local learner's test shard,
+    run on its own stream over a FROZEN copy of the model (``FlatState.
+    detached_copy``), so the learners train the next round meanwhile.  One
+    snapshot serves all co-located learners (they hold the same community
+    model); each learner's shard is evaluated by a model of its architecture
+    bound to the snapshot (its evaluation twin)."""
+
+    def __init__(self, nets: list, test_dss: list):
+        self.src = nets[0].state
+        self.state = self.src.detached_copy()
+        self.evals = [n.detached_evaluator(d, self.state) if d is not None else None
+                      for n, d in zip(nets, test_dss)]
+        self.stream = torch.cuda.Stream(device=self.src.model32.device)
+        self.event = torch.cuda.Event()
+        self.pending = None  # (global_iteration, owners)
+
+    @classmethod
+    def build(cls, nets: list, test_dss: list):
+        """None when a learner's model has no detached evaluator (models
+        without evaluation twins, CPU runs): evaluation stays synchronous."""
+        if not nets or nets[0].state.model32.device.type != "cuda" or not hasattr(nets[0], "detached_evaluator"):
+            return None
+        if all(d is None for d in test_dss):
+            return None
+        ev = cls(nets, test_dss)
+        if any(e is None for e, d in zip(ev.evals, test_dss) if d is not None):
+            return None
+        return ev
+
+    def submit(self, global_iteration: int, max_steps: int | None = None) -> None:
+        """Snapshot the community model (current stream order) and issue the
+        evaluations on the side stream; no host wait."""
+        assert self.pending is None, "collect the previous evaluation first"
+        cur = torch.cuda.current_stream(self.src.model32.device)
+        self.stream.wait_stream(cur)
+        owners = []
+        with torch.cuda.stream(self.stream):
+            self.state.copy_model_from(self.src)
+            for e in self.evals:
+                owners.append(None if e is None else e[0].begin_evaluate(e[1], max_steps))
+            self.event.record()
+        self.pending = (global_iteration, owners)
+
+    def collect(self):
+        """-> (global_iteration, [metrics or None per local learner]) of the
+        submitted evaluation (waits for it), or None."""
+        if self.pending is None:
+            return None
+        gi, owners = self.pending
+        self.pending = None
+        self.event.synchronize()
+        out = []
+        for e, o in zip(self.evals, owners):
+            out.append(None if o is None else e[0].finish_evaluate(o))
+        return gi, out
+
+
 class CollectiveFederation:
     """Drives rounds for the learner(s) hosted by this rank.
 
@@ -265,6 +330,7 @@ class CollectiveFederation:
         self.last_he_stats: dict = {}
         if cfg.secure_aggregation:
             self._setup_he()
+        self._ce = None  # DeferredCommunityEval, built at the first deferred evaluation
         if broadcast_initial:
             self.broadcast_initial_model()
 
@@ -396,9 +462,14 @@ class CollectiveFederation:
             return [self.local_train(nsteps[0])]
         self.group.reset_train_stats()
         part = [True] * self.L
+        tests = None
         with tracing.range("metisfl.local_train"):
             if self.elastic:
                 ms, nsteps, part = self._train_elastic_group(nsteps, time.perf_counter())
+            elif self.cfg.evaluate_test:
+                # each learner's test evaluation right behind its own last update
+                ms, tests = self.group.train(list(nsteps), list(self.steps_done_l), eval_dss=self.test_dss,
+                                             eval_max_steps=self.cfg.eval_max_steps)
             else:
                 ms = self.group.train(list(nsteps), list(self.steps_done_l))
         out = []
@@ -413,8 +484,9 @@ class CollectiveFederation:
                         "completed_batches": ran, "completed_epochs": ran / spe,
                         "train_loss": tr["loss"], "train_accuracy": tr["accuracy"], "participated": bool(part[j])})
         if self.cfg.evaluate_test:
-            with tracing.range("metisfl.evaluate"):
-                tests = self.group.evaluate(max_steps=self.cfg.eval_max_steps)
+            if tests is None:
+                with tracing.range("metisfl.evaluate"):
+                    tests = self.group.evaluate(max_steps=self.cfg.eval_max_steps)
             for o, t in zip(out, tests):
                 if t is not None:
                     o["test"] = t
@@ -594,14 +666,67 @@ class CollectiveFederation:
         lengths = [e - b for b, e in segs]
         return zeros, [n * 4 for n in lengths], lengths
 
+    def _deferred_eval(self) -> "DeferredCommunityEval | None":
+        if not self.cfg.defer_community_eval:
+            return None
+        if self._ce is None:  # collective decision: every rank defers, or none does
+            ce = DeferredCommunityEval.build(self.nets, self.test_dss)
+            ok = torch.tensor([1.0 if ce is not None else 0.0], dtype=torch.float64, device=self.comm.device)
+            if self.comm.distributed:
+                ok = self.comm.all_gather_rows(ok).min(0).values
+            self._ce = ce if float(ok[0]) > 0.5 else False
+        return self._ce or None
+
+    def _collect_community_eval(self) -> None:
+        """Collective.  Record the deferred evaluation of an earlier round
+        (all-gathered over the ranks) with that round."""
+        ce = self._ce or None
+        got = ce.collect() if ce is not None else None  # every rank submits and collects in lockstep
+        if got is None:
+            return
+        gi, evs = got
+        out = self._community_rows(evs)
+        rec = next((r for r in reversed(self.history) if r.global_iteration == gi), None)
+        if rec is not None:
+            rec.community_eval = out
+        if self.engine is not None and out and hasattr(self.engine, "record_evaluations"):
+            self.engine.record_evaluations(gi, out)
+
+    def finish_evaluations(self) -> None:
+        """Collective.  Wait for and record the pending deferred community
+        evaluation (the bench calls it inside its timed region)."""
+        if self._ce:
+            self._collect_community_eval()
+
+    def _community_rows(self, evs: list) -> list | None:
+        nan = {"loss": float("nan"), "accuracy": float("nan")}
+        vals = []
+        for ev, ds in zip(evs, self.test_dss):
+            ev = ev or nan
+            vals.append([ev["loss"], ev["accuracy"], float(ds.n) if ds is not None and ev is not nan else 0.0])
+        rows = self._gather_learner_rows(vals)
+        out = [{"loss": float(r[0]), "accuracy": float(r[1]), "num_examples": int(r[2])} for r in rows]
+        if all(o["num_examples"] == 0 for o in out):
+            return None
+        return out
+
     def evaluate_community(self) -> tuple[list | None, float]:
         """Every learner evaluates the community model (resident after the
         all-reduce) on its test shard; the metrics are all-gathered (a few
         scalars per learner).  -> ([{"loss", "accuracy", "num_examples"}] per
-        rank, ms)."""
+        rank, ms).  With ``defer_community_eval`` the evaluation is only
+        issued here (-> (None, ms)); its results are recorded with this
+        round at the next round's end or by ``finish_evaluations``."""
         if not self.cfg.evaluate_community:
             return None, 0.0
         t0 = time.perf_counter()
+        ce = self._deferred_eval()
+        if ce is not None:
+            self._collect_community_eval()  # the previous round's (long finished)
+            # (the snapshot reads learner 0's model, where the community model
+            # was reduced: never a pending learner's buffer, weighted_sum_into)
+            ce.submit(self.global_iteration, self.cfg.eval_max_steps)
+            return None, (time.perf_counter() - t0) * 1e3
         nan = {"loss": float("nan"), "accuracy": float("nan")}
         if self.group is not None:
             with tracing.range("metisfl.community_eval"):
@@ -786,7 +911,9 @@ class CollectiveFederation:
 
     def flush_checkpoints(self) -> None:
         """Wait for background checkpoint / lineage writes of this rank (and
-        send the last community model if the lineage skipped its round)."""
+        send the last community model if the lineage skipped its round).
+        Not collective: a deferred community evaluation still pending is
+        collected by ``finish_evaluations``."""
         if self._lineage is not None and getattr(self, "_lineage_skipped", False):
             self._lineage.wait()
             self.snapshot_community()

@@ -231,3 +231,31 @@ def test_colocated_round_closes_without_draining_the_dropped_learner():
     assert torch.equal(nets[2].state.model32, nets[0].state.model32)
     group.settle()
     assert not group.pending
+
+
+def test_deferred_community_eval_matches_the_synchronous_one():
+    """FederationConfig.defer_community_eval: the community model's
+    evaluation runs on a frozen copy while the next round trains; its
+    recorded results equal a synchronous evaluation of the same community
+    model, and each round's results land on that round's record."""
+    from metisfl_amd.parallel.comm import Comm
+    from metisfl_amd.parallel.federation import CollectiveFederation, FederationConfig
+    nets, dss = _learners(3, shard=128)
+    tests = [n.make_dataset(np.random.default_rng(90 + j).standard_normal((300, 32, 32, 3)).astype(np.float32),
+                            np.random.default_rng(j).integers(0, 10, 300), seed=j, shuffle=False)
+             for j, n in enumerate(nets)]
+    cfg = FederationConfig(batch_size=32, local_epochs=1, evaluate_test=True, defer_community_eval=True)
+    fed = CollectiveFederation(Comm(), nets, dss, cfg, test_ds=tests)
+    sync = []
+    for r in range(3):
+        rec = fed.run_round()
+        assert fed._ce, "deferred evaluator not built"
+        assert rec.community_eval is None  # issued, not yet collected
+        sync.append(fed.group.evaluate())  # the same community model, evaluated now on the live replicas
+    fed.finish_evaluations()
+    for r, rec in enumerate(fed.history):
+        assert rec.community_eval is not None and len(rec.community_eval) == 3
+        for got, want in zip(rec.community_eval, sync[r]):
+            assert got["num_examples"] == 300
+            assert abs(got["loss"] - want["loss"]) <= 1e-6 * abs(want["loss"]) and got["accuracy"] == want["accuracy"]
+    assert all(np.isfinite(rec.learner_meta[:, 8]).all() for rec in fed.history)  # learners' own test losses
