@@ -249,6 +249,8 @@ def main() -> int:
         "samples_per_s": (args.train_size * args.local_epochs) / (round_ms / 1e3) if round_ms else 0.0,
     }
     out["community_eval_ms_mean"] = sum(r.community_eval_ms for r in timed) / max(1, len(timed))
+    out["phase_ms_mean"] = ({k: sum(r.phase_ms[k] for r in timed) / len(timed) for k in timed[0].phase_ms}
+                            if timed and timed[0].phase_ms else None)
     out["community_eval"] = ("deferred: on a frozen copy of each community model, overlapping the next round's "
                              "training; the last round's completes inside the timed region"
                              if cfg.defer_community_eval and fed._ce else "synchronous, at the end of its round")

@@ -150,6 +150,11 @@ class RoundRecord:
     community_eval_ms: float = 0.0
     snapshot_ms: float = 0.0               # rank 0: staging the community model for the controller's lineage
     checkpoint_ms: float = 0.0             # this rank: time the round's checkpoint held it (staging)
+    # host wall time of the round's phases (local_train: training + the
+    # learners' test evaluations; gather: metadata all-gather; aggregate;
+    # community_eval; bookkeeping: controller records, quantifiers, lineage
+    # snapshot -- after round_ms)
+    phase_ms: dict | None = None
 
     def to_json(self) -> dict:
         d = asdict(self)
@@ -750,6 +755,7 @@ class CollectiveFederation:
         self.global_iteration += 1
         started = time.time()
         results = self.local_train_all([self.num_local_updates[i] for i in self.local_learners()])
+        t_trained = time.time()
         rows = []
         for ds, res in zip(self.train_dss, results):
             test = res.get("test") or {}
@@ -791,6 +797,9 @@ class CollectiveFederation:
             if self.cfg.snapshot_every and self.global_iteration % self.cfg.snapshot_every == 0:
                 rec.snapshot_ms = self.snapshot_community()
         self.update_templates(meta)
+        rec.phase_ms = {"local_train": (t_trained - started) * 1e3, "gather": (completed - t_trained) * 1e3,
+                        "aggregate": (agg_done - completed) * 1e3, "community_eval": (round_done - agg_done) * 1e3,
+                        "bookkeeping": (time.time() - round_done) * 1e3}
         self.history.append(rec)
         return rec
 

@@ -52,8 +52,9 @@ def main():
         net = ResNet18(batch_size=a.batch, device="cuda", seed=7 + i, dtype=a.dtype,
                        conv_products=a.conv_products,
                        optimizer=OptimizerSpec("momentum_sgd", 0.005, momentum=0.75))
-        x = torch.randn((1024, 32, 32, 3), generator=gen, device="cuda")
-        y = torch.randint(0, 10, (1024,), generator=gen, device="cuda")
+        ns = max(1024, 16 * a.batch)  # >= 2 x K steps per epoch: the K-update graph gets captured
+        x = torch.randn((ns, 32, 32, 3), generator=gen, device="cuda")
+        y = torch.randint(0, 10, (ns,), generator=gen, device="cuda")
         if a.tconv:
             net.set_throughput_conv(True)
         nets.append(net)
