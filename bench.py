@@ -249,6 +249,10 @@ def main() -> int:
         "samples_per_s": (args.train_size * args.local_epochs) / (round_ms / 1e3) if round_ms else 0.0,
     }
     out["community_eval_ms_mean"] = sum(r.community_eval_ms for r in timed) / max(1, len(timed))
+    if fed.group is not None and fed.group.last_eval_ms:
+        out["last_round_device_ms"] = {"train_max": float(timed[-1].train_ms),
+                                       "test_eval_per_learner": [round(x, 2) for x in fed.group.last_eval_ms],
+                                       "first_start_to_last_eval_end": fed.group.last_span_ms}
     out["phase_ms_mean"] = ({k: sum(r.phase_ms[k] for r in timed) / len(timed) for k in timed[0].phase_ms}
                             if timed and timed[0].phase_ms else None)
     out["community_eval"] = ("deferred: on a frozen copy of each community model, overlapping the next round's "

@@ -49,6 +49,9 @@ class CoLocatedLearners:
                     net.set_throughput_conv(True)
         self._ev = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                      for _ in self.nets] if self.cuda else None)
+        self._ev2 = [torch.cuda.Event(enable_timing=True) for _ in self.nets] if self.cuda else None
+        self.last_eval_ms: list[float] = []   # device ms of each learner's test evaluation (train(eval_dss=...))
+        self.last_span_ms = 0.0               # first start -> last evaluation end
         # learners dropped from the last elastic round whose already-issued
         # chunks may still be running on their streams: the round closed
         # without waiting for them, so the current stream is NOT ordered after
@@ -178,6 +181,8 @@ class CoLocatedLearners:
                         host_ms[j] = (time.perf_counter() - t0) * 1e3
                         if eval_dss is not None and eval_dss[j] is not None:
                             owners[j] = self.nets[j].begin_evaluate(eval_dss[j], eval_max_steps)
+                            if self.cuda:
+                                self._ev2[j].record()
             live = nxt
         self._join()
         self.pending = set()
@@ -185,6 +190,14 @@ class CoLocatedLearners:
             for _, e1 in self._ev:
                 e1.synchronize()
             ms = [e0.elapsed_time(e1) for e0, e1 in self._ev]
+            if eval_dss is not None:
+                # device time of each learner's test evaluation, and from the
+                # first learner's start to the last evaluation's end
+                ev = [j for j in range(len(self)) if owners[j] is not None]
+                for j in ev:
+                    self._ev2[j].synchronize()
+                self.last_eval_ms = [self._ev[j][1].elapsed_time(self._ev2[j]) for j in ev]
+                self.last_span_ms = max((self._ev[0][0].elapsed_time(self._ev2[j]) for j in ev), default=0.0)
         else:
             ms = host_ms
         if eval_dss is None:
