@@ -229,9 +229,36 @@ class DeferredCommunityEval:
         self.state = self.src.detached_copy()
         self.evals = [n.detached_evaluator(d, self.state) if d is not None else None
                       for n, d in zip(nets, test_dss)]
-        self.stream = torch.cuda.Stream(device=self.src.model32.device)
+        self.stream = self._make_stream(self.src.model32.device)
         self.event = torch.cuda.Event()
         self.pending = None  # (global_iteration, owners)
+
+    # The evaluation stream must not share a hardware queue with a learner:
+    # HIP deals streams round-robin onto GPU_MAX_HW_QUEUES (4) in-order queues,
+    # so on a shared queue the whole evaluation runs in FIFO order ahead of
+    # that queue's learners' next round (measured: two of 8 learners started
+    # ~70 ms late).  A high-priority stream gets a queue of its own (HIP keeps
+    # queues per priority); MFL_CE_STREAM=plain|cumask|prio (default prio) for
+    # A/B runs -- cumask: a full-chip CU-masked stream, also a queue of its own.
+    stream_kind = os.environ.get("MFL_CE_STREAM", "prio")
+
+    @classmethod
+    def _make_stream(cls, dev):
+        if cls.stream_kind == "plain":
+            return torch.cuda.Stream(device=dev)
+        if cls.stream_kind == "cumask":
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            words = (ncu + 31) // 32
+            arr = (ctypes.c_uint32 * words)(*([0xFFFFFFFF] * words))
+            h = ctypes.c_void_p()
+            with torch.cuda.device(dev):
+                if hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(words), arr) != 0:
+                    raise RuntimeError("hipExtStreamCreateWithCUMask failed")
+            return torch.cuda.ExternalStream(h.value, device=dev)
+        lo, hi = torch.cuda.Stream.priority_range()
+        return torch.cuda.Stream(device=dev, priority=hi)
 
     @classmethod
     def build(cls, nets: list, test_dss: list):
