@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--pair-ring", type=int, default=-1,
                     help="conv32 paired-launch LDS ring stages (-1: what CoLocatedLearners selects for the group)")
     ap.add_argument("--conv-products", default=None, choices=("bf16x3", "exact"))
+    ap.add_argument("--prio-split", action="store_true", help="alternate learner stream priorities")
     a = ap.parse_args()
     gmax = max(a.groups)
     from metisfl_amd.models.colocated import CoLocatedLearners
@@ -62,7 +63,14 @@ def main():
     for net, ds in zip(nets, dss):  # capture (1-step and K-step graphs)
         net.train_steps(ds, 16)
     torch.cuda.synchronize()
-    streams = [torch.cuda.Stream() for _ in range(gmax)]
+    if a.prio_split:
+        # alternate stream priorities: HIP keeps hardware queues per priority,
+        # so the two halves do not share in-order queues
+        lo, hi = torch.cuda.Stream.priority_range()
+        print(f"stream priorities {lo} / {hi} alternating", flush=True)
+        streams = [torch.cuda.Stream(priority=hi if g % 2 else lo) for g in range(gmax)]
+    else:
+        streams = [torch.cuda.Stream() for _ in range(gmax)]
     masked = {}
     if a.cu_mask != "none":
         import ctypes
