@@ -24,6 +24,11 @@ void set_conv32_pair_ring(int64_t ns) {
   mfl::c32s::set_conv32_pair_ring((int)ns);
 }
 
+void set_conv32_plan_overrides(const std::string& spec) {
+  mfl::c32x::set_conv32_plan_overrides(spec.c_str());
+  mfl::c32s::set_conv32_plan_overrides(spec.c_str());
+}
+
 void set_conv32_mode(int64_t m) {
   TORCH_CHECK(m == 0 || m == 1, "conv32 mode is 0 (exact fp32) or 1 (bf16x3)");
   g_c32_mode = (int)m;
@@ -714,6 +719,7 @@ void gather_batch32(torch::Tensor shard, torch::Tensor labels, torch::Tensor per
 void register_fp32(pybind11::module& m) {
   m.def("set_conv32_mode", &set_conv32_mode);
   m.def("set_conv32_pair_ring", &set_conv32_pair_ring);
+  m.def("set_conv32_plan_overrides", &set_conv32_plan_overrides);
   m.def("conv32_mode", &conv32_mode);
   m.def("conv32_plan", &conv32_plan);
   m.def("conv32_forward", &conv32_forward);

@@ -1144,25 +1144,27 @@ constexpr TunedPlan kTuned[] = {
 struct PlanOverride {
   int mode, h, c, co, r, stride, splits;
 };
+static std::vector<PlanOverride> parse_plan_overrides(const std::string& str) {
+  std::vector<PlanOverride> out;
+  size_t pos = 0;
+  while (pos < str.size()) {
+    size_t end = str.find(';', pos);
+    if (end == std::string::npos) end = str.size();
+    PlanOverride o{};
+    if (std::sscanf(str.substr(pos, end - pos).c_str(), "%d,%d,%d,%d,%d,%d,%d", &o.mode, &o.h, &o.c, &o.co, &o.r,
+                    &o.stride, &o.splits) == 7)
+      out.push_back(o);
+    pos = end + 1;
+  }
+  return out;
+}
+// the environment's overrides win over the regime set at run time
+// (set_conv32_plan_overrides: the co-located learners' plans)
+static std::vector<PlanOverride> g_rt_overrides;
 static const std::vector<PlanOverride>& plan_overrides() {
-  static const std::vector<PlanOverride> v = [] {
-    std::vector<PlanOverride> out;
-    const char* e = std::getenv("MFL_C32_PLANS");
-    if (!e) return out;
-    std::string str(e);
-    size_t pos = 0;
-    while (pos < str.size()) {
-      size_t end = str.find(';', pos);
-      if (end == std::string::npos) end = str.size();
-      PlanOverride o{};
-      if (std::sscanf(str.substr(pos, end - pos).c_str(), "%d,%d,%d,%d,%d,%d,%d", &o.mode, &o.h, &o.c, &o.co, &o.r,
-                      &o.stride, &o.splits) == 7)
-        out.push_back(o);
-      pos = end + 1;
-    }
-    return out;
-  }();
-  return v;
+  static const char* env = std::getenv("MFL_C32_PLANS");
+  static const std::vector<PlanOverride> v = env ? parse_plan_overrides(env) : std::vector<PlanOverride>{};
+  return env ? v : g_rt_overrides;
 }
 
 static void tuned_plan(const ConvGeom& g, int mode, int& bm, int& bn, int& sp) {
@@ -1383,6 +1385,7 @@ void launch_conv32_wgrad(const ConvGeom& g, const ConvPlan& p, const float* x, c
 // bf16x3 build carries the 2-stage pair instantiations.
 int g_pair_ns = 0;
 void set_conv32_pair_ring(int ns) { g_pair_ns = ns; }
+void set_conv32_plan_overrides(const char* spec) { g_rt_overrides = parse_plan_overrides(spec ? spec : ""); }
 size_t gemm_lds_ns(int bm, int bn, int ns) {  // ring of ns stages or the gemm epilogue, whichever is larger
   return std::max((size_t)ns * (bm + bn) * kRowB, (size_t)bm * (bn + 4) * 4 + 256 * 8 * 4 + 16);
 }

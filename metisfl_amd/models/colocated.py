@@ -43,6 +43,9 @@ class CoLocatedLearners:
         self.streams = (self._make_streams(dev, len(self.nets)) if self.cuda else [None] * len(nets))
         if self.cuda and len(self.nets) >= self.pair_ring_min_learners and self.pair_ring:
             self._set_pair_ring(int(self.pair_ring))
+        if self.cuda and len(self.nets) >= self.pair_ring_min_learners and self.plans:
+            from metisfl_amd.ops._native import ops
+            ops().set_conv32_plan_overrides(self.plans)
         if self.cuda and len(self.nets) >= self.tconv_min_learners and self.tconv:
             for net in self.nets:
                 if hasattr(net, "set_throughput_conv"):
@@ -69,6 +72,15 @@ class CoLocatedLearners:
     # their graphs.  MFL_COLOC_PAIR_RING=0 keeps the build default.
     pair_ring = os.environ.get("MFL_COLOC_PAIR_RING", "2")
     pair_ring_min_learners = int(os.environ.get("MFL_COLOC_PAIR_RING_MIN", "4"))
+    # ... and the 16x16x128 / 8x8x256 3x3 input gradients split their
+    # reduction into 1 / 2 slices instead of the one-learner table's 2 / 4
+    # (fewer, fuller workgroups when other learners' launches fill the CUs):
+    # 8 co-located learners 0.6678 -> 0.6607 ms per update, one learner
+    # 1.074 -> 1.086 (so only here), same box, 3 alternating repeats
+    # (profiles/r6/bench/plan_confirm.log).  Plans only shrink: the
+    # workspaces sized at model build still fit.  MFL_COLOC_PLANS="" keeps
+    # the table; MFL_C32_PLANS in the environment overrides both.
+    plans = os.environ.get("MFL_COLOC_PLANS", "1,16,128,128,3,1,1;1,8,256,256,3,1,2")
     # MFL_COLOC_TCONV=1: the 3x3 / stride-1 backward GEMMs run as the
     # throughput kernels (tconv.hip, StaticNet.set_throughput_conv) instead of
     # the paired latency-regime launches.  Off by default: faster per call in

@@ -398,7 +398,7 @@ class AsyncCollectiveFederation:
         tr = L.net.train_stats()
         return {"task": L.task_index, "weight": self._weight(L, L.num_local_updates),
                 "loss": tr["loss"], "accuracy": tr["accuracy"], "batches": L.num_local_updates,
-                "base_version": L.base_version, "eval": L.last_eval, "started_at": L.started,
+                "base_version": L.base_version, "eval": self._eval_result(L), "started_at": L.started,
                 "n_train": int(L.train_ds.n), "ms_per_batch": ms_b, "ms_per_epoch": ms_b * spe,
                 "epochs": L.num_local_updates / spe}
 
@@ -437,12 +437,30 @@ class AsyncCollectiveFederation:
         L.task_index += 1
         L.tasks_run += 1
 
-    def _evaluate_received(self, L: _Local) -> dict | None:
+    def _evaluate_received(self, L: _Local) -> None:
+        """Issue learner L's evaluation of the community model it received
+        on its own stream (ahead of its next task there) without waiting:
+        the host goes on serving the other learners; the result is read when
+        it is needed -- in L's next submission, or when L leaves
+        (``_eval_result``)."""
+        L.last_eval = None
+        L.extra.pop("eval_owner", None)
         if L.test_ds is None or not self.cfg.evaluate_community:
-            return None
+            return
         with self._ctx(L):
-            ev = L.net.evaluate(L.test_ds, self.cfg.eval_max_steps)
-        return {"version": L.base_version, "loss": ev["loss"], "accuracy": ev["accuracy"], "n": L.test_ds.n}
+            owner = L.net.begin_evaluate(L.test_ds, self.cfg.eval_max_steps)
+        L.extra["eval_owner"] = (owner, L.base_version)
+        if owner is L.net:  # evaluated in the training statistics' buffer (no twin): read it before the next task
+            self._eval_result(L)
+
+    def _eval_result(self, L: _Local) -> dict | None:
+        pend = L.extra.pop("eval_owner", None)
+        if pend is not None:
+            owner, ver = pend
+            with self._ctx(L):  # the statistics read waits for L's stream only
+                ev = L.net.finish_evaluate(owner)
+            L.last_eval = {"version": ver, "loss": ev["loss"], "accuracy": ev["accuracy"], "n": L.test_ds.n}
+        return L.last_eval
 
     # ---- the event loop over this rank's learners ---------------------------------
     def _drive(self, more_tasks, debug_delay_s: float = 0.0, fault_task: int | None = None, on_fault=None,
@@ -490,7 +508,7 @@ class AsyncCollectiveFederation:
                 progressed = True
                 meta = self._task_meta(L, debug_delay_s)
                 self._submit(L, meta)
-                L.last_eval = self._evaluate_received(L)
+                self._evaluate_received(L)
                 if after_task is not None:
                     after_task(L)
                 start_or_finish(L)
@@ -511,9 +529,9 @@ class AsyncCollectiveFederation:
             return
         if self.rank == 0:
             with self._lock:
-                self._record_eval(L.gid, L.last_eval)
+                self._record_eval(L.gid, self._eval_result(L))
         else:
-            self.store.set(_DONE.format(self.tag, L.gid), json.dumps({"eval": L.last_eval}))
+            self.store.set(_DONE.format(self.tag, L.gid), json.dumps({"eval": self._eval_result(L)}))
 
     # ---- the two entry points -----------------------------------------------------
     _until = False
