@@ -72,15 +72,18 @@ class CoLocatedLearners:
     # their graphs.  MFL_COLOC_PAIR_RING=0 keeps the build default.
     pair_ring = os.environ.get("MFL_COLOC_PAIR_RING", "2")
     pair_ring_min_learners = int(os.environ.get("MFL_COLOC_PAIR_RING_MIN", "4"))
-    # ... and the 16x16x128 / 8x8x256 3x3 input gradients split their
-    # reduction into 1 / 2 slices instead of the one-learner table's 2 / 4
-    # (fewer, fuller workgroups when other learners' launches fill the CUs):
-    # 8 co-located learners 0.6678 -> 0.6607 ms per update, one learner
-    # 1.074 -> 1.086 (so only here), same box, 3 alternating repeats
-    # (profiles/r6/bench/plan_confirm.log).  Plans only shrink: the
-    # workspaces sized at model build still fit.  MFL_COLOC_PLANS="" keeps
-    # the table; MFL_C32_PLANS in the environment overrides both.
-    plans = os.environ.get("MFL_COLOC_PLANS", "1,16,128,128,3,1,1;1,8,256,256,3,1,2")
+    # ... and the input gradients split their reduction into fewer slices
+    # than the one-learner table (fewer, fuller workgroups when other
+    # learners' launches fill the CUs): the 16x16x128 / 8x8x256 3x3 ones 1 / 2
+    # instead of 2 / 4, the stride-2 16x16x128->256 / 8x8x256->512 3x3 ones
+    # 1 / 2 instead of 3 / 4, the 8x8x256->512 1x1 shortcut's 1 instead of 2.
+    # 8 co-located learners 0.6678 -> 0.6607 -> 0.6534 ms per update in two
+    # sweeps (one learner 1.074 -> 1.086: so only here), same box, 3
+    # alternating repeats (profiles/r6/bench/plan_sweep*, plan_confirm*.log).
+    # Plans only shrink: the workspaces sized at model build still fit.
+    # MFL_COLOC_PLANS="" keeps the table; MFL_C32_PLANS overrides both.
+    plans = os.environ.get("MFL_COLOC_PLANS", "1,16,128,128,3,1,1;1,8,256,256,3,1,2;1,16,128,256,3,2,1;"
+                                              "1,8,256,512,3,2,2;1,8,256,512,1,2,1")
     # MFL_COLOC_TCONV=1: the 3x3 / stride-1 backward GEMMs run as the
     # throughput kernels (tconv.hip, StaticNet.set_throughput_conv) instead of
     # the paired latency-regime launches.  Off by default: faster per call in
