@@ -117,6 +117,8 @@ def main() -> int:
     def share(total: int, i: int) -> int:
         return total // nl + (1 if i < total % nl else 0)
 
+    from metisfl_amd.models.colocated import configure_regime
+    configure_regime(L)  # kernel choices for L learners per GPU, before the models are built
     opt = OptimizerSpec("momentum_sgd", args.lr, momentum=args.momentum)
     nets, train_dss, test_dss = [], [], []
     for j in range(L):

@@ -73,6 +73,8 @@ def main() -> int:
     L = max(args.learners, n)
     owners = [min(n - 1, g * n // L) for g in range(L)]  # contiguous blocks of learners per rank
     gids = [g for g in range(L) if owners[g] == comm.rank]
+    from metisfl_amd.models.colocated import configure_regime
+    configure_regime(len(gids))  # kernel choices for this GPU's co-located learners
     nets, dss = [], []
     for g in gids:
         ng = args.train_size // L + (1 if g < args.train_size % L else 0)

@@ -168,6 +168,9 @@ def _main(argv, ctx: dict) -> int:
     model_def = _load_model_def(job)
     train_recipe, test_recipe = _load_recipe(job.get("train_recipe")), _load_recipe(job.get("test_recipe"))
     nets, train_dss, test_dss = [], [], []
+    if comm.device.type == "cuda":
+        from metisfl_amd.models.colocated import configure_regime
+        configure_regime(len(mine))  # this rank's co-located learners, before their models are built
     for lc in mine:
         n_ = model_def.get_model(batch_size=job["batch_size"], device=comm.device, optimizer=opt,
                                  seed=job.get("seed", 0))

@@ -29,6 +29,21 @@ import os
 import torch
 
 
+def configure_regime(learners_per_gpu: int) -> None:
+    """Kernel choices for ``learners_per_gpu`` learners sharing each GPU, made
+    BEFORE their models are built (the layer plans and workspaces are fixed
+    at build): with 4+ co-located learners the 4x4x512 layers run the im2col
+    convolution instead of the halo conv (8-slice split-K at one workgroup
+    per CU: 0.6684 -> 0.6634 and 0.6823 -> 0.6737 ms per update with 8
+    learners on two boxes, profiles/r6/bench/hconv_skip*.log; the one-learner
+    latency regime keeps it), plus the paired-launch ring and plans that
+    ``CoLocatedLearners`` also sets.  MFL_HCONV_SKIP in the environment wins."""
+    from metisfl_amd.models import layers
+    if learners_per_gpu >= CoLocatedLearners.pair_ring_min_learners and "MFL_HCONV_SKIP" not in os.environ:
+        layers.HCONV_SKIP = {int(v) for v in CoLocatedLearners.hconv_skip.split(",") if v.strip()}
+    CoLocatedLearners.apply_kernel_regime(learners_per_gpu)
+
+
 class CoLocatedLearners:
     """L learners on one device; ``nets[j]`` trains ``train_dss[j]``."""
 
@@ -41,11 +56,8 @@ class CoLocatedLearners:
         self.device = dev
         self.cuda = dev.type == "cuda"
         self.streams = (self._make_streams(dev, len(self.nets)) if self.cuda else [None] * len(nets))
-        if self.cuda and len(self.nets) >= self.pair_ring_min_learners and self.pair_ring:
-            self._set_pair_ring(int(self.pair_ring))
-        if self.cuda and len(self.nets) >= self.pair_ring_min_learners and self.plans:
-            from metisfl_amd.ops._native import ops
-            ops().set_conv32_plan_overrides(self.plans)
+        if self.cuda:
+            self.apply_kernel_regime(len(self.nets))
         if self.cuda and len(self.nets) >= self.tconv_min_learners and self.tconv:
             for net in self.nets:
                 if hasattr(net, "set_throughput_conv"):
@@ -92,6 +104,21 @@ class CoLocatedLearners:
     # 0.747 ms per update of the GPU, profiles/r5/tconv/)
     tconv = os.environ.get("MFL_COLOC_TCONV", "0") == "1"
     tconv_min_learners = int(os.environ.get("MFL_COLOC_TCONV_MIN", "4"))
+
+    hconv_skip = os.environ.get("MFL_COLOC_HCONV_SKIP", "4")  # see configure_regime
+
+    @classmethod
+    def apply_kernel_regime(cls, n: int) -> None:
+        """Process-wide launch choices for n co-located learners (before their
+        graphs are captured): the 2-stage pair ring and the plan overrides."""
+        import torch as _t
+        if n < cls.pair_ring_min_learners or not _t.cuda.is_available():
+            return
+        if cls.pair_ring:
+            cls._set_pair_ring(int(cls.pair_ring))
+        if cls.plans:
+            from metisfl_amd.ops._native import ops
+            ops().set_conv32_plan_overrides(cls.plans)
 
     @staticmethod
     def _set_pair_ring(ns: int) -> None:

@@ -144,8 +144,15 @@ HCONV = os.environ.get("MFL_HCONV", "1") == "1"
 # ... for the bf16 option too (MFL_HCONV_BF16=0: BN apply + im2col conv)
 HCONV_BF16 = os.environ.get("MFL_HCONV_BF16", "1") == "1"
 # MFL_HCONV_SKIP="32,16": layers of these input sizes run the im2col path
-# instead (A/B runs of the halo conv per stage)
-HCONV_SKIP = {int(v) for v in os.environ.get("MFL_HCONV_SKIP", "").split(",") if v.strip()}
+# instead (A/B runs of the halo conv per stage; the co-located regime sets it,
+# models/colocated.py configure_regime).  Read when a layer is built.
+HCONV_SKIP: set[int] | None = None
+
+
+def hconv_skip() -> set[int]:
+    if HCONV_SKIP is not None:
+        return HCONV_SKIP
+    return {int(v) for v in os.environ.get("MFL_HCONV_SKIP", "").split(",") if v.strip()}
 def premasked(t: torch.Tensor) -> bool:
     """Whether a dgrad that fuses a consumer BN's backward sums (``bnb``) into
     its epilogue stores dX already multiplied by that BN's ReLU mask (the
@@ -301,7 +308,7 @@ class ConvBN(Layer):
         # products on the GPU (or FUSED_FILL_CPU for the host-side tests), or
         # the bf16 option's activations with plain bf16 products
         self._hconv_ws = -1
-        if HCONV and s.H not in HCONV_SKIP and ((ws.dtype == torch.float32 and (
+        if HCONV and s.H not in hconv_skip() and ((ws.dtype == torch.float32 and (
                 (dev.type == "cuda" and K.conv_products() == "bf16x3") or (dev.type == "cpu" and FUSED_FILL_CPU)))
                 or (ws.dtype == torch.bfloat16 and dev.type == "cuda" and HCONV_BF16)):
             self._hconv_ws = K.hconv_workspace(s, dev)
