@@ -41,7 +41,8 @@ def main():
     ap.add_argument("--prio-split", action="store_true", help="alternate learner stream priorities")
     a = ap.parse_args()
     gmax = max(a.groups)
-    from metisfl_amd.models.colocated import CoLocatedLearners
+    from metisfl_amd.models.colocated import CoLocatedLearners, configure_regime
+    configure_regime(gmax)  # the production regime for gmax co-located learners (plans, halo-conv stages)
     ring = a.pair_ring if a.pair_ring >= 0 else (int(CoLocatedLearners.pair_ring or 0)
                                                  if gmax >= CoLocatedLearners.pair_ring_min_learners else 0)
     if ring:
