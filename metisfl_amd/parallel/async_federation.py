@@ -272,6 +272,14 @@ class AsyncCollectiveFederation:
         self._driver_stop = False
         st = self.net.state
         self.cuda = st.model32.is_cuda
+        # the host-side reads and the rank-0 FedRec of local learners run on a
+        # high-priority stream: a hardware queue of its own (HIP keeps queues
+        # per priority), so they never wait in FIFO order behind the learner
+        # graphs queued on a shared in-order queue (8 learner streams share 4)
+        self._hp = None
+        if st.model32.is_cuda and os.environ.get("MFL_ASYNC_HP", "1") == "1":  # (=0: A/B runs only)
+            lo, hi = torch.cuda.Stream.priority_range()
+            self._hp = torch.cuda.Stream(device=st.model32.device, priority=hi)
         # co-located learners replay their step graphs on their own streams
         if streams is not None:
             self.streams = list(streams)
@@ -343,6 +351,15 @@ class AsyncCollectiveFederation:
         s = self.streams[L.j]
         return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
 
+    def _hp_after(self, ev):
+        """The high-priority stream, ordered after event ``ev`` (a learner's
+        task-end or evaluation-end marker), as a stream context."""
+        if self._hp is None:
+            return contextlib.nullcontext()
+        if ev is not None:
+            self._hp.wait_event(ev)
+        return torch.cuda.stream(self._hp)
+
     def _sync_stream(self) -> None:
         if self.cuda:
             torch.cuda.current_stream(self.net.state.model32.device).synchronize()
@@ -366,7 +383,10 @@ class AsyncCollectiveFederation:
             s.wait_stream(torch.cuda.current_stream(L.net.state.model32.device))
 
     def _start_task(self, L: _Local) -> None:
-        self._order(L)  # after a checkpoint staged on the current stream (after_task)
+        # (ordered after the install / checkpoint staging by _order: those run
+        # on the high-priority stream; ordering after the default stream here
+        # would queue this learner behind whatever shares that stream's
+        # in-order hardware queue)
         with self._ctx(L):
             L.net.reset_train_stats()
             L.gen = L.net.train_steps_iter(L.train_ds, L.num_local_updates, step_offset=L.steps_done)
@@ -395,7 +415,8 @@ class AsyncCollectiveFederation:
         ms_b = (time.time() - L.started) * 1e3 / max(1, L.num_local_updates)
         L.steps_done += L.num_local_updates
         spe = L.train_ds.steps_per_epoch
-        tr = L.net.train_stats()
+        with self._hp_after(L.done_ev):
+            tr = L.net.train_stats()
         return {"task": L.task_index, "weight": self._weight(L, L.num_local_updates),
                 "loss": tr["loss"], "accuracy": tr["accuracy"], "batches": L.num_local_updates,
                 "base_version": L.base_version, "eval": self._eval_result(L), "started_at": L.started,
@@ -404,7 +425,12 @@ class AsyncCollectiveFederation:
 
     def _submit(self, L: _Local, meta: dict) -> None:
         """FedRec of the finished task; the learner leaves holding the new
-        community model."""
+        community model.  Runs on the high-priority stream after the task's
+        end marker; the learner's stream is ordered after it (``_install``)."""
+        with self._hp_after(L.done_ev):
+            self._submit_body(L, meta)
+
+    def _submit_body(self, L: _Local, meta: dict) -> None:
         model = L.net.state.model32
         # secure aggregation: the learner encrypts its model where it lives and
         # decrypts the community ciphertext it gets back
@@ -447,17 +473,21 @@ class AsyncCollectiveFederation:
         L.extra.pop("eval_owner", None)
         if L.test_ds is None or not self.cfg.evaluate_community:
             return
+        ev = None
         with self._ctx(L):
             owner = L.net.begin_evaluate(L.test_ds, self.cfg.eval_max_steps)
-        L.extra["eval_owner"] = (owner, L.base_version)
+            if self.cuda:
+                ev = torch.cuda.Event()
+                ev.record()
+        L.extra["eval_owner"] = (owner, L.base_version, ev)
         if owner is L.net:  # evaluated in the training statistics' buffer (no twin): read it before the next task
             self._eval_result(L)
 
     def _eval_result(self, L: _Local) -> dict | None:
         pend = L.extra.pop("eval_owner", None)
         if pend is not None:
-            owner, ver = pend
-            with self._ctx(L):  # the statistics read waits for L's stream only
+            owner, ver, done = pend
+            with self._hp_after(done):  # the read waits for this evaluation only
                 ev = L.net.finish_evaluate(owner)
             L.last_eval = {"version": ver, "loss": ev["loss"], "accuracy": ev["accuracy"], "n": L.test_ds.n}
         return L.last_eval
@@ -550,7 +580,8 @@ class AsyncCollectiveFederation:
             st = self.net.state
             if st.model32.is_cuda:
                 torch.cuda.set_device(st.model32.device)
-                stream = torch.cuda.Stream(device=st.model32.device)
+                # a hardware queue of its own (see self._hp)
+                stream = torch.cuda.Stream(device=st.model32.device, priority=torch.cuda.Stream.priority_range()[1])
                 ctx = torch.cuda.stream(stream)
             else:
                 ctx = contextlib.nullcontext()
@@ -618,7 +649,9 @@ class AsyncCollectiveFederation:
 
         def after(L: _Local) -> None:
             if self.ckpt_dir and self.ckpt_every and L.task_index % self.ckpt_every == 0:
-                self._checkpoint_learner(L)
+                with self._hp_after(L.done_ev):  # staged after the task, before the next one
+                    self._checkpoint_learner(L)
+                    self._order(L)
 
         self._drive(lambda L: not self._stopped(), debug_delay_s, fault_task, on_fault, after)
         self._end_service(svc)
