@@ -105,7 +105,10 @@ std::vector<int64_t> conv32_plan(int64_t mode, int64_t N, int64_t H, int64_t W, 
   const auto g = mode == 0 ? fwd_geom(N, H, W, C, Co, R, S, stride, pad) : dgrad_geom(N, H, W, C, Co, R, S, stride, pad);
   const auto p = C32_CALL(plan_conv32, g, (int)mode);
   TORCH_CHECK(p.kchunk > 0, "no feasible conv32 plan for this shape");
-  return {p.bm, p.bn, p.splits, p.kchunk, mode == 0 ? 1 : 0, ws_floats(g, p)};
+  // workspace for the larger of the regime's plan and the table's
+  const auto pt = C32_CALL(plan_conv32_table, g, (int)mode);
+  const int64_t ws = std::max(ws_floats(g, p), pt.kchunk > 0 ? ws_floats(g, pt) : (int64_t)0);
+  return {p.bm, p.bn, p.splits, p.kchunk, mode == 0 ? 1 : 0, ws};
 }
 
 // fwd / dgrad B operand: the fp32 weights (exact mode), or in bf16x3 mode their

@@ -412,7 +412,6 @@ void register_bert(pybind11::module& m);
 void register_ckks(pybind11::module& m);
 void register_fp32(pybind11::module& m);
 void register_hconv(pybind11::module& m);
-void register_tconv(pybind11::module& m);
 
 PYBIND11_MODULE(_ops, m) {
   m.doc() = "metisfl_amd hand-written HIP (gfx950) kernels";
@@ -443,5 +442,4 @@ PYBIND11_MODULE(_ops, m) {
   register_ckks(m);
   register_fp32(m);
   register_hconv(m);
-  register_tconv(m);
 }

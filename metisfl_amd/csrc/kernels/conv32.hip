@@ -1161,10 +1161,12 @@ static std::vector<PlanOverride> parse_plan_overrides(const std::string& str) {
 // the environment's overrides win over the regime set at run time
 // (set_conv32_plan_overrides: the co-located learners' plans)
 static std::vector<PlanOverride> g_rt_overrides;
+static thread_local bool g_ignore_rt = false;  // plan_conv32_table: the table / model plan alone
 static const std::vector<PlanOverride>& plan_overrides() {
   static const char* env = std::getenv("MFL_C32_PLANS");
   static const std::vector<PlanOverride> v = env ? parse_plan_overrides(env) : std::vector<PlanOverride>{};
-  return env ? v : g_rt_overrides;
+  static const std::vector<PlanOverride> none;
+  return env ? v : (g_ignore_rt ? none : g_rt_overrides);
 }
 
 static void tuned_plan(const ConvGeom& g, int mode, int& bm, int& bn, int& sp) {
@@ -1248,6 +1250,13 @@ static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
   best.par_mc = par && mode == 1 ? g.N * (g.P / 2) * (g.Q / 2) : 0;
   if (best_t >= 1e30) best.kchunk = 0;  // no feasible tile
   return best;
+}
+
+ConvPlan plan_conv32_table(const ConvGeom& g, int mode) {
+  g_ignore_rt = true;
+  const ConvPlan p = plan_conv32(g, mode);
+  g_ignore_rt = false;
+  return p;
 }
 
 ConvPlan plan_conv32(const ConvGeom& g, int mode) {

@@ -58,10 +58,6 @@ class CoLocatedLearners:
         self.streams = (self._make_streams(dev, len(self.nets)) if self.cuda else [None] * len(nets))
         if self.cuda:
             self.apply_kernel_regime(len(self.nets))
-        if self.cuda and len(self.nets) >= self.tconv_min_learners and self.tconv:
-            for net in self.nets:
-                if hasattr(net, "set_throughput_conv"):
-                    net.set_throughput_conv(True)
         self._ev = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                      for _ in self.nets] if self.cuda else None)
         self._ev2 = [torch.cuda.Event(enable_timing=True) for _ in self.nets] if self.cuda else None
@@ -96,14 +92,6 @@ class CoLocatedLearners:
     # MFL_COLOC_PLANS="" keeps the table; MFL_C32_PLANS overrides both.
     plans = os.environ.get("MFL_COLOC_PLANS", "1,16,128,128,3,1,1;1,8,256,256,3,1,2;1,16,128,256,3,2,1;"
                                               "1,8,256,512,3,2,2;1,8,256,512,1,2,1")
-    # MFL_COLOC_TCONV=1: the 3x3 / stride-1 backward GEMMs run as the
-    # throughput kernels (tconv.hip, StaticNet.set_throughput_conv) instead of
-    # the paired latency-regime launches.  Off by default: faster per call in
-    # isolation (8 learners' launches over 4 streams: ~10 us per wgrad or
-    # dgrad vs ~23 us per pair) but slower in the co-located step (0.690 ->
-    # 0.747 ms per update of the GPU, profiles/r5/tconv/)
-    tconv = os.environ.get("MFL_COLOC_TCONV", "0") == "1"
-    tconv_min_learners = int(os.environ.get("MFL_COLOC_TCONV_MIN", "4"))
 
     hconv_skip = os.environ.get("MFL_COLOC_HCONV_SKIP", "4")  # see configure_regime
 

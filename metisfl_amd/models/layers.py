@@ -82,19 +82,6 @@ class Workspace:
     def need_split(self, n: int) -> None:
         self.split_floats = max(self.split_floats, n)
 
-    # split-K slab floats / arrival tickets of the throughput convolutions: a
-    # buffer of their own (conv32's split-K launches keep their arrival
-    # tickets at the head of ``split`` and need them zero between launches)
-    tc_floats = 0
-    tc_counts = 0
-    # co-located regime: 3x3 / stride-1 backward GEMMs on the throughput
-    # kernels (ops/nn.py conv_backward_pair ``throughput``)
-    throughput = False
-
-    def need_tc(self, floats: int, counters: int) -> None:
-        self.tc_floats = max(self.tc_floats, floats)
-        self.tc_counts = max(self.tc_counts, counters)
-
     def take_acc(self, n: int) -> tuple[int, int]:
         off = self.acc_len
         self.acc_len += (n + 1) // 2 * 2  # keep 16-B alignment of every slice
@@ -107,8 +94,6 @@ class Workspace:
         self.split = torch.zeros(max(4, self.split_floats), dtype=torch.float32, device=device)
         self.split2 = torch.zeros(max(4, self.split_floats), dtype=torch.float32, device=device)
         self.bn_acc = torch.zeros(max(2, self.acc_len), dtype=torch.float64, device=device)
-        self.tc_slab = torch.zeros(max(4, self.tc_floats), dtype=torch.float32, device=device)
-        self.tc_counters = torch.zeros(max(64, self.tc_counts), dtype=torch.int32, device=device)
         # Side stream for work that is off the critical path (weight gradients,
         # projection shortcuts).  Forked/joined with stream waits, so inside a
         # captured hipGraph these become parallel branches that fill CUs the
@@ -301,9 +286,6 @@ class ConvBN(Layer):
         self.pw = K.conv_plan(2, s, dev, ws.dtype)
         ws.need_split(self.pf.workspace)
         ws.need_split(self.pd.workspace)
-        if dev.type == "cuda" and ws.dtype == torch.float32 and K.tconv_shape_ok(s):
-            # throughput backward (co-located learners, ops/nn.py set_throughput_conv)
-            ws.need_tc(*K.tconv_workspace(s))
         # halo conv with the fused BN fill: fp32 activations with bf16x3
         # products on the GPU (or FUSED_FILL_CPU for the host-side tests), or
         # the bf16 option's activations with plain bf16 products
@@ -442,15 +424,9 @@ class ConvBN(Layer):
         # the optimizer launch), so split-K slices accumulate atomically
         if dx is not None and not self.ws.overlap:
             # both GEMMs in one launch (their workgroups share the CUs); the
-            # fp32 launch also carries the next optimizer tail, if any.  The
-            # throughput kernels (co-located regime) carry none: the step's
-            # last optimizer launch takes the rest
-            tput = self.ws.throughput and K.throughput_backward_ok(self.dz, pk, self.xp, self.wp, s)
-            opt = None if tput else self.ws.take_opt_tail()
-            K.conv_backward_pair(self.x, self.dz, self.dw, self.w16, dx, s,
-                                 self.ws.tc_slab if tput else self._split(), accumulate,
-                                 bnb=bnb, wp=self.wp, dy_packed=pk, xp=self.xp, opt=opt,
-                                 counters=self.ws.tc_counters if tput else None, throughput=tput)
+            # fp32 launch also carries the next optimizer tail, if any
+            K.conv_backward_pair(self.x, self.dz, self.dw, self.w16, dx, s, self._split(), accumulate,
+                                 bnb=bnb, wp=self.wp, dy_packed=pk, xp=self.xp, opt=self.ws.take_opt_tail())
             return
         with self.ws.fork():
             K.conv_wgrad(self.x, self.dz, self.dw, s, accumulate=True, dy_packed=pk, xp=self.xp)

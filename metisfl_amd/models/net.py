@@ -255,17 +255,6 @@ class StaticNet:
     def use_graphs(self) -> bool:
         return self.device.type == "cuda"
 
-    def set_throughput_conv(self, on: bool) -> None:
-        """Co-located regime (models/colocated.py): this model's 3x3 /
-        stride-1 backward GEMMs run as the throughput kernels (tconv.hip)
-        instead of the latency-regime paired launches.  Captured step graphs
-        are dropped when the choice changes (they re-capture on next use)."""
-        on = bool(on) and self.device.type == "cuda"
-        if on != self.ws.throughput:
-            self.ws.throughput = on
-            self._train_graph = self._train_graph_k = None
-            self._train_graph_ds = None
-
     # Updates per captured train graph: a K-update graph replays K steps per
     # host launch (the batch gather reads the device step counter, so the
     # steps need nothing from the host); chunks never cross an epoch boundary,

@@ -150,9 +150,6 @@ class TorchNet:
         """User modules run eagerly (arbitrary Python control flow is not a
         capturable static graph)."""
 
-    def set_throughput_conv(self, on: bool) -> None:  # static-model knob (models/colocated.py)
-        return
-
     def _accumulate(self, stats: torch.Tensor, out: torch.Tensor, yb: torch.Tensor, loss: torch.Tensor) -> None:
         n = yb.shape[0]
         stats[0] += loss.detach().double() * n

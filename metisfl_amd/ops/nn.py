@@ -28,6 +28,8 @@ runs "fp32" Keras models on by default on Ampere-class GPUs).
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import torch
@@ -50,31 +52,6 @@ def set_conv_products(mode: str) -> None:
 
 def conv_products() -> str:
     return CONV_PRODUCTS[ops().conv32_mode()]
-
-
-# Co-located regime (models/colocated.py): the 3x3 / stride-1 backward GEMMs
-# of the fp32 / bf16x3 path can run as the throughput kernels (tconv.hip:
-# 4-wave 128 x 128 tiles on the pair-expanded packed operands, separate wgrad
-# and dgrad launches) instead of the latency-regime paired launch
-# (conv32.hip).  Measured with 8 learners' launches over 4 streams
-# (profiles/r5/tconv/): ~10 us per wgrad or dgrad call against ~23 us per
-# paired call.  Chosen per model (layers.Workspace.throughput, set by
-# StaticNet.set_throughput_conv).
-_TCONV_OK: dict = {}
-
-
-def tconv_shape_ok(shp: ConvShape) -> bool:
-    """Whether the throughput kernels take this layer shape."""
-    key = shp.args()
-    if key not in _TCONV_OK:
-        _TCONV_OK[key] = bool(ops().tconv_backward_ok(*key))
-    return _TCONV_OK[key]
-
-
-def tconv_workspace(shp: ConvShape) -> tuple[int, int]:
-    """(split-K slab floats, arrival-counter ints) of the throughput dgrad."""
-    f, c = ops().tconv_workspace(*shp.args())
-    return int(f), int(c)
 
 
 def out_dim(n: int, k: int, stride: int, pad: int) -> int:
@@ -260,18 +237,9 @@ def conv_forward_pair(x, w1, y1, ws1, stats1, w2, y2, ws2, stats2, shp: ConvShap
     conv_forward(x, w2, y2, ConvShape(shp.N, shp.H, shp.W, shp.C, shp.Co, 1, 1, 2, 0), ws2, stats2)
 
 
-def throughput_backward_ok(dy, dy_packed: bool, xp, wp, shp: ConvShape) -> bool:
-    """Whether a layer's backward can run the throughput kernels (tconv.hip):
-    packed bf16x3 operands of a 3x3 / stride-1 fp32 layer.  The one predicate
-    both the caller (which picks the workspace and optimizer tail) and
-    :func:`conv_backward_pair` (which picks the kernel) use."""
-    return (dy.is_cuda and dy.dtype == torch.float32 and bool(dy_packed) and xp is not None
-            and wp is not None and conv_products() == "bf16x3" and tconv_shape_ok(shp))
-
-
 def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bool = False,
                        bnb: BnBwdTarget | None = None, wp=None, dy_packed: bool = False, xp=None,
-                       opt=None, counters=None, throughput: bool = False) -> None:
+                       opt=None) -> None:
     """A layer's weight gradient (dw += ..., dw zero on entry) and input
     gradient (as conv_dgrad) -- on the GPU in ONE paired launch, so the two
     independent, latency-bound GEMMs share the CUs (conv.hip
@@ -280,16 +248,7 @@ def conv_backward_pair(x, dy, dw, w, dx, shp: ConvShape, ws=None, accumulate: bo
     tiles on the fast address paths; MFL_C32_PAIR=0 for two launches).
     ``opt`` (ops.optim.OptRange): an optimizer step over a range whose
     gradients are final, run by extra workgroups of the fp32 paired launch
-    (elsewhere: its own launch after the pair).  ``throughput`` (co-located
-    regime): 3x3 / stride-1 layers with packed operands run the throughput
-    kernels instead (``counters``: their split-K arrival tickets, int32, zero
-    between launches)."""
-    if throughput and throughput_backward_ok(dy, dy_packed, xp, wp, shp):
-        f = (bnb.z, bnb.y, bnb.mean, bnb.invstd, bnb.acc) if bnb is not None else (None,) * 5
-        ops().tconv_backward(xp, dy, dw, wp, dx, ws, counters, *shp.args(), accumulate, *f)
-        if opt is not None:
-            opt.run()
-        return
+    (elsewhere: its own launch after the pair)."""
     if dy.is_cuda and dy.dtype == torch.float32:
         dy = _dy_arg(dy, dy_packed)
         xa = x if xp is None else xp

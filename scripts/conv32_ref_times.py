@@ -1,6 +1,6 @@
 """Per-call device time of the latency-regime fp32 (bf16x3) backward kernels
 (conv32.hip: dgrad, wgrad and the paired launch) at the 3x3 / stride-1
-ResNet-18 CIFAR shapes, for same-box comparison with scripts/tconv_check.cpp.
+ResNet-18 CIFAR shapes (graph-replayed, one stream and 8 learners' launches over 4 streams).
 python scripts/conv32_ref_times.py [batch] [iters]"""
 import os
 import sys

@@ -28,8 +28,6 @@ def main():
     ap.add_argument("--dtype", default="fp32", choices=("fp32", "bf16"))
     ap.add_argument("--serial", action="store_true", help="one stream (baseline)")
     ap.add_argument("--hw-queues", type=int, default=0)
-    ap.add_argument("--tconv", type=int, default=0,
-                    help="1: the throughput backward kernels (tconv.hip), as CoLocatedLearners sets from 4 learners")
     ap.add_argument("--stagger-us", type=float, default=0.0,
                     help="delay stream g's first launch by (g %% 4) x this many microseconds (phase offset)")
     ap.add_argument("--cu-mask", choices=("none", "contig", "interleave"), default="none",
@@ -57,8 +55,6 @@ def main():
         ns = max(1024, 16 * a.batch)  # >= 2 x K steps per epoch: the K-update graph gets captured
         x = torch.randn((ns, 32, 32, 3), generator=gen, device="cuda")
         y = torch.randint(0, 10, (ns,), generator=gen, device="cuda")
-        if a.tconv:
-            net.set_throughput_conv(True)
         nets.append(net)
         dss.append(net.make_dataset(x, y, seed=i))
     for net, ds in zip(nets, dss):  # capture (1-step and K-step graphs)

@@ -392,18 +392,32 @@ def _x8(x):
     return F.pad(torch.as_tensor(x), (0, 5))
 
 
-@pytest.mark.parametrize("conv_products", ["exact", "bf16x3", "bf16x3_halo_dgrad", "bf16x3_throughput"])
+@pytest.mark.parametrize("conv_products", ["exact", "bf16x3", "bf16x3_halo_dgrad", "bf16x3_coloc"])
 def test_fp32_resnet18_step_matches_torch_nn(conv_products, monkeypatch):
     """The whole fp32 training step (gather -> 20 conv/BN layers -> head ->
     backward) vs an independent torch.nn ResNet-18 in fp64, for both fp32
     convolution product modes (and the opt-in halo dgrad backward, and the
-    co-located regime's throughput backward kernels, tconv.hip)."""
+    co-located regime's kernel choices: models/colocated.py configure_regime
+    -- fewer split-K slices for the input gradients, im2col at 4x4x512)."""
     from metisfl_amd.models import layers as L
+    from metisfl_amd.models.colocated import CoLocatedLearners
     from metisfl_amd.models.resnet import ResNet18
-    throughput = conv_products.endswith("_throughput")
+    from metisfl_amd.ops._native import ops
+    coloc = conv_products.endswith("_coloc")
     if conv_products.endswith("_halo_dgrad"):
         monkeypatch.setattr(L, "HALO_DGRAD", True)
-    conv_products = conv_products.split("_")[0]
+    if coloc:
+        monkeypatch.setattr(L, "HCONV_SKIP", {4})
+        ops().set_conv32_plan_overrides(CoLocatedLearners.plans)
+    try:
+        _step_vs_torch_nn(conv_products.split("_")[0])
+    finally:
+        if coloc:
+            ops().set_conv32_plan_overrides("")
+
+
+def _step_vs_torch_nn(conv_products):
+    from metisfl_amd.models.resnet import ResNet18
     from metisfl_amd.ops.optim import OptimizerSpec
     from tests.torch_resnet_ref import reference_step
     rng = np.random.default_rng(0)
@@ -413,8 +427,6 @@ def test_fp32_resnet18_step_matches_torch_nn(conv_products, monkeypatch):
     net = ResNet18(batch_size=B, device=DEV, optimizer=OptimizerSpec("vanilla_sgd", 0.0), seed=4,
                    conv_products=conv_products)
     assert net.compute_dtype == torch.float32
-    if throughput:
-        net.set_throughput_conv(True)
     values = net.state.to_numpy()
     ds = net.make_dataset(x, y, shuffle=False)
     net.zero_grad_in_optimizer = False
