@@ -233,6 +233,8 @@ class DriverSessionBase:
         if learner_instance.devices:
             extra["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in learner_instance.devices)
         ssh = self.federation_environment.launcher == "ssh"
+        if not ssh and not learner_instance.devices:  # host-CPU learners of this machine share its cores
+            extra.update(self._cpu_share(len(self.federation_environment.learners)))
         return self._spawn(f"learner_{learner_instance.learner_id}",
                            self._init_learner_cmd(learner_instance, controller_instance), extra,
                            remote=learner_instance if ssh else None)
@@ -384,8 +386,18 @@ class DriverSessionBase:
             extra["METISFL_WATCHDOG_REPORT_DIR"] = self._watchdog_dir(tag)
             if self.device == "cpu":
                 extra.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+                extra.update(self._cpu_share(len(groups)))
             self._spawn(self._proc_name(g), [sys.executable, "-m", "metisfl_amd.learner.collective", job], extra)
         self._collective_tag = tag
+
+    @staticmethod
+    def _cpu_share(n_procs: int) -> dict:
+        """CPU ranks on one host split its cores: n processes each starting one
+        OpenMP thread per core oversubscribe n-fold, and spin-waiting barriers
+        make that far slower than n-fold.  A user's OMP_NUM_THREADS wins."""
+        if "OMP_NUM_THREADS" in os.environ:
+            return {}
+        return {"OMP_NUM_THREADS": str(max(1, (os.cpu_count() or 1) // max(1, n_procs)))}
 
     @staticmethod
     def _proc_name(group) -> str:
