@@ -126,4 +126,5 @@ def main() -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    from metisfl_amd.utils.launch import exit_process
+    exit_process(main())  # no interpreter finalisation behind live c10d threads (utils/launch.py)

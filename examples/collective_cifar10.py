@@ -74,3 +74,5 @@ def main():
 if __name__ == "__main__":
     torch.set_num_threads(max(1, torch.get_num_threads()))
     main()
+    from metisfl_amd.utils.launch import exit_process
+    exit_process(0)  # no interpreter finalisation behind live c10d threads (utils/launch.py)

@@ -314,4 +314,5 @@ def _main(argv, ctx: dict) -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    from metisfl_amd.utils.launch import exit_process
+    exit_process(main())  # no interpreter finalisation behind live c10d threads (utils/launch.py)

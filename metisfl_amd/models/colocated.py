@@ -63,6 +63,7 @@ class CoLocatedLearners:
         self._ev2 = [torch.cuda.Event(enable_timing=True) for _ in self.nets] if self.cuda else None
         self.last_eval_ms: list[float] = []   # device ms of each learner's test evaluation (train(eval_dss=...))
         self.last_span_ms = 0.0               # first start -> last evaluation end
+        self.last_host_ms: dict = {}          # host-side phases of the last train() call
         # learners dropped from the last elastic round whose already-issued
         # chunks may still be running on their streams: the round closed
         # without waiting for them, so the current stream is NOT ordered after
@@ -183,12 +184,18 @@ class CoLocatedLearners:
         last update -- an early finisher's evaluation overlaps the others'
         training -> (ms, [metrics or None per learner])."""
         import time
+        th = [time.perf_counter()]
+        lead = None
+        if self.cuda:  # how long the device is still busy with earlier work when this call starts
+            lead = torch.cuda.Event(enable_timing=True)
+            lead.record()
         # capture before the streams run concurrently (a capture synchronises
         # the device)
         for net, ds, n in zip(self.nets, self.train_dss, nsteps):
             net.prepare_graphs(ds, n)
         self._fork()
         t0 = time.perf_counter()
+        th.append(t0)
         if self.cuda:
             for j in range(len(self)):
                 with self._ctx(j):
@@ -214,11 +221,13 @@ class CoLocatedLearners:
                             if self.cuda:
                                 self._ev2[j].record()
             live = nxt
+        th.append(time.perf_counter())
         self._join()
         self.pending = set()
         if self.cuda:
             for _, e1 in self._ev:
                 e1.synchronize()
+            th.append(time.perf_counter())
             ms = [e0.elapsed_time(e1) for e0, e1 in self._ev]
             if eval_dss is not None:
                 # device time of each learner's test evaluation, and from the
@@ -230,9 +239,15 @@ class CoLocatedLearners:
                 self.last_span_ms = max((self._ev[0][0].elapsed_time(self._ev2[j]) for j in ev), default=0.0)
         else:
             ms = host_ms
-        if eval_dss is None:
-            return ms
-        return ms, [n.finish_evaluate(o) if o is not None else None for n, o in zip(self.nets, owners)]
+            th.append(time.perf_counter())
+        res = None if eval_dss is None else \
+            [n.finish_evaluate(o) if o is not None else None for n, o in zip(self.nets, owners)]
+        th.append(time.perf_counter())
+        self.last_host_ms = {k: round((b - a) * 1e3, 3) for k, a, b in
+                             zip(("prepare", "issue", "wait", "finish_eval"), th, th[1:])}
+        if lead is not None:
+            self.last_host_ms["device_lead"] = round(lead.elapsed_time(self._ev[0][0]), 3)
+        return ms if eval_dss is None else (ms, res)
 
     def train_elastic(self, nsteps: list[int], step_offsets: list[int], stop, on_finish, poll_steps: int = 64,
                       slow_s: list[float] | None = None, poll_s: float = 0.005):

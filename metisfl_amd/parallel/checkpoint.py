@@ -197,7 +197,14 @@ class AsyncSnapshot:
             except BaseException as e:  # noqa: BLE001 - re-raised by wait()
                 self._error = e
 
-        self._thread = threading.Thread(target=run, name=self.name, daemon=True)
+        # not a daemon: the interpreter joins it before finalising.  A daemon
+        # writer still inside a torch / numpy call (GIL released) when the
+        # process exits is force-unwound through noexcept C++ frames at
+        # finalisation -> std::terminate, SIGABRT after a successful run (seen
+        # as "terminate called without an active exception", ~1 in 60
+        # two-rank runs, traced to this thread with a terminate-handler
+        # backtrace).
+        self._thread = threading.Thread(target=run, name=self.name, daemon=False)
         self._thread.start()
         self.last_stage_ms = (time.perf_counter() - t0) * 1e3
         return self.last_stage_ms

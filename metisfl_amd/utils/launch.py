@@ -39,3 +39,46 @@ def ensure_world(gpus: int, script: str, argv: list[str] | None = None, tag: str
         print(f"[{tag}] error: --gpus {gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
         return 2
     return None
+
+
+def exit_process(code: int | None = 0) -> None:
+    """End a rank process WITHOUT interpreter finalisation, once its work is
+    done: non-daemon threads are joined, logs and stdio flushed, then
+    ``os._exit``.
+
+    Why: a torch.distributed worker thread (gloo's ``runLoop``, after the
+    last barrier has already released the main thread) can still be dropping
+    the last C++ reference to a tensor whose Python object it must decref.
+    If that lands while the interpreter is finalising, Python force-exits the
+    thread through noexcept C++ frames -> ``std::terminate`` -> SIGABRT, after
+    a run that succeeded (~1 in 60 two-rank CPU runs under load; traced with
+    a terminate-handler backtrace to ``ProcessGroupGloo::runLoop`` ->
+    ``TensorImpl::decref_pyobject`` -> ``PyEval_AcquireThread`` ->
+    ``pthread_exit``).  A launcher (torchrun, the driver, the test harness)
+    would count that rank as failed."""
+    import logging
+    import threading
+    me = threading.current_thread()
+    for t in threading.enumerate():
+        if t is not me and not t.daemon:
+            t.join()
+    logging.shutdown()
+    for s in (sys.stdout, sys.stderr):
+        try:
+            s.flush()
+        except Exception:  # noqa: BLE001 - closed stream: nothing to flush
+            pass
+    os._exit(int(code or 0))
+
+
+def exits_hard(fn):
+    """Decorator for ``torch.multiprocessing`` rank functions: a rank that
+    returns normally leaves through ``exit_process(0)``; an exception still
+    propagates to the spawn wrapper (which records it and exits 1)."""
+    import functools
+
+    @functools.wraps(fn)
+    def rank_main(*args, **kwargs):
+        fn(*args, **kwargs)
+        exit_process(0)
+    return rank_main

@@ -10,6 +10,8 @@ import numpy as np
 import torch
 import torch.multiprocessing as mp
 
+from metisfl_amd.utils.launch import exits_hard
+
 
 def _free_port():
     with socket.socket() as s:
@@ -17,6 +19,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
+@exits_hard  # a finished rank skips interpreter finalisation (utils/launch.py)
 def _worker(rank, world, port, out_dir, staleness="none", threaded=True):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -95,6 +98,7 @@ def test_async_staleness_aware_weights(tmp_path):
     assert r0["max_err"] < 1e-5
 
 
+@exits_hard  # a finished rank skips interpreter finalisation (utils/launch.py)
 def _coloc_worker(rank, world, port, out_dir, per_rank, tasks):
     """Rank r hosts ``per_rank`` co-located learners (global ids r*per_rank + j)."""
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
@@ -155,6 +159,7 @@ def test_async_fedrec_colocated_learners_on_two_ranks(tmp_path):
         assert all(np.all(np.isfinite(f)) for f in res["finals"])
 
 
+@exits_hard  # a finished rank skips interpreter finalisation (utils/launch.py)
 def _secure_worker(rank, world, port, out_dir, per_rank, tasks):
     """Secure aggregation (CKKS PWA) with the asynchronous protocol: every
     learner records the plaintext model it submitted (test hook) so the test

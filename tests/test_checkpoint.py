@@ -11,6 +11,7 @@ import pytest
 import torch
 
 from metisfl_amd.parallel import checkpoint as ck
+from metisfl_amd.utils.launch import exits_hard
 
 
 def test_snapshot_is_taken_at_submit_time(tmp_path):
@@ -112,6 +113,7 @@ def test_native_federated_model_writer_matches_python_proto(tmp_path):
     assert got == ref
 
 
+@exits_hard  # a finished rank skips interpreter finalisation (utils/launch.py)
 def _publish_worker(rank, world, port, out_dir):
     import torch.distributed as dist
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),

@@ -12,6 +12,8 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
+from metisfl_amd.utils.launch import exits_hard
+
 
 def _free_port():
     with socket.socket() as s:
@@ -19,6 +21,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
+@exits_hard  # a finished rank skips interpreter finalisation (utils/launch.py)
 def _worker(rank, world, port, out_dir, mode):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -155,6 +158,7 @@ def test_checkpoint_resume_reproduces_the_next_round(tmp_path):
     assert np.allclose(straight, resumed, rtol=1e-6, atol=1e-7)
 
 
+@exits_hard  # a finished rank skips interpreter finalisation (utils/launch.py)
 def _wd_worker(rank, world, port, out_dir):
     import time as _t
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),

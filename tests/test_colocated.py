@@ -14,6 +14,8 @@ import numpy as np
 import torch
 import torch.multiprocessing as mp
 
+from metisfl_amd.utils.launch import exits_hard
+
 N_LEARNERS = 4
 
 
@@ -29,6 +31,7 @@ def _shard(gi):
     return rng.standard_normal((n, 32, 32, 3)).astype(np.float32), rng.integers(0, 10, n), n
 
 
+@exits_hard  # a finished rank skips interpreter finalisation (utils/launch.py)
 def _worker(rank, world, port, out_dir, mode):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))

@@ -16,6 +16,8 @@ import numpy as np
 import torch
 import torch.multiprocessing as mp
 
+from metisfl_amd.utils.launch import exits_hard
+
 
 def _free_port():
     with socket.socket() as s:
@@ -28,6 +30,7 @@ def _shard(rank, n):
     return rng.standard_normal((n, 32, 32, 3)).astype(np.float32), rng.integers(0, 10, n)
 
 
+@exits_hard  # a finished rank skips interpreter finalisation (utils/launch.py)
 def _worker(rank, world, port, out_dir, mode):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -83,6 +86,7 @@ def _worker(rank, world, port, out_dir, mode):
     comm.close()
 
 
+@exits_hard  # a finished rank skips interpreter finalisation (utils/launch.py)
 def _coloc_worker(rank, world, port, out_dir, L, slow, ratio, device="cpu", poison=False):
     """``L`` co-located learners per rank (global learner g = rank * L + j,
     shard of 8 + 4 g examples); learner ``slow`` is deliberately slow.
