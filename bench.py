@@ -255,7 +255,8 @@ def main() -> int:
         out["last_round_device_ms"] = {"train_max": float(timed[-1].train_ms),
                                        "test_eval_per_learner": [round(x, 2) for x in fed.group.last_eval_ms],
                                        "first_start_to_last_eval_end": fed.group.last_span_ms,
-                                       "host_phases": fed.group.last_host_ms}
+                                       "host_phases": fed.group.last_host_ms,
+                                       "train_per_learner": fed.group.last_ms}
     out["phase_ms_mean"] = ({k: sum(r.phase_ms[k] for r in timed) / len(timed) for k in timed[0].phase_ms}
                             if timed and timed[0].phase_ms else None)
     out["community_eval"] = ("deferred: on a frozen copy of each community model, overlapping the next round's "

@@ -64,6 +64,7 @@ class CoLocatedLearners:
         self.last_eval_ms: list[float] = []   # device ms of each learner's test evaluation (train(eval_dss=...))
         self.last_span_ms = 0.0               # first start -> last evaluation end
         self.last_host_ms: dict = {}          # host-side phases of the last train() call
+        self.last_ms: list[float] = []        # per learner: start -> last update (train())
         # learners dropped from the last elastic round whose already-issued
         # chunks may still be running on their streams: the round closed
         # without waiting for them, so the current stream is NOT ordered after
@@ -243,6 +244,7 @@ class CoLocatedLearners:
         res = None if eval_dss is None else \
             [n.finish_evaluate(o) if o is not None else None for n, o in zip(self.nets, owners)]
         th.append(time.perf_counter())
+        self.last_ms = [round(float(x), 2) for x in ms]
         self.last_host_ms = {k: round((b - a) * 1e3, 3) for k, a, b in
                              zip(("prepare", "issue", "wait", "finish_eval"), th, th[1:])}
         if lead is not None:
