@@ -32,7 +32,7 @@ import torch
 def configure_regime(learners_per_gpu: int) -> None:
     """Kernel choices for ``learners_per_gpu`` learners sharing each GPU, made
     BEFORE their models are built (the layer plans and workspaces are fixed
-    at build): with 4+ co-located learners the 4x4x512 layers run the im2col
+    at build): with 2+ co-located learners the 4x4x512 layers run the im2col
     convolution instead of the halo conv (8-slice split-K at one workgroup
     per CU: 0.6684 -> 0.6634 and 0.6823 -> 0.6737 ms per update with 8
     learners on two boxes, profiles/r6/bench/hconv_skip*.log; the one-learner
@@ -81,7 +81,9 @@ class CoLocatedLearners:
     # set_conv32_pair_ring).  Process-wide, set before the learners capture
     # their graphs.  MFL_COLOC_PAIR_RING=0 keeps the build default.
     pair_ring = os.environ.get("MFL_COLOC_PAIR_RING", "2")
-    pair_ring_min_learners = int(os.environ.get("MFL_COLOC_PAIR_RING_MIN", "4"))
+    # from 2 learners on (the bench's N = 4 point: 0.8006 -> 0.7965 ms per
+    # update, 3 alternating repeats, profiles/r6/bench/two_learner_regime_ab.log)
+    pair_ring_min_learners = int(os.environ.get("MFL_COLOC_PAIR_RING_MIN", "2"))
     # ... and the input gradients split their reduction into fewer slices
     # than the one-learner table (fewer, fuller workgroups when other
     # learners' launches fill the CUs): the 16x16x128 / 8x8x256 3x3 ones 1 / 2
