@@ -52,17 +52,26 @@ void gemm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::optional<t
 // run split-K through an fp32 slab workspace taken from the caching
 // allocator on the current stream (stream-ordered: co-located learners on
 // their own streams, and graph capture, get their own).
+// resid: dx = dy w + resid (the residual branch's gradient added in the
+// output stage; not together with accumulate)
 void gemm_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, int64_t M, int64_t N, int64_t K,
-                bool accumulate) {
+                bool accumulate, c10::optional<torch::Tensor> resid) {
   dense_dims(M, N, K);
   need(dy, torch::kBFloat16, M * N, "dy");
   need(w, torch::kBFloat16, N * K, "w");
   need(dx, torch::kBFloat16, M * K, "dx");
+  const uint16_t* rp = nullptr;
+  if (resid.has_value()) {
+    TORCH_CHECK(!accumulate, "gemm_dgrad: resid and accumulate are exclusive");
+    need(*resid, torch::kBFloat16, M * K, "resid");
+    TORCH_CHECK(resid->data_ptr() != dx.data_ptr(), "gemm_dgrad: resid must not alias dx");
+    rp = bfp(*resid);
+  }
   const int64_t wsn = mfl::gemm_dgrad_workspace((int)M, (int)N, (int)K);
   torch::Tensor ws;
   if (wsn > 0) ws = torch::empty({wsn}, dy.options().dtype(torch::kFloat32));
   mfl::launch_gemm_dgrad(bfp(dy), bfp(w), bfp(dx), (int)M, (int)N, (int)K, accumulate, stream_of(dy),
-                         wsn > 0 ? ws.data_ptr<float>() : nullptr);
+                         wsn > 0 ? ws.data_ptr<float>() : nullptr, rp);
 }
 
 // dz = (dy w) * gelu'(z); dbias += colsum(dz)  (FFN1 backward, one launch)
@@ -381,7 +390,9 @@ void register_bert(pybind11::module& m) {
   m.def("gemm_fwd", &gemm_fwd);
   m.def("set_gemm_big", [](bool on) { mfl::set_gemm_big(on ? 1 : 0); });
   m.def("gemm_big_enabled", []() { return mfl::gemm_big_enabled() != 0; });
-  m.def("gemm_dgrad", &gemm_dgrad);
+  m.def("gemm_dgrad", &gemm_dgrad, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("dx"), pybind11::arg("M"),
+        pybind11::arg("N"),
+        pybind11::arg("K"), pybind11::arg("accumulate"), pybind11::arg("resid") = pybind11::none());
   m.def("gemm_dgrad_workspace",
         [](int64_t M, int64_t N, int64_t K) { return mfl::gemm_dgrad_workspace((int)M, (int)N, (int)K); });
   m.def("gemm_dgrad_gelu", &gemm_dgrad_gelu);

@@ -1188,7 +1188,7 @@ static void tuned_plan(const ConvGeom& g, int mode, int& bm, int& bn, int& sp) {
     }
 }
 
-static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
+static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par, bool use_table) {
   const int rows = mode == 2 ? g.Ng : g.M;
   const int cols = mode == 2 ? g.K : g.Ng;
   int kred = mode == 2 ? g.M : g.K;
@@ -1202,7 +1202,7 @@ static ConvPlan plan_conv32_impl(const ConvGeom& g, int mode, bool allow_par) {
   // fewer when co-located learners' launches share the CUs (MFL_C32_SLOTS,
   // A/B runs).  The measured plan table assumes the whole chip.
   const int slots_env = env_int("MFL_C32_SLOTS", 256);
-  if (!fb && !fn && !fs && slots_env == 256) tuned_plan(g, mode, fb, fn, fs);
+  if (use_table && !fb && !fn && !fs && slots_env == 256) tuned_plan(g, mode, fb, fn, fs);
   const double clk = 2.4e3;  // cycles per us
   ConvPlan best;
   double best_t = 1e30;
@@ -1262,8 +1262,14 @@ ConvPlan plan_conv32_table(const ConvGeom& g, int mode) {
 ConvPlan plan_conv32(const ConvGeom& g, int mode) {
   // parity-class dgrad needs class sizes that are whole tiles; otherwise the
   // masked stride-aware gather
-  ConvPlan p = plan_conv32_impl(g, mode, true);
-  if (p.kchunk == 0) p = plan_conv32_impl(g, mode, false);
+  ConvPlan p = plan_conv32_impl(g, mode, true, true);
+  if (p.kchunk == 0) p = plan_conv32_impl(g, mode, false, true);
+  // a split the table / overrides force can be infeasible at another batch
+  // size (the overrides are batch independent: the co-located regime's 2-way
+  // 8x8x256 dgrad split has 2,048 tiles at batch 512, past the counter block
+  // of an in-launch split-K reduce) -- then the throughput model decides
+  if (p.kchunk == 0) p = plan_conv32_impl(g, mode, true, false);
+  if (p.kchunk == 0) p = plan_conv32_impl(g, mode, false, false);
   return p;
 }
 

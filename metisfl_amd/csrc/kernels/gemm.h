@@ -20,11 +20,12 @@ void launch_gemm_nt(const uint16_t* a, const uint16_t* b, uint16_t* c, const flo
 //   y = x W^T + bias (+ resid);  act_out = gelu(y) when given
 void launch_gemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
                      const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s);
-//   dx (+)= dy W
+//   dx (+)= dy W  (+ resid: dx = dy W + resid, the residual branch's gradient
+//   read in the epilogue instead of a copy of it accumulated into)
 //   ws: optional split-K slab workspace of gemm_dgrad_workspace(M, N, K) fp32
 //   elements (long reductions over few output tiles: the MLM decoder)
 void launch_gemm_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
-                       bool accumulate, hipStream_t s, float* ws = nullptr);
+                       bool accumulate, hipStream_t s, float* ws = nullptr, const uint16_t* resid = nullptr);
 int64_t gemm_dgrad_workspace(int M, int N, int K);
 //   dw = dy^T x, or dw += with accumulate (fp32 atomics; split-K plans always
 //   add, so dw must be zero on entry unless accumulating on purpose)
@@ -41,7 +42,7 @@ bool gemm_big_ok(int M, int N, int K);
 void launch_gemm_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
                          const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s);
 void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
-                           bool accumulate, hipStream_t s, float* ws = nullptr);
+                           bool accumulate, hipStream_t s, float* ws = nullptr, const uint16_t* resid = nullptr);
 int gemm_big_dgrad_splits(int M, int N, int K);
 int64_t gemm_big_dgrad_workspace(int M, int N, int K);
 void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,

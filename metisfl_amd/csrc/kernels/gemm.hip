@@ -73,10 +73,14 @@ void launch_gemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const fl
 }
 
 void launch_gemm_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
-                       bool accumulate, hipStream_t s, float* ws) {
+                       bool accumulate, hipStream_t s, float* ws, const uint16_t* resid) {
   if (gemm_big_enabled() && gemm_big_ok(M, K, N)) {
-    launch_gemm_big_dgrad(dy, w, dx, M, N, K, accumulate, s, ws);
+    launch_gemm_big_dgrad(dy, w, dx, M, N, K, accumulate, s, ws, resid);
     return;
+  }
+  if (resid) {  // small shapes (conv-core path): dx = resid, then accumulate
+    (void)hipMemcpyAsync(dx, resid, (size_t)M * K * 2, hipMemcpyDeviceToDevice, s);
+    accumulate = true;
   }
   // dgrad geometry: "dY" has C = N channels, the output dX has Ng = K columns
   ConvGeom g = dense_geom(M, K, N);

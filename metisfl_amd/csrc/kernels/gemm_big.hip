@@ -782,12 +782,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float4* __rest
 
 // bf16 out (+)= sum over the split-K slabs (8 outputs per lane): the output
 // stage of a split long-reduction dgrad (the MLM decoder's 30,528-deep one)
+// add: the bf16 term the slices' sum is added to (out itself when
+// accumulating, a residual gradient, or nothing)
 __global__ __launch_bounds__(256) void splitk_reduce_bf16_kernel(const float4* __restrict__ ws, int splits,
-                                                                 int64_t n8, uint4* __restrict__ out, int accum) {
+                                                                 int64_t n8, uint4* out, const uint4* add) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (accum) unpack8(out[i], v);
+    if (add) unpack8(add[i], v);
     for (int k = 0; k < splits; ++k) {
       const float4 a = ws[(int64_t)k * 2 * n8 + 2 * i], b = ws[(int64_t)k * 2 * n8 + 2 * i + 1];
       v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
@@ -936,7 +938,7 @@ int64_t gemm_big_dgrad_workspace(int M, int N, int K) {
 }
 
 void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
-                           bool accumulate, hipStream_t s, float* ws) {
+                           bool accumulate, hipStream_t s, float* ws, const uint16_t* resid) {
   // dX[M][K] = dY[M][N] . W[N][K]: output columns = K, reduction = N
   BigGemmArgs p{};
   p.a = dy; p.b = w; p.M = M; p.N = K; p.K = N; p.lda = N; p.ldb = K;
@@ -953,10 +955,13 @@ void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, 
     launch_big<false, true, true>(p, N, s);
     const int64_t n8 = (int64_t)M * K / 8;
     splitk_reduce_bf16_kernel<<<stream_grid(n8, 256, 2048), 256, 0, s>>>(
-        reinterpret_cast<const float4*>(ws), p.splits, n8, reinterpret_cast<uint4*>(dx), accumulate ? 1 : 0);
+        reinterpret_cast<const float4*>(ws), p.splits, n8, reinterpret_cast<uint4*>(dx),
+        accumulate ? reinterpret_cast<const uint4*>(dx) : reinterpret_cast<const uint4*>(resid));
     return;
   }
-  p.c16 = dx; p.accum = accumulate;
+  // resid: added in the output stage (big_epilogue), the same single bf16
+  // term an accumulate into a copy of it would add
+  p.c16 = dx; p.accum = accumulate; p.resid = accumulate ? nullptr : resid;
   p.splits = 1; p.kt_per_split = N / GB_KQ;
   launch_big<false, true, false>(p, N, s);
 }

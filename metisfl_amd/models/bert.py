@@ -39,6 +39,10 @@ from metisfl_amd.ops.optim import OptimizerSpec
 # attention-output + QKV weight gradients grouped in one launch (MFL_BERT_WGRAD2=0:
 # two launches, for A/B runs)
 WGRAD2 = os.environ.get("MFL_BERT_WGRAD2", "1") == "1"
+# the residual branch's gradient added in the FFN1 / QKV dgrad output stage
+# (MFL_BERT_RESID_DGRAD=0: the LayerNorm backward writes a second copy of its
+# dx that the dgrad accumulates into -- 25 MB more written per LayerNorm)
+RESID_DGRAD = os.environ.get("MFL_BERT_RESID_DGRAD", "1") == "1"
 
 
 @dataclass
@@ -228,8 +232,11 @@ class BertMLM(StaticNet):
         for i in reversed(range(c.layers)):
             A, p = self.acts[i], f"layer{i}."
             dx = self.g_out[1] if dout is self.g_out[0] else self.g_out[0]
+            # the LN input's gradient g_fo feeds the FFN AND the residual
+            # branch: the FFN1 dgrad below adds it in its output stage (no
+            # second copy of it written here to accumulate into)
             BO.ln_bwd(dout, A["fo"], A["m2"], A["r2"], self._p(p + "ln2.gamma"), self.g_fo, g(p + "ln2.gamma"),
-                      g(p + "ln2.beta"), M, H, dx2=self.g_a, dbias_prev=g(p + "ffn2.b"))
+                      g(p + "ln2.beta"), M, H, dx2=None if RESID_DGRAD else self.g_a, dbias_prev=g(p + "ffn2.b"))
             BO.gemm_wgrad(A["h"], self.g_fo, g(p + "ffn2.w"), M, H, F, zeroed=True)
             # GELU backward + FFN1 bias gradient in the dgrad epilogue: saves the
             # 300 MB round trip of a separate gelu_bwd (scripts/gelu_fuse_probe.py:
@@ -237,9 +244,12 @@ class BertMLM(StaticNet):
             BO.gemm_dgrad_gelu(self.g_fo, self._w(p + "ffn2.w"), self.g_z, A["z"], M, H, F,
                                dbias=g(p + "ffn1.b"))
             BO.gemm_wgrad(A["a"], self.g_z, g(p + "ffn1.w"), M, F, H, zeroed=True)
-            BO.gemm_dgrad(self.g_z, self._w(p + "ffn1.w"), self.g_a, M, F, H, accumulate=True)
+            if RESID_DGRAD:
+                BO.gemm_dgrad(self.g_z, self._w(p + "ffn1.w"), self.g_a, M, F, H, resid=self.g_fo)
+            else:
+                BO.gemm_dgrad(self.g_z, self._w(p + "ffn1.w"), self.g_a, M, F, H, accumulate=True)
             BO.ln_bwd(self.g_a, A["ao"], A["m1"], A["r1"], self._p(p + "ln1.gamma"), self.g_ao, g(p + "ln1.gamma"),
-                      g(p + "ln1.beta"), M, H, dx2=dx, dbias_prev=g(p + "out.b"))
+                      g(p + "ln1.beta"), M, H, dx2=None if RESID_DGRAD else dx, dbias_prev=g(p + "out.b"))
             if not WGRAD2:
                 BO.gemm_wgrad(A["ctx"], self.g_ao, g(p + "out.w"), M, H, H, zeroed=True)
             BO.gemm_dgrad(self.g_ao, self._w(p + "out.w"), self.g_ctx, M, H, H)
@@ -253,7 +263,10 @@ class BertMLM(StaticNet):
                                3 * H, H, M)
             else:
                 BO.gemm_wgrad(A["x"], self.g_qkv, g(p + "qkv.w"), M, 3 * H, H, zeroed=True)
-            BO.gemm_dgrad(self.g_qkv, self._w(p + "qkv.w"), dx, M, 3 * H, H, accumulate=True)
+            if RESID_DGRAD:
+                BO.gemm_dgrad(self.g_qkv, self._w(p + "qkv.w"), dx, M, 3 * H, H, resid=self.g_ao)
+            else:
+                BO.gemm_dgrad(self.g_qkv, self._w(p + "qkv.w"), dx, M, 3 * H, H, accumulate=True)
             dout = dx
         BO.emb_ln_bwd(dout, self.emb_x, self.emb_mean, self.emb_rstd, self._p("emb.ln.gamma"), self.rec,
                       c.rec_stride, B, T, g("emb.word"), g("emb.pos"), g("emb.type"), g("emb.ln.gamma"),

@@ -46,14 +46,17 @@ def gemm_fwd(x, w, y, M, N, K, bias=None, resid=None, act_out=None) -> None:
         _put(act_out, F.gelu(_b(y).reshape(M, N)))
 
 
-def gemm_dgrad(dy, w, dx, M, N, K, accumulate=False) -> None:
-    """dx (+)= dy w."""
+def gemm_dgrad(dy, w, dx, M, N, K, accumulate=False, resid=None) -> None:
+    """dx (+)= dy w; with ``resid``: dx = dy w + resid (a residual branch's
+    gradient added in the output stage, instead of accumulating into a copy)."""
     if dy.is_cuda:
-        ops().gemm_dgrad(dy, w, dx, M, N, K, accumulate)
+        ops().gemm_dgrad(dy, w, dx, M, N, K, accumulate, resid)
         return
     v = _b(dy).reshape(M, N) @ _b(w).reshape(N, K)
     if accumulate:
         v = v + _b(dx).reshape(M, K)
+    if resid is not None:
+        v = v + _b(resid).reshape(M, K)
     _put(dx, v)
 
 

@@ -54,3 +54,32 @@ def test_infeasible_split_override_snaps_to_a_feasible_count():
     weight gradient unwritten)."""
     _, l1, _ = _plans({"MFL_C32_PLANS": "2,32,64,64,3,1,56"})
     assert l1[5] == 54
+
+
+def test_regime_overrides_stay_feasible_at_other_batch_sizes():
+    """The co-located regime's plan overrides are batch independent (set
+    process-wide before the learners' graphs are captured).  At batch 512 -- the
+    evaluation twin of a learner built after the regime was set -- the 2-way
+    8x8x256 dgrad split would have 2,048 tiles, past the in-launch split-K
+    reduce's counter block: the planner must fall back to a feasible plan
+    instead of raising (the GPU suite hit this in test_eval_twin_gpu.py once a
+    two-learner test had set the regime)."""
+    code = """
+from metisfl_amd.models.colocated import CoLocatedLearners
+from metisfl_amd.ops._native import ops
+o = ops(); o.set_conv32_mode(1)
+o.set_conv32_plan_overrides(CoLocatedLearners.plans)
+for s in [(512,8,8,256,256,3,3,1,1), (512,16,16,128,128,3,3,1,1), (32,8,8,256,256,3,3,1,1)]:
+    d = o.conv32_plan(1, *s)
+    print(d[0], d[1], d[2])
+"""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    env.pop("MFL_C32_PLANS", None)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, cwd=ROOT,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    p512, p512b, p32 = [tuple(int(v) for v in l.split()) for l in out.stdout.strip().splitlines()]
+    assert p512[2] >= 1 and p512b[2] >= 1
+    tiles = (512 * 8 * 8 // p512[0]) * (256 // p512[1])
+    assert p512[2] == 1 or tiles <= 1024
+    assert p32 == (64, 64, 2)  # the override itself still applies at batch 32

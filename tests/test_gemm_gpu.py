@@ -159,3 +159,25 @@ def test_dgrad_split_k_uneven_slices():
     _ops().gemm_dgrad(dy, w, dx, M, N, K, False)
     assert torch.isfinite(dx.float()).all()
     assert _rel(dx, dy.float() @ w.float()) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES + [(512, 32000, 768)])
+def test_dgrad_resid_equals_accumulate_into_copy(M, N, K):
+    """dx = dy w + resid (the BERT backward's residual-branch gradient read in
+    the output stage, models/bert.py) is bitwise the old two-step form: a copy
+    of resid accumulated into -- on the plain large-tile path, the split-K
+    slab path (the 32,000-word decoder shape) and the conv-core path."""
+    g = torch.Generator(device="cuda").manual_seed(13 * M + K)
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.05).bfloat16()
+    resid = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    for big in (True, False):
+        _ops().set_gemm_big(big)
+        acc = resid.clone()
+        _ops().gemm_dgrad(dy, w, acc, M, N, K, True)
+        dx = torch.empty_like(resid)
+        _ops().gemm_dgrad(dy, w, dx, M, N, K, False, resid)
+        assert torch.equal(dx, acc), big
+        assert _rel(dx, resid.float() + dy.float() @ w.float()) < 1e-2
+    with pytest.raises(RuntimeError):
+        _ops().gemm_dgrad(dy, w, dx, M, N, K, True, resid)
