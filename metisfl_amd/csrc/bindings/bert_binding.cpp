@@ -33,10 +33,11 @@ void dense_dims(int64_t M, int64_t N, int64_t K) {
   TORCH_CHECK(M * std::max(N, K) < (1LL << 31), "GEMM operand too large for 32-bit indexing");
 }
 
-// y[M][N] = x[M][K] w[N][K]^T (+ bias) (+ resid); act_out = gelu(y)
+// y[M][N] = x[M][K] w[N][K]^T (+ bias) (+ resid); act_out = gelu(y);
+// act_grad (with act_out): y holds gelu'(.) of the pre-activation instead
 void gemm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::optional<torch::Tensor> bias,
               c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> act_out, int64_t M, int64_t N,
-              int64_t K) {
+              int64_t K, bool act_grad) {
   dense_dims(M, N, K);
   need(x, torch::kBFloat16, M * K, "x");
   need(w, torch::kBFloat16, N * K, "w");
@@ -44,8 +45,10 @@ void gemm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, c10::optional<t
   if (bias.has_value() && bias->defined()) need_min(*bias, torch::kFloat32, N, "bias");
   if (resid.has_value() && resid->defined()) need(*resid, torch::kBFloat16, M * N, "resid");
   if (act_out.has_value() && act_out->defined()) need(*act_out, torch::kBFloat16, M * N, "act_out");
+  TORCH_CHECK(!act_grad || (act_out.has_value() && act_out->defined()), "gemm_fwd: act_grad needs act_out");
+  TORCH_CHECK(!act_grad || N % 8 == 0, "gemm_fwd: act_grad width");
   mfl::launch_gemm_fwd(bfp(x), bfp(w), bfp(y), opt_ptr<const float>(bias), opt_ptr<const uint16_t>(resid),
-                       opt_ptr<uint16_t>(act_out), (int)M, (int)N, (int)K, stream_of(x));
+                       opt_ptr<uint16_t>(act_out), (int)M, (int)N, (int)K, stream_of(x), act_grad ? 1 : 0);
 }
 
 // dx[M][K] (+)= dy[M][N] w[N][K].  Long reductions over few output tiles
@@ -75,8 +78,9 @@ void gemm_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, int64_t M, 
 }
 
 // dz = (dy w) * gelu'(z); dbias += colsum(dz)  (FFN1 backward, one launch)
+// pre: z holds gelu'(z) (the forward's act_grad): dz = (dy w) * z
 void gemm_dgrad_gelu(torch::Tensor dy, torch::Tensor w, torch::Tensor dz, torch::Tensor z,
-                     c10::optional<torch::Tensor> dbias, int64_t M, int64_t N, int64_t K) {
+                     c10::optional<torch::Tensor> dbias, int64_t M, int64_t N, int64_t K, bool pre) {
   dense_dims(M, N, K);
   need(dy, torch::kBFloat16, M * N, "dy");
   need(w, torch::kBFloat16, N * K, "w");
@@ -84,7 +88,7 @@ void gemm_dgrad_gelu(torch::Tensor dy, torch::Tensor w, torch::Tensor dz, torch:
   need(z, torch::kBFloat16, M * K, "z");
   if (dbias.has_value() && dbias->defined()) need(*dbias, torch::kFloat32, K, "dbias");
   mfl::launch_gemm_dgrad_gelu(bfp(dy), bfp(w), bfp(dz), bfp(z), opt_ptr<float>(dbias), (int)M, (int)N,
-                              (int)K, stream_of(dy));
+                              (int)K, stream_of(dy), pre ? 1 : 0);
 }
 
 // dw[N][K] (+)= dy^T x  (fp32)
@@ -387,7 +391,9 @@ void vocab_xent(torch::Tensor logits, c10::optional<torch::Tensor> dlogits, torc
 }  // namespace
 
 void register_bert(pybind11::module& m) {
-  m.def("gemm_fwd", &gemm_fwd);
+  m.def("gemm_fwd", &gemm_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("bias"),
+        pybind11::arg("resid"), pybind11::arg("act_out"), pybind11::arg("M"), pybind11::arg("N"),
+        pybind11::arg("K"), pybind11::arg("act_grad") = false);
   m.def("set_gemm_big", [](bool on) { mfl::set_gemm_big(on ? 1 : 0); });
   m.def("gemm_big_enabled", []() { return mfl::gemm_big_enabled() != 0; });
   m.def("gemm_dgrad", &gemm_dgrad, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("dx"), pybind11::arg("M"),
@@ -395,7 +401,9 @@ void register_bert(pybind11::module& m) {
         pybind11::arg("K"), pybind11::arg("accumulate"), pybind11::arg("resid") = pybind11::none());
   m.def("gemm_dgrad_workspace",
         [](int64_t M, int64_t N, int64_t K) { return mfl::gemm_dgrad_workspace((int)M, (int)N, (int)K); });
-  m.def("gemm_dgrad_gelu", &gemm_dgrad_gelu);
+  m.def("gemm_dgrad_gelu", &gemm_dgrad_gelu, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("dz"),
+        pybind11::arg("z"), pybind11::arg("dbias"), pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"),
+        pybind11::arg("pre") = false);
   m.def("gemm_wgrad", &gemm_wgrad);
   m.def("gemm_wgrad2", &gemm_wgrad2);
   m.def("ln_fwd", &ln_fwd);

@@ -86,8 +86,11 @@ struct VocabXentArgs {
 
 void launch_ln_fwd(const LnFwdArgs& a, int H, bool emb, hipStream_t s);
 void launch_ln_bwd(const LnBwdArgs& a, int H, bool emb, hipStream_t s);
+// pre: z holds gelu'(z) already (dz = dh * z)
 void launch_gelu_bwd(const uint16_t* dh, const uint16_t* z, uint16_t* dz, float* dbias, int M, int N,
-                     hipStream_t s);
+                     hipStream_t s, int pre = 0);
+// y <- gelu'(y) in place, n % 8 == 0
+void launch_gelu_grad_inplace(uint16_t* y, int64_t n, hipStream_t s);
 void launch_colsum(const uint16_t* dy, float* dbias, int M, int N, hipStream_t s);
 size_t attn_fwd_lds();
 size_t attn_bwd_lds();

@@ -334,7 +334,7 @@ template <bool GELU>
 __global__ __launch_bounds__(256) void colsum_kernel(const uint16_t* __restrict__ dh,
                                                      const uint16_t* __restrict__ z,
                                                      uint16_t* __restrict__ dz, float* __restrict__ dbias,
-                                                     int M, int N) {
+                                                     int M, int N, int pre) {
   __shared__ float red[4][512];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cv = blockIdx.y * 64 + lane;
@@ -360,9 +360,12 @@ __global__ __launch_bounds__(256) void colsum_kernel(const uint16_t* __restrict_
         if (GELU) {
           float zz[8];
           unpack8(zv[u], zz);
+          if (pre) {  // z holds gelu'(z) (the forward stored it)
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            g[k] *= gelu_grad_f(zz[k]);
+            for (int k = 0; k < 8; ++k) g[k] *= zz[k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) g[k] *= gelu_grad_f(zz[k]);
           }
           const uint4 pk = pack8(g);
           *reinterpret_cast<uint4*>(dz + (int64_t)r * N + cv * 8) = pk;
@@ -384,14 +387,32 @@ __global__ __launch_bounds__(256) void colsum_kernel(const uint16_t* __restrict_
 }
 
 void launch_gelu_bwd(const uint16_t* dh, const uint16_t* z, uint16_t* dz, float* dbias, int M, int N,
-                     hipStream_t s) {
+                     hipStream_t s, int pre) {
   dim3 grid((M + kColRows - 1) / kColRows, (N + 511) / 512);
-  colsum_kernel<true><<<grid, 256, 0, s>>>(dh, z, dz, dbias, M, N);
+  colsum_kernel<true><<<grid, 256, 0, s>>>(dh, z, dz, dbias, M, N, pre);
 }
 
 void launch_colsum(const uint16_t* dy, float* dbias, int M, int N, hipStream_t s) {
   dim3 grid((M + kColRows - 1) / kColRows, (N + 511) / 512);
-  colsum_kernel<false><<<grid, 256, 0, s>>>(dy, nullptr, nullptr, dbias, M, N);
+  colsum_kernel<false><<<grid, 256, 0, s>>>(dy, nullptr, nullptr, dbias, M, N, 0);
+}
+
+// y <- bf16(gelu'(y)) in place (n % 8 == 0): the conv-core GEMM path's
+// stored GELU derivative (launch_gemm_fwd act_grad)
+__global__ __launch_bounds__(256) void gelu_grad_inplace_kernel(uint4* __restrict__ y, int64_t n8) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float f[8];
+    unpack8(y[i], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = gelu_grad_f(f[k]);
+    y[i] = pack8(f);
+  }
+}
+
+void launch_gelu_grad_inplace(uint16_t* y, int64_t n, hipStream_t s) {
+  const int64_t n8 = n / 8;
+  gelu_grad_inplace_kernel<<<stream_grid(n8), 256, 0, s>>>(reinterpret_cast<uint4*>(y), n8);
 }
 
 // =============================================================================

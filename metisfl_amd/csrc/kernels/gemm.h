@@ -17,9 +17,12 @@ void launch_gemm_nt(const uint16_t* a, const uint16_t* b, uint16_t* c, const flo
                     const uint16_t* aux, int M, int N, int K, int epilogue, hipStream_t s);
 
 // Linear layer GEMMs (W is [N][K], K-contiguous):
-//   y = x W^T + bias (+ resid);  act_out = gelu(y) when given
+//   y = x W^T + bias (+ resid);  act_out = gelu(y) when given; with act_grad
+//   (and act_out) y holds gelu'(x W^T + bias) instead, for a backward that
+//   multiplies by it (launch_gemm_dgrad_gelu pre)
 void launch_gemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                     const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s);
+                     const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s,
+                     int act_grad = 0);
 //   dx (+)= dy W  (+ resid: dx = dy W + resid, the residual branch's gradient
 //   read in the epilogue instead of a copy of it accumulated into)
 //   ws: optional split-K slab workspace of gemm_dgrad_workspace(M, N, K) fp32
@@ -40,7 +43,8 @@ int64_t gemm_wgrad_workspace(int M, int N, int K);
 // Large-tile path (gemm_big.hip): 256x256 tiles, exact-tiling shapes only.
 bool gemm_big_ok(int M, int N, int K);
 void launch_gemm_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                         const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s);
+                         const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s,
+                         int act_grad = 0);
 void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
                            bool accumulate, hipStream_t s, float* ws = nullptr, const uint16_t* resid = nullptr);
 int gemm_big_dgrad_splits(int M, int N, int K);
@@ -55,11 +59,12 @@ int64_t gemm_big_wgrad2_workspace(int M, int N0, int K0, int N1, int K1);
 void launch_gemm_big_wgrad2(const uint16_t* x0, const uint16_t* dy0, float* dw0, int N0, int K0, const uint16_t* x1,
                             const uint16_t* dy1, float* dw1, int N1, int K1, int M, hipStream_t s, float* ws);
 void launch_gemm_big_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t* dz, const uint16_t* z,
-                                float* dbias, int M, int N, int K, hipStream_t s);
+                                float* dbias, int M, int N, int K, hipStream_t s, int pre = 0);
 // dz[M][K] = (dy W) * gelu'(z) (exact erf), dbias[K] += column sums of dz:
-// the FFN1 backward in one launch on the large-tile path (else dgrad + gelu_bwd)
+// the FFN1 backward in one launch on the large-tile path (else dgrad + gelu_bwd);
+// pre: z holds gelu'(z) already (the forward's act_grad)
 void launch_gemm_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t* dz, const uint16_t* z,
-                            float* dbias, int M, int N, int K, hipStream_t s);  // > 1: adds into dw (atomics)
+                            float* dbias, int M, int N, int K, hipStream_t s, int pre = 0);  // > 1: adds into dw (atomics)
 // 1 (default; env MFL_GEMM_BIG=0 turns it off): eligible shapes take the large-tile path
 void set_gemm_big(int on);
 int gemm_big_enabled();

@@ -59,9 +59,10 @@ int gemm_big_enabled() {
 }
 
 void launch_gemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                     const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s) {
+                     const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s,
+                     int act_grad) {
   if (gemm_big_enabled() && gemm_big_ok(M, N, K)) {
-    launch_gemm_big_fwd(x, w, y, bias, resid, act_out, M, N, K, s);
+    launch_gemm_big_fwd(x, w, y, bias, resid, act_out, M, N, K, s, act_grad);
     return;
   }
   const ConvGeom g = dense_geom(M, N, K);
@@ -70,6 +71,7 @@ void launch_gemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const fl
   e.resid = resid;
   e.act_out = act_out;
   launch_conv_gemm_epi(g, plan_gemm(M, N, K), x, w, y, nullptr, nullptr, e, s);
+  if (act_out && act_grad) launch_gelu_grad_inplace(y, (int64_t)M * N, s);  // conv-core path: y -> gelu'(y)
 }
 
 void launch_gemm_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int N, int K,
@@ -89,13 +91,13 @@ void launch_gemm_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int 
 }
 
 void launch_gemm_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t* dz, const uint16_t* z,
-                            float* dbias, int M, int N, int K, hipStream_t s) {
+                            float* dbias, int M, int N, int K, hipStream_t s, int pre) {
   if (gemm_big_enabled() && gemm_big_ok(M, K, N)) {
-    launch_gemm_big_dgrad_gelu(dy, w, dz, z, dbias, M, N, K, s);
+    launch_gemm_big_dgrad_gelu(dy, w, dz, z, dbias, M, N, K, s, pre);
     return;
   }
   launch_gemm_dgrad(dy, w, dz, M, N, K, false, s);
-  launch_gelu_bwd(dz, z, dz, dbias, M, K, s);  // in place: each element read then written by one thread
+  launch_gelu_bwd(dz, z, dz, dbias, M, K, s, pre);  // in place: each element read then written by one thread
 }
 
 void launch_gemm_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int N, int K,

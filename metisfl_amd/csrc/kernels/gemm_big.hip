@@ -59,6 +59,12 @@ struct BigGemmArgs {
   //   out = bf16(acc * gelu'(z)),  colsum[col] += sum over rows of out
   const uint16_t* gelu_z;
   float* colsum;
+  // GELU derivative stored by the forward (FFN1 + GELU): c16 <- gelu'(y)
+  // instead of y, and the backward's gelu_z then holds gelu'(z) already
+  // (gelu_pre: dz = dh * gelu_z, one multiply instead of the erf / exp
+  // evaluation over 50M elements in the output stage)
+  int gelu_grad_out;
+  int gelu_pre;
 };
 
 namespace {
@@ -225,13 +231,16 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[
         if (p.gelu_z) {  // dz = dh * gelu'(z), exact erf GELU
           float zz[8];
           unpack8(rd_z[u], zz);
+          if (p.gelu_pre) {  // the forward stored gelu'(z)
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            v[k] *= gelu_grad_f(zz[k]);
+            for (int k = 0; k < 8; ++k) v[k] *= zz[k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] *= gelu_grad_f(zz[k]);
           }
         }
         const uint4 packed = pack8(v);
-        *reinterpret_cast<uint4*>(dst) = packed;
+        if (!p.gelu_grad_out) *reinterpret_cast<uint4*>(dst) = packed;
         if (p.colsum) {  // bias gradient of what the next GEMMs consume (rounded)
           float f[8];
           unpack8(packed, f);
@@ -241,8 +250,20 @@ __device__ __forceinline__ void big_epilogue(const BigGemmArgs& p, f32x4 (&acc)[
         if (p.act_out) {  // exact (erf) GELU of the stored pre-activation
           float f[8], h[8];
           unpack8(packed, f);
+          if (p.gelu_grad_out) {  // and its derivative in place of it
+            float gd[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) h[k] = gelu_f(f[k]);
+            for (int k = 0; k < 8; ++k) {
+              float c, pd;
+              gelu_parts(f[k], c, pd);
+              h[k] = f[k] * c;
+              gd[k] = c + f[k] * pd;
+            }
+            *reinterpret_cast<uint4*>(dst) = pack8(gd);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h[k] = gelu_f(f[k]);
+          }
           *reinterpret_cast<uint4*>(p.act_out + off) = pack8(h);
         }
       }
@@ -912,11 +933,13 @@ bool gemm_big_ok(int M, int N, int K) {
 }
 
 void launch_gemm_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const float* bias,
-                         const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s) {
+                         const uint16_t* resid, uint16_t* act_out, int M, int N, int K, hipStream_t s,
+                         int act_grad) {
   BigGemmArgs p{};
   p.a = x; p.b = w; p.M = M; p.N = N; p.K = K; p.lda = K; p.ldb = K;
   p.a_bytes = (uint32_t)((int64_t)M * K * 2); p.b_bytes = (uint32_t)((int64_t)N * K * 2);
   p.c16 = y; p.ldc = N; p.bias = bias; p.resid = resid; p.act_out = act_out;
+  p.gelu_grad_out = act_out && act_grad;
   p.splits = 1; p.kt_per_split = K / GB_KQ;
   launch_big<false, false, false>(p, K, s);
 }
@@ -967,11 +990,11 @@ void launch_gemm_big_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, 
 }
 
 void launch_gemm_big_dgrad_gelu(const uint16_t* dy, const uint16_t* w, uint16_t* dz, const uint16_t* z,
-                                float* dbias, int M, int N, int K, hipStream_t s) {
+                                float* dbias, int M, int N, int K, hipStream_t s, int pre) {
   BigGemmArgs p{};
   p.a = dy; p.b = w; p.M = M; p.N = K; p.K = N; p.lda = N; p.ldb = K;
   p.a_bytes = (uint32_t)((int64_t)M * N * 2); p.b_bytes = (uint32_t)((int64_t)N * K * 2);
-  p.c16 = dz; p.ldc = K; p.gelu_z = z; p.colsum = dbias;
+  p.c16 = dz; p.ldc = K; p.gelu_z = z; p.colsum = dbias; p.gelu_pre = pre;
   p.splits = 1; p.kt_per_split = N / GB_KQ;
   launch_big<false, true, false>(p, N, s);
 }

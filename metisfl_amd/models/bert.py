@@ -43,6 +43,10 @@ WGRAD2 = os.environ.get("MFL_BERT_WGRAD2", "1") == "1"
 # (MFL_BERT_RESID_DGRAD=0: the LayerNorm backward writes a second copy of its
 # dx that the dgrad accumulates into -- 25 MB more written per LayerNorm)
 RESID_DGRAD = os.environ.get("MFL_BERT_RESID_DGRAD", "1") == "1"
+# FFN1's forward stores gelu'(z) where it stored z, so the FFN2 dgrad's output
+# stage multiplies by it instead of evaluating erf / exp per element
+# (MFL_BERT_GELU_GRAD=0: store z, evaluate gelu'(z) in the backward)
+GELU_GRAD = os.environ.get("MFL_BERT_GELU_GRAD", "1") == "1"
 
 
 @dataclass
@@ -193,7 +197,8 @@ class BertMLM(StaticNet):
             BO.gemm_fwd(A["ctx"], self._w(p + "out.w"), A["ao"], M, H, H, bias=self._p(p + "out.b"), resid=A["x"])
             BO.ln_fwd(A["ao"], self._p(p + "ln1.gamma"), self._p(p + "ln1.beta"), A["a"], A["m1"], A["r1"], M, H,
                       c.eps)
-            BO.gemm_fwd(A["a"], self._w(p + "ffn1.w"), A["z"], M, F, H, bias=self._p(p + "ffn1.b"), act_out=A["h"])
+            BO.gemm_fwd(A["a"], self._w(p + "ffn1.w"), A["z"], M, F, H, bias=self._p(p + "ffn1.b"), act_out=A["h"],
+                        act_grad=GELU_GRAD)
             BO.gemm_fwd(A["h"], self._w(p + "ffn2.w"), A["fo"], M, H, F, bias=self._p(p + "ffn2.b"), resid=A["a"])
             BO.ln_fwd(A["fo"], self._p(p + "ln2.gamma"), self._p(p + "ln2.beta"), A["out"], A["m2"], A["r2"], M,
                       H, c.eps)
@@ -242,7 +247,7 @@ class BertMLM(StaticNet):
             # 300 MB round trip of a separate gelu_bwd (scripts/gelu_fuse_probe.py:
             # 128-134 us fused vs 137-150 unfused, with the A&S erf of common.h)
             BO.gemm_dgrad_gelu(self.g_fo, self._w(p + "ffn2.w"), self.g_z, A["z"], M, H, F,
-                               dbias=g(p + "ffn1.b"))
+                               dbias=g(p + "ffn1.b"), pre=GELU_GRAD)
             BO.gemm_wgrad(A["a"], self.g_z, g(p + "ffn1.w"), M, F, H, zeroed=True)
             if RESID_DGRAD:
                 BO.gemm_dgrad(self.g_z, self._w(p + "ffn1.w"), self.g_a, M, F, H, resid=self.g_fo)

@@ -31,10 +31,12 @@ def _put(dst, val):
 
 
 # ---- Linear -----------------------------------------------------------------
-def gemm_fwd(x, w, y, M, N, K, bias=None, resid=None, act_out=None) -> None:
-    """y = x w^T (+bias) (+resid); act_out = gelu(y) (exact erf)."""
+def gemm_fwd(x, w, y, M, N, K, bias=None, resid=None, act_out=None, act_grad=False) -> None:
+    """y = x w^T (+bias) (+resid); act_out = gelu(y) (exact erf).  ``act_grad``
+    (with act_out): y holds gelu'(z) of the bf16 pre-activation z instead of z,
+    for a backward that multiplies by it (gemm_dgrad_gelu ``pre``)."""
     if x.is_cuda:
-        ops().gemm_fwd(x, w, y, bias, resid, act_out, M, N, K)
+        ops().gemm_fwd(x, w, y, bias, resid, act_out, M, N, K, act_grad)
         return
     v = _b(x).reshape(M, K) @ _b(w).reshape(N, K).t()
     if bias is not None:
@@ -43,7 +45,10 @@ def gemm_fwd(x, w, y, M, N, K, bias=None, resid=None, act_out=None) -> None:
         v = v + _b(resid).reshape(M, N)
     _put(y, v)
     if act_out is not None:
-        _put(act_out, F.gelu(_b(y).reshape(M, N)))
+        z = _b(y).reshape(M, N)
+        _put(act_out, F.gelu(z))
+        if act_grad:
+            _put(y, gelu_grad_ref(z))
 
 
 def gemm_dgrad(dy, w, dx, M, N, K, accumulate=False, resid=None) -> None:
@@ -60,14 +65,16 @@ def gemm_dgrad(dy, w, dx, M, N, K, accumulate=False, resid=None) -> None:
     _put(dx, v)
 
 
-def gemm_dgrad_gelu(dy, w, dz, z, M, N, K, dbias=None) -> None:
+def gemm_dgrad_gelu(dy, w, dz, z, M, N, K, dbias=None, pre=False) -> None:
     """dz = (dy w) * gelu'(z) (exact erf), dbias += column sums of dz: the
-    FFN1 backward GEMM with the GELU backward fused into its epilogue."""
+    FFN1 backward GEMM with the GELU backward fused into its epilogue.
+    ``pre``: z holds gelu'(z) already (the forward's act_grad)."""
     if dy.is_cuda:
-        ops().gemm_dgrad_gelu(dy, w, dz, z, dbias, M, N, K)
+        ops().gemm_dgrad_gelu(dy, w, dz, z, dbias, M, N, K, pre)
         return
     v = _b(dy).reshape(M, N) @ _b(w).reshape(N, K)
-    g = (v * gelu_grad_ref(_b(z).reshape(M, K))).to(BF)
+    zz = _b(z).reshape(M, K)
+    g = (v * (zz if pre else gelu_grad_ref(zz))).to(BF)
     _put(dz, g)
     if dbias is not None:
         dbias.add_(g.float().sum(0).reshape(dbias.shape))

@@ -181,3 +181,37 @@ def test_dgrad_resid_equals_accumulate_into_copy(M, N, K):
         assert _rel(dx, resid.float() + dy.float() @ w.float()) < 1e-2
     with pytest.raises(RuntimeError):
         _ops().gemm_dgrad(dy, w, dx, M, N, K, True, resid)
+
+
+@pytest.mark.parametrize("big", [True, False])
+def test_stored_gelu_derivative(big):
+    """FFN1's forward may store gelu'(z) in place of z (act_grad) and the FFN2
+    dgrad multiply by it (pre) instead of evaluating erf / exp in its output
+    stage (models/bert.py GELU_GRAD).  gelu(z) is unchanged bitwise; the stored
+    derivative is gelu' of the same bf16 pre-activation; the fused backward
+    agrees with the one that evaluates gelu'(z) to bf16 rounding."""
+    _ops().set_gemm_big(big)
+    M, F, H = 1024, 3072, 768
+    g = torch.Generator(device="cuda").manual_seed(17)
+    a = torch.randn(M, H, device="cuda", generator=g).bfloat16()
+    w1 = (torch.randn(F, H, device="cuda", generator=g) * 0.05).bfloat16()
+    b1 = torch.randn(F, device="cuda", generator=g) * 0.1
+    z, h = torch.empty(M, F, device="cuda", dtype=torch.bfloat16), torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+    gp, h2 = torch.empty_like(z), torch.empty_like(h)
+    _ops().gemm_fwd(a, w1, z, b1, None, h, M, F, H)
+    _ops().gemm_fwd(a, w1, gp, b1, None, h2, M, F, H, True)
+    assert torch.equal(h, h2)
+    from metisfl_amd.ops.bert import gelu_grad_ref
+    assert _rel(gp, gelu_grad_ref(z.float())) < 4e-3
+    # backward: dz = (dy w2) * gelu'(z)
+    dy = torch.randn(M, H, device="cuda", generator=g).bfloat16()
+    w2 = (torch.randn(H, F, device="cuda", generator=g) * 0.05).bfloat16()
+    dz0, dz1 = torch.empty_like(z), torch.empty_like(z)
+    db0, db1 = torch.zeros(F, device="cuda"), torch.zeros(F, device="cuda")
+    _ops().gemm_dgrad_gelu(dy, w2, dz0, z, db0, M, H, F)
+    _ops().gemm_dgrad_gelu(dy, w2, dz1, gp, db1, M, H, F, True)
+    ref = (dy.float() @ w2.float()) * gelu_grad_ref(z.float())
+    assert _rel(dz0, ref) < 1e-2 and _rel(dz1, ref) < 1e-2
+    assert _rel(dz1, dz0) < 8e-3
+    assert _rel(db1, db0) < 8e-3
+    _ops().set_gemm_big(True)
