@@ -58,6 +58,16 @@ def exit_process(code: int | None = 0) -> None:
     would count that rank as failed."""
     import logging
     import threading
+    if os.environ.get("MFL_EXIT_FINALIZE") == "1" or any(k.startswith("ROCPROF") for k in os.environ):
+        # under rocprofv3 (or on request) the interpreter must finalise: the
+        # profiler writes its traces from the tool library's exit handlers,
+        # which os._exit skips (a profiled bench left no output at all)
+        for s in (sys.stdout, sys.stderr):
+            try:
+                s.flush()
+            except Exception:  # noqa: BLE001 - closed stream: nothing to flush
+                pass
+        sys.exit(int(code or 0))
     me = threading.current_thread()
     for t in threading.enumerate():
         if t is not me and not t.daemon:
