@@ -1045,6 +1045,12 @@ void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int
 // not fit the grouped kernel (shapes off the 256 grid, other pipelines).
 int gemm_big_wgrad2_splits(int M, int N0, int K0, int N1, int K1) {
   const int tiles = (N0 / GB_BM) * (K0 / GB_BN) + (N1 / GB_BM) * (K1 / GB_BN);
+  // MFL_GB_WGRAD2_SPLITS: A/B override of the grouped launch's slice count
+  static const int forced = [] {
+    const char* v = getenv("MFL_GB_WGRAD2_SPLITS");
+    return v && *v ? atoi(v) : 0;
+  }();
+  if (forced > 0) return std::max(1, std::min(forced, (M / GB_KQ) / 4));
   return std::max(1, std::min(256 / std::max(1, tiles), (M / GB_KQ) / 16));
 }
 

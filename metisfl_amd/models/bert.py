@@ -47,6 +47,9 @@ RESID_DGRAD = os.environ.get("MFL_BERT_RESID_DGRAD", "1") == "1"
 # stage multiplies by it instead of evaluating erf / exp per element
 # (MFL_BERT_GELU_GRAD=0: store z, evaluate gelu'(z) in the backward)
 GELU_GRAD = os.environ.get("MFL_BERT_GELU_GRAD", "1") == "1"
+# the two FFN weight gradients in one grouped launch after the FFN2 dgrad
+# (72 output tiles: 3 split-K slices instead of 7 each, fewer slab bytes)
+FFN_WGRAD2 = os.environ.get("MFL_BERT_FFN_WGRAD2", "1") == "1"
 
 
 @dataclass
@@ -242,13 +245,17 @@ class BertMLM(StaticNet):
             # second copy of it written here to accumulate into)
             BO.ln_bwd(dout, A["fo"], A["m2"], A["r2"], self._p(p + "ln2.gamma"), self.g_fo, g(p + "ln2.gamma"),
                       g(p + "ln2.beta"), M, H, dx2=None if RESID_DGRAD else self.g_a, dbias_prev=g(p + "ffn2.b"))
-            BO.gemm_wgrad(A["h"], self.g_fo, g(p + "ffn2.w"), M, H, F, zeroed=True)
+            if not FFN_WGRAD2:
+                BO.gemm_wgrad(A["h"], self.g_fo, g(p + "ffn2.w"), M, H, F, zeroed=True)
             # GELU backward + FFN1 bias gradient in the dgrad epilogue: saves the
             # 300 MB round trip of a separate gelu_bwd (scripts/gelu_fuse_probe.py:
             # 128-134 us fused vs 137-150 unfused, with the A&S erf of common.h)
             BO.gemm_dgrad_gelu(self.g_fo, self._w(p + "ffn2.w"), self.g_z, A["z"], M, H, F,
                                dbias=g(p + "ffn1.b"), pre=GELU_GRAD)
-            BO.gemm_wgrad(A["a"], self.g_z, g(p + "ffn1.w"), M, F, H, zeroed=True)
+            if FFN_WGRAD2:
+                BO.gemm_wgrad2(A["h"], self.g_fo, g(p + "ffn2.w"), H, F, A["a"], self.g_z, g(p + "ffn1.w"), F, H, M)
+            else:
+                BO.gemm_wgrad(A["a"], self.g_z, g(p + "ffn1.w"), M, F, H, zeroed=True)
             if RESID_DGRAD:
                 BO.gemm_dgrad(self.g_z, self._w(p + "ffn1.w"), self.g_a, M, F, H, resid=self.g_fo)
             else:
