@@ -787,6 +787,26 @@ __global__ __launch_bounds__(512) void gemm_pp_group_kernel(BigGemmArgs p0, BigG
   else gemm_pp_body<AT, BT, OUT32, BN>(p1, w - tiles0, blockIdx.y, smem);
 }
 
+// The grouped weight gradients' two slab sets in one launch: index i < n0
+// reduces into out0, the rest into out1 (the same per-element slice order as
+// two splitk_reduce_kernel launches, so bitwise the same sums)
+__global__ __launch_bounds__(256) void splitk_reduce2_kernel(const float4* __restrict__ ws0, int64_t n0,
+                                                             float4* __restrict__ out0, const float4* __restrict__ ws1,
+                                                             int64_t n1, float4* __restrict__ out1, int splits) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n0 + n1; j += stride) {
+    const bool first = j < n0;
+    const int64_t i = first ? j : j - n0, n = first ? n0 : n1;
+    const float4* ws = first ? ws0 : ws1;
+    float4 a = float4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < splits; ++k) {
+      const float4 v = ws[(int64_t)k * n + i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    (first ? out0 : out1)[i] = a;
+  }
+}
+
 // out (+)= sum over the split-K slabs, 16 B per lane
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float4* __restrict__ ws, int splits,
                                                             int64_t n4, float4* __restrict__ out, int accum) {
@@ -1086,10 +1106,9 @@ void launch_gemm_big_wgrad2(const uint16_t* x0, const uint16_t* dy0, float* dw0,
   launch_pp_group_t<true, true, true, 256>(p0, p1, s);
   if (sp > 1) {
     const int64_t n0 = (int64_t)N0 * K0 / 4, n1 = (int64_t)N1 * K1 / 4;
-    splitk_reduce_kernel<<<stream_grid(n0, 256, 2048), 256, 0, s>>>(reinterpret_cast<const float4*>(p0.ws), sp, n0,
-                                                                     reinterpret_cast<float4*>(dw0), 0);
-    splitk_reduce_kernel<<<stream_grid(n1, 256, 2048), 256, 0, s>>>(reinterpret_cast<const float4*>(p1.ws), sp, n1,
-                                                                     reinterpret_cast<float4*>(dw1), 0);
+    splitk_reduce2_kernel<<<stream_grid(n0 + n1, 256, 2048), 256, 0, s>>>(
+        reinterpret_cast<const float4*>(p0.ws), n0, reinterpret_cast<float4*>(dw0),
+        reinterpret_cast<const float4*>(p1.ws), n1, reinterpret_cast<float4*>(dw1), sp);
   }
 }
 

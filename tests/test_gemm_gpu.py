@@ -215,3 +215,23 @@ def test_stored_gelu_derivative(big):
     assert _rel(dz1, dz0) < 8e-3
     assert _rel(db1, db0) < 8e-3
     _ops().set_gemm_big(True)
+
+
+def test_grouped_wgrad_ffn_pair():
+    """The BERT FFN2 + FFN1 weight gradients in one grouped launch (768 x 3072
+    and 3072 x 768 outputs, 72 tiles, one merged slab reduce) against fp32
+    references and the two single launches."""
+    M, H, F = 4096, 768, 3072
+    g = torch.Generator(device="cuda").manual_seed(23)
+    h = torch.randn(M, F, device="cuda", generator=g).bfloat16()
+    dfo = torch.randn(M, H, device="cuda", generator=g).bfloat16()
+    a = torch.randn(M, H, device="cuda", generator=g).bfloat16()
+    dz = torch.randn(M, F, device="cuda", generator=g).bfloat16()
+    dw2, dw1 = torch.zeros(H, F, device="cuda"), torch.zeros(F, H, device="cuda")
+    assert _ops().gemm_wgrad2(h, dfo, dw2, H, F, a, dz, dw1, F, H, M)
+    assert _rel(dw2, dfo.float().t() @ h.float()) < 2e-3
+    assert _rel(dw1, dz.float().t() @ a.float()) < 2e-3
+    s2, s1 = torch.zeros_like(dw2), torch.zeros_like(dw1)
+    _ops().gemm_wgrad(h, dfo, s2, M, H, F, False, True)
+    _ops().gemm_wgrad(a, dz, s1, M, F, H, False, True)
+    assert _rel(dw2, s2) < 1e-5 and _rel(dw1, s1) < 1e-5
