@@ -331,6 +331,9 @@ void gemm_nt(torch::Tensor a, torch::Tensor b, torch::Tensor c, c10::optional<to
 
 void register_conv(pybind11::module& m) {
   m.def("conv_plan", &conv_plan);
+  m.def("set_conv_plan_targets", [](int64_t conv_target, int64_t wgrad_target) {
+    mfl::set_conv_plan_targets((int)conv_target, (int)wgrad_target);
+  });
   m.def("conv_forward", &conv_forward);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);

@@ -65,6 +65,10 @@ struct ConvArgs {
 
 ConvPlan plan_conv_gemm(const ConvGeom& g, bool dgrad = false);
 ConvPlan plan_conv_wgrad(const ConvGeom& g, int target_blocks = 0);
+// split-K workgroup targets of the bf16 forward / dgrad and weight-gradient
+// plans (0: the defaults, 256 / 512); MFL_CONV_TARGET_BLOCKS /
+// MFL_WGRAD_TARGET_BLOCKS override
+void set_conv_plan_targets(int conv_target, int wgrad_target);
 // number of output tiles (= split-K counter slots) of a gemm plan
 int conv_counter_slots(const ConvGeom& g, const ConvPlan& p);
 

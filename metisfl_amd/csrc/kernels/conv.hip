@@ -824,8 +824,20 @@ static int env_int(const char* name, int dflt) {
   return v && *v ? atoi(v) : dflt;
 }
 
+// Run-time split targets (set_conv_plan_targets: the co-located learners'
+// regime, models/colocated.py): with several learners' launches sharing the
+// CUs, fewer and fuller split-K slices win; the environment variables still
+// override both (sweeps).  Targets only lower split counts, so workspaces
+// sized for the default plans still fit.
+static int g_conv_target_rt = 0, g_wgrad_target_rt = 0;
+void set_conv_plan_targets(int conv_target, int wgrad_target) {
+  g_conv_target_rt = conv_target;
+  g_wgrad_target_rt = wgrad_target;
+}
+
 ConvPlan plan_conv_gemm(const ConvGeom& g, bool dgrad) {
-  static const int target = env_int("MFL_CONV_TARGET_BLOCKS", 256);
+  static const int target_env = env_int("MFL_CONV_TARGET_BLOCKS", 0);
+  const int target = target_env > 0 ? target_env : (g_conv_target_rt > 0 ? g_conv_target_rt : 256);
   static const int min_steps = env_int("MFL_CONV_MIN_KSTEPS", 4);
   static const int parity_on = env_int("MFL_DGRAD_PARITY", 1);
   ConvPlan p;
@@ -938,8 +950,10 @@ void launch_conv_dgrad_bnb(const ConvGeom& g, const ConvPlan& p, const uint16_t*
 }
 
 ConvPlan plan_conv_wgrad(const ConvGeom& g, int target_blocks) {
-  static const int target_env = env_int("MFL_WGRAD_TARGET_BLOCKS", 512);
-  const int target = target_blocks > 0 ? target_blocks : target_env;
+  static const int target_env = env_int("MFL_WGRAD_TARGET_BLOCKS", 0);
+  const int target = target_blocks > 0 ? target_blocks
+                     : target_env > 0  ? target_env
+                                       : (g_wgrad_target_rt > 0 ? g_wgrad_target_rt : 512);
   static const int min_steps = env_int("MFL_WGRAD_MIN_KSTEPS", 8);
   ConvPlan p;
   p.bm = 64;

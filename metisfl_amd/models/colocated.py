@@ -98,6 +98,12 @@ class CoLocatedLearners:
                                               "1,8,256,512,3,2,2;1,8,256,512,1,2,1")
 
     hconv_skip = os.environ.get("MFL_COLOC_HCONV_SKIP", "4")  # see configure_regime
+    # bf16 option: the forward / dgrad and weight-gradient plans aim at 128
+    # split-K workgroups instead of 256 / 512 with 4+ co-located learners
+    # (4 / 8 learners 0.469 / 0.466 -> 0.431 / 0.428 ms per update, 2 learners
+    # neutral, same box, 2 alternating repeats, profiles/r6/s2/bf16_*.log;
+    # one learner keeps the defaults).  "" keeps the defaults.
+    bf16_targets = os.environ.get("MFL_COLOC_BF16_TARGETS", "128,128")
 
     @classmethod
     def apply_kernel_regime(cls, n: int) -> None:
@@ -111,6 +117,10 @@ class CoLocatedLearners:
         if cls.plans:
             from metisfl_amd.ops._native import ops
             ops().set_conv32_plan_overrides(cls.plans)
+        if cls.bf16_targets and n >= 4:  # 2 learners: neutral (0.5765 / 0.5770 ms)
+            from metisfl_amd.ops._native import ops
+            ct, wt = (int(v) for v in cls.bf16_targets.split(","))
+            ops().set_conv_plan_targets(ct, wt)
 
     @staticmethod
     def _set_pair_ring(ns: int) -> None:
