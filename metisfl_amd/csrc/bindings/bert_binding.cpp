@@ -406,6 +406,7 @@ void register_bert(pybind11::module& m) {
         pybind11::arg("pre") = false);
   m.def("gemm_wgrad", &gemm_wgrad);
   m.def("gemm_wgrad2", &gemm_wgrad2);
+  m.def("set_gemm_wgrad2_splits", [](int64_t s) { mfl::set_gemm_wgrad2_splits((int)s); });
   m.def("ln_fwd", &ln_fwd);
   m.def("emb_ln_fwd", &emb_ln_fwd);
   m.def("ln_bwd", &ln_bwd);

@@ -1063,13 +1063,20 @@ void launch_gemm_big_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int
 // dW zero on entry.  ws: split-K slabs of splits * (N0 K0 + N1 K1) floats
 // (gemm_big_wgrad2_workspace).  Falls back to two launches when the pair does
 // not fit the grouped kernel (shapes off the 256 grid, other pipelines).
+// run-time slice count of the grouped weight gradients (co-located BERT
+// learners: their launches fill the CUs, fewer slices move fewer slab bytes;
+// models/colocated.py)
+static int g_wgrad2_splits_rt = 0;
+void set_gemm_wgrad2_splits(int splits) { g_wgrad2_splits_rt = splits; }
+
 int gemm_big_wgrad2_splits(int M, int N0, int K0, int N1, int K1) {
   const int tiles = (N0 / GB_BM) * (K0 / GB_BN) + (N1 / GB_BM) * (K1 / GB_BN);
   // MFL_GB_WGRAD2_SPLITS: A/B override of the grouped launch's slice count
-  static const int forced = [] {
+  static const int env = [] {
     const char* v = getenv("MFL_GB_WGRAD2_SPLITS");
     return v && *v ? atoi(v) : 0;
   }();
+  const int forced = env > 0 ? env : g_wgrad2_splits_rt;
   if (forced > 0) return std::max(1, std::min(forced, (M / GB_KQ) / 4));
   return std::max(1, std::min(256 / std::max(1, tiles), (M / GB_KQ) / 16));
 }

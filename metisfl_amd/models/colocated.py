@@ -104,6 +104,10 @@ class CoLocatedLearners:
     # neutral, same box, 2 alternating repeats, profiles/r6/s2/bf16_*.log;
     # one learner keeps the defaults).  "" keeps the defaults.
     bf16_targets = os.environ.get("MFL_COLOC_BF16_TARGETS", "128,128")
+    # BERT: the grouped weight gradients split 2 ways instead of 3 / 7 with 4+
+    # co-located learners (8 learners 1.330 -> 1.341M tokens/s, 3 alternating
+    # repeats, profiles/r6/s2/bert8_splits*.log).  "" / 0 keeps the plan.
+    wgrad2_splits = int(os.environ.get("MFL_COLOC_WGRAD2_SPLITS", "2") or 0)
 
     @classmethod
     def apply_kernel_regime(cls, n: int) -> None:
@@ -121,6 +125,9 @@ class CoLocatedLearners:
             from metisfl_amd.ops._native import ops
             ct, wt = (int(v) for v in cls.bf16_targets.split(","))
             ops().set_conv_plan_targets(ct, wt)
+        if cls.wgrad2_splits and n >= 4:
+            from metisfl_amd.ops._native import ops
+            ops().set_gemm_wgrad2_splits(cls.wgrad2_splits)
 
     @staticmethod
     def _set_pair_ring(ns: int) -> None:
