@@ -407,6 +407,7 @@ void register_bert(pybind11::module& m) {
   m.def("gemm_wgrad", &gemm_wgrad);
   m.def("gemm_wgrad2", &gemm_wgrad2);
   m.def("set_gemm_wgrad2_splits", [](int64_t s) { mfl::set_gemm_wgrad2_splits((int)s); });
+  m.def("set_gemm_width", [](int64_t w) { mfl::set_gemm_width((int)w); });
   m.def("ln_fwd", &ln_fwd);
   m.def("emb_ln_fwd", &emb_ln_fwd);
   m.def("ln_bwd", &ln_bwd);

@@ -56,6 +56,8 @@ int64_t gemm_big_wgrad_workspace(int M, int N, int K);
 // two weight gradients over the same M in one launch (zeroed dW0 / dW1);
 // set_gemm_wgrad2_splits: run-time slice count (0: the default plan)
 void set_gemm_wgrad2_splits(int splits);
+// ping-pong tile width: 0 = per-shape plan, 192 / 256 forced (co-located regime)
+void set_gemm_width(int w);
 bool gemm_big_wgrad2_ok(int M, int N0, int K0, int N1, int K1);
 int64_t gemm_big_wgrad2_workspace(int M, int N0, int K0, int N1, int K1);
 void launch_gemm_big_wgrad2(const uint16_t* x0, const uint16_t* dy0, float* dw0, int N0, int K0, const uint16_t* x1,

@@ -871,9 +871,14 @@ void launch_pp_group_t(const BigGemmArgs& p0, const BigGemmArgs& p1, hipStream_t
 // Tile width for the ping-pong kernel: 192 when it needs fewer workgroup
 // rounds x tile width (N = 768: 192 -> 256 tiles in one round; N = 2304: 2.25
 // -> 3 rounds of narrower tiles), 256 otherwise (and for the fused column sum).
+// Co-located learners (set_gemm_width 256, models/colocated.py) fill the CUs
+// with each other's launches, so rounds do not matter and the wider tile's
+// operand reuse wins: 8 BERT learners 1.336 -> 1.383M tokens/s.
+int g_width_rt = 0;  // set_gemm_width (defined after the anonymous namespace)
 int pp_width(const BigGemmArgs& p) {
   if (p.colsum || p.N % 192 != 0) return 256;
   if (const char* e = getenv("MFL_GB_WIDTH")) return atoi(e) == 192 ? 192 : 256;
+  if (g_width_rt) return g_width_rt == 192 ? 192 : 256;
   const int64_t mt = (p.M + GB_BM - 1) / GB_BM;
   auto cost = [&](int bn) {
     const int64_t tiles = mt * ((p.N + bn - 1) / bn) * p.splits;
@@ -942,6 +947,8 @@ void launch_big(BigGemmArgs p, int kdim, hipStream_t s) {
 }
 
 }  // namespace
+
+void set_gemm_width(int w) { g_width_rt = w; }
 
 // Exact 256-multiples, or large ragged dimensions (>= 2048: the MLM decoder's
 // 30,528-wide vocabulary) whose partial edge tile is a small fraction of the work.

@@ -108,6 +108,11 @@ class CoLocatedLearners:
     # co-located learners (8 learners 1.330 -> 1.341M tokens/s, 3 alternating
     # repeats, profiles/r6/s2/bert8_splits*.log).  "" / 0 keeps the plan.
     wgrad2_splits = int(os.environ.get("MFL_COLOC_WGRAD2_SPLITS", "2") or 0)
+    # ... and every large-tile GEMM runs 256-wide tiles (the one-learner plan
+    # picks 192 for N = 768 / 2304 to save a round of workgroups; co-located
+    # launches fill the CUs anyway): 8 learners 1.336 -> 1.383M tokens/s,
+    # profiles/r6/s2/bert8_width.log.  "" / 0 keeps the per-shape plan.
+    gemm_width = int(os.environ.get("MFL_COLOC_GB_WIDTH", "256") or 0)
 
     @classmethod
     def apply_kernel_regime(cls, n: int) -> None:
@@ -128,6 +133,9 @@ class CoLocatedLearners:
         if cls.wgrad2_splits and n >= 4:
             from metisfl_amd.ops._native import ops
             ops().set_gemm_wgrad2_splits(cls.wgrad2_splits)
+        if cls.gemm_width and n >= 4:
+            from metisfl_amd.ops._native import ops
+            ops().set_gemm_width(cls.gemm_width)
 
     @staticmethod
     def _set_pair_ring(ns: int) -> None:
