@@ -104,26 +104,30 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwdArgs a) {
 }
 
 constexpr int kLnBwdRows = 16;  // rows per block of the embedding variant (pos_reduced needs B % 16 == 0)
+// 8 waves per block (16 rows per pass): the block count stays ~256 (each
+// block ends with 3 H global atomics) while twice the rows' loads are in
+// flight per CU
+constexpr int kLnBwdWaves = 8, kLnBwdThreads = 64 * kLnBwdWaves, kLnBwdPass = 2 * kLnBwdWaves;
 
 // Embedding variant with a.pos_reduced (B % kLnBwdRows == 0): rows are
 // visited position-major (i -> b = i % B, t = i / B), so a block's rows share
 // one position t and the position-table gradient is reduced in the block
 // instead of by one atomic per element.
 template <int V, bool EMB>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
+__global__ __launch_bounds__(kLnBwdThreads) void ln_bwd_kernel(LnBwdArgs a) {
   constexpr int H = 256 * V;
   // per-wave column partials [wave][dgamma | dbeta | sum dx][H]; every slot is
   // written exactly once (no zeroing, no LDS atomics)
-  __shared__ __attribute__((aligned(16))) float red[4][3][H];
+  __shared__ __attribute__((aligned(16))) float red[kLnBwdWaves][3][H];
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
   float pg[V][8], pb[V][8], pd[V][8];
 #pragma unroll
   for (int v = 0; v < V; ++v)
 #pragma unroll
     for (int k = 0; k < 8; ++k) pg[v][k] = pb[v][k] = pd[v][k] = 0.f;
-  const int rows = EMB ? kLnBwdRows : a.rows;  // multiple of 8
-  for (int pass = 0; pass < rows / 8; ++pass) {
-    const int i = blockIdx.x * rows + pass * 8 + hw;
+  const int rows = EMB ? kLnBwdRows : a.rows;  // multiple of kLnBwdPass
+  for (int pass = 0; pass < rows / kLnBwdPass; ++pass) {
+    const int i = blockIdx.x * rows + pass * kLnBwdPass + hw;
     if (i >= a.M) break;  // uniform per half-wave
     int row = i, b = 0, t = 0, tok = 0;
     if constexpr (EMB) {
@@ -221,11 +225,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < 3; ++q)
-    for (int c = threadIdx.x; c < H; c += 256)
-      red[0][q][c] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
+    for (int c = threadIdx.x; c < H; c += kLnBwdThreads) {
+      float t = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < kLnBwdWaves; ++w2) t += red[w2][q][c];
+      red[0][q][c] = t;
+    }
   __syncthreads();
   if constexpr (MFL_BERT_DBG & 1) return;
-  for (int c = threadIdx.x; c < H; c += 256) {
+  for (int c = threadIdx.x; c < H; c += kLnBwdThreads) {
     atomicAdd(a.dgamma + c, red[0][0][c]);
     atomicAdd(a.dbeta + c, red[0][1][c]);
     // EMB: the type table's gradient (token type 0 for every position);
@@ -305,7 +313,7 @@ void launch_ln_bwd(const LnBwdArgs& args, int H, bool emb, hipStream_t s) {
     const char* v = getenv("MFL_LN_BWD_BLOCKS");
     return v && *v ? atoi(v) : 256;
   }();
-  a.rows = max(16, ((a.M + target_blocks - 1) / target_blocks + 7) / 8 * 8);
+  a.rows = max(kLnBwdPass, ((a.M + target_blocks - 1) / target_blocks + kLnBwdPass - 1) / kLnBwdPass * kLnBwdPass);
   static const int dbg = [] {
     const char* v = getenv("MFL_LN_BWD_DEBUG");
     return v && *v ? atoi(v) : 0;
@@ -315,8 +323,8 @@ void launch_ln_bwd(const LnBwdArgs& args, int H, bool emb, hipStream_t s) {
   const unsigned grid = (a.M + rows - 1) / rows;
 #define MFL_LN_B(V_)                                                               \
   if (H == 256 * V_) {                                                             \
-    if (emb) ln_bwd_kernel<V_, true><<<grid, 256, 0, s>>>(a);                     \
-    else ln_bwd_kernel<V_, false><<<grid, 256, 0, s>>>(a);                        \
+    if (emb) ln_bwd_kernel<V_, true><<<grid, kLnBwdThreads, 0, s>>>(a);           \
+    else ln_bwd_kernel<V_, false><<<grid, kLnBwdThreads, 0, s>>>(a);              \
     return;                                                                        \
   }
   MFL_LN_B(1) MFL_LN_B(2) MFL_LN_B(3) MFL_LN_B(4)
