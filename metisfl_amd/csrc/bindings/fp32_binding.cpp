@@ -723,6 +723,7 @@ void register_fp32(pybind11::module& m) {
   m.def("set_conv32_mode", &set_conv32_mode);
   m.def("set_conv32_pair_ring", &set_conv32_pair_ring);
   m.def("set_conv32_plan_overrides", &set_conv32_plan_overrides);
+  m.def("set_bn32_grid_cap", [](int64_t cap) { mfl::set_bn32_grid_cap((int)cap); });
   m.def("conv32_mode", &conv32_mode);
   m.def("conv32_plan", &conv32_plan);
   m.def("conv32_forward", &conv32_forward);

@@ -82,7 +82,12 @@ void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_
 #ifndef MFL_BN32_GRID
 #define MFL_BN32_GRID 512
 #endif
-inline unsigned apply_grid(int64_t nvec) { return stream_grid(nvec, 256, MFL_BN32_GRID); }
+// run-time cap (set_bn32_grid_cap): 256 for 4+ co-located learners, whose
+// launches fill the CUs anyway (8 learners 5.391 -> 5.343 ms per 8-learner
+// step; one learner 1.038 -> 1.043, so it keeps 512; 1,024 was slower for
+// both: profiles/r6/s2/bn32_grid_*.log)
+static int g_bn32_grid = MFL_BN32_GRID;
+inline unsigned apply_grid(int64_t nvec) { return stream_grid(nvec, 256, g_bn32_grid); }
 
 // Main loops: when C / 4 divides 256 the grid stride is a multiple of C / 4,
 // so a lane's channels never change -- its coefficients live in registers
@@ -550,5 +555,7 @@ void launch_bn32_bwd_apply(const BnBwdArgs32& a, hipStream_t s) {
     else bn32_bwd_apply_kernel<false, false><<<g, 256, sm, s>>>(a, nvec);
   }
 }
+
+void set_bn32_grid_cap(int cap) { g_bn32_grid = cap > 0 ? cap : MFL_BN32_GRID; }
 
 }  // namespace mfl

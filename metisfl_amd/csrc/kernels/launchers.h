@@ -146,6 +146,8 @@ struct BnBwdArgs32 {
 };
 void launch_bn32_stats(const float* x, int64_t M, int C, double* acc, hipStream_t s, int reps = 1);
 void launch_bn32_apply(const BnFwdArgs32& a, hipStream_t s);
+// grid cap of the fp32 BatchNorm apply kernels (0: the build default, 512)
+void set_bn32_grid_cap(int cap);
 void launch_bn32_apply_pair(const BnFwdArgs32& a1, const BnFwdArgs32& a2, hipStream_t s);  // a1 no ReLU, a2 ReLU
 void launch_bn32_bwd_reduce(const float* dy, const float* x, const float* y, const float* mean,
                             const float* invstd, int64_t M, int C, double* acc, hipStream_t s, int reps = 1);

@@ -113,6 +113,10 @@ class CoLocatedLearners:
     # launches fill the CUs anyway): 8 learners 1.336 -> 1.383M tokens/s,
     # profiles/r6/s2/bert8_width.log.  "" / 0 keeps the per-shape plan.
     gemm_width = int(os.environ.get("MFL_COLOC_GB_WIDTH", "256") or 0)
+    # fp32 BatchNorm applies: 256-workgroup grid cap instead of 512 with 4+
+    # learners (8 learners 5.391 -> 5.343 ms per 8-learner step; one learner
+    # keeps 512), profiles/r6/s2/bn32_grid_*.log.  "" / 0 keeps the default.
+    bn32_grid = int(os.environ.get("MFL_COLOC_BN32_GRID", "256") or 0)
 
     @classmethod
     def apply_kernel_regime(cls, n: int) -> None:
@@ -136,6 +140,9 @@ class CoLocatedLearners:
         if cls.gemm_width and n >= 4:
             from metisfl_amd.ops._native import ops
             ops().set_gemm_width(cls.gemm_width)
+        if cls.bn32_grid and n >= 4:
+            from metisfl_amd.ops._native import ops
+            ops().set_bn32_grid_cap(cls.bn32_grid)
 
     @staticmethod
     def _set_pair_ring(ns: int) -> None:
